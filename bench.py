@@ -1,0 +1,198 @@
+#!/usr/bin/env python3
+"""bench.py — RTFx of Paraformer-large offline batch inference on MI355X (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--mode fast|exact]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
+
+One step = one pfm_run (encoder -> CIF -> decoder -> argmax) over this rank's batch of
+B=64 utterances x 30 s (T=500 LFR frames) of synthetic N(0,1) fbank already resident in HBM;
+weights are the seeded random-init Paraformer-large (220.08M params), RCCL-broadcast from
+rank 0 once before timing. Weak scaling: every rank decodes its own 64 utterances, no
+collective inside the timed region. value = audio seconds of all ranks / max-over-ranks wall.
+
+Extra JSON fields: `roofline` of the dominant kernel (the MFMA GEMM, live HIP-event timing),
+`path_roofline` (whole-path algorithmic FLOPs / step time), `cpu_baseline` (the oracle
+torch-CPU restatement timed on a bounded sample on this host), `exact_mode` (the f32-MFMA
+token-parity mode on the same batch) and fast-vs-exact token agreement.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "RTFx (audio-sec/sec) Paraformer-large offline batch, 1/2/4/8 MI355X"
+PEAK_TFLOPS = {"fast": 2500.0, "exact": 157.3}     # MI355X dense bf16 MFMA / f32 MFMA (MICROARCH guide)
+HBM_PEAK_GBS = 8000.0
+FRAME_SEC = 0.06                                    # 10 ms shift x lfr_n 6 (paraformer/model.py:491-493)
+
+
+def path_flops(T: int, L: np.ndarray) -> float:
+    """F(T,L) = 333,634,560 T + 102,400 T^2 + 96,866,304 L + 32,768 L T per utterance."""
+    L = np.asarray(L, dtype=np.float64)
+    return float(np.sum(333634560.0 * T + 102400.0 * T * T + 96866304.0 * L + 32768.0 * L * T))
+
+
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or "unknown"
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--mode", default="fast", choices=["fast", "exact"])
+    ap.add_argument("--batch", type=int, default=64)
+    ap.add_argument("--frames", type=int, default=500)
+    ap.add_argument("--cpu-utts", type=int, default=8, help="cpu_baseline sample size (0 = skip)")
+    ap.add_argument("--exact-steps", type=int, default=2, help="timed exact-mode steps (0 = skip)")
+    ap.add_argument("--seed", type=int, default=0)
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    from funasr_amd.config import paraformer_large
+    from funasr_amd.distributed import broadcast_state_dict
+    from funasr_amd.runtime import PfmEngine
+    from funasr_amd.weights import make_weights, param_layout
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    dev = torch.device("cuda", local)
+    cfg = paraformer_large()
+    B, T = args.batch, args.frames
+
+    # ---- weights: generated on rank 0, one RCCL broadcast (outside the timed region)
+    t0 = time.time()
+    if world > 1:
+        sd = broadcast_state_dict(param_layout(cfg), make_weights(cfg, args.seed) if rank == 0 else None, device=dev)
+    else:
+        sd = make_weights(cfg, args.seed)
+    eng = PfmEngine(cfg, local)
+    eng.load_state_dict(sd)
+    eng.reserve(B, T)
+    t_setup = time.time() - t0
+
+    # ---- synthetic fbank batch resident in HBM (distinct per rank)
+    g = torch.Generator(device=dev)
+    g.manual_seed(1000 + rank)
+    feats = torch.randn((B, T, cfg.input_size), generator=g, device=dev, dtype=torch.float32)
+    lens = torch.full((B,), T, dtype=torch.int32, device=dev)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        eng.run(feats, lens, mode=args.mode)
+    torch.cuda.synchronize()
+
+    eng.profile(True)
+    barrier()
+    torch.cuda.synchronize()
+    ts = time.perf_counter()
+    last = None
+    for _ in range(args.steps):
+        last = eng.run(feats, lens, mode=args.mode)
+    torch.cuda.synchronize()
+    barrier()
+    dt = time.perf_counter() - ts
+    gemm = eng.profile_read(0)
+    attn = eng.profile_read(1)
+    eng.profile(False)
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+
+    ntok = last["ntok"].cpu().numpy()
+    audio_s = B * T * FRAME_SEC * args.steps * world
+    value = audio_s / dt
+    step_ms = dt / args.steps * 1000.0
+    fl_step = path_flops(T, ntok)
+    peak = PEAK_TFLOPS[args.mode]
+    g_ach = gemm["flops"] / (gemm["ms"] / 1e3) / 1e12 if gemm["ms"] > 0 else 0.0
+    roofline = {"bound": "mfma", "kernel": "gemm_nt_kernel<%s>" % ("bf16" if args.mode == "fast" else "float"),
+                "achieved": round(g_ach, 2), "peak": peak, "unit": "TFLOP/s", "frac": round(g_ach / peak, 4),
+                "traffic": None,
+                "avg_launch_us": round(gemm["ms"] * 1e3 / max(1, gemm["launches"]), 2),
+                "launches": int(gemm["launches"]), "share_of_step": round(gemm["ms"] / args.steps / step_ms, 3),
+                "achieved_hbm_gbs": round(gemm["bytes"] / (gemm["ms"] / 1e3) / 1e9, 1) if gemm["ms"] > 0 else None}
+    a_ach = attn["flops"] / (attn["ms"] / 1e3) / 1e12 if attn["ms"] > 0 else 0.0
+    path_tf = fl_step / (step_ms / 1e3) / 1e12
+    out = {
+        "metric": METRIC, "value": round(value, 1), "unit": "audio-sec/sec", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(step_ms, 3), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "bf16" if args.mode == "fast" else "f32",
+        "data": "synthetic N(0,1) fbank [64,500,560] per GPU, seeded random-init Paraformer-large weights",
+        "config": {"workload": "Paraformer-large offline batch, B=64 x 30 s (T=500 LFR frames) fbank per GPU",
+                   "global_batch": B * world, "frames": T, "parallelism": f"dp{world}", "mode": args.mode,
+                   "tokens_per_utt_mean": float(ntok.mean())},
+        "roofline": roofline,
+        "attention": {"achieved": round(a_ach, 2), "unit": "TFLOP/s",
+                      "share_of_step": round(attn["ms"] / args.steps / step_ms, 3)},
+        "path_roofline": {"bound": "mfma", "achieved": round(path_tf, 2), "peak": peak, "unit": "TFLOP/s",
+                          "frac": round(path_tf / peak, 4), "gflop_per_audio_sec": round(fl_step / (B * T * FRAME_SEC) / 1e9, 3)},
+        "setup_s": round(t_setup, 2),
+    }
+
+    # ---- exact (f32 MFMA) mode on the same batch: token-parity mode throughput + agreement
+    if rank == 0 and args.mode == "fast" and args.exact_steps > 0:
+        eng.run(feats, lens, mode="exact")
+        torch.cuda.synchronize()
+        te = time.perf_counter()
+        for _ in range(args.exact_steps):
+            ex = eng.run(feats, lens, mode="exact")
+        torch.cuda.synchronize()
+        dte = (time.perf_counter() - te) / args.exact_steps
+        a, b = last["tokens"].cpu().numpy(), ex["tokens"].cpu().numpy()
+        na, nb = last["ntok"].cpu().numpy(), ex["ntok"].cpu().numpy()
+        agree = [np.mean(a[i, :min(na[i], nb[i])] == b[i, :min(na[i], nb[i])]) for i in range(B)
+                 if min(na[i], nb[i]) > 0]
+        out["exact_mode"] = {"value": round(B * T * FRAME_SEC / dte, 1), "ms_per_step": round(dte * 1e3, 2),
+                             "dtype": "f32", "fast_vs_exact_token_agreement": round(float(np.mean(agree)), 4),
+                             "fast_vs_exact_ntok_equal": round(float(np.mean(na == nb)), 4)}
+
+    # ---- CPU baseline: the oracle torch-CPU restatement on a bounded sample (rank 0, N=1 only)
+    if rank == 0 and world == 1 and args.cpu_utts > 0:
+        from oracle.paraformer_ref import paraformer_infer
+        torch.set_num_threads(int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)))
+        x = feats[: args.cpu_utts].cpu()
+        ln = lens[: args.cpu_utts].cpu()
+        tc = time.perf_counter()
+        paraformer_infer(x, ln, sd, cfg)
+        dtc = time.perf_counter() - tc
+        out["cpu_baseline"] = {"value": round(args.cpu_utts * T * FRAME_SEC / dtc, 2), "unit": "audio-sec/sec",
+                               "cores": torch.get_num_threads(), "kind": "port",
+                               "sample": f"{args.cpu_utts} utts x 30 s (T=500) of the same batch, one call of "
+                                         f"oracle/paraformer_ref.py (torch-CPU fp32, op-for-op restatement), "
+                                         f"{dtc:.1f} s on {cpu_model()}"}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

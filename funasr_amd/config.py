@@ -1,0 +1,138 @@
+"""Paraformer model configuration (the shapes the HIP path is built for).
+
+Mirrors the reference template `funasr/models/paraformer/template.yaml:8-66`
+(encoder_conf / decoder_conf / predictor_conf / frontend_conf) and the kwarg
+names AutoModel passes to the model constructor
+(`funasr/auto/auto_model.py:262-265`).
+"""
+from __future__ import annotations
+
+import dataclasses
+from dataclasses import dataclass, field
+from typing import Any, Dict
+
+
+@dataclass
+class FrontendConf:
+    """`frontend_conf` of `funasr/frontends/wav_frontend.py:80-97` (offline WavFrontend)."""
+    fs: int = 16000
+    window: str = "hamming"
+    n_mels: int = 80
+    frame_length: int = 25          # ms
+    frame_shift: int = 10           # ms
+    lfr_m: int = 7
+    lfr_n: int = 6
+    dither: float = 0.0             # reference default 1.0; parity/golden runs force 0 (C++ runtime does too)
+    cmvn_file: str | None = None
+    upsacle_samples: bool = True    # (sic) reference spelling, wav_frontend.py:96
+
+
+@dataclass
+class ParaformerConfig:
+    """Dimensions of a Paraformer (SAN-M encoder + CIF + SAN-M NAR decoder).
+
+    Defaults are Paraformer-large (220.08M params).
+    """
+    input_size: int = 560           # 80 mel x lfr_m 7
+    d_model: int = 512              # encoder_conf.output_size
+    heads: int = 4
+    ffn: int = 2048                 # linear_units
+    enc_blocks: int = 50            # 1 (encoders0) + 49 (encoders)
+    dec_blocks: int = 16            # att_layer_num == num_blocks -> decoders2 is None
+    kernel_size: int = 11           # FSMN depthwise kernel (encoder and decoder)
+    enc_sanm_shift: int = 0
+    dec_sanm_shift: int = 0
+    vocab_size: int = 8404
+    cif_l_order: int = 1
+    cif_r_order: int = 1
+    cif_threshold: float = 1.0
+    tail_threshold: float = 0.45
+    smooth_factor: float = 1.0
+    noise_threshold: float = 0.0
+    ln_eps: float = 1e-12           # funasr/models/transformer/layer_norm.py:24
+    blank_id: int = 0
+    sos: int = 1
+    eos: int = 2
+
+    @property
+    def d_k(self) -> int:
+        return self.d_model // self.heads
+
+    def to_dict(self) -> Dict[str, Any]:
+        return dataclasses.asdict(self)
+
+    @classmethod
+    def from_kwargs(cls, **kw) -> "ParaformerConfig":
+        """Build from AutoModel-style kwargs (encoder_conf/decoder_conf/predictor_conf)."""
+        c = cls()
+        enc = kw.get("encoder_conf") or {}
+        dec = kw.get("decoder_conf") or {}
+        pred = kw.get("predictor_conf") or {}
+        if "input_size" in kw and kw["input_size"]:
+            c.input_size = int(kw["input_size"])
+        if "vocab_size" in kw and kw["vocab_size"] and int(kw["vocab_size"]) > 0:
+            c.vocab_size = int(kw["vocab_size"])
+        c.d_model = int(enc.get("output_size", c.d_model))
+        c.heads = int(enc.get("attention_heads", c.heads))
+        c.ffn = int(enc.get("linear_units", c.ffn))
+        c.enc_blocks = int(enc.get("num_blocks", c.enc_blocks))
+        c.kernel_size = int(enc.get("kernel_size", c.kernel_size))
+        c.enc_sanm_shift = int(enc.get("sanm_shfit", c.enc_sanm_shift))
+        if enc.get("input_layer", "pe") != "pe":
+            raise ValueError("only input_layer='pe' (SinusoidalPositionEncoder) is on the HIP path")
+        if not enc.get("normalize_before", True):
+            raise ValueError("only normalize_before=True is on the HIP path")
+        nb = int(dec.get("num_blocks", c.dec_blocks))
+        att = int(dec.get("att_layer_num", nb))
+        if nb != att:
+            raise ValueError("decoders2 (num_blocks > att_layer_num) is not on the Paraformer-large path")
+        c.dec_blocks = att
+        if int(dec.get("linear_units", c.ffn)) != c.ffn:
+            raise ValueError("decoder linear_units must equal encoder linear_units")
+        if int(dec.get("kernel_size", c.kernel_size)) != c.kernel_size:
+            raise ValueError("decoder kernel_size must equal encoder kernel_size")
+        c.dec_sanm_shift = int(dec.get("sanm_shfit", c.dec_sanm_shift))
+        c.cif_l_order = int(pred.get("l_order", c.cif_l_order))
+        c.cif_r_order = int(pred.get("r_order", c.cif_r_order))
+        c.cif_threshold = float(pred.get("threshold", c.cif_threshold))
+        c.tail_threshold = float(pred.get("tail_threshold", c.tail_threshold))
+        c.smooth_factor = float(pred.get("smooth_factor", c.smooth_factor))
+        c.noise_threshold = float(pred.get("noise_threshold", c.noise_threshold))
+        for k in ("blank_id", "sos", "eos"):
+            if k in kw and kw[k] is not None:
+                setattr(c, k, int(kw[k]))
+        return c
+
+    def reference_kwargs(self) -> Dict[str, Any]:
+        """The AutoModel / Paraformer constructor kwargs that describe this config."""
+        return dict(
+            encoder="SANMEncoder",
+            encoder_conf=dict(output_size=self.d_model, attention_heads=self.heads,
+                              linear_units=self.ffn, num_blocks=self.enc_blocks,
+                              dropout_rate=0.1, positional_dropout_rate=0.1,
+                              attention_dropout_rate=0.1, input_layer="pe",
+                              pos_enc_class="SinusoidalPositionEncoder", normalize_before=True,
+                              kernel_size=self.kernel_size, sanm_shfit=self.enc_sanm_shift,
+                              selfattention_layer_type="sanm"),
+            decoder="ParaformerSANMDecoder",
+            decoder_conf=dict(attention_heads=self.heads, linear_units=self.ffn,
+                              num_blocks=self.dec_blocks, dropout_rate=0.1,
+                              positional_dropout_rate=0.1, self_attention_dropout_rate=0.1,
+                              src_attention_dropout_rate=0.1, att_layer_num=self.dec_blocks,
+                              kernel_size=self.kernel_size, sanm_shfit=self.dec_sanm_shift),
+            predictor="CifPredictorV2",
+            predictor_conf=dict(idim=self.d_model, threshold=self.cif_threshold,
+                                l_order=self.cif_l_order, r_order=self.cif_r_order,
+                                tail_threshold=self.tail_threshold),
+            input_size=self.input_size,
+            vocab_size=self.vocab_size,
+        )
+
+
+def paraformer_large() -> ParaformerConfig:
+    return ParaformerConfig()
+
+
+def paraformer_tiny(enc_blocks: int = 3, dec_blocks: int = 2, vocab_size: int = 8404) -> ParaformerConfig:
+    """Reduced-depth config used for full-tensor golden vectors (same widths as large)."""
+    return ParaformerConfig(enc_blocks=enc_blocks, dec_blocks=dec_blocks, vocab_size=vocab_size)

@@ -1,0 +1,339 @@
+// HBM-bound kernels of the Paraformer path: LayerNorm (+ embedding prologue), FSMN memory
+// block, CIF predictor head + integrate-and-fire, and the row-argmax reduction.
+#include "pfm_common.h"
+
+namespace {
+
+// ------------------------------------------------------------------------------------------
+// LayerNorm over the last dim (funasr/models/transformer/layer_norm.py:13-39, eps 1e-12).
+// One wave per row, float4 loads; mean/var in f64 (rows are <= 2048 wide) so the result is the
+// correctly-rounded normalisation the CPU reference approximates to ~1 ulp.
+// Optional prologue (encoder input, sanm/encoder.py:377-397):  x = in * in_scale + pe[t].
+// ------------------------------------------------------------------------------------------
+constexpr int LN_MAXV = 8;   // float4 per lane -> D <= 2048
+
+__global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict__ x, RowMap xmap, int M, int D,
+                                                        const float* __restrict__ g, const float* __restrict__ bta,
+                                                        float eps, const float* __restrict__ pe, int pe_T,
+                                                        float in_scale, void* out, RowMap omap, int odt,
+                                                        void* out2, RowMap o2map, int o2dt) {
+    const int lane = threadIdx.x & 63;
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= M) return;
+    const float* xr = x + xmap.off(row);
+    const float* per = pe ? pe + (long long)(row % pe_T) * D : nullptr;
+    float4 v[LN_MAXV];
+    double s = 0.0;
+#pragma unroll
+    for (int i = 0; i < LN_MAXV; ++i) {
+        const int c = (lane + 64 * i) * 4;
+        if (c < D) {
+            float4 t = *(const float4*)(xr + c);
+            if (per) {
+                const float4 p = *(const float4*)(per + c);
+                t.x = t.x * in_scale + p.x; t.y = t.y * in_scale + p.y;
+                t.z = t.z * in_scale + p.z; t.w = t.w * in_scale + p.w;
+            }
+            v[i] = t;
+            s += (double)t.x + (double)t.y + (double)t.z + (double)t.w;
+        }
+    }
+    s = wave_sum_d(s);
+    const double mean = s / D;
+    double q = 0.0;
+#pragma unroll
+    for (int i = 0; i < LN_MAXV; ++i) {
+        const int c = (lane + 64 * i) * 4;
+        if (c < D) {
+            const double a0 = v[i].x - mean, a1 = v[i].y - mean, a2 = v[i].z - mean, a3 = v[i].w - mean;
+            q += a0 * a0 + a1 * a1 + a2 * a2 + a3 * a3;
+        }
+    }
+    q = wave_sum_d(q);
+    const double rstd = 1.0 / sqrt(q / D + (double)eps);
+    const long long ob = omap.off(row), ob2 = out2 ? o2map.off(row) : 0;
+#pragma unroll
+    for (int i = 0; i < LN_MAXV; ++i) {
+        const int c = (lane + 64 * i) * 4;
+        if (c < D) {
+            const float4 gg = *(const float4*)(g + c), bb = *(const float4*)(bta + c);
+            float4 y;
+            y.x = (float)((v[i].x - mean) * rstd) * gg.x + bb.x;
+            y.y = (float)((v[i].y - mean) * rstd) * gg.y + bb.y;
+            y.z = (float)((v[i].z - mean) * rstd) * gg.z + bb.z;
+            y.w = (float)((v[i].w - mean) * rstd) * gg.w + bb.w;
+            if (odt == DT_F32) *(float4*)((float*)out + ob + c) = y;
+            else {
+                bf16x4 t = {f2bf(y.x), f2bf(y.y), f2bf(y.z), f2bf(y.w)};
+                *(bf16x4*)((bf16*)out + ob + c) = t;
+            }
+            if (out2) {
+                if (o2dt == DT_F32) *(float4*)((float*)out2 + ob2 + c) = y;
+                else {
+                    bf16x4 t = {f2bf(y.x), f2bf(y.y), f2bf(y.z), f2bf(y.w)};
+                    *(bf16x4*)((bf16*)out2 + ob2 + c) = t;
+                }
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// FSMN memory block (sanm/attention.py:207-223 encoder; :499-547 decoder):
+//   y[t,c] = m[t] * ( sum_k w[c,k] * m[t+k-left] v[t+k-left,c] + m[t] v[t,c] )  (+ res[t,c])
+// depthwise Conv1d(groups=D, no bias) over the masked sequence with (left, K-1-left) zero pad.
+// One thread per (row, 4 channels); the K-row window is served from L1/L2.
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void fsmn_kernel(const float* __restrict__ v, RowMap vmap,
+                                                   const int* __restrict__ len, int B, int T, int D,
+                                                   const float* __restrict__ w, int K, int left,
+                                                   const float* __restrict__ res, float* __restrict__ out,
+                                                   bf16* __restrict__ out_bf) {
+    const int qpr = D / 4;
+    const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (gid >= (long long)B * T * qpr) return;
+    const int c = (int)(gid % qpr) * 4;
+    const long long row = gid / qpr;
+    const int b = (int)(row / T), t = (int)(row % T);
+    const int L = min(len[b], T);
+    float4 acc = make_float4(0, 0, 0, 0);
+    float4 self = make_float4(0, 0, 0, 0);
+    const bool valid = t < L;
+    if (valid) {
+        for (int k = 0; k < K; ++k) {
+            const int tt = t + k - left;
+            if (tt < 0 || tt >= L) continue;
+            const float4 x = *(const float4*)(v + vmap.off((long long)b * T + tt) + c);
+            acc.x = fmaf(w[(c + 0) * K + k], x.x, acc.x);
+            acc.y = fmaf(w[(c + 1) * K + k], x.y, acc.y);
+            acc.z = fmaf(w[(c + 2) * K + k], x.z, acc.z);
+            acc.w = fmaf(w[(c + 3) * K + k], x.w, acc.w);
+        }
+        self = *(const float4*)(v + vmap.off(row) + c);
+    }
+    float4 y;
+    y.x = valid ? acc.x + self.x : 0.f;
+    y.y = valid ? acc.y + self.y : 0.f;
+    y.z = valid ? acc.z + self.z : 0.f;
+    y.w = valid ? acc.w + self.w : 0.f;
+    if (res) {
+        const float4 r = *(const float4*)(res + row * D + c);
+        y.x = r.x + y.x; y.y = r.y + y.y; y.z = r.z + y.z; y.w = r.w + y.w;
+    }
+    *(float4*)(out + row * D + c) = y;
+    if (out_bf) {
+        bf16x4 tb = {f2bf(y.x), f2bf(y.y), f2bf(y.z), f2bf(y.w)};
+        *(bf16x4*)(out_bf + row * D + c) = tb;
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// CIF predictor head (cif_predictor.py:214-242, 346-370):
+//   alpha[t] = relu(sigmoid(w . relu(conv)[t] + b) * smooth - noise) * mask[t],  t < T
+//   alpha[T] = 0;  alpha[len] += tail_threshold   (tail_process_fn with mask)
+// One wave per (utterance, frame); dot product in f64.
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void cif_alpha_kernel(const float* __restrict__ hc, int D,
+                                                        const float* __restrict__ wout, const float* __restrict__ bout,
+                                                        const int* __restrict__ len, int B, int T, float smooth,
+                                                        float noise, float tail, float* __restrict__ alphas) {
+    const int lane = threadIdx.x & 63;
+    const long long item = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (item >= (long long)B * (T + 1)) return;
+    const int b = (int)(item / (T + 1)), t = (int)(item % (T + 1));
+    const int L = min(len[b], T);
+    float a = 0.f;
+    if (t < T) {
+        const float* hr = hc + ((long long)b * T + t) * D;
+        double s = 0.0;
+        for (int c = lane * 4; c < D; c += 256) {
+            const float4 x = *(const float4*)(hr + c), ww = *(const float4*)(wout + c);
+            s += (double)x.x * ww.x + (double)x.y * ww.y + (double)x.z * ww.z + (double)x.w * ww.w;
+        }
+        s = wave_sum_d(s);
+        const float z = (float)(s + (double)bout[0]);
+        const float sg = (float)(1.0 / (1.0 + exp(-(double)z)));
+        a = fmaxf(sg * smooth - noise, 0.f);
+        if (t >= L) a = 0.f;
+    }
+    if (t == L) a = a + tail;
+    if (lane == 0) alphas[(long long)b * (T + 1) + t] = a;
+}
+
+// ------------------------------------------------------------------------------------------
+// Continuous integrate-and-fire (cif_wo_hidden_v1 / cif_v1, cif_predictor.py:668-735).
+// One workgroup per utterance; every thread walks the T+1 frames (fire decisions are uniform).
+//   P_t  = f32( sum_{s<=t} f64(alpha_s) )            fire_t = floor(P_t) > floor(P_{t-1}), floor(P_-1)=0
+//   fires_t = fire_t + (P_t - floor(P_t))  (f32)      rem_t = fires_t - floor(fires_t)
+//   PH_t = f32( sum_{s<=t} f64(f32(alpha_s * h_s)) )  (torch CPU cumsum accumulates f32 in f64)
+//   emb_k = ((PH_tk - PH_tk-1) + rem_tk-1 h_tk-1) - rem_tk h_tk,    rows >= n_fire are zero
+// token_num = floor(sum_t alpha_t) (f64 sum; the reference sums in f32 — see DESIGN.md).
+// h rows via RowMap; row T of each utterance must be the zero row appended by tail_process_fn.
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void cif_fire_kernel(const float* __restrict__ alphas, const float* __restrict__ h,
+                                                       RowMap hmap, int T, int D, int Lcap,
+                                                       float* __restrict__ emb, float* __restrict__ peaks,
+                                                       int* __restrict__ n_fire, int* __restrict__ ntok) {
+    const int b = blockIdx.x;
+    const float* al = alphas + (long long)b * (T + 1);
+    constexpr int CPT = 4;                 // channels per thread (D <= 1024)
+    double ph[CPT];
+    float pph[CPT], prh[CPT];
+#pragma unroll
+    for (int j = 0; j < CPT; ++j) { ph[j] = 0.0; pph[j] = 0.f; prh[j] = 0.f; }
+    double P = 0.0;
+    float prevfl = 0.f;
+    int k = 0;
+    for (int t = 0; t <= T; ++t) {
+        const float a = al[t];
+        P += (double)a;
+        const float Pf = (float)P;
+        const float fl = floorf(Pf);
+        const bool fire = (fl - prevfl) > 0.f;
+        prevfl = fl;
+        const float fires = (fire ? 1.f : 0.f) + (Pf - fl);
+        if (threadIdx.x == 0 && peaks) peaks[(long long)b * (T + 1) + t] = fires;
+        const float rem = fires - floorf(fires);
+        const float* hr = h + hmap.off((long long)b * (T + 1) + t);
+#pragma unroll
+        for (int j = 0; j < CPT; ++j) {
+            const int c = threadIdx.x + j * blockDim.x;
+            if (c < D) {
+                const float hv = hr[c];
+                ph[j] += (double)(a * hv);
+                if (fire) {
+                    const float phf = (float)ph[j];
+                    const float rh = rem * hv;
+                    if (k < Lcap) emb[((long long)b * Lcap + k) * D + c] = ((phf - pph[j]) + prh[j]) - rh;
+                    pph[j] = phf;
+                    prh[j] = rh;
+                }
+            }
+        }
+        if (fire) ++k;
+    }
+    for (int kk = k; kk < Lcap; ++kk)
+        for (int c = threadIdx.x; c < D; c += blockDim.x) emb[((long long)b * Lcap + kk) * D + c] = 0.f;
+    if (threadIdx.x == 0) {
+        n_fire[b] = k;
+        double s = 0.0;
+        for (int t = 0; t <= T; ++t) s += (double)al[t];
+        ntok[b] = (int)floor(s);
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// Row argmax over the GEMM's per-(row, 64-column block) partial maxima; first index on ties
+// (torch.argmax). argmax(log_softmax(x)) == argmax(x), so logits never reach HBM.
+// tokens[b, l] for l < ntok[b], -1 elsewhere (paraformer/model.py:527-536).
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void argmax_reduce_kernel(const float* __restrict__ val, const int* __restrict__ idx,
+                                                            int ntiles, int B, int L, const int* __restrict__ ntok,
+                                                            int Lcap, int* __restrict__ tokens, float* __restrict__ score) {
+    const int lane = threadIdx.x & 63;
+    const long long row = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= (long long)B * L) return;
+    const int b = (int)(row / L), l = (int)(row % L);
+    float bv = -INFINITY;
+    int bi = 0x7fffffff;
+    for (int i = lane; i < ntiles; i += 64) {
+        const float v = val[row * ntiles + i];
+        const int ii = idx[row * ntiles + i];
+        if (v > bv || (v == bv && ii < bi)) { bv = v; bi = ii; }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const float ov = __shfl_xor(bv, o, 64);
+        const int oi = __shfl_xor(bi, o, 64);
+        if (ov > bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
+    }
+    if (lane == 0 && l < Lcap) {
+        tokens[(long long)b * Lcap + l] = (l < ntok[b]) ? bi : -1;
+        if (score) score[(long long)b * Lcap + l] = bv;
+    }
+}
+
+__global__ void fill_i32_kernel(int* p, long long n, int v) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) p[i] = v;
+}
+
+__global__ void f32_to_bf16_kernel(const float* __restrict__ x, bf16* __restrict__ y, long long n) {
+    const long long i = ((long long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+    if (i + 3 < n) {
+        const float4 v = *(const float4*)(x + i);
+        bf16x4 t = {f2bf(v.x), f2bf(v.y), f2bf(v.z), f2bf(v.w)};
+        *(bf16x4*)(y + i) = t;
+    } else {
+        for (long long j = i; j < n; ++j) y[j] = f2bf(x[j]);
+    }
+}
+
+// Encoder output scatter into the zero-padded [B][T+2][D] layout (rows 0 and T+1 of each
+// utterance stay zero), feeding the k=3 predictor conv as an implicit-im2col GEMM.
+}  // namespace
+
+hipError_t pfm_layernorm(const float* x, RowMap xmap, int M, int D, const float* g, const float* b, float eps,
+                         const float* pe, int pe_T, float in_scale, void* out, RowMap omap, int odt, void* out2,
+                         RowMap o2map, int o2dt, hipStream_t st) {
+    if (M <= 0) return hipSuccess;
+    if (D % 4 != 0 || D > 4 * 64 * LN_MAXV) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(layernorm_kernel, dim3((M + 3) / 4), dim3(256), 0, st, x, xmap, M, D, g, b, eps, pe,
+                       pe_T > 0 ? pe_T : 1, in_scale, out, omap, odt, out2, o2map, o2dt);
+    PFM_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+hipError_t pfm_fsmn(const float* v, RowMap vmap, const int* len, int B, int T, int D, const float* w, int K,
+                    int left, const float* res, float* out, bf16* out_bf, hipStream_t st) {
+    if (B <= 0 || T <= 0) return hipSuccess;
+    if (D % 4 != 0) return hipErrorInvalidValue;
+    const long long n = (long long)B * T * (D / 4);
+    hipLaunchKernelGGL(fsmn_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, v, vmap, len, B, T, D, w,
+                       K, left, res, out, out_bf);
+    PFM_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+hipError_t pfm_cif_alpha(const float* hc, int D, const float* wout, const float* bout, const int* len, int B,
+                         int T, float smooth, float noise, float tail, float* alphas, hipStream_t st) {
+    const long long n = (long long)B * (T + 1);
+    hipLaunchKernelGGL(cif_alpha_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, st, hc, D, wout, bout, len,
+                       B, T, smooth, noise, tail, alphas);
+    PFM_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+hipError_t pfm_cif_fire(const float* alphas, const float* h, RowMap hmap, int B, int T, int D, int Lcap,
+                        float* emb, float* peaks, int* n_fire, int* ntok, hipStream_t st) {
+    if (D > 4 * 256) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(cif_fire_kernel, dim3(B), dim3(256), 0, st, alphas, h, hmap, T, D, Lcap, emb, peaks,
+                       n_fire, ntok);
+    PFM_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+hipError_t pfm_argmax_reduce(const float* val, const int* idx, int ntiles, int B, int L, const int* ntok,
+                             int Lcap, int* tokens, float* score, hipStream_t st) {
+    const long long n = (long long)B * L;
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(argmax_reduce_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, st, val, idx, ntiles, B,
+                       L, ntok, Lcap, tokens, score);
+    PFM_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+hipError_t pfm_fill_i32(int* p, long long n, int v, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(fill_i32_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, p, n, v);
+    PFM_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+hipError_t pfm_f32_to_bf16(const float* x, bf16* y, long long n, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    const long long nt = (n + 3) / 4;
+    hipLaunchKernelGGL(f32_to_bf16_kernel, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, st, x, y, n);
+    PFM_LAUNCH_CHECK();
+    return hipSuccess;
+}

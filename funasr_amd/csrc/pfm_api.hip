@@ -1,0 +1,773 @@
+// C-ABI implementation (include/pfm.h): weight registry, workspace and the Paraformer
+// forward pipeline on one HIP stream. Host code only; kernels live in k_*.hip.
+#include <math.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <memory>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/pfm.h"
+#include "pfm_common.h"
+
+// ---- kernel launchers (k_*.hip)
+hipError_t pfm_gemm(int dtype, const void* A, RowMap amap, const void* W, long long ldw, int M, int N, int K,
+                    const GemmEpi& epi, hipStream_t st);
+int pfm_gemm_amax_tiles(int N);
+hipError_t pfm_attention(int dtype, const void* q, RowMap qmap, const void* k, RowMap kmap, const void* v,
+                         RowMap vmap, float* o, long long ldo, void* o2, const int* klen, int B, int Tq, int Tk,
+                         int heads, int dk, float scale, hipStream_t st);
+int pfm_attention_lds_bytes(int dtype);
+hipError_t pfm_layernorm(const float* x, RowMap xmap, int M, int D, const float* g, const float* b, float eps,
+                         const float* pe, int pe_T, float in_scale, void* out, RowMap omap, int odt, void* out2,
+                         RowMap o2map, int o2dt, hipStream_t st);
+hipError_t pfm_fsmn(const float* v, RowMap vmap, const int* len, int B, int T, int D, const float* w, int K,
+                    int left, const float* res, float* out, bf16* out_bf, hipStream_t st);
+hipError_t pfm_cif_alpha(const float* hc, int D, const float* wout, const float* bout, const int* len, int B,
+                         int T, float smooth, float noise, float tail, float* alphas, hipStream_t st);
+hipError_t pfm_cif_fire(const float* alphas, const float* h, RowMap hmap, int B, int T, int D, int Lcap,
+                        float* emb, float* peaks, int* n_fire, int* ntok, hipStream_t st);
+hipError_t pfm_argmax_reduce(const float* val, const int* idx, int ntiles, int B, int L, const int* ntok,
+                             int Lcap, int* tokens, float* score, hipStream_t st);
+hipError_t pfm_fill_i32(int* p, long long n, int v, hipStream_t st);
+hipError_t pfm_f32_to_bf16(const float* x, bf16* y, long long n, hipStream_t st);
+hipError_t pfm_fbank_launch(const float* wav, const int* nsamp, int B, int S_max, const float* cmvn,
+                            const unsigned char* tables, float* fb_ws, int N_cap, float* feats, int T_cap, int* T_out,
+                            hipStream_t st);
+int pfm_fbank_frames(int nsamp);
+int pfm_fbank_nframes(int nsamp);
+void pfm_fbank_tables(float* melw, int* lo, int* hi, float* window, double* tw);
+size_t pfm_fbank_table_bytes();
+size_t pfm_fbank_twoff();
+
+// ---- error plumbing
+static thread_local std::string g_err;
+static int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+#define HIP_TRY(expr)                                                                            \
+    do {                                                                                         \
+        hipError_t _e = (expr);                                                                  \
+        if (_e != hipSuccess)                                                                    \
+            return fail(PFM_E_HIP, std::string(#expr) + ": " + hipGetErrorString(_e));           \
+    } while (0)
+
+namespace {
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    ~DevBuf() { if (p) (void)hipFree(p); }
+    hipError_t ensure(size_t n) {
+        if (n <= bytes) return hipSuccess;
+        if (p) { hipError_t e = hipFree(p); if (e != hipSuccess) return e; p = nullptr; bytes = 0; }
+        hipError_t e = hipMalloc(&p, n);
+        if (e == hipSuccess) bytes = n;
+        return e;
+    }
+    template <typename T> T* as() const { return (T*)p; }
+};
+
+// One registry entry per reference state_dict tensor we consume.
+struct WEntry {
+    std::vector<int64_t> shape;
+    size_t off = 0;        // element offset in the f32 arena
+    size_t numel = 0;
+    bool set = false;
+    int kind = 0;          // 0 plain, 1 cif conv [O][I][k] -> [O][k*I], 2 ignored
+};
+
+struct EncLayer { size_t ln1g, ln1b, wqkv, bqkv, wo, bo, fsmn, ln2g, ln2b, w1, b1, w2, b2; int din; };
+struct DecLayer { size_t fsmn, wq, bq, wo, bo, w1, b1, w2, ng, nb, n1g, n1b, n2g, n2b, n3g, n3b; };
+
+}  // namespace
+
+struct pfm_handle {
+    pfm_config cfg;
+    int device = 0;
+    std::unordered_map<std::string, WEntry> reg;
+    size_t arena_elems = 0;
+    DevBuf arena;                  // all f32 weights
+    DevBuf arena_bf;               // bf16 copies of GEMM weights (same element offsets)
+    std::vector<std::pair<size_t, size_t>> gemm_ranges;   // (off, numel) converted to bf16
+    bool bf_ready = false;
+    int missing = 0;
+    std::vector<EncLayer> enc;
+    std::vector<DecLayer> dec;
+    size_t an_g, an_b, cif_w, cif_b, cif_ow, cif_ob, dan_g, dan_b, out_w, out_b, d3w1, d3b1, d3w2, d3ng, d3nb,
+        d3n1g, d3n1b, wkv_all, bkv_all;
+    // workspace
+    int capB = 0, capT = 0;
+    DevBuf pe, X, Xn, QKV, QKVb, F, O, Ob, H, encp, encpb, Hc, alphas, peaks, nfire, ntok, emb, KV, Xd, Xdn, Hd,
+        Hdn, Td, Tdn, Qd, Od, Odb, amv, ami, tok_tmp;
+    int pe_T = 0;
+    DevBuf fb_ws, fb_tab;
+    bool fb_tab_ready = false;
+    int32_t* host_ntok = nullptr;
+    int host_ntok_cap = 0;
+    // live profiling: event pairs per launch, per kernel class
+    struct ProfRec { hipEvent_t a, b; int kc; double flops, bytes; };
+    bool prof_on = false;
+    std::vector<ProfRec> prof;
+    std::vector<hipEvent_t> ev_pool;
+    size_t ev_used = 0;
+    double prof_ms[3] = {0, 0, 0}, prof_fl[3] = {0, 0, 0}, prof_by[3] = {0, 0, 0};
+    long long prof_n[3] = {0, 0, 0};
+
+    float* w(size_t off) const { return arena.as<float>() + off; }
+    bf16* wb(size_t off) const { return arena_bf.as<bf16>() + off; }
+};
+
+namespace {
+
+size_t add_entry(pfm_handle* h, const std::string& name, std::vector<int64_t> shape, int kind = 0,
+                 bool gemm = false) {
+    WEntry e;
+    e.shape = shape;
+    e.numel = 1;
+    for (auto s : shape) e.numel *= (size_t)s;
+    e.kind = kind;
+    if (kind != 2) {
+        e.off = h->arena_elems;
+        h->arena_elems += (e.numel + 63) & ~size_t(63);   // 256-B aligned tensors
+        if (gemm) h->gemm_ranges.push_back({e.off, e.numel});
+        h->missing++;
+    }
+    h->reg[name] = e;
+    return e.off;
+}
+
+void build_registry(pfm_handle* h) {
+    const pfm_config& c = h->cfg;
+    const int D = c.d_model, F = c.ffn, K = c.kernel_size, I = c.input_size, V = c.vocab_size;
+    for (int l = 0; l < c.enc_blocks; ++l) {
+        const std::string p = l == 0 ? "encoder.encoders0.0" : "encoder.encoders." + std::to_string(l - 1);
+        const int din = l == 0 ? I : D;
+        EncLayer L;
+        L.din = din;
+        L.wo = add_entry(h, p + ".self_attn.linear_out.weight", {D, D}, 0, true);
+        L.bo = add_entry(h, p + ".self_attn.linear_out.bias", {D});
+        L.wqkv = add_entry(h, p + ".self_attn.linear_q_k_v.weight", {3 * D, din}, 0, true);
+        L.bqkv = add_entry(h, p + ".self_attn.linear_q_k_v.bias", {3 * D});
+        L.fsmn = add_entry(h, p + ".self_attn.fsmn_block.weight", {D, 1, K});
+        L.w1 = add_entry(h, p + ".feed_forward.w_1.weight", {F, D}, 0, true);
+        L.b1 = add_entry(h, p + ".feed_forward.w_1.bias", {F});
+        L.w2 = add_entry(h, p + ".feed_forward.w_2.weight", {D, F}, 0, true);
+        L.b2 = add_entry(h, p + ".feed_forward.w_2.bias", {D});
+        L.ln1g = add_entry(h, p + ".norm1.weight", {din});
+        L.ln1b = add_entry(h, p + ".norm1.bias", {din});
+        L.ln2g = add_entry(h, p + ".norm2.weight", {D});
+        L.ln2b = add_entry(h, p + ".norm2.bias", {D});
+        h->enc.push_back(L);
+    }
+    h->an_g = add_entry(h, "encoder.after_norm.weight", {D});
+    h->an_b = add_entry(h, "encoder.after_norm.bias", {D});
+    add_entry(h, "decoder.embed.0.weight", {V, D}, 2);
+    h->dan_g = add_entry(h, "decoder.after_norm.weight", {D});
+    h->dan_b = add_entry(h, "decoder.after_norm.bias", {D});
+    h->out_w = add_entry(h, "decoder.output_layer.weight", {V, D}, 0, true);
+    h->out_b = add_entry(h, "decoder.output_layer.bias", {V});
+    // cross-attention K/V projections of all decoder layers live in one [nL*2D, D] matrix so the
+    // encoder memory is projected by ONE GEMM (N = nL*2D) instead of nL small ones.
+    const size_t kv_rows = (size_t)c.dec_blocks * 2 * D;
+    h->wkv_all = h->arena_elems;
+    h->arena_elems += (kv_rows * D + 63) & ~size_t(63);
+    h->gemm_ranges.push_back({h->wkv_all, kv_rows * D});
+    h->bkv_all = h->arena_elems;
+    h->arena_elems += (kv_rows + 63) & ~size_t(63);
+    for (int l = 0; l < c.dec_blocks; ++l) {
+        const std::string p = "decoder.decoders." + std::to_string(l);
+        DecLayer L;
+        L.fsmn = add_entry(h, p + ".self_attn.fsmn_block.weight", {D, 1, K});
+        L.wq = add_entry(h, p + ".src_attn.linear_q.weight", {D, D}, 0, true);
+        L.bq = add_entry(h, p + ".src_attn.linear_q.bias", {D});
+        {   // k_v slices point into wkv_all / bkv_all
+            WEntry e; e.shape = {2 * D, D}; e.numel = (size_t)2 * D * D; e.off = h->wkv_all + (size_t)l * 2 * D * D;
+            h->reg[p + ".src_attn.linear_k_v.weight"] = e; h->missing++;
+            WEntry f; f.shape = {2 * D}; f.numel = 2 * D; f.off = h->bkv_all + (size_t)l * 2 * D;
+            h->reg[p + ".src_attn.linear_k_v.bias"] = f; h->missing++;
+        }
+        L.wo = add_entry(h, p + ".src_attn.linear_out.weight", {D, D}, 0, true);
+        L.bo = add_entry(h, p + ".src_attn.linear_out.bias", {D});
+        L.w1 = add_entry(h, p + ".feed_forward.w_1.weight", {F, D}, 0, true);
+        L.b1 = add_entry(h, p + ".feed_forward.w_1.bias", {F});
+        L.w2 = add_entry(h, p + ".feed_forward.w_2.weight", {D, F}, 0, true);
+        L.ng = add_entry(h, p + ".feed_forward.norm.weight", {F});
+        L.nb = add_entry(h, p + ".feed_forward.norm.bias", {F});
+        L.n1g = add_entry(h, p + ".norm1.weight", {D});
+        L.n1b = add_entry(h, p + ".norm1.bias", {D});
+        L.n2g = add_entry(h, p + ".norm2.weight", {D});
+        L.n2b = add_entry(h, p + ".norm2.bias", {D});
+        L.n3g = add_entry(h, p + ".norm3.weight", {D});
+        L.n3b = add_entry(h, p + ".norm3.bias", {D});
+        h->dec.push_back(L);
+    }
+    const std::string p3 = "decoder.decoders3.0";
+    h->d3w1 = add_entry(h, p3 + ".feed_forward.w_1.weight", {F, D}, 0, true);
+    h->d3b1 = add_entry(h, p3 + ".feed_forward.w_1.bias", {F});
+    h->d3w2 = add_entry(h, p3 + ".feed_forward.w_2.weight", {D, F}, 0, true);
+    h->d3ng = add_entry(h, p3 + ".feed_forward.norm.weight", {F});
+    h->d3nb = add_entry(h, p3 + ".feed_forward.norm.bias", {F});
+    h->d3n1g = add_entry(h, p3 + ".norm1.weight", {D});
+    h->d3n1b = add_entry(h, p3 + ".norm1.bias", {D});
+    const int kp = c.cif_l_order + c.cif_r_order + 1;
+    h->cif_w = add_entry(h, "predictor.cif_conv1d.weight", {D, D, kp}, 1, true);
+    h->cif_b = add_entry(h, "predictor.cif_conv1d.bias", {D});
+    h->cif_ow = add_entry(h, "predictor.cif_output.weight", {1, D});
+    h->cif_ob = add_entry(h, "predictor.cif_output.bias", {1});
+}
+
+// Sinusoidal PE table [T][depth] in f32 exactly as funasr/models/transformer/embedding.py:389-413
+// evaluates it: inc = f32(log(f32 1e4)) / (depth/2 - 1); inv_i = f32 exp(-i * inc);
+// arg = f32(pos * inv_i) with pos = 1..T; sin/cos of the f32 argument, rounded to f32.
+void make_pe(std::vector<float>& pe, int T, int depth) {
+    const int half = depth / 2;
+    pe.assign((size_t)T * depth, 0.f);
+    const float lg = logf(10000.0f);
+    const float inc = (float)(lg / (double)((float)depth / 2.f - 1.f));
+    std::vector<float> inv(half);
+    for (int i = 0; i < half; ++i) inv[i] = (float)exp((double)((float)i * -inc));
+    for (int t = 0; t < T; ++t) {
+        const float pos = (float)(t + 1);
+        for (int i = 0; i < half; ++i) {
+            const float st = pos * inv[i];
+            pe[(size_t)t * depth + i] = (float)sin((double)st);
+            pe[(size_t)t * depth + half + i] = (float)cos((double)st);
+        }
+    }
+}
+
+int ensure_bf16(pfm_handle* h, hipStream_t st) {
+    if (h->bf_ready) return PFM_OK;
+    HIP_TRY(h->arena_bf.ensure(h->arena_elems * sizeof(bf16)));
+    for (auto& r : h->gemm_ranges)
+        HIP_TRY(pfm_f32_to_bf16(h->w(r.first), h->wb(r.first), (long long)r.second, st));
+    h->bf_ready = true;
+    return PFM_OK;
+}
+
+int reserve(pfm_handle* h, int B, int T) {
+    if (B <= h->capB && T <= h->capT) return PFM_OK;
+    B = std::max(B, h->capB);
+    T = std::max(T, h->capT);
+    const pfm_config& c = h->cfg;
+    const size_t D = c.d_model, F = c.ffn, I = c.input_size;
+    const size_t M = (size_t)B * T, Lc = (size_t)T + 1, Ml = (size_t)B * Lc;
+    const size_t nkv = (size_t)c.dec_blocks * 2 * D;
+    const int nt = pfm_gemm_amax_tiles(c.vocab_size);
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(h->X.ensure(M * D * 4));
+    HIP_TRY(h->Xn.ensure(M * std::max(I, D) * 4));
+    HIP_TRY(h->QKV.ensure(M * 3 * D * 4));
+    HIP_TRY(h->QKVb.ensure(M * 3 * D * 2));
+    HIP_TRY(h->F.ensure(M * D * 4));
+    HIP_TRY(h->O.ensure(M * D * 4));
+    HIP_TRY(h->Ob.ensure(M * D * 2));
+    HIP_TRY(h->H.ensure(M * F * 4));
+    HIP_TRY(h->encp.ensure((size_t)B * (T + 2) * D * 4));
+    HIP_TRY(h->encpb.ensure((size_t)B * (T + 2) * D * 2));
+    HIP_TRY(h->Hc.ensure(M * D * 4));
+    HIP_TRY(h->alphas.ensure((size_t)B * (T + 1) * 4));
+    HIP_TRY(h->peaks.ensure((size_t)B * (T + 1) * 4));
+    HIP_TRY(h->nfire.ensure((size_t)B * 4));
+    HIP_TRY(h->ntok.ensure((size_t)B * 4));
+    HIP_TRY(h->emb.ensure(Ml * D * 4));
+    HIP_TRY(h->KV.ensure(M * nkv * 4));
+    HIP_TRY(h->Xd.ensure(Ml * D * 4));
+    HIP_TRY(h->Xdn.ensure(Ml * D * 4));
+    HIP_TRY(h->Hd.ensure(Ml * F * 4));
+    HIP_TRY(h->Hdn.ensure(Ml * F * 4));
+    HIP_TRY(h->Td.ensure(Ml * D * 4));
+    HIP_TRY(h->Tdn.ensure(Ml * D * 4));
+    HIP_TRY(h->Qd.ensure(Ml * D * 4));
+    HIP_TRY(h->Od.ensure(Ml * D * 4));
+    HIP_TRY(h->Odb.ensure(Ml * D * 2));
+    HIP_TRY(h->amv.ensure(Ml * nt * 4));
+    HIP_TRY(h->ami.ensure(Ml * nt * 4));
+    HIP_TRY(h->tok_tmp.ensure(Ml * 4));
+    // zero the padded encoder layouts once: rows 0 and T+1 of each utterance are never written
+    HIP_TRY(hipMemset(h->encp.p, 0, h->encp.bytes));
+    HIP_TRY(hipMemset(h->encpb.p, 0, h->encpb.bytes));
+    // positional encoding table for the encoder input (depth = input_size)
+    std::vector<float> pe;
+    make_pe(pe, T, (int)I);
+    HIP_TRY(h->pe.ensure(pe.size() * 4));
+    HIP_TRY(hipMemcpy(h->pe.p, pe.data(), pe.size() * 4, hipMemcpyHostToDevice));
+    h->pe_T = T;
+    if (h->host_ntok_cap < B) {
+        if (h->host_ntok) (void)hipHostFree(h->host_ntok);
+        HIP_TRY(hipHostMalloc((void**)&h->host_ntok, (size_t)B * 4, 0));
+        h->host_ntok_cap = B;
+    }
+    h->capB = B;
+    h->capT = T;
+    return PFM_OK;
+}
+
+hipEvent_t next_event(pfm_handle* h) {
+    if (h->ev_used == h->ev_pool.size()) {
+        hipEvent_t e;
+        if (hipEventCreate(&e) != hipSuccess) return nullptr;
+        h->ev_pool.push_back(e);
+    }
+    return h->ev_pool[h->ev_used++];
+}
+
+// Bracket one launch with events when profiling is on.
+struct ProfScope {
+    pfm_handle* h; hipStream_t st; int kc; double fl, by; hipEvent_t a = nullptr;
+    ProfScope(pfm_handle* h_, hipStream_t st_, int kc_, double fl_, double by_) : h(h_), st(st_), kc(kc_), fl(fl_), by(by_) {
+        if (h->prof_on) { a = next_event(h); if (a) (void)hipEventRecord(a, st); }
+    }
+    ~ProfScope() {
+        if (!a) return;
+        hipEvent_t b = next_event(h);
+        if (!b) return;
+        (void)hipEventRecord(b, st);
+        h->prof.push_back({a, b, kc, fl, by});
+    }
+};
+
+void prof_collect(pfm_handle* h) {
+    for (auto& r : h->prof) {
+        float ms = 0.f;
+        if (hipEventSynchronize(r.b) == hipSuccess && hipEventElapsedTime(&ms, r.a, r.b) == hipSuccess) {
+            h->prof_ms[r.kc] += ms;
+            h->prof_fl[r.kc] += r.flops;
+            h->prof_by[r.kc] += r.bytes;
+            h->prof_n[r.kc] += 1;
+        }
+    }
+    h->prof.clear();
+    h->ev_used = 0;
+}
+
+GemmEpi epi_default() {
+    GemmEpi e;
+    memset(&e, 0, sizeof(e));
+    e.alpha = 1.f;
+    e.out_map = rowmap_plain(0);
+    e.out2_map = rowmap_plain(0);
+    return e;
+}
+
+int set_lds_limits() {
+    static bool done = false;
+    if (done) return PFM_OK;
+    done = true;
+    return PFM_OK;
+}
+
+}  // namespace
+
+// ============================================================================================
+extern "C" {
+
+void pfm_config_default(pfm_config* c) {
+    c->input_size = 560; c->d_model = 512; c->heads = 4; c->ffn = 2048; c->enc_blocks = 50; c->dec_blocks = 16;
+    c->kernel_size = 11; c->enc_sanm_shift = 0; c->dec_sanm_shift = 0; c->vocab_size = 8404;
+    c->cif_l_order = 1; c->cif_r_order = 1; c->cif_threshold = 1.f; c->tail_threshold = 0.45f;
+    c->smooth_factor = 1.f; c->noise_threshold = 0.f; c->ln_eps = 1e-12f;
+}
+
+const char* pfm_last_error(void) { return g_err.c_str(); }
+
+int pfm_create(const pfm_config* cfg, int device, pfm_handle** out) {
+    if (!cfg || !out) return fail(PFM_E_ARG, "pfm_create: null argument");
+    *out = nullptr;
+    if (cfg->d_model % cfg->heads != 0 || cfg->d_model / cfg->heads != 128)
+        return fail(PFM_E_ARG, "pfm_create: head dim must be 128");
+    if (cfg->input_size % 8 || cfg->d_model % 8 || cfg->ffn % 8 || cfg->input_size > 2048 || cfg->ffn > 2048)
+        return fail(PFM_E_ARG, "pfm_create: dims must be multiples of 8 and <= 2048");
+    if (cfg->enc_blocks < 1 || cfg->dec_blocks < 0 || cfg->kernel_size < 1 || cfg->vocab_size < 1)
+        return fail(PFM_E_ARG, "pfm_create: bad block counts");
+    if (cfg->cif_l_order != 1 || cfg->cif_r_order != 1)
+        return fail(PFM_E_ARG, "pfm_create: CIF conv must be l_order = r_order = 1");
+    int ndev = 0;
+    HIP_TRY(hipGetDeviceCount(&ndev));
+    if (device < 0 || device >= ndev) return fail(PFM_E_ARG, "pfm_create: bad device index");
+    HIP_TRY(hipSetDevice(device));
+    std::unique_ptr<pfm_handle> h(new pfm_handle());
+    h->cfg = *cfg;
+    h->device = device;
+    build_registry(h.get());
+    hipError_t e = h->arena.ensure(h->arena_elems * 4);
+    if (e != hipSuccess) return fail(PFM_E_NOMEM, "pfm_create: weight arena allocation failed");
+    HIP_TRY(hipMemset(h->arena.p, 0, h->arena.bytes));
+    *out = h.release();
+    g_err.clear();
+    return PFM_OK;
+}
+
+void pfm_destroy(pfm_handle* h) {
+    if (!h) return;
+    (void)hipSetDevice(h->device);
+    (void)hipDeviceSynchronize();
+    for (auto e : h->ev_pool) (void)hipEventDestroy(e);
+    if (h->host_ntok) (void)hipHostFree(h->host_ntok);
+    delete h;
+}
+
+int pfm_set_weight(pfm_handle* h, const char* name, const void* host_ptr, int dtype, const int64_t* shape,
+                   int ndim) {
+    if (!h || !name || !host_ptr || !shape) return fail(PFM_E_ARG, "pfm_set_weight: null argument");
+    if (dtype != PFM_F32) return fail(PFM_E_ARG, "pfm_set_weight: only PFM_F32 host tensors are accepted");
+    auto it = h->reg.find(name);
+    if (it == h->reg.end()) return fail(PFM_E_NAME, std::string("pfm_set_weight: unknown key ") + name);
+    WEntry& e = it->second;
+    if ((int)e.shape.size() != ndim) return fail(PFM_E_ARG, std::string("pfm_set_weight: rank mismatch for ") + name);
+    for (int i = 0; i < ndim; ++i)
+        if (e.shape[i] != shape[i]) return fail(PFM_E_ARG, std::string("pfm_set_weight: shape mismatch for ") + name);
+    if (e.kind == 2) return PFM_OK;
+    HIP_TRY(hipSetDevice(h->device));
+    const float* src = (const float*)host_ptr;
+    std::vector<float> tmp;
+    if (e.kind == 1) {   // Conv1d [O][I][k] -> GEMM W [O][k*I]: column k*I + i multiplies frame t-1+k, channel i
+        const int64_t O = e.shape[0], I = e.shape[1], KK = e.shape[2];
+        tmp.resize(e.numel);
+        for (int64_t o = 0; o < O; ++o)
+            for (int64_t i = 0; i < I; ++i)
+                for (int64_t k = 0; k < KK; ++k) tmp[(o * KK + k) * I + i] = src[(o * I + i) * KK + k];
+        src = tmp.data();
+    }
+    HIP_TRY(hipMemcpy(h->w(e.off), src, e.numel * 4, hipMemcpyHostToDevice));
+    if (!e.set) { e.set = true; h->missing--; }
+    h->bf_ready = false;
+    return PFM_OK;
+}
+
+int pfm_missing_weights(const pfm_handle* h) { return h ? h->missing : -1; }
+
+int pfm_reserve(pfm_handle* h, int B, int T) {
+    if (!h || B < 1 || T < 1) return fail(PFM_E_ARG, "pfm_reserve: bad arguments");
+    HIP_TRY(hipSetDevice(h->device));
+    return reserve(h, B, T);
+}
+
+int pfm_lfr_frames(int nsamp) { return pfm_fbank_frames(nsamp); }
+
+int pfm_run(pfm_handle* h, void* stream, int mode, const float* feats, const int32_t* lens, int B, int T,
+            int32_t* tokens, int L_cap, int32_t* ntok_out, float* enc_out, float* alphas_out, float* peaks_out) {
+    if (!h || !feats || !lens || !tokens || !ntok_out) return fail(PFM_E_ARG, "pfm_run: null argument");
+    if (B < 1 || T < 1 || L_cap < 0) return fail(PFM_E_ARG, "pfm_run: bad sizes");
+    if (mode != PFM_MODE_EXACT && mode != PFM_MODE_FAST) return fail(PFM_E_ARG, "pfm_run: bad mode");
+    if (h->missing) return fail(PFM_E_STATE, "pfm_run: " + std::to_string(h->missing) + " weights not set");
+    HIP_TRY(hipSetDevice(h->device));
+    hipStream_t st = (hipStream_t)stream;
+    int rc = reserve(h, B, T);
+    if (rc) return rc;
+    const bool fast = mode == PFM_MODE_FAST;
+    if (fast) { rc = ensure_bf16(h, st); if (rc) return rc; }
+    const pfm_config& c = h->cfg;
+    const int D = c.d_model, Fd = c.ffn, I = c.input_size, K = c.kernel_size, nkv = c.dec_blocks * 2 * D;
+    const long long M = (long long)B * T;
+    const int dt = fast ? DT_BF16 : DT_F32;
+    const float qscale = (float)(1.0 / sqrt((double)(D / c.heads)));   // q_h * d_k ** -0.5
+    const int lenc = (K - 1) / 2 + (c.enc_sanm_shift > 0 ? c.enc_sanm_shift : 0);
+    const int ldec = (K - 1) / 2 + (c.dec_sanm_shift > 0 ? c.dec_sanm_shift : 0);
+    if (h->prof_on && h->ev_used > 4096) prof_collect(h);
+    const double es = fast ? 2.0 : 4.0;
+    // launch wrappers: algorithmic flops / bytes per launch for the live roofline
+    auto GEMM = [&](int dtp, const void* A, RowMap am, const void* Wt, long long ldw, int Mm, int N, int Kk,
+                    const GemmEpi& e) -> hipError_t {
+        const double fl = 2.0 * Mm * N * Kk;
+        const double by = ((double)Mm * Kk + (double)N * Kk) * es +
+                          (double)Mm * N * (e.out ? (e.out_dtype == DT_F32 ? 4.0 : 2.0) : 0.0) +
+                          (e.res0 ? 4.0 * Mm * N : 0.0) + (e.res1 ? 4.0 * Mm * N : 0.0) + (e.out2 ? 2.0 * Mm * N : 0.0);
+        ProfScope ps(h, st, PFM_K_GEMM, fl, by);
+        return pfm_gemm(dtp, A, am, Wt, ldw, Mm, N, Kk, e, st);
+    };
+    auto ATTN = [&](int dtp, const void* q, RowMap qm, const void* k, RowMap km, const void* v, RowMap vm, float* o,
+                    long long ldo, void* o2, const int* kl, int Bb, int Tq, int Tk) -> hipError_t {
+        const double dk = c.d_model / c.heads;
+        const double fl = 4.0 * Bb * Tq * (double)Tk * dk * c.heads;
+        const double by = ((double)Bb * Tq + 2.0 * Bb * Tk) * c.d_model * es + (double)Bb * Tq * c.d_model * (o ? 4 : 2);
+        ProfScope ps(h, st, PFM_K_ATTN, fl, by);
+        return pfm_attention(dtp, q, qm, k, km, v, vm, o, ldo, o2, kl, Bb, Tq, Tk, c.heads, (int)dk, qscale, st);
+    };
+    auto OTHER = [&](double by) { return ProfScope(h, st, PFM_K_OTHER, 0.0, by); };
+    (void)OTHER;
+    auto W = [&](size_t off) -> const void* { return fast ? (const void*)h->wb(off) : (const void*)h->w(off); };
+    auto P = [&](size_t off) -> const float* { return h->w(off); };
+    float* X = h->X.as<float>();
+    void* Xn = h->Xn.p;   // LN output, f32 (exact) or bf16 (fast)
+    float* QKV = h->QKV.as<float>();
+    bf16* QKVb = h->QKVb.as<bf16>();
+    float* Fm = h->F.as<float>();
+    float* O = h->O.as<float>();
+    bf16* Ob = h->Ob.as<bf16>();
+    void* Hh = h->H.p;
+    const RowMap plain = rowmap_plain(0);
+
+    // ---------------- encoder (sanm/encoder.py:361-430) ----------------
+    for (int l = 0; l < c.enc_blocks; ++l) {
+        const EncLayer& L = h->enc[l];
+        const int din = L.din;
+        if (l == 0)   // x = feats * sqrt(d_model) + PE ; LN1
+            HIP_TRY(pfm_layernorm(feats, rowmap_plain(I), (int)M, I, P(L.ln1g), P(L.ln1b), c.ln_eps, h->pe.as<float>(),
+                                  T, sqrtf((float)D), Xn, rowmap_plain(I), dt, nullptr, plain, 0, st));
+        else
+            HIP_TRY(pfm_layernorm(X, rowmap_plain(D), (int)M, D, P(L.ln1g), P(L.ln1b), c.ln_eps, nullptr, 0, 1.f, Xn,
+                                  rowmap_plain(D), dt, nullptr, plain, 0, st));
+        {   // q|k|v = LN1(x) Wqkv^T + b
+            GemmEpi e = epi_default();
+            e.bias = P(L.bqkv);
+            e.out = QKV; e.out_map = rowmap_plain(3 * D); e.out_dtype = DT_F32;
+            if (fast) { e.out2 = QKVb; e.out2_map = rowmap_plain(3 * D); }
+            HIP_TRY(GEMM(dt, Xn, rowmap_plain(din), W(L.wqkv), din, (int)M, 3 * D, din, e));
+        }
+        // FSMN memory on v (attention.py:207-223)
+        HIP_TRY(pfm_fsmn(QKV + 2 * D, rowmap_plain(3 * D), lens, B, T, D, P(L.fsmn), K, lenc, nullptr, Fm, nullptr, st));
+        // masked MHA
+        if (fast)
+            HIP_TRY(ATTN(DT_BF16, QKVb, rowmap_plain(3 * D), QKVb + D, rowmap_plain(3 * D), QKVb + 2 * D,
+                                  rowmap_plain(3 * D), nullptr, D, Ob, lens, B, T, T));
+        else
+            HIP_TRY(ATTN(DT_F32, QKV, rowmap_plain(3 * D), QKV + D, rowmap_plain(3 * D), QKV + 2 * D,
+                                  rowmap_plain(3 * D), O, D, nullptr, lens, B, T, T));
+        {   // x = (x +) linear_out(att) + fsmn   (encoder.py:120-137: no residual when in != out)
+            GemmEpi e = epi_default();
+            e.bias = P(L.bo);
+            e.res0 = Fm; e.ld_res0 = D;
+            if (din == D) { e.res1 = X; e.ld_res1 = D; }
+            e.out = X; e.out_map = rowmap_plain(D); e.out_dtype = DT_F32;
+            HIP_TRY(GEMM(dt, fast ? (const void*)Ob : (const void*)O, rowmap_plain(D), W(L.wo), D, (int)M, D, D, e));
+        }
+        HIP_TRY(pfm_layernorm(X, rowmap_plain(D), (int)M, D, P(L.ln2g), P(L.ln2b), c.ln_eps, nullptr, 0, 1.f, Xn,
+                              rowmap_plain(D), dt, nullptr, plain, 0, st));
+        {   // h = relu(LN2(x) W1^T + b1)
+            GemmEpi e = epi_default();
+            e.bias = P(L.b1); e.relu = 1;
+            e.out = Hh; e.out_map = rowmap_plain(Fd); e.out_dtype = dt;
+            HIP_TRY(GEMM(dt, Xn, rowmap_plain(D), W(L.w1), D, (int)M, Fd, D, e));
+        }
+        {   // x = x + h W2^T + b2
+            GemmEpi e = epi_default();
+            e.bias = P(L.b2);
+            e.res0 = X; e.ld_res0 = D;
+            e.out = X; e.out_map = rowmap_plain(D); e.out_dtype = DT_F32;
+            HIP_TRY(GEMM(dt, Hh, rowmap_plain(Fd), W(L.w2), Fd, (int)M, D, Fd, e));
+        }
+    }
+    // after_norm -> zero-padded [B][T+2][D] (row 0 and T+1 of each utterance stay zero)
+    float* encp = h->encp.as<float>();
+    bf16* encpb = h->encpb.as<bf16>();
+    const RowMap encmap = rowmap_seg(T, (long long)(T + 2) * D, D);
+    // rows 0 and T+1 of every utterance are the conv / tail zero rows; the workspace may hold a
+    // previous call's layout (other T), so clear them each call (2*B rows, negligible)
+    HIP_TRY(hipMemset2DAsync(encp, (size_t)(T + 2) * D * 4, 0, (size_t)D * 4, B, st));
+    HIP_TRY(hipMemset2DAsync(encp + (size_t)(T + 1) * D, (size_t)(T + 2) * D * 4, 0, (size_t)D * 4, B, st));
+    if (fast) {
+        HIP_TRY(hipMemset2DAsync(encpb, (size_t)(T + 2) * D * 2, 0, (size_t)D * 2, B, st));
+        HIP_TRY(hipMemset2DAsync(encpb + (size_t)(T + 1) * D, (size_t)(T + 2) * D * 2, 0, (size_t)D * 2, B, st));
+    }
+    HIP_TRY(pfm_layernorm(X, rowmap_plain(D), (int)M, D, P(h->an_g), P(h->an_b), c.ln_eps, nullptr, 0, 1.f,
+                          encp + D, encmap, DT_F32, fast ? (void*)(encpb + D) : nullptr, encmap, DT_BF16, st));
+    if (enc_out)
+        HIP_TRY(hipMemcpy2DAsync(enc_out, (size_t)T * D * 4, encp + D, (size_t)(T + 2) * D * 4, (size_t)T * D * 4, B,
+                                 hipMemcpyDeviceToDevice, st));
+
+    // ---------------- predictor (cif_predictor.py:202-253) ----------------
+    {   // relu(conv1d(k=3, pad 1)) as a GEMM over 3 adjacent rows of the padded layout (K = 3D)
+        GemmEpi e = epi_default();
+        e.bias = P(h->cif_b); e.relu = 1;
+        e.out = h->Hc.p; e.out_map = rowmap_plain(D); e.out_dtype = DT_F32;
+        const void* A = fast ? (const void*)encpb : (const void*)encp;
+        HIP_TRY(GEMM(dt, A, rowmap_seg(T, (long long)(T + 2) * D, D), W(h->cif_w), 3 * D, (int)M, D, 3 * D, e));
+    }
+    float* alphas = h->alphas.as<float>();
+    float* peaks = h->peaks.as<float>();
+    int* ntok = h->ntok.as<int>();
+    const int Lc = T + 1;
+    HIP_TRY(pfm_cif_alpha(h->Hc.as<float>(), D, P(h->cif_ow), P(h->cif_ob), lens, B, T, c.smooth_factor,
+                          c.noise_threshold, c.tail_threshold, alphas, st));
+    HIP_TRY(pfm_cif_fire(alphas, encp + D, rowmap_seg(T + 1, (long long)(T + 2) * D, D), B, T, D, Lc,
+                         h->emb.as<float>(), peaks, h->nfire.as<int>(), ntok, st));
+    if (alphas_out) HIP_TRY(hipMemcpyAsync(alphas_out, alphas, (size_t)B * (T + 1) * 4, hipMemcpyDeviceToDevice, st));
+    if (peaks_out) HIP_TRY(hipMemcpyAsync(peaks_out, peaks, (size_t)B * (T + 1) * 4, hipMemcpyDeviceToDevice, st));
+    HIP_TRY(hipMemcpyAsync(ntok_out, ntok, (size_t)B * 4, hipMemcpyDeviceToDevice, st));
+    HIP_TRY(hipMemcpyAsync(h->host_ntok, ntok, (size_t)B * 4, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    int L = 0;
+    for (int b = 0; b < B; ++b) L = std::max(L, (int)h->host_ntok[b]);
+    L = std::min(L, Lc);   // ntok <= fires <= T+1 frames (+ rounding); decoder never exceeds the CIF rows
+    if (L_cap > 0) HIP_TRY(pfm_fill_i32(tokens, (long long)B * L_cap, -1, st));
+    if (L < 1 || c.dec_blocks < 0) return PFM_OK;   // model.py:514-515: nothing to decode
+
+    // ---------------- decoder (paraformer/decoder.py:359-411) ----------------
+    const long long Ml = (long long)B * L;
+    float* Xd = h->Xd.as<float>();
+    void* Xdn = h->Xdn.p;
+    float* Hd = h->Hd.as<float>();
+    void* Hdn = h->Hdn.p;
+    float* Td = h->Td.as<float>();
+    float* Tdn = h->Tdn.as<float>();
+    void* Qd = h->Qd.p;
+    float* Od = h->Od.as<float>();
+    bf16* Odb = h->Odb.as<bf16>();
+    void* KV = h->KV.p;
+    // compact CIF embeddings [B][T+1][D] -> decoder rows [B][L][D] (acoustic_embeds[:, :L])
+    HIP_TRY(hipMemcpy2DAsync(Xd, (size_t)L * D * 4, h->emb.p, (size_t)Lc * D * 4, (size_t)L * D * 4, B,
+                             hipMemcpyDeviceToDevice, st));
+    {   // memory K|V for all decoder layers: [B*T, nL*2D] = enc . Wkv_all^T + b
+        GemmEpi e = epi_default();
+        e.bias = P(h->bkv_all);
+        e.out = KV; e.out_map = rowmap_plain(nkv); e.out_dtype = dt;
+        const void* A = fast ? (const void*)(encpb + D) : (const void*)(encp + D);
+        HIP_TRY(GEMM(dt, A, encmap, W(h->wkv_all), D, (int)M, nkv, D, e));
+    }
+    auto ffn = [&](const float* x, size_t lng, size_t lnb, size_t w1, size_t b1, size_t fng, size_t fnb, size_t w2,
+                   const float* res, float* out) -> int {
+        // out = (res +) W2 . LN_F(relu(W1 . LN(x) + b1))     (sanm/positionwise_feed_forward.py:26-33)
+        HIP_TRY(pfm_layernorm(x, rowmap_plain(D), (int)Ml, D, P(lng), P(lnb), c.ln_eps, nullptr, 0, 1.f, Xdn,
+                              rowmap_plain(D), dt, nullptr, plain, 0, st));
+        GemmEpi e = epi_default();
+        e.bias = P(b1); e.relu = 1;
+        e.out = Hd; e.out_map = rowmap_plain(Fd); e.out_dtype = DT_F32;
+        HIP_TRY(GEMM(dt, Xdn, rowmap_plain(D), W(w1), D, (int)Ml, Fd, D, e));
+        HIP_TRY(pfm_layernorm(Hd, rowmap_plain(Fd), (int)Ml, Fd, P(fng), P(fnb), c.ln_eps, nullptr, 0, 1.f, Hdn,
+                              rowmap_plain(Fd), dt, nullptr, plain, 0, st));
+        GemmEpi e2 = epi_default();
+        if (res) { e2.res0 = res; e2.ld_res0 = D; }
+        e2.out = out; e2.out_map = rowmap_plain(D); e2.out_dtype = DT_F32;
+        HIP_TRY(GEMM(dt, Hdn, rowmap_plain(Fd), W(w2), Fd, (int)Ml, D, Fd, e2));
+        return PFM_OK;
+    };
+    for (int l = 0; l < c.dec_blocks; ++l) {
+        const DecLayer& Lr = h->dec[l];
+        // t = FFN(LN1(x)); x = x + FSMN(LN2(t))   (decoder.py:97-107)
+        rc = ffn(Xd, Lr.n1g, Lr.n1b, Lr.w1, Lr.b1, Lr.ng, Lr.nb, Lr.w2, nullptr, Td);
+        if (rc) return rc;
+        HIP_TRY(pfm_layernorm(Td, rowmap_plain(D), (int)Ml, D, P(Lr.n2g), P(Lr.n2b), c.ln_eps, nullptr, 0, 1.f, Tdn,
+                              rowmap_plain(D), DT_F32, nullptr, plain, 0, st));
+        HIP_TRY(pfm_fsmn(Tdn, rowmap_plain(D), ntok, B, L, D, P(Lr.fsmn), K, ldec, Xd, Xd, nullptr, st));
+        // x = x + CrossAtt(LN3(x), memory)   (decoder.py:109-119)
+        HIP_TRY(pfm_layernorm(Xd, rowmap_plain(D), (int)Ml, D, P(Lr.n3g), P(Lr.n3b), c.ln_eps, nullptr, 0, 1.f, Xdn,
+                              rowmap_plain(D), dt, nullptr, plain, 0, st));
+        {
+            GemmEpi e = epi_default();
+            e.bias = P(Lr.bq);
+            e.out = Qd; e.out_map = rowmap_plain(D); e.out_dtype = dt;
+            HIP_TRY(GEMM(dt, Xdn, rowmap_plain(D), W(Lr.wq), D, (int)Ml, D, D, e));
+        }
+        {
+            const size_t es = fast ? 2 : 4;
+            const char* kvb = (const char*)KV + (size_t)l * 2 * D * es;
+            HIP_TRY(ATTN(dt, Qd, rowmap_plain(D), kvb, rowmap_plain(nkv), kvb + (size_t)D * es,
+                                  rowmap_plain(nkv), fast ? nullptr : Od, D, fast ? (void*)Odb : nullptr, lens, B, L, T));
+        }
+        {
+            GemmEpi e = epi_default();
+            e.bias = P(Lr.bo);
+            e.res0 = Xd; e.ld_res0 = D;
+            e.out = Xd; e.out_map = rowmap_plain(D); e.out_dtype = DT_F32;
+            HIP_TRY(GEMM(dt, fast ? (const void*)Odb : (const void*)Od, rowmap_plain(D), W(Lr.wo), D, (int)Ml, D, D,
+                             e));
+        }
+    }
+    // decoders3: x = FFN(LN1(x)), no residual (decoder.py:97-100 with self_attn = src_attn = None)
+    rc = ffn(Xd, h->d3n1g, h->d3n1b, h->d3w1, h->d3b1, h->d3ng, h->d3nb, h->d3w2, nullptr, Xd);
+    if (rc) return rc;
+    HIP_TRY(pfm_layernorm(Xd, rowmap_plain(D), (int)Ml, D, P(h->dan_g), P(h->dan_b), c.ln_eps, nullptr, 0, 1.f, Xdn,
+                          rowmap_plain(D), dt, nullptr, plain, 0, st));
+    {   // output layer with fused row-argmax (logits never written)
+        const int ntl = pfm_gemm_amax_tiles(c.vocab_size);
+        GemmEpi e = epi_default();
+        e.bias = P(h->out_b);
+        e.amax_val = h->amv.as<float>(); e.amax_idx = h->ami.as<int>(); e.n_tiles = ntl;
+        e.out = nullptr;
+        HIP_TRY(GEMM(dt, Xdn, rowmap_plain(D), W(h->out_w), D, (int)Ml, c.vocab_size, D, e));
+        if (L_cap > 0)
+            HIP_TRY(pfm_argmax_reduce(h->amv.as<float>(), h->ami.as<int>(), ntl, B, L, ntok, L_cap, tokens, nullptr, st));
+    }
+    return PFM_OK;
+}
+
+int pfm_fbank(pfm_handle* h, void* stream, const float* wav, const int32_t* nsamp, int B, int S_max,
+              const float* cmvn, float* feats, int T_cap, int32_t* T_out) {
+    if (!h || !wav || !nsamp || !feats || !T_out) return fail(PFM_E_ARG, "pfm_fbank: null argument");
+    if (B < 1 || S_max < 1 || T_cap < 1) return fail(PFM_E_ARG, "pfm_fbank: bad sizes");
+    if (pfm_fbank_frames(S_max) > T_cap) return fail(PFM_E_ARG, "pfm_fbank: T_cap smaller than LFR frames of S_max");
+    HIP_TRY(hipSetDevice(h->device));
+    hipStream_t st = (hipStream_t)stream;
+    if (!h->fb_tab_ready) {
+        std::vector<unsigned char> tab(pfm_fbank_table_bytes(), 0);
+        float* melw = (float*)tab.data();
+        int* lo = (int*)(tab.data() + 80 * 256 * 4);
+        int* hi = lo + 80;
+        float* window = (float*)(hi + 80);
+        double* tw = (double*)(tab.data() + pfm_fbank_twoff());
+        pfm_fbank_tables(melw, lo, hi, window, tw);
+        HIP_TRY(h->fb_tab.ensure(tab.size()));
+        HIP_TRY(hipMemcpy(h->fb_tab.p, tab.data(), tab.size(), hipMemcpyHostToDevice));
+        h->fb_tab_ready = true;
+    }
+    const int N_cap = std::max(1, pfm_fbank_nframes(S_max));
+    HIP_TRY(h->fb_ws.ensure((size_t)B * N_cap * 80 * 4));
+    HIP_TRY(pfm_fbank_launch(wav, nsamp, B, S_max, cmvn, h->fb_tab.as<unsigned char>(), h->fb_ws.as<float>(), N_cap,
+                             feats, T_cap, T_out, st));
+    return PFM_OK;
+}
+
+int pfm_profile(pfm_handle* h, int enable) {
+    if (!h) return fail(PFM_E_ARG, "pfm_profile: null handle");
+    prof_collect(h);
+    for (int k = 0; k < 3; ++k) { h->prof_ms[k] = h->prof_fl[k] = h->prof_by[k] = 0; h->prof_n[k] = 0; }
+    h->prof_on = enable != 0;
+    return PFM_OK;
+}
+
+int pfm_profile_read(pfm_handle* h, int kc, double* ms, double* flops, double* bytes, int64_t* launches) {
+    if (!h || kc < 0 || kc > 2) return fail(PFM_E_ARG, "pfm_profile_read: bad arguments");
+    prof_collect(h);
+    if (ms) *ms = h->prof_ms[kc];
+    if (flops) *flops = h->prof_fl[kc];
+    if (bytes) *bytes = h->prof_by[kc];
+    if (launches) *launches = h->prof_n[kc];
+    return PFM_OK;
+}
+
+// ---------------- single-op entry points ----------------
+int pfm_op_gemm(void* stream, int dtype, const void* A, const void* Wt, const float* bias, const float* res, float* C,
+                int M, int N, int K, int act) {
+    GemmEpi e = epi_default();
+    e.bias = bias; e.relu = act == 1;
+    if (res) { e.res0 = res; e.ld_res0 = N; }
+    e.out = C; e.out_map = rowmap_plain(N); e.out_dtype = DT_F32;
+    HIP_TRY(pfm_gemm(dtype, A, rowmap_plain(K), Wt, K, M, N, K, e, (hipStream_t)stream));
+    return PFM_OK;
+}
+
+int pfm_op_attention(void* stream, int dtype, const void* q, const void* k, const void* v, const int32_t* klen,
+                     float* out, int B, int Tq, int Tk, int heads, float scale) {
+    const int D = heads * 128;
+    HIP_TRY(pfm_attention(dtype, q, rowmap_plain(D), k, rowmap_plain(D), v, rowmap_plain(D), out, D, nullptr, klen, B,
+                          Tq, Tk, heads, 128, scale, (hipStream_t)stream));
+    return PFM_OK;
+}
+
+int pfm_op_layernorm(void* stream, const float* x, const float* g, const float* b, float* out, int M, int D,
+                     float eps) {
+    HIP_TRY(pfm_layernorm(x, rowmap_plain(D), M, D, g, b, eps, nullptr, 0, 1.f, out, rowmap_plain(D), DT_F32,
+                          nullptr, rowmap_plain(0), 0, (hipStream_t)stream));
+    return PFM_OK;
+}
+
+int pfm_op_fsmn(void* stream, const float* v, const int32_t* len, const float* w, const float* res, float* out,
+                int B, int T, int D, int K, int left) {
+    HIP_TRY(pfm_fsmn(v, rowmap_plain(D), len, B, T, D, w, K, left, res, out, nullptr, (hipStream_t)stream));
+    return PFM_OK;
+}
+
+int pfm_op_cif(void* stream, const float* alphas, const float* hidden, float* emb, float* peaks, int32_t* n_fire,
+               int32_t* ntok, int B, int T, int D, int L_cap) {
+    HIP_TRY(pfm_cif_fire(alphas, hidden, rowmap_plain(D), B, T, D, L_cap, emb, peaks, n_fire, ntok,
+                         (hipStream_t)stream));
+    return PFM_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,83 @@
+// Shared device/host helpers for the MI355X (gfx950) Paraformer path.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16;
+
+#define PFM_WAVE 64
+
+// dtype codes shared with include/pfm.h
+enum { DT_F32 = 0, DT_BF16 = 1 };
+
+__device__ __forceinline__ float bf2f(bf16 x) { return (float)x; }
+__device__ __forceinline__ bf16 f2bf(float x) { return (bf16)x; }   // RNE, v_cvt_pk_bf16_f32 on gfx950
+
+template <typename T> __device__ __forceinline__ float to_f(T x);
+template <> __device__ __forceinline__ float to_f<float>(float x) { return x; }
+template <> __device__ __forceinline__ float to_f<bf16>(bf16 x) { return (float)x; }
+template <typename T> __device__ __forceinline__ T from_f(float x);
+template <> __device__ __forceinline__ float from_f<float>(float x) { return x; }
+template <> __device__ __forceinline__ bf16 from_f<bf16>(float x) { return (bf16)x; }
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+// Row addressing shared by GEMM operands and element kernels: logical row m lives at
+//   base + (m / rows_per_seg) * seg_stride + (m % rows_per_seg) * ld
+// (rows_per_seg == 0 means a plain [M, ld] matrix). Lets the predictor/cross-attention
+// read the encoder output from its zero-padded [B][T+2][D] layout without copies.
+struct RowMap {
+    int rows_per_seg;
+    long long seg_stride;
+    long long ld;
+    __host__ __device__ __forceinline__ long long off(long long m) const {
+        if (rows_per_seg <= 0) return m * ld;
+        return (m / rows_per_seg) * seg_stride + (m % rows_per_seg) * ld;
+    }
+};
+static inline RowMap rowmap_plain(long long ld) { RowMap r; r.rows_per_seg = 0; r.seg_stride = 0; r.ld = ld; return r; }
+static inline RowMap rowmap_seg(int rows, long long seg_stride, long long ld) {
+    RowMap r; r.rows_per_seg = rows; r.seg_stride = seg_stride; r.ld = ld; return r;
+}
+
+// ---- host-side launch helpers (all return hipError_t) --------------------------------
+#define PFM_LAUNCH_CHECK() do { hipError_t _e = hipGetLastError(); if (_e != hipSuccess) return _e; } while (0)
+
+// Epilogue descriptor for C = act(A . W^T + bias) (+ res0) (+ res1), stored as f32 or bf16.
+struct GemmEpi {
+    const float* bias;      // [N] or null
+    const float* res0;      // residual #1 [M, ld_res0] f32 or null (added after activation)
+    const float* res1;      // residual #2 (same layout as res0, ld_res1) or null
+    long long ld_res0, ld_res1;
+    int relu;               // 1: relu before residual adds
+    float alpha;            // scale applied to A.W^T before bias
+    void* out;              // C
+    RowMap out_map;         // row addressing of C (and of residuals via their own ld)
+    int out_dtype;          // DT_F32 / DT_BF16
+    // optional second output (bf16 copy of the f32 result, same RowMap) for fast mode
+    void* out2;
+    RowMap out2_map;
+    // optional fused row-argmax (output layer): per (row, n-tile) best value + index
+    float* amax_val;        // [M, n_tiles] or null
+    int* amax_idx;
+    int n_tiles;
+};

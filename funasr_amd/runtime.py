@@ -1,0 +1,260 @@
+"""ctypes binding of libpfm_hip.so (include/pfm.h) + a torch-facing engine wrapper.
+
+The HIP library is the only compute path: importing this module does not require a GPU,
+but constructing a `PfmEngine` does, and there is no CPU fallback anywhere in the
+product — a missing library or device raises `PfmError`.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Dict, Optional
+
+import numpy as np
+
+from .config import ParaformerConfig
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("PFM_LIB", os.path.join(_HERE, "_lib", "libpfm_hip.so"))
+
+PFM_F32, PFM_BF16 = 0, 1
+MODE_EXACT, MODE_FAST = 0, 1
+MODES = {"exact": MODE_EXACT, "fp32": MODE_EXACT, "fast": MODE_FAST, "bf16": MODE_FAST}
+
+# every symbol include/pfm.h declares (checked by tests/test_abi.py)
+ABI_SYMBOLS = ("pfm_config_default", "pfm_create", "pfm_set_weight", "pfm_missing_weights", "pfm_reserve",
+               "pfm_run", "pfm_fbank", "pfm_lfr_frames", "pfm_last_error", "pfm_destroy", "pfm_op_gemm",
+               "pfm_op_attention", "pfm_op_layernorm", "pfm_op_fsmn", "pfm_op_cif", "pfm_profile",
+               "pfm_profile_read")
+
+
+class PfmError(RuntimeError):
+    pass
+
+
+class PfmConfig(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int32) for n in ("input_size", "d_model", "heads", "ffn", "enc_blocks", "dec_blocks",
+                                               "kernel_size", "enc_sanm_shift", "dec_sanm_shift", "vocab_size",
+                                               "cif_l_order", "cif_r_order")] + \
+              [(n, ctypes.c_float) for n in ("cif_threshold", "tail_threshold", "smooth_factor", "noise_threshold",
+                                             "ln_eps")]
+
+    @classmethod
+    def from_config(cls, c: ParaformerConfig) -> "PfmConfig":
+        return cls(c.input_size, c.d_model, c.heads, c.ffn, c.enc_blocks, c.dec_blocks, c.kernel_size,
+                   c.enc_sanm_shift, c.dec_sanm_shift, c.vocab_size, c.cif_l_order, c.cif_r_order,
+                   c.cif_threshold, c.tail_threshold, c.smooth_factor, c.noise_threshold, c.ln_eps)
+
+
+_lib = None
+
+
+def load_library(path: Optional[str] = None) -> ctypes.CDLL:
+    """Load (once) and prototype libpfm_hip.so. Raises PfmError if it is missing."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise PfmError(f"{p} not found: build it with `python -m funasr_amd.build` (hipcc, gfx950)")
+    lib = ctypes.CDLL(p, mode=ctypes.RTLD_GLOBAL)
+    vp, i32, f32p, i32p = ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p
+    lib.pfm_config_default.argtypes = [ctypes.POINTER(PfmConfig)]
+    lib.pfm_config_default.restype = None
+    lib.pfm_create.argtypes = [ctypes.POINTER(PfmConfig), i32, ctypes.POINTER(vp)]
+    lib.pfm_set_weight.argtypes = [vp, ctypes.c_char_p, vp, i32, ctypes.POINTER(ctypes.c_int64), i32]
+    lib.pfm_missing_weights.argtypes = [vp]
+    lib.pfm_reserve.argtypes = [vp, i32, i32]
+    lib.pfm_run.argtypes = [vp, vp, i32, f32p, i32p, i32, i32, i32p, i32, i32p, f32p, f32p, f32p]
+    lib.pfm_fbank.argtypes = [vp, vp, f32p, i32p, i32, i32, f32p, f32p, i32, i32p]
+    lib.pfm_lfr_frames.argtypes = [i32]
+    lib.pfm_last_error.argtypes = []
+    lib.pfm_last_error.restype = ctypes.c_char_p
+    lib.pfm_destroy.argtypes = [vp]
+    lib.pfm_destroy.restype = None
+    lib.pfm_profile.argtypes = [vp, i32]
+    lib.pfm_profile_read.argtypes = [vp, i32, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
+                                     ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64)]
+    lib.pfm_op_gemm.argtypes = [vp, i32, vp, vp, f32p, f32p, f32p, i32, i32, i32, i32]
+    lib.pfm_op_attention.argtypes = [vp, i32, vp, vp, vp, i32p, f32p, i32, i32, i32, i32, ctypes.c_float]
+    lib.pfm_op_layernorm.argtypes = [vp, f32p, f32p, f32p, f32p, i32, i32, ctypes.c_float]
+    lib.pfm_op_fsmn.argtypes = [vp, f32p, i32p, f32p, f32p, f32p, i32, i32, i32, i32, i32]
+    lib.pfm_op_cif.argtypes = [vp, f32p, f32p, f32p, f32p, i32p, i32p, i32, i32, i32, i32]
+    for name in ABI_SYMBOLS:
+        getattr(lib, name)
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def check(rc: int, what: str = "pfm call"):
+    if rc != 0:
+        msg = load_library().pfm_last_error().decode(errors="replace")
+        raise PfmError(f"{what} failed ({rc}): {msg}")
+
+
+def _ptr(t) -> Optional[int]:
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+def _stream_ptr(torch, device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+class PfmEngine:
+    """One pfm_handle on one HIP device: weights + workspace, stream-ordered calls."""
+
+    def __init__(self, cfg: ParaformerConfig, device: int = 0):
+        import torch
+        if not torch.cuda.is_available():
+            raise PfmError("PfmEngine needs a ROCm GPU (torch.cuda.is_available() is False); "
+                           "there is no CPU fallback")
+        self.torch = torch
+        self.cfg = cfg
+        self.device = int(device)
+        self.lib = load_library()
+        c = PfmConfig.from_config(cfg)
+        h = ctypes.c_void_p()
+        check(self.lib.pfm_create(ctypes.byref(c), self.device, ctypes.byref(h)), "pfm_create")
+        self.h = h
+
+    def __del__(self):
+        h = getattr(self, "h", None)
+        if h is not None and h.value:
+            try:
+                self.lib.pfm_destroy(h)
+            except Exception:
+                pass
+            self.h = None
+
+    # ---- weights
+    def set_weight(self, name: str, arr) -> None:
+        a = np.ascontiguousarray(arr.detach().cpu().numpy() if hasattr(arr, "detach") else arr, dtype=np.float32)
+        shape = (ctypes.c_int64 * a.ndim)(*a.shape)
+        check(self.lib.pfm_set_weight(self.h, name.encode(), a.ctypes.data_as(ctypes.c_void_p), PFM_F32, shape,
+                                      a.ndim), f"pfm_set_weight({name})")
+
+    def load_state_dict(self, sd: Dict[str, "np.ndarray"], strict: bool = True) -> None:
+        for k, v in sd.items():
+            self.set_weight(k, v)
+        miss = self.lib.pfm_missing_weights(self.h)
+        if strict and miss:
+            raise PfmError(f"{miss} required weights missing after load_state_dict")
+
+    @property
+    def missing_weights(self) -> int:
+        return self.lib.pfm_missing_weights(self.h)
+
+    def reserve(self, B: int, T: int) -> None:
+        check(self.lib.pfm_reserve(self.h, int(B), int(T)), "pfm_reserve")
+
+    # ---- live per-kernel-class timing
+    def profile(self, enable: bool) -> None:
+        check(self.lib.pfm_profile(self.h, 1 if enable else 0), "pfm_profile")
+
+    def profile_read(self, kclass: int) -> dict:
+        ms, fl, by = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
+        n = ctypes.c_int64()
+        check(self.lib.pfm_profile_read(self.h, int(kclass), ctypes.byref(ms), ctypes.byref(fl), ctypes.byref(by),
+                                        ctypes.byref(n)), "pfm_profile_read")
+        return dict(ms=ms.value, flops=fl.value, bytes=by.value, launches=n.value)
+
+    # ---- inference
+    def run(self, feats, lens, mode="exact", L_cap: Optional[int] = None, want_enc=False, want_alphas=False):
+        """feats [B,T,in] f32 cuda, lens [B] int32 cuda -> dict of cuda tensors."""
+        torch = self.torch
+        dev = torch.device("cuda", self.device)
+        if feats.device != dev or feats.dtype != torch.float32 or not feats.is_contiguous():
+            feats = feats.to(device=dev, dtype=torch.float32).contiguous()
+        lens = lens.reshape(-1).to(device=dev, dtype=torch.int32).contiguous()
+        B, T, I = feats.shape
+        if I != self.cfg.input_size:
+            raise PfmError(f"feature dim {I} != input_size {self.cfg.input_size}")
+        if lens.numel() != B:
+            raise PfmError("lens must have one entry per utterance")
+        L_cap = T + 1 if L_cap is None else int(L_cap)
+        tokens = torch.empty((B, max(L_cap, 1)), dtype=torch.int32, device=dev)
+        ntok = torch.empty((B,), dtype=torch.int32, device=dev)
+        enc = torch.empty((B, T, self.cfg.d_model), dtype=torch.float32, device=dev) if want_enc else None
+        alphas = torch.empty((B, T + 1), dtype=torch.float32, device=dev) if want_alphas else None
+        peaks = torch.empty((B, T + 1), dtype=torch.float32, device=dev) if want_alphas else None
+        m = MODES[mode] if isinstance(mode, str) else int(mode)
+        check(self.lib.pfm_run(self.h, _stream_ptr(torch, dev), m, _ptr(feats), _ptr(lens), B, T, _ptr(tokens),
+                               L_cap, _ptr(ntok), _ptr(enc), _ptr(alphas), _ptr(peaks)), "pfm_run")
+        return dict(tokens=tokens, ntok=ntok, enc=enc, alphas=alphas, peaks=peaks)
+
+    def fbank(self, wav, nsamp, cmvn=None):
+        """wav [B,S] f32 cuda in [-1,1), nsamp [B] int32 -> (feats [B,T,560], T_out [B])."""
+        torch = self.torch
+        dev = torch.device("cuda", self.device)
+        wav = wav.to(device=dev, dtype=torch.float32).contiguous()
+        nsamp = nsamp.reshape(-1).to(device=dev, dtype=torch.int32).contiguous()
+        B, S = wav.shape
+        T_cap = max(1, self.lib.pfm_lfr_frames(int(S)))
+        feats = torch.empty((B, T_cap, 560), dtype=torch.float32, device=dev)
+        t_out = torch.empty((B,), dtype=torch.int32, device=dev)
+        cm = None
+        if cmvn is not None:
+            cm = torch.as_tensor(np.asarray(cmvn, dtype=np.float32)).to(dev).contiguous()
+        check(self.lib.pfm_fbank(self.h, _stream_ptr(torch, dev), _ptr(wav), _ptr(nsamp), B, S, _ptr(cm), _ptr(feats),
+                                 T_cap, _ptr(t_out)), "pfm_fbank")
+        return feats, t_out
+
+
+# ---- single-op helpers (kernel-level parity tests) ------------------------------------------
+def op_gemm(A, W, bias=None, res=None, relu=False):
+    import torch
+    lib = load_library()
+    dt = PFM_BF16 if A.dtype == torch.bfloat16 else PFM_F32
+    M, K = A.shape
+    N = W.shape[0]
+    C = torch.empty((M, N), dtype=torch.float32, device=A.device)
+    check(lib.pfm_op_gemm(_stream_ptr(torch, A.device), dt, _ptr(A.contiguous()), _ptr(W.contiguous()), _ptr(bias),
+                          _ptr(res), _ptr(C), M, N, K, 1 if relu else 0), "pfm_op_gemm")
+    return C
+
+
+def op_attention(q, k, v, klen, B, Tq, Tk, heads, scale):
+    import torch
+    lib = load_library()
+    dt = PFM_BF16 if q.dtype == torch.bfloat16 else PFM_F32
+    out = torch.empty((B * Tq, heads * 128), dtype=torch.float32, device=q.device)
+    check(lib.pfm_op_attention(_stream_ptr(torch, q.device), dt, _ptr(q), _ptr(k), _ptr(v),
+                               _ptr(klen.to(torch.int32)), _ptr(out), B, Tq, Tk, heads, float(scale)),
+          "pfm_op_attention")
+    return out
+
+
+def op_layernorm(x, g, b, eps):
+    import torch
+    lib = load_library()
+    M, D = x.shape
+    out = torch.empty_like(x)
+    check(lib.pfm_op_layernorm(_stream_ptr(torch, x.device), _ptr(x), _ptr(g), _ptr(b), _ptr(out), M, D, float(eps)),
+          "pfm_op_layernorm")
+    return out
+
+
+def op_fsmn(v, lens, w, B, T, left, res=None):
+    import torch
+    lib = load_library()
+    D, K = w.shape[0], w.shape[-1]
+    out = torch.empty((B * T, D), dtype=torch.float32, device=v.device)
+    check(lib.pfm_op_fsmn(_stream_ptr(torch, v.device), _ptr(v), _ptr(lens.to(torch.int32)),
+                          _ptr(w.reshape(D, K).contiguous()), _ptr(res), _ptr(out), B, T, D, K, left), "pfm_op_fsmn")
+    return out
+
+
+def op_cif(alphas, hidden, L_cap):
+    import torch
+    lib = load_library()
+    B, T1, D = hidden.shape
+    emb = torch.empty((B, L_cap, D), dtype=torch.float32, device=hidden.device)
+    peaks = torch.empty((B, T1), dtype=torch.float32, device=hidden.device)
+    nf = torch.empty((B,), dtype=torch.int32, device=hidden.device)
+    nt = torch.empty((B,), dtype=torch.int32, device=hidden.device)
+    check(lib.pfm_op_cif(_stream_ptr(torch, hidden.device), _ptr(alphas), _ptr(hidden), _ptr(emb), _ptr(peaks),
+                         _ptr(nf), _ptr(nt), B, T1 - 1, D, L_cap), "pfm_op_cif")
+    return emb, peaks, nf, nt

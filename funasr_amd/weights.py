@@ -1,0 +1,117 @@
+"""Deterministic synthetic Paraformer weights + state_dict key layout.
+
+Pretrained checkpoints cannot be fetched offline, so every parity
+run uses weights from this counter-seeded generator: each tensor is drawn from
+its own PCG64 stream keyed by (seed, crc32(state_dict key)), so any subset of
+tensors can be regenerated independently, on any host, bit-identically.
+
+Distribution follows torch's default module init (what the survey's reference
+timings used): Linear/Conv weights and biases ~ U(-1/sqrt(fan_in), +1/sqrt(fan_in)).
+LayerNorm gamma/beta are perturbed off (1, 0) so the affine path is exercised.
+
+Key names and shapes are exactly the reference `model.state_dict()` of
+`funasr/models/paraformer/model.py:29`, so these dicts load
+into the reference with `load_state_dict(strict=True)` and a real `model.pt`
+state_dict can be fed to the HIP path unchanged.
+"""
+from __future__ import annotations
+
+import zlib
+from typing import Dict, Iterator, List, Tuple
+
+import numpy as np
+
+from .config import ParaformerConfig
+
+Shape = Tuple[int, ...]
+
+
+def param_layout(cfg: ParaformerConfig) -> List[Tuple[str, Shape, int]]:
+    """(key, shape, fan_in) for every parameter, in state_dict order.
+
+    fan_in == 0 marks LayerNorm gamma ('ln_w') / beta ('ln_b') via negative codes.
+    """
+    D, F, K, I, V = cfg.d_model, cfg.ffn, cfg.kernel_size, cfg.input_size, cfg.vocab_size
+    out: List[Tuple[str, Shape, int]] = []
+
+    def lin(name, o, i, bias=True):
+        out.append((f"{name}.weight", (o, i), i))
+        if bias:
+            out.append((f"{name}.bias", (o,), i))
+
+    def ln(name, n):
+        out.append((f"{name}.weight", (n,), -1))
+        out.append((f"{name}.bias", (n,), -2))
+
+    def enc_layer(p, din):
+        lin(f"{p}.self_attn.linear_out", D, D)
+        lin(f"{p}.self_attn.linear_q_k_v", 3 * D, din)
+        out.append((f"{p}.self_attn.fsmn_block.weight", (D, 1, K), K))
+        lin(f"{p}.feed_forward.w_1", F, D)
+        lin(f"{p}.feed_forward.w_2", D, F)
+        ln(f"{p}.norm1", din)
+        ln(f"{p}.norm2", D)
+
+    enc_layer("encoder.encoders0.0", I)
+    for i in range(cfg.enc_blocks - 1):
+        enc_layer(f"encoder.encoders.{i}", D)
+    ln("encoder.after_norm", D)
+
+    out.append(("decoder.embed.0.weight", (V, D), -3))
+    ln("decoder.after_norm", D)
+    lin("decoder.output_layer", V, D)
+    for i in range(cfg.dec_blocks):
+        p = f"decoder.decoders.{i}"
+        out.append((f"{p}.self_attn.fsmn_block.weight", (D, 1, K), K))
+        lin(f"{p}.src_attn.linear_q", D, D)
+        lin(f"{p}.src_attn.linear_k_v", 2 * D, D)
+        lin(f"{p}.src_attn.linear_out", D, D)
+        lin(f"{p}.feed_forward.w_1", F, D)
+        lin(f"{p}.feed_forward.w_2", D, F, bias=False)
+        ln(f"{p}.feed_forward.norm", F)
+        ln(f"{p}.norm1", D)
+        ln(f"{p}.norm2", D)
+        ln(f"{p}.norm3", D)
+    p = "decoder.decoders3.0"
+    lin(f"{p}.feed_forward.w_1", F, D)
+    lin(f"{p}.feed_forward.w_2", D, F, bias=False)
+    ln(f"{p}.feed_forward.norm", F)
+    ln(f"{p}.norm1", D)
+
+    kp = cfg.cif_l_order + cfg.cif_r_order + 1
+    out.append(("predictor.cif_conv1d.weight", (D, D, kp), D * kp))
+    out.append(("predictor.cif_conv1d.bias", (D,), D * kp))
+    lin("predictor.cif_output", 1, D)
+    return out
+
+
+def _stream(seed: int, key: str) -> np.random.Generator:
+    return np.random.Generator(np.random.PCG64([seed & 0xFFFFFFFF, zlib.crc32(key.encode())]))
+
+
+def gen_tensor(seed: int, key: str, shape: Shape, fan_in: int) -> np.ndarray:
+    n = int(np.prod(shape))
+    u = _stream(seed, key).random(n, dtype=np.float32) * np.float32(2.0) - np.float32(1.0)
+    if fan_in > 0:
+        a = u * np.float32(1.0 / np.sqrt(fan_in))
+    elif fan_in == -1:          # LayerNorm gamma
+        a = np.float32(1.0) + np.float32(0.1) * u
+    elif fan_in == -2:          # LayerNorm beta
+        a = np.float32(0.1) * u
+    else:                       # embedding table (unused at inference)
+        a = u
+    return a.astype(np.float32).reshape(shape)
+
+
+def iter_weights(cfg: ParaformerConfig, seed: int = 0) -> Iterator[Tuple[str, np.ndarray]]:
+    for key, shape, fan_in in param_layout(cfg):
+        yield key, gen_tensor(seed, key, shape, fan_in)
+
+
+def make_weights(cfg: ParaformerConfig, seed: int = 0) -> Dict[str, np.ndarray]:
+    """Full synthetic state_dict as fp32 numpy arrays (220.08M params for Paraformer-large)."""
+    return dict(iter_weights(cfg, seed))
+
+
+def num_params(cfg: ParaformerConfig) -> int:
+    return int(sum(int(np.prod(s)) for _, s, _ in param_layout(cfg)))

@@ -1,0 +1,170 @@
+/*
+ * pfm.h — C ABI of libpfm_hip.so, the MI355X (gfx950) Paraformer inference path.
+ *
+ * This is the drop-in boundary for the hot path of funasr.auto.AutoModel.generate():
+ * everything under Paraformer.inference (funasr/models/paraformer/model.py:443-596) from the
+ * fbank tensor to the per-utterance argmax token ids runs behind these entry points. The
+ * host side (funasr_amd/, Python) keeps AutoModel's input handling, batching, tokenizer and
+ * result-dict contract. Plain C types only: pointers, sizes, status codes.
+ *
+ * Conventions
+ *  - Return 0 (PFM_OK) on success, a negative PFM_E_* code on failure; pfm_last_error()
+ *    returns a thread-local message for the last failing call on this thread. No C++
+ *    exception crosses the ABI.
+ *  - All tensor arguments of pfm_run / pfm_fbank / pfm_op_* are caller-owned DEVICE
+ *    memory on the handle's device, row-major, and are consumed/produced in order on the
+ *    caller's `stream` (a hipStream_t; NULL = default stream).
+ *  - A handle owns its weights and workspace; it is not re-entrant (one call at a time per
+ *    handle); distinct handles may be used from distinct threads. One handle per device.
+ */
+#ifndef PFM_H_
+#define PFM_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PFM_ABI_VERSION 1
+
+enum pfm_status {
+    PFM_OK = 0,
+    PFM_E_ARG = -1,      /* bad argument / shape */
+    PFM_E_HIP = -2,      /* HIP runtime error */
+    PFM_E_STATE = -3,    /* call out of order (e.g. run before all weights set) */
+    PFM_E_NOMEM = -4,    /* device allocation failed */
+    PFM_E_NAME = -5      /* unknown weight name */
+};
+
+enum pfm_dtype { PFM_F32 = 0, PFM_BF16 = 1 };
+
+/* Numerics mode of pfm_run.
+ *  EXACT: every contraction on v_mfma_f32_32x32x2_f32 (exact f32 FMA chains), softmax /
+ *         LayerNorm / CIF in f32 (f64 reductions) — the token-ID parity mode.
+ *  FAST : bf16 MFMA operands with f32 accumulation; f32 residual stream, LayerNorm,
+ *         softmax statistics and CIF — the throughput mode.                              */
+enum pfm_mode { PFM_MODE_EXACT = 0, PFM_MODE_FAST = 1 };
+
+/* Model dimensions; mirrors encoder_conf / decoder_conf / predictor_conf of
+ * funasr/models/paraformer/template.yaml:8-66 (Paraformer-large defaults via
+ * pfm_config_default). */
+typedef struct pfm_config {
+    int32_t input_size;      /* 560 = 80 mel x lfr_m 7 */
+    int32_t d_model;         /* 512 */
+    int32_t heads;           /* 4 (d_k must be 128) */
+    int32_t ffn;             /* 2048 */
+    int32_t enc_blocks;      /* 50 (encoders0 + 49 encoders) */
+    int32_t dec_blocks;      /* 16 (att_layer_num == num_blocks) */
+    int32_t kernel_size;     /* 11, FSMN depthwise kernel */
+    int32_t enc_sanm_shift;  /* 0 */
+    int32_t dec_sanm_shift;  /* 0 */
+    int32_t vocab_size;      /* 8404 */
+    int32_t cif_l_order;     /* 1 */
+    int32_t cif_r_order;     /* 1 */
+    float cif_threshold;     /* 1.0 */
+    float tail_threshold;    /* 0.45 */
+    float smooth_factor;     /* 1.0 */
+    float noise_threshold;   /* 0.0 */
+    float ln_eps;            /* 1e-12 */
+} pfm_config;
+
+typedef struct pfm_handle pfm_handle;
+
+/* Paraformer-large defaults. */
+void pfm_config_default(pfm_config* cfg);
+
+/* Create a handle on HIP device `device`. Replaces the model construction of
+ * AutoModel.build_model (funasr/auto/auto_model.py:176-293). */
+int pfm_create(const pfm_config* cfg, int device, pfm_handle** out);
+
+/* Upload one parameter, addressed by its reference state_dict key
+ * (e.g. "encoder.encoders.3.self_attn.linear_q_k_v.weight") with its
+ * reference shape. `host_ptr` is host memory of `dtype` (PFM_F32). Replaces
+ * load_pretrained_model (funasr/train_utils/load_pretrained_model.py:14-47).
+ * Keys that are unused at inference (decoder.embed.0.weight) are accepted and ignored. */
+int pfm_set_weight(pfm_handle* h, const char* name, const void* host_ptr, int dtype,
+                   const int64_t* shape, int ndim);
+
+/* Number of required weights still missing (0 when pfm_run may be called). */
+int pfm_missing_weights(const pfm_handle* h);
+
+/* Pre-size the workspace for batches up to B utterances of up to T LFR frames
+ * (pfm_run grows it on demand otherwise; growing is not stream-capturable). */
+int pfm_reserve(pfm_handle* h, int B, int T);
+
+/* Paraformer inference on an fbank batch — the body of Paraformer.inference for
+ * data_type="fbank" (paraformer/model.py:464-565): SAN-M encoder, CIF predictor, SAN-M
+ * decoder and the greedy argmax.
+ *   feats   [B, T, input_size] f32, frames t >= lens[b] ignored (padding)
+ *   lens    [B] int32 valid LFR frames per utterance (1..T)
+ *   tokens  [B, L_cap] int32 out: argmax token id of decoder position l < ntok[b]
+ *           (blank/sos/eos NOT removed; -1 beyond ntok[b] or when ntok[b] > L_cap)
+ *   ntok    [B] int32 out: predicted token count round(token_num) (model.py:513)
+ * Optional outputs (NULL to skip):
+ *   enc_out [B, T, d_model] f32 encoder output (after after_norm)
+ *   alphas  [B, T+1] f32 CIF weights after tail processing (cif_predictor.py:346-370)
+ *   peaks   [B, T+1] f32 CIF fire values (cif_peak)
+ * The call synchronises `stream` once (to read max(ntok), which sizes the decoder). */
+int pfm_run(pfm_handle* h, void* stream, int mode, const float* feats, const int32_t* lens,
+            int B, int T, int32_t* tokens, int L_cap, int32_t* ntok, float* enc_out,
+            float* alphas, float* peaks);
+
+/* Kaldi fbank (80 mel, 25/10 ms, hamming, dither 0, snip_edges) -> LFR (7, 6) -> CMVN for a
+ * batch of waveforms: WavFrontend.forward (funasr/frontends/wav_frontend.py:118-158).
+ *   wav     [B, S_max] f32 samples in [-1, 1) (scaled by 32768 inside, upsacle_samples)
+ *   nsamp   [B] int32 samples per utterance
+ *   cmvn    [2, 560] f32 (AddShift row, Rescale row) as parsed by load_cmvn, or NULL
+ *   feats   [B, T_cap, 560] f32 out, zero-padded;  T_out [B] int32 out: LFR frames
+ * Requires d_model-independent state only; h may be any handle on the device. */
+int pfm_fbank(pfm_handle* h, void* stream, const float* wav, const int32_t* nsamp, int B,
+              int S_max, const float* cmvn, float* feats, int T_cap, int32_t* T_out);
+
+/* Host-side frame count helper: LFR frames for n samples (ceil(nfbank / 6)). */
+int pfm_lfr_frames(int nsamp);
+
+/* Thread-local message of the last error on this thread ("" if none). */
+const char* pfm_last_error(void);
+
+void pfm_destroy(pfm_handle* h);
+
+/* ---- live kernel timing (bench / roofline) ----
+ * pfm_profile(h, 1) resets and enables HIP-event bracketing of every launch pfm_run makes on
+ * its stream; pfm_profile_read sums, per kernel class (0 = MFMA GEMM, 1 = attention,
+ * 2 = everything else), the event-measured milliseconds, the ALGORITHMIC flops and bytes of
+ * those launches and their count. Reading synchronises the recorded events. */
+enum pfm_kclass { PFM_K_GEMM = 0, PFM_K_ATTN = 1, PFM_K_OTHER = 2 };
+int pfm_profile(pfm_handle* h, int enable);
+int pfm_profile_read(pfm_handle* h, int kclass, double* ms, double* flops, double* bytes,
+                     int64_t* launches);
+
+/* ---- single-op entry points (kernel-level parity tests; same kernels pfm_run uses) ---- */
+
+/* C[M,N] = act(A[M,K] . W[N,K]^T + bias) (+ res), dtype of A/W = PFM_F32 or PFM_BF16;
+ * C is f32. act: 0 none, 1 relu. */
+int pfm_op_gemm(void* stream, int dtype, const void* A, const void* W, const float* bias,
+                const float* res, float* C, int M, int N, int K, int act);
+
+/* Masked attention per (batch, head): q [B*Tq, heads*128], k/v [B*Tk, heads*128] of dtype,
+ * klen [B] int32; out f32 [B*Tq, heads*128]. */
+int pfm_op_attention(void* stream, int dtype, const void* q, const void* k, const void* v,
+                     const int32_t* klen, float* out, int B, int Tq, int Tk, int heads,
+                     float scale);
+
+/* LayerNorm rows of x [M, D] f32 -> out [M, D] f32. */
+int pfm_op_layernorm(void* stream, const float* x, const float* gamma, const float* beta,
+                     float* out, int M, int D, float eps);
+
+/* FSMN block: out = (res) + mask*(dwconv(mask*v) + mask*v); v/res/out [B*T, D], w [D, K]. */
+int pfm_op_fsmn(void* stream, const float* v, const int32_t* len, const float* w,
+                const float* res, float* out, int B, int T, int D, int K, int left);
+
+/* CIF integrate-and-fire on tail-processed alphas [B, T+1] and hidden [B, T+1, D]
+ * (row T zero): emb [B, L_cap, D], peaks [B, T+1], n_fire [B], ntok [B]. */
+int pfm_op_cif(void* stream, const float* alphas, const float* hidden, float* emb, float* peaks,
+               int32_t* n_fire, int32_t* ntok, int B, int T, int D, int L_cap);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PFM_H_ */

@@ -1,0 +1,201 @@
+"""Generate golden vectors by running the REAL reference modules in the build container.
+
+Run (build container only — /root/reference does not exist on the GPU box):
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py
+
+The reference package is imported from /root/reference with four audio/config IO
+modules stubbed (kaldiio, librosa, torchaudio, omegaconf — none is on the fbank-input
+path) and `funasr/__init__.py` bypassed. Weights come from
+funasr_amd.weights (seed 0) loaded with strict load_state_dict; inputs are seeded
+N(0,1) fbank tensors. Only inputs' seeds + outputs are stored (fixtures are data).
+
+Outputs (tests/golden/*.npz):
+  para_tiny.npz     enc 3 / dec 2 blocks, B=2 ragged: full encoder output, alphas,
+                    peaks, token_num, acoustic embeds, decoder argmax, decoder logit rows.
+  para_large_*.npz  Paraformer-large: token ids, token_num, alphas, encoder row slices
+                    and per-utterance checksums, top-2 logit margins.
+  lfr_cmvn.npz      reference apply_lfr / apply_cmvn / load_cmvn on seeded fbank.
+  automodel_tiny.json  AutoModel.generate() result dicts (key/text) for the tiny config.
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+import types
+
+import numpy as np
+
+REF = "/root/reference"
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+sys.dont_write_bytecode = True
+
+
+def install_stubs():
+    pkg = types.ModuleType("funasr")
+    pkg.__path__ = [f"{REF}/funasr"]
+    sys.modules["funasr"] = pkg
+    for n in ["kaldiio", "librosa", "torchaudio", "torchaudio.compliance", "torchaudio.compliance.kaldi"]:
+        sys.modules[n] = types.ModuleType(n)
+    sys.modules["torchaudio"].compliance = sys.modules["torchaudio.compliance"]
+    sys.modules["torchaudio.compliance"].kaldi = sys.modules["torchaudio.compliance.kaldi"]
+    oc = types.ModuleType("omegaconf")
+
+    class DictConfig(dict):
+        pass
+
+    class ListConfig(list):
+        pass
+
+    oc.DictConfig, oc.ListConfig, oc.OmegaConf = DictConfig, ListConfig, None
+    sys.modules["omegaconf"] = oc
+
+
+install_stubs()
+import torch  # noqa: E402
+
+import funasr.models.paraformer.model  # noqa: E402,F401
+import funasr.models.sanm.encoder  # noqa: E402,F401
+import funasr.models.paraformer.decoder  # noqa: E402,F401
+import funasr.models.paraformer.cif_predictor  # noqa: E402,F401
+from funasr.register import tables  # noqa: E402
+
+from funasr_amd.config import paraformer_large, paraformer_tiny  # noqa: E402
+from funasr_amd.weights import make_weights  # noqa: E402
+from tests.golden.inputs import fbank_input, token_list  # noqa: E402
+
+CMVN = f"{REF}/runtime/triton_gpu/model_repo_paraformer_large_online/lfr_cmvn_pe/am.mvn"
+
+
+def build_ref(cfg):
+    kw = cfg.reference_kwargs()
+    cls = tables.model_classes["Paraformer"]
+    m = cls(encoder=kw["encoder"], encoder_conf=kw["encoder_conf"], decoder=kw["decoder"],
+            decoder_conf=kw["decoder_conf"], predictor=kw["predictor"],
+            predictor_conf=kw["predictor_conf"], input_size=cfg.input_size,
+            vocab_size=cfg.vocab_size, ctc_weight=0.0, predictor_bias=1)
+    sd = {k: torch.from_numpy(v) for k, v in make_weights(cfg, seed=0).items()}
+    m.load_state_dict(sd, strict=True)
+    m.eval()
+    return m
+
+
+@torch.no_grad()
+def run_ref(m, feats, lens):
+    """Stage-by-stage reference run (what Paraformer.inference does for fbank input)."""
+    x = torch.from_numpy(feats)
+    ln = torch.from_numpy(lens.astype(np.int64))
+    enc, olens = m.encode(x, ln)
+    embeds, token_num, alphas, peak = m.calc_predictor(enc, olens)
+    ntok = token_num.round().long()
+    logp, _ = m.cal_decoder_with_predictor(enc, olens, embeds, ntok)
+    res = m.inference(x, data_lengths=ln[:, None], key=[f"utt{i}" for i in range(len(lens))],
+                      tokenizer=None, data_type="fbank", device="cpu")[0]
+    tokens = [r["token_int"] for r in res]
+    return dict(enc=enc.numpy(), enc_lens=olens.numpy(), embeds=embeds.numpy(),
+                token_num=token_num.numpy(), alphas=alphas.numpy(), peak=peak.numpy(),
+                ntok=ntok.numpy(), logp=logp.numpy(), tokens=tokens)
+
+
+def pack_tokens(tokens):
+    flat = np.array([t for ts in tokens for t in ts], dtype=np.int32)
+    off = np.cumsum([0] + [len(t) for t in tokens]).astype(np.int32)
+    return flat, off
+
+
+def top2_margin(logp, ntok):
+    out = []
+    for b in range(logp.shape[0]):
+        r = np.sort(logp[b, : ntok[b]], axis=-1)
+        out.append(r[:, -1] - r[:, -2])
+    return np.concatenate(out).astype(np.float32)
+
+
+def save_tiny():
+    cfg = paraformer_tiny()
+    m = build_ref(cfg)
+    feats, lens = fbank_input(seed=11, B=2, T=40, lens=[40, 27])
+    r = run_ref(m, feats, lens)
+    flat, off = pack_tokens(r["tokens"])
+    # decoder logits of a few rows only (full logits are B*L*8404 floats)
+    rows = np.stack([r["logp"][0, 0], r["logp"][0, int(r["ntok"][0]) - 1], r["logp"][1, 0]])
+    np.savez_compressed(f"{HERE}/para_tiny.npz", seed=11, B=2, T=40, lens=lens,
+                        enc=r["enc"], enc_lens=r["enc_lens"], embeds=r["embeds"],
+                        token_num=r["token_num"], alphas=r["alphas"], peak=r["peak"], ntok=r["ntok"],
+                        argmax=r["logp"].argmax(-1).astype(np.int32), logp_rows=rows,
+                        tokens=flat, tokens_off=off, margin=top2_margin(r["logp"], r["ntok"]))
+    print("tiny: ntok", r["ntok"], "tokens", [len(t) for t in r["tokens"]])
+
+
+def save_large(m, name, seed, B, T, lens):
+    feats, lens = fbank_input(seed=seed, B=B, T=T, lens=lens)
+    r = run_ref(m, feats, lens)
+    flat, off = pack_tokens(r["tokens"])
+    enc = r["enc"]
+    sl = []
+    for b in range(B):
+        n = int(lens[b])
+        sl.append(enc[b, [0, 1, n // 2, n - 1]])
+    valid = np.arange(T)[None, :] < lens[:, None]
+    csum = np.array([enc[b][valid[b]].astype(np.float64).sum() for b in range(B)])
+    csq = np.array([(enc[b][valid[b]].astype(np.float64) ** 2).sum() for b in range(B)])
+    np.savez_compressed(f"{HERE}/{name}.npz", seed=seed, B=B, T=T, lens=lens,
+                        enc_rows=np.stack(sl), enc_sum=csum, enc_sumsq=csq, enc_lens=r["enc_lens"],
+                        token_num=r["token_num"], alphas=r["alphas"], peak=r["peak"], ntok=r["ntok"],
+                        tokens=flat, tokens_off=off, margin=top2_margin(r["logp"], r["ntok"]))
+    print(name, "ntok", r["ntok"], "min margin", top2_margin(r["logp"], r["ntok"]).min())
+
+
+def save_lfr_cmvn():
+    from funasr.frontends.wav_frontend import apply_cmvn, apply_lfr, load_cmvn
+    cmvn = load_cmvn(CMVN).numpy()
+    out = dict(cmvn=cmvn)
+    rng = np.random.default_rng(5)
+    for n in [1, 2, 5, 6, 7, 11, 12, 13, 83, 498]:
+        fb = rng.standard_normal((n, 80)).astype(np.float32)
+        lfr = apply_lfr(torch.from_numpy(fb.copy()), 7, 6)
+        cm = apply_cmvn(lfr.clone(), torch.from_numpy(cmvn))
+        out[f"in_{n}"] = fb
+        out[f"lfr_{n}"] = lfr.numpy()
+        out[f"cmvn_{n}"] = cm.numpy()
+    np.savez_compressed(f"{HERE}/lfr_cmvn.npz", **out)
+    print("lfr_cmvn saved")
+
+
+def save_automodel_tiny():
+    """AutoModel.generate() on the tiny config with a CharTokenizer: pins the result-dict contract."""
+    import funasr.tokenizer.char_tokenizer  # noqa: F401
+    import funasr.frontends.wav_frontend  # noqa: F401
+    from funasr.auto.auto_model import AutoModel
+    cfg = paraformer_tiny()
+    kw = cfg.reference_kwargs()
+    am = AutoModel(model="Paraformer", model_conf=dict(ctc_weight=0.0, predictor_bias=1),
+                   device="cpu", ncpu=4, disable_update=True, disable_pbar=True, disable_log=True,
+                   tokenizer="CharTokenizer", tokenizer_conf=dict(token_list=token_list(cfg.vocab_size)),
+                   frontend="WavFrontend", frontend_conf=dict(fs=16000, window="hamming", n_mels=80,
+                                                             frame_length=25, frame_shift=10, lfr_m=7,
+                                                             lfr_n=6, dither=0.0, cmvn_file=CMVN),
+                   **kw)
+    sd = {k: torch.from_numpy(v) for k, v in make_weights(cfg, seed=0).items()}
+    am.model.load_state_dict(sd, strict=True)
+    feats, lens = fbank_input(seed=11, B=2, T=40, lens=[40, 27])
+    res = am.generate(input=torch.from_numpy(feats), input_len=torch.from_numpy(lens.astype(np.int32))[:, None],
+                      data_type="fbank", key=["uttA", "uttB"])
+    res = [{k: (v if not isinstance(v, np.ndarray) else v.tolist()) for k, v in r.items()} for r in res]
+    with open(f"{HERE}/automodel_tiny.json", "w") as f:
+        json.dump(res, f, ensure_ascii=False, indent=1)
+    print("automodel:", [r["text"][:20] for r in res])
+
+
+if __name__ == "__main__":
+    torch.manual_seed(0)
+    torch.set_num_threads(8)
+    save_lfr_cmvn()
+    save_tiny()
+    save_automodel_tiny()
+    m = build_ref(paraformer_large())
+    save_large(m, "para_large_ragged", seed=1, B=3, T=500, lens=[500, 431, 83])
+    save_large(m, "para_large_c1", seed=2, B=1, T=83, lens=[83])
+    save_large(m, "para_large_b4", seed=3, B=4, T=500, lens=[500, 500, 500, 500])

@@ -1,0 +1,128 @@
+"""Kernel-level numerics on the MI355X: each HIP op (through the C-ABI pfm_op_* entry points)
+against a plain PyTorch reference of the same op (fp64 on CPU; tolerances stated per test)."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from funasr_amd import runtime as rt  # noqa: E402
+from oracle import paraformer_ref as ref  # noqa: E402
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    rt.load_library()
+    return torch.device("cuda", 0)
+
+
+def rel(a, b):
+    a = a.double().cpu()
+    b = b.double().cpu()
+    return float((a - b).norm() / max(b.norm(), 1e-30))
+
+
+@pytest.mark.parametrize("M,N,K", [(300, 1536, 560), (128, 512, 512), (77, 8404, 512), (1000, 512, 2048),
+                                   (5, 2048, 512), (129, 1024, 1536)])
+def test_gemm_f32(dev, M, N, K):
+    g = torch.Generator().manual_seed(M * 7 + N)
+    A = torch.randn(M, K, generator=g)
+    W = torch.randn(N, K, generator=g) / K ** 0.5
+    b = torch.randn(N, generator=g)
+    R = torch.randn(M, N, generator=g)
+    want = torch.relu(A.double() @ W.double().T + b.double()) + R.double()
+    got = rt.op_gemm(A.to(dev), W.to(dev), b.to(dev), R.to(dev), relu=True)
+    torch.cuda.synchronize()
+    # exact f32 MFMA chain: error ~ K * 2^-24 relative to sum |a||w|
+    assert rel(got, want) < 2e-6
+    err = (got.double().cpu() - want).abs().max().item()
+    assert err < 1e-4
+
+
+@pytest.mark.parametrize("M,N,K", [(300, 1536, 560), (77, 8404, 512), (1000, 512, 2048)])
+def test_gemm_bf16(dev, M, N, K):
+    g = torch.Generator().manual_seed(M + N)
+    A = torch.randn(M, K, generator=g).bfloat16()
+    W = (torch.randn(N, K, generator=g) / K ** 0.5).bfloat16()
+    want = A.double() @ W.double().T          # products of bf16 values are exact; f32 accumulate
+    got = rt.op_gemm(A.to(dev), W.to(dev))
+    torch.cuda.synchronize()
+    assert rel(got, want) < 1e-5
+
+
+def test_gemm_identity_asymmetric(dev):
+    """A = I with an asymmetric W catches a transposed C write."""
+    K = 256
+    A = torch.eye(K)
+    W = torch.arange(K * 160, dtype=torch.float32).reshape(160, K) % 97
+    got = rt.op_gemm(A.to(dev), W.to(dev)).cpu()
+    assert torch.equal(got, W.T.contiguous())
+
+
+@pytest.mark.parametrize("dt", ["f32", "bf16"])
+@pytest.mark.parametrize("B,Tq,Tk,lens", [(2, 500, 500, [500, 123]), (3, 37, 200, [1, 200, 64]),
+                                          (1, 130, 33, [33])])
+def test_attention(dev, dt, B, Tq, Tk, lens):
+    H, dk = 4, 128
+    g = torch.Generator().manual_seed(B * 1000 + Tq)
+    q = torch.randn(B * Tq, H * dk, generator=g)
+    k = torch.randn(B * Tk, H * dk, generator=g)
+    v = torch.randn(B * Tk, H * dk, generator=g)
+    klen = torch.tensor(lens, dtype=torch.int32)
+    if dt == "bf16":
+        q, k, v = q.bfloat16(), k.bfloat16(), v.bfloat16()
+    want = ref._attend(q.double().reshape(B, Tq, -1), k.double().reshape(B, Tk, -1), v.double().reshape(B, Tk, -1),
+                       (torch.arange(Tk)[None] < klen[:, None]).double(), H).reshape(B * Tq, -1)
+    got = rt.op_attention(q.to(dev), k.to(dev), v.to(dev), klen.to(dev), B, Tq, Tk, H, dk ** -0.5)
+    torch.cuda.synchronize()
+    # f32: exact-f32 products, online softmax; bf16: P and (scaled) q rounded to bf16
+    assert rel(got, want) < (2e-6 if dt == "f32" else 1.5e-2)
+
+
+@pytest.mark.parametrize("M,D", [(1000, 512), (37, 560), (64, 2048)])
+def test_layernorm(dev, M, D):
+    g = torch.Generator().manual_seed(D)
+    x = torch.randn(M, D, generator=g) * 3 + 1
+    gm = 1 + 0.1 * torch.randn(D, generator=g)
+    bt = 0.1 * torch.randn(D, generator=g)
+    want = torch.nn.functional.layer_norm(x.double(), (D,), gm.double(), bt.double(), 1e-12)
+    got = rt.op_layernorm(x.to(dev), gm.to(dev), bt.to(dev), 1e-12)
+    torch.cuda.synchronize()
+    assert (got.double().cpu() - want).abs().max().item() < 2e-6
+
+
+@pytest.mark.parametrize("B,T,lens,left", [(2, 50, [50, 17], 5), (1, 9, [9], 5), (3, 40, [1, 40, 11], 7)])
+def test_fsmn(dev, B, T, lens, left):
+    D, K = 512, 11
+    g = torch.Generator().manual_seed(T)
+    v = torch.randn(B * T, D, generator=g)
+    w = torch.randn(D, 1, K, generator=g) / K ** 0.5
+    res = torch.randn(B * T, D, generator=g)
+    L = torch.tensor(lens, dtype=torch.int32)
+    m = (torch.arange(T)[None] < L[:, None]).double()
+    want = ref.fsmn(v.double().reshape(B, T, D), m, w.double(), left - (K - 1) // 2).reshape(B * T, D) + res.double()
+    got = rt.op_fsmn(v.to(dev), L.to(dev), w.to(dev), B, T, left, res=res.to(dev))
+    torch.cuda.synchronize()
+    assert (got.double().cpu() - want).abs().max().item() < 1e-5
+
+
+def test_cif_bit_exact(dev):
+    """Integrate-and-fire: fire pattern, peaks and token counts bit-exact vs the torch restatement."""
+    B, T, D = 3, 300, 512
+    g = torch.Generator().manual_seed(3)
+    h = torch.randn(B, T, D, generator=g)
+    a = torch.sigmoid(torch.randn(B, T, generator=g))
+    lens = torch.tensor([300, 211, 7])
+    a = a * ref.pad_mask(lens, T)
+    hh, aa, tn = ref.tail_process(h, a, lens, 0.45)
+    want_emb, want_peak, want_nf = ref.cif(hh, aa, 1.0)
+    emb, peaks, nf, nt = rt.op_cif(aa.contiguous().to(dev), hh.contiguous().to(dev), T + 1)
+    torch.cuda.synchronize()
+    assert torch.equal(nf.cpu().long(), want_nf.long())
+    assert torch.equal(peaks.cpu(), want_peak)
+    assert torch.equal(nt.cpu().long(), tn.long())
+    L = want_emb.shape[1]
+    assert torch.equal(emb.cpu()[:, :L], want_emb)
+    assert float(emb.cpu()[:, L:].abs().max() if emb.shape[1] > L else 0.0) == 0.0
