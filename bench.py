@@ -133,7 +133,7 @@ def main():
     fl_step = path_flops(T, ntok)
     peak = PEAK_TFLOPS[args.mode]
     g_ach = gemm["flops"] / (gemm["ms"] / 1e3) / 1e12 if gemm["ms"] > 0 else 0.0
-    roofline = {"bound": "mfma", "kernel": "gemm_nt_kernel<%s>" % ("bf16" if args.mode == "fast" else "float"),
+    roofline = {"bound": "mfma", "kernel": "gemm_bf16_256_kernel (+gemm_nt_kernel<bf16> for K%64!=0)" if args.mode == "fast" else "gemm_nt_kernel<float>",
                 "achieved": round(g_ach, 2), "peak": peak, "unit": "TFLOP/s", "frac": round(g_ach / peak, 4),
                 "traffic": None,
                 "avg_launch_us": round(gemm["ms"] * 1e3 / max(1, gemm["launches"]), 2),

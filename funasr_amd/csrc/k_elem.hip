@@ -104,10 +104,11 @@ __global__ __launch_bounds__(256) void fsmn_kernel(const float* __restrict__ v, 
             const int tt = t + k - left;
             if (tt < 0 || tt >= L) continue;
             const float4 x = *(const float4*)(v + vmap.off((long long)b * T + tt) + c);
-            acc.x = fmaf(w[(c + 0) * K + k], x.x, acc.x);
-            acc.y = fmaf(w[(c + 1) * K + k], x.y, acc.y);
-            acc.z = fmaf(w[(c + 2) * K + k], x.z, acc.z);
-            acc.w = fmaf(w[(c + 3) * K + k], x.w, acc.w);
+            const float4 wk = *(const float4*)(w + (long long)k * D + c);
+            acc.x = fmaf(wk.x, x.x, acc.x);
+            acc.y = fmaf(wk.y, x.y, acc.y);
+            acc.z = fmaf(wk.z, x.z, acc.z);
+            acc.w = fmaf(wk.w, x.w, acc.w);
         }
         self = *(const float4*)(v + vmap.off(row) + c);
     }
@@ -124,6 +125,65 @@ __global__ __launch_bounds__(256) void fsmn_kernel(const float* __restrict__ v, 
     if (out_bf) {
         bf16x4 tb = {f2bf(y.x), f2bf(y.y), f2bf(y.z), f2bf(y.w)};
         *(bf16x4*)(out_bf + row * D + c) = tb;
+    }
+}
+
+// Register-window FSMN: one thread = 4 channels x FR consecutive frames of one utterance.
+// The (FR + K - 1)-frame window of masked inputs lives in registers (each input float4 is
+// loaded once per window instead of K times) and the taps come from the transposed weight
+// wT[K][D] as float4 (coalesced). Same arithmetic order as fsmn_kernel.
+constexpr int FR = 8;
+template <int KK>
+__global__ __launch_bounds__(256) void fsmn_win_kernel(const float* __restrict__ v, RowMap vmap,
+                                                       const int* __restrict__ len, int B, int T, int D,
+                                                       const float* __restrict__ wT, int left,
+                                                       const float* __restrict__ res, float* __restrict__ out,
+                                                       bf16* __restrict__ out_bf) {
+    const int qpr = D / 4;
+    const int nblk = (T + FR - 1) / FR;
+    const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (gid >= (long long)B * nblk * qpr) return;
+    const int c = (int)(gid % qpr) * 4;
+    const long long rb = gid / qpr;
+    const int b = (int)(rb / nblk), t0 = (int)(rb % nblk) * FR;
+    const int L = min(len[b], T);
+    float4 w[KK];
+#pragma unroll
+    for (int k = 0; k < KK; ++k) w[k] = *(const float4*)(wT + (long long)k * D + c);
+    float4 x[FR + KK - 1];
+#pragma unroll
+    for (int i = 0; i < FR + KK - 1; ++i) {
+        const int tt = t0 - left + i;
+        x[i] = (tt >= 0 && tt < L) ? *(const float4*)(v + vmap.off((long long)b * T + tt) + c)
+                                   : make_float4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < FR; ++i) {
+        const int t = t0 + i;
+        if (t >= T) break;
+        const long long row = (long long)b * T + t;
+        float4 y = make_float4(0, 0, 0, 0);
+        if (t < L) {
+            float4 acc = make_float4(0, 0, 0, 0);
+#pragma unroll
+            for (int k = 0; k < KK; ++k) {
+                acc.x = fmaf(w[k].x, x[i + k].x, acc.x);
+                acc.y = fmaf(w[k].y, x[i + k].y, acc.y);
+                acc.z = fmaf(w[k].z, x[i + k].z, acc.z);
+                acc.w = fmaf(w[k].w, x[i + k].w, acc.w);
+            }
+            const float4 self = x[i + left];
+            y = make_float4(acc.x + self.x, acc.y + self.y, acc.z + self.z, acc.w + self.w);
+        }
+        if (res) {
+            const float4 r = *(const float4*)(res + row * D + c);
+            y.x = r.x + y.x; y.y = r.y + y.y; y.z = r.z + y.z; y.w = r.w + y.w;
+        }
+        *(float4*)(out + row * D + c) = y;
+        if (out_bf) {
+            bf16x4 tb = {f2bf(y.x), f2bf(y.y), f2bf(y.z), f2bf(y.w)};
+            *(bf16x4*)(out_bf + row * D + c) = tb;
+        }
     }
 }
 
@@ -284,12 +344,20 @@ hipError_t pfm_layernorm(const float* x, RowMap xmap, int M, int D, const float*
     return hipSuccess;
 }
 
-hipError_t pfm_fsmn(const float* v, RowMap vmap, const int* len, int B, int T, int D, const float* w, int K,
+// wT: taps transposed [K][D] (the registry stores fsmn_block.weight [D,1,K] that way).
+hipError_t pfm_fsmn(const float* v, RowMap vmap, const int* len, int B, int T, int D, const float* wT, int K,
                     int left, const float* res, float* out, bf16* out_bf, hipStream_t st) {
     if (B <= 0 || T <= 0) return hipSuccess;
-    if (D % 4 != 0) return hipErrorInvalidValue;
+    if (D % 4 != 0 || left < 0 || left >= K) return hipErrorInvalidValue;
+    if (K == 11) {
+        const long long n = (long long)B * ((T + FR - 1) / FR) * (D / 4);
+        hipLaunchKernelGGL(fsmn_win_kernel<11>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, v, vmap, len, B,
+                           T, D, wT, left, res, out, out_bf);
+        PFM_LAUNCH_CHECK();
+        return hipSuccess;
+    }
     const long long n = (long long)B * T * (D / 4);
-    hipLaunchKernelGGL(fsmn_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, v, vmap, len, B, T, D, w,
+    hipLaunchKernelGGL(fsmn_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, v, vmap, len, B, T, D, wT,
                        K, left, res, out, out_bf);
     PFM_LAUNCH_CHECK();
     return hipSuccess;

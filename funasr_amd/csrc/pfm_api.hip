@@ -2,6 +2,7 @@
 // forward pipeline on one HIP stream. Host code only; kernels live in k_*.hip.
 #include <math.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -17,6 +18,10 @@
 hipError_t pfm_gemm(int dtype, const void* A, RowMap amap, const void* W, long long ldw, int M, int N, int K,
                     const GemmEpi& epi, hipStream_t st);
 int pfm_gemm_amax_tiles(int N);
+bool pfm_gemm_bf16_256_ok(RowMap amap, long long ldw, int K);
+int pfm_gemm_bf16_256_amax_tiles(int N);
+hipError_t pfm_gemm_bf16_256(const void* A, RowMap amap, const void* W, long long ldw, int M, int N, int K,
+                             const GemmEpi& epi, hipStream_t st);
 hipError_t pfm_attention(int dtype, const void* q, RowMap qmap, const void* k, RowMap kmap, const void* v,
                          RowMap vmap, float* o, long long ldo, void* o2, const int* klen, int B, int Tq, int Tk,
                          int heads, int dk, float scale, hipStream_t st);
@@ -78,7 +83,7 @@ struct WEntry {
     size_t off = 0;        // element offset in the f32 arena
     size_t numel = 0;
     bool set = false;
-    int kind = 0;          // 0 plain, 1 cif conv [O][I][k] -> [O][k*I], 2 ignored
+    int kind = 0;          // 0 plain, 1 cif conv [O][I][k] -> [O][k*I], 2 ignored, 3 fsmn [D,1,K] -> [K][D]
 };
 
 struct EncLayer { size_t ln1g, ln1b, wqkv, bqkv, wo, bo, fsmn, ln2g, ln2b, w1, b1, w2, b2; int din; };
@@ -153,7 +158,7 @@ void build_registry(pfm_handle* h) {
         L.bo = add_entry(h, p + ".self_attn.linear_out.bias", {D});
         L.wqkv = add_entry(h, p + ".self_attn.linear_q_k_v.weight", {3 * D, din}, 0, true);
         L.bqkv = add_entry(h, p + ".self_attn.linear_q_k_v.bias", {3 * D});
-        L.fsmn = add_entry(h, p + ".self_attn.fsmn_block.weight", {D, 1, K});
+        L.fsmn = add_entry(h, p + ".self_attn.fsmn_block.weight", {D, 1, K}, 3);
         L.w1 = add_entry(h, p + ".feed_forward.w_1.weight", {F, D}, 0, true);
         L.b1 = add_entry(h, p + ".feed_forward.w_1.bias", {F});
         L.w2 = add_entry(h, p + ".feed_forward.w_2.weight", {D, F}, 0, true);
@@ -182,7 +187,7 @@ void build_registry(pfm_handle* h) {
     for (int l = 0; l < c.dec_blocks; ++l) {
         const std::string p = "decoder.decoders." + std::to_string(l);
         DecLayer L;
-        L.fsmn = add_entry(h, p + ".self_attn.fsmn_block.weight", {D, 1, K});
+        L.fsmn = add_entry(h, p + ".self_attn.fsmn_block.weight", {D, 1, K}, 3);
         L.wq = add_entry(h, p + ".src_attn.linear_q.weight", {D, D}, 0, true);
         L.bq = add_entry(h, p + ".src_attn.linear_q.bias", {D});
         {   // k_v slices point into wkv_all / bkv_all
@@ -258,7 +263,7 @@ int reserve(pfm_handle* h, int B, int T) {
     const size_t D = c.d_model, F = c.ffn, I = c.input_size;
     const size_t M = (size_t)B * T, Lc = (size_t)T + 1, Ml = (size_t)B * Lc;
     const size_t nkv = (size_t)c.dec_blocks * 2 * D;
-    const int nt = pfm_gemm_amax_tiles(c.vocab_size);
+    const int nt = std::max(pfm_gemm_amax_tiles(c.vocab_size), pfm_gemm_bf16_256_amax_tiles(c.vocab_size));
     HIP_TRY(hipDeviceSynchronize());
     HIP_TRY(h->X.ensure(M * D * 4));
     HIP_TRY(h->Xn.ensure(M * std::max(I, D) * 4));
@@ -344,6 +349,29 @@ void prof_collect(pfm_handle* h) {
     }
     h->prof.clear();
     h->ev_used = 0;
+}
+
+// Kernel choice: bf16 operands go to the 256x256 LDS-DMA kernel whenever its alignment
+// contract holds (K % 64 == 0, 16-B aligned rows); f32 (exact mode) and odd shapes use the
+// 128x128 register-staged kernel.
+int gemm_kernel_override() {   // PFM_GEMM_KERNEL=128 forces the 128x128 kernel (A/B experiments)
+    static int v = -1;
+    if (v < 0) { const char* e = getenv("PFM_GEMM_KERNEL"); v = e ? atoi(e) : 0; }
+    return v;
+}
+
+bool use_big_bf16(int dtype, RowMap amap, long long ldw, int K) {
+    return dtype == DT_BF16 && gemm_kernel_override() != 128 && pfm_gemm_bf16_256_ok(amap, ldw, K);
+}
+
+hipError_t gemm_dispatch(int dtype, const void* A, RowMap amap, const void* W, long long ldw, int M, int N, int K,
+                         const GemmEpi& e, hipStream_t st) {
+    if (use_big_bf16(dtype, amap, ldw, K)) return pfm_gemm_bf16_256(A, amap, W, ldw, M, N, K, e, st);
+    return pfm_gemm(dtype, A, amap, W, ldw, M, N, K, e, st);
+}
+
+int amax_tiles(int dtype, RowMap amap, long long ldw, int N, int K) {
+    return use_big_bf16(dtype, amap, ldw, K) ? pfm_gemm_bf16_256_amax_tiles(N) : pfm_gemm_amax_tiles(N);
 }
 
 GemmEpi epi_default() {
@@ -434,6 +462,13 @@ int pfm_set_weight(pfm_handle* h, const char* name, const void* host_ptr, int dt
                 for (int64_t k = 0; k < KK; ++k) tmp[(o * KK + k) * I + i] = src[(o * I + i) * KK + k];
         src = tmp.data();
     }
+    if (e.kind == 3) {   // depthwise taps [D][1][K] -> [K][D] (float4-coalesced tap loads)
+        const int64_t Dd = e.shape[0], KK = e.shape[2];
+        tmp.resize(e.numel);
+        for (int64_t d = 0; d < Dd; ++d)
+            for (int64_t k = 0; k < KK; ++k) tmp[k * Dd + d] = src[d * KK + k];
+        src = tmp.data();
+    }
     HIP_TRY(hipMemcpy(h->w(e.off), src, e.numel * 4, hipMemcpyHostToDevice));
     if (!e.set) { e.set = true; h->missing--; }
     h->bf_ready = false;
@@ -479,7 +514,7 @@ int pfm_run(pfm_handle* h, void* stream, int mode, const float* feats, const int
                           (double)Mm * N * (e.out ? (e.out_dtype == DT_F32 ? 4.0 : 2.0) : 0.0) +
                           (e.res0 ? 4.0 * Mm * N : 0.0) + (e.res1 ? 4.0 * Mm * N : 0.0) + (e.out2 ? 2.0 * Mm * N : 0.0);
         ProfScope ps(h, st, PFM_K_GEMM, fl, by);
-        return pfm_gemm(dtp, A, am, Wt, ldw, Mm, N, Kk, e, st);
+        return gemm_dispatch(dtp, A, am, Wt, ldw, Mm, N, Kk, e, st);
     };
     auto ATTN = [&](int dtp, const void* q, RowMap qm, const void* k, RowMap km, const void* v, RowMap vm, float* o,
                     long long ldo, void* o2, const int* kl, int Bb, int Tq, int Tk) -> hipError_t {
@@ -675,7 +710,7 @@ int pfm_run(pfm_handle* h, void* stream, int mode, const float* feats, const int
     HIP_TRY(pfm_layernorm(Xd, rowmap_plain(D), (int)Ml, D, P(h->dan_g), P(h->dan_b), c.ln_eps, nullptr, 0, 1.f, Xdn,
                           rowmap_plain(D), dt, nullptr, plain, 0, st));
     {   // output layer with fused row-argmax (logits never written)
-        const int ntl = pfm_gemm_amax_tiles(c.vocab_size);
+        const int ntl = amax_tiles(dt, rowmap_plain(D), D, c.vocab_size, D);
         GemmEpi e = epi_default();
         e.bias = P(h->out_b);
         e.amax_val = h->amv.as<float>(); e.amax_idx = h->ami.as<int>(); e.n_tiles = ntl;
@@ -738,7 +773,7 @@ int pfm_op_gemm(void* stream, int dtype, const void* A, const void* Wt, const fl
     e.bias = bias; e.relu = act == 1;
     if (res) { e.res0 = res; e.ld_res0 = N; }
     e.out = C; e.out_map = rowmap_plain(N); e.out_dtype = DT_F32;
-    HIP_TRY(pfm_gemm(dtype, A, rowmap_plain(K), Wt, K, M, N, K, e, (hipStream_t)stream));
+    HIP_TRY(gemm_dispatch(dtype, A, rowmap_plain(K), Wt, K, M, N, K, e, (hipStream_t)stream));
     return PFM_OK;
 }
 

@@ -80,4 +80,19 @@ struct GemmEpi {
     float* amax_val;        // [M, n_tiles] or null
     int* amax_idx;
     int n_tiles;
+    // set by the launcher: N, residual strides and output row offsets are multiples of 4
+    // (float4 / bf16x4 vector epilogue legal)
+    int vec_ok;
 };
+
+static inline bool rowmap_vec4(const RowMap& m) {
+    return m.ld % 4 == 0 && (m.rows_per_seg <= 0 || m.seg_stride % 4 == 0);
+}
+static inline int epi_vec_ok(const GemmEpi& e, int N) {
+    if (N % 4) return 0;
+    if (e.res0 && e.ld_res0 % 4) return 0;
+    if (e.res1 && e.ld_res1 % 4) return 0;
+    if (e.out && !rowmap_vec4(e.out_map)) return 0;
+    if (e.out2 && !rowmap_vec4(e.out2_map)) return 0;
+    return 1;
+}

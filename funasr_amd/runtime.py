@@ -243,7 +243,8 @@ def op_fsmn(v, lens, w, B, T, left, res=None):
     D, K = w.shape[0], w.shape[-1]
     out = torch.empty((B * T, D), dtype=torch.float32, device=v.device)
     check(lib.pfm_op_fsmn(_stream_ptr(torch, v.device), _ptr(v), _ptr(lens.to(torch.int32)),
-                          _ptr(w.reshape(D, K).contiguous()), _ptr(res), _ptr(out), B, T, D, K, left), "pfm_op_fsmn")
+                          _ptr(w.reshape(D, K).t().contiguous()), _ptr(res), _ptr(out), B, T, D, K, left),
+          "pfm_op_fsmn")
     return out
 
 

@@ -155,7 +155,8 @@ int pfm_op_attention(void* stream, int dtype, const void* q, const void* k, cons
 int pfm_op_layernorm(void* stream, const float* x, const float* gamma, const float* beta,
                      float* out, int M, int D, float eps);
 
-/* FSMN block: out = (res) + mask*(dwconv(mask*v) + mask*v); v/res/out [B*T, D], w [D, K]. */
+/* FSMN block: out = (res) + mask*(dwconv(mask*v) + mask*v); v/res/out [B*T, D]; w holds the
+ * depthwise taps TRANSPOSED, [K, D] (fsmn_block.weight[d, 0, k] at w[k*D + d]). */
 int pfm_op_fsmn(void* stream, const float* v, const int32_t* len, const float* w,
                 const float* res, float* out, int B, int T, int D, int K, int left);
 

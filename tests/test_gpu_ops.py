@@ -41,7 +41,8 @@ def test_gemm_f32(dev, M, N, K):
     assert err < 1e-4
 
 
-@pytest.mark.parametrize("M,N,K", [(300, 1536, 560), (77, 8404, 512), (1000, 512, 2048)])
+@pytest.mark.parametrize("M,N,K", [(300, 1536, 560), (77, 8404, 512), (1000, 512, 2048), (513, 1024, 1536),
+                                   (256, 256, 64), (4000, 2048, 512)])
 def test_gemm_bf16(dev, M, N, K):
     g = torch.Generator().manual_seed(M + N)
     A = torch.randn(M, K, generator=g).bfloat16()
