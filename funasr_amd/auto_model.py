@@ -1,0 +1,195 @@
+"""AutoModel with the reference's generate()/inference() contract over the HIP Paraformer path.
+
+Mirrors funasr/auto/auto_model.py:
+  prepare_data_iterator   :40-108   input forms -> (keys, items)
+  AutoModel.__init__      :113, build_model :176-293  (local model dir: config.yaml + model.pt +
+                                     tokens.json + am.mvn merge, download_model_from_hub.py:60-79)
+  generate / inference    :301-376  batch loop, batch_size, fbank single-tensor batch (:339-341),
+                                     speed stats, results in input order
+Differences (by design): device defaults to the GPU and there is no CPU path; hub names are
+not fetched (no network); VAD/punctuation/speaker pipelines are not built.
+Multi-GPU: when torch.distributed is initialised with world > 1, inference() shards the
+utterances over ranks (funasr_amd.distributed.shard_range) and all-gathers the results.
+"""
+from __future__ import annotations
+
+import json
+import os
+import random
+import string
+import time
+from typing import Any, Dict, List, Optional, Tuple
+
+import numpy as np
+import torch
+
+from . import model as _model  # noqa: F401  (registers "Paraformer")
+from .frontend import WavFrontend
+from .register import tables
+from .text import CharTokenizer
+
+_CHARS = string.ascii_letters + string.digits
+_LIST_EXT = (".scp", ".txt", ".json", ".jsonl", ".text")
+
+
+def _rand_key() -> str:
+    return "rand_key_" + "".join(random.choice(_CHARS) for _ in range(13))
+
+
+def prepare_data_iterator(data_in, input_len=None, data_type=None, key=None) -> Tuple[List[str], List[Any]]:
+    """Normalise generate() input into parallel (key_list, data_list)."""
+    if isinstance(data_in, str) and data_in.startswith(("http://", "https://")):
+        raise ValueError("URL inputs need network access, which this build does not have")
+    if isinstance(data_in, str) and os.path.exists(data_in):
+        ext = os.path.splitext(data_in)[1].lower()
+        if ext in _LIST_EXT:
+            keys, items = [], []
+            with open(data_in, encoding="utf-8") as f:
+                for line in f:
+                    if not line.strip():
+                        continue
+                    if data_in.endswith(".jsonl"):
+                        d = json.loads(line.strip())["source"]
+                        items.append(d)
+                        keys.append(d["key"] if isinstance(d, dict) and "key" in d else _rand_key())
+                    else:
+                        parts = line.strip().split(maxsplit=1)
+                        items.append(parts[1] if len(parts) > 1 else parts[0])
+                        keys.append(parts[0] if len(parts) > 1 else _rand_key())
+            return keys, items
+        k = key if key is not None else os.path.splitext(os.path.basename(data_in))[0]
+        return [k], [data_in]
+    if isinstance(data_in, (list, tuple)):
+        keys = []
+        for d in data_in:
+            if isinstance(d, str) and os.path.exists(d):
+                keys.append(os.path.splitext(os.path.basename(d))[0])
+            else:
+                keys.append(key if key is not None else _rand_key())
+        return keys, list(data_in)
+    return [key if key is not None else _rand_key()], [data_in]
+
+
+def _read_model_dir(path: str, kwargs: Dict[str, Any]) -> Dict[str, Any]:
+    """Local model dir: config.yaml (safe YAML) + model.pt + tokens.json + am.mvn."""
+    import yaml
+    cfg_path = os.path.join(path, "config.yaml")
+    conf: Dict[str, Any] = {}
+    if os.path.exists(cfg_path):
+        with open(cfg_path, encoding="utf-8") as f:
+            conf = yaml.safe_load(f) or {}
+    out = dict(conf)
+    for k, v in kwargs.items():
+        if isinstance(v, dict) and isinstance(out.get(k), dict):
+            out[k] = {**out[k], **v}
+        else:
+            out[k] = v
+    out["model"] = conf.get("model", "Paraformer")
+    if os.path.exists(os.path.join(path, "model.pt")) and "init_param" not in kwargs:
+        out["init_param"] = os.path.join(path, "model.pt")
+    tok = os.path.join(path, "tokens.json")
+    if os.path.exists(tok):
+        out.setdefault("tokenizer_conf", {})
+        out["tokenizer_conf"] = {**out.get("tokenizer_conf", {}), "token_list": tok}
+    mvn = os.path.join(path, "am.mvn")
+    if os.path.exists(mvn):
+        out["frontend_conf"] = {**out.get("frontend_conf", {}), "cmvn_file": mvn}
+    return out
+
+
+def load_pretrained_state(path: str) -> Dict[str, torch.Tensor]:
+    """model.pt -> state_dict, unwrapping 'state_dict' / 'model_state_dict' / 'model'
+    (load_pretrained_model.py:44-47). weights_only=True: nothing in the file executes."""
+    src = torch.load(path, map_location="cpu", weights_only=True)
+    for k in ("state_dict", "model_state_dict", "model"):
+        if isinstance(src, dict) and k in src and isinstance(src[k], dict):
+            src = src[k]
+            break
+    return src
+
+
+class AutoModel:
+    def __init__(self, **kwargs):
+        if kwargs.get("vad_model") or kwargs.get("punc_model") or kwargs.get("spk_model"):
+            raise NotImplementedError("VAD / punctuation / speaker pipelines are SURVEY §8f next rows")
+        self.model, self.kwargs = self.build_model(**kwargs)
+        self.vad_model = None
+
+    @staticmethod
+    def build_model(**kwargs):
+        name = kwargs.get("model", "Paraformer")
+        if isinstance(name, str) and os.path.isdir(name):
+            kwargs = _read_model_dir(name, kwargs)
+            name = kwargs["model"]
+        if name not in tables.model_classes:
+            raise ValueError(f"model {name!r} is not registered (available: {sorted(tables.model_classes)}); "
+                             "hub names cannot be downloaded offline — pass a local model dir")
+        device = kwargs.get("device", "cuda")
+        if not torch.cuda.is_available() or str(device).startswith("cpu") or kwargs.get("ngpu", 1) == 0:
+            raise RuntimeError("the HIP Paraformer path needs a ROCm GPU (device='cuda[:i]'); there is no CPU path")
+        kwargs["device"] = device
+        torch.manual_seed(kwargs.get("seed", 0))
+        tok_conf = kwargs.get("tokenizer_conf") or {}
+        tokenizer = CharTokenizer(**tok_conf) if tok_conf.get("token_list") is not None else None
+        kwargs["tokenizer"] = tokenizer
+        fconf = kwargs.get("frontend_conf") or {}
+        kwargs["frontend"] = WavFrontend(**fconf)
+        vocab = tokenizer.get_num_vocabulary_size() if tokenizer is not None else kwargs.get("vocab_size", -1)
+        model_conf = kwargs.get("model_conf") or {}
+        mk = {**model_conf, **{k: v for k, v in kwargs.items() if k not in ("model_conf",)}}
+        mk["vocab_size"] = vocab
+        mk["input_size"] = kwargs["frontend"].output_size()
+        model = tables.model_classes[name](**mk)
+        if kwargs.get("init_param"):
+            model.load_state_dict(load_pretrained_state(kwargs["init_param"]), strict=True)
+        elif kwargs.get("synthetic_seed") is not None:
+            from .weights import make_weights
+            model.load_state_dict(make_weights(model.cfg, int(kwargs["synthetic_seed"])), strict=True)
+        model.to(device)
+        model.eval()
+        return model, kwargs
+
+    def __call__(self, *args, **cfg):
+        kwargs = dict(self.kwargs)
+        kwargs.update(cfg)
+        return self.model(*args, kwargs)
+
+    def generate(self, input, input_len=None, **cfg):
+        return self.inference(input, input_len=input_len, **cfg)
+
+    def inference(self, input, input_len=None, model=None, kwargs=None, key=None, **cfg):
+        kwargs = dict(self.kwargs if kwargs is None else kwargs)
+        kwargs.update(cfg)
+        model = self.model if model is None else model
+        model.eval()
+        batch_size = int(kwargs.get("batch_size", 1))
+        keys, items = prepare_data_iterator(input, input_len=input_len, data_type=kwargs.get("data_type"), key=key)
+        world, rank = 1, 0
+        if torch.distributed.is_available() and torch.distributed.is_initialized() and kwargs.get("dp", True):
+            world, rank = torch.distributed.get_world_size(), torch.distributed.get_rank()
+        lo, hi = 0, len(items)
+        if world > 1 and len(items) > 1:
+            from .distributed import shard_range
+            lo, hi = shard_range(len(items), world, rank)
+        results = []
+        speech_s, wall_s = 0.0, 0.0
+        for beg in range(lo, hi, batch_size):
+            end = min(hi, beg + batch_size)
+            batch = {"data_in": items[beg:end], "key": keys[beg:end]}
+            if end - beg == 1 and kwargs.get("data_type") == "fbank":
+                batch["data_in"] = items[beg]
+                batch["data_lengths"] = input_len
+            t1 = time.perf_counter()
+            with torch.no_grad():
+                res = model.inference(**batch, **{k: v for k, v in kwargs.items() if k not in ("key",)})
+            t2 = time.perf_counter()
+            out, meta = (res[0], res[1]) if isinstance(res, (list, tuple)) and len(res) > 1 else (res, {})
+            results.extend(out)
+            bt = meta.get("batch_data_time", -1)
+            speech_s += bt if bt > 0 else 0.0
+            wall_s += t2 - t1
+        self.last_speed = {"rtf": (wall_s / speech_s) if speech_s > 0 else None, "forward_s": wall_s}
+        if world > 1 and len(items) > 1:
+            from .distributed import gather_results
+            results = gather_results(results)
+        return results

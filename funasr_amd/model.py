@@ -1,0 +1,137 @@
+"""`Paraformer` model class with the reference's plugin contract, backed by libpfm_hip.so.
+
+Contract (funasr/auto/auto_model.py:260-288, funasr/models/paraformer/model.py:443-596):
+  * constructed as cls(**model_conf, encoder_conf=..., decoder_conf=..., predictor_conf=...,
+    input_size=560, vocab_size=V, **AutoModel kwargs);
+  * an nn.Module with >= 1 parameter (AutoModel reads next(model.parameters()).device);
+  * state_dict() / load_state_dict() speak the reference state_dict keys and shapes, so
+    load_pretrained_model (funasr/train_utils/load_pretrained_model.py:14-47) and this
+    package's loader both work unchanged;
+  * inference(data_in, data_lengths=None, key=None, tokenizer=None, frontend=None, **kwargs)
+    -> (results, meta) with results [{"key", "text"}] or [{"key", "token_int"}] when
+    tokenizer is None; meta has load_data / extract_feat / batch_data_time.
+All compute runs in the HIP library; there is no CPU/PyTorch fallback.
+"""
+from __future__ import annotations
+
+import time
+from typing import Dict, List, Optional
+
+import numpy as np
+import torch
+
+from .config import ParaformerConfig
+from .register import tables
+from .runtime import PfmEngine, PfmError
+from .text import sentence_postprocess
+from .weights import param_layout
+
+
+@tables.register("model_classes", "Paraformer")
+class Paraformer(torch.nn.Module):
+    def __init__(self, *args, **kwargs):
+        super().__init__()
+        self.cfg = ParaformerConfig.from_kwargs(**kwargs)
+        self.blank_id, self.sos, self.eos = self.cfg.blank_id, self.cfg.sos, self.cfg.eos
+        self.mode = kwargs.get("mode", "exact")
+        # device anchor: AutoModel and callers read next(model.parameters()).device
+        self._anchor = torch.nn.Parameter(torch.zeros(1), requires_grad=False)
+        self._host_sd: Dict[str, np.ndarray] = {}
+        self._engine: Optional[PfmEngine] = None
+        self._engine_dev: Optional[int] = None
+
+    # ---------------- weights (reference key names) ----------------
+    def state_dict(self, *args, **kwargs):
+        out = {}
+        for k, shape, _ in param_layout(self.cfg):
+            v = self._host_sd.get(k)
+            out[k] = torch.from_numpy(v) if v is not None else torch.zeros(shape)
+        return out
+
+    def load_state_dict(self, state_dict, strict: bool = True, assign: bool = False):
+        want = {k: s for k, s, _ in param_layout(self.cfg)}
+        missing = [k for k in want if k not in state_dict]
+        unexpected = [k for k in state_dict if k not in want]
+        if strict and (missing or unexpected):
+            raise RuntimeError(f"Paraformer.load_state_dict: missing {missing[:5]} unexpected {unexpected[:5]}")
+        for k, v in state_dict.items():
+            if k not in want:
+                continue
+            a = v.detach().cpu().float().numpy() if isinstance(v, torch.Tensor) else np.asarray(v, np.float32)
+            if tuple(a.shape) != tuple(want[k]):
+                raise RuntimeError(f"{k}: shape {a.shape} != {want[k]}")
+            self._host_sd[k] = np.ascontiguousarray(a, dtype=np.float32)
+            if self._engine is not None:
+                self._engine.set_weight(k, self._host_sd[k])
+        return torch.nn.modules.module._IncompatibleKeys(missing, unexpected)
+
+    # ---------------- device / engine ----------------
+    def _device_index(self) -> int:
+        d = self._anchor.device
+        if d.type != "cuda":
+            if not torch.cuda.is_available():
+                raise PfmError("Paraformer (HIP) needs a ROCm GPU; there is no CPU path in this build")
+            return torch.cuda.current_device()
+        return d.index if d.index is not None else torch.cuda.current_device()
+
+    def engine(self) -> PfmEngine:
+        dev = self._device_index()
+        if self._engine is None or self._engine_dev != dev:
+            eng = PfmEngine(self.cfg, dev)
+            if self._host_sd:
+                eng.load_state_dict(self._host_sd, strict=False)
+            self._engine, self._engine_dev = eng, dev
+        if self._engine.missing_weights:
+            raise PfmError(f"{self._engine.missing_weights} Paraformer weights not loaded "
+                           "(load_state_dict / init_param)")
+        return self._engine
+
+    # ---------------- inference (paraformer/model.py:443-596) ----------------
+    @torch.no_grad()
+    def inference(self, data_in, data_lengths=None, key: List[str] = None, tokenizer=None, frontend=None,
+                  **kwargs):
+        if kwargs.get("decoding_ctc_weight", 0.0) > 1e-5 or kwargs.get("lm_weight", 0.0) > 1e-5:
+            raise NotImplementedError("CTC / LM beam search is not on the HIP Paraformer path (greedy only)")
+        if kwargs.get("pred_timestamp", False):
+            raise NotImplementedError("timestamp prediction is a next-row item (SURVEY §8f)")
+        eng = self.engine()
+        mode = kwargs.get("mode", self.mode)
+        meta = {}
+        if isinstance(data_in, torch.Tensor) and kwargs.get("data_type", "sound") == "fbank":
+            speech = data_in if data_in.dim() == 3 else data_in[None]
+            if data_lengths is None:
+                lens = torch.full((speech.shape[0],), speech.shape[1], dtype=torch.int32)
+            else:
+                lens = torch.as_tensor(data_lengths).reshape(-1)
+        else:
+            if frontend is None:
+                raise ValueError("waveform input needs a frontend (frontend_conf)")
+            items = data_in if isinstance(data_in, (list, tuple)) else [data_in]
+            t1 = time.perf_counter()
+            speech, lens, _ = frontend(eng, items)
+            torch.cuda.synchronize(speech.device)
+            t2 = time.perf_counter()
+            meta["load_data"] = "0.000"
+            meta["extract_feat"] = f"{t2 - t1:0.3f}"
+            meta["batch_data_time"] = float(lens.sum().item()) * frontend.frame_shift * frontend.lfr_n / 1000
+        r = eng.run(speech, lens, mode=mode)
+        toks = r["tokens"].cpu().numpy()           # one device->host copy for the whole batch
+        ntok = r["ntok"].cpu().numpy()
+        b = toks.shape[0]
+        if key is None:
+            key = [f"utt{i}" for i in range(b)]
+        if isinstance(key[0], (list, tuple)):
+            key = key[0]
+        if len(key) < b:
+            key = key * b
+        results = []
+        for i in range(b):
+            n = int(ntok[i])
+            ids = toks[i, :n].tolist() if n <= toks.shape[1] else []
+            ids = [t for t in ids if t not in (self.eos, self.sos, self.blank_id)]
+            if tokenizer is not None:
+                text, _ = sentence_postprocess(tokenizer.ids2tokens(ids))
+                results.append({"key": key[i], "text": text})
+            else:
+                results.append({"key": key[i], "token_int": ids})
+        return results, meta

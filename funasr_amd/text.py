@@ -1,0 +1,149 @@
+"""Host-side detokenisation: CharTokenizer + sentence post-processing.
+
+Restates the reference's L0 host stage:
+  CharTokenizer.ids2tokens / tokens2text   funasr/tokenizer/abs_tokenizer.py:79-82,
+                                           funasr/tokenizer/char_tokenizer.py:76-78
+  sentence_postprocess (no timestamps)     funasr/utils/postprocess_utils.py:144-249
+  abbreviation joining (abbr_dispose)      funasr/utils/postprocess_utils.py:56-141
+Pinned by tests/golden/postprocess.json (outputs of the reference functions).
+"""
+from __future__ import annotations
+
+import json
+import os
+from typing import Iterable, List, Sequence, Union
+
+_SPECIAL = ("<s>", "</s>", "<unk>", "<OOV>")
+
+
+def load_token_list(token_list: Union[str, Sequence[str], None]) -> List[str]:
+    """token_list as a list, a tokens.json path (list) or a tokens.txt path (one per line)."""
+    if token_list is None:
+        return []
+    if isinstance(token_list, (list, tuple)):
+        return list(token_list)
+    p = str(token_list)
+    with open(p, encoding="utf-8") as f:
+        if p.endswith(".json"):
+            return list(json.load(f))
+        return [line.rstrip("\n").split()[0] if line.strip() else "" for line in f]
+
+
+class CharTokenizer:
+    """ids <-> tokens <-> text for character vocabularies (tokenizer_conf.token_list)."""
+
+    def __init__(self, token_list=None, space_symbol: str = "<space>", unk_symbol: str = "<unk>", **kwargs):
+        self.token_list = load_token_list(token_list)
+        self.token2id = {t: i for i, t in enumerate(self.token_list)}
+        self.space_symbol = space_symbol
+        self.unk_symbol = unk_symbol
+        self.unk_id = self.token2id.get(unk_symbol, -1)
+
+    def get_num_vocabulary_size(self) -> int:
+        return len(self.token_list)
+
+    def ids2tokens(self, ids: Iterable[int]) -> List[str]:
+        return [self.token_list[int(i)] for i in ids]
+
+    def tokens2text(self, tokens: Iterable[str]) -> str:
+        return "".join(" " if t == self.space_symbol else t for t in tokens)
+
+    def text2tokens(self, line: str) -> List[str]:
+        return [c for c in line if c != " "]
+
+    def tokens2ids(self, tokens: Iterable[str]) -> List[int]:
+        return [self.token2id.get(t, self.unk_id) for t in tokens]
+
+    def decode(self, ids: Iterable[int]) -> str:
+        return self.tokens2text(self.ids2tokens(ids))
+
+
+def _strip_specials(w: str) -> str:
+    w = w.replace(" ", "")
+    for s in ("</s>", "<s>", "<unk>", "<OOV>"):
+        w = w.replace(s, "")
+    return w
+
+
+def _is_zh(w: str) -> bool:
+    # same (string-range) test as the reference's isChinese: CJK block, a digit-led string, or "@"
+    return ("一" <= w <= "鿿") or ("0" <= w <= "9") or w == "@"
+
+
+def _all_zh(words) -> bool:
+    ws = [_strip_specials(w) for w in words]
+    return len(ws) > 0 and all(_is_zh(w) for w in ws)
+
+
+def _all_alpha(words) -> bool:
+    ws = [_strip_specials(w) for w in words]
+    if not ws:
+        return False
+    for w in ws:
+        if not w.isalpha() and w != "'":
+            return False
+        if w.isalpha() and _is_zh(w):
+            return False
+    return True
+
+
+def _single_letter(w: str) -> bool:
+    return len(w) == 1 and w.encode("utf-8").isalpha()
+
+
+def _join_abbreviations(words: List[str]) -> List[str]:
+    """Runs 'a', ' ', 'b', ' ', 'c' of single ASCII letters become one upper-case word 'ABC'."""
+    out: List[str] = []
+    n, i = len(words), 0
+    while i < n:
+        if _single_letter(words[i]) and i + 2 < n and words[i + 1] == " " and _single_letter(words[i + 2]):
+            j = i + 2
+            while j + 2 < n and words[j + 1] == " " and _single_letter(words[j + 2]):
+                j += 2
+            out.append("".join(words[k].upper() for k in range(i, j + 1) if words[k] != " "))
+            i = j + 1
+        else:
+            out.append(words[i])
+            i += 1
+    return out
+
+
+def sentence_postprocess(words: Sequence[Union[str, bytes]]):
+    """Token list -> (sentence, word list); Chinese chars joined, BPE '@@' pieces merged,
+    alphabetic words space-separated, single-letter runs joined as abbreviations."""
+    mid = []
+    for w in words:
+        w = w if isinstance(w, str) else w.decode("utf-8")
+        if w not in _SPECIAL:
+            mid.append(w)
+    out: List[str] = []
+    if _all_zh(mid):
+        out = [w.replace(" ", "") for w in mid]
+    elif _all_alpha(mid):
+        piece = ""
+        for w in mid:
+            if "@@" in w:
+                piece += w.replace("@@", "")
+            else:
+                out += [piece + w, " "]
+                piece = ""
+    else:
+        piece, after_alpha = "", False
+        for w in mid:
+            if _all_zh(w):
+                if after_alpha:
+                    out.pop()
+                out.append(w)
+                after_alpha = False
+            elif "@@" in w:
+                piece += w.replace("@@", "")
+                after_alpha = False
+            elif _all_alpha(w):
+                out += [piece + w, " "]
+                piece = ""
+                after_alpha = True
+            else:
+                out.append(w)
+    out = _join_abbreviations(out)
+    real = [w for w in out if w != " "]
+    return "".join(out).strip(), real

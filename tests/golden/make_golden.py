@@ -189,8 +189,28 @@ def save_automodel_tiny():
     print("automodel:", [r["text"][:20] for r in res])
 
 
+POSTPROC_CASES = [
+    ["欢", "迎", "大", "家"], ["he@@", "llo", "world"], ["a", "b", "c"], ["i", "am", "o@@", "k"],
+    ["你", "好", "hello", "世", "界"], ["<s>", "今", "天", "</s>", "<unk>"], ["12", "月", "3", "号"],
+    ["g", "p", "u", "是", "a", "m", "d"], ["x", "<unk>", "y", "z"], ["don't", "stop"], ["@", "a"],
+    ["中", "a@@", "b", "文"], ["!", "好"], [], ["<s>"], ["a", " ", "b"], ["hel@@", "lo"], ["A", "b", "C", "d@@", "e"],
+]
+
+
+def save_postprocess():
+    from funasr.utils.postprocess_utils import sentence_postprocess
+    out = []
+    for toks in POSTPROC_CASES:
+        sent, words = sentence_postprocess(list(toks))
+        out.append({"tokens": toks, "sentence": sent, "words": words})
+    with open(f"{HERE}/postprocess.json", "w") as f:
+        json.dump(out, f, ensure_ascii=False, indent=1)
+    print("postprocess cases", len(out))
+
+
 if __name__ == "__main__":
     torch.manual_seed(0)
+    save_postprocess()
     torch.set_num_threads(8)
     save_lfr_cmvn()
     save_tiny()

@@ -1,0 +1,78 @@
+"""Multi-process data-parallel plumbing on CPU with gloo (world_size 2): the same
+funasr_amd.distributed functions bench.py / AutoModel run over RCCL on the GPU node."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from funasr_amd.distributed import broadcast_state_dict, gather_results, length_sorted_shards, shard_range
+
+
+def test_shard_range_covers_exactly():
+    for n in [1, 2, 5, 64, 513]:
+        for world in [1, 2, 3, 4, 8]:
+            spans = [shard_range(n, world, r) for r in range(world)]
+            got = [i for a, b in spans for i in range(a, b)]
+            assert got == list(range(n))
+            sizes = [b - a for a, b in spans]
+            assert max(sizes) - min(sizes) <= 1
+
+
+def test_length_sorted_shards_balance():
+    lens = [500, 83, 431, 500, 120, 300, 222, 17]
+    sh = length_sorted_shards(lens, 2)
+    assert sorted(sum(sh, [])) == list(range(len(lens)))
+    tot = [sum(lens[i] for i in s) for s in sh]
+    assert abs(tot[0] - tot[1]) <= max(lens)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        layout = [("a.weight", (3, 4), 4), ("b.bias", (5,), 4), ("c", (2, 2, 2), 8)]
+        sd = None
+        if rank == 0:
+            rng = np.random.default_rng(0)
+            sd = {k: rng.standard_normal(s).astype(np.float32) for k, s, _ in layout}
+        got = broadcast_state_dict(layout, sd)
+        items = list(range(11))
+        lo, hi = shard_range(len(items), world, rank)
+        local = [{"key": f"u{i}", "rank": rank} for i in items[lo:hi]]
+        allres = gather_results(local)
+        q.put((rank, {k: v.tolist() for k, v in got.items()}, allres))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world2_broadcast_and_gather():
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    out.sort(key=lambda x: x[0])
+    rng = np.random.default_rng(0)
+    want = {k: rng.standard_normal(s).astype(np.float32).tolist() for k, s in
+            [("a.weight", (3, 4)), ("b.bias", (5,)), ("c", (2, 2, 2))]}
+    for rank, sd, allres in out:
+        assert sd == want
+        assert [r["key"] for r in allres] == [f"u{i}" for i in range(11)]
+        assert [r["rank"] for r in allres] == [0] * 6 + [1] * 5
