@@ -27,6 +27,19 @@ from .text import sentence_postprocess
 from .weights import param_layout
 
 
+def _as_hip_frontend(frontend):
+    """Accept the reference's WavFrontend (plugin route: reference AutoModel builds it) by taking
+    its CMVN over into the HIP frontend; the fbank itself always runs in k_fbank.hip."""
+    from .frontend import WavFrontend
+    if isinstance(frontend, WavFrontend):
+        return frontend
+    fe = WavFrontend(cmvn_file=None)
+    cm = getattr(frontend, "cmvn", None)
+    if cm is not None:
+        fe.cmvn = np.asarray(cm.detach().cpu().numpy() if hasattr(cm, "detach") else cm, dtype=np.float32)
+    return fe
+
+
 @tables.register("model_classes", "Paraformer")
 class Paraformer(torch.nn.Module):
     def __init__(self, *args, **kwargs):
@@ -106,6 +119,7 @@ class Paraformer(torch.nn.Module):
         else:
             if frontend is None:
                 raise ValueError("waveform input needs a frontend (frontend_conf)")
+            frontend = _as_hip_frontend(frontend)
             items = data_in if isinstance(data_in, (list, tuple)) else [data_in]
             t1 = time.perf_counter()
             speech, lens, _ = frontend(eng, items)
