@@ -133,8 +133,15 @@ __global__ __launch_bounds__(256) void fsmn_kernel(const float* __restrict__ v, 
 // loaded once per window instead of K times) and the taps come from the transposed weight
 // wT[K][D] as float4 (coalesced). Same arithmetic order as fsmn_kernel.
 constexpr int FR = 8;
-template <int KK>
-__global__ __launch_bounds__(256) void fsmn_win_kernel(const float* __restrict__ v, RowMap vmap,
+template <typename T> __device__ __forceinline__ float4 load4(const T* p);
+template <> __device__ __forceinline__ float4 load4<float>(const float* p) { return *(const float4*)p; }
+template <> __device__ __forceinline__ float4 load4<bf16>(const bf16* p) {
+    const bf16x4 b = *(const bf16x4*)p;
+    return make_float4(bf2f(b[0]), bf2f(b[1]), bf2f(b[2]), bf2f(b[3]));
+}
+
+template <int KK, typename TIN>
+__global__ __launch_bounds__(256) void fsmn_win_kernel(const TIN* __restrict__ v, RowMap vmap,
                                                        const int* __restrict__ len, int B, int T, int D,
                                                        const float* __restrict__ wT, int left,
                                                        const float* __restrict__ res, float* __restrict__ out,
@@ -154,7 +161,7 @@ __global__ __launch_bounds__(256) void fsmn_win_kernel(const float* __restrict__
 #pragma unroll
     for (int i = 0; i < FR + KK - 1; ++i) {
         const int tt = t0 - left + i;
-        x[i] = (tt >= 0 && tt < L) ? *(const float4*)(v + vmap.off((long long)b * T + tt) + c)
+        x[i] = (tt >= 0 && tt < L) ? load4<TIN>(v + vmap.off((long long)b * T + tt) + c)
                                    : make_float4(0, 0, 0, 0);
     }
 #pragma unroll
@@ -179,7 +186,7 @@ __global__ __launch_bounds__(256) void fsmn_win_kernel(const float* __restrict__
             const float4 r = *(const float4*)(res + row * D + c);
             y.x = r.x + y.x; y.y = r.y + y.y; y.z = r.z + y.z; y.w = r.w + y.w;
         }
-        *(float4*)(out + row * D + c) = y;
+        if (out) *(float4*)(out + row * D + c) = y;
         if (out_bf) {
             bf16x4 tb = {f2bf(y.x), f2bf(y.y), f2bf(y.z), f2bf(y.w)};
             *(bf16x4*)(out_bf + row * D + c) = tb;
@@ -351,14 +358,26 @@ hipError_t pfm_fsmn(const float* v, RowMap vmap, const int* len, int B, int T, i
     if (D % 4 != 0 || left < 0 || left >= K) return hipErrorInvalidValue;
     if (K == 11) {
         const long long n = (long long)B * ((T + FR - 1) / FR) * (D / 4);
-        hipLaunchKernelGGL(fsmn_win_kernel<11>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, v, vmap, len, B,
-                           T, D, wT, left, res, out, out_bf);
+        hipLaunchKernelGGL((fsmn_win_kernel<11, float>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, v, vmap,
+                           len, B, T, D, wT, left, res, out, out_bf);
         PFM_LAUNCH_CHECK();
         return hipSuccess;
     }
     const long long n = (long long)B * T * (D / 4);
     hipLaunchKernelGGL(fsmn_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, v, vmap, len, B, T, D, wT,
                        K, left, res, out, out_bf);
+    PFM_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+// bf16 input V (fast mode): out_bf only (f32 out optional)
+hipError_t pfm_fsmn_bf16in(const bf16* v, RowMap vmap, const int* len, int B, int T, int D, const float* wT, int K,
+                           int left, const float* res, float* out, bf16* out_bf, hipStream_t st) {
+    if (B <= 0 || T <= 0) return hipSuccess;
+    if (D % 4 != 0 || K != 11 || left < 0 || left >= K) return hipErrorInvalidValue;
+    const long long n = (long long)B * ((T + FR - 1) / FR) * (D / 4);
+    hipLaunchKernelGGL((fsmn_win_kernel<11, bf16>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, v, vmap, len,
+                       B, T, D, wT, left, res, out, out_bf);
     PFM_LAUNCH_CHECK();
     return hipSuccess;
 }

@@ -191,7 +191,8 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(const T* __restrict__ A, R
                 float v = acc[i][j][e] * epi.alpha;
                 if (epi.bias) v += epi.bias[col];
                 if (epi.relu) v = fmaxf(v, 0.f);
-                if (epi.res0) v += epi.res0[(long long)row * epi.ld_res0 + col];
+                if (epi.res0) v += epi.res0_bf16 ? bf2f(((const bf16*)epi.res0)[(long long)row * epi.ld_res0 + col])
+                                                 : epi.res0[(long long)row * epi.ld_res0 + col];
                 if (epi.res1) v += epi.res1[(long long)row * epi.ld_res1 + col];
                 if (epi.out_dtype == DT_F32) ((float*)epi.out)[ob + col] = v;
                 else ((bf16*)epi.out)[ob + col] = f2bf(v);

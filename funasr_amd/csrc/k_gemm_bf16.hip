@@ -14,24 +14,47 @@
 // step k run from LDS, then vmcnt(0) + barrier.
 // Requirements (checked by the launcher): K % 64 == 0, row strides % 8 == 0 (16-B aligned
 // rows). Rows beyond M / N are clamped (valid memory) and dropped in the epilogue.
+#include <stdlib.h>
+
 #include "pfm_common.h"
 
 namespace {
 
-constexpr int BM = 256, BN = 256, BK = 64;
-constexpr int ROWB = BK * 2;                       // 128 B per row per stage
-constexpr int TILE = BM * ROWB;                    // 32 KiB (A); W tile is the same size
-constexpr int STAGE = 2 * TILE;                    // 64 KiB
-constexpr int LDS_BYTES = 2 * STAGE;               // 128 KiB
+constexpr int BM = 256, BN = 256;
+
+// Geometry of one variant: BK (K per stage, bf16 elements) and NS (LDS ring stages).
+template <int BK_, int NS_> struct Geo {
+    static constexpr int BK = BK_, NS = NS_;
+    static constexpr int ROWB = BK * 2;              // bytes per tile row per stage (128 or 64)
+    static constexpr int CPR = ROWB / 16;            // 16-B chunks per row (8 or 4)
+    static constexpr int TILE = BM * ROWB;           // A tile bytes (W tile the same)
+    static constexpr int STAGE = 2 * TILE;
+    static constexpr int PIECES = TILE / 1024 / 8;   // 1-KiB DMA pieces per wave per operand
+    static constexpr int LDS = NS * STAGE;
+    // bank swizzle of 16-B slot within a row: conflict-free ds_read_b128 of 16 distinct rows
+    __device__ static inline int swz(int row) { return CPR == 8 ? ((row >> 1) & 7) : ((row >> 2) & 3); }
+};
 
 typedef __attribute__((address_space(3))) void lds_void;
 typedef const __attribute__((address_space(1))) void gbl_void;
 
 __device__ __forceinline__ bool better(float v, int i, float bv, int bi) { return v > bv || (v == bv && i < bi); }
 
+template <int Vb, int Vs> __device__ __forceinline__ void wait_stage(int rem) {
+    // wait until at most `rem` later stages (each 2*PIECES DMA instructions per thread) are in flight
+    constexpr int P = 2 * Geo<Vb, Vs>::PIECES;
+    if (rem >= 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * P) : "memory");
+    else if (rem == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * P) : "memory");
+    else if (rem == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(P) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+template <int BK_, int NS_>
 __global__ __launch_bounds__(512) void gemm_bf16_256_kernel(const bf16* __restrict__ A, RowMap amap,
                                                             const bf16* __restrict__ W, long long ldw, int M, int N,
                                                             int K, int tiles_n, GemmEpi epi) {
+    using G = Geo<BK_, NS_>;
+    constexpr int BK = G::BK, ROWB = G::ROWB, TILE = G::TILE, STAGE = G::STAGE, PIECES = G::PIECES, NS = G::NS;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int nwg = gridDim.x, bid = blockIdx.x;
     const int q = nwg / 8, r = nwg % 8, xcd = bid % 8;
@@ -41,15 +64,16 @@ __global__ __launch_bounds__(512) void gemm_bf16_256_kernel(const bf16* __restri
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wm = wid >> 2, wn = wid & 3;
 
-    // ---- DMA source addresses: wave w, piece j (0..3) covers rows 8*(4w+j) .. +7 of each tile
-    const bf16* ga[4];
-    const bf16* gw[4];
+    // ---- DMA source addresses: wave w, piece j covers rows (PIECES*w + j) * RPP .. +RPP-1
+    constexpr int RPP = 1024 / ROWB;   // rows per 1-KiB piece
+    const bf16* ga[PIECES];
+    const bf16* gw[PIECES];
     {
-        const int sub = lane >> 3, slot = lane & 7;
+        const int sub = lane / G::CPR, slot = lane % G::CPR;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int row = 8 * (4 * wid + j) + sub;
-            const int chunk = slot ^ ((row >> 1) & 7);
+        for (int j = 0; j < PIECES; ++j) {
+            const int row = RPP * (PIECES * wid + j) + sub;
+            const int chunk = slot ^ G::swz(row);
             const int am = min(m0 + row, M - 1), wr = min(n0 + row, N - 1);
             ga[j] = A + amap.off(am) + chunk * 8;
             gw[j] = W + (long long)wr * ldw + chunk * 8;
@@ -58,8 +82,8 @@ __global__ __launch_bounds__(512) void gemm_bf16_256_kernel(const bf16* __restri
     auto stage = [&](int k0, int s) {
         unsigned char* base = smem + s * STAGE;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int piece = 4 * wid + j;
+        for (int j = 0; j < PIECES; ++j) {
+            const int piece = PIECES * wid + j;
             __builtin_amdgcn_global_load_lds((gbl_void*)(ga[j] + k0), (lds_void*)(base + piece * 1024), 16, 0, 0);
             __builtin_amdgcn_global_load_lds((gbl_void*)(gw[j] + k0), (lds_void*)(base + TILE + piece * 1024), 16, 0,
                                              0);
@@ -81,24 +105,31 @@ __global__ __launch_bounds__(512) void gemm_bf16_256_kernel(const bf16* __restri
     for (int i = 0; i < 4; ++i) {
         const int row = wm * 128 + i * 32 + fr;
         aoff[i] = row * ROWB;
-        asw[i] = (row >> 1) & 7;
+        asw[i] = G::swz(row);
     }
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
         const int row = wn * 64 + j * 32 + fr;
         woff[j] = TILE + row * ROWB;
-        wsw[j] = (row >> 1) & 7;
+        wsw[j] = G::swz(row);
     }
 
     const int nk = K / BK;
-    stage(0, 0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    for (int kt = 0; kt < nk; ++kt) {
-        if (kt + 1 < nk) stage((kt + 1) * BK, (kt + 1) & 1);
-        const unsigned char* sb = smem + (kt & 1) * STAGE;
+    // prologue: NS-1 stages in flight
 #pragma unroll
-        for (int kq = 0; kq < 4; ++kq) {
+    for (int sidx = 0; sidx < NS - 1; ++sidx)
+        if (sidx < nk) stage(sidx * BK, sidx);
+    for (int kt = 0; kt < nk; ++kt) {
+        // stage kt landed for this wave's DMAs (later stages may stay in flight), then the barrier
+        // makes every wave's pieces visible and frees slot (kt-1) % NS for re-staging
+        wait_stage<BK_, NS_>(min(NS - 2, nk - 1 - kt));
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        if (kt + NS - 1 < nk) stage((kt + NS - 1) * BK, (kt + NS - 1) % NS);
+        const unsigned char* sb = smem + (kt % NS) * STAGE;
+#pragma unroll
+        for (int kq = 0; kq < BK / 16; ++kq) {
             const int c = 2 * kq + fh;
             bf16x8 af[4], bfr[2];
 #pragma unroll
@@ -111,9 +142,9 @@ __global__ __launch_bounds__(512) void gemm_bf16_256_kernel(const bf16* __restri
                 for (int j = 0; j < 2; ++j)
                     acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
     }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __syncthreads();
 
     // ---- epilogue (C/D map: col = lane&31, row = (e&3) + 8(e>>2) + 4(lane>>5))
     if (epi.amax_val) {
@@ -177,7 +208,13 @@ __global__ __launch_bounds__(512) void gemm_bf16_256_kernel(const bf16* __restri
                 }
                 if (epi.relu) { v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f); }
                 if (epi.res0) {
-                    const float4 r0 = *(const float4*)(epi.res0 + (long long)row * epi.ld_res0 + col);
+                    float4 r0;
+                    if (epi.res0_bf16) {
+                        const bf16x4 rb = *(const bf16x4*)((const bf16*)epi.res0 + (long long)row * epi.ld_res0 + col);
+                        r0 = make_float4(bf2f(rb[0]), bf2f(rb[1]), bf2f(rb[2]), bf2f(rb[3]));
+                    } else {
+                        r0 = *(const float4*)(epi.res0 + (long long)row * epi.ld_res0 + col);
+                    }
                     v.x += r0.x; v.y += r0.y; v.z += r0.z; v.w += r0.w;
                 }
                 if (epi.res1) {
@@ -215,7 +252,8 @@ __global__ __launch_bounds__(512) void gemm_bf16_256_kernel(const bf16* __restri
                 float v = acc[i][j][e] * epi.alpha;
                 if (epi.bias) v += epi.bias[col];
                 if (epi.relu) v = fmaxf(v, 0.f);
-                if (epi.res0) v += epi.res0[(long long)row * epi.ld_res0 + col];
+                if (epi.res0) v += epi.res0_bf16 ? bf2f(((const bf16*)epi.res0)[(long long)row * epi.ld_res0 + col])
+                                                 : epi.res0[(long long)row * epi.ld_res0 + col];
                 if (epi.res1) v += epi.res1[(long long)row * epi.ld_res1 + col];
                 if (epi.out_dtype == DT_F32) ((float*)epi.out)[ob + col] = v;
                 else ((bf16*)epi.out)[ob + col] = f2bf(v);
@@ -225,10 +263,34 @@ __global__ __launch_bounds__(512) void gemm_bf16_256_kernel(const bf16* __restri
     }
 }
 
+int gemm_variant() {   // PFM_GEMM_VARIANT: 0 = BK64 x 2 stages, 1 = BK32 x 4, 2 = BK32 x 5, 3 = BK64 x 2 (alias)
+    static int v = -1;
+    if (v < 0) { const char* e = getenv("PFM_GEMM_VARIANT"); v = e ? atoi(e) : 0; }
+    return v;
+}
+
+template <int BK_, int NS_>
+hipError_t launch_variant(const void* A, RowMap amap, const void* W, long long ldw, int M, int N, int K,
+                          const GemmEpi& e2, hipStream_t st) {
+    using G = Geo<BK_, NS_>;
+    static bool attr_done = false;
+    if (!attr_done) {
+        attr_done = true;
+        (void)hipFuncSetAttribute((const void*)gemm_bf16_256_kernel<BK_, NS_>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS);
+    }
+    const int tiles_m = (M + BM - 1) / BM, tiles_n = (N + BN - 1) / BN;
+    hipLaunchKernelGGL((gemm_bf16_256_kernel<BK_, NS_>), dim3(tiles_m * tiles_n), dim3(512), G::LDS, st,
+                       (const bf16*)A, amap, (const bf16*)W, ldw, M, N, K, tiles_n, e2);
+    PFM_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
 }  // namespace
 
+
 bool pfm_gemm_bf16_256_ok(RowMap amap, long long ldw, int K) {
-    return K % BK == 0 && ldw % 8 == 0 && amap.ld % 8 == 0 && (amap.rows_per_seg <= 0 || amap.seg_stride % 8 == 0);
+    return K % 64 == 0 && ldw % 8 == 0 && amap.ld % 8 == 0 && (amap.rows_per_seg <= 0 || amap.seg_stride % 8 == 0);
 }
 
 int pfm_gemm_bf16_256_amax_tiles(int N) { return ((N + BN - 1) / BN) * (BN / 64); }
@@ -237,17 +299,11 @@ hipError_t pfm_gemm_bf16_256(const void* A, RowMap amap, const void* W, long lon
                              const GemmEpi& epi, hipStream_t st) {
     if (M <= 0 || N <= 0) return hipSuccess;
     if (!pfm_gemm_bf16_256_ok(amap, ldw, K)) return hipErrorInvalidValue;
-    static bool attr_done = false;
-    if (!attr_done) {
-        attr_done = true;
-        (void)hipFuncSetAttribute((const void*)gemm_bf16_256_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  LDS_BYTES);
-    }
-    const int tiles_m = (M + BM - 1) / BM, tiles_n = (N + BN - 1) / BN;
     GemmEpi e2 = epi;
     e2.vec_ok = epi_vec_ok(epi, N);
-    hipLaunchKernelGGL(gemm_bf16_256_kernel, dim3(tiles_m * tiles_n), dim3(512), LDS_BYTES, st, (const bf16*)A, amap,
-                       (const bf16*)W, ldw, M, N, K, tiles_n, e2);
-    PFM_LAUNCH_CHECK();
-    return hipSuccess;
+    switch (gemm_variant()) {
+        case 1: return launch_variant<32, 4>(A, amap, W, ldw, M, N, K, e2, st);
+        case 2: return launch_variant<32, 5>(A, amap, W, ldw, M, N, K, e2, st);
+        default: return launch_variant<64, 2>(A, amap, W, ldw, M, N, K, e2, st);
+    }
 }

@@ -31,6 +31,8 @@ hipError_t pfm_layernorm(const float* x, RowMap xmap, int M, int D, const float*
                          RowMap o2map, int o2dt, hipStream_t st);
 hipError_t pfm_fsmn(const float* v, RowMap vmap, const int* len, int B, int T, int D, const float* w, int K,
                     int left, const float* res, float* out, bf16* out_bf, hipStream_t st);
+hipError_t pfm_fsmn_bf16in(const bf16* v, RowMap vmap, const int* len, int B, int T, int D, const float* wT, int K,
+                           int left, const float* res, float* out, bf16* out_bf, hipStream_t st);
 hipError_t pfm_cif_alpha(const float* hc, int D, const float* wout, const float* bout, const int* len, int B,
                          int T, float smooth, float noise, float tail, float* alphas, hipStream_t st);
 hipError_t pfm_cif_fire(const float* alphas, const float* h, RowMap hmap, int B, int T, int D, int Lcap,
@@ -533,6 +535,7 @@ int pfm_run(pfm_handle* h, void* stream, int mode, const float* feats, const int
     float* QKV = h->QKV.as<float>();
     bf16* QKVb = h->QKVb.as<bf16>();
     float* Fm = h->F.as<float>();
+    bf16* Fb = h->F.as<bf16>();   // fast mode: FSMN memory in bf16 (same buffer)
     float* O = h->O.as<float>();
     bf16* Ob = h->Ob.as<bf16>();
     void* Hh = h->H.p;
@@ -548,26 +551,31 @@ int pfm_run(pfm_handle* h, void* stream, int mode, const float* feats, const int
         else
             HIP_TRY(pfm_layernorm(X, rowmap_plain(D), (int)M, D, P(L.ln1g), P(L.ln1b), c.ln_eps, nullptr, 0, 1.f, Xn,
                                   rowmap_plain(D), dt, nullptr, plain, 0, st));
-        {   // q|k|v = LN1(x) Wqkv^T + b
+        {   // q|k|v = LN1(x) Wqkv^T + b   (fast mode: bf16 only — attention and FSMN read bf16)
             GemmEpi e = epi_default();
             e.bias = P(L.bqkv);
-            e.out = QKV; e.out_map = rowmap_plain(3 * D); e.out_dtype = DT_F32;
-            if (fast) { e.out2 = QKVb; e.out2_map = rowmap_plain(3 * D); }
+            if (fast) { e.out = QKVb; e.out_map = rowmap_plain(3 * D); e.out_dtype = DT_BF16; }
+            else { e.out = QKV; e.out_map = rowmap_plain(3 * D); e.out_dtype = DT_F32; }
             HIP_TRY(GEMM(dt, Xn, rowmap_plain(din), W(L.wqkv), din, (int)M, 3 * D, din, e));
         }
-        // FSMN memory on v (attention.py:207-223)
-        HIP_TRY(pfm_fsmn(QKV + 2 * D, rowmap_plain(3 * D), lens, B, T, D, P(L.fsmn), K, lenc, nullptr, Fm, nullptr, st));
+        // FSMN memory on v (attention.py:207-223); fast mode: bf16 in / bf16 out
+        if (fast)
+            HIP_TRY(pfm_fsmn_bf16in(QKVb + 2 * D, rowmap_plain(3 * D), lens, B, T, D, P(L.fsmn), K, lenc, nullptr,
+                                    nullptr, Fb, st));
+        else
+            HIP_TRY(pfm_fsmn(QKV + 2 * D, rowmap_plain(3 * D), lens, B, T, D, P(L.fsmn), K, lenc, nullptr, Fm, nullptr,
+                             st));
         // masked MHA
         if (fast)
             HIP_TRY(ATTN(DT_BF16, QKVb, rowmap_plain(3 * D), QKVb + D, rowmap_plain(3 * D), QKVb + 2 * D,
-                                  rowmap_plain(3 * D), nullptr, D, Ob, lens, B, T, T));
+                         rowmap_plain(3 * D), nullptr, D, Ob, lens, B, T, T));
         else
             HIP_TRY(ATTN(DT_F32, QKV, rowmap_plain(3 * D), QKV + D, rowmap_plain(3 * D), QKV + 2 * D,
-                                  rowmap_plain(3 * D), O, D, nullptr, lens, B, T, T));
+                         rowmap_plain(3 * D), O, D, nullptr, lens, B, T, T));
         {   // x = (x +) linear_out(att) + fsmn   (encoder.py:120-137: no residual when in != out)
             GemmEpi e = epi_default();
             e.bias = P(L.bo);
-            e.res0 = Fm; e.ld_res0 = D;
+            e.res0 = fast ? (const float*)Fb : Fm; e.ld_res0 = D; e.res0_bf16 = fast ? 1 : 0;
             if (din == D) { e.res1 = X; e.ld_res1 = D; }
             e.out = X; e.out_map = rowmap_plain(D); e.out_dtype = DT_F32;
             HIP_TRY(GEMM(dt, fast ? (const void*)Ob : (const void*)O, rowmap_plain(D), W(L.wo), D, (int)M, D, D, e));

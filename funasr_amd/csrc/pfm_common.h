@@ -69,6 +69,7 @@ struct GemmEpi {
     const float* res1;      // residual #2 (same layout as res0, ld_res1) or null
     long long ld_res0, ld_res1;
     int relu;               // 1: relu before residual adds
+    int res0_bf16;          // res0 points at bf16 data (fast mode FSMN memory)
     float alpha;            // scale applied to A.W^T before bias
     void* out;              // C
     RowMap out_map;         // row addressing of C (and of residuals via their own ld)
