@@ -295,7 +295,7 @@ __global__ __launch_bounds__(256) void cif_fire_kernel(const float* __restrict__
 // tokens[b, l] for l < ntok[b], -1 elsewhere (paraformer/model.py:527-536).
 // ------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void argmax_reduce_kernel(const float* __restrict__ val, const int* __restrict__ idx,
-                                                            int ntiles, int B, int L, const int* __restrict__ ntok,
+                                                            int ntiles, int ncount, int B, int L, const int* __restrict__ ntok,
                                                             int Lcap, int* __restrict__ tokens, float* __restrict__ score) {
     const int lane = threadIdx.x & 63;
     const long long row = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -303,7 +303,7 @@ __global__ __launch_bounds__(256) void argmax_reduce_kernel(const float* __restr
     const int b = (int)(row / L), l = (int)(row % L);
     float bv = -INFINITY;
     int bi = 0x7fffffff;
-    for (int i = lane; i < ntiles; i += 64) {
+    for (int i = lane; i < ncount; i += 64) {
         const float v = val[row * ntiles + i];
         const int ii = idx[row * ntiles + i];
         if (v > bv || (v == bv && ii < bi)) { bv = v; bi = ii; }
@@ -400,12 +400,14 @@ hipError_t pfm_cif_fire(const float* alphas, const float* h, RowMap hmap, int B,
     return hipSuccess;
 }
 
-hipError_t pfm_argmax_reduce(const float* val, const int* idx, int ntiles, int B, int L, const int* ntok,
+// ntiles: row stride of the partial buffers; ncount: valid 64-column blocks (ceil(N/64))
+hipError_t pfm_argmax_reduce(const float* val, const int* idx, int ntiles, int ncount, int B, int L, const int* ntok,
                              int Lcap, int* tokens, float* score, hipStream_t st) {
     const long long n = (long long)B * L;
     if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(argmax_reduce_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, st, val, idx, ntiles, B,
-                       L, ntok, Lcap, tokens, score);
+    if (ncount > ntiles) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(argmax_reduce_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, st, val, idx, ntiles, ncount,
+                       B, L, ntok, Lcap, tokens, score);
     PFM_LAUNCH_CHECK();
     return hipSuccess;
 }

@@ -147,38 +147,7 @@ __global__ __launch_bounds__(512) void gemm_bf16_256_kernel(const bf16* __restri
     __syncthreads();
 
     // ---- epilogue (C/D map: col = lane&31, row = (e&3) + 8(e>>2) + 4(lane>>5))
-    if (epi.amax_val) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-#pragma unroll
-            for (int e = 0; e < 16; ++e) {
-                const int row = m0 + wm * 128 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * fh;
-                float bv = -INFINITY;
-                int bi = 0x7fffffff;
-#pragma unroll
-                for (int j = 0; j < 2; ++j) {
-                    const int col = n0 + wn * 64 + j * 32 + fr;
-                    if (col < N) {
-                        const float v = acc[i][j][e] * epi.alpha + (epi.bias ? epi.bias[col] : 0.f);
-                        if (better(v, col, bv, bi)) { bv = v; bi = col; }
-                    }
-                }
-#pragma unroll
-                for (int o = 1; o < 32; o <<= 1) {
-                    const float ov = __shfl_xor(bv, o, 64);
-                    const int oi = __shfl_xor(bi, o, 64);
-                    if (better(ov, oi, bv, bi)) { bv = ov; bi = oi; }
-                }
-                if (fr == 0 && row < M) {
-                    const long long p = (long long)row * epi.n_tiles + (tn * 4 + wn);
-                    epi.amax_val[p] = bv;
-                    epi.amax_idx[p] = bi;
-                }
-            }
-        }
-        if (!epi.out) return;
-    }
-    if (epi.vec_ok) {
+    if (epi.vec_ok || epi.amax_val) {
         // LDS-staged epilogue: each wave re-lays its 32x64 sub-tiles row-major in its own 8.5 KiB
         // LDS slice, then every lane handles float4 column groups of whole rows: 16-B bias /
         // residual loads and 16-B (f32) or 8-B (bf16) stores, 256 contiguous bytes per 16 lanes.
@@ -194,8 +163,33 @@ __global__ __launch_bounds__(512) void gemm_bf16_256_kernel(const bf16* __restri
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            if (epi.amax_val) {
+                // fused row-argmax of the output layer over this wave's 64 columns: 2 lanes per staged
+                // row scan 32 columns each in order (first index wins ties, like torch.argmax)
+                const int rr = lane >> 1, half = lane & 1;
+                const int cb = n0 + wn * 64 + half * 32;
+                float bv = -INFINITY;
+                int bi = 0x7fffffff;
+                for (int cc = 0; cc < 32; ++cc) {
+                    const int col = cb + cc;
+                    if (col < N) {
+                        const float v = ep[rr * EP + half * 32 + cc] * epi.alpha + (epi.bias ? epi.bias[col] : 0.f);
+                        if (v > bv) { bv = v; bi = col; }
+                    }
+                }
+                const float ov = __shfl_xor(bv, 1, 64);
+                const int oi = __shfl_xor(bi, 1, 64);
+                if (better(ov, oi, bv, bi)) { bv = ov; bi = oi; }
+                const int row = m0 + wm * 128 + i * 32 + rr;
+                if (half == 0 && row < M) {
+                    const long long p = (long long)row * epi.n_tiles + (tn * 4 + wn);
+                    epi.amax_val[p] = bv;
+                    epi.amax_idx[p] = bi;
+                }
+            }
 #pragma unroll
             for (int sidx = 0; sidx < 8; ++sidx) {
+                if (!epi.out) break;
                 const int f = lane + 64 * sidx, rr = f >> 4, c4 = f & 15;
                 const int row = m0 + wm * 128 + i * 32 + rr;
                 const int col = n0 + wn * 64 + c4 * 4;

@@ -37,7 +37,7 @@ hipError_t pfm_cif_alpha(const float* hc, int D, const float* wout, const float*
                          int T, float smooth, float noise, float tail, float* alphas, hipStream_t st);
 hipError_t pfm_cif_fire(const float* alphas, const float* h, RowMap hmap, int B, int T, int D, int Lcap,
                         float* emb, float* peaks, int* n_fire, int* ntok, hipStream_t st);
-hipError_t pfm_argmax_reduce(const float* val, const int* idx, int ntiles, int B, int L, const int* ntok,
+hipError_t pfm_argmax_reduce(const float* val, const int* idx, int ntiles, int ncount, int B, int L, const int* ntok,
                              int Lcap, int* tokens, float* score, hipStream_t st);
 hipError_t pfm_fill_i32(int* p, long long n, int v, hipStream_t st);
 hipError_t pfm_f32_to_bf16(const float* x, bf16* y, long long n, hipStream_t st);
@@ -725,7 +725,8 @@ int pfm_run(pfm_handle* h, void* stream, int mode, const float* feats, const int
         e.out = nullptr;
         HIP_TRY(GEMM(dt, Xdn, rowmap_plain(D), W(h->out_w), D, (int)Ml, c.vocab_size, D, e));
         if (L_cap > 0)
-            HIP_TRY(pfm_argmax_reduce(h->amv.as<float>(), h->ami.as<int>(), ntl, B, L, ntok, L_cap, tokens, nullptr, st));
+            HIP_TRY(pfm_argmax_reduce(h->amv.as<float>(), h->ami.as<int>(), ntl, (c.vocab_size + 63) / 64, B, L, ntok,
+                                      L_cap, tokens, nullptr, st));
     }
     return PFM_OK;
 }
