@@ -15,6 +15,8 @@
 // bf16 ("fast"): v_mfma_f32_32x32x16_bf16 — 8 + 8 MFMA per tile; P^T feeds the second
 //   product straight from the S^T accumulator registers (k-order permuted accordingly) and
 //   V is staged transposed in LDS.
+#include <stdlib.h>
+
 #include "pfm_common.h"
 
 namespace {
@@ -163,8 +165,23 @@ __global__ __launch_bounds__(256) void attn_f32_kernel(AttnArgs a) {
         }
 }
 
-__global__ __launch_bounds__(256) void attn_bf16_kernel(AttnArgs a) {
+// ---- bf16 kernel geometry: 64-key tiles; K row-major with a 16-B chunk XOR swizzle (conflict-free
+// ds_read_b128 of 16 distinct rows); V row-major with a 320-B pitch so the transposing
+// ds_read_b64_tr_b16 reads (4 key rows x 32 B per half-wave) hit 64 distinct banks.
+constexpr int KT2 = 64;
+constexpr int KROW = DK * 2;                    // 256 B
+constexpr int VROW = DK * 2 + 64;               // 320 B
+constexpr int KTILE = KT2 * KROW, VTILE = KT2 * VROW;
+constexpr int STG2 = KTILE + VTILE;             // 36 KiB per stage
+constexpr float RESCALE_THR = 8.0f;             // lazy O rescale: only when a row max grows by > 8
+
+typedef short v4i16 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
+
+template <int NWV>
+__global__ __launch_bounds__(NWV * 64) void attn_bf16_kernel(AttnArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    constexpr int NT = NWV * 64, QBLK = NWV * QW;
     const int qt = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int fr = lane & 31, fh = lane >> 5;
@@ -173,7 +190,8 @@ __global__ __launch_bounds__(256) void attn_bf16_kernel(AttnArgs a) {
     const bf16* K = (const bf16*)a.k;
     const bf16* V = (const bf16*)a.v;
 
-    const int qrow = qt * 128 + wid * QW + fr;
+    // Q fragment (B operand of S^T = K.Q^T): lane (q = fr) holds dims 16kq + 8fh + j, pre-scaled
+    const int qrow = qt * QBLK + wid * QW + fr;
     bf16x8 qf[8];
     {
         const bool ok = qrow < a.Tq;
@@ -195,85 +213,114 @@ __global__ __launch_bounds__(256) void attn_bf16_kernel(AttnArgs a) {
     for (int d = 0; d < 4; ++d)
 #pragma unroll
         for (int e = 0; e < 16; ++e) o[d][e] = 0.f;
-    float mrun = -INFINITY, lrun = 0.f;
-    const int ntiles = (klen + KT - 1) / KT;
-    // K tile: 32 rows x 256 B = 512 chunks; V tile 32 keys x 256 B = 512 chunks -> 2+2 per thread
-    auto stage = [&](int t, int s) {
-        unsigned char* Ks = smem + s * (KT * KP16 + DK * VTP16);
-        unsigned char* Vt = Ks + KT * KP16;
+    float mused = -INFINITY, lrun = 0.f;
+    const int ntiles = (klen + KT2 - 1) / KT2;
+
+    // register staging: each thread moves (64 rows x 16 chunks) / NT chunks of K and of V per tile
+    constexpr int CPT = KT2 * 16 / NT;
+    uint4 rk[CPT], rv[CPT];
+    auto gload = [&](int t) {
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            const int c = tid + 256 * i, row = c >> 4, ch = c & 15;
-            const int key = t * KT + row;
-            uint4 kx = make_uint4(0, 0, 0, 0), vx = make_uint4(0, 0, 0, 0);
+        for (int i = 0; i < CPT; ++i) {
+            const int c = tid + NT * i, row = c >> 4, ch = c & 15;
+            const int key = t * KT2 + row;
+            rk[i] = make_uint4(0, 0, 0, 0);
+            rv[i] = make_uint4(0, 0, 0, 0);
             if (key < klen) {
                 const long long m = (long long)b * a.Tk + key;
-                kx = *(const uint4*)(K + a.kmap.off(m) + h * DK + ch * 8);
-                vx = *(const uint4*)(V + a.vmap.off(m) + h * DK + ch * 8);
+                rk[i] = *(const uint4*)(K + a.kmap.off(m) + h * DK + ch * 8);
+                rv[i] = *(const uint4*)(V + a.vmap.off(m) + h * DK + ch * 8);
             }
-            *(uint4*)(Ks + row * KP16 + ch * 16) = kx;
-            const unsigned short* vs = (const unsigned short*)&vx;
-#pragma unroll
-            for (int j = 0; j < 8; ++j)
-                *(unsigned short*)(Vt + (ch * 8 + j) * VTP16 + row * 2) = vs[j];
         }
     };
-    if (ntiles > 0) stage(0, 0);
+    auto sstore = [&](int s) {
+        unsigned char* Ks = smem + s * STG2;
+        unsigned char* Vs = Ks + KTILE;
+#pragma unroll
+        for (int i = 0; i < CPT; ++i) {
+            const int c = tid + NT * i, row = c >> 4, ch = c & 15;
+            *(uint4*)(Ks + row * KROW + ((ch ^ (row & 15)) << 4)) = rk[i];
+            *(uint4*)(Vs + row * VROW + ch * 16) = rv[i];
+        }
+    };
+    // per-lane constants of the transposed V read: lane 4q+p of its 16-lane group addresses key
+    // row q, head dims 4p..4p+3 of the group's 16-column block
+    const int tg = lane >> 4, ti = lane & 15;
+    const int tr_key = 4 * (tg >> 1) + (ti >> 2);
+    const int tr_col = 16 * (tg & 1) + 4 * (ti & 3);
+
+    if (ntiles > 0) { gload(0); sstore(0); }
     __syncthreads();
     for (int t = 0; t < ntiles; ++t) {
         const int cur = t & 1;
-        if (t + 1 < ntiles) stage(t + 1, cur ^ 1);
-        const unsigned char* Ks = smem + cur * (KT * KP16 + DK * VTP16);
-        const unsigned char* Vt = Ks + KT * KP16;
-        f32x16 s;
+        if (t + 1 < ntiles) gload(t + 1);
+        const unsigned char* Ks = smem + cur * STG2;
+        const unsigned char* Vs = Ks + KTILE;
+        f32x16 s[2];
 #pragma unroll
-        for (int e = 0; e < 16; ++e) s[e] = 0.f;
+        for (int kb = 0; kb < 2; ++kb) {
 #pragma unroll
-        for (int kq = 0; kq < 8; ++kq) {
-            const bf16x8 kx = *(const bf16x8*)(Ks + fr * KP16 + kq * 32 + fh * 16);
-            s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kx, qf[kq], s, 0, 0, 0);
-        }
-        float mt = -INFINITY;
+            for (int e = 0; e < 16; ++e) s[kb][e] = 0.f;
+            const int row = kb * 32 + fr;
 #pragma unroll
-        for (int e = 0; e < 16; ++e) {
-            const int key = t * KT + kappa(e) + 4 * fh;
-            if (key >= klen) s[e] = -INFINITY;
-            mt = fmaxf(mt, s[e]);
-        }
-        mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
-        const float mnew = fmaxf(mrun, mt);
-        const float corr = __expf(mrun - mnew);
-        float ls = 0.f;
-#pragma unroll
-        for (int e = 0; e < 16; ++e) {
-            s[e] = __expf(s[e] - mnew);
-            ls += s[e];
-        }
-        ls += __shfl_xor(ls, 32, 64);
-        lrun = lrun * corr + ls;
-        mrun = mnew;
-#pragma unroll
-        for (int d = 0; d < 4; ++d)
-#pragma unroll
-            for (int e = 0; e < 16; ++e) o[d][e] *= corr;
-        // P^T as B operand: k-step st uses registers 8st..8st+7; element j of half fh is key
-        // 16st + 8(j>>2) + 4fh + (j&3). V^T operand element j must be that same key.
-#pragma unroll
-        for (int st = 0; st < 2; ++st) {
-            bf16x8 pb;
-#pragma unroll
-            for (int j = 0; j < 8; ++j) pb[j] = f2bf(s[8 * st + j]);
-#pragma unroll
-            for (int d = 0; d < 4; ++d) {
-                const unsigned char* vr = Vt + (d * 32 + fr) * VTP16;
-                const uint2 lo = *(const uint2*)(vr + (16 * st + 4 * fh) * 2);
-                const uint2 hi = *(const uint2*)(vr + (16 * st + 8 + 4 * fh) * 2);
-                uint4 vv = make_uint4(lo.x, lo.y, hi.x, hi.y);
-                bf16x8 va;
-                __builtin_memcpy(&va, &vv, 16);
-                o[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va, pb, o[d], 0, 0, 0);
+            for (int kq = 0; kq < 8; ++kq) {
+                const bf16x8 kx = *(const bf16x8*)(Ks + row * KROW + (((2 * kq + fh) ^ (row & 15)) << 4));
+                s[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kx, qf[kq], s[kb], 0, 0, 0);
             }
         }
+        // lane holds S^T[key = t*64 + kb*32 + kappa(e) + 4fh][q = fr]
+        float mt = -INFINITY;
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                const int key = t * KT2 + kb * 32 + kappa(e) + 4 * fh;
+                if (key >= klen) s[kb][e] = -INFINITY;
+                mt = fmaxf(mt, s[kb][e]);
+            }
+        mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+        if (mt > mused + RESCALE_THR) {    // lazy rescale (per query row; rare after the first tile)
+            const float corr = __expf(mused - mt);
+            lrun *= corr;
+#pragma unroll
+            for (int d = 0; d < 4; ++d)
+#pragma unroll
+                for (int e = 0; e < 16; ++e) o[d][e] *= corr;
+            mused = mt;
+        }
+        float ls = 0.f;
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                s[kb][e] = __expf(s[kb][e] - mused);
+                ls += s[kb][e];
+            }
+        ls += __shfl_xor(ls, 32, 64);
+        lrun += ls;
+        // O^T[d][q] += sum_key V[key][d] P[q][key]; P^T from the accumulator registers (k-step st of
+        // key block kb = registers 8st..8st+7: key 16st + 8(j>>2) + 4fh + (j&3)), V^T by tr reads
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+            for (int st = 0; st < 2; ++st) {
+                bf16x8 pb;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) pb[j] = f2bf(s[kb][8 * st + j]);
+                const int key0 = kb * 32 + 16 * st + tr_key;
+#pragma unroll
+                for (int d = 0; d < 4; ++d) {
+                    const unsigned char* vp = Vs + key0 * VROW + (d * 32 + tr_col) * 2;
+                    const v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)vp);
+                    const v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(vp + 8 * VROW));
+                    bf16x8 va;
+                    __builtin_memcpy(&va, &lo, 8);
+                    __builtin_memcpy(((char*)&va) + 8, &hi, 8);
+                    o[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va, pb, o[d], 0, 0, 0);
+                }
+            }
+        }
+        if (t + 1 < ntiles) sstore(cur ^ 1);
         __syncthreads();
     }
     if (qrow >= a.Tq) return;
@@ -283,11 +330,15 @@ __global__ __launch_bounds__(256) void attn_bf16_kernel(AttnArgs a) {
 #pragma unroll
     for (int d = 0; d < 4; ++d)
 #pragma unroll
-        for (int e = 0; e < 16; ++e) {
-            const int col = d * 32 + kappa(e) + 4 * fh;
-            const float v = o[d][e] * inv;
-            if (op) op[col] = v;
-            if (op2) op2[col] = f2bf(v);
+        for (int g = 0; g < 4; ++g) {   // registers 4g..4g+3 are 4 consecutive head dims
+            const int col = d * 32 + 8 * g + 4 * fh;
+            const float v0 = o[d][4 * g] * inv, v1 = o[d][4 * g + 1] * inv;
+            const float v2 = o[d][4 * g + 2] * inv, v3 = o[d][4 * g + 3] * inv;
+            if (op) *(float4*)(op + col) = make_float4(v0, v1, v2, v3);
+            if (op2) {
+                bf16x4 t4 = {f2bf(v0), f2bf(v1), f2bf(v2), f2bf(v3)};
+                *(bf16x4*)(op2 + col) = t4;
+            }
         }
 }
 
@@ -307,13 +358,27 @@ hipError_t pfm_attention(int dtype, const void* q, RowMap qmap, const void* k, R
     if (!attr_done) {
         attr_done = true;
         (void)hipFuncSetAttribute((const void*)attn_f32_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, LDS32);
-        (void)hipFuncSetAttribute((const void*)attn_bf16_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, LDS16);
+        (void)hipFuncSetAttribute((const void*)attn_bf16_kernel<4>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  2 * STG2);
+        (void)hipFuncSetAttribute((const void*)attn_bf16_kernel<8>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  2 * STG2);
     }
-    dim3 grid((Tq + 127) / 128, heads, B), block(256);
-    if (dtype == DT_F32) hipLaunchKernelGGL(attn_f32_kernel, grid, block, LDS32, st, a);
-    else hipLaunchKernelGGL(attn_bf16_kernel, grid, block, LDS16, st, a);
+    if (dtype == DT_F32) {
+        dim3 grid((Tq + 127) / 128, heads, B), block(256);
+        hipLaunchKernelGGL(attn_f32_kernel, grid, block, LDS32, st, a);
+    } else {
+        const char* e = getenv("PFM_ATTN_WAVES");
+        const int nw = e ? atoi(e) : 8;
+        if (nw == 8) {
+            dim3 grid((Tq + 255) / 256, heads, B), block(512);
+            hipLaunchKernelGGL(attn_bf16_kernel<8>, grid, block, 2 * STG2, st, a);
+        } else {
+            dim3 grid((Tq + 127) / 128, heads, B), block(256);
+            hipLaunchKernelGGL(attn_bf16_kernel<4>, grid, block, 2 * STG2, st, a);
+        }
+    }
     PFM_LAUNCH_CHECK();
     return hipSuccess;
 }
 
-int pfm_attention_lds_bytes(int dtype) { return dtype == DT_F32 ? LDS32 : LDS16; }
+int pfm_attention_lds_bytes(int dtype) { return dtype == DT_F32 ? LDS32 : 2 * STG2; }

@@ -1,0 +1,45 @@
+"""In-process interleaved A/B of bf16 GEMM tile configs (PFM_GEMM_CFG read per launch) on the path's
+shapes; N=512 shapes carry an f32 residual like the out-proj / FFN2 epilogues. Median of rounds."""
+import os, sys
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np
+import torch
+from funasr_amd import runtime as rt
+
+SHAPES = [("qkv", 32000, 1536, 512), ("out+res", 32000, 512, 512), ("ffn1", 32000, 2048, 512),
+          ("ffn2+res", 32000, 512, 2048), ("conv", 32000, 512, 1536), ("kv_all", 32000, 16384, 512),
+          ("dffn1", 14784, 2048, 512), ("dffn2+res", 14784, 512, 2048), ("dq", 14784, 512, 512),
+          ("sq4k", 4096, 4096, 4096)]
+CFGS = [int(c) for c in (sys.argv[1] if len(sys.argv) > 1 else "1,2,3,4,5").split(",")]
+
+
+def main():
+    dev = torch.device("cuda", 0)
+    ev = lambda: torch.cuda.Event(enable_timing=True)
+    for name, M, N, K in SHAPES:
+        torch.manual_seed(0)
+        A = torch.randn(M, K, device=dev).bfloat16()
+        W = (torch.randn(N, K, device=dev) / K ** 0.5).bfloat16()
+        R = torch.randn(M, N, device=dev) if "res" in name else None
+        fl = 2.0 * M * N * K
+        res = {c: [] for c in CFGS}
+        for rnd in range(5):
+            for c in CFGS:
+                os.environ["PFM_GEMM_CFG"] = str(c)
+                rt.op_gemm(A, W, res=R)
+                a, b = ev(), ev()
+                a.record()
+                for _ in range(10):
+                    rt.op_gemm(A, W, res=R)
+                b.record()
+                torch.cuda.synchronize()
+                res[c].append(a.elapsed_time(b) / 10)
+        line = f"{name:10s} M={M:6d} N={N:6d} K={K:5d} |"
+        for c in CFGS:
+            ms = float(np.median(res[c]))
+            line += f" c{c}: {ms*1e3:7.1f}us {fl/ms/1e9:6.0f}TF |"
+        print(line, flush=True)
+
+
+if __name__ == "__main__":
+    main()
