@@ -157,12 +157,29 @@ __global__ __launch_bounds__(256) void fsmn_win_kernel(const TIN* __restrict__ v
     float4 w[KK];
 #pragma unroll
     for (int k = 0; k < KK; ++k) w[k] = *(const float4*)(wT + (long long)k * D + c);
+    // rows of one utterance are contiguous (plain map, or one segment per utterance: host-checked), so
+    // the window is ubase + tt*ld. Loads are unconditional from a clamped row and masked afterwards:
+    // all FR+KK-1 loads are in flight together instead of one branch + vmcnt(0) round trip per row.
+    const long long ubase = vmap.rows_per_seg > 0 ? (long long)b * vmap.seg_stride : (long long)b * T * vmap.ld;
     float4 x[FR + KK - 1];
 #pragma unroll
     for (int i = 0; i < FR + KK - 1; ++i) {
         const int tt = t0 - left + i;
-        x[i] = (tt >= 0 && tt < L) ? load4<TIN>(v + vmap.off((long long)b * T + tt) + c)
-                                   : make_float4(0, 0, 0, 0);
+        const int tc = min(max(tt, 0), T - 1);
+        x[i] = load4<TIN>(v + ubase + (long long)tc * vmap.ld + c);
+    }
+#pragma unroll
+    for (int i = 0; i < FR + KK - 1; ++i) {
+        const int tt = t0 - left + i;
+        if (!(tt >= 0 && tt < L)) x[i] = make_float4(0, 0, 0, 0);
+    }
+    // residual rows are read before any store: vmcnt retires in order, so a load issued after a
+    // store would wait for that store
+    float4 rv[FR];
+    if (res) {
+#pragma unroll
+        for (int i = 0; i < FR; ++i)
+            rv[i] = *(const float4*)(res + ((long long)b * T + min(t0 + i, T - 1)) * D + c);
     }
 #pragma unroll
     for (int i = 0; i < FR; ++i) {
@@ -183,7 +200,7 @@ __global__ __launch_bounds__(256) void fsmn_win_kernel(const TIN* __restrict__ v
             y = make_float4(acc.x + self.x, acc.y + self.y, acc.z + self.z, acc.w + self.w);
         }
         if (res) {
-            const float4 r = *(const float4*)(res + row * D + c);
+            const float4 r = rv[i];
             y.x = r.x + y.x; y.y = r.y + y.y; y.z = r.z + y.z; y.w = r.w + y.w;
         }
         if (out) *(float4*)(out + row * D + c) = y;
@@ -356,7 +373,7 @@ hipError_t pfm_fsmn(const float* v, RowMap vmap, const int* len, int B, int T, i
                     int left, const float* res, float* out, bf16* out_bf, hipStream_t st) {
     if (B <= 0 || T <= 0) return hipSuccess;
     if (D % 4 != 0 || left < 0 || left >= K) return hipErrorInvalidValue;
-    if (K == 11) {
+    if (K == 11 && (vmap.rows_per_seg <= 0 || vmap.rows_per_seg == T)) {
         const long long n = (long long)B * ((T + FR - 1) / FR) * (D / 4);
         hipLaunchKernelGGL((fsmn_win_kernel<11, float>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, v, vmap,
                            len, B, T, D, wT, left, res, out, out_bf);
@@ -375,6 +392,7 @@ hipError_t pfm_fsmn_bf16in(const bf16* v, RowMap vmap, const int* len, int B, in
                            int left, const float* res, float* out, bf16* out_bf, hipStream_t st) {
     if (B <= 0 || T <= 0) return hipSuccess;
     if (D % 4 != 0 || K != 11 || left < 0 || left >= K) return hipErrorInvalidValue;
+    if (vmap.rows_per_seg > 0 && vmap.rows_per_seg != T) return hipErrorInvalidValue;
     const long long n = (long long)B * ((T + FR - 1) / FR) * (D / 4);
     hipLaunchKernelGGL((fsmn_win_kernel<11, bf16>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, v, vmap, len,
                        B, T, D, wT, left, res, out, out_bf);

@@ -15,6 +15,8 @@
 // are clamped to valid memory and dropped in the epilogue.
 #include <stdlib.h>
 
+#include <algorithm>
+
 #include "pfm_common.h"
 
 namespace {
@@ -22,8 +24,9 @@ namespace {
 typedef __attribute__((address_space(3))) void lds_void;
 typedef const __attribute__((address_space(1))) void gbl_void;
 
-template <int BM_, int BN_, int WGM_, int WGN_, int BK_, int NS_> struct Cfg {
+template <int BM_, int BN_, int WGM_, int WGN_, int BK_, int NS_, bool PP_ = false> struct Cfg {
     static constexpr int BM = BM_, BN = BN_, WGM = WGM_, WGN = WGN_, BK = BK_, NS = NS_;
+    static constexpr bool PP = PP_;   // ping-pong: wave-row groups staggered by one barrier
     static constexpr int NW = WGM * WGN, NT = NW * 64;
     static constexpr int WTM = BM / WGM, WTN = BN / WGN;
     static constexpr int MI = WTM / 32, NI = WTN / 32;
@@ -35,6 +38,7 @@ template <int BM_, int BN_, int WGM_, int WGN_, int BK_, int NS_> struct Cfg {
     static constexpr int LDS = (NS * STAGE > NW * EPW) ? NS * STAGE : NW * EPW;
     static_assert(TA % (1024 * NW) == 0 && TW % (1024 * NW) == 0, "tile not divisible into DMA pieces");
     static_assert(WTN == 64, "epilogue / argmax partials assume 64-column wave tiles");
+    static_assert(!PP || (WGM == 2 && NS >= 3), "ping-pong needs two wave-row groups and >= 3 stages");
     __device__ static inline int swz(int row) { return CPR == 8 ? ((row >> 1) & 7) : ((row >> 2) & 3); }
 };
 
@@ -57,7 +61,7 @@ __global__ __launch_bounds__(C::NT) void gemm_bf16_kernel(const bf16* __restrict
     const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
     const int tm = wg / tiles_n, tn = wg % tiles_n;
     const int m0 = tm * C::BM, n0 = tn * C::BN;
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wid / C::WGN, wn = wid % C::WGN;
     const int fr = lane & 31, fh = lane >> 5;
 
@@ -113,6 +117,65 @@ __global__ __launch_bounds__(C::NT) void gemm_bf16_kernel(const bf16* __restrict
 #pragma unroll
     for (int s = 0; s < NS - 1; ++s)
         if (s < nk) stage(s * BK, s);
+    if constexpr (C::PP) {
+        // Ping-pong schedule. Wave-row group g = wm (0/1; the two groups share every SIMD). Per K-tile t
+        // each wave runs an R phase (issue the DMA for stage t+NS-1, read all fragments of stage t,
+        // lgkmcnt(0)) and an M phase (the MFMAs), each closed by an s_barrier. Group 1 starts one
+        // barrier late, so one group's LDS reads + DMA issue overlap the other group's MFMAs.
+        // Common barrier numbering: G0 runs R(t) before #2t+1 and M(t) before #2t+2; G1 runs R(t)
+        // before #2t+2 and M(t) before #2t+3.
+        //  RAW: every wave retires its own stage-(t+1) DMA before common barrier #2t+2 (G0: end of
+        //       M(t), G1: end of R(t)); readers of stage t+1 start after #2t+2 (G0) / #2t+3 (G1).
+        //  WAR: stage t+NS-1 overwrites buffer (t-1)%NS in R(t), i.e. after #2t (G0) / #2t+1 (G1);
+        //       the last reads of that buffer (R(t-1)) were retired before #2t-1 (G0) / #2t (G1).
+        constexpr int P = PA + PW;
+        const int grp = wm;
+        auto retire_next = [&](int kt) {   // stage kt+1 landed (own pieces)
+            const int rem = nk - 2 - kt;    // stages issued beyond kt+1
+            if (rem >= NS - 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(P * (NS - 2)) : "memory");
+            else if (NS - 2 >= 2 && rem == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(P) : "memory");
+            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        };
+        // stage 0 complete and visible to everyone before either group reads it
+        if (nk - 1 >= NS - 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(P * (NS - 2)) : "memory");
+        else if (NS - 2 >= 2 && nk - 1 == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(P) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (grp == 1) __builtin_amdgcn_s_barrier();
+        for (int kt = 0; kt < nk; ++kt) {
+            __builtin_amdgcn_sched_barrier(0);
+            if (kt + NS - 1 < nk) stage((kt + NS - 1) * BK, (kt + NS - 1) % NS);
+            const unsigned char* sb = smem + (kt % NS) * C::STAGE;
+            bf16x8 af[BK / 16][MI], bfr[BK / 16][NI];
+#pragma unroll
+            for (int kq = 0; kq < BK / 16; ++kq) {
+                const int c = 2 * kq + fh;
+#pragma unroll
+                for (int j = 0; j < NI; ++j) bfr[kq][j] = *(const bf16x8*)(sb + woff[j] + ((c ^ wsw[j]) << 4));
+#pragma unroll
+                for (int i = 0; i < MI; ++i) af[kq][i] = *(const bf16x8*)(sb + aoff[i] + ((c ^ asw[i]) << 4));
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            if (grp == 1 && kt + 1 < nk) retire_next(kt);
+            __builtin_amdgcn_sched_barrier(0);
+            __builtin_amdgcn_s_barrier();
+            __builtin_amdgcn_sched_barrier(0);
+            __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+            for (int kq = 0; kq < BK / 16; ++kq)
+#pragma unroll
+                for (int i = 0; i < MI; ++i)
+#pragma unroll
+                    for (int j = 0; j < NI; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[kq][i], bfr[kq][j], acc[i][j], 0, 0, 0);
+            __builtin_amdgcn_s_setprio(0);
+            if (grp == 0 && kt + 1 < nk) retire_next(kt);
+            __builtin_amdgcn_sched_barrier(0);
+            __builtin_amdgcn_s_barrier();
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        if (grp == 0) __builtin_amdgcn_s_barrier();   // match group 1's stagger barrier
+    } else
     for (int kt = 0; kt < nk; ++kt) {
         wait_vm<PA + PW>(min(NS - 2, nk - 1 - kt));
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -247,12 +310,192 @@ __global__ __launch_bounds__(C::NT) void gemm_bf16_kernel(const bf16* __restrict
     }
 }
 
+// Persistent variant: gridDim.x = min(tiles, CUs) blocks; block b walks tiles slot(b), slot(b)+grid, ...
+// The LDS-DMA ring runs over the flattened (tile, k-step) sequence, so the next tile's first NS-1
+// stages are in flight while the current tile finishes and runs its epilogue; the epilogue stages
+// 16-row halves of each wave's 32-row sub-tiles in a wave-private LDS slice next to the ring, and its
+// stores drain behind the next tile's MFMAs. Blocks that share an XCD (bid % 8) take consecutive
+// tile slots, so each XCD's L2 holds a compact band of A rows / W columns.
+template <class C, int EPR>
+__global__ __launch_bounds__(C::NT) void gemm_bf16_persist_kernel(const bf16* __restrict__ A, RowMap amap,
+                                                                  const bf16* __restrict__ W, long long ldw, int M,
+                                                                  int N, int K, int tiles_m, int tiles_n, GemmEpi epi) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    constexpr int BK = C::BK, NS = C::NS, ROWB = C::ROWB, MI = C::MI, NI = C::NI, PA = C::PA, PW = C::PW;
+    constexpr int EP = C::EP, EPH = EPR * EP * 4;   // EPR-row epilogue chunks (8 or 16)
+    static_assert(EPR == 8 || EPR == 16, "epilogue chunk rows");
+    const int ntiles = tiles_m * tiles_n;
+    const int nb = gridDim.x, bid = blockIdx.x;
+    const int q = nb / 8, r = nb % 8, xcd = bid % 8;
+    const int slot = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
+    const int my_tiles = slot < ntiles ? (ntiles - 1 - slot) / nb + 1 : 0;
+    const int nk = K / BK;
+    const int total = my_tiles * nk;
+    const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wid / C::WGN, wn = wid % C::WGN;
+    const int fr = lane & 31, fh = lane >> 5;
+    const int sub = lane / C::CPR, sl = lane % C::CPR;
+    int arow[PA], wrow[PW], acol[PA], wcol[PW];
+#pragma unroll
+    for (int j = 0; j < PA; ++j) {
+        arow[j] = C::RPP * (PA * wid + j) + sub;
+        acol[j] = (sl ^ C::swz(arow[j])) * 8;
+    }
+#pragma unroll
+    for (int j = 0; j < PW; ++j) {
+        wrow[j] = C::RPP * (PW * wid + j) + sub;
+        wcol[j] = (sl ^ C::swz(wrow[j])) * 8;
+    }
+    auto stage = [&](int g, int s) {
+        const int ti = g / nk, kt = g - ti * nk;
+        const int t = slot + ti * nb;
+        const int tm = t / tiles_n, tn = t - tm * tiles_n;
+        const int k0 = kt * BK;
+        unsigned char* base = smem + s * C::STAGE;
+#pragma unroll
+        for (int j = 0; j < PA; ++j)
+            __builtin_amdgcn_global_load_lds(
+                (gbl_void*)(A + amap.off(min(tm * C::BM + arow[j], M - 1)) + acol[j] + k0),
+                (lds_void*)(base + (PA * wid + j) * 1024), 16, 0, 0);
+#pragma unroll
+        for (int j = 0; j < PW; ++j)
+            __builtin_amdgcn_global_load_lds(
+                (gbl_void*)(W + (long long)min(tn * C::BN + wrow[j], N - 1) * ldw + wcol[j] + k0),
+                (lds_void*)(base + C::TA + (PW * wid + j) * 1024), 16, 0, 0);
+    };
+    int aoff[MI], asw[MI], woff[NI], wsw[NI];
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+        const int row = wm * C::WTM + i * 32 + fr;
+        aoff[i] = row * ROWB;
+        asw[i] = C::swz(row);
+    }
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+        const int row = wn * C::WTN + j * 32 + fr;
+        woff[j] = C::TA + row * ROWB;
+        wsw[j] = C::swz(row);
+    }
+    f32x16 acc[MI][NI];
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+    float* ep = (float*)(smem + NS * C::STAGE + wid * EPH);
+    const bool f32o = epi.out_dtype == DT_F32;
+#pragma unroll
+    for (int s = 0; s < NS - 1; ++s)
+        if (s < total) stage(s, s);
+    for (int g = 0; g < total; ++g) {
+        wait_vm<PA + PW>(min(NS - 2, total - 1 - g));
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        if (g + NS - 1 < total) stage(g + NS - 1, (g + NS - 1) % NS);
+        const unsigned char* sb = smem + (g % NS) * C::STAGE;
+#pragma unroll
+        for (int kq = 0; kq < BK / 16; ++kq) {
+            const int c = 2 * kq + fh;
+            bf16x8 af[MI], bfr[NI];
+#pragma unroll
+            for (int i = 0; i < MI; ++i) af[i] = *(const bf16x8*)(sb + aoff[i] + ((c ^ asw[i]) << 4));
+#pragma unroll
+            for (int j = 0; j < NI; ++j) bfr[j] = *(const bf16x8*)(sb + woff[j] + ((c ^ wsw[j]) << 4));
+#pragma unroll
+            for (int i = 0; i < MI; ++i)
+#pragma unroll
+                for (int j = 0; j < NI; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+        }
+        const int ti = g / nk;
+        if (g - ti * nk != nk - 1) continue;
+        // ---- epilogue of tile t (wave-private LDS slice; no block barrier)
+        const int t = slot + ti * nb;
+        const int tm = t / tiles_n, tn = t - tm * tiles_n;
+        const int m0 = tm * C::BM, n0 = tn * C::BN;
+        const int c4 = lane & 15, col = n0 + wn * 64 + c4 * 4;
+        float4 bb = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (epi.bias && col < N) bb = *(const float4*)(epi.bias + col);
+#pragma unroll
+        for (int i = 0; i < MI; ++i) {
+#pragma unroll
+            for (int h = 0; h < 32 / EPR; ++h) {
+                constexpr int EC = EPR / 2;   // accumulator elements per chunk: rows 8(e>>2)+(e&3)+4fh
+#pragma unroll
+                for (int j = 0; j < NI; ++j)
+#pragma unroll
+                    for (int e = EC * h; e < EC * h + EC; ++e)
+                        ep[((e & 3) + 8 * ((e >> 2) - 2 * EC * h / 8) + 4 * fh) * EP + j * 32 + fr] = acc[i][j][e];
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+                for (int sidx = 0; sidx < EPR / 4; ++sidx) {
+                    const int rr = (lane >> 4) + 4 * sidx;
+                    const int row = m0 + wm * C::WTM + i * 32 + EPR * h + rr;
+                    if (row >= M || col >= N) continue;
+                    float4 v = *(const float4*)(ep + rr * EP + c4 * 4);
+                    v.x = v.x * epi.alpha + bb.x; v.y = v.y * epi.alpha + bb.y;
+                    v.z = v.z * epi.alpha + bb.z; v.w = v.w * epi.alpha + bb.w;
+                    if (epi.relu) { v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f); }
+                    if (epi.res0) {
+                        float4 r0;
+                        if (epi.res0_bf16) {
+                            const bf16x4 rb = *(const bf16x4*)((const bf16*)epi.res0 + (long long)row * epi.ld_res0 + col);
+                            r0 = make_float4(bf2f(rb[0]), bf2f(rb[1]), bf2f(rb[2]), bf2f(rb[3]));
+                        } else {
+                            r0 = *(const float4*)(epi.res0 + (long long)row * epi.ld_res0 + col);
+                        }
+                        v.x += r0.x; v.y += r0.y; v.z += r0.z; v.w += r0.w;
+                    }
+                    if (epi.res1) {
+                        const float4 r1 = *(const float4*)(epi.res1 + (long long)row * epi.ld_res1 + col);
+                        v.x += r1.x; v.y += r1.y; v.z += r1.z; v.w += r1.w;
+                    }
+                    const long long ob = epi.out_map.off(row) + col;
+                    if (f32o) *(float4*)((float*)epi.out + ob) = v;
+                    else {
+                        bf16x4 tt = {f2bf(v.x), f2bf(v.y), f2bf(v.z), f2bf(v.w)};
+                        *(bf16x4*)((bf16*)epi.out + ob) = tt;
+                    }
+                    if (epi.out2) {
+                        bf16x4 tt = {f2bf(v.x), f2bf(v.y), f2bf(v.z), f2bf(v.w)};
+                        *(bf16x4*)((bf16*)epi.out2 + epi.out2_map.off(row) + col) = tt;
+                    }
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            }
+        }
+        // retire the bias load on every path (all rows of a tail tile may be skipped): a load left
+        // pending across the back-edge makes the compiler drain the whole DMA ring (vmcnt(0)) before
+        // those registers are reused in the next k-step
+        asm volatile("" ::"v"(bb.x), "v"(bb.y), "v"(bb.z), "v"(bb.w));
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+            for (int j = 0; j < NI; ++j)
+#pragma unroll
+                for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+    }
+}
+
 // tile configurations (PFM_GEMM_CFG selects one per launch for A/B runs; 0 = automatic)
 using C1 = Cfg<256, 256, 2, 4, 64, 2>;   // 128 KiB LDS, 8 waves, wave 128x64, 1 block/CU
 using C2 = Cfg<256, 128, 4, 2, 32, 3>;   // 72 KiB, 8 waves, wave 64x64, 2 blocks/CU
 using C3 = Cfg<128, 128, 2, 2, 64, 2>;   // 64 KiB, 4 waves, wave 64x64, 2 blocks/CU
 using C4 = Cfg<128, 256, 2, 4, 32, 3>;   // 72 KiB, 8 waves, wave 64x64, 2 blocks/CU
 using C5 = Cfg<256, 256, 2, 4, 32, 4>;   // 128 KiB, BK 32 x 4 stages
+using C6 = Cfg<256, 256, 2, 4, 32, 4, true>;   // 128 KiB, BK 32 x 4 stages, ping-pong wave groups
+using C7 = Cfg<256, 256, 2, 4, 32, 3>;   // persistent: 96 KiB ring + 34 KiB epilogue slices (16-row chunks)
+using C8 = Cfg<256, 256, 2, 4, 32, 4>;   // persistent: 128 KiB ring + 17 KiB slices (8-row chunks)
+using C9 = Cfg<256, 256, 2, 4, 64, 2>;   // persistent: 2 x 64 KiB ring + 17 KiB slices
+using C10 = Cfg<256, 128, 2, 2, 32, 3>;  // 4 waves (wave 128x64), 72 KiB: 2 blocks/CU -> epilogue/main-loop overlap
+using C11 = Cfg<256, 128, 2, 2, 32, 2>;  // 4 waves, 48 KiB
+using C12 = Cfg<256, 128, 2, 2, 64, 2>;  // 4 waves, 96 KiB (1 block/CU; control)
 
 template <class C>
 hipError_t launch(const void* A, RowMap amap, const void* W, long long ldw, int M, int N, int K, const GemmEpi& e2,
@@ -269,13 +512,228 @@ hipError_t launch(const void* A, RowMap amap, const void* W, long long ldw, int 
     return hipSuccess;
 }
 
+int num_cus() {
+    static int n = 0;
+    if (!n) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    }
+    return n;
+}
+
+template <class C, int EPR>
+hipError_t launch_persist(const void* A, RowMap amap, const void* W, long long ldw, int M, int N, int K,
+                          const GemmEpi& e2, hipStream_t st) {
+    constexpr int LDS = C::NS * C::STAGE + C::NW * EPR * C::EP * 4;
+    static_assert(LDS <= 160 * 1024, "persistent GEMM LDS budget");
+    static bool attr_done = false;
+    if (!attr_done) {
+        attr_done = true;
+        (void)hipFuncSetAttribute((const void*)(gemm_bf16_persist_kernel<C, EPR>), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  LDS);
+    }
+    const int tiles_m = (M + C::BM - 1) / C::BM, tiles_n = (N + C::BN - 1) / C::BN;
+    const int grid = std::min(tiles_m * tiles_n, num_cus());
+    hipLaunchKernelGGL((gemm_bf16_persist_kernel<C, EPR>), dim3(grid), dim3(C::NT), LDS, st, (const bf16*)A, amap,
+                       (const bf16*)W, ldw, M, N, K, tiles_m, tiles_n, e2);
+    PFM_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
 int pick_cfg(int M, int N) {
     const char* e = getenv("PFM_GEMM_CFG");   // read per launch: lets one process A/B configurations
     const int f = e ? atoi(e) : 0;
-    if (f >= 1 && f <= 5) return f;
+    if (f >= 1 && f <= 12) return f;
     // 256x256 when the grid has >= 2 tiles per CU, else 128x256 (64x64 wave tiles, 2 blocks / CU)
     const long long big = (long long)((M + 255) / 256) * ((N + 255) / 256);
     return big >= 512 ? 1 : 4;
+}
+
+// ------------------------------------------------------------------------------------------
+// Full-row GEMM + LayerNorm epilogue (N == 512 == d_model): one block owns 128 whole rows.
+//   x = act(A.W^T + bias) (+ res0) (+ res1)          -> out (f32, optional)
+//   y = LayerNorm(x) * gamma + beta                  -> ln_out (f32/bf16), ln_out2 (bf16, optional)
+// Fuses the LN that follows every 512-wide projection on the path (encoder out-proj -> norm2,
+// FFN w2 -> next norm1 / after_norm, decoder w2 -> norm2, decoder out-proj -> next norm1),
+// removing one full HBM read+write pass of the residual stream per fused LN.
+// 8 waves as 2 x 4 (wave tile 64 x 128 = 2x4 MFMA 32x32x16 blocks: 6 LDS fragment reads per 8 MFMAs,
+// the same ratio as the 256x256 kernel), BK 32, 3-stage LDS-DMA ring (A 8 KiB + W 32 KiB per stage,
+// 5 x 1-KiB pieces per wave). Epilogue: two halves of 64 rows; the half's waves stage their f32
+// accumulators in LDS, then every wave normalises 8 whole rows (lane = 8 columns, float4 I/O).
+constexpr int LN_BM = 128, LN_N = 512, LN_BK = 32, LN_NS = 3;
+constexpr int LN_ROWB = LN_BK * 2;                          // 64 B
+constexpr int LN_TA = LN_BM * LN_ROWB, LN_TW = LN_N * LN_ROWB, LN_STAGE = LN_TA + LN_TW;   // 8K + 32K
+constexpr int LN_CP = LN_N + 8;                             // staged C row pitch (floats): rows r, r+4 on disjoint banks
+constexpr int LN_HALF = 64;
+constexpr int LN_LDS = (LN_NS * LN_STAGE > LN_HALF * LN_CP * 4) ? LN_NS * LN_STAGE : LN_HALF * LN_CP * 4;
+
+struct LnEpi {
+    const float* gamma; const float* beta; float eps;
+    void* out; RowMap map; int dtype;            // LN output (f32 or bf16)
+    void* out2; RowMap map2;                     // optional bf16 copy
+};
+
+__device__ __forceinline__ int ln_swz(int row) { return (row >> 2) & 3; }   // 64-B rows
+
+__global__ __launch_bounds__(512) void gemm_bf16_ln_kernel(const bf16* __restrict__ A, RowMap amap,
+                                                           const bf16* __restrict__ W, long long ldw, int M, int K,
+                                                           GemmEpi epi, LnEpi ln) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int m0 = blockIdx.x * LN_BM;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int wm = wid >> 2, wn = wid & 3;
+    const int fr = lane & 31, fh = lane >> 5;
+    const int sub = lane >> 2, slot = lane & 3;     // 16 rows x 4 chunks per 1-KiB piece
+    const int arow = 16 * wid + sub;
+    const bf16* ga = A + amap.off(min(m0 + arow, M - 1)) + (slot ^ ln_swz(arow)) * 8;
+    const bf16* gw[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int row = 16 * (4 * wid + j) + sub;
+        gw[j] = W + (long long)row * ldw + (slot ^ ln_swz(row)) * 8;
+    }
+    auto stage = [&](int k0, int s) {
+        unsigned char* base = smem + s * LN_STAGE;
+        __builtin_amdgcn_global_load_lds((gbl_void*)(ga + k0), (lds_void*)(base + wid * 1024), 16, 0, 0);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            __builtin_amdgcn_global_load_lds((gbl_void*)(gw[j] + k0),
+                                             (lds_void*)(base + LN_TA + (4 * wid + j) * 1024), 16, 0, 0);
+    };
+    f32x16 acc[2][4];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+    int aoff[2], asw[2], woff[4], wsw[4];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int ar = wm * 64 + i * 32 + fr;
+        aoff[i] = ar * LN_ROWB; asw[i] = ln_swz(ar);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int wr = wn * 128 + j * 32 + fr;
+        woff[j] = LN_TA + wr * LN_ROWB; wsw[j] = ln_swz(wr);
+    }
+    const int nk = K / LN_BK;
+#pragma unroll
+    for (int s = 0; s < LN_NS - 1; ++s)
+        if (s < nk) stage(s * LN_BK, s);
+    for (int kt = 0; kt < nk; ++kt) {
+        if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");   // NS=3: one stage (5 loads) in flight
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        if (kt + LN_NS - 1 < nk) stage((kt + LN_NS - 1) * LN_BK, (kt + LN_NS - 1) % LN_NS);
+        const unsigned char* sb = smem + (kt % LN_NS) * LN_STAGE;
+#pragma unroll
+        for (int kq = 0; kq < LN_BK / 16; ++kq) {
+            const int c = 2 * kq + fh;
+            bf16x8 af[2], bfr[4];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) af[i] = *(const bf16x8*)(sb + aoff[i] + ((c ^ asw[i]) << 4));
+#pragma unroll
+            for (int j = 0; j < 4; ++j) bfr[j] = *(const bf16x8*)(sb + woff[j] + ((c ^ wsw[j]) << 4));
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __syncthreads();
+    // (1) in the accumulator layout: x = act(alpha*acc + bias) (+ res0) (+ res1). The residual reads of a
+    // wave are independent scalar loads (32 lanes = 128 contiguous bytes), so they all overlap.
+    {
+        float bj[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bj[j] = epi.bias ? epi.bias[wn * 128 + j * 32 + fr] : 0.f;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                const long long row = min(m0 + wm * 64 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * fh, M - 1);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int col = wn * 128 + j * 32 + fr;
+                    float v = acc[i][j][e] * epi.alpha + bj[j];
+                    if (epi.relu) v = fmaxf(v, 0.f);
+                    if (epi.res0)
+                        v += epi.res0_bf16 ? bf2f(((const bf16*)epi.res0)[row * epi.ld_res0 + col])
+                                           : epi.res0[row * epi.ld_res0 + col];
+                    if (epi.res1) v += epi.res1[row * epi.ld_res1 + col];
+                    acc[i][j][e] = v;
+                }
+            }
+    }
+    float4 gam[2], bet[2];
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf) {
+        const int col = hf * 256 + lane * 4;
+        gam[hf] = *(const float4*)(ln.gamma + col);
+        bet[hf] = *(const float4*)(ln.beta + col);
+    }
+    // (2) per 64-row half: stage x in LDS, then each wave normalises 8 whole rows (no global reads)
+    float* ct = (float*)smem;
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+        if (half) __syncthreads();   // previous half fully consumed
+        if (wm == half) {
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+#pragma unroll
+                    for (int e = 0; e < 16; ++e)
+                        ct[(i * 32 + (e & 3) + 8 * (e >> 2) + 4 * fh) * LN_CP + wn * 128 + j * 32 + fr] = acc[i][j][e];
+        }
+        __syncthreads();
+        for (int rr = 0; rr < 8; ++rr) {
+            const int lr = wid * 8 + rr, row = m0 + half * LN_HALF + lr;
+            if (row >= M) break;
+            float4 x[2];
+#pragma unroll
+            for (int hf = 0; hf < 2; ++hf) {
+                const int col = hf * 256 + lane * 4;
+                x[hf] = *(const float4*)(ct + lr * LN_CP + col);
+                if (epi.out) *(float4*)((float*)epi.out + epi.out_map.off(row) + col) = x[hf];
+            }
+            float sm = x[0].x + x[0].y + x[0].z + x[0].w + x[1].x + x[1].y + x[1].z + x[1].w;
+            const float mean = wave_sum(sm) * (1.f / LN_N);
+            float q = 0.f;
+#pragma unroll
+            for (int hf = 0; hf < 2; ++hf) {
+                const float a0 = x[hf].x - mean, a1 = x[hf].y - mean, a2 = x[hf].z - mean, a3 = x[hf].w - mean;
+                q += a0 * a0 + a1 * a1 + a2 * a2 + a3 * a3;
+            }
+            const float rstd = rsqrtf(wave_sum(q) * (1.f / LN_N) + ln.eps);
+#pragma unroll
+            for (int hf = 0; hf < 2; ++hf) {
+                const int col = hf * 256 + lane * 4;
+                float4 y;
+                y.x = (x[hf].x - mean) * rstd * gam[hf].x + bet[hf].x;
+                y.y = (x[hf].y - mean) * rstd * gam[hf].y + bet[hf].y;
+                y.z = (x[hf].z - mean) * rstd * gam[hf].z + bet[hf].z;
+                y.w = (x[hf].w - mean) * rstd * gam[hf].w + bet[hf].w;
+                const long long o1 = ln.map.off(row) + col;
+                if (ln.dtype == DT_F32) *(float4*)((float*)ln.out + o1) = y;
+                else {
+                    bf16x4 t = {f2bf(y.x), f2bf(y.y), f2bf(y.z), f2bf(y.w)};
+                    *(bf16x4*)((bf16*)ln.out + o1) = t;
+                }
+                if (ln.out2) {
+                    bf16x4 t = {f2bf(y.x), f2bf(y.y), f2bf(y.z), f2bf(y.w)};
+                    *(bf16x4*)((bf16*)ln.out2 + ln.map2.off(row) + col) = t;
+                }
+            }
+        }
+    }
 }
 
 }  // namespace
@@ -298,6 +756,40 @@ hipError_t pfm_gemm_bf16_256(const void* A, RowMap amap, const void* W, long lon
         case 3: return launch<C3>(A, amap, W, ldw, M, N, K, e2, st);
         case 4: return launch<C4>(A, amap, W, ldw, M, N, K, e2, st);
         case 5: return launch<C5>(A, amap, W, ldw, M, N, K, e2, st);
+        case 6: return launch<C6>(A, amap, W, ldw, M, N, K, e2, st);
+        case 7: if (!e2.amax_val && e2.vec_ok) return launch_persist<C7, 16>(A, amap, W, ldw, M, N, K, e2, st);
+                return launch<C1>(A, amap, W, ldw, M, N, K, e2, st);
+        case 8: if (!e2.amax_val && e2.vec_ok) return launch_persist<C8, 8>(A, amap, W, ldw, M, N, K, e2, st);
+                return launch<C1>(A, amap, W, ldw, M, N, K, e2, st);
+        case 9: if (!e2.amax_val && e2.vec_ok) return launch_persist<C9, 8>(A, amap, W, ldw, M, N, K, e2, st);
+                return launch<C1>(A, amap, W, ldw, M, N, K, e2, st);
+        case 10: return launch<C10>(A, amap, W, ldw, M, N, K, e2, st);
+        case 11: return launch<C11>(A, amap, W, ldw, M, N, K, e2, st);
+        case 12: return launch<C12>(A, amap, W, ldw, M, N, K, e2, st);
         default: return launch<C1>(A, amap, W, ldw, M, N, K, e2, st);
     }
+}
+
+// Full-row projection + LayerNorm (fast mode). N is fixed to 512; K % 32 == 0; 16-B aligned rows.
+hipError_t pfm_gemm_bf16_ln(const void* A, RowMap amap, const void* W, long long ldw, int M, int N, int K,
+                            const GemmEpi& epi, const float* gamma, const float* beta, float eps, void* ln_out,
+                            RowMap ln_map, int ln_dtype, void* ln_out2, RowMap ln_map2, hipStream_t st) {
+    if (M <= 0) return hipSuccess;
+    if (N != LN_N || K % LN_BK || ldw % 8 || amap.ld % 8 || (amap.rows_per_seg > 0 && amap.seg_stride % 8))
+        return hipErrorInvalidValue;
+    if ((epi.res0 && epi.ld_res0 % 4) || (epi.res1 && epi.ld_res1 % 4) || (epi.out && !rowmap_vec4(epi.out_map)) ||
+        !rowmap_vec4(ln_map) || (ln_out2 && !rowmap_vec4(ln_map2)))
+        return hipErrorInvalidValue;
+    static bool attr_done = false;
+    if (!attr_done) {
+        attr_done = true;
+        (void)hipFuncSetAttribute((const void*)gemm_bf16_ln_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, LN_LDS);
+    }
+    LnEpi ln;
+    ln.gamma = gamma; ln.beta = beta; ln.eps = eps; ln.out = ln_out; ln.map = ln_map; ln.dtype = ln_dtype;
+    ln.out2 = ln_out2; ln.map2 = ln_map2;
+    hipLaunchKernelGGL(gemm_bf16_ln_kernel, dim3((M + LN_BM - 1) / LN_BM), dim3(512), LN_LDS, st, (const bf16*)A, amap,
+                       (const bf16*)W, ldw, M, K, epi, ln);
+    PFM_LAUNCH_CHECK();
+    return hipSuccess;
 }

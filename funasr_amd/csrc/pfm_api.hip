@@ -22,6 +22,9 @@ bool pfm_gemm_bf16_256_ok(RowMap amap, long long ldw, int K);
 int pfm_gemm_bf16_256_amax_tiles(int N);
 hipError_t pfm_gemm_bf16_256(const void* A, RowMap amap, const void* W, long long ldw, int M, int N, int K,
                              const GemmEpi& epi, hipStream_t st);
+hipError_t pfm_gemm_bf16_ln(const void* A, RowMap amap, const void* W, long long ldw, int M, int N, int K,
+                            const GemmEpi& epi, const float* gamma, const float* beta, float eps, void* ln_out,
+                            RowMap ln_map, int ln_dtype, void* ln_out2, RowMap ln_map2, hipStream_t st);
 hipError_t pfm_attention(int dtype, const void* q, RowMap qmap, const void* k, RowMap kmap, const void* v,
                          RowMap vmap, float* o, long long ldo, void* o2, const int* klen, int B, int Tq, int Tk,
                          int heads, int dk, float scale, hipStream_t st);
@@ -372,6 +375,11 @@ hipError_t gemm_dispatch(int dtype, const void* A, RowMap amap, const void* W, l
     return pfm_gemm(dtype, A, amap, W, ldw, M, N, K, e, st);
 }
 
+bool gemm_ln_enabled() {   // PFM_GEMM_LN=1 enables the full-row GEMM+LayerNorm fusion (measured slower
+    const char* e = getenv("PFM_GEMM_LN");   // than GEMM + standalone LN on MI355X; kept for A/B runs)
+    return e && e[0] == '1';
+}
+
 int amax_tiles(int dtype, RowMap amap, long long ldw, int N, int K) {
     return use_big_bf16(dtype, amap, ldw, K) ? pfm_gemm_bf16_256_amax_tiles(N) : pfm_gemm_amax_tiles(N);
 }
@@ -526,8 +534,18 @@ int pfm_run(pfm_handle* h, void* stream, int mode, const float* feats, const int
         ProfScope ps(h, st, PFM_K_ATTN, fl, by);
         return pfm_attention(dtp, q, qm, k, km, v, vm, o, ldo, o2, kl, Bb, Tq, Tk, c.heads, (int)dk, qscale, st);
     };
-    auto OTHER = [&](double by) { return ProfScope(h, st, PFM_K_OTHER, 0.0, by); };
-    (void)OTHER;
+    // fast mode: 512-wide projections finish the residual sum AND the following LayerNorm in one
+    // kernel (k_gemm_bf16.hip gemm_bf16_ln_kernel); exact mode keeps the unfused reference order
+    const bool fuse_ln = fast && D == 512 && Fd % 32 == 0 && c.enc_blocks >= 1 && gemm_ln_enabled();
+    auto GEMM_LN = [&](const void* A, RowMap am, const void* Wt, long long ldw, int Mm, int Kk, const GemmEpi& e,
+                       size_t g, size_t b, void* lo, RowMap lm, int ldt, void* lo2, RowMap lm2) -> hipError_t {
+        const double fl = 2.0 * Mm * D * Kk;
+        const double by = ((double)Mm * Kk + (double)D * Kk) * 2.0 + (double)Mm * D * (e.out ? 4.0 : 0.0) +
+                          (e.res0 ? (e.res0_bf16 ? 2.0 : 4.0) * Mm * D : 0.0) + (e.res1 ? 4.0 * Mm * D : 0.0) +
+                          (double)Mm * D * (ldt == DT_F32 ? 4.0 : 2.0) + (lo2 ? 2.0 * Mm * D : 0.0);
+        ProfScope ps(h, st, PFM_K_GEMM, fl, by);
+        return pfm_gemm_bf16_ln(A, am, Wt, ldw, Mm, D, Kk, e, h->w(g), h->w(b), c.ln_eps, lo, lm, ldt, lo2, lm2, st);
+    };
     auto W = [&](size_t off) -> const void* { return fast ? (const void*)h->wb(off) : (const void*)h->w(off); };
     auto P = [&](size_t off) -> const float* { return h->w(off); };
     float* X = h->X.as<float>();
@@ -541,6 +559,19 @@ int pfm_run(pfm_handle* h, void* stream, int mode, const float* feats, const int
     void* Hh = h->H.p;
     const RowMap plain = rowmap_plain(0);
 
+    // after_norm -> zero-padded [B][T+2][D] (row 0 and T+1 of each utterance stay zero)
+    float* encp = h->encp.as<float>();
+    bf16* encpb = h->encpb.as<bf16>();
+    const RowMap encmap = rowmap_seg(T, (long long)(T + 2) * D, D);
+    // rows 0 and T+1 of every utterance are the conv / tail zero rows; the workspace may hold a
+    // previous call's layout (other T), so clear them each call (2*B rows, negligible)
+    HIP_TRY(hipMemset2DAsync(encp, (size_t)(T + 2) * D * 4, 0, (size_t)D * 4, B, st));
+    HIP_TRY(hipMemset2DAsync(encp + (size_t)(T + 1) * D, (size_t)(T + 2) * D * 4, 0, (size_t)D * 4, B, st));
+    if (fast) {
+        HIP_TRY(hipMemset2DAsync(encpb, (size_t)(T + 2) * D * 2, 0, (size_t)D * 2, B, st));
+        HIP_TRY(hipMemset2DAsync(encpb + (size_t)(T + 1) * D, (size_t)(T + 2) * D * 2, 0, (size_t)D * 2, B, st));
+    }
+
     // ---------------- encoder (sanm/encoder.py:361-430) ----------------
     for (int l = 0; l < c.enc_blocks; ++l) {
         const EncLayer& L = h->enc[l];
@@ -548,7 +579,7 @@ int pfm_run(pfm_handle* h, void* stream, int mode, const float* feats, const int
         if (l == 0)   // x = feats * sqrt(d_model) + PE ; LN1
             HIP_TRY(pfm_layernorm(feats, rowmap_plain(I), (int)M, I, P(L.ln1g), P(L.ln1b), c.ln_eps, h->pe.as<float>(),
                                   T, sqrtf((float)D), Xn, rowmap_plain(I), dt, nullptr, plain, 0, st));
-        else
+        else if (!fuse_ln)   // fused: the previous layer's w2 GEMM already wrote LN1(x) to Xn
             HIP_TRY(pfm_layernorm(X, rowmap_plain(D), (int)M, D, P(L.ln1g), P(L.ln1b), c.ln_eps, nullptr, 0, 1.f, Xn,
                                   rowmap_plain(D), dt, nullptr, plain, 0, st));
         {   // q|k|v = LN1(x) Wqkv^T + b   (fast mode: bf16 only — attention and FSMN read bf16)
@@ -578,10 +609,16 @@ int pfm_run(pfm_handle* h, void* stream, int mode, const float* feats, const int
             e.res0 = fast ? (const float*)Fb : Fm; e.ld_res0 = D; e.res0_bf16 = fast ? 1 : 0;
             if (din == D) { e.res1 = X; e.ld_res1 = D; }
             e.out = X; e.out_map = rowmap_plain(D); e.out_dtype = DT_F32;
-            HIP_TRY(GEMM(dt, fast ? (const void*)Ob : (const void*)O, rowmap_plain(D), W(L.wo), D, (int)M, D, D, e));
+            if (fuse_ln) {   // ... and Xn = LN2(x)
+                HIP_TRY(GEMM_LN(Ob, rowmap_plain(D), W(L.wo), D, (int)M, D, e, L.ln2g, L.ln2b, Xn, rowmap_plain(D),
+                                DT_BF16, nullptr, plain));
+            } else {
+                HIP_TRY(GEMM(dt, fast ? (const void*)Ob : (const void*)O, rowmap_plain(D), W(L.wo), D, (int)M, D, D,
+                             e));
+                HIP_TRY(pfm_layernorm(X, rowmap_plain(D), (int)M, D, P(L.ln2g), P(L.ln2b), c.ln_eps, nullptr, 0, 1.f,
+                                      Xn, rowmap_plain(D), dt, nullptr, plain, 0, st));
+            }
         }
-        HIP_TRY(pfm_layernorm(X, rowmap_plain(D), (int)M, D, P(L.ln2g), P(L.ln2b), c.ln_eps, nullptr, 0, 1.f, Xn,
-                              rowmap_plain(D), dt, nullptr, plain, 0, st));
         {   // h = relu(LN2(x) W1^T + b1)
             GemmEpi e = epi_default();
             e.bias = P(L.b1); e.relu = 1;
@@ -593,23 +630,21 @@ int pfm_run(pfm_handle* h, void* stream, int mode, const float* feats, const int
             e.bias = P(L.b2);
             e.res0 = X; e.ld_res0 = D;
             e.out = X; e.out_map = rowmap_plain(D); e.out_dtype = DT_F32;
-            HIP_TRY(GEMM(dt, Hh, rowmap_plain(Fd), W(L.w2), Fd, (int)M, D, Fd, e));
+            if (!fuse_ln) {
+                HIP_TRY(GEMM(dt, Hh, rowmap_plain(Fd), W(L.w2), Fd, (int)M, D, Fd, e));
+            } else if (l + 1 < c.enc_blocks) {   // ... and Xn = LN1_{l+1}(x)
+                HIP_TRY(GEMM_LN(Hh, rowmap_plain(Fd), W(L.w2), Fd, (int)M, Fd, e, h->enc[l + 1].ln1g,
+                                h->enc[l + 1].ln1b, Xn, rowmap_plain(D), DT_BF16, nullptr, plain));
+            } else {   // last layer: x itself is dead; after_norm straight into the padded encp / encpb
+                e.out = nullptr;
+                HIP_TRY(GEMM_LN(Hh, rowmap_plain(Fd), W(L.w2), Fd, (int)M, Fd, e, h->an_g, h->an_b, encp + D, encmap,
+                                DT_F32, encpb + D, encmap));
+            }
         }
     }
-    // after_norm -> zero-padded [B][T+2][D] (row 0 and T+1 of each utterance stay zero)
-    float* encp = h->encp.as<float>();
-    bf16* encpb = h->encpb.as<bf16>();
-    const RowMap encmap = rowmap_seg(T, (long long)(T + 2) * D, D);
-    // rows 0 and T+1 of every utterance are the conv / tail zero rows; the workspace may hold a
-    // previous call's layout (other T), so clear them each call (2*B rows, negligible)
-    HIP_TRY(hipMemset2DAsync(encp, (size_t)(T + 2) * D * 4, 0, (size_t)D * 4, B, st));
-    HIP_TRY(hipMemset2DAsync(encp + (size_t)(T + 1) * D, (size_t)(T + 2) * D * 4, 0, (size_t)D * 4, B, st));
-    if (fast) {
-        HIP_TRY(hipMemset2DAsync(encpb, (size_t)(T + 2) * D * 2, 0, (size_t)D * 2, B, st));
-        HIP_TRY(hipMemset2DAsync(encpb + (size_t)(T + 1) * D, (size_t)(T + 2) * D * 2, 0, (size_t)D * 2, B, st));
-    }
-    HIP_TRY(pfm_layernorm(X, rowmap_plain(D), (int)M, D, P(h->an_g), P(h->an_b), c.ln_eps, nullptr, 0, 1.f,
-                          encp + D, encmap, DT_F32, fast ? (void*)(encpb + D) : nullptr, encmap, DT_BF16, st));
+    if (!fuse_ln)
+        HIP_TRY(pfm_layernorm(X, rowmap_plain(D), (int)M, D, P(h->an_g), P(h->an_b), c.ln_eps, nullptr, 0, 1.f,
+                              encp + D, encmap, DT_F32, fast ? (void*)(encpb + D) : nullptr, encmap, DT_BF16, st));
     if (enc_out)
         HIP_TRY(hipMemcpy2DAsync(enc_out, (size_t)T * D * 4, encp + D, (size_t)(T + 2) * D * 4, (size_t)T * D * 4, B,
                                  hipMemcpyDeviceToDevice, st));
@@ -663,11 +698,12 @@ int pfm_run(pfm_handle* h, void* stream, int mode, const float* feats, const int
         const void* A = fast ? (const void*)(encpb + D) : (const void*)(encp + D);
         HIP_TRY(GEMM(dt, A, encmap, W(h->wkv_all), D, (int)M, nkv, D, e));
     }
-    auto ffn = [&](const float* x, size_t lng, size_t lnb, size_t w1, size_t b1, size_t fng, size_t fnb, size_t w2,
-                   const float* res, float* out) -> int {
-        // out = (res +) W2 . LN_F(relu(W1 . LN(x) + b1))     (sanm/positionwise_feed_forward.py:26-33)
-        HIP_TRY(pfm_layernorm(x, rowmap_plain(D), (int)Ml, D, P(lng), P(lnb), c.ln_eps, nullptr, 0, 1.f, Xdn,
-                              rowmap_plain(D), dt, nullptr, plain, 0, st));
+    auto ffn = [&](const float* x, bool xdn_ready, size_t lng, size_t lnb, size_t w1, size_t b1, size_t fng,
+                   size_t fnb, size_t w2, float* out, size_t pg, size_t pb, void* pout, int pdt) -> int {
+        // out = W2 . LN_F(relu(W1 . LN(x) + b1)); pout = LN_P(out)   (sanm/positionwise_feed_forward.py:26-33)
+        if (!xdn_ready)
+            HIP_TRY(pfm_layernorm(x, rowmap_plain(D), (int)Ml, D, P(lng), P(lnb), c.ln_eps, nullptr, 0, 1.f, Xdn,
+                                  rowmap_plain(D), dt, nullptr, plain, 0, st));
         GemmEpi e = epi_default();
         e.bias = P(b1); e.relu = 1;
         e.out = Hd; e.out_map = rowmap_plain(Fd); e.out_dtype = DT_F32;
@@ -675,18 +711,23 @@ int pfm_run(pfm_handle* h, void* stream, int mode, const float* feats, const int
         HIP_TRY(pfm_layernorm(Hd, rowmap_plain(Fd), (int)Ml, Fd, P(fng), P(fnb), c.ln_eps, nullptr, 0, 1.f, Hdn,
                               rowmap_plain(Fd), dt, nullptr, plain, 0, st));
         GemmEpi e2 = epi_default();
-        if (res) { e2.res0 = res; e2.ld_res0 = D; }
-        e2.out = out; e2.out_map = rowmap_plain(D); e2.out_dtype = DT_F32;
-        HIP_TRY(GEMM(dt, Hdn, rowmap_plain(Fd), W(w2), Fd, (int)Ml, D, Fd, e2));
+        if (fuse_ln) {   // out itself is dead; only LN_P(out) is consumed
+            HIP_TRY(GEMM_LN(Hdn, rowmap_plain(Fd), W(w2), Fd, (int)Ml, Fd, e2, pg, pb, pout, rowmap_plain(D), pdt,
+                            nullptr, plain));
+        } else {
+            e2.out = out; e2.out_map = rowmap_plain(D); e2.out_dtype = DT_F32;
+            HIP_TRY(GEMM(dt, Hdn, rowmap_plain(Fd), W(w2), Fd, (int)Ml, D, Fd, e2));
+            HIP_TRY(pfm_layernorm(out, rowmap_plain(D), (int)Ml, D, P(pg), P(pb), c.ln_eps, nullptr, 0, 1.f, pout,
+                                  rowmap_plain(D), pdt, nullptr, plain, 0, st));
+        }
         return PFM_OK;
     };
+    bool xdn_ready = false;   // Xdn already holds LN1(x) of the next block (fused out-proj epilogue)
     for (int l = 0; l < c.dec_blocks; ++l) {
         const DecLayer& Lr = h->dec[l];
         // t = FFN(LN1(x)); x = x + FSMN(LN2(t))   (decoder.py:97-107)
-        rc = ffn(Xd, Lr.n1g, Lr.n1b, Lr.w1, Lr.b1, Lr.ng, Lr.nb, Lr.w2, nullptr, Td);
+        rc = ffn(Xd, xdn_ready, Lr.n1g, Lr.n1b, Lr.w1, Lr.b1, Lr.ng, Lr.nb, Lr.w2, Td, Lr.n2g, Lr.n2b, Tdn, DT_F32);
         if (rc) return rc;
-        HIP_TRY(pfm_layernorm(Td, rowmap_plain(D), (int)Ml, D, P(Lr.n2g), P(Lr.n2b), c.ln_eps, nullptr, 0, 1.f, Tdn,
-                              rowmap_plain(D), DT_F32, nullptr, plain, 0, st));
         HIP_TRY(pfm_fsmn(Tdn, rowmap_plain(D), ntok, B, L, D, P(Lr.fsmn), K, ldec, Xd, Xd, nullptr, st));
         // x = x + CrossAtt(LN3(x), memory)   (decoder.py:109-119)
         HIP_TRY(pfm_layernorm(Xd, rowmap_plain(D), (int)Ml, D, P(Lr.n3g), P(Lr.n3b), c.ln_eps, nullptr, 0, 1.f, Xdn,
@@ -708,15 +749,22 @@ int pfm_run(pfm_handle* h, void* stream, int mode, const float* feats, const int
             e.bias = P(Lr.bo);
             e.res0 = Xd; e.ld_res0 = D;
             e.out = Xd; e.out_map = rowmap_plain(D); e.out_dtype = DT_F32;
-            HIP_TRY(GEMM(dt, fast ? (const void*)Odb : (const void*)Od, rowmap_plain(D), W(Lr.wo), D, (int)Ml, D, D,
-                             e));
+            if (fuse_ln) {   // ... and Xdn = LN1 of the next block (decoders[l+1] or decoders3)
+                const size_t ng = l + 1 < c.dec_blocks ? h->dec[l + 1].n1g : h->d3n1g;
+                const size_t nb = l + 1 < c.dec_blocks ? h->dec[l + 1].n1b : h->d3n1b;
+                HIP_TRY(GEMM_LN(Odb, rowmap_plain(D), W(Lr.wo), D, (int)Ml, D, e, ng, nb, Xdn, rowmap_plain(D), dt,
+                                nullptr, plain));
+                xdn_ready = true;
+            } else {
+                HIP_TRY(GEMM(dt, fast ? (const void*)Odb : (const void*)Od, rowmap_plain(D), W(Lr.wo), D, (int)Ml, D,
+                             D, e));
+            }
         }
     }
     // decoders3: x = FFN(LN1(x)), no residual (decoder.py:97-100 with self_attn = src_attn = None)
-    rc = ffn(Xd, h->d3n1g, h->d3n1b, h->d3w1, h->d3b1, h->d3ng, h->d3nb, h->d3w2, nullptr, Xd);
+    rc = ffn(Xd, xdn_ready, h->d3n1g, h->d3n1b, h->d3w1, h->d3b1, h->d3ng, h->d3nb, h->d3w2, Xd, h->dan_g, h->dan_b,
+             Xdn, dt);
     if (rc) return rc;
-    HIP_TRY(pfm_layernorm(Xd, rowmap_plain(D), (int)Ml, D, P(h->dan_g), P(h->dan_b), c.ln_eps, nullptr, 0, 1.f, Xdn,
-                          rowmap_plain(D), dt, nullptr, plain, 0, st));
     {   // output layer with fused row-argmax (logits never written)
         const int ntl = amax_tiles(dt, rowmap_plain(D), D, c.vocab_size, D);
         GemmEpi e = epi_default();
@@ -783,6 +831,19 @@ int pfm_op_gemm(void* stream, int dtype, const void* A, const void* Wt, const fl
     if (res) { e.res0 = res; e.ld_res0 = N; }
     e.out = C; e.out_map = rowmap_plain(N); e.out_dtype = DT_F32;
     HIP_TRY(gemm_dispatch(dtype, A, rowmap_plain(K), Wt, K, M, N, K, e, (hipStream_t)stream));
+    return PFM_OK;
+}
+
+int pfm_op_gemm_layernorm(void* stream, const void* A, const void* Wt, const float* bias, const float* res, float* C,
+                          const float* gamma, const float* beta, float eps, float* Y, int M, int N, int K) {
+    if (!A || !Wt || !gamma || !beta || !Y || M < 0) return fail(PFM_E_ARG, "pfm_op_gemm_layernorm: null argument");
+    if (N != 512 || K % 32) return fail(PFM_E_ARG, "pfm_op_gemm_layernorm: needs N == 512 and K % 32 == 0");
+    GemmEpi e = epi_default();
+    e.bias = bias;
+    if (res) { e.res0 = res; e.ld_res0 = N; }
+    if (C) { e.out = C; e.out_map = rowmap_plain(N); e.out_dtype = DT_F32; }
+    HIP_TRY(pfm_gemm_bf16_ln(A, rowmap_plain(K), Wt, K, M, N, K, e, gamma, beta, eps, Y, rowmap_plain(N), DT_F32,
+                             nullptr, rowmap_plain(0), (hipStream_t)stream));
     return PFM_OK;
 }
 

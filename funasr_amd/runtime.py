@@ -24,7 +24,7 @@ MODES = {"exact": MODE_EXACT, "fp32": MODE_EXACT, "fast": MODE_FAST, "bf16": MOD
 # every symbol include/pfm.h declares (checked by tests/test_abi.py)
 ABI_SYMBOLS = ("pfm_config_default", "pfm_create", "pfm_set_weight", "pfm_missing_weights", "pfm_reserve",
                "pfm_run", "pfm_fbank", "pfm_lfr_frames", "pfm_last_error", "pfm_destroy", "pfm_op_gemm",
-               "pfm_op_attention", "pfm_op_layernorm", "pfm_op_fsmn", "pfm_op_cif", "pfm_profile",
+               "pfm_op_attention", "pfm_op_layernorm", "pfm_op_fsmn", "pfm_op_cif", "pfm_profile", "pfm_op_gemm_layernorm",
                "pfm_profile_read")
 
 
@@ -80,6 +80,8 @@ def load_library(path: Optional[str] = None) -> ctypes.CDLL:
     lib.pfm_op_layernorm.argtypes = [vp, f32p, f32p, f32p, f32p, i32, i32, ctypes.c_float]
     lib.pfm_op_fsmn.argtypes = [vp, f32p, i32p, f32p, f32p, f32p, i32, i32, i32, i32, i32]
     lib.pfm_op_cif.argtypes = [vp, f32p, f32p, f32p, f32p, i32p, i32p, i32, i32, i32, i32]
+    lib.pfm_op_gemm_layernorm.argtypes = [vp, vp, vp, f32p, f32p, f32p, f32p, f32p, ctypes.c_float, f32p, i32, i32,
+                                          i32]
     for name in ABI_SYMBOLS:
         getattr(lib, name)
     if path is None:
@@ -214,6 +216,20 @@ def op_gemm(A, W, bias=None, res=None, relu=False):
     check(lib.pfm_op_gemm(_stream_ptr(torch, A.device), dt, _ptr(A.contiguous()), _ptr(W.contiguous()), _ptr(bias),
                           _ptr(res), _ptr(C), M, N, K, 1 if relu else 0), "pfm_op_gemm")
     return C
+
+
+def op_gemm_layernorm(A, W, gamma, beta, eps, bias=None, res=None, want_x=False):
+    """bf16 A [M,K] . W [512,K]^T (+bias +res) -> LayerNorm; returns Y (and x when want_x)."""
+    import torch
+    lib = load_library()
+    M, K = A.shape
+    N = W.shape[0]
+    Y = torch.empty((M, N), dtype=torch.float32, device=A.device)
+    C = torch.empty((M, N), dtype=torch.float32, device=A.device) if want_x else None
+    check(lib.pfm_op_gemm_layernorm(_stream_ptr(torch, A.device), _ptr(A.contiguous()), _ptr(W.contiguous()),
+                                    _ptr(bias), _ptr(res), _ptr(C), _ptr(gamma), _ptr(beta), ctypes.c_float(eps),
+                                    _ptr(Y), M, N, K), "pfm_op_gemm_layernorm")
+    return (Y, C) if want_x else Y
 
 
 def op_attention(q, k, v, klen, B, Tq, Tk, heads, scale):

@@ -41,9 +41,13 @@ def test_gemm_f32(dev, M, N, K):
     assert err < 1e-4
 
 
+@pytest.mark.parametrize("cfg", ["0", "1", "2", "3", "4", "5", "6", "7", "8", "9", "10", "11", "12"])
 @pytest.mark.parametrize("M,N,K", [(300, 1536, 560), (77, 8404, 512), (1000, 512, 2048), (513, 1024, 1536),
-                                   (256, 256, 64), (4000, 2048, 512)])
-def test_gemm_bf16(dev, M, N, K):
+                                   (256, 256, 64), (4000, 2048, 512), (2000, 768, 96), (600, 256, 32)])
+def test_gemm_bf16(dev, M, N, K, cfg, monkeypatch):
+    """Every bf16 tile configuration (PFM_GEMM_CFG, read per launch; 0 = automatic policy), including
+    K-tile counts below the pipeline depth (K = 32, 64, 96)."""
+    monkeypatch.setenv("PFM_GEMM_CFG", cfg)
     g = torch.Generator().manual_seed(M + N)
     A = torch.randn(M, K, generator=g).bfloat16()
     W = (torch.randn(N, K, generator=g) / K ** 0.5).bfloat16()
@@ -60,6 +64,41 @@ def test_gemm_identity_asymmetric(dev):
     W = torch.arange(K * 160, dtype=torch.float32).reshape(160, K) % 97
     got = rt.op_gemm(A.to(dev), W.to(dev)).cpu()
     assert torch.equal(got, W.T.contiguous())
+
+
+@pytest.mark.parametrize("M,K,with_res", [(1, 512, True), (63, 512, False), (64, 2048, True), (65, 512, True),
+                                          (1000, 2048, True), (32000, 512, True)])
+def test_gemm_layernorm(dev, M, K, with_res):
+    """Fused 512-wide projection + LayerNorm (fast-mode epilogue) vs fp64 torch on the same bf16
+    operands: x within rel-L2 1e-5 (f32 accumulate), LN(x) within abs 2e-4 (f32 statistics)."""
+    N = 512
+    g = torch.Generator().manual_seed(M * 3 + K)
+    A = torch.randn(M, K, generator=g).bfloat16()
+    W = (torch.randn(N, K, generator=g) / K ** 0.5).bfloat16()
+    b = torch.randn(N, generator=g)
+    R = torch.randn(M, N, generator=g) * 3 if with_res else None
+    gam = 1 + 0.1 * torch.randn(N, generator=g)
+    bet = 0.1 * torch.randn(N, generator=g)
+    x = A.double() @ W.double().T + b.double() + (R.double() if with_res else 0)
+    mu = x.mean(-1, keepdim=True)
+    var = ((x - mu) ** 2).mean(-1, keepdim=True)
+    want = (x - mu) / torch.sqrt(var + 1e-12) * gam.double() + bet.double()
+    Y, C = rt.op_gemm_layernorm(A.to(dev), W.to(dev), gam.to(dev), bet.to(dev), 1e-12, bias=b.to(dev),
+                                res=R.to(dev) if with_res else None, want_x=True)
+    torch.cuda.synchronize()
+    assert rel(C, x) < 1e-5
+    assert (Y.double().cpu() - want).abs().max().item() < 2e-4
+    Y2 = rt.op_gemm_layernorm(A.to(dev), W.to(dev), gam.to(dev), bet.to(dev), 1e-12, bias=b.to(dev),
+                              res=R.to(dev) if with_res else None)
+    assert torch.equal(Y, Y2)
+
+
+def test_gemm_layernorm_rejects_bad_shape(dev):
+    A = torch.zeros(4, 512, dtype=torch.bfloat16, device=dev)
+    W = torch.zeros(256, 512, dtype=torch.bfloat16, device=dev)
+    g = torch.ones(256, device=dev)
+    with pytest.raises(rt.PfmError):
+        rt.op_gemm_layernorm(A, W, g, g, 1e-12)
 
 
 @pytest.mark.parametrize("dt", ["f32", "bf16"])
