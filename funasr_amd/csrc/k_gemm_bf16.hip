@@ -13,6 +13,7 @@
 // stores), or scan rows for the fused row-argmax of the output layer.
 // Launcher contract: K % BK == 0, row strides % 8 == 0 (16-B aligned rows). Rows beyond M / N
 // are clamped to valid memory and dropped in the epilogue.
+#include <stdint.h>
 #include <stdlib.h>
 
 #include <algorithm>
@@ -92,6 +93,11 @@ __global__ __launch_bounds__(C::NT) void gemm_bf16_kernel(const bf16* __restrict
                                              (lds_void*)(base + C::TA + (PW * wid + j) * 1024), 16, 0, 0);
     };
 
+    // Residual GEMMs (alpha 1, no activation): the accumulators start from res0 + res1, read here in
+    // the accumulator layout (32 lanes = 128 contiguous bytes per row) ahead of the prologue DMA, so
+    // the epilogue carries no loads. vmcnt retires in order: an epilogue load issued after stores
+    // waits for them, which serialised one HBM round trip per 4 rows before.
+    const bool pre_res = (epi.res0 || epi.res1) && epi.alpha == 1.f && !epi.relu;
     f32x16 acc[MI][NI];
 #pragma unroll
     for (int i = 0; i < MI; ++i)
@@ -99,6 +105,24 @@ __global__ __launch_bounds__(C::NT) void gemm_bf16_kernel(const bf16* __restrict
         for (int j = 0; j < NI; ++j)
 #pragma unroll
             for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+    if (pre_res) {
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                const long long row = min(m0 + wm * C::WTM + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * fh, M - 1);
+#pragma unroll
+                for (int j = 0; j < NI; ++j) {
+                    const int col = min(n0 + wn * C::WTN + j * 32 + fr, N - 1);
+                    float v = 0.f;
+                    if (epi.res0)
+                        v = epi.res0_bf16 ? bf2f(((const bf16*)epi.res0)[row * epi.ld_res0 + col])
+                                          : epi.res0[row * epi.ld_res0 + col];
+                    if (epi.res1) v += epi.res1[row * epi.ld_res1 + col];
+                    acc[i][j][e] = v;
+                }
+            }
+    }
     int aoff[MI], asw[MI], woff[NI], wsw[NI];
 #pragma unroll
     for (int i = 0; i < MI; ++i) {
@@ -206,6 +230,18 @@ __global__ __launch_bounds__(C::NT) void gemm_bf16_kernel(const bf16* __restrict
         constexpr int EP = C::EP;
         float* ep = (float*)(smem + wid * C::EPW);
         const bool f32o = epi.out_dtype == DT_F32;
+        // a lane's output columns are the same for every row it writes: one bias load, before any store
+        const bool st16 = epi.st16_ok && (pre_res || !(epi.res0 || epi.res1));
+        const int colv = n0 + wn * 64 + (st16 ? (lane & 7) * 8 : (lane & 15) * 4);
+        float4 bb = make_float4(0.f, 0.f, 0.f, 0.f), bb2 = bb;
+        if (epi.out && epi.bias && colv < N) {
+            bb = *(const float4*)(epi.bias + colv);
+            if (st16) bb2 = *(const float4*)(epi.bias + colv + 4);
+        }
+        // consume it here, before any store: otherwise paths that skip rows leave it "pending" and the
+        // compiler re-waits vmcnt(0) (draining the stores issued since) at every use below
+        asm volatile("" ::"v"(bb.x), "v"(bb.y), "v"(bb.z), "v"(bb.w), "v"(bb2.x), "v"(bb2.y), "v"(bb2.z),
+                     "v"(bb2.w));
 #pragma unroll
         for (int i = 0; i < MI; ++i) {
 #pragma unroll
@@ -239,6 +275,27 @@ __global__ __launch_bounds__(C::NT) void gemm_bf16_kernel(const bf16* __restrict
                     epi.amax_idx[p] = bi;
                 }
             }
+            if (st16) {
+#pragma unroll
+                for (int sidx = 0; sidx < 4; ++sidx) {
+                    const int f = lane + 64 * sidx, rr = f >> 3, c8 = f & 7;
+                    const int row = m0 + wm * C::WTM + i * 32 + rr;
+                    const int col = n0 + wn * 64 + c8 * 8;
+                    if (row >= M || col >= N) continue;
+                    float4 v = *(const float4*)(ep + rr * EP + c8 * 8);
+                    float4 u = *(const float4*)(ep + rr * EP + c8 * 8 + 4);
+                    v.x = v.x * epi.alpha + bb.x; v.y = v.y * epi.alpha + bb.y;
+                    v.z = v.z * epi.alpha + bb.z; v.w = v.w * epi.alpha + bb.w;
+                    u.x = u.x * epi.alpha + bb2.x; u.y = u.y * epi.alpha + bb2.y;
+                    u.z = u.z * epi.alpha + bb2.z; u.w = u.w * epi.alpha + bb2.w;
+                    if (epi.relu) {
+                        v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
+                        u.x = fmaxf(u.x, 0.f); u.y = fmaxf(u.y, 0.f); u.z = fmaxf(u.z, 0.f); u.w = fmaxf(u.w, 0.f);
+                    }
+                    bf16x8 t = {f2bf(v.x), f2bf(v.y), f2bf(v.z), f2bf(v.w), f2bf(u.x), f2bf(u.y), f2bf(u.z), f2bf(u.w)};
+                    *(bf16x8*)((bf16*)epi.out + epi.out_map.off(row) + col) = t;
+                }
+            } else
 #pragma unroll
             for (int sidx = 0; sidx < 8; ++sidx) {
                 if (!epi.out) break;
@@ -247,13 +304,10 @@ __global__ __launch_bounds__(C::NT) void gemm_bf16_kernel(const bf16* __restrict
                 const int col = n0 + wn * 64 + c4 * 4;
                 if (row >= M || col >= N) continue;
                 float4 v = *(const float4*)(ep + rr * EP + c4 * 4);
-                v.x *= epi.alpha; v.y *= epi.alpha; v.z *= epi.alpha; v.w *= epi.alpha;
-                if (epi.bias) {
-                    const float4 bb = *(const float4*)(epi.bias + col);
-                    v.x += bb.x; v.y += bb.y; v.z += bb.z; v.w += bb.w;
-                }
+                v.x = v.x * epi.alpha + bb.x; v.y = v.y * epi.alpha + bb.y;
+                v.z = v.z * epi.alpha + bb.z; v.w = v.w * epi.alpha + bb.w;
                 if (epi.relu) { v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f); }
-                if (epi.res0) {
+                if (epi.res0 && !pre_res) {
                     float4 r0;
                     if (epi.res0_bf16) {
                         const bf16x4 rb = *(const bf16x4*)((const bf16*)epi.res0 + (long long)row * epi.ld_res0 + col);
@@ -263,7 +317,7 @@ __global__ __launch_bounds__(C::NT) void gemm_bf16_kernel(const bf16* __restrict
                     }
                     v.x += r0.x; v.y += r0.y; v.z += r0.z; v.w += r0.w;
                 }
-                if (epi.res1) {
+                if (epi.res1 && !pre_res) {
                     const float4 r1 = *(const float4*)(epi.res1 + (long long)row * epi.ld_res1 + col);
                     v.x += r1.x; v.y += r1.y; v.z += r1.z; v.w += r1.w;
                 }
@@ -299,9 +353,10 @@ __global__ __launch_bounds__(C::NT) void gemm_bf16_kernel(const bf16* __restrict
                 float v = acc[i][j][e] * epi.alpha;
                 if (epi.bias) v += epi.bias[col];
                 if (epi.relu) v = fmaxf(v, 0.f);
-                if (epi.res0) v += epi.res0_bf16 ? bf2f(((const bf16*)epi.res0)[(long long)row * epi.ld_res0 + col])
-                                                 : epi.res0[(long long)row * epi.ld_res0 + col];
-                if (epi.res1) v += epi.res1[(long long)row * epi.ld_res1 + col];
+                if (epi.res0 && !pre_res)
+                    v += epi.res0_bf16 ? bf2f(((const bf16*)epi.res0)[(long long)row * epi.ld_res0 + col])
+                                       : epi.res0[(long long)row * epi.ld_res0 + col];
+                if (epi.res1 && !pre_res) v += epi.res1[(long long)row * epi.ld_res1 + col];
                 if (epi.out_dtype == DT_F32) ((float*)epi.out)[ob + col] = v;
                 else ((bf16*)epi.out)[ob + col] = f2bf(v);
                 if (epi.out2) ((bf16*)epi.out2)[epi.out2_map.off(row) + col] = f2bf(v);
@@ -541,13 +596,15 @@ hipError_t launch_persist(const void* A, RowMap amap, const void* W, long long l
     return hipSuccess;
 }
 
-int pick_cfg(int M, int N) {
+int pick_cfg(int M, int N, int K) {
     const char* e = getenv("PFM_GEMM_CFG");   // read per launch: lets one process A/B configurations
     const int f = e ? atoi(e) : 0;
     if (f >= 1 && f <= 12) return f;
-    // 256x256 when the grid has >= 2 tiles per CU, else 128x256 (64x64 wave tiles, 2 blocks / CU)
+    // 256x256 (1 block/CU) when the grid has >= 2 tiles per CU, or when it fills one round and K is
+    // deep enough (>= 1536) to amortise the longer prologue; else 128x256 (64x64 wave tiles,
+    // 2 blocks / CU). Measured on the path shapes with tools/gemm_ab.py.
     const long long big = (long long)((M + 255) / 256) * ((N + 255) / 256);
-    return big >= 512 ? 1 : 4;
+    return (big >= 512 || (K >= 1536 && big >= 240)) ? 1 : 4;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -751,7 +808,14 @@ hipError_t pfm_gemm_bf16_256(const void* A, RowMap amap, const void* W, long lon
     if (!pfm_gemm_bf16_256_ok(amap, ldw, K)) return hipErrorInvalidValue;
     GemmEpi e2 = epi;
     e2.vec_ok = epi_vec_ok(epi, N);
-    switch (pick_cfg(M, N)) {
+    {
+        const char* ev = getenv("PFM_GEMM_ST16");   // read per launch (A/B runs); default on
+        const RowMap& om = epi.out_map;
+        e2.st16_ok = e2.vec_ok && epi.out && epi.out_dtype == DT_BF16 && !epi.out2 && !epi.amax_val && N % 8 == 0 &&
+                     om.ld % 8 == 0 && (om.rows_per_seg <= 0 || om.seg_stride % 8 == 0) &&
+                     ((uintptr_t)epi.out % 16) == 0 && !(ev && ev[0] == '0');
+    }
+    switch (pick_cfg(M, N, K)) {
         case 2: return launch<C2>(A, amap, W, ldw, M, N, K, e2, st);
         case 3: return launch<C3>(A, amap, W, ldw, M, N, K, e2, st);
         case 4: return launch<C4>(A, amap, W, ldw, M, N, K, e2, st);

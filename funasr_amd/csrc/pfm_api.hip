@@ -826,10 +826,11 @@ int pfm_profile_read(pfm_handle* h, int kc, double* ms, double* flops, double* b
 // ---------------- single-op entry points ----------------
 int pfm_op_gemm(void* stream, int dtype, const void* A, const void* Wt, const float* bias, const float* res, float* C,
                 int M, int N, int K, int act) {
+    if ((act & 2) && dtype != DT_BF16) return fail(PFM_E_ARG, "pfm_op_gemm: bf16 output needs bf16 operands");
     GemmEpi e = epi_default();
-    e.bias = bias; e.relu = act == 1;
+    e.bias = bias; e.relu = act & 1;
     if (res) { e.res0 = res; e.ld_res0 = N; }
-    e.out = C; e.out_map = rowmap_plain(N); e.out_dtype = DT_F32;
+    e.out = C; e.out_map = rowmap_plain(N); e.out_dtype = (act & 2) ? DT_BF16 : DT_F32;
     HIP_TRY(gemm_dispatch(dtype, A, rowmap_plain(K), Wt, K, M, N, K, e, (hipStream_t)stream));
     return PFM_OK;
 }

@@ -84,6 +84,9 @@ struct GemmEpi {
     // set by the launcher: N, residual strides and output row offsets are multiples of 4
     // (float4 / bf16x4 vector epilogue legal)
     int vec_ok;
+    // set by the bf16 launcher: bf16-only output with 16-B aligned rows -> 8 columns per lane,
+    // one 16-B store each (halves the store-issue tail of the big bf16 outputs)
+    int st16_ok;
 };
 
 static inline bool rowmap_vec4(const RowMap& m) {

@@ -140,8 +140,9 @@ int pfm_profile_read(pfm_handle* h, int kclass, double* ms, double* flops, doubl
 
 /* ---- single-op entry points (kernel-level parity tests; same kernels pfm_run uses) ---- */
 
-/* C[M,N] = act(A[M,K] . W[N,K]^T + bias) (+ res), dtype of A/W = PFM_F32 or PFM_BF16;
- * C is f32. act: 0 none, 1 relu. */
+/* C[M,N] = act(A[M,K] . W[N,K]^T + bias) (+ res), dtype of A/W = PFM_F32 or PFM_BF16.
+ * act bit 0: relu; act bit 1: C is bf16 (bf16 operands only; the fast-mode QKV / FFN1 output
+ * form), otherwise C is f32. */
 int pfm_op_gemm(void* stream, int dtype, const void* A, const void* W, const float* bias,
                 const float* res, float* C, int M, int N, int K, int act);
 
