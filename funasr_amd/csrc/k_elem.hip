@@ -1,5 +1,7 @@
 // HBM-bound kernels of the Paraformer path: LayerNorm (+ embedding prologue), FSMN memory
 // block, CIF predictor head + integrate-and-fire, and the row-argmax reduction.
+#include <stdint.h>
+
 #include "pfm_common.h"
 
 namespace {
@@ -11,6 +13,91 @@ namespace {
 // Optional prologue (encoder input, sanm/encoder.py:377-397):  x = in * in_scale + pe[t].
 // ------------------------------------------------------------------------------------------
 constexpr int LN_MAXV = 8;   // float4 per lane -> D <= 2048
+
+// Streaming form for D = 512 * VPL (the path's 512- and 2048-wide rows): lane owns 8 contiguous
+// columns per 512-column slab (two float4 loads, one 16-B store), R rows per wave with every row
+// load and gamma / beta issued before the first store (vmcnt retires in order, so a load behind a
+// store waits for it). Same f64 statistics as layernorm_kernel.
+template <int VPL, int R>
+__global__ __launch_bounds__(256) void layernorm_v8_kernel(const float* __restrict__ x, RowMap xmap, int M,
+                                                           const float* __restrict__ g, const float* __restrict__ bta,
+                                                           float eps, void* out, RowMap omap, int odt, void* out2,
+                                                           RowMap o2map, int o2dt) {
+    constexpr int D = 512 * VPL;
+    const int lane = threadIdx.x & 63;
+    const int row0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * R;
+    if (row0 >= M) return;
+    float4 v[R][VPL][2];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const float* xr = x + xmap.off(min(row0 + r, M - 1));
+#pragma unroll
+        for (int i = 0; i < VPL; ++i) {
+            const int c = i * 512 + lane * 8;
+            v[r][i][0] = *(const float4*)(xr + c);
+            v[r][i][1] = *(const float4*)(xr + c + 4);
+        }
+    }
+    float4 gg[VPL][2], bb[VPL][2];
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) {
+        const int c = i * 512 + lane * 8;
+        gg[i][0] = *(const float4*)(g + c); gg[i][1] = *(const float4*)(g + c + 4);
+        bb[i][0] = *(const float4*)(bta + c); bb[i][1] = *(const float4*)(bta + c + 4);
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int row = row0 + r;
+        if (row >= M) break;
+        double s = 0.0;
+#pragma unroll
+        for (int i = 0; i < VPL; ++i)
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+                s += (double)v[r][i][h].x + (double)v[r][i][h].y + (double)v[r][i][h].z + (double)v[r][i][h].w;
+        const double mean = wave_sum_d(s) / D;
+        double q = 0.0;
+#pragma unroll
+        for (int i = 0; i < VPL; ++i)
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const double a0 = v[r][i][h].x - mean, a1 = v[r][i][h].y - mean, a2 = v[r][i][h].z - mean,
+                             a3 = v[r][i][h].w - mean;
+                q += a0 * a0 + a1 * a1 + a2 * a2 + a3 * a3;
+            }
+        const double rstd = 1.0 / sqrt(wave_sum_d(q) / D + (double)eps);
+        const long long ob = omap.off(row), ob2 = out2 ? o2map.off(row) : 0;
+#pragma unroll
+        for (int i = 0; i < VPL; ++i) {
+            const int c = i * 512 + lane * 8;
+            float y[8];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const float4 t = v[r][i][h], ga = gg[i][h], be = bb[i][h];
+                y[4 * h + 0] = (float)((t.x - mean) * rstd) * ga.x + be.x;
+                y[4 * h + 1] = (float)((t.y - mean) * rstd) * ga.y + be.y;
+                y[4 * h + 2] = (float)((t.z - mean) * rstd) * ga.z + be.z;
+                y[4 * h + 3] = (float)((t.w - mean) * rstd) * ga.w + be.w;
+            }
+            if (odt == DT_F32) {
+                *(float4*)((float*)out + ob + c) = make_float4(y[0], y[1], y[2], y[3]);
+                *(float4*)((float*)out + ob + c + 4) = make_float4(y[4], y[5], y[6], y[7]);
+            } else {
+                bf16x8 t = {f2bf(y[0]), f2bf(y[1]), f2bf(y[2]), f2bf(y[3]), f2bf(y[4]), f2bf(y[5]), f2bf(y[6]), f2bf(y[7])};
+                *(bf16x8*)((bf16*)out + ob + c) = t;
+            }
+            if (out2) {
+                if (o2dt == DT_F32) {
+                    *(float4*)((float*)out2 + ob2 + c) = make_float4(y[0], y[1], y[2], y[3]);
+                    *(float4*)((float*)out2 + ob2 + c + 4) = make_float4(y[4], y[5], y[6], y[7]);
+                } else {
+                    bf16x8 t = {f2bf(y[0]), f2bf(y[1]), f2bf(y[2]), f2bf(y[3]), f2bf(y[4]), f2bf(y[5]), f2bf(y[6]), f2bf(y[7])};
+                    *(bf16x8*)((bf16*)out2 + ob2 + c) = t;
+                }
+            }
+        }
+    }
+}
 
 __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict__ x, RowMap xmap, int M, int D,
                                                         const float* __restrict__ g, const float* __restrict__ bta,
@@ -362,6 +449,28 @@ hipError_t pfm_layernorm(const float* x, RowMap xmap, int M, int D, const float*
                          RowMap o2map, int o2dt, hipStream_t st) {
     if (M <= 0) return hipSuccess;
     if (D % 4 != 0 || D > 4 * 64 * LN_MAXV) return hipErrorInvalidValue;
+    // streaming kernel: no prologue, D in {512, 1024, 2048}, 16-B aligned rows (8-element multiples)
+    auto al8 = [](const RowMap& m, const void* p, int dt) {
+        const int q = dt == DT_F32 ? 4 : 8;
+        return m.ld % q == 0 && (m.rows_per_seg <= 0 || m.seg_stride % q == 0) && ((uintptr_t)p % 16) == 0;
+    };
+    if (!pe && (D == 512 || D == 1024 || D == 2048) && al8(xmap, x, DT_F32) && al8(omap, out, odt) &&
+        (!out2 || al8(o2map, out2, o2dt))) {
+        constexpr int R = 2;
+        const unsigned blocks = (unsigned)(((M + R - 1) / R + 3) / 4);
+        const unsigned blocks1 = (unsigned)((M + 3) / 4);   // 2048-wide rows: one row per wave (register budget)
+        if (D == 512)
+            hipLaunchKernelGGL((layernorm_v8_kernel<1, R>), dim3(blocks), dim3(256), 0, st, x, xmap, M, g, b, eps, out,
+                               omap, odt, out2, o2map, o2dt);
+        else if (D == 1024)
+            hipLaunchKernelGGL((layernorm_v8_kernel<2, R>), dim3(blocks), dim3(256), 0, st, x, xmap, M, g, b, eps, out,
+                               omap, odt, out2, o2map, o2dt);
+        else
+            hipLaunchKernelGGL((layernorm_v8_kernel<4, 1>), dim3(blocks1), dim3(256), 0, st, x, xmap, M, g, b, eps, out,
+                               omap, odt, out2, o2map, o2dt);
+        PFM_LAUNCH_CHECK();
+        return hipSuccess;
+    }
     hipLaunchKernelGGL(layernorm_kernel, dim3((M + 3) / 4), dim3(256), 0, st, x, xmap, M, D, g, b, eps, pe,
                        pe_T > 0 ? pe_T : 1, in_scale, out, omap, odt, out2, o2map, o2dt);
     PFM_LAUNCH_CHECK();

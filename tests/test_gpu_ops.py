@@ -136,7 +136,7 @@ def test_attention(dev, dt, B, Tq, Tk, lens):
     assert rel(got, want) < (2e-6 if dt == "f32" else 1.5e-2)
 
 
-@pytest.mark.parametrize("M,D", [(1000, 512), (37, 560), (64, 2048)])
+@pytest.mark.parametrize("M,D", [(1000, 512), (37, 560), (64, 2048), (1, 512), (3, 1024), (77, 2048), (32001, 512)])
 def test_layernorm(dev, M, D):
     g = torch.Generator().manual_seed(D)
     x = torch.randn(M, D, generator=g) * 3 + 1
