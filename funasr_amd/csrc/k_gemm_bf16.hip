@@ -97,7 +97,7 @@ __global__ __launch_bounds__(C::NT) void gemm_bf16_kernel(const bf16* __restrict
     // the accumulator layout (32 lanes = 128 contiguous bytes per row) ahead of the prologue DMA, so
     // the epilogue carries no loads. vmcnt retires in order: an epilogue load issued after stores
     // waits for them, which serialised one HBM round trip per 4 rows before.
-    const bool pre_res = (epi.res0 || epi.res1) && epi.alpha == 1.f && !epi.relu;
+    const bool pre_res = epi.pre_res_ok && (epi.res0 || epi.res1) && epi.alpha == 1.f && !epi.relu;
     f32x16 acc[MI][NI];
 #pragma unroll
     for (int i = 0; i < MI; ++i)
@@ -294,6 +294,54 @@ __global__ __launch_bounds__(C::NT) void gemm_bf16_kernel(const bf16* __restrict
                     }
                     bf16x8 t = {f2bf(v.x), f2bf(v.y), f2bf(v.z), f2bf(v.w), f2bf(u.x), f2bf(u.y), f2bf(u.z), f2bf(u.w)};
                     *(bf16x8*)((bf16*)epi.out + epi.out_map.off(row) + col) = t;
+                }
+            } else if (C::MI <= 2 && epi.res_batch && !pre_res && (epi.res0 || epi.res1) && epi.out) {
+                // (64-row wave tiles only: with 128-row tiles the extra registers spill)
+                // residual loads of 4 row groups first, then their stores (vmcnt retires in order: a load
+                // queued behind a store waits for it)
+#pragma unroll
+                for (int sb = 0; sb < 8; sb += 4) {
+                    float4 r0[4], r1[4];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const int f = lane + 64 * (sb + q), rr = f >> 4, c4 = f & 15;
+                        const long long row = min(m0 + wm * C::WTM + i * 32 + rr, M - 1);
+                        const int col = min(n0 + wn * 64 + c4 * 4, N - 4);
+                        r0[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+                        r1[q] = r0[q];
+                        if (epi.res0) {
+                            if (epi.res0_bf16) {
+                                const bf16x4 t = *(const bf16x4*)((const bf16*)epi.res0 + row * epi.ld_res0 + col);
+                                r0[q] = make_float4(bf2f(t[0]), bf2f(t[1]), bf2f(t[2]), bf2f(t[3]));
+                            } else {
+                                r0[q] = *(const float4*)(epi.res0 + row * epi.ld_res0 + col);
+                            }
+                        }
+                        if (epi.res1) r1[q] = *(const float4*)(epi.res1 + row * epi.ld_res1 + col);
+                    }
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const int f = lane + 64 * (sb + q), rr = f >> 4, c4 = f & 15;
+                        const int row = m0 + wm * C::WTM + i * 32 + rr;
+                        const int col = n0 + wn * 64 + c4 * 4;
+                        if (row >= M || col >= N) continue;
+                        float4 v = *(const float4*)(ep + rr * EP + c4 * 4);
+                        v.x = v.x * epi.alpha + bb.x; v.y = v.y * epi.alpha + bb.y;
+                        v.z = v.z * epi.alpha + bb.z; v.w = v.w * epi.alpha + bb.w;
+                        if (epi.relu) { v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f); }
+                        v.x += r0[q].x + r1[q].x; v.y += r0[q].y + r1[q].y;
+                        v.z += r0[q].z + r1[q].z; v.w += r0[q].w + r1[q].w;
+                        const long long ob = epi.out_map.off(row) + col;
+                        if (f32o) *(float4*)((float*)epi.out + ob) = v;
+                        else {
+                            bf16x4 t = {f2bf(v.x), f2bf(v.y), f2bf(v.z), f2bf(v.w)};
+                            *(bf16x4*)((bf16*)epi.out + ob) = t;
+                        }
+                        if (epi.out2) {
+                            bf16x4 t = {f2bf(v.x), f2bf(v.y), f2bf(v.z), f2bf(v.w)};
+                            *(bf16x4*)((bf16*)epi.out2 + epi.out2_map.off(row) + col) = t;
+                        }
+                    }
                 }
             } else
 #pragma unroll
@@ -604,7 +652,9 @@ int pick_cfg(int M, int N, int K) {
     // deep enough (>= 1536) to amortise the longer prologue; else 128x256 (64x64 wave tiles,
     // 2 blocks / CU). Measured on the path shapes with tools/gemm_ab.py.
     const long long big = (long long)((M + 255) / 256) * ((N + 255) / 256);
-    return (big >= 512 || (K >= 1536 && big >= 240)) ? 1 : 4;
+    const char* kp = getenv("PFM_GEMM_KPOLICY");   // A/B switch for the K-aware rule (default on)
+    const bool kaware = !(kp && kp[0] == '0');
+    return (big >= 512 || (kaware && K >= 1536 && big >= 240)) ? 1 : 4;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -814,6 +864,14 @@ hipError_t pfm_gemm_bf16_256(const void* A, RowMap amap, const void* W, long lon
         e2.st16_ok = e2.vec_ok && epi.out && epi.out_dtype == DT_BF16 && !epi.out2 && !epi.amax_val && N % 8 == 0 &&
                      om.ld % 8 == 0 && (om.rows_per_seg <= 0 || om.seg_stride % 8 == 0) &&
                      ((uintptr_t)epi.out % 16) == 0 && !(ev && ev[0] == '0');
+    }
+    {
+        // residual pre-loaded into the accumulators (accumulator-layout scalar loads ahead of the main
+        // loop): measured 2.2 ms/step SLOWER on the path (bf16 + f32 residual out-proj), so opt-in
+        const char* pr = getenv("PFM_GEMM_PRERES");
+        e2.pre_res_ok = pr && pr[0] == '1';
+        const char* rb = getenv("PFM_GEMM_RESBATCH");   // residual loads batched ahead of the stores
+        e2.res_batch = !(rb && rb[0] == '0');
     }
     switch (pick_cfg(M, N, K)) {
         case 2: return launch<C2>(A, amap, W, ldw, M, N, K, e2, st);

@@ -87,6 +87,9 @@ struct GemmEpi {
     // set by the bf16 launcher: bf16-only output with 16-B aligned rows -> 8 columns per lane,
     // one 16-B store each (halves the store-issue tail of the big bf16 outputs)
     int st16_ok;
+    // set by the bf16 launcher: residual GEMMs may start their accumulators from res0 + res1
+    int pre_res_ok;
+    int res_batch;          // epilogue: residual loads of 4 row groups issued before their stores
 };
 
 static inline bool rowmap_vec4(const RowMap& m) {

@@ -44,17 +44,22 @@ def test_gemm_f32(dev, M, N, K):
 @pytest.mark.parametrize("cfg", ["0", "1", "2", "3", "4", "5", "6", "7", "8", "9", "10", "11", "12"])
 @pytest.mark.parametrize("M,N,K", [(300, 1536, 560), (77, 8404, 512), (1000, 512, 2048), (513, 1024, 1536),
                                    (256, 256, 64), (4000, 2048, 512), (2000, 768, 96), (600, 256, 32)])
-@pytest.mark.parametrize("epi", ["none", "bias_res", "bias_relu_res", "bias_relu_bf16"])
+@pytest.mark.parametrize("epi", ["none", "bias_res", "bias_res_pre", "bias_res_nobatch", "bias_relu_res",
+                                 "bias_relu_bf16"])
 def test_gemm_bf16(dev, M, N, K, cfg, epi, monkeypatch):
     """Every bf16 tile configuration (PFM_GEMM_CFG, read per launch; 0 = automatic policy), including
     K-tile counts below the pipeline depth (K = 32, 64, 96), and the epilogue variants: bias + residual
     (residual pre-loaded into the accumulators) and bias + relu + residual (added in the epilogue)."""
     monkeypatch.setenv("PFM_GEMM_CFG", cfg)
+    if epi == "bias_res_pre":        # residual pre-loaded into the accumulators (opt-in path)
+        monkeypatch.setenv("PFM_GEMM_PRERES", "1")
+    if epi == "bias_res_nobatch":    # residual loads interleaved with the stores
+        monkeypatch.setenv("PFM_GEMM_RESBATCH", "0")
     g = torch.Generator().manual_seed(M + N)
     A = torch.randn(M, K, generator=g).bfloat16()
     W = (torch.randn(N, K, generator=g) / K ** 0.5).bfloat16()
     b = torch.randn(N, generator=g) if epi != "none" else None
-    R = torch.randn(M, N, generator=g) if epi in ("bias_res", "bias_relu_res") else None
+    R = torch.randn(M, N, generator=g) if epi.startswith("bias_res") or epi == "bias_relu_res" else None
     want = A.double() @ W.double().T          # products of bf16 values are exact; f32 accumulate
     if b is not None:
         want = want + b.double()
