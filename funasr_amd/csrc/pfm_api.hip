@@ -869,6 +869,13 @@ int pfm_op_fsmn(void* stream, const float* v, const int32_t* len, const float* w
     return PFM_OK;
 }
 
+int pfm_op_fsmn_bf16(void* stream, const void* v, const int32_t* len, const float* w, void* out, int B, int T, int D,
+                     int K, int left) {
+    HIP_TRY(pfm_fsmn_bf16in((const bf16*)v, rowmap_plain(D), len, B, T, D, w, K, left, nullptr, nullptr, (bf16*)out,
+                            (hipStream_t)stream));
+    return PFM_OK;
+}
+
 int pfm_op_cif(void* stream, const float* alphas, const float* hidden, float* emb, float* peaks, int32_t* n_fire,
                int32_t* ntok, int B, int T, int D, int L_cap) {
     HIP_TRY(pfm_cif_fire(alphas, hidden, rowmap_plain(D), B, T, D, L_cap, emb, peaks, n_fire, ntok,

@@ -169,6 +169,10 @@ int pfm_op_layernorm(void* stream, const float* x, const float* gamma, const flo
 int pfm_op_fsmn(void* stream, const float* v, const int32_t* len, const float* w,
                 const float* res, float* out, int B, int T, int D, int K, int left);
 
+/* FSMN memory block on bf16 input v [B*T, D] -> bf16 out (fast-mode encoder form: no residual). */
+int pfm_op_fsmn_bf16(void* stream, const void* v, const int32_t* len, const float* w, void* out, int B,
+                     int T, int D, int K, int left);
+
 /* CIF integrate-and-fire on tail-processed alphas [B, T+1] and hidden [B, T+1, D]
  * (row T zero): emb [B, L_cap, D], peaks [B, T+1], n_fire [B], ntok [B]. */
 int pfm_op_cif(void* stream, const float* alphas, const float* hidden, float* emb, float* peaks,

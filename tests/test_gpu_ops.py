@@ -168,6 +168,29 @@ def test_fsmn(dev, B, T, lens, left):
     assert (got.double().cpu() - want).abs().max().item() < 1e-5
 
 
+@pytest.mark.parametrize("variant", ["0", "4", "8", "16"])
+@pytest.mark.parametrize("B,T,lens,left", [(2, 50, [50, 17], 5), (1, 9, [9], 5), (3, 40, [1, 40, 11], 7),
+                                           (4, 500, [500, 1, 250, 499], 5)])
+def test_fsmn_bf16(dev, B, T, lens, left, variant, monkeypatch):
+    """Fast-mode FSMN (bf16 in / bf16 out; PFM_FSMN_V2 selects the 4-channel kernel or the 8-channel
+    kernel's frames per thread) vs fp64 on the same bf16 inputs: one bf16 output rounding, so
+    rel-L2 <= 4e-3 and the padded rows exactly zero."""
+    monkeypatch.setenv("PFM_FSMN_V2", variant)
+    D, K = 512, 11
+    g = torch.Generator().manual_seed(T + left)
+    v = torch.randn(B * T, D, generator=g).bfloat16()
+    w = torch.randn(D, 1, K, generator=g) / K ** 0.5
+    L = torch.tensor(lens, dtype=torch.int32)
+    m = (torch.arange(T)[None] < L[:, None]).double()
+    want = ref.fsmn(v.double().reshape(B, T, D), m, w.double(), left - (K - 1) // 2).reshape(B * T, D)
+    got = rt.op_fsmn_bf16(v.to(dev), L.to(dev), w.to(dev), B, T, left)
+    torch.cuda.synchronize()
+    got = got.double().cpu()
+    assert rel(got, want) < 4e-3
+    pad = (m.reshape(-1) == 0)
+    assert torch.all(got[pad] == 0)
+
+
 def test_cif_bit_exact(dev):
     """Integrate-and-fire: fire pattern, peaks and token counts bit-exact vs the torch restatement."""
     B, T, D = 3, 300, 512
