@@ -421,51 +421,58 @@ __global__ __launch_bounds__(256) void cif_alpha_kernel(const float* __restrict_
 // token_num = floor(sum_t alpha_t) (f64 sum; the reference sums in f32 — see DESIGN.md).
 // h rows via RowMap; row T of each utterance must be the zero row appended by tail_process_fn.
 // ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void cif_fire_kernel(const float* __restrict__ alphas, const float* __restrict__ h,
-                                                       RowMap hmap, int T, int D, int Lcap,
-                                                       float* __restrict__ emb, float* __restrict__ peaks,
-                                                       int* __restrict__ n_fire, int* __restrict__ ntok) {
-    const int b = blockIdx.x;
+// Grid (D/64 channel slabs, B): one wave per (slab, utterance), one channel per lane. Every wave
+// recomputes the (uniform) fire schedule, so each channel's operations and their order are those of
+// the sequential reference loop; h rows are prefetched CIF_PF frames ahead of the recurrence.
+constexpr int CIF_PF = 16;
+__global__ __launch_bounds__(64) void cif_fire_kernel(const float* __restrict__ alphas, const float* __restrict__ h,
+                                                      RowMap hmap, int T, int D, int Lcap,
+                                                      float* __restrict__ emb, float* __restrict__ peaks,
+                                                      int* __restrict__ n_fire, int* __restrict__ ntok) {
+    const int b = blockIdx.y;
+    const int c = blockIdx.x * 64 + threadIdx.x;
+    const bool lead = blockIdx.x == 0 && threadIdx.x == 0;
+    const bool act = c < D;
+    const int cc = act ? c : D - 1;
     const float* al = alphas + (long long)b * (T + 1);
-    constexpr int CPT = 4;                 // channels per thread (D <= 1024)
-    double ph[CPT];
-    float pph[CPT], prh[CPT];
-#pragma unroll
-    for (int j = 0; j < CPT; ++j) { ph[j] = 0.0; pph[j] = 0.f; prh[j] = 0.f; }
-    double P = 0.0;
-    float prevfl = 0.f;
+    double ph = 0.0, P = 0.0;
+    float pph = 0.f, prh = 0.f, prevfl = 0.f;
     int k = 0;
-    for (int t = 0; t <= T; ++t) {
-        const float a = al[t];
-        P += (double)a;
-        const float Pf = (float)P;
-        const float fl = floorf(Pf);
-        const bool fire = (fl - prevfl) > 0.f;
-        prevfl = fl;
-        const float fires = (fire ? 1.f : 0.f) + (Pf - fl);
-        if (threadIdx.x == 0 && peaks) peaks[(long long)b * (T + 1) + t] = fires;
-        const float rem = fires - floorf(fires);
-        const float* hr = h + hmap.off((long long)b * (T + 1) + t);
+    for (int t0 = 0; t0 <= T; t0 += CIF_PF) {
+        float hv[CIF_PF], av[CIF_PF];
 #pragma unroll
-        for (int j = 0; j < CPT; ++j) {
-            const int c = threadIdx.x + j * blockDim.x;
-            if (c < D) {
-                const float hv = hr[c];
-                ph[j] += (double)(a * hv);
-                if (fire) {
-                    const float phf = (float)ph[j];
-                    const float rh = rem * hv;
-                    if (k < Lcap) emb[((long long)b * Lcap + k) * D + c] = ((phf - pph[j]) + prh[j]) - rh;
-                    pph[j] = phf;
-                    prh[j] = rh;
-                }
+        for (int i = 0; i < CIF_PF; ++i) {
+            const int t = min(t0 + i, T);
+            av[i] = al[t];
+            hv[i] = h[hmap.off((long long)b * (T + 1) + t) + cc];
+        }
+#pragma unroll
+        for (int i = 0; i < CIF_PF; ++i) {
+            const int t = t0 + i;
+            if (t > T) break;
+            const float a = av[i];
+            P += (double)a;
+            const float Pf = (float)P;
+            const float fl = floorf(Pf);
+            const bool fire = (fl - prevfl) > 0.f;
+            prevfl = fl;
+            const float fires = (fire ? 1.f : 0.f) + (Pf - fl);
+            if (lead && peaks) peaks[(long long)b * (T + 1) + t] = fires;
+            const float rem = fires - floorf(fires);
+            ph += (double)(a * hv[i]);
+            if (fire) {
+                const float phf = (float)ph;
+                const float rh = rem * hv[i];
+                if (act && k < Lcap) emb[((long long)b * Lcap + k) * D + c] = ((phf - pph) + prh) - rh;
+                pph = phf;
+                prh = rh;
+                ++k;
             }
         }
-        if (fire) ++k;
     }
-    for (int kk = k; kk < Lcap; ++kk)
-        for (int c = threadIdx.x; c < D; c += blockDim.x) emb[((long long)b * Lcap + kk) * D + c] = 0.f;
-    if (threadIdx.x == 0) {
+    if (act)
+        for (int kk = k; kk < Lcap; ++kk) emb[((long long)b * Lcap + kk) * D + c] = 0.f;
+    if (lead) {
         n_fire[b] = k;
         double s = 0.0;
         for (int t = 0; t <= T; ++t) s += (double)al[t];
@@ -627,9 +634,9 @@ hipError_t pfm_cif_alpha(const float* hc, int D, const float* wout, const float*
 
 hipError_t pfm_cif_fire(const float* alphas, const float* h, RowMap hmap, int B, int T, int D, int Lcap,
                         float* emb, float* peaks, int* n_fire, int* ntok, hipStream_t st) {
-    if (D > 4 * 256) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(cif_fire_kernel, dim3(B), dim3(256), 0, st, alphas, h, hmap, T, D, Lcap, emb, peaks,
-                       n_fire, ntok);
+    if (B <= 0 || D <= 0) return hipSuccess;
+    hipLaunchKernelGGL(cif_fire_kernel, dim3((D + 63) / 64, B), dim3(64), 0, st, alphas, h, hmap, T, D, Lcap, emb,
+                       peaks, n_fire, ntok);
     PFM_LAUNCH_CHECK();
     return hipSuccess;
 }
