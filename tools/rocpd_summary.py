@@ -11,7 +11,7 @@ import sys
 from collections import defaultdict
 
 
-def main(db, out_csv, marker="argmax_reduce_kernel"):
+def main(db, out_csv, marker="argmax_reduce_kernel", bench_log=None):
     c = sqlite3.connect(db)
     rows = c.execute("select name, duration, grid_x, grid_y, grid_z, workgroup_x from kernels").fetchall()
     agg = defaultdict(list)
@@ -34,6 +34,18 @@ def main(db, out_csv, marker="argmax_reduce_kernel"):
         nm = k.replace("(anonymous namespace)::", "").replace("|", "/")[:80]
         print(f"| `{nm}` | {len(v) / steps:.0f} | {sum(v) / 1e6 / steps:.3f} | {sum(v) / len(v) / 1e3:.1f} | "
               f"{100 * sum(v) / tot:.1f} |")
+    # roofline cross-check: the bench's dominant-kernel set = every bf16 GEMM launch
+    gl = [d for k, v in agg.items() for d in v
+          if "gemm_bf16_kernel" in k or "gemm_nt_kernelIDF16b" in k or "gemm_nt_kernel<__bf16>" in k]
+    if gl:
+        print(f"\nbf16 GEMM launches (bench roofline kernel set): {len(gl)} launches, "
+              f"avg {sum(gl) / len(gl) / 1e3:.2f} us (rocprof)")
+    if bench_log:
+        import json
+        line = [x for x in open(bench_log) if x.startswith("{")][-1]
+        r = json.loads(line)["roofline"]
+        print(f"bench live HIP-event avg_launch_us {r['avg_launch_us']} over {r['launches']} launches; "
+              f"achieved {r['achieved']} TFLOP/s, frac {r['frac']}")
     print("\n| GEMM kernel / blocks | calls/step | ms/step | avg us |\n|---|---|---|---|")
     for k, v in sorted(shapes.items(), key=lambda kv: -sum(kv[1]))[:20]:
         print(f"| `{k[0]}` {k[1]}x{k[2]}x{k[3]} | {len(v) / steps:.0f} | {sum(v) / 1e6 / steps:.3f} | "
