@@ -157,9 +157,19 @@ def main():
     gemm["ms"] = max(1e-9, gemm["ms"] - ev_over_ms * gemm["launches"])
     attn["ms"] = max(1e-9, attn["ms"] - ev_over_ms * attn["launches"])
     g_ach = gemm["flops"] / (gemm["ms"] / 1e3) / 1e12 if gemm["ms"] > 0 else 0.0
+    # HBM bytes per launch of the same kernel set from the committed PMC passes (rocprofv3 --pmc FETCH_SIZE /
+    # WRITE_SIZE, separate runs of this bench, gfx950-corrected by tools/pmc_traffic.py); null when absent
+    traffic, traffic_src = None, None
+    tpath = os.path.join(ROOT, "profiles", "r01_gemm_traffic.json")
+    if args.mode == "fast" and os.path.exists(tpath):
+        with open(tpath) as f:
+            traffic = round(json.load(f)["hbm_bytes_per_launch"])
+        traffic_src = "profiles/r01_gemm_traffic.json (PMC FETCH_SIZE x2 + WRITE_SIZE per bf16 GEMM launch)"
     roofline = {"bound": "mfma", "kernel": "gemm_bf16_256_kernel (+gemm_nt_kernel<bf16> for K%64!=0)" if args.mode == "fast" else "gemm_nt_kernel<float>",
                 "achieved": round(g_ach, 2), "peak": peak, "unit": "TFLOP/s", "frac": round(g_ach / peak, 4),
-                "traffic": None,
+                "traffic": traffic,
+                "traffic_source": traffic_src,
+                "algorithmic_bytes_per_launch": round(gemm["bytes"] / max(1, gemm["launches"])),
                 "avg_launch_us": round(gemm["ms"] * 1e3 / max(1, gemm["launches"]), 2),
                 "avg_launch_us_raw": round(g_raw_ms * 1e3 / max(1, gemm["launches"]), 2),
                 "event_pair_overhead_us": round(ev_over_ms * 1e3, 2),

@@ -218,29 +218,40 @@ __global__ __launch_bounds__(NWV * 64) void attn_bf16_kernel(AttnArgs a) {
 
     // register staging: each thread moves (64 rows x 16 chunks) / NT chunks of K and of V per tile
     constexpr int CPT = KT2 * 16 / NT;
-    uint4 rk[CPT], rv[CPT];
-    auto gload = [&](int t) {
-#pragma unroll
-        for (int i = 0; i < CPT; ++i) {
-            const int c = tid + NT * i, row = c >> 4, ch = c & 15;
-            const int key = t * KT2 + row;
-            rk[i] = make_uint4(0, 0, 0, 0);
-            rv[i] = make_uint4(0, 0, 0, 0);
-            if (key < klen) {
-                const long long m = (long long)b * a.Tk + key;
-                rk[i] = *(const uint4*)(K + a.kmap.off(m) + h * DK + ch * 8);
-                rv[i] = *(const uint4*)(V + a.vmap.off(m) + h * DK + ch * 8);
-            }
-        }
+    static_assert(CPT == 2 || CPT == 4, "staging struct holds 2 or 4 16-B chunks of K and of V per thread");
+    // two register sets: tile t+2 is fetched while tile t computes and tile t+1 (fetched one
+    // iteration earlier) is written to LDS at the end of iteration t -> a full iteration of cover.
+    // Rows past klen load a clamped valid row (masked to -inf in the scores of the last tile).
+    // Named members returned by value (register arrays indexed before unrolling went to scratch).
+    struct Stg { uint4 k0, k1, k2, k3, v0, v1, v2, v3; };
+    auto ld1 = [&](int t, int c, uint4& kk, uint4& vv) {
+        const long long m = (long long)b * a.Tk + min(t * KT2 + (c >> 4), max(klen - 1, 0));
+        kk = *(const uint4*)(K + a.kmap.off(m) + h * DK + (c & 15) * 8);
+        vv = *(const uint4*)(V + a.vmap.off(m) + h * DK + (c & 15) * 8);
     };
-    auto sstore = [&](int s) {
+    auto gload = [&](int t) -> Stg {
+        Stg r = {};
+        ld1(t, tid, r.k0, r.v0);
+        ld1(t, tid + NT, r.k1, r.v1);
+        if constexpr (CPT == 4) {
+            ld1(t, tid + 2 * NT, r.k2, r.v2);
+            ld1(t, tid + 3 * NT, r.k3, r.v3);
+        }
+        return r;
+    };
+    auto st1 = [&](unsigned char* Ks, unsigned char* Vs, int c, const uint4& kk, const uint4& vv) {
+        const int row = c >> 4, ch = c & 15;
+        *(uint4*)(Ks + row * KROW + ((ch ^ (row & 15)) << 4)) = kk;
+        *(uint4*)(Vs + row * VROW + ch * 16) = vv;
+    };
+    auto sstore = [&](int s, const Stg& r) {
         unsigned char* Ks = smem + s * STG2;
         unsigned char* Vs = Ks + KTILE;
-#pragma unroll
-        for (int i = 0; i < CPT; ++i) {
-            const int c = tid + NT * i, row = c >> 4, ch = c & 15;
-            *(uint4*)(Ks + row * KROW + ((ch ^ (row & 15)) << 4)) = rk[i];
-            *(uint4*)(Vs + row * VROW + ch * 16) = rv[i];
+        st1(Ks, Vs, tid, r.k0, r.v0);
+        st1(Ks, Vs, tid + NT, r.k1, r.v1);
+        if constexpr (CPT == 4) {
+            st1(Ks, Vs, tid + 2 * NT, r.k2, r.v2);
+            st1(Ks, Vs, tid + 3 * NT, r.k3, r.v3);
         }
     };
     // per-lane constants of the transposed V read: lane 4q+p of its 16-lane group addresses key
@@ -249,11 +260,13 @@ __global__ __launch_bounds__(NWV * 64) void attn_bf16_kernel(AttnArgs a) {
     const int tr_key = 4 * (tg >> 1) + (ti >> 2);
     const int tr_col = 16 * (tg & 1) + 4 * (ti & 3);
 
-    if (ntiles > 0) { gload(0); sstore(0); }
+    Stg nxt = {}, nxt2 = {};
+    if (ntiles > 0) sstore(0, gload(0));
+    if (ntiles > 1) nxt = gload(1);
     __syncthreads();
     for (int t = 0; t < ntiles; ++t) {
         const int cur = t & 1;
-        if (t + 1 < ntiles) gload(t + 1);
+        if (t + 2 < ntiles) nxt2 = gload(t + 2);
         const unsigned char* Ks = smem + cur * STG2;
         const unsigned char* Vs = Ks + KTILE;
         f32x16 s[2];
@@ -269,15 +282,20 @@ __global__ __launch_bounds__(NWV * 64) void attn_bf16_kernel(AttnArgs a) {
             }
         }
         // lane holds S^T[key = t*64 + kb*32 + kappa(e) + 4fh][q = fr]
+        if ((t + 1) * KT2 > klen) {   // only the last tile can hold keys past klen
+#pragma unroll
+            for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+                for (int e = 0; e < 16; ++e) {
+                    const int key = t * KT2 + kb * 32 + kappa(e) + 4 * fh;
+                    if (key >= klen) s[kb][e] = -INFINITY;
+                }
+        }
         float mt = -INFINITY;
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-            for (int e = 0; e < 16; ++e) {
-                const int key = t * KT2 + kb * 32 + kappa(e) + 4 * fh;
-                if (key >= klen) s[kb][e] = -INFINITY;
-                mt = fmaxf(mt, s[kb][e]);
-            }
+            for (int e = 0; e < 16; ++e) mt = fmaxf(mt, s[kb][e]);
         mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
         if (mt > mused + RESCALE_THR) {    // lazy rescale (per query row; rare after the first tile)
             const float corr = __expf(mused - mt);
@@ -320,7 +338,8 @@ __global__ __launch_bounds__(NWV * 64) void attn_bf16_kernel(AttnArgs a) {
                 }
             }
         }
-        if (t + 1 < ntiles) sstore(cur ^ 1);
+        if (t + 1 < ntiles) sstore(cur ^ 1, nxt);
+        nxt = nxt2;
         __syncthreads();
     }
     if (qrow >= a.Tq) return;

@@ -54,13 +54,25 @@ template <int P> __device__ __forceinline__ void wait_vm(int rem) {
 template <class C>
 __global__ __launch_bounds__(C::NT) void gemm_bf16_kernel(const bf16* __restrict__ A, RowMap amap,
                                                           const bf16* __restrict__ W, long long ldw, int M, int N,
-                                                          int K, int tiles_n, GemmEpi epi) {
+                                                          int K, int tiles_m, int tiles_n, int gm, GemmEpi epi) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr int BK = C::BK, NS = C::NS, ROWB = C::ROWB, MI = C::MI, NI = C::NI, PA = C::PA, PW = C::PW;
     const int nwg = gridDim.x, bid = blockIdx.x;
     const int q = nwg / 8, r = nwg % 8, xcd = bid % 8;
     const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
-    const int tm = wg / tiles_n, tn = wg % tiles_n;
+    // grouped order: consecutive tiles walk down gm tile-rows before moving one tile-column right, so
+    // the ~32 tiles an XCD runs at once share gm A-row bands and a few W-column bands in its 4 MiB L2
+    // (row-major order streamed all of W once per tile-row on the wide-N projections)
+    int tm, tn;
+    if (gm > 0) {
+        const int gsz = gm * tiles_n, g = wg / gsz, idx = wg - g * gsz;
+        const int rows = min(gm, tiles_m - g * gm);
+        tm = g * gm + idx % rows;
+        tn = idx / rows;
+    } else {
+        tm = wg / tiles_n;
+        tn = wg % tiles_n;
+    }
     const int m0 = tm * C::BM, n0 = tn * C::BN;
     const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wid / C::WGN, wn = wid % C::WGN;
@@ -609,8 +621,12 @@ hipError_t launch(const void* A, RowMap amap, const void* W, long long ldw, int 
         (void)hipFuncSetAttribute((const void*)gemm_bf16_kernel<C>, hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
     }
     const int tiles_m = (M + C::BM - 1) / C::BM, tiles_n = (N + C::BN - 1) / C::BN;
+    // grouped tile order (4 tile-rows per group) for the wide-N projections (memory K|V, vocabulary:
+    // +6 % measured), row-major otherwise; PFM_GEMM_GM overrides per launch (A/B)
+    const char* eg = getenv("PFM_GEMM_GM");
+    const int gm = eg ? atoi(eg) : (tiles_n >= 16 ? 4 : 0);
     hipLaunchKernelGGL(gemm_bf16_kernel<C>, dim3(tiles_m * tiles_n), dim3(C::NT), C::LDS, st, (const bf16*)A, amap,
-                       (const bf16*)W, ldw, M, N, K, tiles_n, e2);
+                       (const bf16*)W, ldw, M, N, K, tiles_m, tiles_n, gm, e2);
     PFM_LAUNCH_CHECK();
     return hipSuccess;
 }
