@@ -17,6 +17,8 @@
 //   V is staged transposed in LDS.
 #include <stdlib.h>
 
+#include <stdint.h>
+
 #include "pfm_common.h"
 
 namespace {
@@ -34,6 +36,9 @@ struct AttnArgs {
     const int* klen;              // [B] valid keys
     int Tq, Tk;
     float scale;
+    // optional fused FSMN memory block (encoder self-attention, fast mode): fout[b*Tq + t][h*DK + c] =
+    // mask * (sum_k fw[k][h*DK + c] * vm[t - 5 + k] + vm[t]), vm = V rows masked by klen (K = 11, left 5)
+    const float* fw; bf16* fout; long long fld; int fD;
 };
 
 // ---- f32 tile geometry (bytes)
@@ -173,10 +178,65 @@ constexpr int KROW = DK * 2;                    // 256 B
 constexpr int VROW = DK * 2 + 64;               // 320 B
 constexpr int KTILE = KT2 * KROW, VTILE = KT2 * VROW;
 constexpr int STG2 = KTILE + VTILE;             // 36 KiB per stage
+constexpr int FSMN_LDS = (256 + 10) * DK * 2 + 11 * DK * 4;   // fused FSMN epilogue staging (8-wave kernel)
+constexpr int LDS8 = (2 * STG2 > FSMN_LDS) ? 2 * STG2 : FSMN_LDS;
 constexpr float RESCALE_THR = 8.0f;             // lazy O rescale: only when a row max grows by > 8
 
 typedef short v4i16 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
+
+// Fused FSMN memory block for the block's QB query rows x this head's DK channels (encoder
+// self-attention: query row == key row). V rows [t0-5, t0+QB+5) of head h go to LDS (rows outside
+// [0, klen) as zeros), the 11 taps of the head's channels after them; thread = 8 rows x 8 channels.
+// Same f32 operation order as fsmn_win_kernel<11, bf16, 5> (taps ascending, then + x[t]).
+template <int QB, int NTH>
+__device__ __forceinline__ void fsmn_epilogue(const AttnArgs& a, unsigned char* smem, int qt, int h, int b, int klen) {
+    constexpr int FK = 11, FL = 5, FR = QB + FK - 1, RB = DK * 2;   // 256-B rows
+    static_assert(NTH == (QB / 8) * (DK / 8), "one thread per 8 rows x 8 channels");
+    __syncthreads();                                   // every wave is past its last K/V read
+    const int t0 = qt * QB;
+    const bf16* V = (const bf16*)a.v;
+    unsigned char* xs = smem;
+    float* ws = (float*)(smem + FR * RB);
+    for (int i = threadIdx.x; i < FR * (DK / 8); i += NTH) {
+        const int r = i / (DK / 8), ch = i % (DK / 8), t = t0 - FL + r;
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (t >= 0 && t < klen) v = *(const uint4*)(V + a.vmap.off((long long)b * a.Tk + t) + h * DK + ch * 8);
+        *(uint4*)(xs + r * RB + ch * 16) = v;
+    }
+    for (int i = threadIdx.x; i < FK * (DK / 4); i += NTH) {
+        const int k = i / (DK / 4), c4 = i % (DK / 4);
+        *(float4*)(ws + k * DK + c4 * 4) = *(const float4*)(a.fw + (long long)k * a.fD + h * DK + c4 * 4);
+    }
+    __syncthreads();
+    const int rb = threadIdx.x / (DK / 8), c8 = (threadIdx.x % (DK / 8)) * 8;
+    float y[8][8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) y[i][j] = 0.f;
+#pragma unroll
+    for (int k = 0; k < FK; ++k) {
+        const float4 wa = *(const float4*)(ws + k * DK + c8), wb = *(const float4*)(ws + k * DK + c8 + 4);
+        const float w8[8] = {wa.x, wa.y, wa.z, wa.w, wb.x, wb.y, wb.z, wb.w};
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const bf16x8 x = *(const bf16x8*)(xs + (rb * 8 + i + k) * RB + c8 * 2);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) y[i][j] = fmaf(w8[j], bf2f(x[j]), y[i][j]);
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int t = t0 + rb * 8 + i;
+        if (t >= a.Tq) break;
+        const bf16x8 xself = *(const bf16x8*)(xs + (rb * 8 + i + FL) * RB + c8 * 2);
+        bf16x8 ob;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) ob[j] = f2bf(t < klen ? y[i][j] + bf2f(xself[j]) : 0.f);
+        *(bf16x8*)(a.fout + ((long long)b * a.Tq + t) * a.fld + h * DK + c8) = ob;
+    }
+}
 
 template <int NWV>
 __global__ __launch_bounds__(NWV * 64) void attn_bf16_kernel(AttnArgs a) {
@@ -190,8 +250,10 @@ __global__ __launch_bounds__(NWV * 64) void attn_bf16_kernel(AttnArgs a) {
     const bf16* K = (const bf16*)a.k;
     const bf16* V = (const bf16*)a.v;
 
-    // Q fragment (B operand of S^T = K.Q^T): lane (q = fr) holds dims 16kq + 8fh + j, pre-scaled
+    // Q fragment (B operand of S^T = K.Q^T): lane (q = fr) holds dims 16kq + 8fh + j, pre-scaled by
+    // d_k^-0.5 * log2(e): scores arrive in log2 units, so each probability is one subtract + v_exp_f32
     const int qrow = qt * QBLK + wid * QW + fr;
+    const float qs = a.scale * 1.4426950408889634f;
     bf16x8 qf[8];
     {
         const bool ok = qrow < a.Tq;
@@ -204,7 +266,7 @@ __global__ __launch_bounds__(NWV * 64) void attn_bf16_kernel(AttnArgs a) {
 #pragma unroll
                 for (int j = 0; j < 8; ++j) x[j] = (bf16)0.f;
 #pragma unroll
-            for (int j = 0; j < 8; ++j) x[j] = f2bf(bf2f(x[j]) * a.scale);
+            for (int j = 0; j < 8; ++j) x[j] = f2bf(bf2f(x[j]) * qs);
             qf[kq] = x;
         }
     }
@@ -297,8 +359,8 @@ __global__ __launch_bounds__(NWV * 64) void attn_bf16_kernel(AttnArgs a) {
 #pragma unroll
             for (int e = 0; e < 16; ++e) mt = fmaxf(mt, s[kb][e]);
         mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
-        if (mt > mused + RESCALE_THR) {    // lazy rescale (per query row; rare after the first tile)
-            const float corr = __expf(mused - mt);
+        if (mt > mused + RESCALE_THR * 1.4426950408889634f) {   // lazy rescale (log2 units; rare after tile 0)
+            const float corr = __builtin_amdgcn_exp2f(mused - mt);
             lrun *= corr;
 #pragma unroll
             for (int d = 0; d < 4; ++d)
@@ -311,7 +373,7 @@ __global__ __launch_bounds__(NWV * 64) void attn_bf16_kernel(AttnArgs a) {
         for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
             for (int e = 0; e < 16; ++e) {
-                s[kb][e] = __expf(s[kb][e] - mused);
+                s[kb][e] = __builtin_amdgcn_exp2f(s[kb][e] - mused);
                 ls += s[kb][e];
             }
         ls += __shfl_xor(ls, 32, 64);
@@ -342,6 +404,206 @@ __global__ __launch_bounds__(NWV * 64) void attn_bf16_kernel(AttnArgs a) {
         nxt = nxt2;
         __syncthreads();
     }
+    if (qrow < a.Tq) {
+        const float inv = (klen > 0) ? 1.f / lrun : 0.f;
+        float* op = a.o ? a.o + ((long long)b * a.Tq + qrow) * a.ldo + h * DK : nullptr;
+        bf16* op2 = a.o2 ? (bf16*)a.o2 + ((long long)b * a.Tq + qrow) * a.ldo + h * DK : nullptr;
+#pragma unroll
+        for (int d = 0; d < 4; ++d)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {   // registers 4g..4g+3 are 4 consecutive head dims
+                const int col = d * 32 + 8 * g + 4 * fh;
+                const float v0 = o[d][4 * g] * inv, v1 = o[d][4 * g + 1] * inv;
+                const float v2 = o[d][4 * g + 2] * inv, v3 = o[d][4 * g + 3] * inv;
+                if (op) *(float4*)(op + col) = make_float4(v0, v1, v2, v3);
+                if (op2) {
+                    bf16x4 t4 = {f2bf(v0), f2bf(v1), f2bf(v2), f2bf(v3)};
+                    *(bf16x4*)(op2 + col) = t4;
+                }
+            }
+    }
+    if constexpr (NWV == 8) {
+        if (a.fout) fsmn_epilogue<QBLK, NT>(a, smem, qt, h, b, klen);
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// Ping-pong variant (8 waves, 256 query rows per block). Waves 0-3 (group 0) and 4-7 (group 1) share
+// every SIMD; per key tile each wave runs
+//   phase A(t): QK^T of tile t (16 MFMA) + PV of tile t-1 (16 MFMA)         -> barrier
+//   phase B(t): softmax of tile t (VALU: max, lazy rescale, exp2, row sum, P -> bf16) -> barrier
+// and group 1 runs one barrier behind group 0, so one wave's MFMAs overlap its partner's VALU.
+// Common barrier numbering (b0 = prologue): G0 ends A(t) at b(2t+1), B(t) at b(2t+2); G1 ends A(t) at
+// b(2t+2), B(t) at b(2t+3). Tile t+1 is written to LDS stage (t+1)%3 by G0 in B(t) and by G1 in A(t),
+// i.e. before b(2t+2), and first read after b(2t+2) (G0's A(t+1)). 3 stages: the buffer a write
+// targets last held tile t-2, whose final read (G1's PV(t-2) in A(t-1)) ended at b(2t).
+// Register staging fetches tile t+2 at the start of A(t) (two named sets in flight).
+__global__ __launch_bounds__(512) void attn_bf16_pp_kernel(AttnArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    constexpr int NT = 512, QBLK = 8 * QW, NSTG = 3;
+    const int qt = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+    const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int grp = wid >> 2;
+    const int fr = lane & 31, fh = lane >> 5;
+    const int klen = min(a.klen[b], a.Tk);
+    const bf16* Q = (const bf16*)a.q;
+    const bf16* K = (const bf16*)a.k;
+    const bf16* V = (const bf16*)a.v;
+    const int qrow = qt * QBLK + wid * QW + fr;
+    const float qs = a.scale * 1.4426950408889634f;   // scores in log2 units
+    bf16x8 qf[8];
+    {
+        const bool ok = qrow < a.Tq;
+        const bf16* qp = Q + a.qmap.off((long long)b * a.Tq + (ok ? qrow : 0)) + h * DK;
+#pragma unroll
+        for (int kq = 0; kq < 8; ++kq) {
+            bf16x8 x = *(const bf16x8*)(qp + kq * 16 + fh * 8);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) x[j] = ok ? f2bf(bf2f(x[j]) * qs) : (bf16)0.f;
+            qf[kq] = x;
+        }
+    }
+    f32x16 o[4];
+#pragma unroll
+    for (int d = 0; d < 4; ++d)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) o[d][e] = 0.f;
+    float mused = -INFINITY, lrun = 0.f;
+    const int ntiles = (klen + KT2 - 1) / KT2;
+
+    struct Stg { uint4 k0, k1, v0, v1; };
+    auto ld1 = [&](int t, int c, uint4& kk, uint4& vv) {
+        const long long m = (long long)b * a.Tk + min(t * KT2 + (c >> 4), max(klen - 1, 0));
+        kk = *(const uint4*)(K + a.kmap.off(m) + h * DK + (c & 15) * 8);
+        vv = *(const uint4*)(V + a.vmap.off(m) + h * DK + (c & 15) * 8);
+    };
+    auto gload = [&](int t) -> Stg {
+        Stg r;
+        ld1(t, tid, r.k0, r.v0);
+        ld1(t, tid + NT, r.k1, r.v1);
+        return r;
+    };
+    auto st1 = [&](unsigned char* Ks, unsigned char* Vs, int c, const uint4& kk, const uint4& vv) {
+        const int row = c >> 4, ch = c & 15;
+        *(uint4*)(Ks + row * KROW + ((ch ^ (row & 15)) << 4)) = kk;
+        *(uint4*)(Vs + row * VROW + ch * 16) = vv;
+    };
+    auto sstore = [&](int t, const Stg& r) {
+        unsigned char* Ks = smem + (t % NSTG) * STG2;
+        st1(Ks, Ks + KTILE, tid, r.k0, r.v0);
+        st1(Ks, Ks + KTILE, tid + NT, r.k1, r.v1);
+    };
+    const int tg = lane >> 4, ti = lane & 15;
+    const int tr_key = 4 * (tg >> 1) + (ti >> 2);
+    const int tr_col = 16 * (tg & 1) + 4 * (ti & 3);
+
+    auto qk = [&](int t, f32x16 (&sc)[2]) {
+        const unsigned char* Ks = smem + (t % NSTG) * STG2;
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+            for (int e = 0; e < 16; ++e) sc[kb][e] = 0.f;
+            const int row = kb * 32 + fr;
+#pragma unroll
+            for (int kq = 0; kq < 8; ++kq) {
+                const bf16x8 kx = *(const bf16x8*)(Ks + row * KROW + (((2 * kq + fh) ^ (row & 15)) << 4));
+                sc[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kx, qf[kq], sc[kb], 0, 0, 0);
+            }
+        }
+    };
+    auto pv = [&](int t, const bf16x8 (&pb)[4]) {
+        const unsigned char* Vs = smem + (t % NSTG) * STG2 + KTILE;
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int st = 0; st < 2; ++st) {
+                const int key0 = kb * 32 + 16 * st + tr_key;
+#pragma unroll
+                for (int d = 0; d < 4; ++d) {
+                    const unsigned char* vp = Vs + key0 * VROW + (d * 32 + tr_col) * 2;
+                    const v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)vp);
+                    const v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(vp + 8 * VROW));
+                    bf16x8 va;
+                    __builtin_memcpy(&va, &lo, 8);
+                    __builtin_memcpy(((char*)&va) + 8, &hi, 8);
+                    o[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va, pb[2 * kb + st], o[d], 0, 0, 0);
+                }
+            }
+    };
+    auto softmax = [&](int t, f32x16 (&sc)[2], bf16x8 (&pb)[4]) {
+        if ((t + 1) * KT2 > klen) {
+#pragma unroll
+            for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+                for (int e = 0; e < 16; ++e)
+                    if (t * KT2 + kb * 32 + kappa(e) + 4 * fh >= klen) sc[kb][e] = -INFINITY;
+        }
+        float mt = -INFINITY;
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) mt = fmaxf(mt, sc[kb][e]);
+        mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+        if (mt > mused + RESCALE_THR * 1.4426950408889634f) {   // PV(t-1) is complete (phase A)
+            const float corr = __builtin_amdgcn_exp2f(mused - mt);
+            lrun *= corr;
+#pragma unroll
+            for (int d = 0; d < 4; ++d)
+#pragma unroll
+                for (int e = 0; e < 16; ++e) o[d][e] *= corr;
+            mused = mt;
+        }
+        float ls = 0.f;
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                sc[kb][e] = __builtin_amdgcn_exp2f(sc[kb][e] - mused);
+                ls += sc[kb][e];
+            }
+        ls += __shfl_xor(ls, 32, 64);
+        lrun += ls;
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int st = 0; st < 2; ++st)
+#pragma unroll
+                for (int j = 0; j < 8; ++j) pb[2 * kb + st][j] = f2bf(sc[kb][8 * st + j]);
+    };
+    auto bar = [&]() {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+    };
+
+    Stg nxt = {}, nxt2 = {};
+    if (ntiles > 0) sstore(0, gload(0));
+    if (ntiles > 1) nxt = gload(1);
+    __syncthreads();                                  // b0
+    if (grp == 1) bar();                              // stagger: group 1 one phase behind
+    f32x16 sc[2];
+    bf16x8 pb[4];
+    for (int t = 0; t < ntiles; ++t) {
+        // ---- phase A(t): MFMA
+        if (t + 2 < ntiles) nxt2 = gload(t + 2);
+        qk(t, sc);
+        if (t > 0) pv(t - 1, pb);
+        if (grp == 1) {
+            if (t + 1 < ntiles) sstore(t + 1, nxt);
+            nxt = nxt2;
+        }
+        bar();
+        // ---- phase B(t): softmax (VALU)
+        softmax(t, sc, pb);
+        if (grp == 0) {
+            if (t + 1 < ntiles) sstore(t + 1, nxt);
+            nxt = nxt2;
+        }
+        bar();
+    }
+    if (ntiles > 0) pv(ntiles - 1, pb);
+    if (grp == 0) bar();                              // match group 1's stagger barrier
     if (qrow >= a.Tq) return;
     const float inv = (klen > 0) ? 1.f / lrun : 0.f;
     float* op = a.o ? a.o + ((long long)b * a.Tq + qrow) * a.ldo + h * DK : nullptr;
@@ -349,7 +611,7 @@ __global__ __launch_bounds__(NWV * 64) void attn_bf16_kernel(AttnArgs a) {
 #pragma unroll
     for (int d = 0; d < 4; ++d)
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {   // registers 4g..4g+3 are 4 consecutive head dims
+        for (int g = 0; g < 4; ++g) {
             const int col = d * 32 + 8 * g + 4 * fh;
             const float v0 = o[d][4 * g] * inv, v1 = o[d][4 * g + 1] * inv;
             const float v2 = o[d][4 * g + 2] * inv, v3 = o[d][4 * g + 3] * inv;
@@ -365,14 +627,23 @@ __global__ __launch_bounds__(NWV * 64) void attn_bf16_kernel(AttnArgs a) {
 
 // q/k/v: head-concatenated rows (head h at column h*128). o: f32 [B*Tq, ldo] (may be null in
 // bf16 mode when only o2 is wanted). heads*128 columns per row.
-hipError_t pfm_attention(int dtype, const void* q, RowMap qmap, const void* k, RowMap kmap, const void* v,
-                         RowMap vmap, float* o, long long ldo, void* o2, const int* klen, int B, int Tq,
-                         int Tk, int heads, int dk, float scale, hipStream_t st) {
+hipError_t pfm_attention_fsmn(int dtype, const void* q, RowMap qmap, const void* k, RowMap kmap, const void* v,
+                              RowMap vmap, float* o, long long ldo, void* o2, const int* klen, int B, int Tq,
+                              int Tk, int heads, int dk, float scale, const float* fsmn_wT, bf16* fsmn_out,
+                              long long fsmn_ld, hipStream_t st) {
     if (dk != DK) return hipErrorInvalidValue;
     if (B <= 0 || Tq <= 0) return hipSuccess;
     AttnArgs a;
     a.q = q; a.qmap = qmap; a.k = k; a.kmap = kmap; a.v = v; a.vmap = vmap;
     a.o = o; a.ldo = ldo; a.o2 = o2; a.o2_dtype = DT_BF16; a.klen = klen; a.Tq = Tq; a.Tk = Tk; a.scale = scale;
+    a.fw = fsmn_wT; a.fout = fsmn_out; a.fld = fsmn_ld; a.fD = heads * DK;
+    if (fsmn_out) {   // fused FSMN: bf16 8-wave kernel only, self-attention, 16-B aligned rows
+        const char* e = getenv("PFM_ATTN_WAVES");
+        const char* pp = getenv("PFM_ATTN_PP");
+        if (dtype != DT_BF16 || Tq != Tk || (e && atoi(e) != 8) || (pp && pp[0] == '1') || fsmn_ld % 8 ||
+            vmap.ld % 8 || ((uintptr_t)fsmn_out % 16) || !fsmn_wT)
+            return hipErrorInvalidValue;
+    }
     static bool attr_done = false;
     if (!attr_done) {
         attr_done = true;
@@ -380,7 +651,9 @@ hipError_t pfm_attention(int dtype, const void* q, RowMap qmap, const void* k, R
         (void)hipFuncSetAttribute((const void*)attn_bf16_kernel<4>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   2 * STG2);
         (void)hipFuncSetAttribute((const void*)attn_bf16_kernel<8>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  2 * STG2);
+                                  LDS8);
+        (void)hipFuncSetAttribute((const void*)attn_bf16_pp_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  3 * STG2);
     }
     if (dtype == DT_F32) {
         dim3 grid((Tq + 127) / 128, heads, B), block(256);
@@ -388,9 +661,13 @@ hipError_t pfm_attention(int dtype, const void* q, RowMap qmap, const void* k, R
     } else {
         const char* e = getenv("PFM_ATTN_WAVES");
         const int nw = e ? atoi(e) : 8;
-        if (nw == 8) {
+        const char* pp = getenv("PFM_ATTN_PP");   // ping-pong 8-wave variant (A/B)
+        if (nw == 8 && pp && pp[0] == '1') {
             dim3 grid((Tq + 255) / 256, heads, B), block(512);
-            hipLaunchKernelGGL(attn_bf16_kernel<8>, grid, block, 2 * STG2, st, a);
+            hipLaunchKernelGGL(attn_bf16_pp_kernel, grid, block, 3 * STG2, st, a);
+        } else if (nw == 8) {
+            dim3 grid((Tq + 255) / 256, heads, B), block(512);
+            hipLaunchKernelGGL(attn_bf16_kernel<8>, grid, block, a.fout ? LDS8 : 2 * STG2, st, a);
         } else {
             dim3 grid((Tq + 127) / 128, heads, B), block(256);
             hipLaunchKernelGGL(attn_bf16_kernel<4>, grid, block, 2 * STG2, st, a);
@@ -398,6 +675,13 @@ hipError_t pfm_attention(int dtype, const void* q, RowMap qmap, const void* k, R
     }
     PFM_LAUNCH_CHECK();
     return hipSuccess;
+}
+
+hipError_t pfm_attention(int dtype, const void* q, RowMap qmap, const void* k, RowMap kmap, const void* v,
+                         RowMap vmap, float* o, long long ldo, void* o2, const int* klen, int B, int Tq,
+                         int Tk, int heads, int dk, float scale, hipStream_t st) {
+    return pfm_attention_fsmn(dtype, q, qmap, k, kmap, v, vmap, o, ldo, o2, klen, B, Tq, Tk, heads, dk, scale, nullptr,
+                              nullptr, 0, st);
 }
 
 int pfm_attention_lds_bytes(int dtype) { return dtype == DT_F32 ? LDS32 : 2 * STG2; }

@@ -28,6 +28,10 @@ hipError_t pfm_gemm_bf16_ln(const void* A, RowMap amap, const void* W, long long
 hipError_t pfm_attention(int dtype, const void* q, RowMap qmap, const void* k, RowMap kmap, const void* v,
                          RowMap vmap, float* o, long long ldo, void* o2, const int* klen, int B, int Tq, int Tk,
                          int heads, int dk, float scale, hipStream_t st);
+hipError_t pfm_attention_fsmn(int dtype, const void* q, RowMap qmap, const void* k, RowMap kmap, const void* v,
+                              RowMap vmap, float* o, long long ldo, void* o2, const int* klen, int B, int Tq,
+                              int Tk, int heads, int dk, float scale, const float* fsmn_wT, bf16* fsmn_out,
+                              long long fsmn_ld, hipStream_t st);
 int pfm_attention_lds_bytes(int dtype);
 hipError_t pfm_layernorm(const float* x, RowMap xmap, int M, int D, const float* g, const float* b, float eps,
                          const float* pe, int pe_T, float in_scale, void* out, RowMap omap, int odt, void* out2,
@@ -375,6 +379,13 @@ hipError_t gemm_dispatch(int dtype, const void* A, RowMap amap, const void* W, l
     return pfm_gemm(dtype, A, amap, W, ldw, M, N, K, e, st);
 }
 
+bool attn_fsmn_enabled() {   // PFM_ATTN_FSMN=0: separate FSMN kernel (A/B; parity test compares both)
+    const char* e = getenv("PFM_ATTN_FSMN");
+    const char* w = getenv("PFM_ATTN_WAVES");
+    const char* p = getenv("PFM_ATTN_PP");
+    return !(e && e[0] == '0') && !(w && atoi(w) != 8) && !(p && p[0] == '1');
+}
+
 bool gemm_ln_enabled() {   // PFM_GEMM_LN=1 enables the full-row GEMM+LayerNorm fusion (measured slower
     const char* e = getenv("PFM_GEMM_LN");   // than GEMM + standalone LN on MI355X; kept for A/B runs)
     return e && e[0] == '1';
@@ -534,6 +545,7 @@ int pfm_run(pfm_handle* h, void* stream, int mode, const float* feats, const int
         ProfScope ps(h, st, PFM_K_ATTN, fl, by);
         return pfm_attention(dtp, q, qm, k, km, v, vm, o, ldo, o2, kl, Bb, Tq, Tk, c.heads, (int)dk, qscale, st);
     };
+    const bool fuse_fsmn = fast && K == 11 && lenc == 5 && c.d_model / c.heads == 128 && attn_fsmn_enabled();
     // fast mode: 512-wide projections finish the residual sum AND the following LayerNorm in one
     // kernel (k_gemm_bf16.hip gemm_bf16_ln_kernel); exact mode keeps the unfused reference order
     const bool fuse_ln = fast && D == 512 && Fd % 32 == 0 && c.enc_blocks >= 1 && gemm_ln_enabled();
@@ -589,18 +601,27 @@ int pfm_run(pfm_handle* h, void* stream, int mode, const float* feats, const int
             else { e.out = QKV; e.out_map = rowmap_plain(3 * D); e.out_dtype = DT_F32; }
             HIP_TRY(GEMM(dt, Xn, rowmap_plain(din), W(L.wqkv), din, (int)M, 3 * D, din, e));
         }
-        // FSMN memory on v (attention.py:207-223); fast mode: bf16 in / bf16 out
-        if (fast)
+        // FSMN memory on v (attention.py:207-223) + masked MHA. Fast mode: the FSMN runs in the attention
+        // kernel's epilogue (each block owns its rows x head channels; V is L2-resident) when the shape
+        // allows (K 11, left 5); bf16 in / bf16 out either way
+        if (fast && fuse_fsmn) {
+            const double dk = c.d_model / c.heads;
+            const double fl = 4.0 * B * (double)T * T * dk * c.heads;
+            const double by = 3.0 * B * T * c.d_model * 2.0 + 2.0 * B * T * c.d_model * 2.0;
+            ProfScope ps(h, st, PFM_K_ATTN, fl, by);
+            HIP_TRY(pfm_attention_fsmn(DT_BF16, QKVb, rowmap_plain(3 * D), QKVb + D, rowmap_plain(3 * D),
+                                       QKVb + 2 * D, rowmap_plain(3 * D), nullptr, D, Ob, lens, B, T, T, c.heads,
+                                       (int)dk, qscale, P(L.fsmn), Fb, D, st));
+        } else if (fast) {
             HIP_TRY(pfm_fsmn_bf16in(QKVb + 2 * D, rowmap_plain(3 * D), lens, B, T, D, P(L.fsmn), K, lenc, nullptr,
                                     nullptr, Fb, st));
-        else
-            HIP_TRY(pfm_fsmn(QKV + 2 * D, rowmap_plain(3 * D), lens, B, T, D, P(L.fsmn), K, lenc, nullptr, Fm, nullptr,
-                             st));
-        // masked MHA
-        if (fast)
             HIP_TRY(ATTN(DT_BF16, QKVb, rowmap_plain(3 * D), QKVb + D, rowmap_plain(3 * D), QKVb + 2 * D,
                          rowmap_plain(3 * D), nullptr, D, Ob, lens, B, T, T));
-        else
+        } else {
+            HIP_TRY(pfm_fsmn(QKV + 2 * D, rowmap_plain(3 * D), lens, B, T, D, P(L.fsmn), K, lenc, nullptr, Fm, nullptr,
+                             st));
+        }
+        if (!fast)
             HIP_TRY(ATTN(DT_F32, QKV, rowmap_plain(3 * D), QKV + D, rowmap_plain(3 * D), QKV + 2 * D,
                          rowmap_plain(3 * D), O, D, nullptr, lens, B, T, T));
         {   // x = (x +) linear_out(att) + fsmn   (encoder.py:120-137: no residual when in != out)

@@ -121,18 +121,31 @@ def test_gemm_layernorm_rejects_bad_shape(dev):
         rt.op_gemm_layernorm(A, W, g, g, 1e-12)
 
 
-@pytest.mark.parametrize("dt", ["f32", "bf16"])
+@pytest.mark.parametrize("dt", ["f32", "bf16", "bf16_pp", "bf16_w4"])
 @pytest.mark.parametrize("B,Tq,Tk,lens", [(2, 500, 500, [500, 123]), (3, 37, 200, [1, 200, 64]),
-                                          (1, 130, 33, [33])])
-def test_attention(dev, dt, B, Tq, Tk, lens):
+                                          (1, 130, 33, [33]), (2, 231, 500, [500, 64]), (1, 300, 129, [0])])
+def test_attention(dev, dt, B, Tq, Tk, lens, monkeypatch):
+    """f32 / bf16 attention kernels (bf16_pp: the ping-pong 8-wave variant; bf16_w4: the 4-wave one)
+    incl. ragged and empty key lengths; klen 0 gives zero rows."""
+    if dt == "bf16_pp":
+        monkeypatch.setenv("PFM_ATTN_PP", "1")
+    if dt == "bf16_w4":
+        monkeypatch.setenv("PFM_ATTN_WAVES", "4")
+    if dt != "f32":
+        monkeypatch.setenv("PFM_ATTN_PP", "1" if dt == "bf16_pp" else "0")
     H, dk = 4, 128
     g = torch.Generator().manual_seed(B * 1000 + Tq)
     q = torch.randn(B * Tq, H * dk, generator=g)
     k = torch.randn(B * Tk, H * dk, generator=g)
     v = torch.randn(B * Tk, H * dk, generator=g)
     klen = torch.tensor(lens, dtype=torch.int32)
-    if dt == "bf16":
+    if dt != "f32":
         q, k, v = q.bfloat16(), k.bfloat16(), v.bfloat16()
+    if 0 in lens:   # empty utterance: the kernels write zeros (the reference masks everything -> nan-free 0)
+        got = rt.op_attention(q.to(dev), k.to(dev), v.to(dev), klen.to(dev), B, Tq, Tk, H, dk ** -0.5)
+        torch.cuda.synchronize()
+        assert torch.all(got.cpu() == 0)
+        return
     want = ref._attend(q.double().reshape(B, Tq, -1), k.double().reshape(B, Tk, -1), v.double().reshape(B, Tk, -1),
                        (torch.arange(Tk)[None] < klen[:, None]).double(), H).reshape(B * Tq, -1)
     got = rt.op_attention(q.to(dev), k.to(dev), v.to(dev), klen.to(dev), B, Tq, Tk, H, dk ** -0.5)
