@@ -25,9 +25,11 @@ namespace {
 typedef __attribute__((address_space(3))) void lds_void;
 typedef const __attribute__((address_space(1))) void gbl_void;
 
-template <int BM_, int BN_, int WGM_, int WGN_, int BK_, int NS_, bool PP_ = false> struct Cfg {
+template <int BM_, int BN_, int WGM_, int WGN_, int BK_, int NS_, int PP_ = 0> struct Cfg {
     static constexpr int BM = BM_, BN = BN_, WGM = WGM_, WGN = WGN_, BK = BK_, NS = NS_;
-    static constexpr bool PP = PP_;   // ping-pong: wave-row groups staggered by one barrier
+    // schedule: 0 = one barrier per K-step; 1 = ping-pong (wave-row groups staggered by one barrier,
+    // one K-step per phase); 2 = 8-phase (quadrant phases, one half-tile of DMA per phase, staggered)
+    static constexpr int PP = PP_;
     static constexpr int NW = WGM * WGN, NT = NW * 64;
     static constexpr int WTM = BM / WGM, WTN = BN / WGN;
     static constexpr int MI = WTM / 32, NI = WTN / 32;
@@ -39,7 +41,11 @@ template <int BM_, int BN_, int WGM_, int WGN_, int BK_, int NS_, bool PP_ = fal
     static constexpr int LDS = (NS * STAGE > NW * EPW) ? NS * STAGE : NW * EPW;
     static_assert(TA % (1024 * NW) == 0 && TW % (1024 * NW) == 0, "tile not divisible into DMA pieces");
     static_assert(WTN == 64, "epilogue / argmax partials assume 64-column wave tiles");
-    static_assert(!PP || (WGM == 2 && NS >= 3), "ping-pong needs two wave-row groups and >= 3 stages");
+    static_assert(PP != 1 || (WGM == 2 && NS >= 3), "ping-pong needs two wave-row groups and >= 3 stages");
+    static_assert(PP != 2 || (BM == 256 && BN == 256 && WGM == 2 && WGN == 4 && BK == 64 && NS == 2),
+                  "8-phase schedule: 256x256 tile, 2x4 waves, BK 64, two K-tile buffers");
+    static_assert(PP != 3 || (BM == 256 && BN == 256 && WGM == 2 && WGN == 4 && BK == 32 && NS == 4),
+                  "k-step phase schedule: 256x256 tile, 2x4 waves, BK 32, four K-tile buffers");
     __device__ static inline int swz(int row) { return CPR == 8 ? ((row >> 1) & 7) : ((row >> 2) & 3); }
 };
 
@@ -150,10 +156,191 @@ __global__ __launch_bounds__(C::NT) void gemm_bf16_kernel(const bf16* __restrict
     }
 
     const int nk = K / BK;
+    if constexpr (C::PP != 2 && C::PP != 3) {
 #pragma unroll
-    for (int s = 0; s < NS - 1; ++s)
-        if (s < nk) stage(s * BK, s);
-    if constexpr (C::PP) {
+        for (int s = 0; s < NS - 1; ++s)
+            if (s < nk) stage(s * BK, s);
+    }
+    if constexpr (C::PP == 3) {
+        // k-step phases (BK 32 = 2 phases per K-tile, 4 K-tile buffers): phase (j, kk) runs the 8 MFMAs
+        // of k-step kk of K-tile j over the whole 128x64 wave tile (6 fragment reads: A m-blocks 0..3,
+        // B n-blocks 0..1) and issues ONE 16-KiB operand tile of K-tile j+3 (phase kk=0: its A tile,
+        // kk=1: its W tile; 2 DMA pieces per wave). R = reads + DMA -> barrier -> M = MFMAs -> barrier;
+        // wave-row group 1 runs one barrier behind.
+        //  WAR: K-tile j+3 goes to buffer (j-1)&3, whose last reads were in the phase before (j, 0).
+        //  RAW: K-tile j+3 is first read in phase (j+3, 0); it is retired at the end of phase (j+2, 1)
+        //       with vmcnt(8) (the 4 operand tiles issued in the 4 phases after it stay in flight); G0
+        //       waits after M, G1 after R, both before the common barrier ahead of the first read.
+        const bf16* osrc[2][2];
+        {
+            const int sub = lane >> 2, slot = lane & 3;
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int row = 16 * (2 * wid + j) + sub;
+                osrc[0][j] = A + amap.off(min(m0 + row, M - 1)) + (slot ^ C::swz(row)) * 8;
+                osrc[1][j] = W + (long long)min(n0 + row, N - 1) * ldw + (slot ^ C::swz(row)) * 8;
+            }
+        }
+        auto issue = [&](int tile, int op) -> bool {
+            if (tile >= nk) return false;
+            unsigned char* base = smem + (tile & 3) * C::STAGE + op * C::TA;
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+                __builtin_amdgcn_global_load_lds((gbl_void*)(osrc[op][j] + tile * BK),
+                                                 (lds_void*)(base + (2 * wid + j) * 1024), 16, 0, 0);
+            return true;
+        };
+        auto bar = [&]() {
+            __builtin_amdgcn_sched_barrier(0);
+            __builtin_amdgcn_s_barrier();
+            __builtin_amdgcn_sched_barrier(0);
+        };
+        const int grp = wm;
+        // retire K-tile `need` (all its DMA) with `after` K-tiles' worth of later issues allowed in flight
+        auto wait_tile = [&](int need, int tj) {
+            if (need >= nk) return;
+            const int later = min(nk, tj + 4) - (need + 1);   // K-tiles issued after `need` (2 ops each)
+            if (later >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+            else if (later == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        };
+        auto phase = [&](int j, int kk) {
+            const unsigned char* sb = smem + (j & 3) * C::STAGE;
+            const int c = 2 * kk + fh;
+            bf16x8 af[MI], bfr[NI];
+#pragma unroll
+            for (int jn = 0; jn < NI; ++jn) bfr[jn] = *(const bf16x8*)(sb + woff[jn] + ((c ^ wsw[jn]) << 4));
+#pragma unroll
+            for (int i = 0; i < MI; ++i) af[i] = *(const bf16x8*)(sb + aoff[i] + ((c ^ asw[i]) << 4));
+            issue(j + 3, kk);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            if (grp == 1 && kk == 1) wait_tile(j + 1, j);
+            bar();
+            __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+            for (int i = 0; i < MI; ++i)
+#pragma unroll
+                for (int jn = 0; jn < NI; ++jn)
+                    acc[i][jn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[jn], acc[i][jn], 0, 0, 0);
+            __builtin_amdgcn_s_setprio(0);
+            if (grp == 0 && kk == 1) wait_tile(j + 1, j);
+            bar();
+        };
+        // prologue: K-tiles 0, 1, 2 in flight; K-tile 0 retired
+#pragma unroll
+        for (int t = 0; t < 3; ++t) { issue(t, 0); issue(t, 1); }
+        {
+            const int later = min(nk, 3) - 1;
+            if (later >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+            else if (later == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __syncthreads();
+        if (grp == 1) bar();
+        for (int j = 0; j < nk; ++j) {
+            phase(j, 0);
+            phase(j, 1);
+        }
+        if (grp == 0) bar();   // match group 1's stagger barrier
+    } else if constexpr (C::PP == 2) {
+        // 8-phase schedule (2 K-tiles per iteration, even tile -> buffer 0, odd -> buffer 1). Each phase
+        // computes one quadrant of the wave's 128x64 tile for one K-tile (8 MFMAs): q0 = m-blocks 0,1 x
+        // n-block 0 (reads A(m0,1) + B(n0)), q1 = m0,1 x n1 (reads B(n1)), q2 = m2,3 x n1 (reads A(m2,3)),
+        // q3 = m2,3 x n0 (reads B(n0)). Per phase: R = fragment reads + ONE half-tile (16 KiB: A rows
+        // 0-127 / 128-255, W rows 0-127 / 128-255; 2 DMA pieces per wave) -> barrier -> M = MFMAs ->
+        // barrier; wave-row group 1 runs one barrier behind (ping-pong on every SIMD).
+        //  WAR: a buffer's A halves are restaged from the phase after their last read (q2), its W
+        //       halves from the phase after q3; reads are retired (lgkmcnt 0) before the barrier ending R.
+        //  RAW: a K-tile's last half is issued >= 1 phase before the wait that retires it (end of phases
+        //       3 and 7: vmcnt(2) = only the phase's own half-tile in flight; G0 waits after M, G1
+        //       after R, both before the common barrier that precedes the first read).
+        const bf16* hsrc[4][2];
+        {
+            const int sub = lane >> 3, slot = lane & 7;
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int prow = 8 * (2 * wid + j) + sub;
+#pragma unroll
+                for (int hh = 0; hh < 2; ++hh) {
+                    const int row = hh * 128 + prow;
+                    hsrc[hh][j] = A + amap.off(min(m0 + row, M - 1)) + (slot ^ C::swz(row)) * 8;
+                    hsrc[2 + hh][j] = W + (long long)min(n0 + row, N - 1) * ldw + (slot ^ C::swz(row)) * 8;
+                }
+            }
+        }
+        auto issue = [&](int tile, int hh) -> bool {
+            if (tile >= nk) return false;
+            unsigned char* base = smem + (tile & 1) * C::STAGE + (hh >> 1) * C::TA + (hh & 1) * 16384;
+            const int k0 = tile * BK;
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+                __builtin_amdgcn_global_load_lds((gbl_void*)(hsrc[hh][j] + k0),
+                                                 (lds_void*)(base + (2 * wid + j) * 1024), 16, 0, 0);
+            return true;
+        };
+        auto bar = [&]() {
+            __builtin_amdgcn_sched_barrier(0);
+            __builtin_amdgcn_s_barrier();
+            __builtin_amdgcn_sched_barrier(0);
+        };
+        const int grp = wm;
+        bf16x8 aF[2][4], bF[4];
+        auto phase = [&](int tile, int q, int itile, int ih, bool wait_after) {
+            const unsigned char* sb = smem + (tile & 1) * C::STAGE;
+            const int i0 = (q >= 2) ? 2 : 0, jn = (q == 1 || q == 2) ? 1 : 0;
+            if (q == 0 || q == 2) {
+#pragma unroll
+                for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+                    for (int kk = 0; kk < 4; ++kk)
+                        aF[ii][kk] = *(const bf16x8*)(sb + aoff[i0 + ii] + (((2 * kk + fh) ^ asw[i0 + ii]) << 4));
+            }
+            if (q != 2) {
+#pragma unroll
+                for (int kk = 0; kk < 4; ++kk)
+                    bF[kk] = *(const bf16x8*)(sb + woff[jn] + (((2 * kk + fh) ^ wsw[jn]) << 4));
+            }
+            const bool did = issue(itile, ih);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            if (grp == 1 && wait_after) {
+                if (did) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+                else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            bar();
+            __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk)
+#pragma unroll
+                for (int ii = 0; ii < 2; ++ii)
+                    acc[i0 + ii][jn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aF[ii][kk], bF[kk], acc[i0 + ii][jn], 0,
+                                                                              0, 0);
+            __builtin_amdgcn_s_setprio(0);
+            if (grp == 0 && wait_after) {
+                if (did) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+                else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            bar();
+        };
+        // prologue: K-tile 0 whole, K-tile 1's first half (its A0) in flight
+#pragma unroll
+        for (int hh = 0; hh < 4; ++hh) issue(0, hh);
+        if (issue(1, 0)) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (grp == 1) bar();
+        for (int e = 0; e < nk; e += 2) {
+            const int o = e + 1;
+            phase(e, 0, o, 1, false);
+            phase(e, 1, o, 2, false);
+            phase(e, 2, o, 3, false);
+            phase(e, 3, e + 2, 0, true);
+            phase(o, 0, e + 2, 1, false);
+            phase(o, 1, e + 2, 2, false);
+            phase(o, 2, e + 2, 3, false);
+            phase(o, 3, o + 2, 0, true);
+        }
+        if (grp == 0) bar();   // match group 1's stagger barrier
+    } else if constexpr (C::PP == 1) {
         // Ping-pong schedule. Wave-row group g = wm (0/1; the two groups share every SIMD). Per K-tile t
         // each wave runs an R phase (issue the DMA for stage t+NS-1, read all fragments of stage t,
         // lgkmcnt(0)) and an M phase (the MFMAs), each closed by an s_barrier. Group 1 starts one
@@ -604,13 +791,15 @@ using C2 = Cfg<256, 128, 4, 2, 32, 3>;   // 72 KiB, 8 waves, wave 64x64, 2 block
 using C3 = Cfg<128, 128, 2, 2, 64, 2>;   // 64 KiB, 4 waves, wave 64x64, 2 blocks/CU
 using C4 = Cfg<128, 256, 2, 4, 32, 3>;   // 72 KiB, 8 waves, wave 64x64, 2 blocks/CU
 using C5 = Cfg<256, 256, 2, 4, 32, 4>;   // 128 KiB, BK 32 x 4 stages
-using C6 = Cfg<256, 256, 2, 4, 32, 4, true>;   // 128 KiB, BK 32 x 4 stages, ping-pong wave groups
+using C6 = Cfg<256, 256, 2, 4, 32, 4, 1>;   // 128 KiB, BK 32 x 4 stages, ping-pong wave groups
 using C7 = Cfg<256, 256, 2, 4, 32, 3>;   // persistent: 96 KiB ring + 34 KiB epilogue slices (16-row chunks)
 using C8 = Cfg<256, 256, 2, 4, 32, 4>;   // persistent: 128 KiB ring + 17 KiB slices (8-row chunks)
 using C9 = Cfg<256, 256, 2, 4, 64, 2>;   // persistent: 2 x 64 KiB ring + 17 KiB slices
 using C10 = Cfg<256, 128, 2, 2, 32, 3>;  // 4 waves (wave 128x64), 72 KiB: 2 blocks/CU -> epilogue/main-loop overlap
 using C11 = Cfg<256, 128, 2, 2, 32, 2>;  // 4 waves, 48 KiB
 using C12 = Cfg<256, 128, 2, 2, 64, 2>;  // 4 waves, 96 KiB (1 block/CU; control)
+using C13 = Cfg<256, 256, 2, 4, 64, 2, 2>;  // 8-phase schedule (K % 128 == 0)
+using C14 = Cfg<256, 256, 2, 4, 32, 4, 3>;  // k-step phases, BK 32 x 4 buffers
 
 template <class C>
 hipError_t launch(const void* A, RowMap amap, const void* W, long long ldw, int M, int N, int K, const GemmEpi& e2,
@@ -660,17 +849,25 @@ hipError_t launch_persist(const void* A, RowMap amap, const void* W, long long l
     return hipSuccess;
 }
 
-int pick_cfg(int M, int N, int K) {
+int pick_cfg(int M, int N, int K, bool amax) {
     const char* e = getenv("PFM_GEMM_CFG");   // read per launch: lets one process A/B configurations
     const int f = e ? atoi(e) : 0;
-    if (f >= 1 && f <= 12) return f;
-    // 256x256 (1 block/CU) when the grid has >= 2 tiles per CU, or when it fills one round and K is
-    // deep enough (>= 1536) to amortise the longer prologue; else 128x256 (64x64 wave tiles,
-    // 2 blocks / CU). Measured on the path shapes with tools/gemm_ab.py.
+    if (f >= 1 && f <= 14) return f;
+    // Measured on the path shapes (tools/gemm_ab.py): decoder-sized M (B*L rows) and the vocabulary
+    // projection run best on 128x256 tiles (2 blocks / CU); the encoder's wide grids (>= 2 tiles per
+    // CU, or one full round at K >= 1536) on 256x256 tiles with the 8-phase schedule (C13, needs
+    // K % 128 == 0; C1 otherwise); everything else on 128x256.
+    // In the full pipeline C13 and C1 time the same on the encoder shapes (rocprof, same box), and the
+    // grid-size-only policy measured 0.1-0.3 ms/step faster overall: it is the default;
+    // PFM_GEMM_POLICY=2 selects C13 / C4-for-decoder-shapes.
+    const char* pol = getenv("PFM_GEMM_POLICY");
+    const bool prev = !(pol && pol[0] == '2');
+    if (!prev && M <= 16384 && !amax) return 4;   // (the fused-argmax vocabulary GEMM stays on 256x256)
     const long long big = (long long)((M + 255) / 256) * ((N + 255) / 256);
     const char* kp = getenv("PFM_GEMM_KPOLICY");   // A/B switch for the K-aware rule (default on)
     const bool kaware = !(kp && kp[0] == '0');
-    return (big >= 512 || (kaware && K >= 1536 && big >= 240)) ? 1 : 4;
+    if (big >= 512 || (kaware && K >= 1536 && big >= 240)) return (!prev && K % 128 == 0) ? 13 : 1;
+    return 4;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -889,7 +1086,7 @@ hipError_t pfm_gemm_bf16_256(const void* A, RowMap amap, const void* W, long lon
         const char* rb = getenv("PFM_GEMM_RESBATCH");   // residual loads batched ahead of the stores
         e2.res_batch = !(rb && rb[0] == '0');
     }
-    switch (pick_cfg(M, N, K)) {
+    switch (pick_cfg(M, N, K, epi.amax_val != nullptr)) {
         case 2: return launch<C2>(A, amap, W, ldw, M, N, K, e2, st);
         case 3: return launch<C3>(A, amap, W, ldw, M, N, K, e2, st);
         case 4: return launch<C4>(A, amap, W, ldw, M, N, K, e2, st);
@@ -904,6 +1101,9 @@ hipError_t pfm_gemm_bf16_256(const void* A, RowMap amap, const void* W, long lon
         case 10: return launch<C10>(A, amap, W, ldw, M, N, K, e2, st);
         case 11: return launch<C11>(A, amap, W, ldw, M, N, K, e2, st);
         case 12: return launch<C12>(A, amap, W, ldw, M, N, K, e2, st);
+        case 13: if (K % 128 == 0) return launch<C13>(A, amap, W, ldw, M, N, K, e2, st);
+                 return launch<C1>(A, amap, W, ldw, M, N, K, e2, st);
+        case 14: return launch<C14>(A, amap, W, ldw, M, N, K, e2, st);
         default: return launch<C1>(A, amap, W, ldw, M, N, K, e2, st);
     }
 }

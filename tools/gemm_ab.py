@@ -6,10 +6,11 @@ import numpy as np
 import torch
 from funasr_amd import runtime as rt
 
-SHAPES = [("qkv", 32000, 1536, 512), ("out+res", 32000, 512, 512), ("ffn1", 32000, 2048, 512),
+SHAPES_ALL = [("qkv", 32000, 1536, 512), ("out+res", 32000, 512, 512), ("ffn1", 32000, 2048, 512),
           ("ffn2+res", 32000, 512, 2048), ("conv", 32000, 512, 1536), ("kv_all", 32000, 16384, 512),
           ("dffn1", 14784, 2048, 512), ("dffn2+res", 14784, 512, 2048), ("dq", 14784, 512, 512),
           ("vocab", 14784, 8404, 512), ("sq4k", 4096, 4096, 4096)]
+SHAPES = [x for x in SHAPES_ALL if not os.environ.get("AB_SHAPES") or x[0] in os.environ["AB_SHAPES"].split(",")]
 # tokens: "<cfg>" or "<cfg>:VAR=VAL" (extra env for that arm, e.g. 4:PFM_GEMM_ST16=0)
 CFGS = (sys.argv[1] if len(sys.argv) > 1 else "1,2,3,4,5").split(",")
 
