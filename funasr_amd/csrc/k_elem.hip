@@ -424,7 +424,7 @@ __global__ __launch_bounds__(256) void cif_alpha_kernel(const float* __restrict_
 // Grid (D/64 channel slabs, B): one wave per (slab, utterance), one channel per lane. Every wave
 // recomputes the (uniform) fire schedule, so each channel's operations and their order are those of
 // the sequential reference loop; h rows are prefetched CIF_PF frames ahead of the recurrence.
-constexpr int CIF_PF = 16;
+constexpr int CIF_PF = 16;   // frames per batch; the next batch is in flight while one is scanned
 __global__ __launch_bounds__(64) void cif_fire_kernel(const float* __restrict__ alphas, const float* __restrict__ h,
                                                       RowMap hmap, int T, int D, int Lcap,
                                                       float* __restrict__ emb, float* __restrict__ peaks,
@@ -438,14 +438,15 @@ __global__ __launch_bounds__(64) void cif_fire_kernel(const float* __restrict__ 
     double ph = 0.0, P = 0.0;
     float pph = 0.f, prh = 0.f, prevfl = 0.f;
     int k = 0;
-    for (int t0 = 0; t0 <= T; t0 += CIF_PF) {
-        float hv[CIF_PF], av[CIF_PF];
+    auto fetch = [&](int t0, float (&hv)[CIF_PF], float (&av)[CIF_PF]) {
 #pragma unroll
         for (int i = 0; i < CIF_PF; ++i) {
             const int t = min(t0 + i, T);
             av[i] = al[t];
             hv[i] = h[hmap.off((long long)b * (T + 1) + t) + cc];
         }
+    };
+    auto scan = [&](int t0, const float (&hv)[CIF_PF], const float (&av)[CIF_PF]) {
 #pragma unroll
         for (int i = 0; i < CIF_PF; ++i) {
             const int t = t0 + i;
@@ -469,6 +470,16 @@ __global__ __launch_bounds__(64) void cif_fire_kernel(const float* __restrict__ 
                 ++k;
             }
         }
+    };
+    // two named batches: batch n+1 is loading while batch n is scanned (arrays stay in registers)
+    float hA[CIF_PF], aA[CIF_PF], hB[CIF_PF], aB[CIF_PF];
+    fetch(0, hA, aA);
+    for (int t0 = 0; t0 <= T; t0 += 2 * CIF_PF) {
+        if (t0 + CIF_PF <= T) fetch(t0 + CIF_PF, hB, aB);
+        scan(t0, hA, aA);
+        if (t0 + CIF_PF > T) break;
+        if (t0 + 2 * CIF_PF <= T) fetch(t0 + 2 * CIF_PF, hA, aA);
+        scan(t0 + CIF_PF, hB, aB);
     }
     if (act)
         for (int kk = k; kk < Lcap; ++kk) emb[((long long)b * Lcap + kk) * D + c] = 0.f;
