@@ -123,6 +123,9 @@ struct pfm_handle {
     bool fb_tab_ready = false;
     int32_t* host_ntok = nullptr;
     int host_ntok_cap = 0;
+    // side stream: the decoder's memory K|V projection overlaps the predictor / CIF / token-count sync
+    hipStream_t st2 = nullptr;
+    hipEvent_t ev_enc = nullptr, ev_kv = nullptr;
     // live profiling: event pairs per launch, per kernel class
     struct ProfRec { hipEvent_t a, b; int kc; double flops, bytes; };
     bool prof_on = false;
@@ -386,6 +389,11 @@ bool attn_fsmn_enabled() {   // PFM_ATTN_FSMN=0: separate FSMN kernel (A/B; pari
     return !(e && e[0] == '0') && !(w && atoi(w) != 8) && !(p && p[0] == '1');
 }
 
+bool kv_overlap_enabled() {   // PFM_KV_OVERLAP=0: memory K|V projection in-line on the caller's stream
+    const char* e = getenv("PFM_KV_OVERLAP");
+    return !(e && e[0] == '0');
+}
+
 bool gemm_ln_enabled() {   // PFM_GEMM_LN=1 enables the full-row GEMM+LayerNorm fusion (measured slower
     const char* e = getenv("PFM_GEMM_LN");   // than GEMM + standalone LN on MI355X; kept for A/B runs)
     return e && e[0] == '1';
@@ -457,6 +465,9 @@ void pfm_destroy(pfm_handle* h) {
     (void)hipSetDevice(h->device);
     (void)hipDeviceSynchronize();
     for (auto e : h->ev_pool) (void)hipEventDestroy(e);
+    if (h->ev_enc) (void)hipEventDestroy(h->ev_enc);
+    if (h->ev_kv) (void)hipEventDestroy(h->ev_kv);
+    if (h->st2) (void)hipStreamDestroy(h->st2);
     if (h->host_ntok) (void)hipHostFree(h->host_ntok);
     delete h;
 }
@@ -669,6 +680,32 @@ int pfm_run(pfm_handle* h, void* stream, int mode, const float* feats, const int
     if (enc_out)
         HIP_TRY(hipMemcpy2DAsync(enc_out, (size_t)T * D * 4, encp + D, (size_t)(T + 2) * D * 4, (size_t)T * D * 4, B,
                                  hipMemcpyDeviceToDevice, st));
+    // memory K|V for all decoder layers: [B*T, nL*2D] = enc . Wkv_all^T + b. It needs only the encoder
+    // output, so it runs on the side stream while the predictor, the CIF and the host's token-count
+    // sync proceed; the caller's stream joins it before the first cross-attention (or any return).
+    void* KV = h->KV.p;
+    auto launch_kv = [&](hipStream_t s) -> hipError_t {
+        GemmEpi e = epi_default();
+        e.bias = P(h->bkv_all);
+        e.out = KV; e.out_map = rowmap_plain(nkv); e.out_dtype = dt;
+        const void* A = fast ? (const void*)(encpb + D) : (const void*)(encp + D);
+        const double fl = 2.0 * M * nkv * D;
+        const double by = ((double)M * D + (double)nkv * D) * es + (double)M * nkv * es;
+        ProfScope ps(h, s, PFM_K_GEMM, fl, by);
+        return gemm_dispatch(dt, A, encmap, W(h->wkv_all), D, (int)M, nkv, D, e, s);
+    };
+    const bool kv_async = kv_overlap_enabled() && c.dec_blocks > 0;
+    if (kv_async) {
+        if (!h->st2) {
+            HIP_TRY(hipStreamCreateWithFlags(&h->st2, hipStreamNonBlocking));
+            HIP_TRY(hipEventCreateWithFlags(&h->ev_enc, hipEventDisableTiming));
+            HIP_TRY(hipEventCreateWithFlags(&h->ev_kv, hipEventDisableTiming));
+        }
+        HIP_TRY(hipEventRecord(h->ev_enc, st));
+        HIP_TRY(hipStreamWaitEvent(h->st2, h->ev_enc, 0));
+        HIP_TRY(launch_kv(h->st2));
+        HIP_TRY(hipEventRecord(h->ev_kv, h->st2));
+    }
 
     // ---------------- predictor (cif_predictor.py:202-253) ----------------
     {   // relu(conv1d(k=3, pad 1)) as a GEMM over 3 adjacent rows of the padded layout (K = 3D)
@@ -695,7 +732,10 @@ int pfm_run(pfm_handle* h, void* stream, int mode, const float* feats, const int
     for (int b = 0; b < B; ++b) L = std::max(L, (int)h->host_ntok[b]);
     L = std::min(L, Lc);   // ntok <= fires <= T+1 frames (+ rounding); decoder never exceeds the CIF rows
     if (L_cap > 0) HIP_TRY(pfm_fill_i32(tokens, (long long)B * L_cap, -1, st));
-    if (L < 1 || c.dec_blocks < 0) return PFM_OK;   // model.py:514-515: nothing to decode
+    if (L < 1 || c.dec_blocks < 0) {   // model.py:514-515: nothing to decode
+        if (kv_async) HIP_TRY(hipStreamWaitEvent(st, h->ev_kv, 0));   // the side stream still reads encp
+        return PFM_OK;
+    }
 
     // ---------------- decoder (paraformer/decoder.py:359-411) ----------------
     const long long Ml = (long long)B * L;
@@ -708,17 +748,10 @@ int pfm_run(pfm_handle* h, void* stream, int mode, const float* feats, const int
     void* Qd = h->Qd.p;
     float* Od = h->Od.as<float>();
     bf16* Odb = h->Odb.as<bf16>();
-    void* KV = h->KV.p;
     // compact CIF embeddings [B][T+1][D] -> decoder rows [B][L][D] (acoustic_embeds[:, :L])
     HIP_TRY(hipMemcpy2DAsync(Xd, (size_t)L * D * 4, h->emb.p, (size_t)Lc * D * 4, (size_t)L * D * 4, B,
                              hipMemcpyDeviceToDevice, st));
-    {   // memory K|V for all decoder layers: [B*T, nL*2D] = enc . Wkv_all^T + b
-        GemmEpi e = epi_default();
-        e.bias = P(h->bkv_all);
-        e.out = KV; e.out_map = rowmap_plain(nkv); e.out_dtype = dt;
-        const void* A = fast ? (const void*)(encpb + D) : (const void*)(encp + D);
-        HIP_TRY(GEMM(dt, A, encmap, W(h->wkv_all), D, (int)M, nkv, D, e));
-    }
+    if (!kv_async) HIP_TRY(launch_kv(st));
     auto ffn = [&](const float* x, bool xdn_ready, size_t lng, size_t lnb, size_t w1, size_t b1, size_t fng,
                    size_t fnb, size_t w2, float* out, size_t pg, size_t pb, void* pout, int pdt) -> int {
         // out = W2 . LN_F(relu(W1 . LN(x) + b1)); pout = LN_P(out)   (sanm/positionwise_feed_forward.py:26-33)
@@ -759,6 +792,7 @@ int pfm_run(pfm_handle* h, void* stream, int mode, const float* feats, const int
             e.out = Qd; e.out_map = rowmap_plain(D); e.out_dtype = dt;
             HIP_TRY(GEMM(dt, Xdn, rowmap_plain(D), W(Lr.wq), D, (int)Ml, D, D, e));
         }
+        if (l == 0 && kv_async) HIP_TRY(hipStreamWaitEvent(st, h->ev_kv, 0));   // join the side stream
         {
             const size_t es = fast ? 2 : 4;
             const char* kvb = (const char*)KV + (size_t)l * 2 * D * es;
