@@ -19,8 +19,8 @@ constexpr int LN_MAXV = 8;   // float4 per lane -> D <= 2048
 // columns per 512-column slab (two float4 loads, one 16-B store), R rows per wave with every row
 // load and gamma / beta issued before the first store (vmcnt retires in order, so a load behind a
 // store waits for it). Same f64 statistics as layernorm_kernel.
-template <int VPL, int R>
-__global__ __launch_bounds__(256) void layernorm_v8_kernel(const float* __restrict__ x, RowMap xmap, int M,
+template <int VPL, int R, typename TIN = float>   // TIN bf16: fast-mode FFN hidden (one 16-B load per 8 columns)
+__global__ __launch_bounds__(256) void layernorm_v8_kernel(const TIN* __restrict__ x, RowMap xmap, int M,
                                                            const float* __restrict__ g, const float* __restrict__ bta,
                                                            float eps, void* out, RowMap omap, int odt, void* out2,
                                                            RowMap o2map, int o2dt) {
@@ -31,12 +31,18 @@ __global__ __launch_bounds__(256) void layernorm_v8_kernel(const float* __restri
     float4 v[R][VPL][2];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-        const float* xr = x + xmap.off(min(row0 + r, M - 1));
+        const TIN* xr = x + xmap.off(min(row0 + r, M - 1));
 #pragma unroll
         for (int i = 0; i < VPL; ++i) {
             const int c = i * 512 + lane * 8;
-            v[r][i][0] = *(const float4*)(xr + c);
-            v[r][i][1] = *(const float4*)(xr + c + 4);
+            if constexpr (sizeof(TIN) == 4) {
+                v[r][i][0] = *(const float4*)(xr + c);
+                v[r][i][1] = *(const float4*)(xr + c + 4);
+            } else {
+                const bf16x8 t = *(const bf16x8*)(xr + c);
+                v[r][i][0] = make_float4(bf2f(t[0]), bf2f(t[1]), bf2f(t[2]), bf2f(t[3]));
+                v[r][i][1] = make_float4(bf2f(t[4]), bf2f(t[5]), bf2f(t[6]), bf2f(t[7]));
+            }
         }
     }
     float4 gg[VPL][2], bb[VPL][2];
@@ -571,6 +577,27 @@ hipError_t pfm_layernorm(const float* x, RowMap xmap, int M, int D, const float*
     }
     hipLaunchKernelGGL(layernorm_kernel, dim3((M + 3) / 4), dim3(256), 0, st, x, xmap, M, D, g, b, eps, pe,
                        pe_T > 0 ? pe_T : 1, in_scale, out, omap, odt, out2, o2map, o2dt);
+    PFM_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+// bf16-input LayerNorm (fast mode; D in {512, 1024, 2048}, 16-B aligned rows)
+hipError_t pfm_layernorm_bf16in(const bf16* x, RowMap xmap, int M, int D, const float* g, const float* b, float eps,
+                                void* out, RowMap omap, int odt, hipStream_t st) {
+    if (M <= 0) return hipSuccess;
+    if (!(D == 512 || D == 1024 || D == 2048) || xmap.ld % 8 || (xmap.rows_per_seg > 0 && xmap.seg_stride % 8) ||
+        ((uintptr_t)x % 16) || ((uintptr_t)out % 16) || omap.ld % 8)
+        return hipErrorInvalidValue;
+    const unsigned blocks2 = (unsigned)(((M + 1) / 2 + 3) / 4), blocks1 = (unsigned)((M + 3) / 4);
+    if (D == 512)
+        hipLaunchKernelGGL((layernorm_v8_kernel<1, 2, bf16>), dim3(blocks2), dim3(256), 0, st, x, xmap, M, g, b, eps, out,
+                           omap, odt, nullptr, rowmap_plain(0), 0);
+    else if (D == 1024)
+        hipLaunchKernelGGL((layernorm_v8_kernel<2, 2, bf16>), dim3(blocks2), dim3(256), 0, st, x, xmap, M, g, b, eps, out,
+                           omap, odt, nullptr, rowmap_plain(0), 0);
+    else
+        hipLaunchKernelGGL((layernorm_v8_kernel<4, 1, bf16>), dim3(blocks1), dim3(256), 0, st, x, xmap, M, g, b, eps, out,
+                           omap, odt, nullptr, rowmap_plain(0), 0);
     PFM_LAUNCH_CHECK();
     return hipSuccess;
 }

@@ -36,6 +36,8 @@ int pfm_attention_lds_bytes(int dtype);
 hipError_t pfm_layernorm(const float* x, RowMap xmap, int M, int D, const float* g, const float* b, float eps,
                          const float* pe, int pe_T, float in_scale, void* out, RowMap omap, int odt, void* out2,
                          RowMap o2map, int o2dt, hipStream_t st);
+hipError_t pfm_layernorm_bf16in(const bf16* x, RowMap xmap, int M, int D, const float* g, const float* b, float eps,
+                                void* out, RowMap omap, int odt, hipStream_t st);
 hipError_t pfm_fsmn(const float* v, RowMap vmap, const int* len, int B, int T, int D, const float* w, int K,
                     int left, const float* res, float* out, bf16* out_bf, hipStream_t st);
 hipError_t pfm_fsmn_bf16in(const bf16* v, RowMap vmap, const int* len, int B, int T, int D, const float* wT, int K,
@@ -760,10 +762,14 @@ int pfm_run(pfm_handle* h, void* stream, int mode, const float* feats, const int
                                   rowmap_plain(D), dt, nullptr, plain, 0, st));
         GemmEpi e = epi_default();
         e.bias = P(b1); e.relu = 1;
-        e.out = Hd; e.out_map = rowmap_plain(Fd); e.out_dtype = DT_F32;
+        e.out = Hd; e.out_map = rowmap_plain(Fd); e.out_dtype = fast ? DT_BF16 : DT_F32;   // fast: bf16 hidden
         HIP_TRY(GEMM(dt, Xdn, rowmap_plain(D), W(w1), D, (int)Ml, Fd, D, e));
-        HIP_TRY(pfm_layernorm(Hd, rowmap_plain(Fd), (int)Ml, Fd, P(fng), P(fnb), c.ln_eps, nullptr, 0, 1.f, Hdn,
-                              rowmap_plain(Fd), dt, nullptr, plain, 0, st));
+        if (fast)
+            HIP_TRY(pfm_layernorm_bf16in((const bf16*)Hd, rowmap_plain(Fd), (int)Ml, Fd, P(fng), P(fnb), c.ln_eps, Hdn,
+                                         rowmap_plain(Fd), dt, st));
+        else
+            HIP_TRY(pfm_layernorm(Hd, rowmap_plain(Fd), (int)Ml, Fd, P(fng), P(fnb), c.ln_eps, nullptr, 0, 1.f, Hdn,
+                                  rowmap_plain(Fd), dt, nullptr, plain, 0, st));
         GemmEpi e2 = epi_default();
         if (fuse_ln) {   // out itself is dead; only LN_P(out) is consumed
             HIP_TRY(GEMM_LN(Hdn, rowmap_plain(Fd), W(w2), Fd, (int)Ml, Fd, e2, pg, pb, pout, rowmap_plain(D), pdt,
@@ -921,6 +927,13 @@ int pfm_op_layernorm(void* stream, const float* x, const float* g, const float* 
 int pfm_op_fsmn(void* stream, const float* v, const int32_t* len, const float* w, const float* res, float* out,
                 int B, int T, int D, int K, int left) {
     HIP_TRY(pfm_fsmn(v, rowmap_plain(D), len, B, T, D, w, K, left, res, out, nullptr, (hipStream_t)stream));
+    return PFM_OK;
+}
+
+int pfm_op_layernorm_bf16(void* stream, const void* x, const float* g, const float* b, float* out, int M, int D,
+                          float eps) {
+    HIP_TRY(pfm_layernorm_bf16in((const bf16*)x, rowmap_plain(D), M, D, g, b, eps, out, rowmap_plain(D), DT_F32,
+                                 (hipStream_t)stream));
     return PFM_OK;
 }
 

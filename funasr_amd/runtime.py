@@ -24,7 +24,7 @@ MODES = {"exact": MODE_EXACT, "fp32": MODE_EXACT, "fast": MODE_FAST, "bf16": MOD
 # every symbol include/pfm.h declares (checked by tests/test_abi.py)
 ABI_SYMBOLS = ("pfm_config_default", "pfm_create", "pfm_set_weight", "pfm_missing_weights", "pfm_reserve",
                "pfm_run", "pfm_fbank", "pfm_lfr_frames", "pfm_last_error", "pfm_destroy", "pfm_op_gemm",
-               "pfm_op_attention", "pfm_op_layernorm", "pfm_op_fsmn", "pfm_op_cif", "pfm_profile", "pfm_op_gemm_layernorm", "pfm_op_fsmn_bf16",
+               "pfm_op_attention", "pfm_op_layernorm", "pfm_op_fsmn", "pfm_op_cif", "pfm_profile", "pfm_op_gemm_layernorm", "pfm_op_fsmn_bf16", "pfm_op_layernorm_bf16",
                "pfm_profile_read")
 
 
@@ -80,6 +80,7 @@ def load_library(path: Optional[str] = None) -> ctypes.CDLL:
     lib.pfm_op_layernorm.argtypes = [vp, f32p, f32p, f32p, f32p, i32, i32, ctypes.c_float]
     lib.pfm_op_fsmn.argtypes = [vp, f32p, i32p, f32p, f32p, f32p, i32, i32, i32, i32, i32]
     lib.pfm_op_cif.argtypes = [vp, f32p, f32p, f32p, f32p, i32p, i32p, i32, i32, i32, i32]
+    lib.pfm_op_layernorm_bf16.argtypes = [vp, vp, f32p, f32p, f32p, i32, i32, ctypes.c_float]
     lib.pfm_op_fsmn_bf16.argtypes = [vp, vp, i32p, f32p, vp, i32, i32, i32, i32, i32]
     lib.pfm_op_gemm_layernorm.argtypes = [vp, vp, vp, f32p, f32p, f32p, f32p, f32p, ctypes.c_float, f32p, i32, i32,
                                           i32]
@@ -263,6 +264,17 @@ def op_fsmn(v, lens, w, B, T, left, res=None):
     check(lib.pfm_op_fsmn(_stream_ptr(torch, v.device), _ptr(v), _ptr(lens.to(torch.int32)),
                           _ptr(w.reshape(D, K).t().contiguous()), _ptr(res), _ptr(out), B, T, D, K, left),
           "pfm_op_fsmn")
+    return out
+
+
+def op_layernorm_bf16(x, g, b, eps):
+    """LayerNorm of bf16 rows -> f32 (fast-mode FFN-hidden kernel)."""
+    import torch
+    lib = load_library()
+    M, D = x.shape
+    out = torch.empty((M, D), dtype=torch.float32, device=x.device)
+    check(lib.pfm_op_layernorm_bf16(_stream_ptr(torch, x.device), _ptr(x.contiguous()), _ptr(g), _ptr(b), _ptr(out),
+                                    M, D, ctypes.c_float(eps)), "pfm_op_layernorm_bf16")
     return out
 
 

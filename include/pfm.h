@@ -169,6 +169,10 @@ int pfm_op_layernorm(void* stream, const float* x, const float* gamma, const flo
 int pfm_op_fsmn(void* stream, const float* v, const int32_t* len, const float* w,
                 const float* res, float* out, int B, int T, int D, int K, int left);
 
+/* LayerNorm rows of bf16 x [M, D] (D in 512/1024/2048) -> out [M, D] f32 (fast-mode FFN hidden). */
+int pfm_op_layernorm_bf16(void* stream, const void* x, const float* gamma, const float* beta, float* out,
+                          int M, int D, float eps);
+
 /* FSMN memory block on bf16 input v [B*T, D] -> bf16 out (fast-mode encoder form: no residual). */
 int pfm_op_fsmn_bf16(void* stream, const void* v, const int32_t* len, const float* w, void* out, int B,
                      int T, int D, int K, int left);

@@ -166,6 +166,19 @@ def test_layernorm(dev, M, D):
     assert (got.double().cpu() - want).abs().max().item() < 2e-6
 
 
+@pytest.mark.parametrize("M,D", [(1, 512), (77, 2048), (14784, 2048), (5, 1024)])
+def test_layernorm_bf16_input(dev, M, D):
+    """bf16-input LayerNorm (decoder FFN hidden in fast mode) vs fp64 on the same bf16 values."""
+    g = torch.Generator().manual_seed(D + M)
+    x = (torch.randn(M, D, generator=g) * 3 + 1).bfloat16()
+    gm = 1 + 0.1 * torch.randn(D, generator=g)
+    bt = 0.1 * torch.randn(D, generator=g)
+    want = torch.nn.functional.layer_norm(x.double(), (D,), gm.double(), bt.double(), 1e-12)
+    got = rt.op_layernorm_bf16(x.to(dev), gm.to(dev), bt.to(dev), 1e-12)
+    torch.cuda.synchronize()
+    assert (got.double().cpu() - want).abs().max().item() < 2e-6
+
+
 @pytest.mark.parametrize("B,T,lens,left", [(2, 50, [50, 17], 5), (1, 9, [9], 5), (3, 40, [1, 40, 11], 7)])
 def test_fsmn(dev, B, T, lens, left):
     D, K = 512, 11
