@@ -786,9 +786,15 @@ int pfm_run(pfm_handle* h, void* stream, int mode, const float* feats, const int
     for (int l = 0; l < c.dec_blocks; ++l) {
         const DecLayer& Lr = h->dec[l];
         // t = FFN(LN1(x)); x = x + FSMN(LN2(t))   (decoder.py:97-107)
-        rc = ffn(Xd, xdn_ready, Lr.n1g, Lr.n1b, Lr.w1, Lr.b1, Lr.ng, Lr.nb, Lr.w2, Td, Lr.n2g, Lr.n2b, Tdn, DT_F32);
+        // fast mode: LN2(t) in bf16 feeding the bf16-input FSMN (x += FSMN(LN2(t)) stays f32)
+        rc = ffn(Xd, xdn_ready, Lr.n1g, Lr.n1b, Lr.w1, Lr.b1, Lr.ng, Lr.nb, Lr.w2, Td, Lr.n2g, Lr.n2b, Tdn,
+                 fast ? DT_BF16 : DT_F32);
         if (rc) return rc;
-        HIP_TRY(pfm_fsmn(Tdn, rowmap_plain(D), ntok, B, L, D, P(Lr.fsmn), K, ldec, Xd, Xd, nullptr, st));
+        if (fast)
+            HIP_TRY(pfm_fsmn_bf16in((const bf16*)Tdn, rowmap_plain(D), ntok, B, L, D, P(Lr.fsmn), K, ldec, Xd, Xd,
+                                    nullptr, st));
+        else
+            HIP_TRY(pfm_fsmn(Tdn, rowmap_plain(D), ntok, B, L, D, P(Lr.fsmn), K, ldec, Xd, Xd, nullptr, st));
         // x = x + CrossAtt(LN3(x), memory)   (decoder.py:109-119)
         HIP_TRY(pfm_layernorm(Xd, rowmap_plain(D), (int)Ml, D, P(Lr.n3g), P(Lr.n3b), c.ln_eps, nullptr, 0, 1.f, Xdn,
                               rowmap_plain(D), dt, nullptr, plain, 0, st));
