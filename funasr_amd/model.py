@@ -24,6 +24,7 @@ from .config import ParaformerConfig
 from .register import tables
 from .runtime import PfmEngine, PfmError
 from .text import sentence_postprocess
+from .timestamp import ts_prediction_lfr6_standard
 from .weights import param_layout
 
 
@@ -105,8 +106,6 @@ class Paraformer(torch.nn.Module):
                   **kwargs):
         if kwargs.get("decoding_ctc_weight", 0.0) > 1e-5 or kwargs.get("lm_weight", 0.0) > 1e-5:
             raise NotImplementedError("CTC / LM beam search is not on the HIP Paraformer path (greedy only)")
-        if kwargs.get("pred_timestamp", False):
-            raise NotImplementedError("timestamp prediction is a next-row item (SURVEY §8f)")
         eng = self.engine()
         mode = kwargs.get("mode", self.mode)
         meta = {}
@@ -128,9 +127,12 @@ class Paraformer(torch.nn.Module):
             meta["load_data"] = "0.000"
             meta["extract_feat"] = f"{t2 - t1:0.3f}"
             meta["batch_data_time"] = float(lens.sum().item()) * frontend.frame_shift * frontend.lfr_n / 1000
-        r = eng.run(speech, lens, mode=mode)
+        pred_ts = bool(kwargs.get("pred_timestamp", False))
+        r = eng.run(speech, lens, mode=mode, want_alphas=pred_ts)
         toks = r["tokens"].cpu().numpy()           # one device->host copy for the whole batch
         ntok = r["ntok"].cpu().numpy()
+        if pred_ts:   # CIF outputs for ts_prediction_lfr6_standard (paraformer/model.py:572-582)
+            peaks_h, alphas_h = r["peaks"].cpu(), r["alphas"].cpu()
         b = toks.shape[0]
         if key is None:
             key = [f"utt{i}" for i in range(b)]
@@ -144,8 +146,16 @@ class Paraformer(torch.nn.Module):
             ids = toks[i, :n].tolist() if n <= toks.shape[1] else []
             ids = [t for t in ids if t not in (self.eos, self.sos, self.blank_id)]
             if tokenizer is not None:
-                text, _ = sentence_postprocess(tokenizer.ids2tokens(ids))
-                results.append({"key": key[i], "text": text})
+                toks_i = tokenizer.ids2tokens(ids)
+                if pred_ts:
+                    # the reference passes the CIF peaks as `us_alphas` and the alphas as `us_peaks`
+                    _, ts = ts_prediction_lfr6_standard(peaks_h[i], alphas_h[i], list(toks_i),
+                                                        vad_offset=kwargs.get("begin_time", 0), upsample_rate=1)
+                    text, ts_pp, _ = sentence_postprocess(toks_i, ts)
+                    results.append({"key": key[i], "text": text, "timestamp": ts_pp})
+                else:
+                    text, _ = sentence_postprocess(toks_i)
+                    results.append({"key": key[i], "text": text})
             else:
                 results.append({"key": key[i], "token_int": ids})
         return results, meta

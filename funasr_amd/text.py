@@ -11,7 +11,7 @@ from __future__ import annotations
 
 import json
 import os
-from typing import Iterable, List, Sequence, Union
+from typing import Optional, Iterable, List, Sequence, Union
 
 _SPECIAL = ("<s>", "</s>", "<unk>", "<OOV>")
 
@@ -108,42 +108,138 @@ def _join_abbreviations(words: List[str]) -> List[str]:
     return out
 
 
-def sentence_postprocess(words: Sequence[Union[str, bytes]]):
-    """Token list -> (sentence, word list); Chinese chars joined, BPE '@@' pieces merged,
-    alphabetic words space-separated, single-letter runs joined as abbreviations."""
+def _abbreviations_with_spans(words: List[str], spans: List[List[int]]):
+    """Abbreviation merge carrying token time spans (postprocess_utils.py:56-141): a run of single
+    ASCII letters separated by ' ' becomes one upper-case word spanning first start -> last end;
+    other non-space words keep their own span (indexed by their position among non-space words)."""
+    n = len(words)
+    starts, ends = [], []
+    last = -1
+    for i in range(n):                                   # pass 1: runs (reference detection order)
+        if i <= last:
+            continue
+        if _single_letter(words[i]) and i + 2 < n and words[i + 1] == " " and _single_letter(words[i + 2]):
+            starts.append(i)
+            j = i + 2
+            ends.append(j)
+            while True:
+                j += 1
+                if j < n and words[j] == " ":
+                    j += 1
+                    if j < n and _single_letter(words[j]):
+                        ends[-1] = j
+                        last = j
+                    else:
+                        break
+                else:
+                    break
+    before = []                                          # non-space words before position i
+    cnt = 0
+    for w in words:
+        before.append(cnt)
+        if w != " ":
+            cnt += 1
+    out, out_spans = [], []
+    last = -1
+    begin = end = None
+    i = 0
+    while i < n:
+        if i <= last:
+            i += 1
+            continue
+        if i in starts:
+            begin = spans[before[i]][0]
+            word = words[i].upper()
+            i += 1
+            while i < n:
+                if i in ends:
+                    word += words[i].upper()
+                    last = i
+                    break
+                if words[i].encode("utf-8").isalpha():
+                    word += words[i].upper()
+                i += 1
+            out.append(word)
+            if i < n and before[i] < len(spans):
+                end = spans[before[i]][1]
+                out_spans.append([begin, end])
+        else:
+            out.append(words[i])
+            if before[i] < len(spans) and words[i] != " ":
+                begin, end = spans[before[i]]
+                out_spans.append([begin, end])
+        i += 1
+    return out, out_spans
+
+
+def sentence_postprocess(words: Sequence[Union[str, bytes]], time_stamp: Optional[List[List[int]]] = None):
+    """Token list -> (sentence, word list); with `time_stamp` (one [start, end] per token) ->
+    (sentence, word spans, word list), words then joined by spaces (postprocess_utils.py:144-251).
+    Chinese chars joined, BPE '@@' pieces merged, alphabetic words space-separated, single-letter
+    runs joined as upper-case abbreviations."""
     mid = []
     for w in words:
         w = w if isinstance(w, str) else w.decode("utf-8")
         if w not in _SPECIAL:
             mid.append(w)
+    ts = time_stamp is not None
     out: List[str] = []
+    spans: List[List[int]] = []
     if _all_zh(mid):
         out = [w.replace(" ", "") for w in mid]
+        if ts:
+            spans = time_stamp
     elif _all_alpha(mid):
-        piece = ""
-        for w in mid:
+        piece, open_span = "", True
+        begin = end = None
+        for i, w in enumerate(mid):
+            if ts and open_span:
+                begin, end = time_stamp[i][0], time_stamp[i][1]
             if "@@" in w:
                 piece += w.replace("@@", "")
+                if ts:
+                    open_span, end = False, time_stamp[i][1]
             else:
                 out += [piece + w, " "]
                 piece = ""
+                if ts:
+                    open_span, end = True, time_stamp[i][1]
+                    spans.append([begin, end])
+                    begin = end
     else:
-        piece, after_alpha = "", False
-        for w in mid:
+        piece, after_alpha, open_span = "", False, True
+        begin = end = -1
+        for i, w in enumerate(mid):
+            if ts and open_span:
+                begin, end = time_stamp[i][0], time_stamp[i][1]
             if _all_zh(w):
                 if after_alpha:
                     out.pop()
                 out.append(w)
                 after_alpha = False
+                if ts:
+                    open_span = True
+                    spans.append([begin, end])
+                    begin = end
             elif "@@" in w:
                 piece += w.replace("@@", "")
                 after_alpha = False
+                if ts:
+                    open_span, end = False, time_stamp[i][1]
             elif _all_alpha(w):
                 out += [piece + w, " "]
                 piece = ""
                 after_alpha = True
+                if ts:
+                    open_span, end = True, time_stamp[i][1]
+                    spans.append([begin, end])
+                    begin = end
             else:
                 out.append(w)
+    if ts:
+        out, spans = _abbreviations_with_spans(out, spans)
+        real = [w for w in out if w != " "]
+        return " ".join(real).strip(), spans, real
     out = _join_abbreviations(out)
     real = [w for w in out if w != " "]
     return "".join(out).strip(), real

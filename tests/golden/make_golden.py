@@ -208,8 +208,74 @@ def save_postprocess():
     print("postprocess cases", len(out))
 
 
-if __name__ == "__main__":
+def save_timestamps():
+    """Reference ts_prediction_lfr6_standard + sentence_postprocess(words, time_stamp) on seeded
+    synthetic CIF weights (both fire-search branches, '</s>', VAD offset, upsample rates)."""
+    from funasr.utils.postprocess_utils import sentence_postprocess
+    from funasr.utils.timestamp_tools import cif_wo_hidden, ts_prediction_lfr6_standard
+    rng = np.random.default_rng(5)
+    cases = []
+    for ci, (T, ntok_extra, upsample, offset, eos) in enumerate([
+            (40, 0, 1, 0, False), (83, 0, 1, 0, True), (200, 3, 1, 0, False), (501, 0, 1, 0, False),
+            (501, -7, 1, 1230, False), (120, 0, 3, 0, False), (300, 2, 1, 0, True), (60, -1, 1, 0, False)]):
+        a = (rng.random(T) * 0.6).astype(np.float32)
+        a[rng.random(T) < 0.3] = 0.0
+        peaks = cif_wo_hidden(torch.from_numpy(a)[None].clone(), 1.0 - 1e-4)[0].numpy()
+        n_fire = int((peaks >= 1.0 - 1e-4).sum())
+        nchar = max(1, n_fire - 1 + ntok_extra)
+        chars = [f"t{i}" for i in range(nchar)] + (["</s>"] if eos else [])
+        # the Paraformer call site passes (peaks, alphas) as (us_alphas, us_peaks)
+        txt, ts = ts_prediction_lfr6_standard(torch.from_numpy(peaks.copy()), torch.from_numpy(a.copy()),
+                                              list(chars), vad_offset=offset, upsample_rate=upsample)
+        cases.append({"alphas": a.tolist(), "peaks": peaks.tolist(), "chars": chars, "vad_offset": offset,
+                      "upsample_rate": upsample, "text": txt, "timestamp": ts})
+    pp = []
+    for toks in POSTPROC_CASES:
+        spans = [[100 * i, 100 * i + 80] for i in range(len(toks))]
+        try:
+            sent, ts, words = sentence_postprocess(list(toks), spans)
+        except Exception as e:   # noqa: BLE001 - record the reference's failure mode
+            pp.append({"tokens": toks, "error": type(e).__name__})
+            continue
+        pp.append({"tokens": toks, "spans": spans, "sentence": sent, "timestamp": ts, "words": words})
+    with open(f"{HERE}/timestamps.json", "w") as f:
+        json.dump({"ts_prediction": cases, "postprocess_ts": pp}, f, ensure_ascii=False, indent=1)
+    print("timestamp cases", len(cases), "postprocess_ts", len(pp))
+
+
+def save_automodel_tiny_ts():
+    """AutoModel.generate(..., pred_timestamp=True) on the tiny config: text + word timestamps."""
+    import funasr.tokenizer.char_tokenizer  # noqa: F401
+    import funasr.frontends.wav_frontend  # noqa: F401
+    from funasr.auto.auto_model import AutoModel
+    cfg = paraformer_tiny()
+    kw = cfg.reference_kwargs()
+    am = AutoModel(model="Paraformer", model_conf=dict(ctc_weight=0.0, predictor_bias=1),
+                   device="cpu", ncpu=4, disable_update=True, disable_pbar=True, disable_log=True,
+                   tokenizer="CharTokenizer", tokenizer_conf=dict(token_list=token_list(cfg.vocab_size)),
+                   frontend="WavFrontend", frontend_conf=dict(fs=16000, window="hamming", n_mels=80,
+                                                             frame_length=25, frame_shift=10, lfr_m=7,
+                                                             lfr_n=6, dither=0.0, cmvn_file=CMVN),
+                   **kw)
+    sd = {k: torch.from_numpy(v) for k, v in make_weights(cfg, seed=0).items()}
+    am.model.load_state_dict(sd, strict=True)
+    feats, lens = fbank_input(seed=11, B=2, T=40, lens=[40, 27])
+    res = am.generate(input=torch.from_numpy(feats), input_len=torch.from_numpy(lens.astype(np.int32))[:, None],
+                      data_type="fbank", key=["uttA", "uttB"], pred_timestamp=True)
+    res = [{k: (v if not isinstance(v, np.ndarray) else v.tolist()) for k, v in r.items()} for r in res]
+    with open(f"{HERE}/automodel_tiny_ts.json", "w") as f:
+        json.dump(res, f, ensure_ascii=False, indent=1)
+    print("automodel ts:", [(r["text"][:12], r["timestamp"][:2]) for r in res])
+
+
+if __name__ == "__main__" and len(sys.argv) > 1:
     torch.manual_seed(0)
+    for part in sys.argv[1:]:
+        globals()["save_" + part]()
+elif __name__ == "__main__":
+    torch.manual_seed(0)
+    save_timestamps()
+    save_automodel_tiny_ts()
     save_postprocess()
     torch.set_num_threads(8)
     save_lfr_cmvn()

@@ -111,3 +111,14 @@ def test_automodel_waveform_path_matches_oracle():
         n = min(len(got), len(w))
         assert abs(len(got) - len(w)) <= 1 and sum(a == b for a, b in zip(got[:n], w[:n])) >= 0.9 * n
     del cmvn
+
+
+def test_automodel_pred_timestamp_matches_reference_generate():
+    """generate(..., pred_timestamp=True): text + word timestamps equal the reference's result dicts
+    (CIF peaks / alphas from pfm_run, exact mode)."""
+    am = _automodel()
+    feats, lens = fbank_input(seed=11, B=2, T=40, lens=[40, 27])
+    res = am.generate(input=torch.from_numpy(feats), input_len=torch.from_numpy(lens)[:, None],
+                      data_type="fbank", key=["uttA", "uttB"], pred_timestamp=True)
+    want = json.load(open(f"{GOLD}/automodel_tiny_ts.json", encoding="utf-8"))
+    assert res == want

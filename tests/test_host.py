@@ -151,3 +151,27 @@ def test_registry():
     from funasr_amd import tables
     import funasr_amd.model  # noqa: F401
     assert "Paraformer" in tables.model_classes
+
+
+def test_timestamps_match_reference():
+    """ts_prediction_lfr6_standard restatement vs the reference on seeded CIF weights (both fire-search
+    branches, '</s>', VAD offset, upsample 1/3): identical text and [start_ms, end_ms] lists."""
+    from funasr_amd.timestamp import ts_prediction_lfr6_standard
+    g = json.load(open(os.path.join(GOLD, "timestamps.json"), encoding="utf-8"))
+    for c in g["ts_prediction"]:
+        txt, ts = ts_prediction_lfr6_standard(torch.tensor(c["peaks"], dtype=torch.float32),
+                                              torch.tensor(c["alphas"], dtype=torch.float32), list(c["chars"]),
+                                              vad_offset=c["vad_offset"], upsample_rate=c["upsample_rate"])
+        assert txt == c["text"]
+        assert ts == c["timestamp"]
+
+
+def test_postprocess_with_timestamps_matches_reference():
+    g = json.load(open(os.path.join(GOLD, "timestamps.json"), encoding="utf-8"))
+    for c in g["postprocess_ts"]:
+        if "error" in c:   # the reference raises on these inputs; so must the restatement
+            with pytest.raises(Exception):
+                sentence_postprocess(list(c["tokens"]), [[100 * i, 100 * i + 80] for i in range(len(c["tokens"]))])
+            continue
+        sent, ts, words = sentence_postprocess(list(c["tokens"]), c["spans"])
+        assert (sent, ts, words) == (c["sentence"], c["timestamp"], c["words"]), c["tokens"]
