@@ -136,3 +136,86 @@ def paraformer_large() -> ParaformerConfig:
 def paraformer_tiny(enc_blocks: int = 3, dec_blocks: int = 2, vocab_size: int = 8404) -> ParaformerConfig:
     """Reduced-depth config used for full-tensor golden vectors (same widths as large)."""
     return ParaformerConfig(enc_blocks=enc_blocks, dec_blocks=dec_blocks, vocab_size=vocab_size)
+
+
+@dataclass
+class SenseVoiceConfig:
+    """Dimensions of SenseVoiceSmall (SAN-M encoder x 50 + tp encoder x 20 + CTC head).
+
+    Mirrors `SenseVoiceEncoderSmall.__init__` (funasr/models/sense_voice/model.py:452-548) and
+    `SenseVoiceSmall.__init__` (:592-663): LayerNorm is nn.LayerNorm (eps 1e-5, :275-287), the
+    four query rows come from `embed` = Embedding(7 + len(lid_dict) + len(textnorm_dict), 560)
+    (:646-648), the CTC head is `ctc.ctc_lo` Linear(512, vocab) (funasr/models/ctc/ctc.py:33).
+    Vocabulary 25,055 (runtime/triton_gpu/model_repo_sense_voice_small/encoder/config.pbtxt:51).
+    """
+    input_size: int = 560
+    d_model: int = 512
+    heads: int = 4
+    ffn: int = 2048
+    enc_blocks: int = 50            # 1 (encoders0) + 49 (encoders)
+    tp_blocks: int = 20
+    kernel_size: int = 11
+    enc_sanm_shift: int = 0
+    vocab_size: int = 25055
+    n_embed: int = 16               # 7 + 7 languages + 2 text-norm styles
+    ln_eps: float = 1e-5
+    blank_id: int = 0
+    sos: int = 1
+    eos: int = 2
+    # SenseVoiceSmall.__init__ :638-656 (query ids and special token ids)
+    lid_dict: Dict[str, int] = field(default_factory=lambda: {"auto": 0, "zh": 3, "en": 4, "yue": 7, "ja": 11,
+                                                              "ko": 12, "nospeech": 13})
+    textnorm_dict: Dict[str, int] = field(default_factory=lambda: {"withitn": 14, "woitn": 15})
+    emo_unk: int = 25009
+
+    @property
+    def d_k(self) -> int:
+        return self.d_model // self.heads
+
+    def to_dict(self) -> Dict[str, Any]:
+        return dataclasses.asdict(self)
+
+    @classmethod
+    def from_kwargs(cls, **kw) -> "SenseVoiceConfig":
+        c = cls()
+        enc = kw.get("encoder_conf") or {}
+        if "input_size" in kw and kw["input_size"]:
+            c.input_size = int(kw["input_size"])
+        if "vocab_size" in kw and kw["vocab_size"] and int(kw["vocab_size"]) > 0:
+            c.vocab_size = int(kw["vocab_size"])
+        c.d_model = int(enc.get("output_size", c.d_model))
+        c.heads = int(enc.get("attention_heads", c.heads))
+        c.ffn = int(enc.get("linear_units", c.ffn))
+        c.enc_blocks = int(enc.get("num_blocks", c.enc_blocks))
+        c.tp_blocks = int(enc.get("tp_blocks", c.tp_blocks))
+        c.kernel_size = int(enc.get("kernel_size", c.kernel_size))
+        c.enc_sanm_shift = int(enc.get("sanm_shfit", c.enc_sanm_shift))
+        if not enc.get("normalize_before", True):
+            raise ValueError("only normalize_before=True is on the HIP path")
+        for k in ("blank_id", "sos", "eos"):
+            if k in kw and kw[k] is not None:
+                setattr(c, k, int(kw[k]))
+        return c
+
+    def reference_kwargs(self) -> Dict[str, Any]:
+        """SenseVoiceSmall constructor kwargs (the released model's config.yaml encoder_conf)."""
+        return dict(
+            encoder="SenseVoiceEncoderSmall",
+            encoder_conf=dict(output_size=self.d_model, attention_heads=self.heads, linear_units=self.ffn,
+                              num_blocks=self.enc_blocks, tp_blocks=self.tp_blocks, dropout_rate=0.1,
+                              positional_dropout_rate=0.1, attention_dropout_rate=0.1, input_layer="pe",
+                              pos_enc_class="SinusoidalPositionEncoder", normalize_before=True,
+                              kernel_size=self.kernel_size, sanm_shfit=self.enc_sanm_shift,
+                              selfattention_layer_type="sanm"),
+            input_size=self.input_size,
+            vocab_size=self.vocab_size,
+        )
+
+
+def sense_voice_small() -> SenseVoiceConfig:
+    return SenseVoiceConfig()
+
+
+def sense_voice_tiny(enc_blocks: int = 3, tp_blocks: int = 2, vocab_size: int = 25055) -> SenseVoiceConfig:
+    """Reduced-depth SenseVoice config for full-tensor golden vectors (same widths as Small)."""
+    return SenseVoiceConfig(enc_blocks=enc_blocks, tp_blocks=tp_blocks, vocab_size=vocab_size)

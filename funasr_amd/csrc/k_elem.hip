@@ -544,9 +544,79 @@ __global__ void f32_to_bf16_kernel(const float* __restrict__ x, bf16* __restrict
     }
 }
 
-// Encoder output scatter into the zero-padded [B][T+2][D] layout (rows 0 and T+1 of each
-// utterance stay zero), feeding the k=3 predictor conv as an implicit-im2col GEMM.
+// ------------------------------------------------------------------------------------------
+// SenseVoiceSmall input (sense_voice/model.py:851-876): every utterance gets the four query
+// embeddings [language, event, emotion, text-norm] in front of its frames; lengths grow by nq.
+//   x[b, t] = t < nq ? embed[qid[t]] : feats[b, t - nq]      x: [B, T + nq, I]
+// One wave per output row, float4 copies (I % 4 == 0).
+// ------------------------------------------------------------------------------------------
+struct QueryIds { int id[4]; };
+__global__ __launch_bounds__(256) void sv_input_kernel(const float* __restrict__ feats, const int* __restrict__ lens,
+                                                       const float* __restrict__ embed, QueryIds q, int nq, int B,
+                                                       int T, int I, float* __restrict__ x, int* __restrict__ olen) {
+    const int lane = threadIdx.x & 63;
+    const long long row = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int Tq = T + nq;
+    if (row >= (long long)B * Tq) return;
+    const int b = (int)(row / Tq), t = (int)(row % Tq);
+    const float* src = t < nq ? embed + (long long)q.id[t] * I : feats + ((long long)b * T + (t - nq)) * I;
+    float* dst = x + row * I;
+    for (int c = lane * 4; c < I; c += 256) *(float4*)(dst + c) = *(const float4*)(src + c);
+    if (t == 0 && lane == 0) olen[b] = lens[b] + nq;
+}
+
+// ------------------------------------------------------------------------------------------
+// Greedy CTC collapse (sense_voice/model.py:893-906; ctc/model.py greedy): per utterance,
+// unique_consecutive over the frame argmax ids [0, olen), then drop blank. One wave per
+// utterance walks 64-frame chunks: keep[t] = id[t] != blank && (t == 0 || id[t] != id[t-1]);
+// ballot + popcount give each kept frame its output slot. tokens [B, Lcap] (-1 beyond ntok).
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void ctc_collapse_kernel(const int* __restrict__ ids, long long ld, const int* __restrict__ olen,
+                                                          int blank, int Lcap, int* __restrict__ tokens,
+                                                          int* __restrict__ ntok) {
+    const int lane = threadIdx.x;
+    const int b = blockIdx.x;
+    const int n = olen[b];
+    const int* r = ids + (long long)b * ld;
+    int* out = tokens + (long long)b * Lcap;
+    int cnt = 0;
+    for (int base = 0; base < n; base += 64) {
+        const int t = base + lane;
+        const int v = t < n ? r[t] : blank;
+        const int pv = (t > 0 && t - 1 < n) ? r[t - 1] : -2;
+        const bool keep = t < n && v != blank && v != pv;
+        const unsigned long long m = __ballot(keep);
+        const int pos = cnt + __popcll(m & ((1ull << lane) - 1ull));
+        if (keep && pos < Lcap) out[pos] = v;
+        cnt += __popcll(m);
+    }
+    for (int i = cnt + lane; i < Lcap; i += 64) out[i] = -1;
+    if (lane == 0) ntok[b] = cnt;
+}
+
 }  // namespace
+
+hipError_t pfm_sv_input(const float* feats, const int* lens, const float* embed, const int* qid, int nq, int B, int T,
+                        int I, float* x, int* olen, hipStream_t st) {
+    if (nq < 0 || nq > 4 || I % 4) return hipErrorInvalidValue;
+    QueryIds q = {{0, 0, 0, 0}};
+    for (int i = 0; i < nq; ++i) q.id[i] = qid[i];
+    const long long rows = (long long)B * (T + nq);
+    if (rows <= 0) return hipSuccess;
+    hipLaunchKernelGGL(sv_input_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, st, feats, lens, embed, q, nq,
+                       B, T, I, x, olen);
+    PFM_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+hipError_t pfm_ctc_collapse(const int* ids, long long ld, const int* olen, int B, int blank, int Lcap, int* tokens,
+                            int* ntok, hipStream_t st) {
+    if (B <= 0) return hipSuccess;
+    hipLaunchKernelGGL(ctc_collapse_kernel, dim3((unsigned)B), dim3(64), 0, st, ids, ld, olen, blank, Lcap, tokens,
+                       ntok);
+    PFM_LAUNCH_CHECK();
+    return hipSuccess;
+}
 
 hipError_t pfm_layernorm(const float* x, RowMap xmap, int M, int D, const float* g, const float* b, float eps,
                          const float* pe, int pe_T, float in_scale, void* out, RowMap omap, int odt, void* out2,

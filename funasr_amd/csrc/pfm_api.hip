@@ -49,6 +49,10 @@ hipError_t pfm_cif_fire(const float* alphas, const float* h, RowMap hmap, int B,
 hipError_t pfm_argmax_reduce(const float* val, const int* idx, int ntiles, int ncount, int B, int L, const int* ntok,
                              int Lcap, int* tokens, float* score, hipStream_t st);
 hipError_t pfm_fill_i32(int* p, long long n, int v, hipStream_t st);
+hipError_t pfm_sv_input(const float* feats, const int* lens, const float* embed, const int* qid, int nq, int B, int T,
+                        int I, float* x, int* olen, hipStream_t st);
+hipError_t pfm_ctc_collapse(const int* ids, long long ld, const int* olen, int B, int blank, int Lcap, int* tokens,
+                            int* ntok, hipStream_t st);
 hipError_t pfm_f32_to_bf16(const float* x, bf16* y, long long n, hipStream_t st);
 hipError_t pfm_fbank_launch(const float* wav, const int* nsamp, int B, int S_max, const float* cmvn,
                             const unsigned char* tables, float* fb_ws, int N_cap, float* feats, int T_cap, int* T_out,
@@ -116,6 +120,10 @@ struct pfm_handle {
     std::vector<DecLayer> dec;
     size_t an_g, an_b, cif_w, cif_b, cif_ow, cif_ob, dan_g, dan_b, out_w, out_b, d3w1, d3b1, d3w2, d3ng, d3nb,
         d3n1g, d3n1b, wkv_all, bkv_all;
+    // SenseVoice (PFM_ARCH_SENSEVOICE): tp_norm, CTC head, query embedding table
+    size_t tp_g = 0, tp_b = 0, ctc_w = 0, ctc_b = 0, embed = 0;
+    DevBuf Xin, X2, olen, fids, ban_bias;   // query-prefixed input, tp-stack residual, lens + 4, frame argmax
+    int ban_tok = -1;                        // token whose bias in ban_bias is -inf
     // workspace
     int capB = 0, capT = 0;
     DevBuf pe, X, Xn, QKV, QKVb, F, O, Ob, H, encp, encpb, Hc, alphas, peaks, nfire, ntok, emb, KV, Xd, Xdn, Hd,
@@ -163,8 +171,12 @@ size_t add_entry(pfm_handle* h, const std::string& name, std::vector<int64_t> sh
 void build_registry(pfm_handle* h) {
     const pfm_config& c = h->cfg;
     const int D = c.d_model, F = c.ffn, K = c.kernel_size, I = c.input_size, V = c.vocab_size;
-    for (int l = 0; l < c.enc_blocks; ++l) {
-        const std::string p = l == 0 ? "encoder.encoders0.0" : "encoder.encoders." + std::to_string(l - 1);
+    const bool sv = c.arch == PFM_ARCH_SENSEVOICE;
+    const int n_enc = c.enc_blocks + (sv ? c.tp_blocks : 0);
+    for (int l = 0; l < n_enc; ++l) {
+        const std::string p = l == 0 ? "encoder.encoders0.0"
+                              : l < c.enc_blocks ? "encoder.encoders." + std::to_string(l - 1)
+                                                 : "encoder.tp_encoders." + std::to_string(l - c.enc_blocks);
         const int din = l == 0 ? I : D;
         EncLayer L;
         L.din = din;
@@ -185,6 +197,14 @@ void build_registry(pfm_handle* h) {
     }
     h->an_g = add_entry(h, "encoder.after_norm.weight", {D});
     h->an_b = add_entry(h, "encoder.after_norm.bias", {D});
+    if (sv) {   // sense_voice/model.py:542-548, ctc/ctc.py:33, model.py:646-648
+        h->tp_g = add_entry(h, "encoder.tp_norm.weight", {D});
+        h->tp_b = add_entry(h, "encoder.tp_norm.bias", {D});
+        h->ctc_w = add_entry(h, "ctc.ctc_lo.weight", {V, D}, 0, true);
+        h->ctc_b = add_entry(h, "ctc.ctc_lo.bias", {V});
+        h->embed = add_entry(h, "embed.weight", {c.n_embed, I});
+        return;
+    }
     add_entry(h, "decoder.embed.0.weight", {V, D}, 2);
     h->dan_g = add_entry(h, "decoder.after_norm.weight", {D});
     h->dan_b = add_entry(h, "decoder.after_norm.bias", {D});
@@ -274,11 +294,13 @@ int reserve(pfm_handle* h, int B, int T) {
     B = std::max(B, h->capB);
     T = std::max(T, h->capT);
     const pfm_config& c = h->cfg;
+    const bool sv = c.arch == PFM_ARCH_SENSEVOICE;
     const size_t D = c.d_model, F = c.ffn, I = c.input_size;
     const size_t M = (size_t)B * T, Lc = (size_t)T + 1, Ml = (size_t)B * Lc;
     const size_t nkv = (size_t)c.dec_blocks * 2 * D;
     const int nt = std::max(pfm_gemm_amax_tiles(c.vocab_size), pfm_gemm_bf16_256_amax_tiles(c.vocab_size));
     HIP_TRY(hipDeviceSynchronize());
+    // encoder (both families)
     HIP_TRY(h->X.ensure(M * D * 4));
     HIP_TRY(h->Xn.ensure(M * std::max(I, D) * 4));
     HIP_TRY(h->QKV.ensure(M * 3 * D * 4));
@@ -287,30 +309,39 @@ int reserve(pfm_handle* h, int B, int T) {
     HIP_TRY(h->O.ensure(M * D * 4));
     HIP_TRY(h->Ob.ensure(M * D * 2));
     HIP_TRY(h->H.ensure(M * F * 4));
-    HIP_TRY(h->encp.ensure((size_t)B * (T + 2) * D * 4));
-    HIP_TRY(h->encpb.ensure((size_t)B * (T + 2) * D * 2));
-    HIP_TRY(h->Hc.ensure(M * D * 4));
-    HIP_TRY(h->alphas.ensure((size_t)B * (T + 1) * 4));
-    HIP_TRY(h->peaks.ensure((size_t)B * (T + 1) * 4));
-    HIP_TRY(h->nfire.ensure((size_t)B * 4));
-    HIP_TRY(h->ntok.ensure((size_t)B * 4));
-    HIP_TRY(h->emb.ensure(Ml * D * 4));
-    HIP_TRY(h->KV.ensure(M * nkv * 4));
-    HIP_TRY(h->Xd.ensure(Ml * D * 4));
-    HIP_TRY(h->Xdn.ensure(Ml * D * 4));
-    HIP_TRY(h->Hd.ensure(Ml * F * 4));
-    HIP_TRY(h->Hdn.ensure(Ml * F * 4));
-    HIP_TRY(h->Td.ensure(Ml * D * 4));
-    HIP_TRY(h->Tdn.ensure(Ml * D * 4));
-    HIP_TRY(h->Qd.ensure(Ml * D * 4));
-    HIP_TRY(h->Od.ensure(Ml * D * 4));
-    HIP_TRY(h->Odb.ensure(Ml * D * 2));
-    HIP_TRY(h->amv.ensure(Ml * nt * 4));
-    HIP_TRY(h->ami.ensure(Ml * nt * 4));
-    HIP_TRY(h->tok_tmp.ensure(Ml * 4));
-    // zero the padded encoder layouts once: rows 0 and T+1 of each utterance are never written
-    HIP_TRY(hipMemset(h->encp.p, 0, h->encp.bytes));
-    HIP_TRY(hipMemset(h->encpb.p, 0, h->encpb.bytes));
+    if (sv) {   // query-prefixed input, tp residual, CTC argmax partials (rows = frames)
+        HIP_TRY(h->Xin.ensure(M * I * 4));
+        HIP_TRY(h->X2.ensure(M * D * 4));
+        HIP_TRY(h->olen.ensure((size_t)B * 4));
+        HIP_TRY(h->fids.ensure(M * 4));
+        HIP_TRY(h->amv.ensure(M * nt * 4));
+        HIP_TRY(h->ami.ensure(M * nt * 4));
+    } else {
+        HIP_TRY(h->encp.ensure((size_t)B * (T + 2) * D * 4));
+        HIP_TRY(h->encpb.ensure((size_t)B * (T + 2) * D * 2));
+        HIP_TRY(h->Hc.ensure(M * D * 4));
+        HIP_TRY(h->alphas.ensure((size_t)B * (T + 1) * 4));
+        HIP_TRY(h->peaks.ensure((size_t)B * (T + 1) * 4));
+        HIP_TRY(h->nfire.ensure((size_t)B * 4));
+        HIP_TRY(h->ntok.ensure((size_t)B * 4));
+        HIP_TRY(h->emb.ensure(Ml * D * 4));
+        HIP_TRY(h->KV.ensure(M * nkv * 4));
+        HIP_TRY(h->Xd.ensure(Ml * D * 4));
+        HIP_TRY(h->Xdn.ensure(Ml * D * 4));
+        HIP_TRY(h->Hd.ensure(Ml * F * 4));
+        HIP_TRY(h->Hdn.ensure(Ml * F * 4));
+        HIP_TRY(h->Td.ensure(Ml * D * 4));
+        HIP_TRY(h->Tdn.ensure(Ml * D * 4));
+        HIP_TRY(h->Qd.ensure(Ml * D * 4));
+        HIP_TRY(h->Od.ensure(Ml * D * 4));
+        HIP_TRY(h->Odb.ensure(Ml * D * 2));
+        HIP_TRY(h->amv.ensure(Ml * nt * 4));
+        HIP_TRY(h->ami.ensure(Ml * nt * 4));
+        HIP_TRY(h->tok_tmp.ensure(Ml * 4));
+        // zero the padded encoder layouts once: rows 0 and T+1 of each utterance are never written
+        HIP_TRY(hipMemset(h->encp.p, 0, h->encp.bytes));
+        HIP_TRY(hipMemset(h->encpb.p, 0, h->encpb.bytes));
+    }
     // positional encoding table for the encoder input (depth = input_size)
     std::vector<float> pe;
     make_pe(pe, T, (int)I);
@@ -414,10 +445,181 @@ GemmEpi epi_default() {
     return e;
 }
 
-int set_lds_limits() {
-    static bool done = false;
-    if (done) return PFM_OK;
-    done = true;
+
+
+// Per-call launch context shared by the Paraformer and SenseVoice pipelines: numerics mode,
+// weight views and launch wrappers that attach algorithmic flops / bytes to every MFMA launch
+// for the live roofline (pfm_profile).
+struct Run {
+    pfm_handle* h;
+    hipStream_t st;
+    bool fast;
+    int dt;          // operand dtype of every contraction: DT_BF16 (fast) / DT_F32 (exact)
+    double es;       // operand element size
+    float qscale;    // d_k ** -0.5
+    bool fuse_fsmn;  // fast mode: encoder FSMN in the attention epilogue
+    bool fuse_ln;    // opt-in (PFM_GEMM_LN=1): LayerNorm fused into the 512-wide projections
+
+    Run(pfm_handle* h_, hipStream_t st_, bool fast_) : h(h_), st(st_), fast(fast_) {
+        const pfm_config& c = h->cfg;
+        dt = fast ? DT_BF16 : DT_F32;
+        es = fast ? 2.0 : 4.0;
+        qscale = (float)(1.0 / sqrt((double)(c.d_model / c.heads)));
+        const int lenc = (c.kernel_size - 1) / 2 + (c.enc_sanm_shift > 0 ? c.enc_sanm_shift : 0);
+        fuse_fsmn = fast && c.kernel_size == 11 && lenc == 5 && c.d_model / c.heads == 128 && attn_fsmn_enabled();
+        fuse_ln = fast && c.d_model == 512 && c.ffn % 32 == 0 && gemm_ln_enabled();
+    }
+    const void* W(size_t off) const { return fast ? (const void*)h->wb(off) : (const void*)h->w(off); }
+    const float* P(size_t off) const { return h->w(off); }
+
+    hipError_t gemm(int dtp, const void* A, RowMap am, const void* Wt, long long ldw, int Mm, int N, int Kk,
+                    const GemmEpi& e, hipStream_t s = nullptr) const {
+        if (!s) s = st;
+        const double fl = 2.0 * Mm * N * Kk;
+        const double by = ((double)Mm * Kk + (double)N * Kk) * es +
+                          (double)Mm * N * (e.out ? (e.out_dtype == DT_F32 ? 4.0 : 2.0) : 0.0) +
+                          (e.res0 ? (e.res0_bf16 ? 2.0 : 4.0) * Mm * N : 0.0) + (e.res1 ? 4.0 * Mm * N : 0.0) +
+                          (e.out2 ? 2.0 * Mm * N : 0.0);
+        ProfScope ps(h, s, PFM_K_GEMM, fl, by);
+        return gemm_dispatch(dtp, A, am, Wt, ldw, Mm, N, Kk, e, s);
+    }
+    hipError_t attn(int dtp, const void* q, RowMap qm, const void* k, RowMap km, const void* v, RowMap vm, float* o,
+                    long long ldo, void* o2, const int* kl, int Bb, int Tq, int Tk) const {
+        const pfm_config& c = h->cfg;
+        const double dk = c.d_model / c.heads;
+        const double fl = 4.0 * Bb * Tq * (double)Tk * dk * c.heads;
+        const double by = ((double)Bb * Tq + 2.0 * Bb * Tk) * c.d_model * es + (double)Bb * Tq * c.d_model * (o ? 4 : 2);
+        ProfScope ps(h, st, PFM_K_ATTN, fl, by);
+        return pfm_attention(dtp, q, qm, k, km, v, vm, o, ldo, o2, kl, Bb, Tq, Tk, c.heads, (int)dk, qscale, st);
+    }
+    // 512-wide projection with the following LayerNorm in its epilogue (opt-in fusion)
+    hipError_t gemm_ln(const void* A, RowMap am, const void* Wt, long long ldw, int Mm, int Kk, const GemmEpi& e,
+                       size_t g, size_t b, void* lo, RowMap lm, int ldt, void* lo2, RowMap lm2) const {
+        const int D = h->cfg.d_model;
+        const double fl = 2.0 * Mm * D * Kk;
+        const double by = ((double)Mm * Kk + (double)D * Kk) * 2.0 + (double)Mm * D * (e.out ? 4.0 : 0.0) +
+                          (e.res0 ? (e.res0_bf16 ? 2.0 : 4.0) * Mm * D : 0.0) + (e.res1 ? 4.0 * Mm * D : 0.0) +
+                          (double)Mm * D * (ldt == DT_F32 ? 4.0 : 2.0) + (lo2 ? 2.0 * Mm * D : 0.0);
+        ProfScope ps(h, st, PFM_K_GEMM, fl, by);
+        return pfm_gemm_bf16_ln(A, am, Wt, ldw, Mm, D, Kk, e, h->w(g), h->w(b), h->cfg.ln_eps, lo, lm, ldt, lo2, lm2,
+                                st);
+    }
+};
+
+// LayerNorm that closes an encoder stack (after_norm / tp_norm): out (+ optional second copy).
+struct FinalLN {
+    size_t g, b;
+    void* out; RowMap omap; int odt;
+    void* out2; RowMap o2map; int o2dt;
+};
+
+// Encoder layers [l0, l1) of h->enc (EncoderLayerSANM, sanm/encoder.py:72-148 ==
+// sense_voice/model.py:329-405) on the f32 residual X [B*T, D], then the closing LayerNorm `fin`.
+// l0 == 0: the stack input is x_in [B*T, input_size] (before x sqrt(d) + PE, encoder.py:378-379),
+// and layer 0 has no residual (in_size != size, encoder.py:129-137). lens: valid frames per utterance.
+int encoder_stack(const Run& r, const float* x_in, const int* lens, int B, int T, int l0, int l1, float* X,
+                  const FinalLN& fin) {
+    pfm_handle* h = r.h;
+    const pfm_config& c = h->cfg;
+    const hipStream_t st = r.st;
+    const bool fast = r.fast;
+    const int dt = r.dt;
+    const int D = c.d_model, Fd = c.ffn, I = c.input_size, K = c.kernel_size;
+    const long long M = (long long)B * T;
+    const int lenc = (K - 1) / 2 + (c.enc_sanm_shift > 0 ? c.enc_sanm_shift : 0);
+    void* Xn = h->Xn.p;   // LN output, f32 (exact) or bf16 (fast)
+    float* QKV = h->QKV.as<float>();
+    bf16* QKVb = h->QKVb.as<bf16>();
+    float* Fm = h->F.as<float>();
+    bf16* Fb = h->F.as<bf16>();   // fast mode: FSMN memory in bf16 (same buffer)
+    float* O = h->O.as<float>();
+    bf16* Ob = h->Ob.as<bf16>();
+    void* Hh = h->H.p;
+    const RowMap plain = rowmap_plain(0);
+    const bool fuse_last = r.fuse_ln && (!fin.out2 || fin.o2dt == DT_BF16);
+    for (int l = l0; l < l1; ++l) {
+        const EncLayer& L = h->enc[l];
+        const int din = L.din;
+        if (l == 0)   // x = x_in * sqrt(d_model) + PE ; LN1
+            HIP_TRY(pfm_layernorm(x_in, rowmap_plain(I), (int)M, I, r.P(L.ln1g), r.P(L.ln1b), c.ln_eps,
+                                  h->pe.as<float>(), T, sqrtf((float)D), Xn, rowmap_plain(I), dt, nullptr, plain, 0,
+                                  st));
+        else if (!r.fuse_ln || l == l0)   // fused: the previous layer's w2 GEMM already wrote LN1(x) to Xn
+            HIP_TRY(pfm_layernorm(X, rowmap_plain(D), (int)M, D, r.P(L.ln1g), r.P(L.ln1b), c.ln_eps, nullptr, 0, 1.f,
+                                  Xn, rowmap_plain(D), dt, nullptr, plain, 0, st));
+        {   // q|k|v = LN1(x) Wqkv^T + b   (fast mode: bf16 only — attention and FSMN read bf16)
+            GemmEpi e = epi_default();
+            e.bias = r.P(L.bqkv);
+            if (fast) { e.out = QKVb; e.out_map = rowmap_plain(3 * D); e.out_dtype = DT_BF16; }
+            else { e.out = QKV; e.out_map = rowmap_plain(3 * D); e.out_dtype = DT_F32; }
+            HIP_TRY(r.gemm(dt, Xn, rowmap_plain(din), r.W(L.wqkv), din, (int)M, 3 * D, din, e));
+        }
+        // FSMN memory on v (attention.py:207-223) + masked MHA. Fast mode: the FSMN runs in the attention
+        // kernel's epilogue (each block owns its rows x head channels; V is L2-resident) when the shape
+        // allows (K 11, left 5); bf16 in / bf16 out either way
+        if (r.fuse_fsmn) {
+            const double dk = c.d_model / c.heads;
+            const double fl = 4.0 * B * (double)T * T * dk * c.heads;
+            const double by = 3.0 * B * T * c.d_model * 2.0 + 2.0 * B * T * c.d_model * 2.0;
+            ProfScope ps(h, st, PFM_K_ATTN, fl, by);
+            HIP_TRY(pfm_attention_fsmn(DT_BF16, QKVb, rowmap_plain(3 * D), QKVb + D, rowmap_plain(3 * D),
+                                       QKVb + 2 * D, rowmap_plain(3 * D), nullptr, D, Ob, lens, B, T, T, c.heads,
+                                       (int)dk, r.qscale, r.P(L.fsmn), Fb, D, st));
+        } else if (fast) {
+            HIP_TRY(pfm_fsmn_bf16in(QKVb + 2 * D, rowmap_plain(3 * D), lens, B, T, D, r.P(L.fsmn), K, lenc, nullptr,
+                                    nullptr, Fb, st));
+            HIP_TRY(r.attn(DT_BF16, QKVb, rowmap_plain(3 * D), QKVb + D, rowmap_plain(3 * D), QKVb + 2 * D,
+                           rowmap_plain(3 * D), nullptr, D, Ob, lens, B, T, T));
+        } else {
+            HIP_TRY(pfm_fsmn(QKV + 2 * D, rowmap_plain(3 * D), lens, B, T, D, r.P(L.fsmn), K, lenc, nullptr, Fm,
+                             nullptr, st));
+            HIP_TRY(r.attn(DT_F32, QKV, rowmap_plain(3 * D), QKV + D, rowmap_plain(3 * D), QKV + 2 * D,
+                           rowmap_plain(3 * D), O, D, nullptr, lens, B, T, T));
+        }
+        {   // x = (x +) linear_out(att) + fsmn   (encoder.py:120-137: no residual when in != out)
+            GemmEpi e = epi_default();
+            e.bias = r.P(L.bo);
+            e.res0 = fast ? (const float*)Fb : Fm; e.ld_res0 = D; e.res0_bf16 = fast ? 1 : 0;
+            if (din == D) { e.res1 = X; e.ld_res1 = D; }
+            e.out = X; e.out_map = rowmap_plain(D); e.out_dtype = DT_F32;
+            if (r.fuse_ln) {   // ... and Xn = LN2(x)
+                HIP_TRY(r.gemm_ln(Ob, rowmap_plain(D), r.W(L.wo), D, (int)M, D, e, L.ln2g, L.ln2b, Xn,
+                                  rowmap_plain(D), DT_BF16, nullptr, plain));
+            } else {
+                HIP_TRY(r.gemm(dt, fast ? (const void*)Ob : (const void*)O, rowmap_plain(D), r.W(L.wo), D, (int)M, D,
+                               D, e));
+                HIP_TRY(pfm_layernorm(X, rowmap_plain(D), (int)M, D, r.P(L.ln2g), r.P(L.ln2b), c.ln_eps, nullptr, 0,
+                                      1.f, Xn, rowmap_plain(D), dt, nullptr, plain, 0, st));
+            }
+        }
+        {   // h = relu(LN2(x) W1^T + b1)
+            GemmEpi e = epi_default();
+            e.bias = r.P(L.b1); e.relu = 1;
+            e.out = Hh; e.out_map = rowmap_plain(Fd); e.out_dtype = dt;
+            HIP_TRY(r.gemm(dt, Xn, rowmap_plain(D), r.W(L.w1), D, (int)M, Fd, D, e));
+        }
+        {   // x = x + h W2^T + b2
+            GemmEpi e = epi_default();
+            e.bias = r.P(L.b2);
+            e.res0 = X; e.ld_res0 = D;
+            e.out = X; e.out_map = rowmap_plain(D); e.out_dtype = DT_F32;
+            if (!r.fuse_ln) {
+                HIP_TRY(r.gemm(dt, Hh, rowmap_plain(Fd), r.W(L.w2), Fd, (int)M, D, Fd, e));
+            } else if (l + 1 < l1) {   // ... and Xn = LN1_{l+1}(x)
+                HIP_TRY(r.gemm_ln(Hh, rowmap_plain(Fd), r.W(L.w2), Fd, (int)M, Fd, e, h->enc[l + 1].ln1g,
+                                  h->enc[l + 1].ln1b, Xn, rowmap_plain(D), DT_BF16, nullptr, plain));
+            } else if (fuse_last) {   // last layer: x itself is dead; the closing LN straight into its outputs
+                e.out = nullptr;
+                HIP_TRY(r.gemm_ln(Hh, rowmap_plain(Fd), r.W(L.w2), Fd, (int)M, Fd, e, fin.g, fin.b, fin.out,
+                                  fin.omap, fin.odt, fin.out2, fin.o2map));
+            } else {
+                HIP_TRY(r.gemm(dt, Hh, rowmap_plain(Fd), r.W(L.w2), Fd, (int)M, D, Fd, e));
+            }
+        }
+    }
+    if (!fuse_last || l1 == l0)
+        HIP_TRY(pfm_layernorm(X, rowmap_plain(D), (int)M, D, r.P(fin.g), r.P(fin.b), c.ln_eps, nullptr, 0, 1.f, fin.out,
+                              fin.omap, fin.odt, fin.out2, fin.o2map, fin.o2dt, st));
     return PFM_OK;
 }
 
@@ -431,6 +633,13 @@ void pfm_config_default(pfm_config* c) {
     c->kernel_size = 11; c->enc_sanm_shift = 0; c->dec_sanm_shift = 0; c->vocab_size = 8404;
     c->cif_l_order = 1; c->cif_r_order = 1; c->cif_threshold = 1.f; c->tail_threshold = 0.45f;
     c->smooth_factor = 1.f; c->noise_threshold = 0.f; c->ln_eps = 1e-12f;
+    c->arch = PFM_ARCH_PARAFORMER; c->tp_blocks = 0; c->n_embed = 0;
+}
+
+void pfm_config_sensevoice(pfm_config* c) {
+    pfm_config_default(c);
+    c->arch = PFM_ARCH_SENSEVOICE; c->dec_blocks = 0; c->tp_blocks = 20; c->n_embed = 16; c->vocab_size = 25055;
+    c->ln_eps = 1e-5f;
 }
 
 const char* pfm_last_error(void) { return g_err.c_str(); }
@@ -444,8 +653,12 @@ int pfm_create(const pfm_config* cfg, int device, pfm_handle** out) {
         return fail(PFM_E_ARG, "pfm_create: dims must be multiples of 8 and <= 2048");
     if (cfg->enc_blocks < 1 || cfg->dec_blocks < 0 || cfg->kernel_size < 1 || cfg->vocab_size < 1)
         return fail(PFM_E_ARG, "pfm_create: bad block counts");
-    if (cfg->cif_l_order != 1 || cfg->cif_r_order != 1)
+    if (cfg->arch != PFM_ARCH_PARAFORMER && cfg->arch != PFM_ARCH_SENSEVOICE)
+        return fail(PFM_E_ARG, "pfm_create: unknown arch");
+    if (cfg->arch == PFM_ARCH_PARAFORMER && (cfg->cif_l_order != 1 || cfg->cif_r_order != 1))
         return fail(PFM_E_ARG, "pfm_create: CIF conv must be l_order = r_order = 1");
+    if (cfg->arch == PFM_ARCH_SENSEVOICE && (cfg->tp_blocks < 0 || cfg->n_embed < 1))
+        return fail(PFM_E_ARG, "pfm_create: SenseVoice needs tp_blocks >= 0 and n_embed >= 1");
     int ndev = 0;
     HIP_TRY(hipGetDeviceCount(&ndev));
     if (device < 0 || device >= ndev) return fail(PFM_E_ARG, "pfm_create: bad device index");
@@ -506,6 +719,7 @@ int pfm_set_weight(pfm_handle* h, const char* name, const void* host_ptr, int dt
     HIP_TRY(hipMemcpy(h->w(e.off), src, e.numel * 4, hipMemcpyHostToDevice));
     if (!e.set) { e.set = true; h->missing--; }
     h->bf_ready = false;
+    h->ban_tok = -1;   // the banned-token bias copy follows ctc.ctc_lo.bias
     return PFM_OK;
 }
 
@@ -525,6 +739,7 @@ int pfm_run(pfm_handle* h, void* stream, int mode, const float* feats, const int
     if (B < 1 || T < 1 || L_cap < 0) return fail(PFM_E_ARG, "pfm_run: bad sizes");
     if (mode != PFM_MODE_EXACT && mode != PFM_MODE_FAST) return fail(PFM_E_ARG, "pfm_run: bad mode");
     if (h->missing) return fail(PFM_E_STATE, "pfm_run: " + std::to_string(h->missing) + " weights not set");
+    if (h->cfg.arch != PFM_ARCH_PARAFORMER) return fail(PFM_E_STATE, "pfm_run: handle is not a Paraformer");
     HIP_TRY(hipSetDevice(h->device));
     hipStream_t st = (hipStream_t)stream;
     int rc = reserve(h, B, T);
@@ -532,56 +747,26 @@ int pfm_run(pfm_handle* h, void* stream, int mode, const float* feats, const int
     const bool fast = mode == PFM_MODE_FAST;
     if (fast) { rc = ensure_bf16(h, st); if (rc) return rc; }
     const pfm_config& c = h->cfg;
-    const int D = c.d_model, Fd = c.ffn, I = c.input_size, K = c.kernel_size, nkv = c.dec_blocks * 2 * D;
+    const int D = c.d_model, Fd = c.ffn, K = c.kernel_size, nkv = c.dec_blocks * 2 * D;
     const long long M = (long long)B * T;
     const int dt = fast ? DT_BF16 : DT_F32;
-    const float qscale = (float)(1.0 / sqrt((double)(D / c.heads)));   // q_h * d_k ** -0.5
-    const int lenc = (K - 1) / 2 + (c.enc_sanm_shift > 0 ? c.enc_sanm_shift : 0);
     const int ldec = (K - 1) / 2 + (c.dec_sanm_shift > 0 ? c.dec_sanm_shift : 0);
     if (h->prof_on && h->ev_used > 4096) prof_collect(h);
     const double es = fast ? 2.0 : 4.0;
-    // launch wrappers: algorithmic flops / bytes per launch for the live roofline
+    const Run run(h, st, fast);
+    const bool fuse_ln = run.fuse_ln;
     auto GEMM = [&](int dtp, const void* A, RowMap am, const void* Wt, long long ldw, int Mm, int N, int Kk,
-                    const GemmEpi& e) -> hipError_t {
-        const double fl = 2.0 * Mm * N * Kk;
-        const double by = ((double)Mm * Kk + (double)N * Kk) * es +
-                          (double)Mm * N * (e.out ? (e.out_dtype == DT_F32 ? 4.0 : 2.0) : 0.0) +
-                          (e.res0 ? 4.0 * Mm * N : 0.0) + (e.res1 ? 4.0 * Mm * N : 0.0) + (e.out2 ? 2.0 * Mm * N : 0.0);
-        ProfScope ps(h, st, PFM_K_GEMM, fl, by);
-        return gemm_dispatch(dtp, A, am, Wt, ldw, Mm, N, Kk, e, st);
-    };
+                    const GemmEpi& e) -> hipError_t { return run.gemm(dtp, A, am, Wt, ldw, Mm, N, Kk, e); };
     auto ATTN = [&](int dtp, const void* q, RowMap qm, const void* k, RowMap km, const void* v, RowMap vm, float* o,
                     long long ldo, void* o2, const int* kl, int Bb, int Tq, int Tk) -> hipError_t {
-        const double dk = c.d_model / c.heads;
-        const double fl = 4.0 * Bb * Tq * (double)Tk * dk * c.heads;
-        const double by = ((double)Bb * Tq + 2.0 * Bb * Tk) * c.d_model * es + (double)Bb * Tq * c.d_model * (o ? 4 : 2);
-        ProfScope ps(h, st, PFM_K_ATTN, fl, by);
-        return pfm_attention(dtp, q, qm, k, km, v, vm, o, ldo, o2, kl, Bb, Tq, Tk, c.heads, (int)dk, qscale, st);
+        return run.attn(dtp, q, qm, k, km, v, vm, o, ldo, o2, kl, Bb, Tq, Tk);
     };
-    const bool fuse_fsmn = fast && K == 11 && lenc == 5 && c.d_model / c.heads == 128 && attn_fsmn_enabled();
-    // fast mode: 512-wide projections finish the residual sum AND the following LayerNorm in one
-    // kernel (k_gemm_bf16.hip gemm_bf16_ln_kernel); exact mode keeps the unfused reference order
-    const bool fuse_ln = fast && D == 512 && Fd % 32 == 0 && c.enc_blocks >= 1 && gemm_ln_enabled();
     auto GEMM_LN = [&](const void* A, RowMap am, const void* Wt, long long ldw, int Mm, int Kk, const GemmEpi& e,
                        size_t g, size_t b, void* lo, RowMap lm, int ldt, void* lo2, RowMap lm2) -> hipError_t {
-        const double fl = 2.0 * Mm * D * Kk;
-        const double by = ((double)Mm * Kk + (double)D * Kk) * 2.0 + (double)Mm * D * (e.out ? 4.0 : 0.0) +
-                          (e.res0 ? (e.res0_bf16 ? 2.0 : 4.0) * Mm * D : 0.0) + (e.res1 ? 4.0 * Mm * D : 0.0) +
-                          (double)Mm * D * (ldt == DT_F32 ? 4.0 : 2.0) + (lo2 ? 2.0 * Mm * D : 0.0);
-        ProfScope ps(h, st, PFM_K_GEMM, fl, by);
-        return pfm_gemm_bf16_ln(A, am, Wt, ldw, Mm, D, Kk, e, h->w(g), h->w(b), c.ln_eps, lo, lm, ldt, lo2, lm2, st);
+        return run.gemm_ln(A, am, Wt, ldw, Mm, Kk, e, g, b, lo, lm, ldt, lo2, lm2);
     };
-    auto W = [&](size_t off) -> const void* { return fast ? (const void*)h->wb(off) : (const void*)h->w(off); };
-    auto P = [&](size_t off) -> const float* { return h->w(off); };
-    float* X = h->X.as<float>();
-    void* Xn = h->Xn.p;   // LN output, f32 (exact) or bf16 (fast)
-    float* QKV = h->QKV.as<float>();
-    bf16* QKVb = h->QKVb.as<bf16>();
-    float* Fm = h->F.as<float>();
-    bf16* Fb = h->F.as<bf16>();   // fast mode: FSMN memory in bf16 (same buffer)
-    float* O = h->O.as<float>();
-    bf16* Ob = h->Ob.as<bf16>();
-    void* Hh = h->H.p;
+    auto W = [&](size_t off) -> const void* { return run.W(off); };
+    auto P = [&](size_t off) -> const float* { return run.P(off); };
     const RowMap plain = rowmap_plain(0);
 
     // after_norm -> zero-padded [B][T+2][D] (row 0 and T+1 of each utterance stay zero)
@@ -598,87 +783,12 @@ int pfm_run(pfm_handle* h, void* stream, int mode, const float* feats, const int
     }
 
     // ---------------- encoder (sanm/encoder.py:361-430) ----------------
-    for (int l = 0; l < c.enc_blocks; ++l) {
-        const EncLayer& L = h->enc[l];
-        const int din = L.din;
-        if (l == 0)   // x = feats * sqrt(d_model) + PE ; LN1
-            HIP_TRY(pfm_layernorm(feats, rowmap_plain(I), (int)M, I, P(L.ln1g), P(L.ln1b), c.ln_eps, h->pe.as<float>(),
-                                  T, sqrtf((float)D), Xn, rowmap_plain(I), dt, nullptr, plain, 0, st));
-        else if (!fuse_ln)   // fused: the previous layer's w2 GEMM already wrote LN1(x) to Xn
-            HIP_TRY(pfm_layernorm(X, rowmap_plain(D), (int)M, D, P(L.ln1g), P(L.ln1b), c.ln_eps, nullptr, 0, 1.f, Xn,
-                                  rowmap_plain(D), dt, nullptr, plain, 0, st));
-        {   // q|k|v = LN1(x) Wqkv^T + b   (fast mode: bf16 only — attention and FSMN read bf16)
-            GemmEpi e = epi_default();
-            e.bias = P(L.bqkv);
-            if (fast) { e.out = QKVb; e.out_map = rowmap_plain(3 * D); e.out_dtype = DT_BF16; }
-            else { e.out = QKV; e.out_map = rowmap_plain(3 * D); e.out_dtype = DT_F32; }
-            HIP_TRY(GEMM(dt, Xn, rowmap_plain(din), W(L.wqkv), din, (int)M, 3 * D, din, e));
-        }
-        // FSMN memory on v (attention.py:207-223) + masked MHA. Fast mode: the FSMN runs in the attention
-        // kernel's epilogue (each block owns its rows x head channels; V is L2-resident) when the shape
-        // allows (K 11, left 5); bf16 in / bf16 out either way
-        if (fast && fuse_fsmn) {
-            const double dk = c.d_model / c.heads;
-            const double fl = 4.0 * B * (double)T * T * dk * c.heads;
-            const double by = 3.0 * B * T * c.d_model * 2.0 + 2.0 * B * T * c.d_model * 2.0;
-            ProfScope ps(h, st, PFM_K_ATTN, fl, by);
-            HIP_TRY(pfm_attention_fsmn(DT_BF16, QKVb, rowmap_plain(3 * D), QKVb + D, rowmap_plain(3 * D),
-                                       QKVb + 2 * D, rowmap_plain(3 * D), nullptr, D, Ob, lens, B, T, T, c.heads,
-                                       (int)dk, qscale, P(L.fsmn), Fb, D, st));
-        } else if (fast) {
-            HIP_TRY(pfm_fsmn_bf16in(QKVb + 2 * D, rowmap_plain(3 * D), lens, B, T, D, P(L.fsmn), K, lenc, nullptr,
-                                    nullptr, Fb, st));
-            HIP_TRY(ATTN(DT_BF16, QKVb, rowmap_plain(3 * D), QKVb + D, rowmap_plain(3 * D), QKVb + 2 * D,
-                         rowmap_plain(3 * D), nullptr, D, Ob, lens, B, T, T));
-        } else {
-            HIP_TRY(pfm_fsmn(QKV + 2 * D, rowmap_plain(3 * D), lens, B, T, D, P(L.fsmn), K, lenc, nullptr, Fm, nullptr,
-                             st));
-        }
-        if (!fast)
-            HIP_TRY(ATTN(DT_F32, QKV, rowmap_plain(3 * D), QKV + D, rowmap_plain(3 * D), QKV + 2 * D,
-                         rowmap_plain(3 * D), O, D, nullptr, lens, B, T, T));
-        {   // x = (x +) linear_out(att) + fsmn   (encoder.py:120-137: no residual when in != out)
-            GemmEpi e = epi_default();
-            e.bias = P(L.bo);
-            e.res0 = fast ? (const float*)Fb : Fm; e.ld_res0 = D; e.res0_bf16 = fast ? 1 : 0;
-            if (din == D) { e.res1 = X; e.ld_res1 = D; }
-            e.out = X; e.out_map = rowmap_plain(D); e.out_dtype = DT_F32;
-            if (fuse_ln) {   // ... and Xn = LN2(x)
-                HIP_TRY(GEMM_LN(Ob, rowmap_plain(D), W(L.wo), D, (int)M, D, e, L.ln2g, L.ln2b, Xn, rowmap_plain(D),
-                                DT_BF16, nullptr, plain));
-            } else {
-                HIP_TRY(GEMM(dt, fast ? (const void*)Ob : (const void*)O, rowmap_plain(D), W(L.wo), D, (int)M, D, D,
-                             e));
-                HIP_TRY(pfm_layernorm(X, rowmap_plain(D), (int)M, D, P(L.ln2g), P(L.ln2b), c.ln_eps, nullptr, 0, 1.f,
-                                      Xn, rowmap_plain(D), dt, nullptr, plain, 0, st));
-            }
-        }
-        {   // h = relu(LN2(x) W1^T + b1)
-            GemmEpi e = epi_default();
-            e.bias = P(L.b1); e.relu = 1;
-            e.out = Hh; e.out_map = rowmap_plain(Fd); e.out_dtype = dt;
-            HIP_TRY(GEMM(dt, Xn, rowmap_plain(D), W(L.w1), D, (int)M, Fd, D, e));
-        }
-        {   // x = x + h W2^T + b2
-            GemmEpi e = epi_default();
-            e.bias = P(L.b2);
-            e.res0 = X; e.ld_res0 = D;
-            e.out = X; e.out_map = rowmap_plain(D); e.out_dtype = DT_F32;
-            if (!fuse_ln) {
-                HIP_TRY(GEMM(dt, Hh, rowmap_plain(Fd), W(L.w2), Fd, (int)M, D, Fd, e));
-            } else if (l + 1 < c.enc_blocks) {   // ... and Xn = LN1_{l+1}(x)
-                HIP_TRY(GEMM_LN(Hh, rowmap_plain(Fd), W(L.w2), Fd, (int)M, Fd, e, h->enc[l + 1].ln1g,
-                                h->enc[l + 1].ln1b, Xn, rowmap_plain(D), DT_BF16, nullptr, plain));
-            } else {   // last layer: x itself is dead; after_norm straight into the padded encp / encpb
-                e.out = nullptr;
-                HIP_TRY(GEMM_LN(Hh, rowmap_plain(Fd), W(L.w2), Fd, (int)M, Fd, e, h->an_g, h->an_b, encp + D, encmap,
-                                DT_F32, encpb + D, encmap));
-            }
-        }
+    {
+        const FinalLN fin = {h->an_g, h->an_b, encp + D, encmap, DT_F32, fast ? (void*)(encpb + D) : nullptr, encmap,
+                             DT_BF16};
+        rc = encoder_stack(run, feats, lens, B, T, 0, c.enc_blocks, h->X.as<float>(), fin);
+        if (rc) return rc;
     }
-    if (!fuse_ln)
-        HIP_TRY(pfm_layernorm(X, rowmap_plain(D), (int)M, D, P(h->an_g), P(h->an_b), c.ln_eps, nullptr, 0, 1.f,
-                              encp + D, encmap, DT_F32, fast ? (void*)(encpb + D) : nullptr, encmap, DT_BF16, st));
     if (enc_out)
         HIP_TRY(hipMemcpy2DAsync(enc_out, (size_t)T * D * 4, encp + D, (size_t)(T + 2) * D * 4, (size_t)T * D * 4, B,
                                  hipMemcpyDeviceToDevice, st));
@@ -846,6 +956,75 @@ int pfm_run(pfm_handle* h, void* stream, int mode, const float* feats, const int
     return PFM_OK;
 }
 
+int pfm_run_ctc(pfm_handle* h, void* stream, int mode, const float* feats, const int32_t* lens, int B, int T,
+                const int32_t* query, int ban_token, int32_t* tokens, int L_cap, int32_t* ntok_out, float* enc_out,
+                int32_t* frame_ids) {
+    if (!h || !feats || !lens || !query || !tokens || !ntok_out) return fail(PFM_E_ARG, "pfm_run_ctc: null argument");
+    if (B < 1 || T < 1 || L_cap < 0) return fail(PFM_E_ARG, "pfm_run_ctc: bad sizes");
+    if (mode != PFM_MODE_EXACT && mode != PFM_MODE_FAST) return fail(PFM_E_ARG, "pfm_run_ctc: bad mode");
+    if (h->cfg.arch != PFM_ARCH_SENSEVOICE) return fail(PFM_E_STATE, "pfm_run_ctc: handle is not a SenseVoice model");
+    if (h->missing) return fail(PFM_E_STATE, "pfm_run_ctc: " + std::to_string(h->missing) + " weights not set");
+    const pfm_config& c = h->cfg;
+    constexpr int NQ = 4;   // [language, event, emotion, textnorm] (sense_voice/model.py:851-876)
+    for (int i = 0; i < NQ; ++i)
+        if (query[i] < 0 || query[i] >= c.n_embed) return fail(PFM_E_ARG, "pfm_run_ctc: query id out of range");
+    if (ban_token >= c.vocab_size) return fail(PFM_E_ARG, "pfm_run_ctc: ban_token out of range");
+    HIP_TRY(hipSetDevice(h->device));
+    hipStream_t st = (hipStream_t)stream;
+    const int Tq = T + NQ;
+    int rc = reserve(h, B, Tq);
+    if (rc) return rc;
+    const bool fast = mode == PFM_MODE_FAST;
+    if (fast) { rc = ensure_bf16(h, st); if (rc) return rc; }
+    if (h->prof_on && h->ev_used > 4096) prof_collect(h);
+    const Run run(h, st, fast);
+    const int D = c.d_model, I = c.input_size, V = c.vocab_size;
+    const long long M = (long long)B * Tq;
+    int* olen = h->olen.as<int>();
+    // x = [embed(query) ; feats], lens + 4 (model.py:851-876)
+    HIP_TRY(pfm_sv_input(feats, lens, h->w(h->embed), query, NQ, B, T, I, h->Xin.as<float>(), olen, st));
+    // encoder: 50 SAN-M layers -> after_norm (f32, feeds the tp stack) -> 20 tp layers -> tp_norm
+    // (SenseVoiceEncoderSmall.forward, model.py:553-585)
+    {
+        const FinalLN fin = {h->an_g, h->an_b, h->X2.p, rowmap_plain(D), DT_F32, nullptr, rowmap_plain(0), 0};
+        rc = encoder_stack(run, h->Xin.as<float>(), olen, B, Tq, 0, c.enc_blocks, h->X.as<float>(), fin);
+        if (rc) return rc;
+    }
+    {
+        const FinalLN fin = {h->tp_g, h->tp_b, h->Xn.p, rowmap_plain(D), run.dt, enc_out, rowmap_plain(D), DT_F32};
+        rc = encoder_stack(run, nullptr, olen, B, Tq, c.enc_blocks, c.enc_blocks + c.tp_blocks, h->X2.as<float>(), fin);
+        if (rc) return rc;
+    }
+    // CTC head (ctc.py:173-184) with fused row-argmax; ban_emo_unk (model.py:885-886) sets the banned
+    // token's log-prob to -inf: a -inf bias entry excludes it from the argmax the same way
+    const float* bias = run.P(h->ctc_b);
+    if (ban_token >= 0) {
+        if (h->ban_tok != ban_token || !h->ban_bias.p) {
+            HIP_TRY(h->ban_bias.ensure((size_t)V * 4));
+            HIP_TRY(hipMemcpyAsync(h->ban_bias.p, bias, (size_t)V * 4, hipMemcpyDeviceToDevice, st));
+            const float ninf = -INFINITY;
+            HIP_TRY(hipMemcpyAsync(h->ban_bias.as<float>() + ban_token, &ninf, 4, hipMemcpyHostToDevice, st));
+            HIP_TRY(hipStreamSynchronize(st));   // the host source of the -inf entry is a stack value
+            h->ban_tok = ban_token;
+        }
+        bias = h->ban_bias.as<float>();
+    }
+    const int ntl = amax_tiles(run.dt, rowmap_plain(D), D, V, D);
+    {
+        GemmEpi e = epi_default();
+        e.bias = bias;
+        e.amax_val = h->amv.as<float>(); e.amax_idx = h->ami.as<int>(); e.n_tiles = ntl;
+        e.out = nullptr;
+        HIP_TRY(run.gemm(run.dt, h->Xn.p, rowmap_plain(D), run.W(h->ctc_w), D, (int)M, V, D, e));
+    }
+    int* fid = frame_ids ? frame_ids : h->fids.as<int>();
+    HIP_TRY(pfm_argmax_reduce(h->amv.as<float>(), h->ami.as<int>(), ntl, (V + 63) / 64, B, Tq, olen, Tq, fid, nullptr,
+                              st));
+    // unique_consecutive + drop blank (model.py:894-906)
+    HIP_TRY(pfm_ctc_collapse(fid, Tq, olen, B, 0, L_cap, tokens, ntok_out, st));
+    return PFM_OK;
+}
+
 int pfm_fbank(pfm_handle* h, void* stream, const float* wav, const int32_t* nsamp, int B, int S_max,
               const float* cmvn, float* feats, int T_cap, int32_t* T_out) {
     if (!h || !wav || !nsamp || !feats || !T_out) return fail(PFM_E_ARG, "pfm_fbank: null argument");
@@ -947,6 +1126,13 @@ int pfm_op_fsmn_bf16(void* stream, const void* v, const int32_t* len, const floa
                      int K, int left) {
     HIP_TRY(pfm_fsmn_bf16in((const bf16*)v, rowmap_plain(D), len, B, T, D, w, K, left, nullptr, nullptr, (bf16*)out,
                             (hipStream_t)stream));
+    return PFM_OK;
+}
+
+int pfm_op_ctc_collapse(void* stream, const int32_t* ids, int64_t ld, const int32_t* olen, int B, int blank,
+                        int32_t* tokens, int L_cap, int32_t* ntok) {
+    if (!ids || !olen || !tokens || !ntok || B < 0 || L_cap < 0) return fail(PFM_E_ARG, "pfm_op_ctc_collapse: bad arguments");
+    HIP_TRY(pfm_ctc_collapse(ids, ld, olen, B, blank, L_cap, tokens, ntok, (hipStream_t)stream));
     return PFM_OK;
 }
 

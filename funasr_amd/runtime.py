@@ -12,18 +12,19 @@ from typing import Dict, Optional
 
 import numpy as np
 
-from .config import ParaformerConfig
+from .config import ParaformerConfig, SenseVoiceConfig
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("PFM_LIB", os.path.join(_HERE, "_lib", "libpfm_hip.so"))
 
 PFM_F32, PFM_BF16 = 0, 1
+ARCH_PARAFORMER, ARCH_SENSEVOICE = 0, 1
 MODE_EXACT, MODE_FAST = 0, 1
 MODES = {"exact": MODE_EXACT, "fp32": MODE_EXACT, "fast": MODE_FAST, "bf16": MODE_FAST}
 
 # every symbol include/pfm.h declares (checked by tests/test_abi.py)
-ABI_SYMBOLS = ("pfm_config_default", "pfm_create", "pfm_set_weight", "pfm_missing_weights", "pfm_reserve",
-               "pfm_run", "pfm_fbank", "pfm_lfr_frames", "pfm_last_error", "pfm_destroy", "pfm_op_gemm",
+ABI_SYMBOLS = ("pfm_config_default", "pfm_config_sensevoice", "pfm_create", "pfm_set_weight",
+               "pfm_missing_weights", "pfm_reserve", "pfm_run", "pfm_run_ctc", "pfm_op_ctc_collapse", "pfm_fbank", "pfm_lfr_frames", "pfm_last_error", "pfm_destroy", "pfm_op_gemm",
                "pfm_op_attention", "pfm_op_layernorm", "pfm_op_fsmn", "pfm_op_cif", "pfm_profile", "pfm_op_gemm_layernorm", "pfm_op_fsmn_bf16", "pfm_op_layernorm_bf16",
                "pfm_profile_read")
 
@@ -37,13 +38,18 @@ class PfmConfig(ctypes.Structure):
                                                "kernel_size", "enc_sanm_shift", "dec_sanm_shift", "vocab_size",
                                                "cif_l_order", "cif_r_order")] + \
               [(n, ctypes.c_float) for n in ("cif_threshold", "tail_threshold", "smooth_factor", "noise_threshold",
-                                             "ln_eps")]
+                                             "ln_eps")] + \
+              [(n, ctypes.c_int32) for n in ("arch", "tp_blocks", "n_embed")]
 
     @classmethod
-    def from_config(cls, c: ParaformerConfig) -> "PfmConfig":
+    def from_config(cls, c) -> "PfmConfig":
+        if isinstance(c, SenseVoiceConfig):
+            return cls(c.input_size, c.d_model, c.heads, c.ffn, c.enc_blocks, 0, c.kernel_size, c.enc_sanm_shift, 0,
+                       c.vocab_size, 1, 1, 1.0, 0.45, 1.0, 0.0, c.ln_eps, ARCH_SENSEVOICE, c.tp_blocks, c.n_embed)
         return cls(c.input_size, c.d_model, c.heads, c.ffn, c.enc_blocks, c.dec_blocks, c.kernel_size,
                    c.enc_sanm_shift, c.dec_sanm_shift, c.vocab_size, c.cif_l_order, c.cif_r_order,
-                   c.cif_threshold, c.tail_threshold, c.smooth_factor, c.noise_threshold, c.ln_eps)
+                   c.cif_threshold, c.tail_threshold, c.smooth_factor, c.noise_threshold, c.ln_eps,
+                   ARCH_PARAFORMER, 0, 0)
 
 
 _lib = None
@@ -61,6 +67,11 @@ def load_library(path: Optional[str] = None) -> ctypes.CDLL:
     vp, i32, f32p, i32p = ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p
     lib.pfm_config_default.argtypes = [ctypes.POINTER(PfmConfig)]
     lib.pfm_config_default.restype = None
+    lib.pfm_config_sensevoice.argtypes = [ctypes.POINTER(PfmConfig)]
+    lib.pfm_config_sensevoice.restype = None
+    lib.pfm_run_ctc.argtypes = [vp, vp, i32, f32p, i32p, i32, i32, ctypes.POINTER(ctypes.c_int32), i32, i32p, i32,
+                                i32p, f32p, i32p]
+    lib.pfm_op_ctc_collapse.argtypes = [vp, i32p, ctypes.c_int64, i32p, i32, i32, i32p, i32, i32p]
     lib.pfm_create.argtypes = [ctypes.POINTER(PfmConfig), i32, ctypes.POINTER(vp)]
     lib.pfm_set_weight.argtypes = [vp, ctypes.c_char_p, vp, i32, ctypes.POINTER(ctypes.c_int64), i32]
     lib.pfm_missing_weights.argtypes = [vp]
@@ -110,7 +121,7 @@ def _stream_ptr(torch, device) -> int:
 class PfmEngine:
     """One pfm_handle on one HIP device: weights + workspace, stream-ordered calls."""
 
-    def __init__(self, cfg: ParaformerConfig, device: int = 0):
+    def __init__(self, cfg, device: int = 0):   # ParaformerConfig | SenseVoiceConfig
         import torch
         if not torch.cuda.is_available():
             raise PfmError("PfmEngine needs a ROCm GPU (torch.cuda.is_available() is False); "
@@ -188,6 +199,37 @@ class PfmEngine:
         check(self.lib.pfm_run(self.h, _stream_ptr(torch, dev), m, _ptr(feats), _ptr(lens), B, T, _ptr(tokens),
                                L_cap, _ptr(ntok), _ptr(enc), _ptr(alphas), _ptr(peaks)), "pfm_run")
         return dict(tokens=tokens, ntok=ntok, enc=enc, alphas=alphas, peaks=peaks)
+
+    def run_ctc(self, feats, lens, query, mode="exact", ban_token: int = -1, L_cap: Optional[int] = None,
+                want_enc=False, want_frames=False):
+        """SenseVoice: feats [B,T,in] f32 cuda, lens [B] int32 cuda, query 4 ints -> dict of cuda tensors
+        (tokens [B, L_cap] collapsed CTC ids, ntok [B]; enc [B,T+4,D], frame_ids [B,T+4] on request)."""
+        torch = self.torch
+        if not isinstance(self.cfg, SenseVoiceConfig):
+            raise PfmError("run_ctc needs a SenseVoice engine")
+        dev = torch.device("cuda", self.device)
+        if feats.device != dev or feats.dtype != torch.float32 or not feats.is_contiguous():
+            feats = feats.to(device=dev, dtype=torch.float32).contiguous()
+        lens = lens.reshape(-1).to(device=dev, dtype=torch.int32).contiguous()
+        B, T, I = feats.shape
+        if I != self.cfg.input_size:
+            raise PfmError(f"feature dim {I} != input_size {self.cfg.input_size}")
+        if lens.numel() != B:
+            raise PfmError("lens must have one entry per utterance")
+        q = [int(x) for x in query]
+        if len(q) != 4:
+            raise PfmError("query must hold 4 embedding ids [language, event, emotion, textnorm]")
+        L_cap = T + 4 if L_cap is None else int(L_cap)
+        tokens = torch.empty((B, max(L_cap, 1)), dtype=torch.int32, device=dev)
+        ntok = torch.empty((B,), dtype=torch.int32, device=dev)
+        enc = torch.empty((B, T + 4, self.cfg.d_model), dtype=torch.float32, device=dev) if want_enc else None
+        frames = torch.empty((B, T + 4), dtype=torch.int32, device=dev) if want_frames else None
+        qa = (ctypes.c_int32 * 4)(*q)
+        m = MODES[mode] if isinstance(mode, str) else int(mode)
+        check(self.lib.pfm_run_ctc(self.h, _stream_ptr(torch, dev), m, _ptr(feats), _ptr(lens), B, T, qa,
+                                   int(ban_token), _ptr(tokens), L_cap, _ptr(ntok), _ptr(enc), _ptr(frames)),
+              "pfm_run_ctc")
+        return dict(tokens=tokens, ntok=ntok, enc=enc, frame_ids=frames)
 
     def fbank(self, wav, nsamp, cmvn=None):
         """wav [B,S] f32 cuda in [-1,1), nsamp [B] int32 -> (feats [B,T,560], T_out [B])."""
@@ -301,3 +343,17 @@ def op_cif(alphas, hidden, L_cap):
     check(lib.pfm_op_cif(_stream_ptr(torch, hidden.device), _ptr(alphas), _ptr(hidden), _ptr(emb), _ptr(peaks),
                          _ptr(nf), _ptr(nt), B, T1 - 1, D, L_cap), "pfm_op_cif")
     return emb, peaks, nf, nt
+
+
+def op_ctc_collapse(ids, olen, blank=0, L_cap=None):
+    """Greedy CTC collapse of int32 frame ids [B, T] (first olen[b] valid) -> (tokens [B, L_cap], ntok [B])."""
+    import torch
+    lib = load_library()
+    ids = ids.to(torch.int32).contiguous()
+    B, T = ids.shape
+    L_cap = T if L_cap is None else int(L_cap)
+    tokens = torch.empty((B, max(L_cap, 1)), dtype=torch.int32, device=ids.device)
+    ntok = torch.empty((B,), dtype=torch.int32, device=ids.device)
+    check(lib.pfm_op_ctc_collapse(_stream_ptr(torch, ids.device), _ptr(ids), T, _ptr(olen.to(torch.int32).contiguous()),
+                                  B, int(blank), _ptr(tokens), L_cap, _ptr(ntok)), "pfm_op_ctc_collapse")
+    return tokens, ntok

@@ -21,16 +21,18 @@ from typing import Dict, Iterator, List, Tuple
 
 import numpy as np
 
-from .config import ParaformerConfig
+from .config import ParaformerConfig, SenseVoiceConfig
 
 Shape = Tuple[int, ...]
 
 
-def param_layout(cfg: ParaformerConfig) -> List[Tuple[str, Shape, int]]:
+def param_layout(cfg) -> List[Tuple[str, Shape, int]]:
     """(key, shape, fan_in) for every parameter, in state_dict order.
 
-    fan_in == 0 marks LayerNorm gamma ('ln_w') / beta ('ln_b') via negative codes.
+    Negative fan_in codes: -1 LayerNorm gamma, -2 LayerNorm beta, -3 embedding table.
     """
+    if isinstance(cfg, SenseVoiceConfig):
+        return sense_voice_layout(cfg)
     D, F, K, I, V = cfg.d_model, cfg.ffn, cfg.kernel_size, cfg.input_size, cfg.vocab_size
     out: List[Tuple[str, Shape, int]] = []
 
@@ -85,6 +87,35 @@ def param_layout(cfg: ParaformerConfig) -> List[Tuple[str, Shape, int]]:
     return out
 
 
+def _enc_layer(out, p: str, din: int, D: int, F: int, K: int):
+    """EncoderLayerSANM parameters (sanm/encoder.py:72-148 == sense_voice/model.py:301-327)."""
+    out += [(f"{p}.self_attn.linear_out.weight", (D, D), D), (f"{p}.self_attn.linear_out.bias", (D,), D),
+            (f"{p}.self_attn.linear_q_k_v.weight", (3 * D, din), din),
+            (f"{p}.self_attn.linear_q_k_v.bias", (3 * D,), din),
+            (f"{p}.self_attn.fsmn_block.weight", (D, 1, K), K),
+            (f"{p}.feed_forward.w_1.weight", (F, D), D), (f"{p}.feed_forward.w_1.bias", (F,), D),
+            (f"{p}.feed_forward.w_2.weight", (D, F), F), (f"{p}.feed_forward.w_2.bias", (D,), F),
+            (f"{p}.norm1.weight", (din,), -1), (f"{p}.norm1.bias", (din,), -2),
+            (f"{p}.norm2.weight", (D,), -1), (f"{p}.norm2.bias", (D,), -2)]
+
+
+def sense_voice_layout(cfg: SenseVoiceConfig) -> List[Tuple[str, Shape, int]]:
+    """SenseVoiceSmall state_dict keys (sense_voice/model.py:445-663; ctc/ctc.py:33):
+    encoder.{encoders0.0, encoders.*, tp_encoders.*}, after_norm, tp_norm, ctc.ctc_lo, embed."""
+    D, F, K, I, V = cfg.d_model, cfg.ffn, cfg.kernel_size, cfg.input_size, cfg.vocab_size
+    out: List[Tuple[str, Shape, int]] = []
+    _enc_layer(out, "encoder.encoders0.0", I, D, F, K)
+    for i in range(cfg.enc_blocks - 1):
+        _enc_layer(out, f"encoder.encoders.{i}", D, D, F, K)
+    for i in range(cfg.tp_blocks):
+        _enc_layer(out, f"encoder.tp_encoders.{i}", D, D, F, K)
+    out += [("encoder.after_norm.weight", (D,), -1), ("encoder.after_norm.bias", (D,), -2),
+            ("encoder.tp_norm.weight", (D,), -1), ("encoder.tp_norm.bias", (D,), -2),
+            ("ctc.ctc_lo.weight", (V, D), D), ("ctc.ctc_lo.bias", (V,), D),
+            ("embed.weight", (cfg.n_embed, I), -3)]
+    return out
+
+
 def _stream(seed: int, key: str) -> np.random.Generator:
     return np.random.Generator(np.random.PCG64([seed & 0xFFFFFFFF, zlib.crc32(key.encode())]))
 
@@ -98,20 +129,21 @@ def gen_tensor(seed: int, key: str, shape: Shape, fan_in: int) -> np.ndarray:
         a = np.float32(1.0) + np.float32(0.1) * u
     elif fan_in == -2:          # LayerNorm beta
         a = np.float32(0.1) * u
-    else:                       # embedding table (unused at inference)
+    else:                       # embedding tables: U(-1, 1)
         a = u
     return a.astype(np.float32).reshape(shape)
 
 
-def iter_weights(cfg: ParaformerConfig, seed: int = 0) -> Iterator[Tuple[str, np.ndarray]]:
+def iter_weights(cfg, seed: int = 0) -> Iterator[Tuple[str, np.ndarray]]:
     for key, shape, fan_in in param_layout(cfg):
         yield key, gen_tensor(seed, key, shape, fan_in)
 
 
-def make_weights(cfg: ParaformerConfig, seed: int = 0) -> Dict[str, np.ndarray]:
-    """Full synthetic state_dict as fp32 numpy arrays (220.08M params for Paraformer-large)."""
+def make_weights(cfg, seed: int = 0) -> Dict[str, np.ndarray]:
+    """Full synthetic state_dict as fp32 numpy arrays (220.08M params for Paraformer-large;
+    SenseVoiceSmall layout when cfg is a SenseVoiceConfig)."""
     return dict(iter_weights(cfg, seed))
 
 
-def num_params(cfg: ParaformerConfig) -> int:
+def num_params(cfg) -> int:
     return int(sum(int(np.prod(s)) for _, s, _ in param_layout(cfg)))

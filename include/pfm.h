@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define PFM_ABI_VERSION 1
+#define PFM_ABI_VERSION 2
 
 enum pfm_status {
     PFM_OK = 0,
@@ -46,9 +46,15 @@ enum pfm_dtype { PFM_F32 = 0, PFM_BF16 = 1 };
  *         softmax statistics and CIF — the throughput mode.                              */
 enum pfm_mode { PFM_MODE_EXACT = 0, PFM_MODE_FAST = 1 };
 
+/* Model family of a handle.
+ *  PARAFORMER : SAN-M encoder + CIF predictor + SAN-M NAR decoder (funasr/models/paraformer/model.py)
+ *  SENSEVOICE : SenseVoiceSmall — 4 query rows + SAN-M encoder + tp encoder + CTC head
+ *               (funasr/models/sense_voice/model.py:445-950); decoder / predictor fields ignored */
+enum pfm_arch { PFM_ARCH_PARAFORMER = 0, PFM_ARCH_SENSEVOICE = 1 };
+
 /* Model dimensions; mirrors encoder_conf / decoder_conf / predictor_conf of
  * funasr/models/paraformer/template.yaml:8-66 (Paraformer-large defaults via
- * pfm_config_default). */
+ * pfm_config_default; SenseVoiceSmall via pfm_config_sensevoice). */
 typedef struct pfm_config {
     int32_t input_size;      /* 560 = 80 mel x lfr_m 7 */
     int32_t d_model;         /* 512 */
@@ -66,13 +72,19 @@ typedef struct pfm_config {
     float tail_threshold;    /* 0.45 */
     float smooth_factor;     /* 1.0 */
     float noise_threshold;   /* 0.0 */
-    float ln_eps;            /* 1e-12 */
+    float ln_eps;            /* 1e-12 (Paraformer, transformer/layer_norm.py:24); 1e-5 (SenseVoice) */
+    int32_t arch;            /* pfm_arch */
+    int32_t tp_blocks;       /* SenseVoice: 20 tp_encoders (sense_voice/model.py:529-540) */
+    int32_t n_embed;         /* SenseVoice: 16 rows of the query Embedding (model.py:646-648) */
 } pfm_config;
 
 typedef struct pfm_handle pfm_handle;
 
 /* Paraformer-large defaults. */
 void pfm_config_default(pfm_config* cfg);
+
+/* SenseVoiceSmall defaults: d 512, 4 heads, FFN 2048, 50 + 20 blocks, vocab 25055, eps 1e-5. */
+void pfm_config_sensevoice(pfm_config* cfg);
 
 /* Create a handle on HIP device `device`. Replaces the model construction of
  * AutoModel.build_model (funasr/auto/auto_model.py:176-293). */
@@ -109,6 +121,24 @@ int pfm_reserve(pfm_handle* h, int B, int T);
 int pfm_run(pfm_handle* h, void* stream, int mode, const float* feats, const int32_t* lens,
             int B, int T, int32_t* tokens, int L_cap, int32_t* ntok, float* enc_out,
             float* alphas, float* peaks);
+
+/* SenseVoiceSmall inference on an fbank batch — SenseVoiceSmall.inference for
+ * data_type="fbank" (sense_voice/model.py:809-906) up to token_int: query rows, encoder,
+ * tp encoder, ctc_lo, per-frame argmax (log_softmax is monotone), unique_consecutive and
+ * blank removal. Handle must be PFM_ARCH_SENSEVOICE.
+ *   feats   [B, T, input_size] f32; lens [B] int32 valid frames (1..T)
+ *   query   4 HOST int32: embed rows [language, event, emotion, textnorm] prepended to every
+ *           utterance (lid_dict / 1 / 2 / textnorm_dict of model.py:638-656)
+ *   ban_token  vocabulary id excluded from the argmax (ban_emo_unk: 25009) or -1
+ *   tokens  [B, L_cap] int32 out: collapsed CTC token ids (blank removed), -1 beyond ntok[b]
+ *   ntok    [B] int32 out: tokens per utterance (may exceed L_cap: then tokens is truncated)
+ * Optional outputs (NULL to skip):
+ *   enc_out    [B, T+4, d_model] f32 encoder output (after tp_norm)
+ *   frame_ids  [B, T+4] int32 per-frame argmax (-1 beyond lens[b] + 4)
+ * No host synchronisation. */
+int pfm_run_ctc(pfm_handle* h, void* stream, int mode, const float* feats, const int32_t* lens,
+                int B, int T, const int32_t* query, int ban_token, int32_t* tokens, int L_cap,
+                int32_t* ntok, float* enc_out, int32_t* frame_ids);
 
 /* Kaldi fbank (80 mel, 25/10 ms, hamming, dither 0, snip_edges) -> LFR (7, 6) -> CMVN for a
  * batch of waveforms: WavFrontend.forward (funasr/frontends/wav_frontend.py:118-158).
@@ -181,6 +211,11 @@ int pfm_op_fsmn_bf16(void* stream, const void* v, const int32_t* len, const floa
  * (row T zero): emb [B, L_cap, D], peaks [B, T+1], n_fire [B], ntok [B]. */
 int pfm_op_cif(void* stream, const float* alphas, const float* hidden, float* emb, float* peaks,
                int32_t* n_fire, int32_t* ntok, int B, int T, int D, int L_cap);
+
+/* Greedy CTC collapse of frame ids [B, ld] (first olen[b] valid): unique_consecutive then drop
+ * `blank` -> tokens [B, L_cap] (-1 padded), ntok [B]. Same kernel pfm_run_ctc uses. */
+int pfm_op_ctc_collapse(void* stream, const int32_t* ids, int64_t ld, const int32_t* olen, int B, int blank,
+                        int32_t* tokens, int L_cap, int32_t* ntok);
 
 #ifdef __cplusplus
 }

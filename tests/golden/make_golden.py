@@ -268,6 +268,112 @@ def save_automodel_tiny_ts():
     print("automodel ts:", [(r["text"][:12], r["timestamp"][:2]) for r in res])
 
 
+# ---------------------------------------------------------------- SenseVoiceSmall (config C4)
+class _IdTokenizer:
+    """decode(ids) -> "id id id": lets the reference's tokenizer.decode call return token_int."""
+
+    def decode(self, ids):
+        return " ".join(str(int(i)) for i in ids)
+
+
+def build_sv_ref(cfg, bias_boost=None):
+    import funasr.models.sense_voice.model  # noqa: F401
+    kw = cfg.reference_kwargs()
+    m = tables.model_classes["SenseVoiceSmall"](encoder=kw["encoder"], encoder_conf=kw["encoder_conf"],
+                                                input_size=cfg.input_size, vocab_size=cfg.vocab_size)
+    sd = {k: torch.from_numpy(v) for k, v in make_weights(cfg, seed=0).items()}
+    if bias_boost:
+        b = sd["ctc.ctc_lo.bias"].clone()
+        for tok, add in bias_boost.items():
+            b[tok] += add
+        sd["ctc.ctc_lo.bias"] = b
+    m.load_state_dict(sd, strict=True)
+    m.eval()
+    return m
+
+
+@torch.no_grad()
+def run_sv_ref(m, feats, lens, **opts):
+    """Reference SenseVoiceSmall.inference (data_type fbank) + hooks on encoder / ctc_lo outputs."""
+    cap = {}
+    h1 = m.encoder.register_forward_hook(lambda mod, i, o: cap.__setitem__("enc", o))
+    h2 = m.ctc.ctc_lo.register_forward_hook(lambda mod, i, o: cap.__setitem__("logits", o))
+    try:
+        res, _ = m.inference(torch.from_numpy(feats.copy()), data_lengths=torch.from_numpy(lens.astype(np.int64)),
+                             key=[f"utt{i}" for i in range(len(lens))], tokenizer=_IdTokenizer(),
+                             data_type="fbank", device="cpu", **opts)
+    finally:
+        h1.remove()
+        h2.remove()
+    enc, olens = cap["enc"]
+    logp = torch.log_softmax(cap["logits"], dim=2)
+    if opts.get("ban_emo_unk"):
+        logp[:, :, m.emo_dict["unk"]] = -float("inf")
+    tokens = [[int(t) for t in r["text"].split()] for r in res]
+    return dict(enc=enc.numpy(), enc_lens=olens.numpy(), logp=logp.numpy(), tokens=tokens,
+                frame_ids=logp.argmax(-1).numpy().astype(np.int32))
+
+
+def _frame_margin(logp, olens):
+    out = []
+    for b in range(logp.shape[0]):
+        r = np.sort(logp[b, : olens[b]], axis=-1)
+        out.append(r[:, -1] - r[:, -2])
+    return np.concatenate(out).astype(np.float32)
+
+
+def save_sv_tiny():
+    """SenseVoice tiny (3 + 2 blocks): full encoder output; option / bias-boost variants pin the
+    query rows, ban_emo_unk and the CTC collapse (blank-heavy frames)."""
+    from funasr_amd.config import sense_voice_tiny
+    cfg = sense_voice_tiny()
+    feats, lens = fbank_input(seed=21, B=2, T=40, lens=[40, 27])
+    out = dict(seed=21, B=2, T=40, lens=lens)
+    m = build_sv_ref(cfg)
+    r = run_sv_ref(m, feats, lens)
+    flat, off = pack_tokens(r["tokens"])
+    out.update(enc=r["enc"], enc_lens=r["enc_lens"], frame_ids=r["frame_ids"], tokens=flat, tokens_off=off,
+               logp_rows=np.stack([r["logp"][0, 0], r["logp"][0, 5], r["logp"][1, 30]]),
+               margin=_frame_margin(r["logp"], r["enc_lens"]))
+    r = run_sv_ref(m, feats, lens, language="zh", use_itn=True)
+    flat, off = pack_tokens(r["tokens"])
+    out.update(zh_itn_tokens=flat, zh_itn_off=off, zh_itn_frame_ids=r["frame_ids"])
+    # blank-heavy variant: bias of blank raised so roughly half the frames emit blank
+    mb = build_sv_ref(cfg, bias_boost={0: 2.5})
+    r = run_sv_ref(mb, feats, lens, language="en", text_norm="withitn")
+    flat, off = pack_tokens(r["tokens"])
+    out.update(blank_tokens=flat, blank_off=off, blank_frame_ids=r["frame_ids"],
+               blank_margin=_frame_margin(r["logp"], r["enc_lens"]))
+    # emo-unk variant: token 25009 dominates every frame unless banned
+    me = build_sv_ref(cfg, bias_boost={25009: 50.0})
+    r = run_sv_ref(me, feats, lens)
+    out.update(emo_tokens=pack_tokens(r["tokens"])[0], emo_off=pack_tokens(r["tokens"])[1])
+    r = run_sv_ref(me, feats, lens, ban_emo_unk=True)
+    flat, off = pack_tokens(r["tokens"])
+    out.update(ban_tokens=flat, ban_off=off, ban_frame_ids=r["frame_ids"])
+    np.savez_compressed(f"{HERE}/sv_tiny.npz", **out)
+    print("sv_tiny tokens", [len(t) for t in r["tokens"]], "blank frac",
+          float((out["blank_frame_ids"] == 0).mean()), "emo", out["emo_tokens"][:6])
+
+
+def save_sv_large():
+    from funasr_amd.config import sense_voice_small
+    m = build_sv_ref(sense_voice_small())
+    for name, seed, B, T, ln in [("sv_large_ragged", 4, 3, 500, [500, 431, 83]), ("sv_large_c1", 5, 1, 83, [83])]:
+        feats, lens = fbank_input(seed=seed, B=B, T=T, lens=ln)
+        r = run_sv_ref(m, feats, lens)
+        flat, off = pack_tokens(r["tokens"])
+        enc, ol = r["enc"], r["enc_lens"]
+        rows = np.stack([enc[b, [0, 3, 4, int(ol[b]) // 2, int(ol[b]) - 1]] for b in range(B)])
+        valid = np.arange(enc.shape[1])[None, :] < ol[:, None]
+        csum = np.array([enc[b][valid[b]].astype(np.float64).sum() for b in range(B)])
+        csq = np.array([(enc[b][valid[b]].astype(np.float64) ** 2).sum() for b in range(B)])
+        np.savez_compressed(f"{HERE}/{name}.npz", seed=seed, B=B, T=T, lens=lens, enc_rows=rows, enc_sum=csum,
+                            enc_sumsq=csq, enc_lens=ol, frame_ids=r["frame_ids"], tokens=flat, tokens_off=off,
+                            margin=_frame_margin(r["logp"], ol))
+        print(name, "tokens", [len(t) for t in r["tokens"]], "min margin", _frame_margin(r["logp"], ol).min())
+
+
 if __name__ == "__main__" and len(sys.argv) > 1:
     torch.manual_seed(0)
     for part in sys.argv[1:]:

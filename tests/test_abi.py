@@ -79,3 +79,15 @@ def test_product_path_does_not_import_oracle():
             if f.endswith((".py", ".hip", ".h", ".cpp")):
                 txt = open(os.path.join(dirpath, f), encoding="utf-8").read()
                 assert "oracle" not in re.sub(r"#.*|//.*", "", txt).replace("oracle/", ""), f
+
+
+def test_config_sensevoice_is_sensevoice_small():
+    lib = rt.load_library()
+    c = rt.PfmConfig()
+    lib.pfm_config_sensevoice(ctypes.byref(c))
+    from funasr_amd.config import sense_voice_small
+    want = rt.PfmConfig.from_config(sense_voice_small())
+    for name in ("input_size", "d_model", "heads", "ffn", "enc_blocks", "kernel_size", "enc_sanm_shift", "vocab_size",
+                 "ln_eps", "arch", "tp_blocks", "n_embed"):
+        assert getattr(c, name) == pytest.approx(getattr(want, name)), name
+    assert c.arch == rt.ARCH_SENSEVOICE and c.dec_blocks == 0

@@ -1,0 +1,192 @@
+"""SenseVoiceSmall (BASELINE config C4) through the C-ABI (pfm_run_ctc) against goldens captured
+from the reference SenseVoiceSmall.inference (tests/golden/make_golden.py sv_tiny / sv_large).
+
+EXACT mode (f32 MFMA): encoder rel-L2 <= 1e-5 (tiny, full tensors), row slices <= 1e-4 abs (large),
+per-frame argmax identical wherever the reference's top-2 log-prob margin is >= 1e-4 (f32 rounding
+of a different summation order can only flip closer frames), and token ids identical.
+FAST mode (bf16 MFMA, f32 accumulate/residual): encoder rel-L2 <= 2e-2, frame agreement reported
+and floored (random weights leave small CTC margins).
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from funasr_amd.config import sense_voice_small, sense_voice_tiny  # noqa: E402
+from funasr_amd.runtime import PfmEngine, op_ctc_collapse  # noqa: E402
+from funasr_amd.weights import make_weights  # noqa: E402
+from tests.golden.inputs import fbank_input  # noqa: E402
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+MARGIN = 1e-4
+
+
+def _tok(g, flat="tokens", off="tokens_off"):
+    o = g[off]
+    return [g[flat][o[i]:o[i + 1]].tolist() for i in range(len(o) - 1)]
+
+
+def _weights(cfg, boost=None):
+    w = make_weights(cfg, seed=0)
+    if boost:
+        b = w["ctc.ctc_lo.bias"].copy()
+        for t, a in boost.items():
+            b[t] += np.float32(a)
+        w["ctc.ctc_lo.bias"] = b
+    return w
+
+
+def _query(cfg, language="auto", use_itn=False, text_norm=None):
+    if text_norm is None:
+        text_norm = "withitn" if use_itn else "woitn"
+    return [cfg.lid_dict.get(language, 0), 1, 2, cfg.textnorm_dict[text_norm]]
+
+
+def _run(e, g, mode, **kw):
+    x, l = fbank_input(int(g["seed"]), int(g["B"]), int(g["T"]), g["lens"])
+    q = _query(e.cfg, **{k: v for k, v in kw.items() if k != "ban"})
+    return e.run_ctc(torch.from_numpy(x).cuda(), torch.from_numpy(l).cuda(), q, mode=mode,
+                     ban_token=e.cfg.emo_unk if kw.get("ban") else -1, want_enc=True, want_frames=True)
+
+
+def _tokens(r):
+    toks, nt = r["tokens"].cpu().numpy(), r["ntok"].cpu().numpy()
+    return [toks[b, : nt[b]].tolist() for b in range(toks.shape[0])]
+
+
+def _frames_close(fr, g_fr, lens, margin):
+    """Frame argmax equal on every frame whose reference margin >= MARGIN; returns #close-call flips."""
+    flips, k = 0, 0
+    for b in range(len(lens)):
+        n = int(lens[b]) + 4
+        a, w = fr[b, :n], g_fr[b, :n]
+        m = margin[k:k + n]
+        k += n
+        bad = a != w
+        assert not np.any(bad & (m >= MARGIN)), (b, np.nonzero(bad & (m >= MARGIN))[0][:10])
+        flips += int(bad.sum())
+        assert np.all(fr[b, n:] == -1)
+    return flips
+
+
+@pytest.fixture(scope="module")
+def sv():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    out = {}
+    for name, cfg in (("tiny", sense_voice_tiny()), ("large", sense_voice_small())):
+        e = PfmEngine(cfg, 0)
+        e.load_state_dict(make_weights(cfg, seed=0))
+        out[name] = e
+    return out
+
+
+def test_tiny_exact_full_tensors(sv):
+    e = sv["tiny"]
+    g = np.load(f"{GOLD}/sv_tiny.npz")
+    r = _run(e, g, "exact")
+    torch.cuda.synchronize()
+    enc = r["enc"].cpu().numpy()
+    for b, n in enumerate(g["enc_lens"]):
+        d = enc[b, :n] - g["enc"][b, :n]
+        assert np.linalg.norm(d) / np.linalg.norm(g["enc"][b, :n]) < 1e-5
+    assert _frames_close(r["frame_ids"].cpu().numpy(), g["frame_ids"], g["lens"], g["margin"]) == 0
+    assert _tokens(r) == _tok(g)
+    r = _run(e, g, "exact", language="zh", use_itn=True)
+    assert _tokens(r) == _tok(g, "zh_itn_tokens", "zh_itn_off")
+
+
+def test_tiny_exact_blank_heavy_and_ban(sv):
+    """Blank-dominated frames exercise the collapse; a +50 bias on <|unk|> emotion (25009) makes it every
+    frame's argmax unless ban_emo_unk excludes it (model.py:885-886)."""
+    cfg = sense_voice_tiny()
+    g = np.load(f"{GOLD}/sv_tiny.npz")
+    e = PfmEngine(cfg, 0)
+    e.load_state_dict(_weights(cfg, {0: 2.5}))
+    r = _run(e, g, "exact", language="en", text_norm="withitn")
+    torch.cuda.synchronize()
+    _frames_close(r["frame_ids"].cpu().numpy(), g["blank_frame_ids"], g["lens"], g["blank_margin"])
+    assert _tokens(r) == _tok(g, "blank_tokens", "blank_off")
+    e.load_state_dict(_weights(cfg, {25009: 50.0}))
+    assert _tokens(_run(e, g, "exact")) == _tok(g, "emo_tokens", "emo_off")
+    r = _run(e, g, "exact", ban=True)
+    assert _tokens(r) == _tok(g, "ban_tokens", "ban_off")
+    assert not np.any(r["frame_ids"].cpu().numpy() == 25009)
+    r = _run(e, g, "fast", ban=True)
+    assert not np.any(r["frame_ids"].cpu().numpy() == 25009)
+
+
+@pytest.mark.parametrize("name", ["sv_large_ragged", "sv_large_c1"])
+def test_large_exact(sv, name):
+    e = sv["large"]
+    g = np.load(f"{GOLD}/{name}.npz")
+    r = _run(e, g, "exact")
+    torch.cuda.synchronize()
+    enc = r["enc"].cpu().numpy()
+    ol = g["enc_lens"]
+    rows = np.stack([enc[b, [0, 3, 4, int(ol[b]) // 2, int(ol[b]) - 1]] for b in range(len(ol))])
+    assert np.abs(rows - g["enc_rows"]).max() < 1e-4
+    for b in range(len(ol)):
+        s = enc[b, : int(ol[b])].astype(np.float64)
+        assert abs((s ** 2).sum() - g["enc_sumsq"][b]) < 1e-5 * g["enc_sumsq"][b]
+    flips = _frames_close(r["frame_ids"].cpu().numpy(), g["frame_ids"], g["lens"], g["margin"])
+    print(f"{name}: exact-mode close-call frame flips {flips}")
+    if flips == 0:
+        assert _tokens(r) == _tok(g)
+
+
+@pytest.mark.parametrize("name", ["sv_large_ragged"])
+def test_large_fast_agreement(sv, name):
+    e = sv["large"]
+    g = np.load(f"{GOLD}/{name}.npz")
+    r = _run(e, g, "fast")
+    torch.cuda.synchronize()
+    enc = r["enc"].cpu().numpy()
+    ol = g["enc_lens"]
+    rows = np.stack([enc[b, [0, 3, 4, int(ol[b]) // 2, int(ol[b]) - 1]] for b in range(len(ol))])
+    rel = np.linalg.norm(rows - g["enc_rows"]) / np.linalg.norm(g["enc_rows"])
+    assert rel < 2e-2, rel
+    fr = r["frame_ids"].cpu().numpy()
+    agree = np.mean(np.concatenate([fr[b, : ol[b]] == g["frame_ids"][b, : ol[b]] for b in range(len(ol))]))
+    print(f"SenseVoice fast-mode frame agreement {agree:.4f}, enc rows rel {rel:.2e}")
+    assert agree > 0.6
+
+
+def test_ctc_collapse_op_matches_unique_consecutive():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    """unique_consecutive + drop blank on frames with long repeats, blanks, ragged lengths, an empty
+    utterance and L_cap truncation (sense_voice/model.py:894-906)."""
+    rng = np.random.default_rng(3)
+    B, T = 6, 700
+    ids = rng.integers(0, 5, size=(B, T)).astype(np.int32)
+    ids[1] = np.repeat(rng.integers(0, 3, size=T // 7), 7)   # runs of 7 equal ids
+    ids[2] = 0
+    ids[3, ::2] = 0
+    olen = np.array([700, 699, 650, 64, 0, 65], dtype=np.int32)
+    want = []
+    for b in range(B):
+        y = torch.unique_consecutive(torch.from_numpy(ids[b, : olen[b]]))
+        want.append(y[y != 0].tolist())
+    tok, nt = op_ctc_collapse(torch.from_numpy(ids).cuda(), torch.from_numpy(olen).cuda(), blank=0, L_cap=T)
+    tok, nt = tok.cpu().numpy(), nt.cpu().numpy()
+    for b in range(B):
+        assert nt[b] == len(want[b])
+        assert tok[b, : nt[b]].tolist() == want[b]
+        assert np.all(tok[b, nt[b]:] == -1)
+    tok, nt = op_ctc_collapse(torch.from_numpy(ids).cuda(), torch.from_numpy(olen).cuda(), blank=0, L_cap=10)
+    tok, nt = tok.cpu().numpy(), nt.cpu().numpy()
+    for b in range(B):
+        assert nt[b] == len(want[b])
+        assert tok[b].tolist() == (want[b] + [-1] * 10)[:10]
+
+
+def test_sensevoice_deterministic(sv):
+    e = sv["large"]
+    g = np.load(f"{GOLD}/sv_large_c1.npz")
+    r1, r2 = _run(e, g, "fast"), _run(e, g, "fast")
+    torch.cuda.synchronize()
+    assert torch.equal(r1["tokens"], r2["tokens"]) and torch.equal(r1["enc"], r2["enc"])

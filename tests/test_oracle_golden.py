@@ -89,3 +89,56 @@ def test_knf_binary_matches_fixture_when_buildable():
         subprocess.run([exe, f"{d}/i", f"{d}/o"], check=True)
         out = np.fromfile(f"{d}/o", dtype=np.float32).reshape(-1, 80)
     assert np.array_equal(out, g["syn4_fbank"])
+
+
+# ---------------------------------------------------------------- SenseVoiceSmall (config C4)
+def _tok(g, flat, off):
+    o = g[off]
+    return [g[flat][o[i]:o[i + 1]].tolist() for i in range(len(o) - 1)]
+
+
+def _sv_weights(cfg, boost=None):
+    w = make_weights(cfg, seed=0)
+    if boost:
+        b = w["ctc.ctc_lo.bias"].copy()
+        for t, a in boost.items():
+            b[t] += np.float32(a)
+        w["ctc.ctc_lo.bias"] = b
+    return w
+
+
+def test_sensevoice_tiny_vs_reference():
+    from funasr_amd.config import sense_voice_tiny
+    from oracle.sensevoice_ref import sensevoice_infer
+    g = np.load(f"{GOLD}/sv_tiny.npz")
+    cfg = sense_voice_tiny()
+    x, lens = fbank_input(int(g["seed"]), int(g["B"]), int(g["T"]), g["lens"])
+    w = _sv_weights(cfg)
+    r = sensevoice_infer(x, lens, w, cfg, keep_logits=True)
+    assert np.abs(r["enc"].numpy() - g["enc"]).max() < 1e-5
+    assert np.array_equal(r["enc_lens"].numpy(), g["enc_lens"])
+    lp = r["logp"].numpy()
+    assert np.abs(np.stack([lp[0, 0], lp[0, 5], lp[1, 30]]) - g["logp_rows"]).max() < 1e-4
+    assert np.array_equal(r["frame_ids"].numpy(), g["frame_ids"])
+    assert r["tokens"] == _tok(g, "tokens", "tokens_off")
+    r = sensevoice_infer(x, lens, w, cfg, language="zh", use_itn=True)
+    assert r["tokens"] == _tok(g, "zh_itn_tokens", "zh_itn_off")
+    r = sensevoice_infer(x, lens, _sv_weights(cfg, {0: 2.5}), cfg, language="en", text_norm="withitn")
+    assert r["tokens"] == _tok(g, "blank_tokens", "blank_off")
+    we = _sv_weights(cfg, {25009: 50.0})
+    assert sensevoice_infer(x, lens, we, cfg)["tokens"] == _tok(g, "emo_tokens", "emo_off")
+    assert sensevoice_infer(x, lens, we, cfg, ban_emo_unk=True)["tokens"] == _tok(g, "ban_tokens", "ban_off")
+
+
+@pytest.mark.parametrize("name", ["sv_large_ragged", "sv_large_c1"])
+def test_sensevoice_large_vs_reference(name):
+    from funasr_amd.config import sense_voice_small
+    from oracle.sensevoice_ref import sensevoice_infer
+    g = np.load(f"{GOLD}/{name}.npz")
+    x, lens = fbank_input(int(g["seed"]), int(g["B"]), int(g["T"]), g["lens"])
+    torch.set_num_threads(min(8, os.cpu_count() or 1))
+    r = sensevoice_infer(x, lens, make_weights(sense_voice_small(), seed=0), sense_voice_small())
+    assert r["tokens"] == _tok(g, "tokens", "tokens_off")
+    enc, ol = r["enc"].numpy(), r["enc_lens"].numpy()
+    rows = np.stack([enc[b, [0, 3, 4, int(ol[b]) // 2, int(ol[b]) - 1]] for b in range(len(lens))])
+    assert np.abs(rows - g["enc_rows"]).max() < 1e-5
