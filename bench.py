@@ -44,6 +44,12 @@ def path_flops(T: int, L: np.ndarray) -> float:
     return float(np.sum(333634560.0 * T + 102400.0 * T * T + 96866304.0 * L + 32768.0 * L * T))
 
 
+def sensevoice_flops(Tq: int, V: int = 25055, blocks: int = 70) -> float:
+    """SenseVoiceSmall per utterance of Tq = T + 4 frames: per SAN-M layer 6,291,456 Tq + 2,048 Tq^2
+    (QKV, out-proj, FFN, QK^T, PV), +147,456 Tq for the 560-wide layer-0 QKV, CTC head 1,024 V Tq."""
+    return blocks * (6291456.0 * Tq + 2048.0 * Tq * Tq) + 147456.0 * Tq + 1024.0 * V * Tq
+
+
 def cpu_model() -> str:
     try:
         with open("/proc/cpuinfo") as f:
@@ -66,6 +72,7 @@ def main():
     ap.add_argument("--cpu-utts", type=int, default=8, help="cpu_baseline sample size (0 = skip)")
     ap.add_argument("--exact-steps", type=int, default=2, help="timed exact-mode steps (0 = skip)")
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--sv-steps", type=int, default=3, help="timed SenseVoiceSmall (config C4) steps (0 = skip)")
     args = ap.parse_args()
 
     import torch
@@ -210,6 +217,30 @@ def main():
         out["exact_mode"] = {"value": round(B * T * FRAME_SEC / dte, 1), "ms_per_step": round(dte * 1e3, 2),
                              "dtype": "f32", "fast_vs_exact_token_agreement": round(float(np.mean(agree)), 4),
                              "fast_vs_exact_ntok_equal": round(float(np.mean(na == nb)), 4)}
+
+    # ---- SenseVoiceSmall (BASELINE config C4): B x 30 s on the same fbank batch, rank 0
+    if rank == 0 and args.sv_steps > 0:
+        from funasr_amd.config import sense_voice_small
+        scfg = sense_voice_small()
+        seng = PfmEngine(scfg, local)
+        seng.load_state_dict(make_weights(scfg, args.seed))
+        seng.reserve(B, T + 4)
+        q = [0, 1, 2, 15]   # language auto, event, emotion, woitn
+        for _ in range(2):
+            seng.run_ctc(feats, lens, q, mode=args.mode)
+        torch.cuda.synchronize()
+        tsv = time.perf_counter()
+        for _ in range(args.sv_steps):
+            sv_last = seng.run_ctc(feats, lens, q, mode=args.mode)
+        torch.cuda.synchronize()
+        dsv = (time.perf_counter() - tsv) / args.sv_steps
+        sv_tf = B * sensevoice_flops(T + 4) / dsv / 1e12
+        out["sensevoice"] = {"workload": f"SenseVoiceSmall B={B} x 30 s (T={T}+4 query rows), CTC greedy",
+                             "value": round(B * T * FRAME_SEC / dsv, 1), "unit": "audio-sec/sec",
+                             "ms_per_step": round(dsv * 1e3, 3), "dtype": out["dtype"],
+                             "path_tflops": round(sv_tf, 2), "path_frac": round(sv_tf / peak, 4),
+                             "tokens_per_utt_mean": float(sv_last["ntok"].float().mean().item())}
+        del seng
 
     # ---- CPU baseline: the oracle torch-CPU restatement on a bounded sample (rank 0, N=1 only)
     if rank == 0 and world == 1 and args.cpu_utts > 0:

@@ -1,9 +1,11 @@
-"""funasr_amd — MI355X-native (gfx950) Paraformer inference behind FunASR's AutoModel contract.
+"""funasr_amd — MI355X-native (gfx950) Paraformer / SenseVoiceSmall inference behind FunASR's
+AutoModel contract.
 
 Importing the package does not touch the GPU. Compute lives in libpfm_hip.so (C ABI,
 include/pfm.h); `funasr_amd.runtime` binds it. Build with `python -m funasr_amd.build`.
 """
-from .config import ParaformerConfig, paraformer_large, paraformer_tiny  # noqa: F401
+from .config import (ParaformerConfig, SenseVoiceConfig, paraformer_large, paraformer_tiny,  # noqa: F401
+                     sense_voice_small, sense_voice_tiny)
 from .register import tables  # noqa: F401
 
 __version__ = "0.1.0"
@@ -17,4 +19,7 @@ def __getattr__(name):
     if name == "Paraformer":
         from .model import Paraformer
         return Paraformer
+    if name == "SenseVoiceSmall":
+        from .sense_voice import SenseVoiceSmall
+        return SenseVoiceSmall
     raise AttributeError(name)

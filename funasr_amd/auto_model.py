@@ -24,9 +24,29 @@ import numpy as np
 import torch
 
 from . import model as _model  # noqa: F401  (registers "Paraformer")
+from . import sense_voice as _sense_voice  # noqa: F401  (registers "SenseVoiceSmall")
 from .frontend import WavFrontend
 from .register import tables
-from .text import CharTokenizer
+from .text import CharTokenizer, SentencepiecesTokenizer
+
+_TOKENIZERS = {"CharTokenizer": CharTokenizer, "SentencepiecesTokenizer": SentencepiecesTokenizer}
+
+
+def build_tokenizer(name, conf):
+    """tokenizer name + tokenizer_conf -> (tokenizer, vocab_size) (auto_model.py:192-248: vocab from the
+    token list, else get_vocab_size()). Without a name the conf decides: bpemodel -> sentencepiece,
+    token_list -> CharTokenizer."""
+    conf = dict(conf or {})
+    if name is None:
+        name = "SentencepiecesTokenizer" if conf.get("bpemodel") else (
+            "CharTokenizer" if conf.get("token_list") is not None else None)
+    if name is None:
+        return None, -1
+    if not isinstance(name, str) or name not in _TOKENIZERS:
+        raise ValueError(f"tokenizer {name!r} is not available (have {sorted(_TOKENIZERS)})")
+    tok = _TOKENIZERS[name](**conf)
+    vocab = tok.get_num_vocabulary_size() if hasattr(tok, "get_num_vocabulary_size") else tok.get_vocab_size()
+    return tok, vocab
 
 _CHARS = string.ascii_letters + string.digits
 _LIST_EXT = (".scp", ".txt", ".json", ".jsonl", ".text")
@@ -91,6 +111,9 @@ def _read_model_dir(path: str, kwargs: Dict[str, Any]) -> Dict[str, Any]:
     if os.path.exists(tok):
         out.setdefault("tokenizer_conf", {})
         out["tokenizer_conf"] = {**out.get("tokenizer_conf", {}), "token_list": tok}
+    bpe = out.get("tokenizer_conf", {}).get("bpemodel") if isinstance(out.get("tokenizer_conf"), dict) else None
+    if bpe and not os.path.isabs(bpe) and os.path.exists(os.path.join(path, os.path.basename(bpe))):
+        out["tokenizer_conf"] = {**out["tokenizer_conf"], "bpemodel": os.path.join(path, os.path.basename(bpe))}
     mvn = os.path.join(path, "am.mvn")
     if os.path.exists(mvn):
         out["frontend_conf"] = {**out.get("frontend_conf", {}), "cmvn_file": mvn}
@@ -129,12 +152,13 @@ class AutoModel:
             raise RuntimeError("the HIP Paraformer path needs a ROCm GPU (device='cuda[:i]'); there is no CPU path")
         kwargs["device"] = device
         torch.manual_seed(kwargs.get("seed", 0))
-        tok_conf = kwargs.get("tokenizer_conf") or {}
-        tokenizer = CharTokenizer(**tok_conf) if tok_conf.get("token_list") is not None else None
+        tok_name = kwargs.get("tokenizer") if isinstance(kwargs.get("tokenizer"), str) else None
+        tokenizer, vocab = build_tokenizer(tok_name, kwargs.get("tokenizer_conf"))
         kwargs["tokenizer"] = tokenizer
         fconf = kwargs.get("frontend_conf") or {}
         kwargs["frontend"] = WavFrontend(**fconf)
-        vocab = tokenizer.get_num_vocabulary_size() if tokenizer is not None else kwargs.get("vocab_size", -1)
+        if tokenizer is None:
+            vocab = kwargs.get("vocab_size", -1)
         model_conf = kwargs.get("model_conf") or {}
         mk = {**model_conf, **{k: v for k, v in kwargs.items() if k not in ("model_conf",)}}
         mk["vocab_size"] = vocab

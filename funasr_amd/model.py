@@ -41,12 +41,13 @@ def _as_hip_frontend(frontend):
     return fe
 
 
-@tables.register("model_classes", "Paraformer")
-class Paraformer(torch.nn.Module):
-    def __init__(self, *args, **kwargs):
-        super().__init__()
-        self.cfg = ParaformerConfig.from_kwargs(**kwargs)
-        self.blank_id, self.sos, self.eos = self.cfg.blank_id, self.cfg.sos, self.cfg.eos
+class HipModel(torch.nn.Module):
+    """Shared plugin contract of the HIP-backed model classes: reference state_dict keys and shapes,
+    a device anchor parameter, one PfmEngine (C-ABI handle) per device. Subclasses set `self.cfg`."""
+
+    family = "model"
+
+    def _init_common(self, kwargs):
         self.mode = kwargs.get("mode", "exact")
         # device anchor: AutoModel and callers read next(model.parameters()).device
         self._anchor = torch.nn.Parameter(torch.zeros(1), requires_grad=False)
@@ -67,7 +68,8 @@ class Paraformer(torch.nn.Module):
         missing = [k for k in want if k not in state_dict]
         unexpected = [k for k in state_dict if k not in want]
         if strict and (missing or unexpected):
-            raise RuntimeError(f"Paraformer.load_state_dict: missing {missing[:5]} unexpected {unexpected[:5]}")
+            raise RuntimeError(f"{type(self).__name__}.load_state_dict: missing {missing[:5]} "
+                               f"unexpected {unexpected[:5]}")
         for k, v in state_dict.items():
             if k not in want:
                 continue
@@ -84,7 +86,7 @@ class Paraformer(torch.nn.Module):
         d = self._anchor.device
         if d.type != "cuda":
             if not torch.cuda.is_available():
-                raise PfmError("Paraformer (HIP) needs a ROCm GPU; there is no CPU path in this build")
+                raise PfmError(f"{type(self).__name__} (HIP) needs a ROCm GPU; there is no CPU path in this build")
             return torch.cuda.current_device()
         return d.index if d.index is not None else torch.cuda.current_device()
 
@@ -96,9 +98,53 @@ class Paraformer(torch.nn.Module):
                 eng.load_state_dict(self._host_sd, strict=False)
             self._engine, self._engine_dev = eng, dev
         if self._engine.missing_weights:
-            raise PfmError(f"{self._engine.missing_weights} Paraformer weights not loaded "
+            raise PfmError(f"{self._engine.missing_weights} {type(self).__name__} weights not loaded "
                            "(load_state_dict / init_param)")
         return self._engine
+
+    # ---------------- shared input handling (model.py:452-493 / sense_voice/model.py:819-846) -------------
+    def _speech(self, eng, data_in, data_lengths, frontend, kwargs, meta):
+        """fbank tensor or waveforms -> (feats [B,T,560] on the device, lens [B])."""
+        if isinstance(data_in, torch.Tensor) and kwargs.get("data_type", "sound") == "fbank":
+            speech = data_in if data_in.dim() == 3 else data_in[None]
+            if data_lengths is None:
+                lens = torch.full((speech.shape[0],), speech.shape[1], dtype=torch.int32)
+            else:
+                lens = torch.as_tensor(data_lengths).reshape(-1)
+            return speech, lens
+        if frontend is None:
+            raise ValueError("waveform input needs a frontend (frontend_conf)")
+        frontend = _as_hip_frontend(frontend)
+        items = data_in if isinstance(data_in, (list, tuple)) else [data_in]
+        t1 = time.perf_counter()
+        speech, lens, _ = frontend(eng, items)
+        torch.cuda.synchronize(speech.device)
+        t2 = time.perf_counter()
+        meta["load_data"] = "0.000"
+        meta["extract_feat"] = f"{t2 - t1:0.3f}"
+        meta["batch_data_time"] = float(lens.sum().item()) * frontend.frame_shift * frontend.lfr_n / 1000
+        return speech, lens
+
+    @staticmethod
+    def _keys(key, b):
+        if key is None:
+            key = [f"utt{i}" for i in range(b)]
+        if isinstance(key[0], (list, tuple)):
+            key = key[0]
+        if len(key) < b:
+            key = key * b
+        return key
+
+
+@tables.register("model_classes", "Paraformer")
+class Paraformer(HipModel):
+    family = "paraformer"
+
+    def __init__(self, *args, **kwargs):
+        super().__init__()
+        self.cfg = ParaformerConfig.from_kwargs(**kwargs)
+        self.blank_id, self.sos, self.eos = self.cfg.blank_id, self.cfg.sos, self.cfg.eos
+        self._init_common(kwargs)
 
     # ---------------- inference (paraformer/model.py:443-596) ----------------
     @torch.no_grad()
@@ -109,24 +155,7 @@ class Paraformer(torch.nn.Module):
         eng = self.engine()
         mode = kwargs.get("mode", self.mode)
         meta = {}
-        if isinstance(data_in, torch.Tensor) and kwargs.get("data_type", "sound") == "fbank":
-            speech = data_in if data_in.dim() == 3 else data_in[None]
-            if data_lengths is None:
-                lens = torch.full((speech.shape[0],), speech.shape[1], dtype=torch.int32)
-            else:
-                lens = torch.as_tensor(data_lengths).reshape(-1)
-        else:
-            if frontend is None:
-                raise ValueError("waveform input needs a frontend (frontend_conf)")
-            frontend = _as_hip_frontend(frontend)
-            items = data_in if isinstance(data_in, (list, tuple)) else [data_in]
-            t1 = time.perf_counter()
-            speech, lens, _ = frontend(eng, items)
-            torch.cuda.synchronize(speech.device)
-            t2 = time.perf_counter()
-            meta["load_data"] = "0.000"
-            meta["extract_feat"] = f"{t2 - t1:0.3f}"
-            meta["batch_data_time"] = float(lens.sum().item()) * frontend.frame_shift * frontend.lfr_n / 1000
+        speech, lens = self._speech(eng, data_in, data_lengths, frontend, kwargs, meta)
         pred_ts = bool(kwargs.get("pred_timestamp", False))
         r = eng.run(speech, lens, mode=mode, want_alphas=pred_ts)
         toks = r["tokens"].cpu().numpy()           # one device->host copy for the whole batch
@@ -134,12 +163,7 @@ class Paraformer(torch.nn.Module):
         if pred_ts:   # CIF outputs for ts_prediction_lfr6_standard (paraformer/model.py:572-582)
             peaks_h, alphas_h = r["peaks"].cpu(), r["alphas"].cpu()
         b = toks.shape[0]
-        if key is None:
-            key = [f"utt{i}" for i in range(b)]
-        if isinstance(key[0], (list, tuple)):
-            key = key[0]
-        if len(key) < b:
-            key = key * b
+        key = self._keys(key, b)
         results = []
         for i in range(b):
             n = int(ntok[i])

@@ -58,6 +58,39 @@ class CharTokenizer:
         return self.tokens2text(self.ids2tokens(ids))
 
 
+class SentencepiecesTokenizer:
+    """BPE tokenizer over a sentencepiece model file (the SenseVoice tokenizer,
+    funasr/tokenizer/sentencepiece_tokenizer.py:12-60): decode = SentencePieceProcessor.DecodeIds."""
+
+    def __init__(self, bpemodel, **kwargs):
+        import sentencepiece as spm
+        self.bpemodel = str(bpemodel)
+        self.sp = spm.SentencePieceProcessor()
+        if not self.sp.load(self.bpemodel):
+            raise ValueError(f"cannot load sentencepiece model {self.bpemodel}")
+
+    def text2tokens(self, line: str) -> List[str]:
+        return self.sp.EncodeAsPieces(line)
+
+    def tokens2text(self, tokens: Iterable[str]) -> str:
+        return self.sp.DecodePieces(list(tokens))
+
+    def encode(self, line: str, **kwargs) -> List[int]:
+        return self.sp.EncodeAsIds(line)
+
+    def decode(self, line: List[int], **kwargs) -> str:
+        return self.sp.DecodeIds([int(i) for i in line])
+
+    def get_vocab_size(self) -> int:
+        return self.sp.GetPieceSize()
+
+    def ids2tokens(self, *args, **kwargs):
+        return self.decode(*args, **kwargs)
+
+    def tokens2ids(self, *args, **kwargs):
+        return self.encode(*args, **kwargs)
+
+
 def _strip_specials(w: str) -> str:
     w = w.replace(" ", "")
     for s in ("</s>", "<s>", "<unk>", "<OOV>"):

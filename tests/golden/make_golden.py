@@ -374,6 +374,56 @@ def save_sv_large():
         print(name, "tokens", [len(t) for t in r["tokens"]], "min margin", _frame_margin(r["logp"], ol).min())
 
 
+def make_sv_bpe(path, vocab=300):
+    """Tiny sentencepiece BPE model trained on seeded synthetic text (stands in for SenseVoice's
+    chn_jpn_yue_eng_ko_spectok.bpe.model, which cannot be fetched offline)."""
+    import io
+
+    import sentencepiece as spm
+    rng = np.random.default_rng(7)
+    syll = ["ka", "to", "ri", "me", "su", "na", "lo", "pe", "di", "gu", "ba", "ze", "ho", "vi", "qu"]
+    lines = [" ".join("".join(rng.choice(syll, size=rng.integers(1, 4))) for _ in range(rng.integers(4, 12)))
+             for _ in range(3000)]
+    model = io.BytesIO()
+    spm.SentencePieceTrainer.train(sentence_iterator=iter(lines), model_writer=model, vocab_size=vocab,
+                                   model_type="bpe", character_coverage=1.0, num_threads=1, normalization_rule_name="identity",
+                                   minloglevel=2)
+    with open(path, "wb") as f:
+        f.write(model.getvalue())
+
+
+def save_automodel_sv_tiny():
+    """Reference AutoModel.generate() with SenseVoiceSmall (tiny, vocab 300) + SentencepiecesTokenizer:
+    pins the SenseVoice result-dict contract (language / use_itn query rows, tokenizer.decode)."""
+    import funasr.models.sense_voice.model  # noqa: F401
+    import funasr.tokenizer.sentencepiece_tokenizer  # noqa: F401
+    import funasr.frontends.wav_frontend  # noqa: F401
+    from funasr.auto.auto_model import AutoModel
+    from funasr_amd.config import sense_voice_tiny
+    bpe = f"{HERE}/sv_bpe.model"
+    if not os.path.exists(bpe):
+        make_sv_bpe(bpe)
+    cfg = sense_voice_tiny(vocab_size=300)
+    kw = cfg.reference_kwargs()
+    am = AutoModel(model="SenseVoiceSmall", model_conf={}, device="cpu", ncpu=4, disable_update=True,
+                   disable_pbar=True, disable_log=True, tokenizer="SentencepiecesTokenizer",
+                   tokenizer_conf=dict(bpemodel=bpe), frontend="WavFrontend",
+                   frontend_conf=dict(fs=16000, window="hamming", n_mels=80, frame_length=25, frame_shift=10,
+                                      lfr_m=7, lfr_n=6, dither=0.0, cmvn_file=CMVN),
+                   encoder=kw["encoder"], encoder_conf=kw["encoder_conf"])
+    sd = {k: torch.from_numpy(v) for k, v in make_weights(cfg, seed=0).items()}
+    am.model.load_state_dict(sd, strict=True)
+    feats, lens = fbank_input(seed=11, B=2, T=40, lens=[40, 27])
+    out = {}
+    for tag, opts in (("auto", {}), ("en_itn", dict(language="en", use_itn=True))):
+        res = am.generate(input=torch.from_numpy(feats), input_len=torch.from_numpy(lens.astype(np.int32)),
+                          data_type="fbank", key=["uttA", "uttB"], batch_size=2, **opts)
+        out[tag] = [{k: (v if not isinstance(v, np.ndarray) else v.tolist()) for k, v in r.items()} for r in res]
+    with open(f"{HERE}/automodel_sv_tiny.json", "w") as f:
+        json.dump(out, f, ensure_ascii=False, indent=1)
+    print("automodel sv:", {k: [r["text"][:20] for r in v] for k, v in out.items()})
+
+
 if __name__ == "__main__" and len(sys.argv) > 1:
     torch.manual_seed(0)
     for part in sys.argv[1:]:

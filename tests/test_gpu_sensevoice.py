@@ -190,3 +190,53 @@ def test_sensevoice_deterministic(sv):
     r1, r2 = _run(e, g, "fast"), _run(e, g, "fast")
     torch.cuda.synchronize()
     assert torch.equal(r1["tokens"], r2["tokens"]) and torch.equal(r1["enc"], r2["enc"])
+
+
+def _sv_automodel():
+    from funasr_amd.auto_model import AutoModel
+    cfg = sense_voice_tiny(vocab_size=300)
+    kw = cfg.reference_kwargs()
+    return AutoModel(model="SenseVoiceSmall", model_conf={}, synthetic_seed=0, tokenizer="SentencepiecesTokenizer",
+                     tokenizer_conf=dict(bpemodel=os.path.join(GOLD, "sv_bpe.model")), device="cuda", mode="exact",
+                     encoder=kw["encoder"], encoder_conf=kw["encoder_conf"])
+
+
+def test_automodel_sensevoice_matches_reference_generate():
+    """AutoModel(model="SenseVoiceSmall").generate(fbank, language/use_itn) returns the reference's
+    result dicts (text = sentencepiece decode of the collapsed CTC ids)."""
+    import json
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    am = _sv_automodel()
+    feats, lens = fbank_input(seed=11, B=2, T=40, lens=[40, 27])
+    want = json.load(open(f"{GOLD}/automodel_sv_tiny.json", encoding="utf-8"))
+    for tag, opts in (("auto", {}), ("en_itn", dict(language="en", use_itn=True))):
+        res = am.generate(input=torch.from_numpy(feats), input_len=torch.from_numpy(lens), data_type="fbank",
+                          key=["uttA", "uttB"], batch_size=2, **opts)
+        assert res == want[tag], tag
+
+
+def test_automodel_sensevoice_waveform_path():
+    """Waveform input: pfm_fbank -> LFR/CMVN -> pfm_run_ctc; tokens equal the oracle's on the same
+    features except near-tie frames (the fbank agrees with knf to ~1e-4, not bit-exactly)."""
+    from oracle import fbank_ref
+    from oracle.sensevoice_ref import sensevoice_infer
+    from tests.golden.inputs import waveform
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    am = _sv_automodel()
+    wavs = [waveform(41, 16000 * 2), waveform(42, 16000 * 4 + 77)]
+    res = am.generate(input=wavs, batch_size=2, key=["a", "b"])
+    assert [r["key"] for r in res] == ["a", "b"]
+    cfg = sense_voice_tiny(vocab_size=300)
+    feats = [fbank_ref.frontend(w) for w in wavs]
+    T = max(f.shape[0] for f in feats)
+    x = np.zeros((2, T, 560), np.float32)
+    for i, f in enumerate(feats):
+        x[i, : f.shape[0]] = f
+    r = sensevoice_infer(x, np.array([f.shape[0] for f in feats]), make_weights(cfg), cfg)
+    tok = am.kwargs["tokenizer"]
+    for got, want_ids in zip([x["text"] for x in res], r["tokens"]):
+        want = tok.decode(want_ids)
+        n = min(len(got), len(want))
+        assert sum(a == b for a, b in zip(got[:n], want[:n])) >= 0.8 * max(len(got), len(want))

@@ -175,3 +175,33 @@ def test_postprocess_with_timestamps_matches_reference():
             continue
         sent, ts, words = sentence_postprocess(list(c["tokens"]), c["spans"])
         assert (sent, ts, words) == (c["sentence"], c["timestamp"], c["words"]), c["tokens"]
+
+
+def test_sensevoice_state_dict_contract_and_registry():
+    from funasr_amd import tables
+    from funasr_amd.config import sense_voice_small, sense_voice_tiny
+    from funasr_amd.sense_voice import SenseVoiceSmall
+    assert tables.model_classes["SenseVoiceSmall"] is SenseVoiceSmall
+    cfg = sense_voice_tiny(vocab_size=300)
+    m = SenseVoiceSmall(**cfg.reference_kwargs())
+    assert m.cfg == cfg
+    assert set(m.state_dict()) == {k for k, _, _ in param_layout(cfg)}
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in make_weights(cfg).items()})
+    assert m.query_ids() == [0, 1, 2, 15]
+    assert m.query_ids("zh", use_itn=True) == [3, 1, 2, 14]
+    assert m.query_ids("xx", text_norm="withitn") == [0, 1, 2, 14]
+    from funasr_amd.weights import num_params
+    assert num_params(sense_voice_small()) == 233_999_167
+
+
+def test_sentencepiece_tokenizer_and_build_tokenizer():
+    from funasr_amd.auto_model import build_tokenizer
+    from funasr_amd.text import CharTokenizer, SentencepiecesTokenizer
+    bpe = os.path.join(GOLD, "sv_bpe.model")
+    tok, vocab = build_tokenizer(None, dict(bpemodel=bpe))
+    assert isinstance(tok, SentencepiecesTokenizer) and vocab == 300
+    ids = tok.encode("loto rito hona")
+    assert tok.decode(ids) == "loto rito hona"
+    tok2, v2 = build_tokenizer("CharTokenizer", dict(token_list=["<blank>", "<s>", "</s>", "a", "<unk>"]))
+    assert isinstance(tok2, CharTokenizer) and v2 == 5
+    assert build_tokenizer(None, {}) == (None, -1)
