@@ -239,7 +239,7 @@ __device__ __forceinline__ void fsmn_epilogue(const AttnArgs& a, unsigned char* 
 }
 
 template <int NWV>
-__global__ __launch_bounds__(NWV * 64) void attn_bf16_kernel(AttnArgs a) {
+__global__ __launch_bounds__(NWV * 64, 8 / NWV) void attn_bf16_kernel(AttnArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr int NT = NWV * 64, QBLK = NWV * QW;
     const int qt = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
@@ -278,21 +278,26 @@ __global__ __launch_bounds__(NWV * 64) void attn_bf16_kernel(AttnArgs a) {
     float mused = -INFINITY, lrun = 0.f;
     const int ntiles = (klen + KT2 - 1) / KT2;
 
-    // register staging: each thread moves (64 rows x 16 chunks) / NT chunks of K and of V per tile
+    // register staging: each thread moves (64 rows x 16 chunks) / NT chunks of K and of V per tile.
+    // An utterance's key rows are `ld` apart (plain map, or one segment per utterance: launcher check),
+    // so a chunk's source is utterance base + row * row_bytes + chunk * 16 with 32-bit offsets; rows
+    // past klen load the clamped last valid row (masked to -inf in the last tile's scores).
     constexpr int CPT = KT2 * 16 / NT;
     static_assert(CPT == 2 || CPT == 4, "staging struct holds 2 or 4 16-B chunks of K and of V per thread");
-    // two register sets: tile t+2 is fetched while tile t computes and tile t+1 (fetched one
-    // iteration earlier) is written to LDS at the end of iteration t -> a full iteration of cover.
-    // Rows past klen load a clamped valid row (masked to -inf in the scores of the last tile).
+    const char* kbase = (const char*)(K + a.kmap.off((long long)b * a.Tk) + h * DK);
+    const char* vbase = (const char*)(V + a.vmap.off((long long)b * a.Tk) + h * DK);
+    const unsigned krb = (unsigned)a.kmap.ld * 2u, vrb = (unsigned)a.vmap.ld * 2u;
+    const int lastrow = max(klen - 1, 0);
     // Named members returned by value (register arrays indexed before unrolling went to scratch).
     struct Stg { uint4 k0, k1, k2, k3, v0, v1, v2, v3; };
     auto ld1 = [&](int t, int c, uint4& kk, uint4& vv) {
-        const long long m = (long long)b * a.Tk + min(t * KT2 + (c >> 4), max(klen - 1, 0));
-        kk = *(const uint4*)(K + a.kmap.off(m) + h * DK + (c & 15) * 8);
-        vv = *(const uint4*)(V + a.vmap.off(m) + h * DK + (c & 15) * 8);
+        const unsigned row = (unsigned)min(t * KT2 + (c >> 4), lastrow);
+        const unsigned cb = (unsigned)(c & 15) * 16u;
+        kk = *(const uint4*)(kbase + (row * krb + cb));
+        vv = *(const uint4*)(vbase + (row * vrb + cb));
     };
     auto gload = [&](int t) -> Stg {
-        Stg r = {};
+        Stg r;
         ld1(t, tid, r.k0, r.v0);
         ld1(t, tid + NT, r.k1, r.v1);
         if constexpr (CPT == 4) {
@@ -301,19 +306,18 @@ __global__ __launch_bounds__(NWV * 64) void attn_bf16_kernel(AttnArgs a) {
         }
         return r;
     };
-    auto st1 = [&](unsigned char* Ks, unsigned char* Vs, int c, const uint4& kk, const uint4& vv) {
+    auto st1 = [&](unsigned char* base, int c, const uint4& kk, const uint4& vv) {
         const int row = c >> 4, ch = c & 15;
-        *(uint4*)(Ks + row * KROW + ((ch ^ (row & 15)) << 4)) = kk;
-        *(uint4*)(Vs + row * VROW + ch * 16) = vv;
+        *(uint4*)(base + row * KROW + ((ch ^ (row & 15)) << 4)) = kk;
+        *(uint4*)(base + KTILE + row * VROW + ch * 16) = vv;
     };
     auto sstore = [&](int s, const Stg& r) {
-        unsigned char* Ks = smem + s * STG2;
-        unsigned char* Vs = Ks + KTILE;
-        st1(Ks, Vs, tid, r.k0, r.v0);
-        st1(Ks, Vs, tid + NT, r.k1, r.v1);
+        unsigned char* base = smem + s * STG2;
+        st1(base, tid, r.k0, r.v0);
+        st1(base, tid + NT, r.k1, r.v1);
         if constexpr (CPT == 4) {
-            st1(Ks, Vs, tid + 2 * NT, r.k2, r.v2);
-            st1(Ks, Vs, tid + 3 * NT, r.k3, r.v3);
+            st1(base, tid + 2 * NT, r.k2, r.v2);
+            st1(base, tid + 3 * NT, r.k3, r.v3);
         }
     };
     // per-lane constants of the transposed V read: lane 4q+p of its 16-lane group addresses key
@@ -322,14 +326,8 @@ __global__ __launch_bounds__(NWV * 64) void attn_bf16_kernel(AttnArgs a) {
     const int tr_key = 4 * (tg >> 1) + (ti >> 2);
     const int tr_col = 16 * (tg & 1) + 4 * (ti & 3);
 
-    Stg nxt = {}, nxt2 = {};
-    if (ntiles > 0) sstore(0, gload(0));
-    if (ntiles > 1) nxt = gload(1);
-    __syncthreads();
-    for (int t = 0; t < ntiles; ++t) {
-        const int cur = t & 1;
-        if (t + 2 < ntiles) nxt2 = gload(t + 2);
-        const unsigned char* Ks = smem + cur * STG2;
+    auto compute = [&](int t) {
+        const unsigned char* Ks = smem + (t & 1) * STG2;
         const unsigned char* Vs = Ks + KTILE;
         f32x16 s[2];
 #pragma unroll
@@ -400,8 +398,18 @@ __global__ __launch_bounds__(NWV * 64) void attn_bf16_kernel(AttnArgs a) {
                 }
             }
         }
-        if (t + 1 < ntiles) sstore(cur ^ 1, nxt);
-        nxt = nxt2;
+    };
+
+    // One staging set: tile t+1 is fetched into registers before tile t's products and written to
+    // the other LDS buffer after them (that buffer's last reader, tile t-1, finished before the
+    // previous barrier), so the fetch has one tile of compute to land. The fetch index is clamped so
+    // every iteration issues the same loads (the last one is unused).
+    if (ntiles > 0) sstore(0, gload(0));
+    __syncthreads();
+    for (int t = 0; t < ntiles; ++t) {
+        const Stg nx = gload(min(t + 1, ntiles - 1));
+        compute(t);
+        if (t + 1 < ntiles) sstore((t + 1) & 1, nx);
         __syncthreads();
     }
     if (qrow < a.Tq) {
@@ -655,6 +663,11 @@ hipError_t pfm_attention_fsmn(int dtype, const void* q, RowMap qmap, const void*
         (void)hipFuncSetAttribute((const void*)attn_bf16_pp_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   3 * STG2);
     }
+    // bf16 kernels address an utterance's key rows as base + t * ld (32-bit offsets)
+    auto contiguous = [&](const RowMap& m) {
+        return (m.rows_per_seg <= 0 || m.rows_per_seg == Tk) && (long long)Tk * m.ld * 2 < (1ll << 31);
+    };
+    if (dtype == DT_BF16 && (!contiguous(kmap) || !contiguous(vmap))) return hipErrorInvalidValue;
     if (dtype == DT_F32) {
         dim3 grid((Tq + 127) / 128, heads, B), block(256);
         hipLaunchKernelGGL(attn_f32_kernel, grid, block, LDS32, st, a);

@@ -35,7 +35,7 @@ def main():
         W = (torch.randn(N, K, device=dev) / K ** 0.5).to(ty)
         C = torch.empty(M, N, device=dev)
         fl = 2.0 * M * N * K
-        ms = tm(lambda: rt.op_gemm(A, W))
+        ms = tm(lambda: rt.op_gemm(A, W, out_bf16=(dt == "bf16")))
         ms_t = tm(lambda: torch.matmul(A, W.t()))
         print(f"{name:7s} M={M:6d} N={N:6d} K={K:5d}  pfm {ms*1e3:8.1f} us {fl/ms/1e9:7.1f} TF   "
               f"torch {ms_t*1e3:8.1f} us {fl/ms_t/1e9:7.1f} TF", flush=True)
