@@ -133,6 +133,13 @@ struct pfm_handle {
     bool fb_tab_ready = false;
     int32_t* host_ntok = nullptr;
     int host_ntok_cap = 0;
+    // encoder sub-batch streams: the batch is split into NSUB utterance groups whose layer sequences run
+    // concurrently, so one group's HBM-bound phases (LayerNorm, GEMM epilogues, attention) overlap the
+    // other's MFMA main loops
+    static constexpr int MAXSUB = 4;
+    hipStream_t sub_st[MAXSUB] = {nullptr, nullptr, nullptr, nullptr};
+    hipEvent_t ev_fork = nullptr, ev_join[MAXSUB] = {nullptr, nullptr, nullptr, nullptr};
+    DevBuf Xf;                               // SenseVoice: tp_norm output (CTC GEMM input), [M, D]
     // side stream: the decoder's memory K|V projection overlaps the predictor / CIF / token-count sync
     hipStream_t st2 = nullptr;
     hipEvent_t ev_enc = nullptr, ev_kv = nullptr;
@@ -312,6 +319,7 @@ int reserve(pfm_handle* h, int B, int T) {
     if (sv) {   // query-prefixed input, tp residual, CTC argmax partials (rows = frames)
         HIP_TRY(h->Xin.ensure(M * I * 4));
         HIP_TRY(h->X2.ensure(M * D * 4));
+        HIP_TRY(h->Xf.ensure(M * D * 4));
         HIP_TRY(h->olen.ensure((size_t)B * 4));
         HIP_TRY(h->fids.ensure(M * 4));
         HIP_TRY(h->amv.ensure(M * nt * 4));
@@ -513,12 +521,29 @@ struct FinalLN {
     void* out2; RowMap o2map; int o2dt;
 };
 
+// Encoder workspace of one utterance group: the handle's buffers from row r0 on (each buffer is
+// sized for its widest row, so a group's region never overlaps another group's).
+struct EncWs { void* Xn; float* QKV; bf16* QKVb; float* F; float* O; bf16* Ob; void* H; };
+EncWs enc_ws(pfm_handle* h, long long r0) {
+    const pfm_config& c = h->cfg;
+    const long long D = c.d_model, I = c.input_size, Fd = c.ffn;
+    EncWs w;
+    w.Xn = (char*)h->Xn.p + r0 * std::max(I, D) * 4;
+    w.QKV = h->QKV.as<float>() + r0 * 3 * D;
+    w.QKVb = h->QKVb.as<bf16>() + r0 * 3 * D;
+    w.F = h->F.as<float>() + r0 * D;
+    w.O = h->O.as<float>() + r0 * D;
+    w.Ob = h->Ob.as<bf16>() + r0 * D;
+    w.H = (char*)h->H.p + r0 * Fd * 4;
+    return w;
+}
+
 // Encoder layers [l0, l1) of h->enc (EncoderLayerSANM, sanm/encoder.py:72-148 ==
 // sense_voice/model.py:329-405) on the f32 residual X [B*T, D], then the closing LayerNorm `fin`.
 // l0 == 0: the stack input is x_in [B*T, input_size] (before x sqrt(d) + PE, encoder.py:378-379),
 // and layer 0 has no residual (in_size != size, encoder.py:129-137). lens: valid frames per utterance.
 int encoder_stack(const Run& r, const float* x_in, const int* lens, int B, int T, int l0, int l1, float* X,
-                  const FinalLN& fin) {
+                  const FinalLN& fin, const EncWs& ws) {
     pfm_handle* h = r.h;
     const pfm_config& c = h->cfg;
     const hipStream_t st = r.st;
@@ -527,14 +552,14 @@ int encoder_stack(const Run& r, const float* x_in, const int* lens, int B, int T
     const int D = c.d_model, Fd = c.ffn, I = c.input_size, K = c.kernel_size;
     const long long M = (long long)B * T;
     const int lenc = (K - 1) / 2 + (c.enc_sanm_shift > 0 ? c.enc_sanm_shift : 0);
-    void* Xn = h->Xn.p;   // LN output, f32 (exact) or bf16 (fast)
-    float* QKV = h->QKV.as<float>();
-    bf16* QKVb = h->QKVb.as<bf16>();
-    float* Fm = h->F.as<float>();
-    bf16* Fb = h->F.as<bf16>();   // fast mode: FSMN memory in bf16 (same buffer)
-    float* O = h->O.as<float>();
-    bf16* Ob = h->Ob.as<bf16>();
-    void* Hh = h->H.p;
+    void* Xn = ws.Xn;   // LN output, f32 (exact) or bf16 (fast)
+    float* QKV = ws.QKV;
+    bf16* QKVb = ws.QKVb;
+    float* Fm = ws.F;
+    bf16* Fb = (bf16*)ws.F;   // fast mode: FSMN memory in bf16 (same buffer)
+    float* O = ws.O;
+    bf16* Ob = ws.Ob;
+    void* Hh = ws.H;
     const RowMap plain = rowmap_plain(0);
     const bool fuse_last = r.fuse_ln && (!fin.out2 || fin.o2dt == DT_BF16);
     for (int l = l0; l < l1; ++l) {
@@ -623,6 +648,49 @@ int encoder_stack(const Run& r, const float* x_in, const int* lens, int B, int T
     return PFM_OK;
 }
 
+
+int subbatch_count(pfm_handle* h, int B) {   // PFM_SUBBATCH=n (1 disables); profiling runs unsplit
+    static int v = -1;
+    if (v < 0) { const char* e = getenv("PFM_SUBBATCH"); v = e ? std::max(1, std::min(atoi(e), (int)pfm_handle::MAXSUB)) : 2; }
+    if (h->prof_on) return 1;
+    return std::max(1, std::min(v, B));
+}
+
+size_t dt_size(int dt) { return dt == DT_F32 ? 4 : 2; }
+
+// encoder_stack over the batch split into utterance groups on concurrent streams (forked from and
+// joined back into r.st). Row-addressed arguments are offset per group: x_in / X rows, lens, and the
+// closing LN outputs through their RowMaps (one segment per utterance or plain rows).
+int encoder_split(pfm_handle* h, const Run& r, const float* x_in, const int* lens, int B, int T, int l0, int l1,
+                  float* X, const FinalLN& fin) {
+    const pfm_config& c = h->cfg;
+    const int ns = subbatch_count(h, B);
+    if (ns == 1) return encoder_stack(r, x_in, lens, B, T, l0, l1, X, fin, enc_ws(h, 0));
+    if (!h->ev_fork) HIP_TRY(hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming));
+    HIP_TRY(hipEventRecord(h->ev_fork, r.st));
+    for (int k = 0; k < ns; ++k) {
+        if (!h->sub_st[k]) {
+            HIP_TRY(hipStreamCreateWithFlags(&h->sub_st[k], hipStreamNonBlocking));
+            HIP_TRY(hipEventCreateWithFlags(&h->ev_join[k], hipEventDisableTiming));
+        }
+        const int b0 = (int)((long long)B * k / ns), b1 = (int)((long long)B * (k + 1) / ns);
+        if (b1 <= b0) continue;
+        const long long r0 = (long long)b0 * T;
+        HIP_TRY(hipStreamWaitEvent(h->sub_st[k], h->ev_fork, 0));
+        Run rk = r;
+        rk.st = h->sub_st[k];
+        FinalLN fk = fin;
+        fk.out = (char*)fin.out + fin.omap.off(r0) * dt_size(fin.odt);
+        if (fin.out2) fk.out2 = (char*)fin.out2 + fin.o2map.off(r0) * dt_size(fin.o2dt);
+        const int rc = encoder_stack(rk, x_in ? x_in + r0 * c.input_size : nullptr, lens + b0, b1 - b0, T, l0, l1,
+                                     X + r0 * c.d_model, fk, enc_ws(h, r0));
+        if (rc) return rc;
+        HIP_TRY(hipEventRecord(h->ev_join[k], h->sub_st[k]));
+        HIP_TRY(hipStreamWaitEvent(r.st, h->ev_join[k], 0));
+    }
+    return PFM_OK;
+}
+
 }  // namespace
 
 // ============================================================================================
@@ -683,6 +751,11 @@ void pfm_destroy(pfm_handle* h) {
     if (h->ev_enc) (void)hipEventDestroy(h->ev_enc);
     if (h->ev_kv) (void)hipEventDestroy(h->ev_kv);
     if (h->st2) (void)hipStreamDestroy(h->st2);
+    for (int k = 0; k < pfm_handle::MAXSUB; ++k) {
+        if (h->sub_st[k]) (void)hipStreamDestroy(h->sub_st[k]);
+        if (h->ev_join[k]) (void)hipEventDestroy(h->ev_join[k]);
+    }
+    if (h->ev_fork) (void)hipEventDestroy(h->ev_fork);
     if (h->host_ntok) (void)hipHostFree(h->host_ntok);
     delete h;
 }
@@ -786,7 +859,7 @@ int pfm_run(pfm_handle* h, void* stream, int mode, const float* feats, const int
     {
         const FinalLN fin = {h->an_g, h->an_b, encp + D, encmap, DT_F32, fast ? (void*)(encpb + D) : nullptr, encmap,
                              DT_BF16};
-        rc = encoder_stack(run, feats, lens, B, T, 0, c.enc_blocks, h->X.as<float>(), fin);
+        rc = encoder_split(h, run, feats, lens, B, T, 0, c.enc_blocks, h->X.as<float>(), fin);
         if (rc) return rc;
     }
     if (enc_out)
@@ -987,12 +1060,13 @@ int pfm_run_ctc(pfm_handle* h, void* stream, int mode, const float* feats, const
     // (SenseVoiceEncoderSmall.forward, model.py:553-585)
     {
         const FinalLN fin = {h->an_g, h->an_b, h->X2.p, rowmap_plain(D), DT_F32, nullptr, rowmap_plain(0), 0};
-        rc = encoder_stack(run, h->Xin.as<float>(), olen, B, Tq, 0, c.enc_blocks, h->X.as<float>(), fin);
+        rc = encoder_split(h, run, h->Xin.as<float>(), olen, B, Tq, 0, c.enc_blocks, h->X.as<float>(), fin);
         if (rc) return rc;
     }
     {
-        const FinalLN fin = {h->tp_g, h->tp_b, h->Xn.p, rowmap_plain(D), run.dt, enc_out, rowmap_plain(D), DT_F32};
-        rc = encoder_stack(run, nullptr, olen, B, Tq, c.enc_blocks, c.enc_blocks + c.tp_blocks, h->X2.as<float>(), fin);
+        const FinalLN fin = {h->tp_g, h->tp_b, h->Xf.p, rowmap_plain(D), run.dt, enc_out, rowmap_plain(D), DT_F32};
+        rc = encoder_split(h, run, nullptr, olen, B, Tq, c.enc_blocks, c.enc_blocks + c.tp_blocks, h->X2.as<float>(),
+                           fin);
         if (rc) return rc;
     }
     // CTC head (ctc.py:173-184) with fused row-argmax; ban_emo_unk (model.py:885-886) sets the banned
@@ -1015,7 +1089,7 @@ int pfm_run_ctc(pfm_handle* h, void* stream, int mode, const float* feats, const
         e.bias = bias;
         e.amax_val = h->amv.as<float>(); e.amax_idx = h->ami.as<int>(); e.n_tiles = ntl;
         e.out = nullptr;
-        HIP_TRY(run.gemm(run.dt, h->Xn.p, rowmap_plain(D), run.W(h->ctc_w), D, (int)M, V, D, e));
+        HIP_TRY(run.gemm(run.dt, h->Xf.p, rowmap_plain(D), run.W(h->ctc_w), D, (int)M, V, D, e));
     }
     int* fid = frame_ids ? frame_ids : h->fids.as<int>();
     HIP_TRY(pfm_argmax_reduce(h->amv.as<float>(), h->ami.as<int>(), ntl, (V + 63) / 64, B, Tq, olen, Tq, fid, nullptr,
