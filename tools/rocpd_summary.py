@@ -1,7 +1,10 @@
 """Summarise a rocprofv3 rocpd database (--kernel-trace; ROCm 7 writes <name>_results.db) into a
 per-kernel stats CSV (the --stats columns) and a markdown table per step.
 
-usage: python tools/rocpd_summary.py run_results.db out_stats.csv [step_marker_kernel]
+usage: python tools/rocpd_summary.py run_results.db out_stats.csv [step_marker_kernel [bench.log [W K]]]
+With W K (the bench's --warmup / --steps), the GEMM average is also reported over the bench's second
+(HIP-event instrumented, roofline) pass alone: the pfm_run calls W+K .. W+2K-1, delimited by the step
+marker's end times.
 Steps are counted as the number of launches of step_marker_kernel (default: argmax_reduce_kernel,
 launched once per pfm_run). GEMM launches are additionally split by grid (= shape) in the markdown.
 """
@@ -11,7 +14,11 @@ import sys
 from collections import defaultdict
 
 
-def main(db, out_csv, marker="argmax_reduce_kernel", bench_log=None):
+def is_gemm(k):
+    return "gemm_bf16_kernel" in k or "gemm_nt_kernelIDF16b" in k or "gemm_nt_kernel<__bf16>" in k
+
+
+def main(db, out_csv, marker="argmax_reduce_kernel", bench_log=None, warmup=None, ksteps=None):
     c = sqlite3.connect(db)
     rows = c.execute("select name, duration, grid_x, grid_y, grid_z, workgroup_x from kernels").fetchall()
     agg = defaultdict(list)
@@ -40,6 +47,16 @@ def main(db, out_csv, marker="argmax_reduce_kernel", bench_log=None):
     if gl:
         print(f"\nbf16 GEMM launches (bench roofline kernel set): {len(gl)} launches, "
               f"avg {sum(gl) / len(gl) / 1e3:.2f} us (rocprof)")
+    if warmup is not None and ksteps is not None:
+        W, K = int(warmup), int(ksteps)
+        ends = sorted(e for (e,) in c.execute("select end from kernels where name like ?", (f"%{marker}%",)))
+        if len(ends) >= W + 2 * K:
+            lo, hi = ends[W + K - 1], ends[W + 2 * K - 1]
+            g2 = [d for (n, st, en, d) in c.execute("select name, start, end, duration from kernels")
+                  if is_gemm(n) and lo < st and en <= hi]
+            if g2:
+                print(f"bf16 GEMM launches of the bench's roofline pass (pfm_run calls {W + K}..{W + 2 * K - 1}): "
+                      f"{len(g2)} launches, avg {sum(g2) / len(g2) / 1e3:.2f} us (rocprof)")
     if bench_log:
         import json
         line = [x for x in open(bench_log) if x.startswith("{")][-1]
