@@ -25,8 +25,10 @@ namespace {
 typedef __attribute__((address_space(3))) void lds_void;
 typedef const __attribute__((address_space(1))) void gbl_void;
 
-template <int BM_, int BN_, int WGM_, int WGN_, int BK_, int NS_, int PP_ = 0> struct Cfg {
+template <int BM_, int BN_, int WGM_, int WGN_, int BK_, int NS_, int PP_ = 0, int MF_ = 0> struct Cfg {
     static constexpr int BM = BM_, BN = BN_, WGM = WGM_, WGN = WGN_, BK = BK_, NS = NS_;
+    // MFMA shape: 0 = v_mfma_f32_32x32x16_bf16, 1 = v_mfma_f32_16x16x32_bf16 (one-barrier schedule only)
+    static constexpr int MF = MF_;
     // schedule: 0 = one barrier per K-step; 1 = ping-pong (wave-row groups staggered by one barrier,
     // one K-step per phase); 2 = 8-phase (quadrant phases, one half-tile of DMA per phase, staggered)
     static constexpr int PP = PP_;
@@ -41,6 +43,7 @@ template <int BM_, int BN_, int WGM_, int WGN_, int BK_, int NS_, int PP_ = 0> s
     static constexpr int LDS = (NS * STAGE > NW * EPW) ? NS * STAGE : NW * EPW;
     static_assert(TA % (1024 * NW) == 0 && TW % (1024 * NW) == 0, "tile not divisible into DMA pieces");
     static_assert(WTN == 64, "epilogue / argmax partials assume 64-column wave tiles");
+    static_assert(MF == 0 || (PP == 0 && BK % 32 == 0), "16x16x32 MFMA: one-barrier schedule, BK multiple of 32");
     static_assert(PP != 1 || (WGM == 2 && NS >= 3), "ping-pong needs two wave-row groups and >= 3 stages");
     static_assert(PP != 2 || (BM == 256 && BN == 256 && WGM == 2 && WGN == 4 && BK == 64 && NS == 2),
                   "8-phase schedule: 256x256 tile, 2x4 waves, BK 64, two K-tile buffers");
@@ -115,14 +118,26 @@ __global__ __launch_bounds__(C::NT) void gemm_bf16_kernel(const bf16* __restrict
     // the accumulator layout (32 lanes = 128 contiguous bytes per row) ahead of the prologue DMA, so
     // the epilogue carries no loads. vmcnt retires in order: an epilogue load issued after stores
     // waits for them, which serialised one HBM round trip per 4 rows before.
-    const bool pre_res = epi.pre_res_ok && (epi.res0 || epi.res1) && epi.alpha == 1.f && !epi.relu;
+    const bool pre_res = C::MF == 0 && epi.pre_res_ok && (epi.res0 || epi.res1) && epi.alpha == 1.f && !epi.relu;
     f32x16 acc[MI][NI];
+    // MF 1: 16x16 blocks, block (i4, j4) = rows 16 i4.., cols 16 j4.. of the wave tile;
+    // C/D map col = lane & 15, row = 4 (lane >> 4) + reg
+    f32x4 acc4[C::MF ? 2 * MI : 1][C::MF ? 2 * NI : 1];
+    if constexpr (C::MF == 0) {
 #pragma unroll
-    for (int i = 0; i < MI; ++i)
+        for (int i = 0; i < MI; ++i)
 #pragma unroll
-        for (int j = 0; j < NI; ++j)
+            for (int j = 0; j < NI; ++j)
 #pragma unroll
-            for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+                for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+    } else {
+#pragma unroll
+        for (int i = 0; i < 2 * MI; ++i)
+#pragma unroll
+            for (int j = 0; j < 2 * NI; ++j)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) acc4[i][j][e] = 0.f;
+    }
     if (pre_res) {
 #pragma unroll
         for (int i = 0; i < MI; ++i)
@@ -398,6 +413,39 @@ __global__ __launch_bounds__(C::NT) void gemm_bf16_kernel(const bf16* __restrict
         }
         __builtin_amdgcn_sched_barrier(0);
         if (grp == 0) __builtin_amdgcn_s_barrier();   // match group 1's stagger barrier
+    } else if constexpr (C::MF == 1) {
+        // 16x16x32 fragments: lane (r = lane & 15, g = lane >> 4) reads row r of a 16-row block, K chunk
+        // 4 kq + g of the 32-wide k-substep kq (the same source-side swizzle keeps the 16 rows x 4 chunks
+        // of every ds_read_b128 lane group on distinct banks)
+        const int r16 = lane & 15, g16 = lane >> 4;
+        // 16-row blocks start at multiples of 16 rows, so the row swizzle depends on r16 only and every
+        // block's fragment address is one base + a compile-time offset (ds_read immediate)
+        const int sw = C::swz(r16);
+        const int abase = (wm * C::WTM + r16) * ROWB, wbase = C::TA + (wn * C::WTN + r16) * ROWB;
+        for (int kt = 0; kt < nk; ++kt) {
+            wait_vm<PA + PW>(min(NS - 2, nk - 1 - kt));
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            __builtin_amdgcn_sched_barrier(0);
+            if (kt + NS - 1 < nk) stage((kt + NS - 1) * BK, (kt + NS - 1) % NS);
+            const unsigned char* sb = smem + (kt % NS) * C::STAGE;
+#pragma unroll
+            for (int kq = 0; kq < BK / 32; ++kq) {
+                const int co = ((4 * kq + g16) ^ sw) << 4;
+                const unsigned char* pa = sb + abase + co;
+                const unsigned char* pw = sb + wbase + co;
+                bf16x8 af[2 * MI], bfr[2 * NI];
+#pragma unroll
+                for (int i = 0; i < 2 * MI; ++i) af[i] = *(const bf16x8*)(pa + i * 16 * ROWB);
+#pragma unroll
+                for (int j = 0; j < 2 * NI; ++j) bfr[j] = *(const bf16x8*)(pw + j * 16 * ROWB);
+#pragma unroll
+                for (int i = 0; i < 2 * MI; ++i)
+#pragma unroll
+                    for (int j = 0; j < 2 * NI; ++j)
+                        acc4[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc4[i][j], 0, 0, 0);
+            }
+        }
     } else
     for (int kt = 0; kt < nk; ++kt) {
         wait_vm<PA + PW>(min(NS - 2, nk - 1 - kt));
@@ -443,10 +491,20 @@ __global__ __launch_bounds__(C::NT) void gemm_bf16_kernel(const bf16* __restrict
                      "v"(bb2.w));
 #pragma unroll
         for (int i = 0; i < MI; ++i) {
+            if constexpr (C::MF == 0) {
 #pragma unroll
-            for (int j = 0; j < NI; ++j)
+                for (int j = 0; j < NI; ++j)
 #pragma unroll
-                for (int e = 0; e < 16; ++e) ep[((e & 3) + 8 * (e >> 2) + 4 * fh) * EP + j * 32 + fr] = acc[i][j][e];
+                    for (int e = 0; e < 16; ++e) ep[((e & 3) + 8 * (e >> 2) + 4 * fh) * EP + j * 32 + fr] = acc[i][j][e];
+            } else {
+#pragma unroll
+                for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+                    for (int j = 0; j < 2 * NI; ++j)
+#pragma unroll
+                        for (int e = 0; e < 4; ++e)
+                            ep[(ii * 16 + 4 * (lane >> 4) + e) * EP + j * 16 + (lane & 15)] = acc4[2 * i + ii][j][e];
+            }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -586,6 +644,36 @@ __global__ __launch_bounds__(C::NT) void gemm_bf16_kernel(const bf16* __restrict
         return;
     }
     // scalar fallback epilogue (odd N / strides): straight from the accumulators
+    if constexpr (C::MF == 1) {   // re-pack the 16x16 blocks into the 32x32 register map
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+            for (int j = 0; j < NI; ++j)
+#pragma unroll
+                for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+        float* ep = (float*)(smem + wid * C::EPW);
+        constexpr int EP = C::EP;
+#pragma unroll
+        for (int i = 0; i < MI; ++i) {
+#pragma unroll
+            for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+                for (int j = 0; j < 2 * NI; ++j)
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)
+                        ep[(ii * 16 + 4 * (lane >> 4) + e) * EP + j * 16 + (lane & 15)] = acc4[2 * i + ii][j][e];
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+            for (int j = 0; j < NI; ++j)
+#pragma unroll
+                for (int e = 0; e < 16; ++e) acc[i][j][e] = ep[((e & 3) + 8 * (e >> 2) + 4 * fh) * EP + j * 32 + fr];
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+    }
 #pragma unroll
     for (int i = 0; i < MI; ++i) {
 #pragma unroll
@@ -800,6 +888,8 @@ using C11 = Cfg<256, 128, 2, 2, 32, 2>;  // 4 waves, 48 KiB
 using C12 = Cfg<256, 128, 2, 2, 64, 2>;  // 4 waves, 96 KiB (1 block/CU; control)
 using C13 = Cfg<256, 256, 2, 4, 64, 2, 2>;  // 8-phase schedule (K % 128 == 0)
 using C14 = Cfg<256, 256, 2, 4, 32, 4, 3>;  // k-step phases, BK 32 x 4 buffers
+using C15 = Cfg<256, 256, 2, 4, 64, 2, 0, 1>;  // C1 on v_mfma_f32_16x16x32_bf16
+using C16 = Cfg<128, 256, 2, 4, 32, 3, 0, 1>;  // C4 on v_mfma_f32_16x16x32_bf16
 
 template <class C>
 hipError_t launch(const void* A, RowMap amap, const void* W, long long ldw, int M, int N, int K, const GemmEpi& e2,
@@ -852,7 +942,7 @@ hipError_t launch_persist(const void* A, RowMap amap, const void* W, long long l
 int pick_cfg(int M, int N, int K, bool amax) {
     const char* e = getenv("PFM_GEMM_CFG");   // read per launch: lets one process A/B configurations
     const int f = e ? atoi(e) : 0;
-    if (f >= 1 && f <= 14) return f;
+    if (f >= 1 && f <= 16) return f;
     // Measured on the path shapes (tools/gemm_ab.py): decoder-sized M (B*L rows) and the vocabulary
     // projection run best on 128x256 tiles (2 blocks / CU); the encoder's wide grids (>= 2 tiles per
     // CU, or one full round at K >= 1536) on 256x256 tiles with the 8-phase schedule (C13, needs
@@ -866,7 +956,9 @@ int pick_cfg(int M, int N, int K, bool amax) {
     const long long big = (long long)((M + 255) / 256) * ((N + 255) / 256);
     const char* kp = getenv("PFM_GEMM_KPOLICY");   // A/B switch for the K-aware rule (default on)
     const bool kaware = !(kp && kp[0] == '0');
-    if (big >= 512 || (kaware && K >= 1536 && big >= 240)) return (!prev && K % 128 == 0) ? 13 : 1;
+    // 256x256 tiles run on v_mfma_f32_16x16x32_bf16 (C15): 5-18 % faster than the 32x32x16 form (C1)
+    // on every path shape (tools/gemm_kscan.py: 1.50 vs 1.82 us per 64-deep K-step at N = 512)
+    if (big >= 512 || (kaware && K >= 1536 && big >= 240)) return (!prev && K % 128 == 0) ? 13 : 15;
     return 4;
 }
 
@@ -1104,7 +1196,10 @@ hipError_t pfm_gemm_bf16_256(const void* A, RowMap amap, const void* W, long lon
         case 13: if (K % 128 == 0) return launch<C13>(A, amap, W, ldw, M, N, K, e2, st);
                  return launch<C1>(A, amap, W, ldw, M, N, K, e2, st);
         case 14: return launch<C14>(A, amap, W, ldw, M, N, K, e2, st);
-        default: return launch<C1>(A, amap, W, ldw, M, N, K, e2, st);
+        case 15: return launch<C15>(A, amap, W, ldw, M, N, K, e2, st);
+        case 16: return launch<C16>(A, amap, W, ldw, M, N, K, e2, st);
+        case 1: return launch<C1>(A, amap, W, ldw, M, N, K, e2, st);
+        default: return launch<C15>(A, amap, W, ldw, M, N, K, e2, st);
     }
 }
 
