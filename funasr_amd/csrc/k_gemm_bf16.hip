@@ -43,7 +43,7 @@ template <int BM_, int BN_, int WGM_, int WGN_, int BK_, int NS_, int PP_ = 0, i
     static constexpr int LDS = (NS * STAGE > NW * EPW) ? NS * STAGE : NW * EPW;
     static_assert(TA % (1024 * NW) == 0 && TW % (1024 * NW) == 0, "tile not divisible into DMA pieces");
     static_assert(WTN == 64, "epilogue / argmax partials assume 64-column wave tiles");
-    static_assert(MF == 0 || (PP == 0 && BK % 32 == 0), "16x16x32 MFMA: one-barrier schedule, BK multiple of 32");
+    static_assert(MF == 0 || ((PP == 0 || PP == 2) && BK % 32 == 0), "16x16x32 MFMA: one-barrier or 8-phase schedule");
     static_assert(PP != 1 || (WGM == 2 && NS >= 3), "ping-pong needs two wave-row groups and >= 3 stages");
     static_assert(PP != 2 || (BM == 256 && BN == 256 && WGM == 2 && WGN == 4 && BK == 64 && NS == 2),
                   "8-phase schedule: 256x256 tile, 2x4 waves, BK 64, two K-tile buffers");
@@ -300,7 +300,54 @@ __global__ __launch_bounds__(C::NT) void gemm_bf16_kernel(const bf16* __restrict
         };
         const int grp = wm;
         bf16x8 aF[2][4], bF[4];
+        // MF 1: quadrant = 4 m16 x 2 n16 blocks over two 32-deep k-substeps (16 MFMAs, 8 A + 4 B reads)
+        bf16x8 aF16[4][2], bF16[2][2];
+        const int r16 = lane & 15, g16 = lane >> 4, sw16 = C::swz(r16);
+        auto phase16 = [&](int tile, int q, int itile, int ih, bool wait_after) {
+            const unsigned char* sb = smem + (tile & 1) * C::STAGE;
+            const int i0 = (q >= 2) ? 4 : 0, j0 = (q == 1 || q == 2) ? 2 : 0;
+            // B first (4 reads), then A (8): an lgkmcnt count would retire B before A
+            if (q != 2) {
+#pragma unroll
+                for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+                    for (int kq = 0; kq < 2; ++kq)
+                        bF16[jj][kq] = *(const bf16x8*)(sb + C::TA + (wn * C::WTN + (j0 + jj) * 16 + r16) * ROWB +
+                                                        (((4 * kq + g16) ^ sw16) << 4));
+            }
+            if (q == 0 || q == 2) {
+#pragma unroll
+                for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+                    for (int kq = 0; kq < 2; ++kq)
+                        aF16[ii][kq] = *(const bf16x8*)(sb + (wm * C::WTM + (i0 + ii) * 16 + r16) * ROWB +
+                                                        (((4 * kq + g16) ^ sw16) << 4));
+            }
+            const bool did = issue(itile, ih);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            if (grp == 1 && wait_after) {
+                if (did) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+                else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            bar();
+            __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+            for (int kq = 0; kq < 2; ++kq)
+#pragma unroll
+                for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+                    for (int jj = 0; jj < 2; ++jj)
+                        acc4[i0 + ii][j0 + jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aF16[ii][kq], bF16[jj][kq],
+                                                                                        acc4[i0 + ii][j0 + jj], 0, 0, 0);
+            __builtin_amdgcn_s_setprio(0);
+            if (grp == 0 && wait_after) {
+                if (did) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+                else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            bar();
+        };
         auto phase = [&](int tile, int q, int itile, int ih, bool wait_after) {
+            if constexpr (C::MF == 1) { phase16(tile, q, itile, ih, wait_after); return; }
             const unsigned char* sb = smem + (tile & 1) * C::STAGE;
             const int i0 = (q >= 2) ? 2 : 0, jn = (q == 1 || q == 2) ? 1 : 0;
             if (q == 0 || q == 2) {
@@ -890,6 +937,7 @@ using C13 = Cfg<256, 256, 2, 4, 64, 2, 2>;  // 8-phase schedule (K % 128 == 0)
 using C14 = Cfg<256, 256, 2, 4, 32, 4, 3>;  // k-step phases, BK 32 x 4 buffers
 using C15 = Cfg<256, 256, 2, 4, 64, 2, 0, 1>;  // C1 on v_mfma_f32_16x16x32_bf16
 using C16 = Cfg<128, 256, 2, 4, 32, 3, 0, 1>;  // C4 on v_mfma_f32_16x16x32_bf16
+using C17 = Cfg<256, 256, 2, 4, 64, 2, 2, 1>;  // 8-phase schedule on v_mfma_f32_16x16x32_bf16 (K % 128 == 0)
 
 template <class C>
 hipError_t launch(const void* A, RowMap amap, const void* W, long long ldw, int M, int N, int K, const GemmEpi& e2,
@@ -942,23 +990,27 @@ hipError_t launch_persist(const void* A, RowMap amap, const void* W, long long l
 int pick_cfg(int M, int N, int K, bool amax) {
     const char* e = getenv("PFM_GEMM_CFG");   // read per launch: lets one process A/B configurations
     const int f = e ? atoi(e) : 0;
-    if (f >= 1 && f <= 16) return f;
-    // Measured on the path shapes (tools/gemm_ab.py): decoder-sized M (B*L rows) and the vocabulary
-    // projection run best on 128x256 tiles (2 blocks / CU); the encoder's wide grids (>= 2 tiles per
-    // CU, or one full round at K >= 1536) on 256x256 tiles with the 8-phase schedule (C13, needs
-    // K % 128 == 0; C1 otherwise); everything else on 128x256.
-    // In the full pipeline C13 and C1 time the same on the encoder shapes (rocprof, same box), and the
-    // grid-size-only policy measured 0.1-0.3 ms/step faster overall: it is the default;
-    // PFM_GEMM_POLICY=2 selects C13 / C4-for-decoder-shapes.
+    if (f >= 1 && f <= 17) return f;
+    // Default (measured on the path, tools/bench_ab.py with the two concurrent encoder groups: 24.2 vs
+    // 25.0-25.3 ms/step for the policies below). Grids are counted in 256x256 tiles; each encoder group
+    // sees half the batch's rows:
+    //  - N <= 512 with K >= 1024 (FFN w2, CIF conv) on the 8-phase 16x16x32 schedule (C17);
+    //  - >= one 256x256 tile per CU (QKV, FFN w1, memory K|V) on the one-barrier 16x16x32 kernel (C15);
+    //  - everything else (out-projections, decoder-sized M, the fused-argmax vocabulary GEMM) on
+    //    128x256 tiles, two blocks per CU (C4).
+    // PFM_GEMM_POLICY=1: the earlier grid-size policy (C15 at >= 2 tiles / CU or K >= 1536 with >= 240
+    // tiles, else C4); =2: C13 / C4 for decoder-sized M.
     const char* pol = getenv("PFM_GEMM_POLICY");
-    const bool prev = !(pol && pol[0] == '2');
-    if (!prev && M <= 16384 && !amax) return 4;   // (the fused-argmax vocabulary GEMM stays on 256x256)
+    const int p = pol ? atoi(pol) : 0;
     const long long big = (long long)((M + 255) / 256) * ((N + 255) / 256);
-    const char* kp = getenv("PFM_GEMM_KPOLICY");   // A/B switch for the K-aware rule (default on)
-    const bool kaware = !(kp && kp[0] == '0');
-    // 256x256 tiles run on v_mfma_f32_16x16x32_bf16 (C15): 5-18 % faster than the 32x32x16 form (C1)
-    // on every path shape (tools/gemm_kscan.py: 1.50 vs 1.82 us per 64-deep K-step at N = 512)
-    if (big >= 512 || (kaware && K >= 1536 && big >= 240)) return (!prev && K % 128 == 0) ? 13 : 15;
+    if (p == 1 || p == 2) {
+        if (p == 2 && M <= 16384 && !amax) return 4;
+        if (big >= 512 || (K >= 1536 && big >= 240)) return (p == 2 && K % 128 == 0) ? 13 : 15;
+        return 4;
+    }
+    if (amax) return big >= 512 ? 15 : 4;
+    if (N <= 512 && K % 128 == 0 && K >= 1024 && big >= 120) return 17;
+    if (big >= 256) return 15;
     return 4;
 }
 
@@ -1198,6 +1250,8 @@ hipError_t pfm_gemm_bf16_256(const void* A, RowMap amap, const void* W, long lon
         case 14: return launch<C14>(A, amap, W, ldw, M, N, K, e2, st);
         case 15: return launch<C15>(A, amap, W, ldw, M, N, K, e2, st);
         case 16: return launch<C16>(A, amap, W, ldw, M, N, K, e2, st);
+        case 17: if (K % 128 == 0) return launch<C17>(A, amap, W, ldw, M, N, K, e2, st);
+                 return launch<C15>(A, amap, W, ldw, M, N, K, e2, st);
         case 1: return launch<C1>(A, amap, W, ldw, M, N, K, e2, st);
         default: return launch<C15>(A, amap, W, ldw, M, N, K, e2, st);
     }
