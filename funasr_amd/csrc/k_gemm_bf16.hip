@@ -60,7 +60,9 @@ template <int P> __device__ __forceinline__ void wait_vm(int rem) {
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-template <class C>
+// LN: 0 plain epilogue; 1 folded-LayerNorm consumer; 2 LayerNorm-statistics producer (compile-time, so the
+// plain kernels carry none of the extra epilogue state: the runtime-flag version spilled to scratch)
+template <class C, int LN = 0>
 __global__ __launch_bounds__(C::NT) void gemm_bf16_kernel(const bf16* __restrict__ A, RowMap amap,
                                                           const bf16* __restrict__ W, long long ldw, int M, int N,
                                                           int K, int tiles_m, int tiles_n, int gm, GemmEpi epi) {
@@ -532,10 +534,45 @@ __global__ __launch_bounds__(C::NT) void gemm_bf16_kernel(const bf16* __restrict
             bb = *(const float4*)(epi.bias + colv);
             if (st16) bb2 = *(const float4*)(epi.bias + colv + 4);
         }
+        // LayerNorm folded into this projection: column sums of bf16(W o gamma) for the lane's columns
+        constexpr bool lnf = LN == 1;
+        float4 lc = make_float4(0.f, 0.f, 0.f, 0.f), lc2 = lc;
+        if (lnf && epi.out && colv < N) {
+            lc = *(const float4*)(epi.ln_colsum + colv);
+            if (st16) lc2 = *(const float4*)(epi.ln_colsum + colv + 4);
+        }
         // consume it here, before any store: otherwise paths that skip rows leave it "pending" and the
         // compiler re-waits vmcnt(0) (draining the stores issued since) at every use below
         asm volatile("" ::"v"(bb.x), "v"(bb.y), "v"(bb.z), "v"(bb.w), "v"(bb2.x), "v"(bb2.y), "v"(bb2.z),
                      "v"(bb2.w));
+        asm volatile("" ::"v"(lc.x), "v"(lc.y), "v"(lc.z), "v"(lc.w), "v"(lc2.x), "v"(lc2.y), "v"(lc2.z),
+                     "v"(lc2.w));
+        // folded LayerNorm: the producer's partials of row (lane & 31) of 32-row group ig; group i+1's are
+        // loaded while group i is processed (their latency stays off the store stream)
+        auto ln_load = [&](int ig, float2 (&d)[8]) {
+            const long long row = min(m0 + wm * C::WTM + ig * 32 + (lane & 31), M - 1);
+            const float2* sp = epi.ln_st_in + row * epi.ln_parts;
+#pragma unroll
+            for (int p = 0; p < 8; ++p) d[p] = p < epi.ln_parts ? sp[p] : make_float2(0.f, 0.f);
+        };
+        float2 ln_cur[8], ln_nxt[8];
+        if constexpr (lnf) ln_load(0, ln_cur);
+        // producer statistics of a 16-lane row group's 64 values (4 per lane): (mean, M2) of the slice
+        auto ln_stats_out = [&](const float4& v, long long row, int c4) {
+            float sm = (v.x + v.y) + (v.z + v.w);
+            sm += __shfl_xor(sm, 1, 64);
+            sm += __shfl_xor(sm, 2, 64);
+            sm += __shfl_xor(sm, 4, 64);
+            sm += __shfl_xor(sm, 8, 64);
+            const float mu = sm * (1.f / 64.f);
+            const float dx = v.x - mu, dy = v.y - mu, dz = v.z - mu, dw = v.w - mu;
+            float q = (dx * dx + dy * dy) + (dz * dz + dw * dw);
+            q += __shfl_xor(q, 1, 64);
+            q += __shfl_xor(q, 2, 64);
+            q += __shfl_xor(q, 4, 64);
+            q += __shfl_xor(q, 8, 64);
+            if (c4 == 0) epi.ln_st_out[row * epi.ln_parts + (n0 + wn * 64) / 64] = make_float2(mu, q);
+        };
 #pragma unroll
         for (int i = 0; i < MI; ++i) {
             if constexpr (C::MF == 0) {
@@ -555,6 +592,23 @@ __global__ __launch_bounds__(C::NT) void gemm_bf16_kernel(const bf16* __restrict
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            // folded LayerNorm: lane l holds (mean, rstd) of row (l & 31) of this 32-row group, combined
+            // from the producer's per-slice partials (Chan: M2 = sum M2_p + 64 sum (m_p - mean)^2)
+            float g_mean = 0.f, g_rstd = 0.f;
+            if constexpr (lnf) {
+                if (i + 1 < MI) ln_load(i + 1, ln_nxt);
+                const int P = epi.ln_parts;
+                float msum = 0.f;
+#pragma unroll
+                for (int p = 0; p < 8; ++p) msum += ln_cur[p].x;
+                const float mean = msum / (float)P;
+                float m2 = 0.f;
+#pragma unroll
+                for (int p = 0; p < 8; ++p)
+                    if (p < P) m2 += ln_cur[p].y + 64.f * (ln_cur[p].x - mean) * (ln_cur[p].x - mean);
+                g_mean = mean;
+                g_rstd = 1.f / sqrtf(m2 / (64.f * (float)P) + epi.ln_eps);
+            }
             if (epi.amax_val) {
                 // fused row-argmax of the output layer over this wave's 64 columns: 2 lanes per staged
                 // row scan 32 columns each in order (first index wins ties, like torch.argmax)
@@ -585,13 +639,22 @@ __global__ __launch_bounds__(C::NT) void gemm_bf16_kernel(const bf16* __restrict
                     const int f = lane + 64 * sidx, rr = f >> 3, c8 = f & 7;
                     const int row = m0 + wm * C::WTM + i * 32 + rr;
                     const int col = n0 + wn * 64 + c8 * 8;
+                    const float mr = lnf ? __shfl(g_mean, rr, 64) : 0.f;   // every lane active here
+                    const float rs = lnf ? __shfl(g_rstd, rr, 64) : 0.f;
                     if (row >= M || col >= N) continue;
                     float4 v = *(const float4*)(ep + rr * EP + c8 * 8);
                     float4 u = *(const float4*)(ep + rr * EP + c8 * 8 + 4);
-                    v.x = v.x * epi.alpha + bb.x; v.y = v.y * epi.alpha + bb.y;
-                    v.z = v.z * epi.alpha + bb.z; v.w = v.w * epi.alpha + bb.w;
-                    u.x = u.x * epi.alpha + bb2.x; u.y = u.y * epi.alpha + bb2.y;
-                    u.z = u.z * epi.alpha + bb2.z; u.w = u.w * epi.alpha + bb2.w;
+                    if (lnf) {
+                        v.x = rs * (v.x - mr * lc.x) + bb.x; v.y = rs * (v.y - mr * lc.y) + bb.y;
+                        v.z = rs * (v.z - mr * lc.z) + bb.z; v.w = rs * (v.w - mr * lc.w) + bb.w;
+                        u.x = rs * (u.x - mr * lc2.x) + bb2.x; u.y = rs * (u.y - mr * lc2.y) + bb2.y;
+                        u.z = rs * (u.z - mr * lc2.z) + bb2.z; u.w = rs * (u.w - mr * lc2.w) + bb2.w;
+                    } else {
+                        v.x = v.x * epi.alpha + bb.x; v.y = v.y * epi.alpha + bb.y;
+                        v.z = v.z * epi.alpha + bb.z; v.w = v.w * epi.alpha + bb.w;
+                        u.x = u.x * epi.alpha + bb2.x; u.y = u.y * epi.alpha + bb2.y;
+                        u.z = u.z * epi.alpha + bb2.z; u.w = u.w * epi.alpha + bb2.w;
+                    }
                     if (epi.relu) {
                         v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
                         u.x = fmaxf(u.x, 0.f); u.y = fmaxf(u.y, 0.f); u.z = fmaxf(u.z, 0.f); u.w = fmaxf(u.w, 0.f);
@@ -635,6 +698,7 @@ __global__ __launch_bounds__(C::NT) void gemm_bf16_kernel(const bf16* __restrict
                         if (epi.relu) { v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f); }
                         v.x += r0[q].x + r1[q].x; v.y += r0[q].y + r1[q].y;
                         v.z += r0[q].z + r1[q].z; v.w += r0[q].w + r1[q].w;
+                        if constexpr (LN == 2) ln_stats_out(v, row, c4);
                         const long long ob = epi.out_map.off(row) + col;
                         if (f32o) *(float4*)((float*)epi.out + ob) = v;
                         else {
@@ -654,10 +718,17 @@ __global__ __launch_bounds__(C::NT) void gemm_bf16_kernel(const bf16* __restrict
                 const int f = lane + 64 * sidx, rr = f >> 4, c4 = f & 15;
                 const int row = m0 + wm * C::WTM + i * 32 + rr;
                 const int col = n0 + wn * 64 + c4 * 4;
+                const float mr = lnf ? __shfl(g_mean, rr, 64) : 0.f;   // every lane active here
+                const float rs = lnf ? __shfl(g_rstd, rr, 64) : 0.f;
                 if (row >= M || col >= N) continue;
                 float4 v = *(const float4*)(ep + rr * EP + c4 * 4);
-                v.x = v.x * epi.alpha + bb.x; v.y = v.y * epi.alpha + bb.y;
-                v.z = v.z * epi.alpha + bb.z; v.w = v.w * epi.alpha + bb.w;
+                if (lnf) {
+                    v.x = rs * (v.x - mr * lc.x) + bb.x; v.y = rs * (v.y - mr * lc.y) + bb.y;
+                    v.z = rs * (v.z - mr * lc.z) + bb.z; v.w = rs * (v.w - mr * lc.w) + bb.w;
+                } else {
+                    v.x = v.x * epi.alpha + bb.x; v.y = v.y * epi.alpha + bb.y;
+                    v.z = v.z * epi.alpha + bb.z; v.w = v.w * epi.alpha + bb.w;
+                }
                 if (epi.relu) { v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f); }
                 if (epi.res0 && !pre_res) {
                     float4 r0;
@@ -673,6 +744,7 @@ __global__ __launch_bounds__(C::NT) void gemm_bf16_kernel(const bf16* __restrict
                     const float4 r1 = *(const float4*)(epi.res1 + (long long)row * epi.ld_res1 + col);
                     v.x += r1.x; v.y += r1.y; v.z += r1.z; v.w += r1.w;
                 }
+                if constexpr (LN == 2) ln_stats_out(v, row, c4);
                 const long long ob = epi.out_map.off(row) + col;
                 if (f32o) *(float4*)((float*)epi.out + ob) = v;
                 else {
@@ -687,6 +759,11 @@ __global__ __launch_bounds__(C::NT) void gemm_bf16_kernel(const bf16* __restrict
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            if constexpr (lnf) {
+                if (i + 1 < MI)
+#pragma unroll
+                    for (int p = 0; p < 8; ++p) ln_cur[p] = ln_nxt[p];
+            }
         }
         return;
     }
@@ -939,23 +1016,33 @@ using C15 = Cfg<256, 256, 2, 4, 64, 2, 0, 1>;  // C1 on v_mfma_f32_16x16x32_bf16
 using C16 = Cfg<128, 256, 2, 4, 32, 3, 0, 1>;  // C4 on v_mfma_f32_16x16x32_bf16
 using C17 = Cfg<256, 256, 2, 4, 64, 2, 2, 1>;  // 8-phase schedule on v_mfma_f32_16x16x32_bf16 (K % 128 == 0)
 
-template <class C>
+template <class C, int LN = 0>
 hipError_t launch(const void* A, RowMap amap, const void* W, long long ldw, int M, int N, int K, const GemmEpi& e2,
                   hipStream_t st) {
     static bool attr_done = false;
     if (!attr_done) {
         attr_done = true;
-        (void)hipFuncSetAttribute((const void*)gemm_bf16_kernel<C>, hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
+        (void)hipFuncSetAttribute((const void*)gemm_bf16_kernel<C, LN>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  C::LDS);
     }
     const int tiles_m = (M + C::BM - 1) / C::BM, tiles_n = (N + C::BN - 1) / C::BN;
     // grouped tile order (4 tile-rows per group) for the wide-N projections (memory K|V, vocabulary:
     // +6 % measured), row-major otherwise; PFM_GEMM_GM overrides per launch (A/B)
     const char* eg = getenv("PFM_GEMM_GM");
     const int gm = eg ? atoi(eg) : (tiles_n >= 16 ? 4 : 0);
-    hipLaunchKernelGGL(gemm_bf16_kernel<C>, dim3(tiles_m * tiles_n), dim3(C::NT), C::LDS, st, (const bf16*)A, amap,
+    hipLaunchKernelGGL((gemm_bf16_kernel<C, LN>), dim3(tiles_m * tiles_n), dim3(C::NT), C::LDS, st, (const bf16*)A, amap,
                        (const bf16*)W, ldw, M, N, K, tiles_m, tiles_n, gm, e2);
     PFM_LAUNCH_CHECK();
     return hipSuccess;
+}
+
+// the configurations the path uses (C4, C15, C17) carry the LayerNorm epilogue variants
+template <class C>
+hipError_t launch_ln(const void* A, RowMap amap, const void* W, long long ldw, int M, int N, int K, const GemmEpi& e2,
+                     hipStream_t st) {
+    if (e2.ln_st_in) return launch<C, 1>(A, amap, W, ldw, M, N, K, e2, st);
+    if (e2.ln_st_out) return launch<C, 2>(A, amap, W, ldw, M, N, K, e2, st);
+    return launch<C, 0>(A, amap, W, ldw, M, N, K, e2, st);
 }
 
 int num_cus() {
@@ -1215,6 +1302,12 @@ hipError_t pfm_gemm_bf16_256(const void* A, RowMap amap, const void* W, long lon
     if (!pfm_gemm_bf16_256_ok(amap, ldw, K)) return hipErrorInvalidValue;
     GemmEpi e2 = epi;
     e2.vec_ok = epi_vec_ok(epi, N);
+    // the folded-LayerNorm consumer / statistics producer live in the vector epilogue of the tiled kernel
+    // (64-column wave slices: partial index = column / 64, at most 8 partials per row)
+    if ((epi.ln_st_in || epi.ln_st_out) &&
+        (!e2.vec_ok || epi.amax_val || epi.ln_parts < 1 || epi.ln_parts > 8 || (epi.ln_st_out && N != 64 * epi.ln_parts) ||
+         (epi.ln_st_in && (!epi.ln_colsum || epi.pre_res_ok))))
+        return hipErrorInvalidValue;
     {
         const char* ev = getenv("PFM_GEMM_ST16");   // read per launch (A/B runs); default on
         const RowMap& om = epi.out_map;
@@ -1230,10 +1323,13 @@ hipError_t pfm_gemm_bf16_256(const void* A, RowMap amap, const void* W, long lon
         const char* rb = getenv("PFM_GEMM_RESBATCH");   // residual loads batched ahead of the stores
         e2.res_batch = !(rb && rb[0] == '0');
     }
-    switch (pick_cfg(M, N, K, epi.amax_val != nullptr)) {
+    const bool ln = e2.ln_st_in || e2.ln_st_out;
+    int cfg = pick_cfg(M, N, K, epi.amax_val != nullptr);
+    if (ln && cfg != 4 && cfg != 15 && cfg != 17) cfg = 15;
+    switch (cfg) {
         case 2: return launch<C2>(A, amap, W, ldw, M, N, K, e2, st);
         case 3: return launch<C3>(A, amap, W, ldw, M, N, K, e2, st);
-        case 4: return launch<C4>(A, amap, W, ldw, M, N, K, e2, st);
+        case 4: return launch_ln<C4>(A, amap, W, ldw, M, N, K, e2, st);
         case 5: return launch<C5>(A, amap, W, ldw, M, N, K, e2, st);
         case 6: return launch<C6>(A, amap, W, ldw, M, N, K, e2, st);
         case 7: if (!e2.amax_val && e2.vec_ok) return launch_persist<C7, 16>(A, amap, W, ldw, M, N, K, e2, st);
@@ -1248,12 +1344,11 @@ hipError_t pfm_gemm_bf16_256(const void* A, RowMap amap, const void* W, long lon
         case 13: if (K % 128 == 0) return launch<C13>(A, amap, W, ldw, M, N, K, e2, st);
                  return launch<C1>(A, amap, W, ldw, M, N, K, e2, st);
         case 14: return launch<C14>(A, amap, W, ldw, M, N, K, e2, st);
-        case 15: return launch<C15>(A, amap, W, ldw, M, N, K, e2, st);
         case 16: return launch<C16>(A, amap, W, ldw, M, N, K, e2, st);
-        case 17: if (K % 128 == 0) return launch<C17>(A, amap, W, ldw, M, N, K, e2, st);
-                 return launch<C15>(A, amap, W, ldw, M, N, K, e2, st);
+        case 17: if (K % 128 == 0) return launch_ln<C17>(A, amap, W, ldw, M, N, K, e2, st);
+                 return launch_ln<C15>(A, amap, W, ldw, M, N, K, e2, st);
         case 1: return launch<C1>(A, amap, W, ldw, M, N, K, e2, st);
-        default: return launch<C15>(A, amap, W, ldw, M, N, K, e2, st);
+        default: return launch_ln<C15>(A, amap, W, ldw, M, N, K, e2, st);
     }
 }
 

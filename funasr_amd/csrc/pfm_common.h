@@ -90,6 +90,16 @@ struct GemmEpi {
     // set by the bf16 launcher: residual GEMMs may start their accumulators from res0 + res1
     int pre_res_ok;
     int res_batch;          // epilogue: residual loads of 4 row groups issued before their stores
+    // LayerNorm statistics producer (fast mode): per (output row, 64-column wave slice) the slice's
+    // (mean, M2) of the final values, at ln_st_out[row * ln_parts + col / 64]
+    float2* ln_st_out;
+    int ln_parts;
+    // LayerNorm folded into this GEMM (consumer): A = bf16(x), W = bf16(W o gamma) and
+    //   out = rstd_r * (acc - mean_r * ln_colsum[n]) + bias[n]        (bias = b + W.beta)
+    // with (mean_r, rstd_r) combined from the producer's ln_parts partials of row r
+    const float2* ln_st_in;
+    const float* ln_colsum;
+    float ln_eps;
 };
 
 static inline bool rowmap_vec4(const RowMap& m) {
