@@ -58,6 +58,8 @@ class ParaformerConfig:
     def d_k(self) -> int:
         return self.d_model // self.heads
 
+    input_layer = "pe"              # class constant (SinusoidalPositionEncoder), not a field
+
     def to_dict(self) -> Dict[str, Any]:
         return dataclasses.asdict(self)
 
@@ -78,8 +80,8 @@ class ParaformerConfig:
         c.enc_blocks = int(enc.get("num_blocks", c.enc_blocks))
         c.kernel_size = int(enc.get("kernel_size", c.kernel_size))
         c.enc_sanm_shift = int(enc.get("sanm_shfit", c.enc_sanm_shift))
-        if enc.get("input_layer", "pe") != "pe":
-            raise ValueError("only input_layer='pe' (SinusoidalPositionEncoder) is on the HIP path")
+        if enc.get("input_layer", cls.input_layer) != cls.input_layer:
+            raise ValueError(f"only input_layer='{cls.input_layer}' is on the HIP path of {cls.__name__}")
         if not enc.get("normalize_before", True):
             raise ValueError("only normalize_before=True is on the HIP path")
         nb = int(dec.get("num_blocks", c.dec_blocks))
@@ -136,6 +138,31 @@ def paraformer_large() -> ParaformerConfig:
 def paraformer_tiny(enc_blocks: int = 3, dec_blocks: int = 2, vocab_size: int = 8404) -> ParaformerConfig:
     """Reduced-depth config used for full-tensor golden vectors (same widths as large)."""
     return ParaformerConfig(enc_blocks=enc_blocks, dec_blocks=dec_blocks, vocab_size=vocab_size)
+
+
+@dataclass
+class ParaformerStreamingConfig(ParaformerConfig):
+    """Streaming Paraformer-large (paraformer_streaming/template.yaml): the Paraformer state_dict
+    with SANMEncoderChunkOpt (input_layer pe_online = StreamSinusoidalPositionEncoder,
+    scama/encoder.py:188) and a causal decoder FSMN (decoder sanm_shfit 5 -> left pad 10)."""
+    dec_sanm_shift: int = 5
+    input_layer = "pe_online"
+
+    def reference_kwargs(self) -> Dict[str, Any]:
+        kw = super().reference_kwargs()
+        kw["encoder"] = "SANMEncoderChunkOpt"
+        kw["encoder_conf"].update(input_layer="pe_online", chunk_size=[12, 15], stride=[8, 10], pad_left=[0, 0],
+                                  encoder_att_look_back_factor=[4, 4], decoder_att_look_back_factor=[1, 1])
+        return kw
+
+
+def paraformer_streaming() -> ParaformerStreamingConfig:
+    return ParaformerStreamingConfig()
+
+
+def paraformer_streaming_tiny(enc_blocks: int = 3, dec_blocks: int = 2,
+                              vocab_size: int = 8404) -> ParaformerStreamingConfig:
+    return ParaformerStreamingConfig(enc_blocks=enc_blocks, dec_blocks=dec_blocks, vocab_size=vocab_size)
 
 
 @dataclass

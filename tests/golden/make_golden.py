@@ -424,6 +424,137 @@ def save_automodel_sv_tiny():
     print("automodel sv:", {k: [r["text"][:20] for r in v] for k, v in out.items()})
 
 
+def build_stream_ref(cfg):
+    import funasr.models.scama.encoder  # noqa: F401
+    import funasr.models.paraformer_streaming.model  # noqa: F401
+    kw = cfg.reference_kwargs()
+    m = tables.model_classes["ParaformerStreaming"](
+        **{k: kw[k] for k in ("encoder", "encoder_conf", "decoder", "decoder_conf", "predictor", "predictor_conf")},
+        input_size=cfg.input_size, vocab_size=cfg.vocab_size, ctc_weight=0.0, predictor_bias=1)
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in make_weights(cfg, seed=0).items()}, strict=True)
+    m.eval()
+    return m
+
+
+class _Recorder:
+    """Wraps the reference encoder / predictor forward_chunk to keep each chunk's outputs."""
+
+    def __init__(self, m):
+        self.enc, self.alphas_in = [], []
+        fe, fp = m.encoder.forward_chunk, m.predictor.forward_chunk
+
+        def enc_chunk(*a, **k):
+            r = fe(*a, **k)
+            self.enc.append(r[0][0].detach().clone())
+            return r
+
+        def pred_chunk(hidden, cache=None, **k):
+            return fp(hidden, cache=cache, **k)
+
+        m.encoder.forward_chunk = enc_chunk
+        m.predictor.forward_chunk = pred_chunk
+
+
+def _stream_cache(m, elb, dlb):
+    cache = {}
+    m.init_cache(cache, chunk_size=[0, 10, 5], encoder_chunk_look_back=elb, decoder_chunk_look_back=dlb,
+                 encoder_conf={"output_size": 512}, frontend_conf={"n_mels": 80, "lfr_m": 7})
+    return cache
+
+
+class _IdsTok:
+    def ids2tokens(self, ids):
+        return list(ids)
+
+
+def save_stream():
+    """ParaformerStreaming (tiny: enc 3 / dec 2) chunk-level goldens: seeded LFR+CMVN chunks of 10
+    frames through the reference generate_chunk with its cache, for (encoder, decoder) look-back
+    (0, 0) and (4, 1), ending in a short final chunk or in the tail chunk (cached overlap only).
+    Then the waveform path: reference inference() over 600 ms sample chunks with WavFrontendOnline
+    (kaldi.fbank patched to oracle/fbank_ref.fbank, the pinned fbank restatement)."""
+    from funasr_amd.config import paraformer_streaming_tiny
+    cfg = paraformer_streaming_tiny()
+    m = build_stream_ref(cfg)
+    rec = _Recorder(m)
+    rng = np.random.default_rng(21)
+    chunks = [rng.standard_normal((10, 560), dtype=np.float32) for _ in range(8)]
+    last = rng.standard_normal((7, 560), dtype=np.float32)
+    out = dict(seed=21, chunks=np.stack(chunks), last=last)
+    for tag, (elb, dlb), tail in (("lb00", (0, 0), False), ("lb41", (4, 1), False), ("lb41_tail", (4, 1), True)):
+        cache = _stream_cache(m, elb, dlb)
+        rec.enc.clear()
+        toks = []
+        seq = chunks + ([None] if tail else [last])
+        for i, x in enumerate(seq):
+            fin = i == len(seq) - 1
+            if x is None:
+                cache["encoder"]["tail_chunk"] = True
+                t = cache["encoder"]["feats"]
+            else:
+                t = torch.from_numpy(x.copy())[None]
+            with torch.no_grad():
+                toks.append(m.generate_chunk(t, torch.tensor([t.shape[1]]), key=["k"], tokenizer=_IdsTok(),
+                                             cache=cache, is_final=fin, device="cpu"))
+        flat, off = pack_tokens(toks)
+        enc = [e.numpy() for e in rec.enc]
+        out[f"{tag}_tokens"], out[f"{tag}_off"] = flat, off
+        out[f"{tag}_enc"] = np.concatenate(enc)
+        out[f"{tag}_enc_off"] = np.cumsum([0] + [e.shape[0] for e in enc]).astype(np.int32)
+        print(tag, [len(t) for t in toks])
+    np.savez_compressed(f"{HERE}/stream_tiny.npz", **out)
+
+    # waveform path through the reference online frontend and inference()
+    import funasr.frontends.wav_frontend as wf
+    from oracle import fbank_ref
+    from tests.golden.inputs import waveform
+
+    def kfbank(w, **kw):
+        return torch.from_numpy(fbank_ref.fbank(w[0].numpy().astype(np.float32) / np.float32(32768.0)))
+
+    sys.modules["torchaudio.compliance.kaldi"].fbank = kfbank
+    wf.kaldi.fbank = kfbank
+    front = wf.WavFrontendOnline(cmvn_file=CMVN, fs=16000, window="hamming", n_mels=80, frame_length=25,
+                                 frame_shift=10, lfr_m=7, lfr_n=6, dither=0.0)
+    feats_log = []
+    ff = front.forward
+
+    def front_fwd(*a, **k):
+        r = ff(*a, **k)
+        feats_log.append(r[0][0].numpy().copy() if r[0].numel() else np.zeros((0, 560), np.float32))
+        return r
+
+    front.forward = front_fwd
+    vocab = token_list(cfg.vocab_size)
+
+    class Tok:
+        def ids2tokens(self, ids):
+            return [vocab[i] for i in ids]
+
+    wout = {}
+    for tag, n_total, calls in (("w1", 57600 + 2000, [9600] * 6 + [2000]), ("w2", 48000 + 500, [19200, 28800, 500])):
+        wav = waveform(seed=31 if tag == "w1" else 32, n=n_total)
+        cache = {}
+        texts, feats_log[:] = [], []
+        pos = 0
+        for j, n in enumerate(calls):
+            fin = j == len(calls) - 1
+            with torch.no_grad():
+                res, _ = m.inference([torch.from_numpy(wav[pos:pos + n].copy())], key=["s"], tokenizer=Tok(),
+                                     frontend=front, cache=cache, is_final=fin, chunk_size=[0, 10, 5],
+                                     encoder_chunk_look_back=4, decoder_chunk_look_back=1,
+                                     encoder_conf={"output_size": 512}, frontend_conf={"n_mels": 80, "lfr_m": 7},
+                                     device="cpu", data_type="sound")
+            texts.append(res[0]["text"])
+            pos += n
+        wout[tag] = dict(seed=31 if tag == "w1" else 32, n=n_total, calls=calls, texts=texts,
+                         feat_rows=[int(f.shape[0]) for f in feats_log])
+        np.save(f"{HERE}/stream_{tag}_feats.npy", np.concatenate(feats_log).astype(np.float32))
+        print(tag, texts, wout[tag]["feat_rows"])
+    with open(f"{HERE}/stream_wave.json", "w") as f:
+        json.dump(wout, f, ensure_ascii=False, indent=1)
+
+
 if __name__ == "__main__" and len(sys.argv) > 1:
     torch.manual_seed(0)
     for part in sys.argv[1:]:

@@ -142,3 +142,69 @@ def test_sensevoice_large_vs_reference(name):
     enc, ol = r["enc"].numpy(), r["enc_lens"].numpy()
     rows = np.stack([enc[b, [0, 3, 4, int(ol[b]) // 2, int(ol[b]) - 1]] for b in range(len(lens))])
     assert np.abs(rows - g["enc_rows"]).max() < 1e-5
+
+
+# ---------------------------------------------------------------- streaming Paraformer (config C5)
+@pytest.fixture(scope="module")
+def stream_tiny():
+    from funasr_amd.config import paraformer_streaming_tiny
+    cfg = paraformer_streaming_tiny()
+    return cfg, make_weights(cfg, seed=0), np.load(f"{GOLD}/stream_tiny.npz")
+
+
+@pytest.mark.parametrize("tag,elb,dlb,tail", [("lb00", 0, 0, False), ("lb41", 4, 1, False),
+                                              ("lb41_tail", 4, 1, True)])
+def test_streaming_chunks_vs_reference(stream_tiny, tag, elb, dlb, tail):
+    """oracle/streaming_ref.chunk_step vs the reference generate_chunk with its cache: token ids of
+    every chunk exact, the encoder window of every chunk to 1e-4."""
+    from oracle.streaming_ref import StreamState, chunk_step
+    cfg, w, g = stream_tiny
+    st = StreamState(cfg, (0, 10, 5), elb, dlb)
+    seq = list(g["chunks"]) + ([None] if tail else [g["last"]])
+    off, eoff = g[f"{tag}_off"], g[f"{tag}_enc_off"]
+    for i, x in enumerate(seq):
+        if x is None:
+            st.tail_chunk = True
+        r = chunk_step(x, st, w, cfg, i == len(seq) - 1)
+        assert r["tokens"] == g[f"{tag}_tokens"][off[i]:off[i + 1]].tolist(), (tag, i)
+        ref = g[f"{tag}_enc"][eoff[i]:eoff[i + 1]]
+        assert r["enc"].shape == ref.shape
+        np.testing.assert_allclose(r["enc"].numpy(), ref, atol=1e-4, rtol=1e-4)
+
+
+def test_streaming_waveform_vs_reference(stream_tiny):
+    """stream_infer (online frontend + chunk loop + prev_samples) vs the reference inference():
+    per-call text and every LFR+CMVN feature row the online frontend emitted."""
+    import json
+    from funasr_amd.text import sentence_postprocess
+    from oracle.streaming_ref import stream_infer
+    from tests.golden.inputs import token_list
+    cfg, w, _ = stream_tiny
+    cmvn = np.load(f"{GOLD}/lfr_cmvn.npz")["cmvn"]
+    vocab = token_list(cfg.vocab_size)
+    gold = json.load(open(f"{GOLD}/stream_wave.json"))
+    import oracle.streaming_ref as sr
+    for tag, gw in gold.items():
+        wav = waveform(seed=gw["seed"], n=gw["n"])
+        feats = []
+        orig = sr.FrontendOnline.__call__
+
+        def rec(self, seg, fin):
+            f = orig(self, seg, fin)
+            feats.append(f)
+            return f
+
+        sr.FrontendOnline.__call__ = rec
+        try:
+            state, pos = None, 0
+            for j, n in enumerate(gw["calls"]):
+                fin = j == len(gw["calls"]) - 1
+                toks, state = stream_infer(wav[pos:pos + n], w, cfg, cmvn=cmvn, enc_look_back=4, dec_look_back=1,
+                                           is_final=fin, state=state)
+                text, _ = sentence_postprocess([vocab[t] for ts in toks for t in ts])
+                assert text == gw["texts"][j], (tag, j)
+                pos += n
+        finally:
+            sr.FrontendOnline.__call__ = orig
+        assert [f.shape[0] for f in feats] == gw["feat_rows"], tag
+        np.testing.assert_allclose(np.concatenate(feats), np.load(f"{GOLD}/stream_{tag}_feats.npy"), atol=1e-5)
