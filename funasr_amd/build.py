@@ -23,7 +23,7 @@ LIB = os.path.join(OUT_DIR, "libpfm_hip.so")
 ARCH = os.environ.get("PFM_OFFLOAD_ARCH", "gfx950")
 
 # bit-exact host-order arithmetic (CIF / LayerNorm / fbank): no FMA contraction
-NO_CONTRACT = {"k_elem.hip", "k_fbank.hip"}
+NO_CONTRACT = {"k_elem.hip", "k_fbank.hip", "k_stream.hip"}
 
 
 def hipcc() -> str:

@@ -13,6 +13,7 @@
 
 #include "../../include/pfm.h"
 #include "pfm_common.h"
+#include "pfm_stream.h"
 
 // ---- kernel launchers (k_*.hip)
 hipError_t pfm_gemm(int dtype, const void* A, RowMap amap, const void* W, long long ldw, int M, int N, int K,
@@ -512,6 +513,8 @@ struct Run {
     float qscale;    // d_k ** -0.5
     bool fuse_fsmn;  // fast mode: encoder FSMN in the attention epilogue
     bool fuse_ln;    // opt-in (PFM_GEMM_LN=1): LayerNorm fused into the 512-wide projections
+    bool raw_input = false;                 // streaming: the stack input is already x sqrt(d) + PE
+    const struct ChunkKV* ck = nullptr;     // streaming: self-attention keys = K/V cache ++ window
 
     Run(pfm_handle* h_, hipStream_t st_, bool fast_) : h(h_), st(st_), fast(fast_) {
         const pfm_config& c = h->cfg;
@@ -557,6 +560,18 @@ struct Run {
         return pfm_gemm_bf16_ln(A, am, Wt, ldw, Mm, D, Kk, e, h->w(g), h->w(b), h->cfg.ln_eps, lo, lm, ldt, lo2, lm2,
                                 st);
     }
+};
+
+// Streaming encoder self-attention with encoder_chunk_look_back (sanm/attention.py:313-339): per layer the
+// keys are [that layer's K/V cache ; the window's K|V rows], gathered into buf [n][Tk][2d]; afterwards
+// the cache keeps the last C rows of [cache ; window minus its `drop` look-ahead rows].
+struct ChunkKV {
+    void* cache;              // [layers][slots][C][2d] in the operand dtype
+    long long layer_stride;   // elements per layer
+    int C, drop, Tk;
+    void* buf;                // [n][Tk][2d]
+    const SPrm* prm;          // device, n entries
+    const int* klen;          // device [n]: cle + tw
 };
 
 // LayerNorm that closes an encoder stack (after_norm / tp_norm): out (+ optional second copy).
@@ -625,7 +640,10 @@ int encoder_stack(const Run& r, const float* x_in, const int* lens, int B, int T
     for (int l = l0; l < l1; ++l) {
         const EncLayer& L = h->enc[l];
         const int din = L.din;
-        if (l == 0)   // x = x_in * sqrt(d_model) + PE ; LN1
+        if (l == 0 && r.raw_input)   // streaming: the window already holds x sqrt(d) + PE
+            HIP_TRY(pfm_layernorm(x_in, rowmap_plain(I), (int)M, I, r.P(L.ln1g), r.P(L.ln1b), c.ln_eps, nullptr, 0,
+                                  1.f, Xn, rowmap_plain(I), dt, nullptr, plain, 0, st));
+        else if (l == 0)   // x = x_in * sqrt(d_model) + PE ; LN1
             HIP_TRY(pfm_layernorm(x_in, rowmap_plain(I), (int)M, I, r.P(L.ln1g), r.P(L.ln1b), c.ln_eps,
                                   h->pe.as<float>(), T, sqrtf((float)D), Xn, rowmap_plain(I), dt, nullptr, plain, 0,
                                   st));
@@ -647,7 +665,24 @@ int encoder_stack(const Run& r, const float* x_in, const int* lens, int B, int T
         // FSMN memory on v (attention.py:207-223) + masked MHA. Fast mode: the FSMN runs in the attention
         // kernel's epilogue (each block owns its rows x head channels; V is L2-resident) when the shape
         // allows (K 11, left 5); bf16 in / bf16 out either way
-        if (r.fuse_fsmn) {
+        if (r.ck) {   // streaming with look-back: FSMN over the window, attention over cache ++ window
+            const ChunkKV& ck = *r.ck;
+            const size_t es = fast ? 2 : 4;
+            const void* qkv = fast ? (const void*)QKVb : (const void*)QKV;
+            void* cache = (char*)ck.cache + (size_t)l * ck.layer_stride * es;
+            HIP_TRY(pfm_kv_gather(dt, cache, ck.C, ck.prm, B, 0, (const char*)qkv + (size_t)D * es, 3 * D, T, ck.buf,
+                                  ck.Tk, 2 * D, st));
+            if (fast)
+                HIP_TRY(pfm_fsmn_bf16in(QKVb + 2 * D, rowmap_plain(3 * D), lens, B, T, D, r.P(L.fsmn), K, lenc, nullptr,
+                                        nullptr, Fb, st));
+            else
+                HIP_TRY(pfm_fsmn(QKV + 2 * D, rowmap_plain(3 * D), lens, B, T, D, r.P(L.fsmn), K, lenc, nullptr, Fm,
+                                 nullptr, st));
+            const RowMap km = rowmap_seg(ck.Tk, (long long)ck.Tk * 2 * D, 2 * D);
+            HIP_TRY(r.attn(dt, qkv, rowmap_plain(3 * D), ck.buf, km, (const char*)ck.buf + (size_t)D * es, km,
+                           fast ? nullptr : O, D, fast ? (void*)Ob : nullptr, ck.klen, B, T, ck.Tk));
+            HIP_TRY(pfm_kv_retain(dt, ck.buf, ck.Tk, ck.prm, B, 0, ck.drop, nullptr, cache, ck.C, 2 * D, st));
+        } else if (r.fuse_fsmn) {
             const double dk = c.d_model / c.heads;
             const double fl = 4.0 * B * (double)T * T * dk * c.heads;
             const double by = 3.0 * B * T * c.d_model * 2.0 + 2.0 * B * T * c.d_model * 2.0;
@@ -1289,6 +1324,365 @@ int pfm_op_cif(void* stream, const float* alphas, const float* hidden, float* em
     HIP_TRY(pfm_cif_fire(alphas, hidden, rowmap_plain(D), B, T, D, L_cap, emb, peaks, n_fire, ntok,
                          (hipStream_t)stream));
     return PFM_OK;
+}
+
+}  // extern "C"
+
+// ============================================================================================
+// Streaming Paraformer (include/pfm.h, pfm_streams_*): per-slot chunk caches in HBM.
+// ============================================================================================
+struct pfm_streams {
+    pfm_handle* h = nullptr;
+    int slots = 0, cs[3] = {0, 10, 5}, elb = 0, dlb = 0, mode = PFM_MODE_EXACT;
+    int C0 = 5, Ce = 0, Cd = 0;   // overlap rows, encoder / decoder K/V cache capacities (rows)
+    DevBuf fcache;                // [slots][C0][I] f32   cache["encoder"]["feats"]
+    DevBuf ekv;                   // [enc layers][slots][Ce][2d] operand dtype
+    DevBuf dkv;                   // [dec layers][slots][Cd][2d] operand dtype
+    DevBuf dfs;                   // [dec layers][slots][K-1][d] f32   decode_fsmn
+    DevBuf chid, calpha;          // [slots][d], [slots] f32           cif_hidden / cif_alphas
+    DevBuf prm;                   // per step: SPrm[n] | tw[n] | kle[n] | kld[n]
+    DevBuf xin, kvbuf, kvw, pe;   // window input, gathered keys, decoder memory K|V, PE table
+    int pe_T = 0;
+    std::vector<int> start, cle, cld;   // host mirrors per slot
+    std::vector<unsigned char> hprm;
+    int32_t* hntok = nullptr;
+    int hntok_cap = 0;
+};
+
+namespace {
+
+// One streaming decoder pass (decoder.py:461-528 over n streams x L token rows): decoders with FFN ->
+// causal FSMN (chunk cache) -> cross attention over [K/V cache ;] the window memory, decoders3, after_norm,
+// output layer with fused argmax.
+int stream_decoder(pfm_streams* s, const Run& r, int n, int Tw, int L, const SPrm* prm, const int* tw_d,
+                   const int* kld_d, const int* ntok, int32_t* tokens, int L_cap) {
+    pfm_handle* h = s->h;
+    const pfm_config& c = h->cfg;
+    const hipStream_t st = r.st;
+    const bool fast = r.fast;
+    const int dt = r.dt, D = c.d_model, Fd = c.ffn, K = c.kernel_size, nkv = c.dec_blocks * 2 * D;
+    const size_t es = fast ? 2 : 4;
+    const long long Ml = (long long)n * L, Mw = (long long)n * Tw;
+    const RowMap plain = rowmap_plain(0);
+    float* Xd = h->Xd.as<float>();
+    void* Xdn = h->Xdn.p;
+    float* Hd = h->Hd.as<float>();
+    void* Hdn = h->Hdn.p;
+    float* Td = h->Td.as<float>();
+    void* Tdn = h->Tdn.p;
+    void* Qd = h->Qd.p;
+    float* Od = h->Od.as<float>();
+    bf16* Odb = h->Odb.as<bf16>();
+    const float* encp = h->encp.as<float>();
+    const bf16* encpb = h->encpb.as<bf16>();
+    const RowMap encmap = rowmap_seg(Tw, (long long)(Tw + 2) * D, D);
+    const int Lc = Tw + 2;
+    HIP_TRY(hipMemcpy2DAsync(Xd, (size_t)L * D * 4, h->emb.p, (size_t)Lc * D * 4, (size_t)L * D * 4, n,
+                             hipMemcpyDeviceToDevice, st));
+    HIP_TRY(s->kvw.ensure((size_t)Mw * nkv * es));
+    {   // memory K|V of every decoder layer from the window (rows i*Tw + t)
+        GemmEpi e = epi_default();
+        e.bias = r.P(h->bkv_all);
+        e.out = s->kvw.p; e.out_map = rowmap_plain(nkv); e.out_dtype = dt;
+        const void* A = fast ? (const void*)(encpb + D) : (const void*)(encp + D);
+        HIP_TRY(r.gemm(dt, A, encmap, r.W(h->wkv_all), D, (int)Mw, nkv, D, e));
+    }
+    auto ffn = [&](const float* x, size_t lng, size_t lnb, size_t w1, size_t b1, size_t fng, size_t fnb, size_t w2,
+                   float* out, size_t pg, size_t pb, void* pout, int pdt) -> int {
+        HIP_TRY(pfm_layernorm(x, rowmap_plain(D), (int)Ml, D, r.P(lng), r.P(lnb), c.ln_eps, nullptr, 0, 1.f, Xdn,
+                              rowmap_plain(D), dt, nullptr, plain, 0, st));
+        GemmEpi e = epi_default();
+        e.bias = r.P(b1); e.relu = 1;
+        e.out = Hd; e.out_map = rowmap_plain(Fd); e.out_dtype = dt;
+        HIP_TRY(r.gemm(dt, Xdn, rowmap_plain(D), r.W(w1), D, (int)Ml, Fd, D, e));
+        if (fast)
+            HIP_TRY(pfm_layernorm_bf16in((const bf16*)Hd, rowmap_plain(Fd), (int)Ml, Fd, r.P(fng), r.P(fnb), c.ln_eps,
+                                         Hdn, rowmap_plain(Fd), dt, st));
+        else
+            HIP_TRY(pfm_layernorm(Hd, rowmap_plain(Fd), (int)Ml, Fd, r.P(fng), r.P(fnb), c.ln_eps, nullptr, 0, 1.f,
+                                  Hdn, rowmap_plain(Fd), dt, nullptr, plain, 0, st));
+        GemmEpi e2 = epi_default();
+        e2.out = out; e2.out_map = rowmap_plain(D); e2.out_dtype = DT_F32;
+        HIP_TRY(r.gemm(dt, Hdn, rowmap_plain(Fd), r.W(w2), Fd, (int)Ml, D, Fd, e2));
+        HIP_TRY(pfm_layernorm(out, rowmap_plain(D), (int)Ml, D, r.P(pg), r.P(pb), c.ln_eps, nullptr, 0, 1.f, pout,
+                              rowmap_plain(D), pdt, nullptr, plain, 0, st));
+        return PFM_OK;
+    };
+    const int Tk = s->Cd + Tw;
+    if (s->dlb > 0) HIP_TRY(s->kvbuf.ensure((size_t)n * std::max(Tk, s->Ce + Tw) * 2 * D * es));
+    for (int l = 0; l < c.dec_blocks; ++l) {
+        const DecLayer& Lr = h->dec[l];
+        int rc = ffn(Xd, Lr.n1g, Lr.n1b, Lr.w1, Lr.b1, Lr.ng, Lr.nb, Lr.w2, Td, Lr.n2g, Lr.n2b, Tdn, dt);
+        if (rc) return rc;
+        HIP_TRY(pfm_dec_fsmn_stream(dt, Tdn, r.P(Lr.fsmn), K, s->dfs.as<float>() + (size_t)l * s->slots * (K - 1) * D,
+                                    prm, ntok, n, L, D, Xd, st));
+        HIP_TRY(pfm_layernorm(Xd, rowmap_plain(D), (int)Ml, D, r.P(Lr.n3g), r.P(Lr.n3b), c.ln_eps, nullptr, 0, 1.f,
+                              Xdn, rowmap_plain(D), dt, nullptr, plain, 0, st));
+        {
+            GemmEpi e = epi_default();
+            e.bias = r.P(Lr.bq);
+            e.out = Qd; e.out_map = rowmap_plain(D); e.out_dtype = dt;
+            HIP_TRY(r.gemm(dt, Xdn, rowmap_plain(D), r.W(Lr.wq), D, (int)Ml, D, D, e));
+        }
+        const char* kvl = (const char*)s->kvw.p + (size_t)l * 2 * D * es;
+        if (s->dlb > 0) {
+            void* cache = (char*)s->dkv.p + (size_t)l * s->slots * s->Cd * 2 * D * es;
+            HIP_TRY(pfm_kv_gather(dt, cache, s->Cd, prm, n, 1, kvl, nkv, Tw, s->kvbuf.p, Tk, 2 * D, st));
+            const RowMap km = rowmap_seg(Tk, (long long)Tk * 2 * D, 2 * D);
+            HIP_TRY(r.attn(dt, Qd, rowmap_plain(D), s->kvbuf.p, km, (const char*)s->kvbuf.p + (size_t)D * es, km,
+                           fast ? nullptr : Od, D, fast ? (void*)Odb : nullptr, kld_d, n, L, Tk));
+            HIP_TRY(pfm_kv_retain(dt, s->kvbuf.p, Tk, prm, n, 1, 0, ntok, cache, s->Cd, 2 * D, st));
+        } else {
+            HIP_TRY(r.attn(dt, Qd, rowmap_plain(D), kvl, rowmap_plain(nkv), kvl + (size_t)D * es, rowmap_plain(nkv),
+                           fast ? nullptr : Od, D, fast ? (void*)Odb : nullptr, tw_d, n, L, Tw));
+        }
+        {
+            GemmEpi e = epi_default();
+            e.bias = r.P(Lr.bo);
+            e.res0 = Xd; e.ld_res0 = D;
+            e.out = Xd; e.out_map = rowmap_plain(D); e.out_dtype = DT_F32;
+            HIP_TRY(r.gemm(dt, fast ? (const void*)Odb : (const void*)Od, rowmap_plain(D), r.W(Lr.wo), D, (int)Ml, D,
+                           D, e));
+        }
+    }
+    int rc = ffn(Xd, h->d3n1g, h->d3n1b, h->d3w1, h->d3b1, h->d3ng, h->d3nb, h->d3w2, Xd, h->dan_g, h->dan_b, Xdn, dt);
+    if (rc) return rc;
+    const int ntl = amax_tiles(dt, rowmap_plain(D), D, c.vocab_size, D);
+    GemmEpi e = epi_default();
+    e.bias = r.P(h->out_b);
+    e.amax_val = h->amv.as<float>(); e.amax_idx = h->ami.as<int>(); e.n_tiles = ntl;
+    e.out = nullptr;
+    HIP_TRY(r.gemm(dt, Xdn, rowmap_plain(D), r.W(h->out_w), D, (int)Ml, c.vocab_size, D, e));
+    if (L_cap > 0)
+        HIP_TRY(pfm_argmax_reduce(h->amv.as<float>(), h->ami.as<int>(), ntl, (c.vocab_size + 63) / 64, n, L, ntok,
+                                  L_cap, tokens, nullptr, st));
+    return PFM_OK;
+}
+
+int streams_zero(pfm_streams* s, hipStream_t st, int slot) {
+    const pfm_config& c = s->h->cfg;
+    const size_t D = c.d_model, I = c.input_size, K1 = c.kernel_size - 1;
+    const size_t es = s->mode == PFM_MODE_FAST ? 2 : 4;
+    HIP_TRY(hipMemsetAsync(s->fcache.as<float>() + (size_t)slot * s->C0 * I, 0, (size_t)s->C0 * I * 4, st));
+    HIP_TRY(hipMemsetAsync(s->chid.as<float>() + (size_t)slot * D, 0, D * 4, st));
+    HIP_TRY(hipMemsetAsync(s->calpha.as<float>() + slot, 0, 4, st));
+    for (int l = 0; l < c.dec_blocks; ++l)
+        HIP_TRY(hipMemsetAsync(s->dfs.as<float>() + ((size_t)l * s->slots + slot) * K1 * D, 0, K1 * D * 4, st));
+    // K/V caches need no clearing: rows beyond cle / cld are never read
+    (void)es;
+    s->start[slot] = 0;
+    s->cle[slot] = 0;
+    s->cld[slot] = 0;
+    return PFM_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int pfm_streams_create(pfm_handle* h, int slots, const int32_t* chunk_size, int enc_look_back, int dec_look_back,
+                       int mode, pfm_streams** out) {
+    if (!h || !chunk_size || !out) return fail(PFM_E_ARG, "pfm_streams_create: null argument");
+    *out = nullptr;
+    const pfm_config& c = h->cfg;
+    if (c.arch != PFM_ARCH_PARAFORMER) return fail(PFM_E_STATE, "pfm_streams_create: handle is not a Paraformer");
+    if (c.dec_sanm_shift != 5 || c.kernel_size != 11)
+        return fail(PFM_E_ARG, "pfm_streams_create: streaming needs the causal decoder FSMN (kernel 11, sanm_shfit 5)");
+    if (slots < 1) return fail(PFM_E_ARG, "pfm_streams_create: slots must be >= 1");
+    if (chunk_size[0] < 0 || chunk_size[1] < 1 || chunk_size[2] < 0 || chunk_size[0] + chunk_size[2] < 1 ||
+        chunk_size[0] + chunk_size[1] + chunk_size[2] > 60)
+        return fail(PFM_E_ARG, "pfm_streams_create: bad chunk_size");
+    if (enc_look_back < 0 || dec_look_back < 0 || enc_look_back > 64 || dec_look_back > 64)
+        return fail(PFM_E_ARG, "pfm_streams_create: look-back must be in [0, 64] (unbounded -1 is not supported)");
+    if (mode != PFM_MODE_EXACT && mode != PFM_MODE_FAST) return fail(PFM_E_ARG, "pfm_streams_create: bad mode");
+    HIP_TRY(hipSetDevice(h->device));
+    std::unique_ptr<pfm_streams> s(new pfm_streams());
+    s->h = h;
+    s->slots = slots;
+    for (int k = 0; k < 3; ++k) s->cs[k] = chunk_size[k];
+    s->elb = enc_look_back;
+    s->dlb = dec_look_back;
+    s->mode = mode;
+    s->C0 = chunk_size[0] + chunk_size[2];
+    s->Ce = enc_look_back * chunk_size[1];
+    s->Cd = dec_look_back * chunk_size[1];
+    const size_t D = c.d_model, I = c.input_size, K1 = c.kernel_size - 1, es = mode == PFM_MODE_FAST ? 2 : 4;
+    HIP_TRY(s->fcache.ensure((size_t)slots * s->C0 * I * 4));
+    HIP_TRY(s->chid.ensure((size_t)slots * D * 4));
+    HIP_TRY(s->calpha.ensure((size_t)slots * 4));
+    HIP_TRY(s->dfs.ensure((size_t)std::max(c.dec_blocks, 1) * slots * K1 * D * 4));
+    if (s->Ce) HIP_TRY(s->ekv.ensure((size_t)c.enc_blocks * slots * s->Ce * 2 * D * es));
+    if (s->Cd) HIP_TRY(s->dkv.ensure((size_t)std::max(c.dec_blocks, 1) * slots * s->Cd * 2 * D * es));
+    s->start.assign(slots, 0);
+    s->cle.assign(slots, 0);
+    s->cld.assign(slots, 0);
+    for (int k = 0; k < slots; ++k) {
+        int rc = streams_zero(s.get(), nullptr, k);
+        if (rc) return rc;
+    }
+    HIP_TRY(hipDeviceSynchronize());
+    *out = s.release();
+    return PFM_OK;
+}
+
+int pfm_streams_reset(pfm_streams* s, void* stream, const int32_t* slot_ids, int n) {
+    if (!s || (n > 0 && !slot_ids)) return fail(PFM_E_ARG, "pfm_streams_reset: null argument");
+    HIP_TRY(hipSetDevice(s->h->device));
+    for (int k = 0; k < n; ++k) {
+        if (slot_ids[k] < 0 || slot_ids[k] >= s->slots) return fail(PFM_E_ARG, "pfm_streams_reset: bad slot id");
+        int rc = streams_zero(s, (hipStream_t)stream, slot_ids[k]);
+        if (rc) return rc;
+    }
+    return PFM_OK;
+}
+
+int pfm_stream_step(pfm_streams* s, void* stream, int n, const int32_t* slot_ids, const float* feats, int Tn,
+                    const int32_t* nfeat, const int32_t* is_final, int32_t* tokens, int L_cap, int32_t* ntok_out,
+                    float* enc_out, float* alphas_out) {
+    if (!s || !slot_ids || !nfeat || !is_final || !tokens || !ntok_out)
+        return fail(PFM_E_ARG, "pfm_stream_step: null argument");
+    if (n < 1 || Tn < 0 || L_cap < 0) return fail(PFM_E_ARG, "pfm_stream_step: bad sizes");
+    pfm_handle* h = s->h;
+    const pfm_config& c = h->cfg;
+    if (h->missing) return fail(PFM_E_STATE, "pfm_stream_step: weights not set");
+    int maxn = 0;
+    std::vector<char> seen(s->slots, 0);
+    for (int i = 0; i < n; ++i) {
+        const int sl = slot_ids[i];
+        if (sl < 0 || sl >= s->slots || seen[sl]) return fail(PFM_E_ARG, "pfm_stream_step: bad or repeated slot id");
+        seen[sl] = 1;
+        if (nfeat[i] < 0 || nfeat[i] > Tn) return fail(PFM_E_ARG, "pfm_stream_step: nfeat out of [0, Tn]");
+        if (nfeat[i] == 0 && !is_final[i]) return fail(PFM_E_ARG, "pfm_stream_step: the tail chunk (nfeat 0) must be final");
+        maxn = std::max(maxn, (int)nfeat[i]);
+    }
+    if (maxn > 0 && !feats) return fail(PFM_E_ARG, "pfm_stream_step: feats is null");
+    HIP_TRY(hipSetDevice(h->device));
+    hipStream_t st = (hipStream_t)stream;
+    const bool fast = s->mode == PFM_MODE_FAST;
+    const int D = c.d_model, I = c.input_size, C0 = s->C0;
+    const int Tw = C0 + maxn;
+    int rc = reserve(h, n, Tw + 2);
+    if (rc) return rc;
+    if (fast) { rc = ensure_bf16(h, st); if (rc) return rc; }
+    // PE rows up to the furthest position of this step (grown by doubling)
+    int need = 1;
+    for (int i = 0; i < n; ++i) need = std::max(need, s->start[slot_ids[i]] + (int)nfeat[i]);
+    if (need > s->pe_T) {
+        const int T2 = std::max(need, std::max(2 * s->pe_T, 1024));
+        std::vector<float> pe;
+        make_pe(pe, T2, I);
+        HIP_TRY(hipStreamSynchronize(st));
+        HIP_TRY(s->pe.ensure(pe.size() * 4));
+        HIP_TRY(hipMemcpy(s->pe.p, pe.data(), pe.size() * 4, hipMemcpyHostToDevice));
+        s->pe_T = T2;
+    }
+    // per-stream parameters: SPrm[n] | tw[n] | kle[n] | kld[n]
+    const size_t pb = (size_t)n * sizeof(SPrm), ib = (size_t)n * 4;
+    s->hprm.resize(pb + 3 * ib);
+    SPrm* hp = (SPrm*)s->hprm.data();
+    int* htw = (int*)(s->hprm.data() + pb);
+    int* hkle = htw + n;
+    int* hkld = hkle + n;
+    for (int i = 0; i < n; ++i) {
+        const int sl = slot_ids[i];
+        SPrm p;
+        p.slot = sl; p.nfeat = nfeat[i]; p.start = s->start[sl]; p.tw = C0 + nfeat[i]; p.fin = is_final[i] ? 1 : 0;
+        p.cle = s->Ce ? s->cle[sl] : 0; p.cld = s->Cd ? s->cld[sl] : 0; p.pad = 0;
+        hp[i] = p;
+        htw[i] = p.tw;
+        hkle[i] = p.cle + p.tw;
+        hkld[i] = p.cld + p.tw;
+    }
+    HIP_TRY(s->prm.ensure(s->hprm.size()));
+    HIP_TRY(hipMemcpyAsync(s->prm.p, s->hprm.data(), s->hprm.size(), hipMemcpyHostToDevice, st));
+    const SPrm* prm = s->prm.as<SPrm>();
+    const int* tw_d = (const int*)((const char*)s->prm.p + pb);
+    const int* kle_d = tw_d + n;
+    const int* kld_d = kle_d + n;
+
+    // ---- encoder window + SANMEncoderChunkOpt.forward_chunk (scama/encoder.py:456-499)
+    HIP_TRY(s->xin.ensure((size_t)n * Tw * I * 4));
+    float* xin = s->xin.as<float>();
+    HIP_TRY(pfm_stream_window(feats, Tn, prm, n, s->fcache.as<float>(), s->pe.as<float>(), I, C0, Tw,
+                              sqrtf((float)D), xin, st));
+    HIP_TRY(pfm_stream_fcache(xin, prm, n, I, C0, Tw, s->fcache.as<float>(), st));
+    Run run(h, st, fast);
+    run.fuse_fsmn = false;
+    run.raw_input = true;
+    ChunkKV ck;
+    const size_t es = fast ? 2 : 4;
+    if (s->Ce) {
+        const int Tk = s->Ce + Tw;
+        HIP_TRY(s->kvbuf.ensure((size_t)n * std::max(Tk, s->Cd + Tw) * 2 * D * es));
+        ck.cache = s->ekv.p;
+        ck.layer_stride = (long long)s->slots * s->Ce * 2 * D;
+        ck.C = s->Ce; ck.drop = s->cs[2]; ck.Tk = Tk;
+        ck.buf = s->kvbuf.p; ck.prm = prm; ck.klen = kle_d;
+        run.ck = &ck;
+    }
+    float* encp = h->encp.as<float>();
+    bf16* encpb = h->encpb.as<bf16>();
+    const RowMap encmap = rowmap_seg(Tw, (long long)(Tw + 2) * D, D);
+    HIP_TRY(hipMemset2DAsync(encp, (size_t)(Tw + 2) * D * 4, 0, (size_t)D * 4, n, st));
+    HIP_TRY(hipMemset2DAsync(encp + (size_t)(Tw + 1) * D, (size_t)(Tw + 2) * D * 4, 0, (size_t)D * 4, n, st));
+    if (fast) {
+        HIP_TRY(hipMemset2DAsync(encpb, (size_t)(Tw + 2) * D * 2, 0, (size_t)D * 2, n, st));
+        HIP_TRY(hipMemset2DAsync(encpb + (size_t)(Tw + 1) * D, (size_t)(Tw + 2) * D * 2, 0, (size_t)D * 2, n, st));
+    }
+    {
+        const FinalLN fin = {h->an_g, h->an_b, encp + D, encmap, DT_F32, fast ? (void*)(encpb + D) : nullptr, encmap,
+                             DT_BF16};
+        rc = encoder_stack(run, xin, tw_d, n, Tw, 0, c.enc_blocks, h->X.as<float>(), fin, enc_ws(h, 0));
+        if (rc) return rc;
+    }
+    HIP_TRY(pfm_stream_mask_rows(encp, fast ? encpb : nullptr, prm, n, Tw, D, st));
+    if (enc_out)
+        HIP_TRY(hipMemcpy2DAsync(enc_out, (size_t)Tw * D * 4, encp + D, (size_t)(Tw + 2) * D * 4, (size_t)Tw * D * 4, n,
+                                 hipMemcpyDeviceToDevice, st));
+    // ---- CifPredictorV2.forward_chunk (cif_predictor.py:255-344)
+    {
+        GemmEpi e = epi_default();
+        e.bias = run.P(h->cif_b); e.relu = 1;
+        e.out = h->Hc.p; e.out_map = rowmap_plain(D); e.out_dtype = DT_F32;
+        const void* A = fast ? (const void*)encpb : (const void*)encp;
+        HIP_TRY(run.gemm(run.dt, A, rowmap_seg(Tw, (long long)(Tw + 2) * D, D), run.W(h->cif_w), 3 * D, n * Tw, D,
+                         3 * D, e));
+    }
+    const int Lc = Tw + 2;
+    int* ntok = h->ntok.as<int>();
+    HIP_TRY(pfm_cif_chunk(h->Hc.as<float>(), run.P(h->cif_ow), run.P(h->cif_ob), encp, prm, n, Tw, D, s->cs[0],
+                          s->cs[0] + s->cs[1], c.smooth_factor, c.noise_threshold, c.tail_threshold, c.cif_threshold,
+                          s->chid.as<float>(), s->calpha.as<float>(), h->emb.as<float>(), Lc, ntok, alphas_out, st));
+    HIP_TRY(hipMemcpyAsync(ntok_out, ntok, (size_t)n * 4, hipMemcpyDeviceToDevice, st));
+    if (s->hntok_cap < n) {
+        if (s->hntok) (void)hipHostFree(s->hntok);
+        s->hntok = nullptr;
+        HIP_TRY(hipHostMalloc((void**)&s->hntok, (size_t)n * 4, 0));
+        s->hntok_cap = n;
+    }
+    HIP_TRY(hipMemcpyAsync(s->hntok, ntok, (size_t)n * 4, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    int L = 0;
+    for (int i = 0; i < n; ++i) L = std::max(L, (int)s->hntok[i]);
+    // host mirrors of the caches (the device caches were advanced by the kernels above / below)
+    for (int i = 0; i < n; ++i) {
+        const int sl = slot_ids[i];
+        const int tw = C0 + nfeat[i];
+        s->start[sl] += nfeat[i] ? nfeat[i] : C0;
+        if (s->Ce) s->cle[sl] = std::min(s->Ce, s->cle[sl] + tw - s->cs[2]);
+        if (s->Cd && s->hntok[i] > 0) s->cld[sl] = std::min(s->Cd, s->cld[sl] + tw);
+    }
+    if (L_cap > 0) HIP_TRY(pfm_fill_i32(tokens, (long long)n * L_cap, -1, st));
+    if (L < 1 || c.dec_blocks < 1) return PFM_OK;   // model.py:490-491: nothing to decode
+    return stream_decoder(s, run, n, Tw, L, prm, tw_d, kld_d, ntok, tokens, L_cap);
+}
+
+void pfm_streams_destroy(pfm_streams* s) {
+    if (!s) return;
+    (void)hipSetDevice(s->h->device);
+    (void)hipDeviceSynchronize();
+    if (s->hntok) (void)hipHostFree(s->hntok);
+    delete s;
 }
 
 }  // extern "C"

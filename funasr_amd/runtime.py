@@ -26,7 +26,8 @@ MODES = {"exact": MODE_EXACT, "fp32": MODE_EXACT, "fast": MODE_FAST, "bf16": MOD
 ABI_SYMBOLS = ("pfm_config_default", "pfm_config_sensevoice", "pfm_create", "pfm_set_weight",
                "pfm_missing_weights", "pfm_reserve", "pfm_run", "pfm_run_ctc", "pfm_op_ctc_collapse", "pfm_fbank", "pfm_lfr_frames", "pfm_last_error", "pfm_destroy", "pfm_op_gemm",
                "pfm_op_attention", "pfm_op_layernorm", "pfm_op_fsmn", "pfm_op_cif", "pfm_profile", "pfm_op_gemm_layernorm", "pfm_op_fsmn_bf16", "pfm_op_layernorm_bf16",
-               "pfm_profile_read")
+               "pfm_profile_read", "pfm_streams_create", "pfm_streams_reset", "pfm_stream_step",
+               "pfm_streams_destroy")
 
 
 class PfmError(RuntimeError):
@@ -95,6 +96,13 @@ def load_library(path: Optional[str] = None) -> ctypes.CDLL:
     lib.pfm_op_fsmn_bf16.argtypes = [vp, vp, i32p, f32p, vp, i32, i32, i32, i32, i32]
     lib.pfm_op_gemm_layernorm.argtypes = [vp, vp, vp, f32p, f32p, f32p, f32p, f32p, ctypes.c_float, f32p, i32, i32,
                                           i32]
+    lib.pfm_streams_create.argtypes = [vp, i32, ctypes.POINTER(ctypes.c_int32), i32, i32, i32, ctypes.POINTER(vp)]
+    lib.pfm_streams_reset.argtypes = [vp, vp, ctypes.POINTER(ctypes.c_int32), i32]
+    lib.pfm_stream_step.argtypes = [vp, vp, i32, ctypes.POINTER(ctypes.c_int32), f32p, i32,
+                                    ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32), i32p, i32, i32p,
+                                    f32p, f32p]
+    lib.pfm_streams_destroy.argtypes = [vp]
+    lib.pfm_streams_destroy.restype = None
     for name in ABI_SYMBOLS:
         getattr(lib, name)
     if path is None:
@@ -250,6 +258,70 @@ class PfmEngine:
 
 
 # ---- single-op helpers (kernel-level parity tests) ------------------------------------------
+class PfmStreams:
+    """A pfm_streams object: `slots` streaming-Paraformer streams with their chunk caches in HBM
+    (ParaformerStreaming.init_cache, paraformer_streaming/model.py:435-466, one per slot)."""
+
+    def __init__(self, engine: PfmEngine, slots: int, chunk_size=(0, 10, 5), encoder_chunk_look_back: int = 0,
+                 decoder_chunk_look_back: int = 0, mode="exact"):
+        self.engine, self.lib, self.torch = engine, engine.lib, engine.torch
+        self.slots = int(slots)
+        self.chunk_size = [int(x) for x in chunk_size]
+        self.mode = MODES[mode] if isinstance(mode, str) else int(mode)
+        cs = (ctypes.c_int32 * 3)(*self.chunk_size)
+        h = ctypes.c_void_p()
+        check(self.lib.pfm_streams_create(engine.h, self.slots, cs, int(encoder_chunk_look_back),
+                                          int(decoder_chunk_look_back), self.mode, ctypes.byref(h)),
+              "pfm_streams_create")
+        self.h = h
+
+    def __del__(self):
+        h = getattr(self, "h", None)
+        if h is not None and h.value:
+            try:
+                self.lib.pfm_streams_destroy(h)
+            except Exception:
+                pass
+            self.h = None
+
+    def reset(self, slot_ids) -> None:
+        ids = [int(x) for x in slot_ids]
+        arr = (ctypes.c_int32 * max(len(ids), 1))(*ids)
+        dev = self.torch.device("cuda", self.engine.device)
+        check(self.lib.pfm_streams_reset(self.h, _stream_ptr(self.torch, dev), arr, len(ids)), "pfm_streams_reset")
+
+    def step(self, slot_ids, feats, nfeat, is_final, L_cap: Optional[int] = None, want_enc=False, want_alphas=False):
+        """One chunk for len(slot_ids) streams. feats [n, Tn, input_size] f32 cuda (or None when every
+        stream is on its tail chunk), nfeat / is_final: n host ints -> dict of cuda tensors."""
+        torch = self.torch
+        dev = torch.device("cuda", self.engine.device)
+        ids = [int(x) for x in slot_ids]
+        n = len(ids)
+        nf = [int(x) for x in nfeat]
+        fin = [1 if x else 0 for x in is_final]
+        if len(nf) != n or len(fin) != n:
+            raise PfmError("slot_ids, nfeat and is_final must have one entry per stream")
+        Tn = 0
+        if feats is not None:
+            if feats.device != dev or feats.dtype != torch.float32 or not feats.is_contiguous():
+                feats = feats.to(device=dev, dtype=torch.float32).contiguous()
+            if feats.dim() != 3 or feats.shape[0] != n or feats.shape[2] != self.engine.cfg.input_size:
+                raise PfmError(f"feats must be [n, Tn, {self.engine.cfg.input_size}]")
+            Tn = feats.shape[1]
+        C0 = self.chunk_size[0] + self.chunk_size[2]
+        Tw = C0 + max(nf)
+        L_cap = Tw + 2 if L_cap is None else int(L_cap)
+        tokens = torch.empty((n, max(L_cap, 1)), dtype=torch.int32, device=dev)
+        ntok = torch.empty((n,), dtype=torch.int32, device=dev)
+        enc = torch.empty((n, Tw, self.engine.cfg.d_model), dtype=torch.float32, device=dev) if want_enc else None
+        alphas = torch.empty((n, Tw), dtype=torch.float32, device=dev) if want_alphas else None
+        I32 = ctypes.c_int32 * n
+        check(self.lib.pfm_stream_step(self.h, _stream_ptr(torch, dev), n, I32(*ids), _ptr(feats), Tn, I32(*nf),
+                                       I32(*fin), _ptr(tokens), L_cap, _ptr(ntok), _ptr(enc), _ptr(alphas)),
+              "pfm_stream_step")
+        return dict(tokens=tokens, ntok=ntok, enc=enc, alphas=alphas)
+
+
 def op_gemm(A, W, bias=None, res=None, relu=False, out_bf16=False):
     import torch
     lib = load_library()

@@ -140,6 +140,45 @@ int pfm_run_ctc(pfm_handle* h, void* stream, int mode, const float* feats, const
                 int B, int T, const int32_t* query, int ban_token, int32_t* tokens, int L_cap,
                 int32_t* ntok, float* enc_out, int32_t* frame_ids);
 
+/* ---- Streaming Paraformer (ParaformerStreaming, paraformer_streaming/model.py:435-656) ----
+ * A pfm_streams object holds `slots` independent streams whose chunk caches live in HBM:
+ * the encoder input overlap (cache["encoder"]["feats"]), the per-layer encoder K/V look-back
+ * cache (encoder_chunk_look_back), the CIF carry (cif_hidden / cif_alphas), the decoder FSMN
+ * caches (decode_fsmn) and the decoder cross-attention K/V cache (decoder_chunk_look_back).
+ * One pfm_stream_step advances any subset of slots by one chunk in a single batched pass —
+ * the reference's generate_chunk (model.py:468-554) applied to each listed stream.
+ * The handle must be a Paraformer whose config has dec_sanm_shift 5 (causal decoder FSMN).
+ *   chunk_size      3 host ints [0, 10, 5] (chunk_size kwarg); chunk_size[0] + chunk_size[2]
+ *                   rows of overlap, alphas beyond chunk_size[0] + chunk_size[1] masked
+ *   enc_look_back   encoder_chunk_look_back >= 0 (-1, unbounded, is rejected)
+ *   dec_look_back   decoder_chunk_look_back >= 0
+ *   mode            PFM_MODE_EXACT / PFM_MODE_FAST for every step of this object
+ * Replaces init_cache (model.py:435-466). */
+typedef struct pfm_streams pfm_streams;
+int pfm_streams_create(pfm_handle* h, int slots, const int32_t* chunk_size, int enc_look_back,
+                       int dec_look_back, int mode, pfm_streams** out);
+
+/* Reset slots to the init_cache state (zero caches, start_idx 0). slot_ids: n HOST ints. */
+int pfm_streams_reset(pfm_streams* s, void* stream, const int32_t* slot_ids, int n);
+
+/* One chunk for n streams (generate_chunk, greedy path):
+ *   slot_ids  n HOST ints, distinct
+ *   feats     [n, Tn, input_size] f32 device: the chunk's LFR+CMVN rows (WavFrontendOnline output)
+ *   nfeat     n HOST ints, rows of feats per stream (<= Tn); 0 = the tail chunk (model.py:601-607:
+ *             final call with < 960 samples; the encoder sees the cached overlap only)
+ *   is_final  n HOST ints
+ *   tokens    [n, L_cap] int32 out: argmax ids of the chunk's decoder rows (blank/sos/eos NOT
+ *             removed), -1 beyond ntok
+ *   ntok      [n] int32 out: CIF fires this chunk (0: the decoder did not run for that stream)
+ * Optional (NULL to skip): enc_out [n, 5 + max(nfeat), d_model] f32 encoder window after
+ * after_norm (rows >= window length zero); alphas [n, 5 + max(nfeat)] f32 chunk-masked CIF weights.
+ * Synchronises `stream` once (max ntok sizes the decoder). */
+int pfm_stream_step(pfm_streams* s, void* stream, int n, const int32_t* slot_ids, const float* feats,
+                    int Tn, const int32_t* nfeat, const int32_t* is_final, int32_t* tokens, int L_cap,
+                    int32_t* ntok, float* enc_out, float* alphas);
+
+void pfm_streams_destroy(pfm_streams* s);
+
 /* Kaldi fbank (80 mel, 25/10 ms, hamming, dither 0, snip_edges) -> LFR (7, 6) -> CMVN for a
  * batch of waveforms: WavFrontend.forward (funasr/frontends/wav_frontend.py:118-158).
  *   wav     [B, S_max] f32 samples in [-1, 1) (scaled by 32768 inside, upsacle_samples)

@@ -1,0 +1,179 @@
+"""Streaming Paraformer (config C5) through the C-ABI: pfm_streams_create / pfm_stream_step vs the
+reference generate_chunk goldens (tests/golden/stream_tiny.npz) and vs oracle/streaming_ref.chunk_step
+for batched, ragged streams that join and finish at different steps.
+
+EXACT mode: token ids of every chunk exact; encoder window rows within 1e-4 (as the oracle's own
+golden check); CIF chunk-masked alphas within 1e-5. FAST mode: token agreement floor.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from funasr_amd.config import paraformer_streaming, paraformer_streaming_tiny  # noqa: E402
+from funasr_amd.runtime import PfmEngine, PfmStreams  # noqa: E402
+from funasr_amd.weights import make_weights  # noqa: E402
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+DROP = (0, 1, 2)
+
+
+def _eng(cfg):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    w = make_weights(cfg, seed=0)
+    e = PfmEngine(cfg, 0)
+    e.load_state_dict(w)
+    return e, w
+
+
+@pytest.fixture(scope="module")
+def tiny():
+    cfg = paraformer_streaming_tiny()
+    e, w = _eng(cfg)
+    return cfg, e, w
+
+
+def _toks(r, i):
+    n = int(r["ntok"][i])
+    return [t for t in r["tokens"][i, :n].tolist() if t not in DROP]
+
+
+@pytest.mark.parametrize("tag,elb,dlb,tail", [("lb00", 0, 0, False), ("lb41", 4, 1, False),
+                                              ("lb41_tail", 4, 1, True)])
+def test_stream_golden_one_slot(tiny, tag, elb, dlb, tail):
+    cfg, e, _ = tiny
+    g = np.load(f"{GOLD}/stream_tiny.npz")
+    s = PfmStreams(e, 1, (0, 10, 5), elb, dlb, "exact")
+    seq = list(g["chunks"]) + ([None] if tail else [g["last"]])
+    off, eoff = g[f"{tag}_off"], g[f"{tag}_enc_off"]
+    for i, x in enumerate(seq):
+        fin = i == len(seq) - 1
+        feats = None if x is None else torch.from_numpy(np.ascontiguousarray(x[None])).cuda()
+        nf = 0 if x is None else x.shape[0]
+        r = s.step([0], feats, [nf], [fin], want_enc=True)
+        torch.cuda.synchronize()
+        r = {k: (v.cpu() if v is not None else None) for k, v in r.items()}
+        assert _toks(r, 0) == g[f"{tag}_tokens"][off[i]:off[i + 1]].tolist(), (tag, i)
+        ref = g[f"{tag}_enc"][eoff[i]:eoff[i + 1]]
+        np.testing.assert_allclose(r["enc"][0, : ref.shape[0]].numpy(), ref, atol=1e-4, rtol=1e-4)
+
+
+def _schedules(rng, I):
+    """Three streams: A full chunks, B ragged chunks (joins at step 1), C short (ends with a tail)."""
+    def chunks(ns):
+        return [rng.standard_normal((n, I)).astype(np.float32) if n else None for n in ns]
+    return {0: (0, chunks([10, 10, 10, 10, 6])), 1: (1, chunks([10, 7, 10, 3])), 2: (0, chunks([10, 10, 0]))}
+
+
+@pytest.mark.parametrize("elb,dlb", [(0, 0), (4, 1), (2, 2)])
+def test_stream_batched_ragged_vs_oracle(tiny, elb, dlb):
+    from oracle.streaming_ref import StreamState, chunk_step
+    cfg, e, w = tiny
+    rng = np.random.default_rng(5 + elb)
+    sched = _schedules(rng, cfg.input_size)
+    s = PfmStreams(e, 4, (0, 10, 5), elb, dlb, "exact")
+    # slots deliberately not 0..n-1: stream k lives in slot 3-k
+    states = {k: StreamState(cfg, (0, 10, 5), elb, dlb) for k in sched}
+    nsteps = max(j0 + len(cs) for j0, cs in sched.values())
+    for step in range(nsteps):
+        act = [k for k, (j0, cs) in sched.items() if j0 <= step < j0 + len(cs)]
+        xs = [sched[k][1][step - sched[k][0]] for k in act]
+        fins = [step - sched[k][0] == len(sched[k][1]) - 1 for k in act]
+        nf = [0 if x is None else x.shape[0] for x in xs]
+        Tn = max(nf)
+        feats = None
+        if Tn:
+            f = np.zeros((len(act), Tn, cfg.input_size), np.float32)
+            for i, x in enumerate(xs):
+                if x is not None:
+                    f[i, : x.shape[0]] = x
+            feats = torch.from_numpy(f).cuda()
+        r = s.step([3 - k for k in act], feats, nf, fins, want_enc=True, want_alphas=True)
+        torch.cuda.synchronize()
+        r = {k: (v.cpu() if v is not None else None) for k, v in r.items()}
+        for i, k in enumerate(act):
+            st = states[k]
+            if xs[i] is None:
+                st.tail_chunk = True
+            ref = chunk_step(xs[i], st, w, cfg, fins[i])
+            assert int(r["ntok"][i]) == ref["ntok"], (step, k)
+            assert _toks(r, i) == ref["tokens"], (step, k)
+            tw = ref["enc"].shape[0]
+            np.testing.assert_allclose(r["enc"][i, :tw].numpy(), ref["enc"].numpy(), atol=1e-4, rtol=1e-4)
+            assert np.abs(r["enc"][i, tw:].numpy()).max(initial=0.0) == 0.0
+            np.testing.assert_allclose(r["alphas"][i, :tw].numpy(), ref["alphas"].numpy(), atol=1e-5)
+
+
+def test_stream_reset_reuses_slot(tiny):
+    """A finished slot reset by pfm_streams_reset behaves like a fresh stream."""
+    cfg, e, _ = tiny
+    g = np.load(f"{GOLD}/stream_tiny.npz")
+    s = PfmStreams(e, 2, (0, 10, 5), 4, 1, "exact")
+    seq = list(g["chunks"][:3])
+    for x in seq:
+        s.step([1], torch.from_numpy(np.ascontiguousarray(x[None])).cuda(), [10], [False])
+    s.reset([1])
+    off = g["lb41_off"]
+    for i, x in enumerate(list(g["chunks"]) + [g["last"]]):
+        r = s.step([1], torch.from_numpy(np.ascontiguousarray(x[None])).cuda(), [x.shape[0]], [i == 8])
+        torch.cuda.synchronize()
+        assert _toks({k: v.cpu() for k, v in r.items() if v is not None}, 0) == \
+            g["lb41_tokens"][off[i]:off[i + 1]].tolist(), i
+
+
+def test_stream_fast_mode_agreement(tiny):
+    cfg, e, _ = tiny
+    g = np.load(f"{GOLD}/stream_tiny.npz")
+    s = PfmStreams(e, 1, (0, 10, 5), 4, 1, "fast")
+    seq = list(g["chunks"]) + [g["last"]]
+    off = g["lb41_off"]
+    agree = total = 0
+    for i, x in enumerate(seq):
+        r = s.step([0], torch.from_numpy(np.ascontiguousarray(x[None])).cuda(), [x.shape[0]], [i == len(seq) - 1])
+        torch.cuda.synchronize()
+        got = _toks({k: v.cpu() for k, v in r.items() if v is not None}, 0)
+        ref = g["lb41_tokens"][off[i]:off[i + 1]].tolist()
+        total += max(len(ref), len(got))
+        agree += sum(a == b for a, b in zip(got, ref))
+    assert total > 0 and agree / total >= 0.6, (agree, total)
+
+
+def test_stream_large_exact_vs_oracle():
+    """Paraformer-streaming large (50 + 16 layers): 6 chunks of one stream, token ids exact."""
+    from oracle.streaming_ref import StreamState, chunk_step
+    cfg = paraformer_streaming()
+    e, w = _eng(cfg)
+    rng = np.random.default_rng(3)
+    s = PfmStreams(e, 1, (0, 10, 5), 4, 1, "exact")
+    st = StreamState(cfg, (0, 10, 5), 4, 1)
+    ns = [10, 10, 10, 10, 10, 4]
+    for i, n in enumerate(ns):
+        x = rng.standard_normal((n, cfg.input_size)).astype(np.float32)
+        fin = i == len(ns) - 1
+        r = s.step([0], torch.from_numpy(x[None]).cuda(), [n], [fin], want_enc=True)
+        torch.cuda.synchronize()
+        r = {k: (v.cpu() if v is not None else None) for k, v in r.items()}
+        ref = chunk_step(x, st, w, cfg, fin)
+        assert _toks(r, 0) == ref["tokens"], i
+        tw = ref["enc"].shape[0]
+        d = r["enc"][0, :tw].numpy() - ref["enc"].numpy()
+        assert np.linalg.norm(d) / np.linalg.norm(ref["enc"].numpy()) < 1e-5, i
+
+
+def test_stream_bad_args(tiny):
+    from funasr_amd.runtime import PfmError
+    cfg, e, _ = tiny
+    s = PfmStreams(e, 2, (0, 10, 5), 0, 0, "exact")
+    x = torch.zeros((1, 10, cfg.input_size), device="cuda")
+    with pytest.raises(PfmError):
+        s.step([2], x, [10], [False])            # slot out of range
+    with pytest.raises(PfmError):
+        s.step([0], x, [0], [False])             # tail chunk must be final
+    with pytest.raises(PfmError):
+        s.step([0, 0], torch.zeros((2, 10, cfg.input_size), device="cuda"), [10, 10], [False, False])
+    with pytest.raises(PfmError):
+        PfmStreams(e, 1, (0, 10, 5), -1, 0, "exact")
