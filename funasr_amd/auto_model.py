@@ -25,7 +25,8 @@ import torch
 
 from . import model as _model  # noqa: F401  (registers "Paraformer")
 from . import sense_voice as _sense_voice  # noqa: F401  (registers "SenseVoiceSmall")
-from .frontend import WavFrontend
+from . import streaming as _streaming  # noqa: F401  (registers "ParaformerStreaming")
+from .frontend import WavFrontend, WavFrontendOnline
 from .register import tables
 from .text import CharTokenizer, SentencepiecesTokenizer
 
@@ -156,7 +157,8 @@ class AutoModel:
         tokenizer, vocab = build_tokenizer(tok_name, kwargs.get("tokenizer_conf"))
         kwargs["tokenizer"] = tokenizer
         fconf = kwargs.get("frontend_conf") or {}
-        kwargs["frontend"] = WavFrontend(**fconf)
+        online = kwargs.get("frontend") == "WavFrontendOnline" or name == "ParaformerStreaming"
+        kwargs["frontend"] = (WavFrontendOnline if online else WavFrontend)(**fconf)
         if tokenizer is None:
             vocab = kwargs.get("vocab_size", -1)
         model_conf = kwargs.get("model_conf") or {}

@@ -140,7 +140,58 @@ __global__ __launch_bounds__(256) void lfr_cmvn_kernel(const float* __restrict__
     *(float4*)(feats + row * (LFR_M * NMEL) + c4 * 4) = v;
 }
 
+// Online LFR (WavFrontendOnline.apply_lfr, wav_frontend.py:275-310, + apply_cmvn): row r stacks the
+// m frames frames[idx[r * m + j]], j = 0..m-1 (indices computed on the host from the splice-cache and
+// frame counts, the only state the reference's as_strided depends on). One float4 of output per thread.
+__global__ __launch_bounds__(256) void lfr_gather_kernel(const float* __restrict__ frames, const int* __restrict__ idx,
+                                                         int rows, int m, const float* __restrict__ cmvn,
+                                                         float* __restrict__ out) {
+    const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    const int q = m * NMEL / 4;
+    if (gid >= (long long)rows * q) return;
+    const int c4 = (int)(gid % q);
+    const int r = (int)(gid / q);
+    const int col = c4 * 4, j = col / NMEL, mm = col % NMEL;
+    float4 v = *(const float4*)(frames + (long long)idx[r * m + j] * NMEL + mm);
+    if (cmvn) {
+        const float4 sh = *(const float4*)(cmvn + col), sc = *(const float4*)(cmvn + m * NMEL + col);
+        v.x = (v.x + sh.x) * sc.x; v.y = (v.y + sh.y) * sc.y;
+        v.z = (v.z + sh.z) * sc.z; v.w = (v.w + sh.w) * sc.w;
+    }
+    *(float4*)(out + (long long)r * (m * NMEL) + col) = v;
+}
+
 }  // namespace
+
+hipError_t pfm_fbank_raw_launch(const float* wav, const int* nsamp, int B, int S_max, const unsigned char* tables,
+                                float* fb, int N_cap, hipStream_t st) {
+    const float* melw = (const float*)tables;
+    const int* lo = (const int*)(tables + NMEL * NBIN * 4);
+    const int* hi = lo + NMEL;
+    const float* window = (const float*)(hi + NMEL);
+    const size_t twoff = ((size_t)(NMEL * NBIN * 4 + NMEL * 8 + FL * 4) + 15) & ~size_t(15);
+    const double2* tw = (const double2*)(tables + twoff);
+    const long long nfr = (long long)B * N_cap;
+    {
+        hipError_t e = hipMemsetAsync(fb, 0, (size_t)nfr * NMEL * 4, st);
+        if (e != hipSuccess) return e;
+    }
+    if (nfr == 0) return hipSuccess;
+    hipLaunchKernelGGL(fbank_kernel, dim3((unsigned)((nfr + FPB - 1) / FPB)), dim3(256), 0, st, wav, nsamp, B, S_max,
+                       N_cap, window, tw, melw, lo, hi, fb);
+    PFM_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+hipError_t pfm_lfr_gather_launch(const float* frames, const int* idx, int rows, int m, const float* cmvn, float* out,
+                                 hipStream_t st) {
+    const long long n4 = (long long)rows * (m * NMEL / 4);
+    if (n4 == 0) return hipSuccess;
+    hipLaunchKernelGGL(lfr_gather_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, st, frames, idx, rows, m,
+                       cmvn, out);
+    PFM_LAUNCH_CHECK();
+    return hipSuccess;
+}
 
 int pfm_fbank_frames(int nsamp) {
     const int n = frames_of(nsamp);

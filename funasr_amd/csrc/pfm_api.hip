@@ -60,6 +60,10 @@ hipError_t pfm_f32_to_bf16(const float* x, bf16* y, long long n, hipStream_t st)
 hipError_t pfm_fbank_launch(const float* wav, const int* nsamp, int B, int S_max, const float* cmvn,
                             const unsigned char* tables, float* fb_ws, int N_cap, float* feats, int T_cap, int* T_out,
                             hipStream_t st);
+hipError_t pfm_fbank_raw_launch(const float* wav, const int* nsamp, int B, int S_max, const unsigned char* tables,
+                                float* fb, int N_cap, hipStream_t st);
+hipError_t pfm_lfr_gather_launch(const float* frames, const int* idx, int rows, int m, const float* cmvn, float* out,
+                                 hipStream_t st);
 int pfm_fbank_frames(int nsamp);
 int pfm_fbank_nframes(int nsamp);
 void pfm_fbank_tables(float* melw, int* lo, int* hi, float* window, double* tw);
@@ -1208,6 +1212,41 @@ int pfm_run_ctc(pfm_handle* h, void* stream, int mode, const float* feats, const
     return PFM_OK;
 }
 
+static int fbank_tables_ready(pfm_handle* h) {
+    if (h->fb_tab_ready) return PFM_OK;
+    std::vector<unsigned char> tab(pfm_fbank_table_bytes(), 0);
+    float* melw = (float*)tab.data();
+    int* lo = (int*)(tab.data() + 80 * 256 * 4);
+    int* hi = lo + 80;
+    float* window = (float*)(hi + 80);
+    double* tw = (double*)(tab.data() + pfm_fbank_twoff());
+    pfm_fbank_tables(melw, lo, hi, window, tw);
+    HIP_TRY(h->fb_tab.ensure(tab.size()));
+    HIP_TRY(hipMemcpy(h->fb_tab.p, tab.data(), tab.size(), hipMemcpyHostToDevice));
+    h->fb_tab_ready = true;
+    return PFM_OK;
+}
+
+int pfm_fbank_raw(pfm_handle* h, void* stream, const float* wav, const int32_t* nsamp, int B, int S_max, float* fb,
+                  int N_cap) {
+    if (!h || !wav || !nsamp || !fb) return fail(PFM_E_ARG, "pfm_fbank_raw: null argument");
+    if (B < 1 || S_max < 1 || N_cap < 1) return fail(PFM_E_ARG, "pfm_fbank_raw: bad sizes");
+    if (pfm_fbank_nframes(S_max) > N_cap) return fail(PFM_E_ARG, "pfm_fbank_raw: N_cap smaller than frames of S_max");
+    HIP_TRY(hipSetDevice(h->device));
+    int rc = fbank_tables_ready(h);
+    if (rc) return rc;
+    HIP_TRY(pfm_fbank_raw_launch(wav, nsamp, B, S_max, h->fb_tab.as<unsigned char>(), fb, N_cap, (hipStream_t)stream));
+    return PFM_OK;
+}
+
+int pfm_lfr_gather(void* stream, const float* frames, const int32_t* idx, int rows, int m, const float* cmvn,
+                   float* out) {
+    if (rows < 0 || m < 1 || (m * 80) % 4) return fail(PFM_E_ARG, "pfm_lfr_gather: bad sizes");
+    if (rows > 0 && (!frames || !idx || !out)) return fail(PFM_E_ARG, "pfm_lfr_gather: null argument");
+    HIP_TRY(pfm_lfr_gather_launch(frames, idx, rows, m, cmvn, out, (hipStream_t)stream));
+    return PFM_OK;
+}
+
 int pfm_fbank(pfm_handle* h, void* stream, const float* wav, const int32_t* nsamp, int B, int S_max,
               const float* cmvn, float* feats, int T_cap, int32_t* T_out) {
     if (!h || !wav || !nsamp || !feats || !T_out) return fail(PFM_E_ARG, "pfm_fbank: null argument");
@@ -1215,18 +1254,9 @@ int pfm_fbank(pfm_handle* h, void* stream, const float* wav, const int32_t* nsam
     if (pfm_fbank_frames(S_max) > T_cap) return fail(PFM_E_ARG, "pfm_fbank: T_cap smaller than LFR frames of S_max");
     HIP_TRY(hipSetDevice(h->device));
     hipStream_t st = (hipStream_t)stream;
-    if (!h->fb_tab_ready) {
-        std::vector<unsigned char> tab(pfm_fbank_table_bytes(), 0);
-        float* melw = (float*)tab.data();
-        int* lo = (int*)(tab.data() + 80 * 256 * 4);
-        int* hi = lo + 80;
-        float* window = (float*)(hi + 80);
-        double* tw = (double*)(tab.data() + pfm_fbank_twoff());
-        pfm_fbank_tables(melw, lo, hi, window, tw);
-        HIP_TRY(h->fb_tab.ensure(tab.size()));
-        HIP_TRY(hipMemcpy(h->fb_tab.p, tab.data(), tab.size(), hipMemcpyHostToDevice));
-        h->fb_tab_ready = true;
-    }
+    int rc = fbank_tables_ready(h);
+    if (rc) return rc;
+
     const int N_cap = std::max(1, pfm_fbank_nframes(S_max));
     HIP_TRY(h->fb_ws.ensure((size_t)B * N_cap * 80 * 4));
     HIP_TRY(pfm_fbank_launch(wav, nsamp, B, S_max, cmvn, h->fb_tab.as<unsigned char>(), h->fb_ws.as<float>(), N_cap,

@@ -93,3 +93,118 @@ class WavFrontend:
         dev = torch.device("cuda", engine.device)
         feats, t_out = engine.fbank(torch.from_numpy(buf).to(dev), torch.from_numpy(ns).to(dev), self.cmvn)
         return feats, t_out, ns
+
+
+class WavFrontendOnline(WavFrontend):
+    """Online fbank + LFR + CMVN (WavFrontendOnline, funasr/frontends/wav_frontend.py:211-478), batched
+    over streams. Per stream the cache holds what the reference's does, reduced to what its outputs
+    depend on: the carried samples (`input_cache`, forward_fbank :322-333), the length of
+    `reserve_waveforms` (its contents are never read, only its size and emptiness, :424-445), and the
+    LFR splice frames (`lfr_splice_cache`, kept on the device). The integer bookkeeping of apply_lfr
+    (:275-310) runs on the host; the fbank frames (pfm_fbank_raw) and the LFR/CMVN row gather
+    (pfm_lfr_gather) run in k_fbank.hip.
+    """
+    FL, FS = 400, 160
+
+    def __init__(self, cmvn_file: Optional[str] = None, **kwargs):
+        super().__init__(cmvn_file=cmvn_file, **kwargs)
+        self.lfr_m = 7
+        self._cmvn_dev = {}
+
+    @staticmethod
+    def init_cache(cache: dict) -> dict:
+        cache.clear()
+        cache.update(input_cache=np.zeros((0,), np.float32), reserve_len=0, splice=None)
+        return cache
+
+    def _cmvn_on(self, torch, dev):
+        if self.cmvn is None:
+            return None
+        k = str(dev)
+        if k not in self._cmvn_dev:
+            self._cmvn_dev[k] = torch.from_numpy(np.ascontiguousarray(self.cmvn, dtype=np.float32)).to(dev)
+        return self._cmvn_dev[k]
+
+    def _lfr_index(self, T: int, is_final: bool):
+        """apply_lfr on T frames: (frame index per output row [rows, m], splice_idx). Padded frames of the
+        final chunk repeat the last frame (:285-293)."""
+        m, n = self.lfr_m, self.lfr_n
+        T_lfr = int(np.ceil((T - (m - 1) // 2) / n))
+        splice_idx = T_lfr
+        last_idx = (T - m) // n + 1
+        num_padding = m - (T - last_idx * n)
+        rows, T_in = T_lfr, T
+        if is_final:
+            if num_padding > 0:
+                num_padding = (2 * m - 2 * T + (T_lfr - 1 + last_idx) * n) / 2 * (T_lfr - last_idx)
+                T_in = T + int(num_padding)
+        elif num_padding > 0:
+            rows = last_idx
+            splice_idx = last_idx
+        splice_idx = min(T - 1, splice_idx * n)
+        rows = max(rows, 0)
+        idx = np.arange(rows)[:, None] * n + np.arange(m)[None, :]
+        if rows and idx.max() >= T_in:
+            raise ValueError("online LFR would read past the input frames (apply_lfr as_strided)")
+        return np.minimum(idx, T - 1).astype(np.int32), splice_idx
+
+    def step(self, engine, items):
+        """items: list of (wav chunk (1-D f32), is_final, cache) -> list of feats [rows, 560] cuda f32
+        (rows may be 0), one pfm_fbank_raw launch and one pfm_lfr_gather launch for all streams."""
+        import torch
+        dev = torch.device("cuda", engine.device)
+        xs, nfrs = [], []
+        for wav, _, cache in items:
+            if not cache:
+                self.init_cache(cache)
+            x = np.concatenate([cache["input_cache"], self.load(wav)])
+            nfr = int((x.shape[0] - self.FL) / self.FS + 1)
+            nfr = nfr if nfr >= 1 and x.shape[0] >= self.FL else 0
+            keep = x.shape[0] - nfr * self.FS
+            cache["input_cache"] = x[-keep:] if keep else x     # x[-0:] is all of x (:331-333)
+            xs.append(x[: (nfr - 1) * self.FS + self.FL] if nfr else x[:0])
+            nfrs.append(nfr)
+        fb = None
+        if any(nfrs):
+            S = max(len(u) for u in xs)
+            buf = np.zeros((len(xs), S), np.float32)
+            for k, u in enumerate(xs):
+                buf[k, : len(u)] = u
+            fb = engine.fbank_raw(torch.from_numpy(buf).to(dev), [len(u) for u in xs])
+        srcs, idxs, offs, out_rows = [], [], 0, []
+        for k, (wav, is_final, cache) in enumerate(items):
+            nfr, used = nfrs[k], xs[k]
+            rows_k = 0
+            if nfr:
+                fbk = fb[k, :nfr]
+                waves_len = cache["reserve_len"] + len(used)
+                if cache["splice"] is None:
+                    cache["splice"] = fbk[:1].repeat((self.lfr_m - 1) // 2, 1)
+                if nfr + cache["splice"].shape[0] >= self.lfr_m:
+                    feats = torch.cat([cache["splice"], fbk])
+                    idx, sidx = self._lfr_index(feats.shape[0], is_final)
+                    from_w = int((waves_len - self.FL) / self.FS + 1)
+                    minus = (self.lfr_m - 1) // 2 if cache["reserve_len"] == 0 else 0
+                    lo = min(max((sidx - minus) * self.FS, 0), waves_len)
+                    hi = min(max(from_w * self.FS, 0), waves_len)
+                    cache["reserve_len"] = max(0, hi - lo)
+                    cache["splice"] = feats[sidx:].clone()
+                    srcs.append(feats)
+                    idxs.append(idx + offs)
+                    offs += feats.shape[0]
+                    rows_k = idx.shape[0]
+                else:
+                    cache["reserve_len"] = max(0, waves_len - (self.FL - self.FS))
+                    cache["splice"] = torch.cat([cache["splice"], fbk])
+            elif is_final and cache["splice"] is not None:
+                idx, _ = self._lfr_index(cache["splice"].shape[0], True)
+                srcs.append(cache["splice"])
+                idxs.append(idx + offs)
+                offs += cache["splice"].shape[0]
+                rows_k = idx.shape[0]
+            out_rows.append(rows_k)
+        if not srcs or sum(out_rows) == 0:
+            return [torch.zeros((0, 80 * self.lfr_m), dtype=torch.float32, device=dev) for _ in items]
+        frames = torch.cat(srcs) if len(srcs) > 1 else srcs[0]
+        allf = engine.lfr_gather(frames, np.concatenate(idxs), self.lfr_m, self._cmvn_on(torch, dev))
+        return list(torch.split(allf, out_rows))

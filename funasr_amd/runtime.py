@@ -27,7 +27,7 @@ ABI_SYMBOLS = ("pfm_config_default", "pfm_config_sensevoice", "pfm_create", "pfm
                "pfm_missing_weights", "pfm_reserve", "pfm_run", "pfm_run_ctc", "pfm_op_ctc_collapse", "pfm_fbank", "pfm_lfr_frames", "pfm_last_error", "pfm_destroy", "pfm_op_gemm",
                "pfm_op_attention", "pfm_op_layernorm", "pfm_op_fsmn", "pfm_op_cif", "pfm_profile", "pfm_op_gemm_layernorm", "pfm_op_fsmn_bf16", "pfm_op_layernorm_bf16",
                "pfm_profile_read", "pfm_streams_create", "pfm_streams_reset", "pfm_stream_step",
-               "pfm_streams_destroy")
+               "pfm_streams_destroy", "pfm_fbank_raw", "pfm_lfr_gather")
 
 
 class PfmError(RuntimeError):
@@ -101,6 +101,8 @@ def load_library(path: Optional[str] = None) -> ctypes.CDLL:
     lib.pfm_stream_step.argtypes = [vp, vp, i32, ctypes.POINTER(ctypes.c_int32), f32p, i32,
                                     ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32), i32p, i32, i32p,
                                     f32p, f32p]
+    lib.pfm_fbank_raw.argtypes = [vp, vp, f32p, i32p, i32, i32, f32p, i32]
+    lib.pfm_lfr_gather.argtypes = [vp, f32p, i32p, i32, i32, f32p, f32p]
     lib.pfm_streams_destroy.argtypes = [vp]
     lib.pfm_streams_destroy.restype = None
     for name in ABI_SYMBOLS:
@@ -255,6 +257,35 @@ class PfmEngine:
         check(self.lib.pfm_fbank(self.h, _stream_ptr(torch, dev), _ptr(wav), _ptr(nsamp), B, S, _ptr(cm), _ptr(feats),
                                  T_cap, _ptr(t_out)), "pfm_fbank")
         return feats, t_out
+
+    def fbank_raw(self, wav, nsamp_host):
+        """wav [B,S] f32 cuda, nsamp_host: B host ints -> raw fbank frames [B, N_cap, 80] (pfm_fbank_raw)."""
+        torch = self.torch
+        dev = torch.device("cuda", self.device)
+        wav = wav.to(device=dev, dtype=torch.float32).contiguous()
+        B, S = wav.shape
+        ns = torch.tensor([int(x) for x in nsamp_host], dtype=torch.int32).to(dev)
+        N_cap = max(1, 1 + (S - 400) // 160 if S >= 400 else 1)
+        fb = torch.empty((B, N_cap, 80), dtype=torch.float32, device=dev)
+        check(self.lib.pfm_fbank_raw(self.h, _stream_ptr(torch, dev), _ptr(wav), _ptr(ns), B, S, _ptr(fb), N_cap),
+              "pfm_fbank_raw")
+        return fb
+
+    def lfr_gather(self, frames, idx, m, cmvn=None):
+        """frames [F,80] f32 cuda, idx [rows, m] host int array -> [rows, m*80] (pfm_lfr_gather)."""
+        torch = self.torch
+        dev = torch.device("cuda", self.device)
+        idx_h = np.ascontiguousarray(np.asarray(idx, dtype=np.int32).reshape(-1, m))
+        rows = idx_h.shape[0]
+        out = torch.empty((rows, m * 80), dtype=torch.float32, device=dev)
+        if rows:
+            if int(idx_h.min()) < 0 or int(idx_h.max()) >= frames.shape[0]:
+                raise PfmError("lfr_gather: frame index out of range")
+            frames = frames.contiguous()
+            idx = torch.from_numpy(idx_h).to(dev)
+            check(self.lib.pfm_lfr_gather(_stream_ptr(torch, dev), _ptr(frames), _ptr(idx), rows, m, _ptr(cmvn),
+                                          _ptr(out)), "pfm_lfr_gather")
+        return out
 
 
 # ---- single-op helpers (kernel-level parity tests) ------------------------------------------

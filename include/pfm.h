@@ -189,6 +189,21 @@ void pfm_streams_destroy(pfm_streams* s);
 int pfm_fbank(pfm_handle* h, void* stream, const float* wav, const int32_t* nsamp, int B,
               int S_max, const float* cmvn, float* feats, int T_cap, int32_t* T_out);
 
+/* Raw Kaldi fbank frames (no LFR / CMVN) for a batch of sample runs: the kaldi.fbank call of
+ * WavFrontendOnline.forward_fbank (funasr/frontends/wav_frontend.py:336-364), which the online
+ * frontend feeds with the samples it carries between chunks.
+ *   wav [B, S_max] f32 in [-1, 1); nsamp [B] int32 device; fb [B, N_cap, 80] f32 out (rows beyond
+ *   a run's frame count are zero); N_cap >= frames of S_max. */
+int pfm_fbank_raw(pfm_handle* h, void* stream, const float* wav, const int32_t* nsamp, int B, int S_max,
+                  float* fb, int N_cap);
+
+/* Online LFR + CMVN (WavFrontendOnline.apply_lfr / apply_cmvn, wav_frontend.py:275-328): out row r
+ * = concat_j frames[idx[r*m + j]] (j < m), then (x + shift) * scale when cmvn != NULL.
+ *   frames [F, 80] f32 device; idx [rows * m] int32 device (host-computed from the splice cache and
+ *   frame counts); cmvn [2, m*80] f32 device or NULL; out [rows, m*80] f32 device. */
+int pfm_lfr_gather(void* stream, const float* frames, const int32_t* idx, int rows, int m,
+                   const float* cmvn, float* out);
+
 /* Host-side frame count helper: LFR frames for n samples (ceil(nfbank / 6)). */
 int pfm_lfr_frames(int nsamp);
 

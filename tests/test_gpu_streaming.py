@@ -177,3 +177,108 @@ def test_stream_bad_args(tiny):
         s.step([0, 0], torch.zeros((2, 10, cfg.input_size), device="cuda"), [10, 10], [False, False])
     with pytest.raises(PfmError):
         PfmStreams(e, 1, (0, 10, 5), -1, 0, "exact")
+
+
+# ---------------------------------------------------------------- online frontend + model contract
+TOL_LOGMEL = 2e-4   # GPU fbank vs the reference's kaldi-native-fbank (tests/test_gpu_frontend.py)
+
+
+def _stream_model(tiny_cfg):
+    import json  # noqa: F401
+    from funasr_amd.auto_model import AutoModel
+    from tests.golden.inputs import token_list
+    kw = tiny_cfg.reference_kwargs()
+    return AutoModel(model="ParaformerStreaming", model_conf=dict(ctc_weight=0.0, predictor_bias=1),
+                     synthetic_seed=0, tokenizer_conf=dict(token_list=token_list(tiny_cfg.vocab_size)),
+                     device="cuda", mode="exact", frontend_conf=dict(cmvn_file=None), **kw)
+
+
+@pytest.mark.parametrize("tag", ["w1", "w2"])
+def test_online_frontend_vs_reference(tiny, tag):
+    """WavFrontendOnline.step (pfm_fbank_raw + pfm_lfr_gather) over the reference's own 600 ms chunking
+    of each call: every LFR+CMVN row the reference frontend emitted (tests/golden/stream_<tag>_feats.npy)."""
+    import json
+    from funasr_amd.frontend import WavFrontendOnline
+    from tests.golden.inputs import waveform
+    cfg, e, _ = tiny
+    gw = json.load(open(f"{GOLD}/stream_wave.json"))[tag]
+    cmvn = np.load(f"{GOLD}/lfr_cmvn.npz")["cmvn"]
+    fe = WavFrontendOnline(cmvn_file=None)
+    fe.cmvn = cmvn
+    wav = waveform(seed=gw["seed"], n=gw["n"])
+    cache, prev, pos, got = {}, np.zeros(0, np.float32), 0, []
+    for j, n in enumerate(gw["calls"]):
+        fin = j == len(gw["calls"]) - 1
+        a = np.concatenate([prev, wav[pos:pos + n]])
+        pos += n
+        nch = int(len(a) // 9600 + int(fin))
+        m = int(len(a) % 9600 * (1 - int(fin)))
+        for i in range(nch):
+            seg = a[i * 9600:(i + 1) * 9600]
+            last = fin and i == nch - 1
+            if last and len(seg) < 960:
+                continue
+            got.append(fe.step(e, [(seg, last, cache)])[0].cpu().numpy())
+        prev = a[:-m] if m else a[:0]
+    assert [f.shape[0] for f in got] == gw["feat_rows"]
+    ref = np.load(f"{GOLD}/stream_{tag}_feats.npy")
+    assert np.abs(np.concatenate(got) - ref).max() < TOL_LOGMEL * float(np.abs(cmvn[1]).max())
+
+
+def test_automodel_streaming_generate_vs_reference():
+    """AutoModel(model="ParaformerStreaming").generate(chunk, cache=cache, is_final=...) per call: the
+    text of every call equals the reference inference() goldens (stream_wave.json, look-back 4 / 1)."""
+    import json
+    from tests.golden.inputs import waveform
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    cfg = paraformer_streaming_tiny()
+    am = _stream_model(cfg)
+    am.model.load_state_dict(make_weights(cfg, seed=0))
+    am.kwargs["frontend"].cmvn = np.load(f"{GOLD}/lfr_cmvn.npz")["cmvn"]
+    gold = json.load(open(f"{GOLD}/stream_wave.json"))
+    for tag, gw in gold.items():
+        wav = waveform(seed=gw["seed"], n=gw["n"])
+        cache, pos = {}, 0
+        for j, n in enumerate(gw["calls"]):
+            fin = j == len(gw["calls"]) - 1
+            res = am.generate(input=wav[pos:pos + n], cache=cache, is_final=fin, chunk_size=[0, 10, 5],
+                              encoder_chunk_look_back=4, decoder_chunk_look_back=1)
+            pos += n
+            assert res[0]["text"] == gw["texts"][j], (tag, j)
+
+
+def test_inference_streams_batched_equals_single():
+    """inference_streams over 3 concurrent streams (different lengths / call sizes) gives each stream the
+    tokens it gets alone."""
+    from tests.golden.inputs import waveform
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    cfg = paraformer_streaming_tiny()
+    am = _stream_model(cfg)
+    mdl = am.model
+    kw = dict(chunk_size=[0, 10, 5], encoder_chunk_look_back=4, decoder_chunk_look_back=1)
+    wavs = [waveform(seed=40 + i, n=n) for i, n in enumerate([40000, 23456, 31000])]
+    calls = [[9600, 9600, 20800], [5000, 18456], [31000]]
+    fe = am.kwargs["frontend"]
+    single = []
+    for w, cs in zip(wavs, calls):
+        cache, pos, toks = {}, 0, []
+        for j, n in enumerate(cs):
+            toks += mdl.inference_streams([(w[pos:pos + n], cache, j == len(cs) - 1)], frontend=fe, **kw)[0]
+            pos += n
+        single.append(toks)
+    caches = [{} for _ in wavs]
+    pos = [0, 0, 0]
+    batched = [[], [], []]
+    for j in range(3):
+        act = [k for k in range(3) if j < len(calls[k])]
+        items = []
+        for k in act:
+            n = calls[k][j]
+            items.append((wavs[k][pos[k]:pos[k] + n], caches[k], j == len(calls[k]) - 1))
+            pos[k] += n
+        for k, t in zip(act, mdl.inference_streams(items, frontend=fe, **kw)):
+            batched[k] += t
+    assert batched == single
+    assert sum(len(t) for t in single) > 0
