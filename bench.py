@@ -61,6 +61,50 @@ def cpu_model() -> str:
     return platform.processor() or "unknown"
 
 
+def stream_leg(args, dev, torch, make_weights) -> dict:
+    from funasr_amd.config import paraformer_streaming
+    from funasr_amd.runtime import PfmEngine, PfmStreams
+    cfg = paraformer_streaming()
+    eng = PfmEngine(cfg, dev.index or 0)
+    eng.load_state_dict(make_weights(cfg, args.seed))
+    C = args.stream_chunks
+    g = torch.Generator(device=dev)
+    g.manual_seed(2000)
+    res = {"workload": f"Paraformer-large streaming, chunk [0,10,5] (600 ms), look-back 4/1, {C} chunks "
+                       f"({C * 0.6:.0f} s) per stream, synthetic LFR+CMVN rows", "dtype": "bf16" if args.mode == "fast"
+                       else "f32", "mode": args.mode}
+    for S in (1, args.stream_batch):
+        chunks = torch.randn((C, S, 10, cfg.input_size), generator=g, device=dev, dtype=torch.float32)
+        st = PfmStreams(eng, S, (0, 10, 5), 4, 1, args.mode)
+        ids = list(range(S))
+
+        def one_stream():
+            st.reset(ids)
+            toks = 0
+            lat = []
+            for c in range(C):
+                t0 = time.perf_counter()
+                r = st.step(ids, chunks[c], [10] * S, [c == C - 1] * S)
+                toks += int(r["ntok"].sum().item())    # the host needs the tokens of every chunk
+                lat.append(time.perf_counter() - t0)
+            return toks, lat
+
+        one_stream()   # warmup (workspace growth, first-call setup)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        toks, lat = one_stream()
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        key = "single" if S == 1 else f"streams_{S}"
+        res[key] = {"streams": S, "value": round(S * C * 0.6 / dt, 1), "unit": "audio-sec/sec",
+                    "chunk_ms_mean": round(float(np.mean(lat)) * 1e3, 3),
+                    "chunk_ms_p90": round(float(np.percentile(lat, 90)) * 1e3, 3),
+                    "tokens_per_chunk_mean": round(toks / (S * C), 2)}
+        del st, chunks
+    del eng
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -73,6 +117,9 @@ def main():
     ap.add_argument("--exact-steps", type=int, default=2, help="timed exact-mode steps (0 = skip)")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--sv-steps", type=int, default=3, help="timed SenseVoiceSmall (config C4) steps (0 = skip)")
+    ap.add_argument("--stream-chunks", type=int, default=50,
+                    help="600 ms chunks per stream in the streaming (config C5) leg (0 = skip)")
+    ap.add_argument("--stream-batch", type=int, default=64, help="concurrent streams of the C5 serving line")
     args = ap.parse_args()
 
     import torch
@@ -241,6 +288,12 @@ def main():
                              "path_tflops": round(sv_tf, 2), "path_frac": round(sv_tf / peak, 4),
                              "tokens_per_utt_mean": float(sv_last["ntok"].float().mean().item())}
         del seng
+
+    # ---- streaming Paraformer (BASELINE config C5): 600 ms chunks ([0, 10, 5], look-back 4 / 1) of
+    # 30 s streams through pfm_stream_step, synthetic LFR+CMVN chunk rows resident in HBM; one stream
+    # (the reference's batch 1: per-chunk latency) and S concurrent streams (serving throughput), rank 0
+    if rank == 0 and args.stream_chunks > 0:
+        out["streaming"] = stream_leg(args, dev, torch, make_weights)
 
     # ---- CPU baseline: the oracle torch-CPU restatement on a bounded sample (rank 0, N=1 only)
     if rank == 0 and world == 1 and args.cpu_utts > 0:

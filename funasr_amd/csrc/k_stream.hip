@@ -321,3 +321,40 @@ hipError_t pfm_dec_fsmn_stream(int dtype, const void* v, const float* wT, int K,
     PFM_LAUNCH_CHECK();
     return hipSuccess;
 }
+
+// ------------------------------------------------------------------------------------------
+// Plain kernels for the two layout fixes of a step (kept as kernel nodes in the step graphs):
+//   pad rows: rows 0 and Tw+1 of each stream's [Tw+2][D] encoder image are zero (CIF conv padding)
+//   row copy: dst[r][0..w) = src[r][0..w), w floats (decoder input <- the CIF embeds)
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void pad_rows_zero_kernel(float* __restrict__ encp, bf16* __restrict__ encpb, int Tw,
+                                                            int D) {
+    const long long row = (long long)blockIdx.x * (Tw + 2) + (blockIdx.y ? Tw + 1 : 0);
+    for (int c = threadIdx.x; c < D; c += 256) {
+        encp[row * D + c] = 0.f;
+        if (encpb) encpb[row * D + c] = f2bf(0.f);
+    }
+}
+
+__global__ __launch_bounds__(256) void rows_copy_kernel(float* __restrict__ dst, long long dld,
+                                                        const float* __restrict__ src, long long sld, int w4) {
+    const int r = blockIdx.y;
+    const int c = blockIdx.x * 256 + threadIdx.x;
+    if (c < w4) ((float4*)(dst + r * dld))[c] = ((const float4*)(src + r * sld))[c];
+}
+
+hipError_t pfm_pad_rows_zero(float* encp, bf16* encpb, int n, int Tw, int D, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(pad_rows_zero_kernel, dim3(n, 2), dim3(256), 0, st, encp, encpb, Tw, D);
+    PFM_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+hipError_t pfm_rows_copy(float* dst, long long dld, const float* src, long long sld, int w, int rows, hipStream_t st) {
+    if (rows <= 0 || w <= 0) return hipSuccess;
+    if (w % 4 || dld % 4 || sld % 4) return hipErrorInvalidValue;
+    const int w4 = w / 4;
+    hipLaunchKernelGGL(rows_copy_kernel, dim3((w4 + 255) / 256, rows), dim3(256), 0, st, dst, dld, src, sld, w4);
+    PFM_LAUNCH_CHECK();
+    return hipSuccess;
+}

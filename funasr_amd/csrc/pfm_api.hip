@@ -11,6 +11,10 @@
 #include <unordered_map>
 #include <vector>
 
+#include <atomic>
+#include <map>
+#include <array>
+
 #include "../../include/pfm.h"
 #include "pfm_common.h"
 #include "pfm_stream.h"
@@ -85,12 +89,17 @@ static int fail(int code, const std::string& msg) {
 
 namespace {
 
+// Bumped whenever any DevBuf is (re)allocated: captured HIP graphs hold raw buffer addresses and are
+// valid only while this is unchanged.
+std::atomic<unsigned long long> g_buf_gen{0};
+
 struct DevBuf {
     void* p = nullptr;
     size_t bytes = 0;
     ~DevBuf() { if (p) (void)hipFree(p); }
     hipError_t ensure(size_t n) {
         if (n <= bytes) return hipSuccess;
+        g_buf_gen.fetch_add(1);
         if (p) { hipError_t e = hipFree(p); if (e != hipSuccess) return e; p = nullptr; bytes = 0; }
         hipError_t e = hipMalloc(&p, n);
         if (e == hipSuccess) bytes = n;
@@ -1374,9 +1383,23 @@ struct pfm_streams {
     DevBuf xin, kvbuf, kvw, pe;   // window input, gathered keys, decoder memory K|V, PE table
     int pe_T = 0;
     std::vector<int> start, cle, cld;   // host mirrors per slot
-    std::vector<unsigned char> hprm;
+    unsigned char* hprm = nullptr;      // pinned host staging of the per-step parameters
+    size_t hprm_cap = 0;
     int32_t* hntok = nullptr;
     int hntok_cap = 0;
+    DevBuf fin, tok;                    // chunk rows [n][maxn][I] (graph-stable copy), tokens [n][L_cap]
+    // HIP graphs of the two launch sequences of a step (encoder + CIF; decoder), keyed by shape
+    struct Graph { hipGraphExec_t exec = nullptr; unsigned long long gen = 0; int seen = 0; bool bad = false; };
+    std::map<std::array<int, 4>, Graph> graphs;
+    hipStream_t cap = nullptr;          // work stream of every step: eager launches, graph capture and replay
+    hipEvent_t ev_in = nullptr;
+    ~pfm_streams() {
+        if (ev_in) (void)hipEventDestroy(ev_in);
+        for (auto& kv : graphs)
+            if (kv.second.exec) (void)hipGraphExecDestroy(kv.second.exec);
+        if (cap) (void)hipStreamDestroy(cap);
+        if (hprm) (void)hipHostFree(hprm);
+    }
 };
 
 namespace {
@@ -1407,8 +1430,7 @@ int stream_decoder(pfm_streams* s, const Run& r, int n, int Tw, int L, const SPr
     const bf16* encpb = h->encpb.as<bf16>();
     const RowMap encmap = rowmap_seg(Tw, (long long)(Tw + 2) * D, D);
     const int Lc = Tw + 2;
-    HIP_TRY(hipMemcpy2DAsync(Xd, (size_t)L * D * 4, h->emb.p, (size_t)Lc * D * 4, (size_t)L * D * 4, n,
-                             hipMemcpyDeviceToDevice, st));
+    HIP_TRY(pfm_rows_copy(Xd, (long long)L * D, h->emb.as<float>(), (long long)Lc * D, L * D, n, st));
     HIP_TRY(s->kvw.ensure((size_t)Mw * nkv * es));
     {   // memory K|V of every decoder layer from the window (rows i*Tw + t)
         GemmEpi e = epi_default();
@@ -1489,6 +1511,55 @@ int stream_decoder(pfm_streams* s, const Run& r, int n, int Tw, int L, const SPr
     return PFM_OK;
 }
 
+bool stream_graphs_enabled() {
+    const char* e = getenv("PFM_STREAM_GRAPH");   // 0 = eager launches (A/B, debugging)
+    return !(e && e[0] == '0');
+}
+
+// Run `body` on `st`, through a HIP graph of its launches when `use`: the first step of a shape runs eagerly
+// (one-time launcher setup happens there), the second captures on the object's capture stream and every
+// later one replays. A graph is rebuilt when any workspace buffer was reallocated since its capture.
+template <class F>
+int stream_graphed(pfm_streams* s, std::array<int, 4> key, bool use, hipStream_t st, F&& body) {
+    if (!use) return body(st);
+    auto& g = s->graphs[key];
+    const unsigned long long gen = g_buf_gen.load();
+    static const bool log = getenv("PFM_STREAM_GRAPH_LOG") != nullptr;
+    if (log)
+        fprintf(stderr, "[stream graph] key %d/%d/%d/%d %s gen %llu/%llu seen %d\n", key[0], key[1], key[2], key[3],
+                g.exec && g.gen == gen ? "replay" : (g.bad || g.seen == 0 ? "eager" : "capture"), g.gen, gen, g.seen);
+    if (g.exec && g.gen == gen) {
+        HIP_TRY(hipGraphLaunch(g.exec, st));
+        return PFM_OK;
+    }
+    if (g.exec) { (void)hipGraphExecDestroy(g.exec); g.exec = nullptr; }
+    if (g.bad || g.seen++ == 0) return body(st);
+    HIP_TRY(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
+    const int rc = body(st);
+    hipGraph_t graph = nullptr;
+    const hipError_t e = hipStreamEndCapture(st, &graph);
+    if (rc != PFM_OK || e != hipSuccess || g_buf_gen.load() != gen) {   // run this step eagerly instead
+        if (graph) (void)hipGraphDestroy(graph);
+        (void)hipGetLastError();
+        if (rc != PFM_OK) return rc;
+        g.bad = e != hipSuccess;   // not capturable: this shape stays eager
+        return body(st);
+    }
+    const hipError_t ei = hipGraphInstantiate(&g.exec, graph, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(graph);
+    if (ei != hipSuccess) {
+        g.exec = nullptr;
+        g.bad = true;
+        (void)hipGetLastError();
+        return body(st);
+    }
+    g.gen = gen;
+    {
+        HIP_TRY(hipGraphLaunch(g.exec, st));
+        return PFM_OK;
+    }
+}
+
 int streams_zero(pfm_streams* s, hipStream_t st, int slot) {
     const pfm_config& c = s->h->cfg;
     const size_t D = c.d_model, I = c.input_size, K1 = c.kernel_size - 1;
@@ -1543,6 +1614,8 @@ int pfm_streams_create(pfm_handle* h, int slots, const int32_t* chunk_size, int 
     HIP_TRY(s->dfs.ensure((size_t)std::max(c.dec_blocks, 1) * slots * K1 * D * 4));
     if (s->Ce) HIP_TRY(s->ekv.ensure((size_t)c.enc_blocks * slots * s->Ce * 2 * D * es));
     if (s->Cd) HIP_TRY(s->dkv.ensure((size_t)std::max(c.dec_blocks, 1) * slots * s->Cd * 2 * D * es));
+    HIP_TRY(hipStreamCreateWithFlags(&s->cap, hipStreamNonBlocking));
+    HIP_TRY(hipEventCreateWithFlags(&s->ev_in, hipEventDisableTiming));
     s->start.assign(slots, 0);
     s->cle.assign(slots, 0);
     s->cld.assign(slots, 0);
@@ -1587,7 +1660,13 @@ int pfm_stream_step(pfm_streams* s, void* stream, int n, const int32_t* slot_ids
     }
     if (maxn > 0 && !feats) return fail(PFM_E_ARG, "pfm_stream_step: feats is null");
     HIP_TRY(hipSetDevice(h->device));
-    hipStream_t st = (hipStream_t)stream;
+    // every launch of a step goes to the object's own stream, ordered after the caller's queued work (the
+    // chunk rows, a reset) by one event; the step synchronises that stream before returning, so its outputs
+    // are ready for any stream. (The caller's stream may be the legacy null stream, whose ordering with
+    // graph launches on other streams was observed to be unreliable.)
+    HIP_TRY(hipEventRecord(s->ev_in, (hipStream_t)stream));
+    HIP_TRY(hipStreamWaitEvent(s->cap, s->ev_in, 0));
+    hipStream_t st = s->cap;
     const bool fast = s->mode == PFM_MODE_FAST;
     const int D = c.d_model, I = c.input_size, C0 = s->C0;
     const int Tw = C0 + maxn;
@@ -1606,11 +1685,32 @@ int pfm_stream_step(pfm_streams* s, void* stream, int n, const int32_t* slot_ids
         HIP_TRY(hipMemcpy(s->pe.p, pe.data(), pe.size() * 4, hipMemcpyHostToDevice));
         s->pe_T = T2;
     }
-    // per-stream parameters: SPrm[n] | tw[n] | kle[n] | kld[n]
+    // every buffer this step touches is sized here, before any launch sequence that may be captured
+    const size_t es = fast ? 2 : 4;
+    const int nkv = c.dec_blocks * 2 * D;
     const size_t pb = (size_t)n * sizeof(SPrm), ib = (size_t)n * 4;
-    s->hprm.resize(pb + 3 * ib);
-    SPrm* hp = (SPrm*)s->hprm.data();
-    int* htw = (int*)(s->hprm.data() + pb);
+    HIP_TRY(s->prm.ensure(pb + 3 * ib));
+    HIP_TRY(s->xin.ensure((size_t)n * Tw * I * 4));
+    HIP_TRY(s->fin.ensure((size_t)n * std::max(maxn, 1) * I * 4));
+    if (s->Ce || s->Cd) HIP_TRY(s->kvbuf.ensure((size_t)n * (std::max(s->Ce, s->Cd) + Tw) * 2 * D * es));
+    if (c.dec_blocks > 0) HIP_TRY(s->kvw.ensure((size_t)n * Tw * nkv * es));
+    HIP_TRY(s->tok.ensure((size_t)n * std::max(L_cap, 1) * 4));
+    if (s->hntok_cap < n) {
+        if (s->hntok) (void)hipHostFree(s->hntok);
+        s->hntok = nullptr;
+        HIP_TRY(hipHostMalloc((void**)&s->hntok, (size_t)n * 4, 0));
+        s->hntok_cap = n;
+    }
+    if (s->hprm_cap < pb + 3 * ib) {
+        if (s->hprm) (void)hipHostFree(s->hprm);
+        s->hprm = nullptr;
+        HIP_TRY(hipHostMalloc((void**)&s->hprm, pb + 3 * ib, 0));
+        s->hprm_cap = pb + 3 * ib;
+    }
+    // per-stream parameters: SPrm[n] | tw[n] | kle[n] | kld[n] (pinned staging; the previous step's upload
+    // has completed: every step synchronises the stream before returning)
+    SPrm* hp = (SPrm*)s->hprm;
+    int* htw = (int*)(s->hprm + pb);
     int* hkle = htw + n;
     int* hkld = hkle + n;
     for (int i = 0; i < n; ++i) {
@@ -1623,73 +1723,67 @@ int pfm_stream_step(pfm_streams* s, void* stream, int n, const int32_t* slot_ids
         hkle[i] = p.cle + p.tw;
         hkld[i] = p.cld + p.tw;
     }
-    HIP_TRY(s->prm.ensure(s->hprm.size()));
-    HIP_TRY(hipMemcpyAsync(s->prm.p, s->hprm.data(), s->hprm.size(), hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(s->prm.p, s->hprm, pb + 3 * ib, hipMemcpyHostToDevice, st));
     const SPrm* prm = s->prm.as<SPrm>();
     const int* tw_d = (const int*)((const char*)s->prm.p + pb);
     const int* kle_d = tw_d + n;
     const int* kld_d = kle_d + n;
-
-    // ---- encoder window + SANMEncoderChunkOpt.forward_chunk (scama/encoder.py:456-499)
-    HIP_TRY(s->xin.ensure((size_t)n * Tw * I * 4));
-    float* xin = s->xin.as<float>();
-    HIP_TRY(pfm_stream_window(feats, Tn, prm, n, s->fcache.as<float>(), s->pe.as<float>(), I, C0, Tw,
-                              sqrtf((float)D), xin, st));
-    HIP_TRY(pfm_stream_fcache(xin, prm, n, I, C0, Tw, s->fcache.as<float>(), st));
-    Run run(h, st, fast);
-    run.fuse_fsmn = false;
-    run.raw_input = true;
-    ChunkKV ck;
-    const size_t es = fast ? 2 : 4;
-    if (s->Ce) {
-        const int Tk = s->Ce + Tw;
-        HIP_TRY(s->kvbuf.ensure((size_t)n * std::max(Tk, s->Cd + Tw) * 2 * D * es));
-        ck.cache = s->ekv.p;
-        ck.layer_stride = (long long)s->slots * s->Ce * 2 * D;
-        ck.C = s->Ce; ck.drop = s->cs[2]; ck.Tk = Tk;
-        ck.buf = s->kvbuf.p; ck.prm = prm; ck.klen = kle_d;
-        run.ck = &ck;
-    }
+    // the chunk rows, re-pitched to maxn rows per stream in a buffer whose address a graph can keep
+    float* fin = s->fin.as<float>();
+    if (maxn > 0)
+        HIP_TRY(hipMemcpy2DAsync(fin, (size_t)maxn * I * 4, feats, (size_t)Tn * I * 4, (size_t)maxn * I * 4, n,
+                                 hipMemcpyDeviceToDevice, st));
     float* encp = h->encp.as<float>();
     bf16* encpb = h->encpb.as<bf16>();
+    int* ntok = h->ntok.as<int>();
+    const int Lc = Tw + 2;
     const RowMap encmap = rowmap_seg(Tw, (long long)(Tw + 2) * D, D);
-    HIP_TRY(hipMemset2DAsync(encp, (size_t)(Tw + 2) * D * 4, 0, (size_t)D * 4, n, st));
-    HIP_TRY(hipMemset2DAsync(encp + (size_t)(Tw + 1) * D, (size_t)(Tw + 2) * D * 4, 0, (size_t)D * 4, n, st));
-    if (fast) {
-        HIP_TRY(hipMemset2DAsync(encpb, (size_t)(Tw + 2) * D * 2, 0, (size_t)D * 2, n, st));
-        HIP_TRY(hipMemset2DAsync(encpb + (size_t)(Tw + 1) * D, (size_t)(Tw + 2) * D * 2, 0, (size_t)D * 2, n, st));
-    }
-    {
-        const FinalLN fin = {h->an_g, h->an_b, encp + D, encmap, DT_F32, fast ? (void*)(encpb + D) : nullptr, encmap,
-                             DT_BF16};
-        rc = encoder_stack(run, xin, tw_d, n, Tw, 0, c.enc_blocks, h->X.as<float>(), fin, enc_ws(h, 0));
-        if (rc) return rc;
-    }
-    HIP_TRY(pfm_stream_mask_rows(encp, fast ? encpb : nullptr, prm, n, Tw, D, st));
-    if (enc_out)
-        HIP_TRY(hipMemcpy2DAsync(enc_out, (size_t)Tw * D * 4, encp + D, (size_t)(Tw + 2) * D * 4, (size_t)Tw * D * 4, n,
-                                 hipMemcpyDeviceToDevice, st));
-    // ---- CifPredictorV2.forward_chunk (cif_predictor.py:255-344)
-    {
+    // HIP graphs replace the ~10 launches per encoder layer when no optional output is requested: kernels
+    // read every per-step value from `prm`, so one graph per (n, maxn) replays any step of that shape
+    const bool graphs = !enc_out && !alphas_out && !h->prof_on && stream_graphs_enabled();
+
+    // ---- phase A: encoder window + SANMEncoderChunkOpt.forward_chunk (scama/encoder.py:456-499) +
+    // CifPredictorV2.forward_chunk (cif_predictor.py:255-344) -> acoustic embeds, ntok on the device
+    auto phaseA = [&](hipStream_t q) -> int {
+        float* xin = s->xin.as<float>();
+        HIP_TRY(pfm_stream_window(fin, maxn, prm, n, s->fcache.as<float>(), s->pe.as<float>(), I, C0, Tw,
+                                  sqrtf((float)D), xin, q));
+        HIP_TRY(pfm_stream_fcache(xin, prm, n, I, C0, Tw, s->fcache.as<float>(), q));
+        Run run(h, q, fast);
+        run.fuse_fsmn = false;
+        run.raw_input = true;
+        ChunkKV ck;
+        if (s->Ce) {
+            ck.cache = s->ekv.p;
+            ck.layer_stride = (long long)s->slots * s->Ce * 2 * D;
+            ck.C = s->Ce; ck.drop = s->cs[2]; ck.Tk = s->Ce + Tw;
+            ck.buf = s->kvbuf.p; ck.prm = prm; ck.klen = kle_d;
+            run.ck = &ck;
+        }
+        HIP_TRY(pfm_pad_rows_zero(encp, fast ? encpb : nullptr, n, Tw, D, q));
+        const FinalLN finln = {h->an_g, h->an_b, encp + D, encmap, DT_F32, fast ? (void*)(encpb + D) : nullptr,
+                               encmap, DT_BF16};
+        int rc2 = encoder_stack(run, xin, tw_d, n, Tw, 0, c.enc_blocks, h->X.as<float>(), finln, enc_ws(h, 0));
+        if (rc2) return rc2;
+        HIP_TRY(pfm_stream_mask_rows(encp, fast ? encpb : nullptr, prm, n, Tw, D, q));
         GemmEpi e = epi_default();
         e.bias = run.P(h->cif_b); e.relu = 1;
         e.out = h->Hc.p; e.out_map = rowmap_plain(D); e.out_dtype = DT_F32;
         const void* A = fast ? (const void*)encpb : (const void*)encp;
         HIP_TRY(run.gemm(run.dt, A, rowmap_seg(Tw, (long long)(Tw + 2) * D, D), run.W(h->cif_w), 3 * D, n * Tw, D,
                          3 * D, e));
-    }
-    const int Lc = Tw + 2;
-    int* ntok = h->ntok.as<int>();
-    HIP_TRY(pfm_cif_chunk(h->Hc.as<float>(), run.P(h->cif_ow), run.P(h->cif_ob), encp, prm, n, Tw, D, s->cs[0],
-                          s->cs[0] + s->cs[1], c.smooth_factor, c.noise_threshold, c.tail_threshold, c.cif_threshold,
-                          s->chid.as<float>(), s->calpha.as<float>(), h->emb.as<float>(), Lc, ntok, alphas_out, st));
+        HIP_TRY(pfm_cif_chunk(h->Hc.as<float>(), run.P(h->cif_ow), run.P(h->cif_ob), encp, prm, n, Tw, D, s->cs[0],
+                              s->cs[0] + s->cs[1], c.smooth_factor, c.noise_threshold, c.tail_threshold,
+                              c.cif_threshold, s->chid.as<float>(), s->calpha.as<float>(), h->emb.as<float>(), Lc,
+                              ntok, alphas_out, q));
+        return PFM_OK;
+    };
+    rc = stream_graphed(s, {0, n, maxn, 0}, graphs, st, phaseA);
+    if (rc) return rc;
+    if (enc_out)
+        HIP_TRY(hipMemcpy2DAsync(enc_out, (size_t)Tw * D * 4, encp + D, (size_t)(Tw + 2) * D * 4, (size_t)Tw * D * 4, n,
+                                 hipMemcpyDeviceToDevice, st));
     HIP_TRY(hipMemcpyAsync(ntok_out, ntok, (size_t)n * 4, hipMemcpyDeviceToDevice, st));
-    if (s->hntok_cap < n) {
-        if (s->hntok) (void)hipHostFree(s->hntok);
-        s->hntok = nullptr;
-        HIP_TRY(hipHostMalloc((void**)&s->hntok, (size_t)n * 4, 0));
-        s->hntok_cap = n;
-    }
     HIP_TRY(hipMemcpyAsync(s->hntok, ntok, (size_t)n * 4, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
     int L = 0;
@@ -1702,9 +1796,24 @@ int pfm_stream_step(pfm_streams* s, void* stream, int n, const int32_t* slot_ids
         if (s->Ce) s->cle[sl] = std::min(s->Ce, s->cle[sl] + tw - s->cs[2]);
         if (s->Cd && s->hntok[i] > 0) s->cld[sl] = std::min(s->Cd, s->cld[sl] + tw);
     }
-    if (L_cap > 0) HIP_TRY(pfm_fill_i32(tokens, (long long)n * L_cap, -1, st));
-    if (L < 1 || c.dec_blocks < 1) return PFM_OK;   // model.py:490-491: nothing to decode
-    return stream_decoder(s, run, n, Tw, L, prm, tw_d, kld_d, ntok, tokens, L_cap);
+    if (L < 1 || c.dec_blocks < 1) {   // model.py:490-491: nothing to decode
+        if (L_cap > 0) HIP_TRY(pfm_fill_i32(tokens, (long long)n * L_cap, -1, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        return PFM_OK;
+    }
+    // ---- phase B: ParaformerSANMDecoder.forward_chunk (decoder.py:461-528) + greedy argmax, tokens into
+    // the step's token buffer
+    int32_t* tk = s->tok.as<int32_t>();
+    auto phaseB = [&](hipStream_t q) -> int {
+        if (L_cap > 0) HIP_TRY(pfm_fill_i32(tk, (long long)n * L_cap, -1, q));
+        Run run(h, q, fast);
+        return stream_decoder(s, run, n, Tw, L, prm, tw_d, kld_d, ntok, tk, L_cap);
+    };
+    rc = stream_graphed(s, {1, n, maxn, L * 4096 + L_cap}, graphs, st, phaseB);
+    if (rc) return rc;
+    if (L_cap > 0) HIP_TRY(hipMemcpyAsync(tokens, tk, (size_t)n * L_cap * 4, hipMemcpyDeviceToDevice, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    return PFM_OK;
 }
 
 void pfm_streams_destroy(pfm_streams* s) {
