@@ -1,0 +1,126 @@
+// Skinny-M bf16 GEMM: C[M, N] = epi(alpha * A[M, K] . W[N, K]^T) for M <= 64 (and the few-tile shapes
+// above it: 64-row blocks on grid.y).
+//
+// The streaming chunk path (paraformer_streaming, pfm_stream_step) projects 5 + 10 window rows per
+// stream through every encoder layer and 1..~10 token rows through every decoder layer. The tiled
+// 128x256 / 256x256 kernels (k_gemm_bf16.hip) give such a GEMM 2-8 workgroups, so 2-8 CUs stream the
+// whole weight matrix over K (measured 12-24 us per projection). Here the weight matrix is the only
+// real traffic (N x K bf16, each byte read once), so the grid is laid out over it:
+//   * one workgroup per 16 output columns (N = 512 -> 32 workgroups, 2048 -> 128), 8 waves;
+//   * the K axis is cut into 32-wide steps dealt round-robin to the 8 waves, so one round of the
+//     workgroup reads 512 contiguous bytes of each of its 16 weight rows (16-B fragments per lane,
+//     straight from HBM into v_mfma_f32_16x16x32_bf16 B operands; no LDS staging);
+//   * A fragments (rows m of 16-row blocks, <= 4 blocks) come from L2 (A is 15..64 rows);
+//   * the 8 waves' 16x16 partials are summed through LDS in wave order (deterministic), then the
+//     GemmEpi epilogue of the tiled kernels is applied per element (bias, alpha, relu, residuals,
+//     f32 / bf16 output, optional bf16 second output).
+// Fragment layout (as k_gemm_bf16.hip, MF == 1): lane (r = lane & 15, g = lane >> 4) holds row r,
+// K chunk g (8 contiguous bf16) of a 16 x 32 operand; the accumulator element e of lane l is
+// row 4 (l >> 4) + e, column l & 15.
+#include "pfm_common.h"
+
+namespace {
+
+constexpr int SK_WAVES = 8;
+constexpr int SK_UNROLL = 4;   // 32-wide K steps whose fragments are in flight per wave
+
+template <int MT>
+__global__ __launch_bounds__(512) void gemm_skinny_kernel(const bf16* __restrict__ A, RowMap amap,
+                                                          const bf16* __restrict__ W, long long ldw, int M, int N,
+                                                          int K, GemmEpi e) {
+    __shared__ float red[SK_WAVES][MT][256];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int r16 = lane & 15, g = lane >> 4;
+    const int n0 = blockIdx.x * 16;
+    const int n = n0 + r16;
+    const int mb = blockIdx.y * 64;   // row block of this workgroup (M > 64: grid.y = ceil(M / 64))
+    const bool nok = n < N;
+    const bf16* wrow = W + (long long)(nok ? n : 0) * ldw + g * 8;
+    const bf16* arow[MT];
+    bool mok[MT];
+#pragma unroll
+    for (int t = 0; t < MT; ++t) {
+        const int m = mb + t * 16 + r16;
+        mok[t] = m < M;
+        arow[t] = A + amap.off(mok[t] ? m : 0) + g * 8;
+    }
+    f32x4 acc[MT];
+#pragma unroll
+    for (int t = 0; t < MT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const bf16x8 zero8 = {};
+    const int nsteps = K / 32;
+    for (int s0 = w; s0 < nsteps; s0 += SK_WAVES * SK_UNROLL) {
+        bf16x8 bw[SK_UNROLL], ba[SK_UNROLL][MT];
+#pragma unroll
+        for (int u = 0; u < SK_UNROLL; ++u) {
+            const int s = s0 + u * SK_WAVES;
+            const bool sok = s < nsteps;
+            bw[u] = (sok && nok) ? *(const bf16x8*)(wrow + s * 32) : zero8;
+#pragma unroll
+            for (int t = 0; t < MT; ++t) ba[u][t] = (sok && mok[t]) ? *(const bf16x8*)(arow[t] + s * 32) : zero8;
+        }
+#pragma unroll
+        for (int u = 0; u < SK_UNROLL; ++u)
+#pragma unroll
+            for (int t = 0; t < MT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ba[u][t], bw[u], acc[t], 0, 0, 0);
+    }
+#pragma unroll
+    for (int t = 0; t < MT; ++t)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) red[w][t][(4 * g + q) * 16 + r16] = acc[t][q];
+    __syncthreads();
+    for (int idx = threadIdx.x; idx < MT * 256; idx += 512) {
+        const int t = idx >> 8, rc = idx & 255;
+        const int row = mb + t * 16 + (rc >> 4), col = n0 + (rc & 15);
+        if (row >= M || col >= N) continue;
+        float v = 0.f;
+#pragma unroll
+        for (int ww = 0; ww < SK_WAVES; ++ww) v += red[ww][t][rc];
+        v *= e.alpha;
+        if (e.bias) v += e.bias[col];
+        if (e.relu) v = fmaxf(v, 0.f);
+        if (e.res0) v += e.res0_bf16 ? bf2f(((const bf16*)e.res0)[(long long)row * e.ld_res0 + col])
+                                     : e.res0[(long long)row * e.ld_res0 + col];
+        if (e.res1) v += e.res1[(long long)row * e.ld_res1 + col];
+        const long long ob = e.out_map.off(row);
+        if (e.out_dtype == DT_F32) ((float*)e.out)[ob + col] = v;
+        else ((bf16*)e.out)[ob + col] = f2bf(v);
+        if (e.out2) ((bf16*)e.out2)[e.out2_map.off(row) + col] = f2bf(v);
+    }
+}
+
+}  // namespace
+
+// Shapes this kernel takes: bf16 operands, M <= 64 or few 128x256 tiles, K % 32 == 0, 16-B aligned rows, and an epilogue
+// without the fused argmax / LayerNorm-statistics features of the tiled kernels.
+bool pfm_gemm_skinny_ok(const void* A, RowMap amap, const void* W, long long ldw, int M, int N, int K,
+                        const GemmEpi& e) {
+    if (M < 1 || K % 32 != 0 || ldw % 8 != 0 || amap.ld % 8 != 0) return false;
+    if (amap.rows_per_seg > 0 && amap.seg_stride % 8 != 0) return false;
+    if (((uintptr_t)A | (uintptr_t)W) % 16 != 0) return false;
+    if (!e.out || e.amax_val || e.ln_st_in || e.ln_st_out) return false;
+    const char* d = getenv("PFM_GEMM_SKINNY");   // 0 = tiled kernels for every M (A/B)
+    if (d && d[0] == '0') return false;
+    const char* c = getenv("PFM_GEMM_CFG");      // a forced tile configuration wins (tile-config tests / A/B)
+    if (c && atoi(c) != 0) return false;
+    // beyond 64 rows: only while the tiled kernels would launch fewer than ~64 128x256 tiles (the
+    // multi-stream chunk batches, M = 15 x streams), i.e. where they leave most CUs idle
+    return M <= 64 || (long long)((M + 127) / 128) * ((N + 255) / 256) < 64;
+}
+
+hipError_t pfm_gemm_skinny(const void* A, RowMap amap, const void* W, long long ldw, int M, int N, int K,
+                           const GemmEpi& e, hipStream_t st) {
+    if (M <= 0 || N <= 0) return hipSuccess;
+    const dim3 grid((N + 15) / 16, (M + 63) / 64), block(512);
+    const bf16* a = (const bf16*)A;
+    const bf16* wt = (const bf16*)W;
+    switch (M > 64 ? 4 : (M + 15) / 16) {
+        case 1: hipLaunchKernelGGL(gemm_skinny_kernel<1>, grid, block, 0, st, a, amap, wt, ldw, M, N, K, e); break;
+        case 2: hipLaunchKernelGGL(gemm_skinny_kernel<2>, grid, block, 0, st, a, amap, wt, ldw, M, N, K, e); break;
+        case 3: hipLaunchKernelGGL(gemm_skinny_kernel<3>, grid, block, 0, st, a, amap, wt, ldw, M, N, K, e); break;
+        case 4: hipLaunchKernelGGL(gemm_skinny_kernel<4>, grid, block, 0, st, a, amap, wt, ldw, M, N, K, e); break;
+        default: return hipErrorInvalidValue;
+    }
+    PFM_LAUNCH_CHECK();
+    return hipSuccess;
+}

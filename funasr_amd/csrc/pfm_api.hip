@@ -64,6 +64,10 @@ hipError_t pfm_f32_to_bf16(const float* x, bf16* y, long long n, hipStream_t st)
 hipError_t pfm_fbank_launch(const float* wav, const int* nsamp, int B, int S_max, const float* cmvn,
                             const unsigned char* tables, float* fb_ws, int N_cap, float* feats, int T_cap, int* T_out,
                             hipStream_t st);
+bool pfm_gemm_skinny_ok(const void* A, RowMap amap, const void* W, long long ldw, int M, int N, int K,
+                        const GemmEpi& e);
+hipError_t pfm_gemm_skinny(const void* A, RowMap amap, const void* W, long long ldw, int M, int N, int K,
+                           const GemmEpi& e, hipStream_t st);
 hipError_t pfm_fbank_raw_launch(const float* wav, const int* nsamp, int B, int S_max, const unsigned char* tables,
                                 float* fb, int N_cap, hipStream_t st);
 hipError_t pfm_lfr_gather_launch(const float* frames, const int* idx, int rows, int m, const float* cmvn, float* out,
@@ -478,6 +482,9 @@ bool use_big_bf16(int dtype, RowMap amap, long long ldw, int K) {
 
 hipError_t gemm_dispatch(int dtype, const void* A, RowMap amap, const void* W, long long ldw, int M, int N, int K,
                          const GemmEpi& e, hipStream_t st) {
+    // <= 64 rows (streaming chunks): weight-streaming kernel over N instead of 2-8 big tiles
+    if (dtype == DT_BF16 && pfm_gemm_skinny_ok(A, amap, W, ldw, M, N, K, e))
+        return pfm_gemm_skinny(A, amap, W, ldw, M, N, K, e, st);
     if (use_big_bf16(dtype, amap, ldw, K)) return pfm_gemm_bf16_256(A, amap, W, ldw, M, N, K, e, st);
     return pfm_gemm(dtype, A, amap, W, ldw, M, N, K, e, st);
 }

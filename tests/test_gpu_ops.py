@@ -77,6 +77,40 @@ def test_gemm_bf16(dev, M, N, K, cfg, epi, monkeypatch):
         assert rel(got, want) < 1e-5
 
 
+@pytest.mark.parametrize("M,N,K", [(1, 512, 512), (15, 1536, 512), (15, 512, 2048), (16, 2048, 512),
+                                   (17, 1024, 1536), (33, 512, 512), (64, 520, 96), (7, 8, 32),
+                                   (960, 512, 2048), (961, 1536, 512), (200, 48, 64)])
+@pytest.mark.parametrize("epi", ["none", "bias_res", "bias_relu_bf16"])
+def test_gemm_bf16_skinny(dev, M, N, K, epi, monkeypatch):
+    """M <= 64 rows (and few-tile shapes above: M 200 / 960 / 961) take the weight-streaming kernel
+    (k_gemm_skinny.hip); same epilogues and tolerance as the tiled kernels, and the tiled kernel's result
+    up to f32 summation order."""
+    g = torch.Generator().manual_seed(M * 31 + N)
+    A = torch.randn(M, K, generator=g).bfloat16()
+    W = (torch.randn(N, K, generator=g) / K ** 0.5).bfloat16()
+    b = torch.randn(N, generator=g) if epi != "none" else None
+    R = torch.randn(M, N, generator=g) if epi == "bias_res" else None
+    want = A.double() @ W.double().T
+    if b is not None:
+        want = want + b.double()
+    if epi == "bias_relu_bf16":
+        want = torch.relu(want)
+    if R is not None:
+        want = want + R.double()
+    args = (A.to(dev), W.to(dev), None if b is None else b.to(dev), None if R is None else R.to(dev))
+    kw = dict(relu=epi == "bias_relu_bf16", out_bf16=epi == "bias_relu_bf16")
+    got = rt.op_gemm(*args, **kw)
+    monkeypatch.setenv("PFM_GEMM_SKINNY", "0")
+    tiled = rt.op_gemm(*args, **kw)
+    torch.cuda.synchronize()
+    if epi == "bias_relu_bf16":
+        assert rel(got, want) < 4e-3
+        assert rel(got, tiled) < 1e-2
+    else:
+        assert rel(got, want) < 1e-5
+        assert rel(got, tiled) < 1e-5
+
+
 def test_gemm_identity_asymmetric(dev):
     """A = I with an asymmetric W catches a transposed C write."""
     K = 256
