@@ -16,7 +16,9 @@ they are kept out of the headline number; its step time is reported as instrumen
 Extra JSON fields: `roofline` of the dominant kernel (the MFMA GEMM, live HIP-event timing),
 `path_roofline` (whole-path algorithmic FLOPs / step time), `cpu_baseline` (the oracle
 torch-CPU restatement timed on a bounded sample on this host), `exact_mode` (the f32-MFMA
-token-parity mode on the same batch) and fast-vs-exact token agreement.
+token-parity mode on the same batch) and fast-vs-exact token agreement, `sensevoice` (config C4) and
+`streaming` (config C5: 600 ms chunks of Paraformer-large streaming through pfm_stream_step, one stream's
+per-chunk latency and 64 concurrent streams' throughput, plus its own torch-CPU oracle baseline).
 """
 from __future__ import annotations
 
@@ -102,6 +104,21 @@ def stream_leg(args, dev, torch, make_weights) -> dict:
                     "tokens_per_chunk_mean": round(toks / (S * C), 2)}
         del st, chunks
     del eng
+    if args.cpu_utts > 0:
+        # the oracle's streaming restatement (torch-CPU fp32, one stream) on the first 10 chunks
+        from oracle.streaming_ref import StreamState, chunk_step
+        w = make_weights(cfg, args.seed)
+        torch.set_num_threads(int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)))
+        ss = StreamState(cfg, (0, 10, 5), 4, 1)
+        xs = torch.randn((10, 10, cfg.input_size), generator=torch.Generator().manual_seed(5))
+        tc = time.perf_counter()
+        for c in range(10):
+            chunk_step(xs[c], ss, w, cfg, c == 9)
+        dtc = time.perf_counter() - tc
+        res["cpu_baseline"] = {"value": round(10 * 0.6 / dtc, 2), "unit": "audio-sec/sec",
+                               "cores": torch.get_num_threads(), "kind": "port",
+                               "sample": f"1 stream x 10 chunks (6 s) through oracle/streaming_ref.chunk_step "
+                                         f"(torch-CPU fp32), {dtc:.2f} s on {cpu_model()}"}
     return res
 
 
@@ -292,7 +309,7 @@ def main():
     # ---- streaming Paraformer (BASELINE config C5): 600 ms chunks ([0, 10, 5], look-back 4 / 1) of
     # 30 s streams through pfm_stream_step, synthetic LFR+CMVN chunk rows resident in HBM; one stream
     # (the reference's batch 1: per-chunk latency) and S concurrent streams (serving throughput), rank 0
-    if rank == 0 and args.stream_chunks > 0:
+    if rank == 0 and world == 1 and args.stream_chunks > 0:
         out["streaming"] = stream_leg(args, dev, torch, make_weights)
 
     # ---- CPU baseline: the oracle torch-CPU restatement on a bounded sample (rank 0, N=1 only)

@@ -172,7 +172,10 @@ int pfm_streams_reset(pfm_streams* s, void* stream, const int32_t* slot_ids, int
  *   ntok      [n] int32 out: CIF fires this chunk (0: the decoder did not run for that stream)
  * Optional (NULL to skip): enc_out [n, 5 + max(nfeat), d_model] f32 encoder window after
  * after_norm (rows >= window length zero); alphas [n, 5 + max(nfeat)] f32 chunk-masked CIF weights.
- * Synchronises `stream` once (max ntok sizes the decoder). */
+ * The step runs on the object's own HIP stream, ordered after the work already queued on `stream` (the
+ * chunk rows), and returns with its outputs complete (the host needs max(ntok) to size the decoder).
+ * Repeated shapes replay HIP graphs of the step's launch sequences when enc_out and alphas are NULL
+ * (PFM_STREAM_GRAPH=0 disables). */
 int pfm_stream_step(pfm_streams* s, void* stream, int n, const int32_t* slot_ids, const float* feats,
                     int Tn, const int32_t* nfeat, const int32_t* is_final, int32_t* tokens, int L_cap,
                     int32_t* ntok, float* enc_out, float* alphas);
