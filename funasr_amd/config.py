@@ -9,7 +9,7 @@ from __future__ import annotations
 
 import dataclasses
 from dataclasses import dataclass, field
-from typing import Any, Dict
+from typing import Any, Dict, List
 
 
 @dataclass
@@ -246,3 +246,80 @@ def sense_voice_small() -> SenseVoiceConfig:
 def sense_voice_tiny(enc_blocks: int = 3, tp_blocks: int = 2, vocab_size: int = 25055) -> SenseVoiceConfig:
     """Reduced-depth SenseVoice config for full-tensor golden vectors (same widths as Small)."""
     return SenseVoiceConfig(enc_blocks=enc_blocks, tp_blocks=tp_blocks, vocab_size=vocab_size)
+
+
+@dataclass
+class CTTransformerConfig:
+    """CT-Transformer punctuation model (funasr/models/ct_transformer/model.py:35-79, template.yaml):
+    embed Embedding(vocab, embed_unit) -> SANMEncoder (input_layer "pe", d 256, 8 heads, FFN 1024,
+    4 blocks, FSMN kernel 11) -> decoder Linear(att_unit, len(punc_list)). The released model
+    (punc_ct-transformer_zh-cn-common-vocab272727) has a 272,727-entry vocabulary and the full-width
+    punc_list below. LayerNorm is funasr's LayerNorm (eps 1e-12)."""
+    input_size: int = 256           # embed_unit (the encoder's input_size)
+    d_model: int = 256              # att_unit / encoder output_size
+    heads: int = 8
+    ffn: int = 1024
+    enc_blocks: int = 4
+    kernel_size: int = 11
+    enc_sanm_shift: int = 0
+    vocab_size: int = 272727        # embedding rows
+    ln_eps: float = 1e-12
+    punc_list: List[str] = field(default_factory=lambda: ["<unk>", "_", "，", "。", "？", "、"])
+    sentence_end_id: int = 3
+
+    @property
+    def d_k(self) -> int:
+        return self.d_model // self.heads
+
+    @property
+    def n_punc(self) -> int:
+        return len(self.punc_list)
+
+    def to_dict(self) -> Dict[str, Any]:
+        return dataclasses.asdict(self)
+
+    @classmethod
+    def from_kwargs(cls, **kw) -> "CTTransformerConfig":
+        c = cls()
+        enc = kw.get("encoder_conf") or {}
+        if kw.get("encoder", "SANMEncoder") != "SANMEncoder":
+            raise ValueError("the HIP CT-Transformer path implements encoder SANMEncoder")
+        if "vocab_size" in kw and kw["vocab_size"] and int(kw["vocab_size"]) > 0:
+            c.vocab_size = int(kw["vocab_size"])
+        c.input_size = int(kw.get("embed_unit", enc.get("input_size", c.input_size)))
+        c.d_model = int(kw.get("att_unit", enc.get("output_size", c.d_model)))
+        c.heads = int(enc.get("attention_heads", c.heads))
+        c.ffn = int(enc.get("linear_units", c.ffn))
+        c.enc_blocks = int(enc.get("num_blocks", c.enc_blocks))
+        c.kernel_size = int(enc.get("kernel_size", c.kernel_size))
+        c.enc_sanm_shift = int(enc.get("sanm_shfit", c.enc_sanm_shift))
+        if enc.get("input_layer", "pe") != "pe" or not enc.get("normalize_before", True):
+            raise ValueError("the HIP CT-Transformer path implements input_layer pe, normalize_before True")
+        if kw.get("punc_list"):
+            c.punc_list = list(kw["punc_list"])
+        if kw.get("sentence_end_id") is not None:
+            c.sentence_end_id = int(kw["sentence_end_id"])
+        return c
+
+    def reference_kwargs(self) -> Dict[str, Any]:
+        """CTTransformer constructor kwargs (template.yaml model_conf + encoder_conf)."""
+        return dict(
+            encoder="SANMEncoder",
+            encoder_conf=dict(input_size=self.input_size, output_size=self.d_model, attention_heads=self.heads,
+                              linear_units=self.ffn, num_blocks=self.enc_blocks, dropout_rate=0.1,
+                              positional_dropout_rate=0.1, attention_dropout_rate=0.0, input_layer="pe",
+                              pos_enc_class="SinusoidalPositionEncoder", normalize_before=True,
+                              kernel_size=self.kernel_size, sanm_shfit=self.enc_sanm_shift,
+                              selfattention_layer_type="sanm", padding_idx=0),
+            vocab_size=self.vocab_size, punc_list=list(self.punc_list), embed_unit=self.input_size,
+            att_unit=self.d_model, dropout_rate=0.1, ignore_id=0, sentence_end_id=self.sentence_end_id,
+        )
+
+
+def ct_transformer() -> CTTransformerConfig:
+    return CTTransformerConfig()
+
+
+def ct_transformer_tiny(enc_blocks: int = 2, vocab_size: int = 4000) -> CTTransformerConfig:
+    """Reduced CT-Transformer for full-tensor goldens (same widths as the released model)."""
+    return CTTransformerConfig(enc_blocks=enc_blocks, vocab_size=vocab_size)

@@ -57,6 +57,11 @@ class CharTokenizer:
     def decode(self, ids: Iterable[int]) -> str:
         return self.tokens2text(self.ids2tokens(ids))
 
+    def encode(self, text, **kwargs) -> List[int]:
+        """text (a string, or a list of words as the punctuation model passes) -> ids
+        (abs_tokenizer.py:65-69; unknown tokens -> unk id)."""
+        return self.tokens2ids(self.text2tokens(text))
+
 
 class SentencepiecesTokenizer:
     """BPE tokenizer over a sentencepiece model file (the SenseVoice tokenizer,

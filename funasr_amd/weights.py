@@ -21,7 +21,7 @@ from typing import Dict, Iterator, List, Tuple
 
 import numpy as np
 
-from .config import ParaformerConfig, SenseVoiceConfig
+from .config import CTTransformerConfig, ParaformerConfig, SenseVoiceConfig
 
 Shape = Tuple[int, ...]
 
@@ -33,6 +33,8 @@ def param_layout(cfg) -> List[Tuple[str, Shape, int]]:
     """
     if isinstance(cfg, SenseVoiceConfig):
         return sense_voice_layout(cfg)
+    if isinstance(cfg, CTTransformerConfig):
+        return ct_transformer_layout(cfg)
     D, F, K, I, V = cfg.d_model, cfg.ffn, cfg.kernel_size, cfg.input_size, cfg.vocab_size
     out: List[Tuple[str, Shape, int]] = []
 
@@ -113,6 +115,19 @@ def sense_voice_layout(cfg: SenseVoiceConfig) -> List[Tuple[str, Shape, int]]:
             ("encoder.tp_norm.weight", (D,), -1), ("encoder.tp_norm.bias", (D,), -2),
             ("ctc.ctc_lo.weight", (V, D), D), ("ctc.ctc_lo.bias", (V,), D),
             ("embed.weight", (cfg.n_embed, I), -3)]
+    return out
+
+
+def ct_transformer_layout(cfg: CTTransformerConfig) -> List[Tuple[str, Shape, int]]:
+    """CTTransformer state_dict keys (ct_transformer/model.py:63-68): embed, encoder (SANMEncoder with
+    input_layer "pe": encoders0.0, encoders.*, after_norm), decoder (Linear att_unit -> punc classes)."""
+    D, F, K, I = cfg.d_model, cfg.ffn, cfg.kernel_size, cfg.input_size
+    out: List[Tuple[str, Shape, int]] = [("embed.weight", (cfg.vocab_size, I), -3)]
+    _enc_layer(out, "encoder.encoders0.0", I, D, F, K)
+    for i in range(cfg.enc_blocks - 1):
+        _enc_layer(out, f"encoder.encoders.{i}", D, D, F, K)
+    out += [("encoder.after_norm.weight", (D,), -1), ("encoder.after_norm.bias", (D,), -2),
+            ("decoder.weight", (cfg.n_punc, D), D), ("decoder.bias", (cfg.n_punc,), D)]
     return out
 
 

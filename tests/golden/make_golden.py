@@ -555,6 +555,68 @@ def save_stream():
         json.dump(wout, f, ensure_ascii=False, indent=1)
 
 
+PUNC_TEXTS = {
+    "short": 12,            # CJK tokens only, one mini-sentence
+    "mixed": 47,            # CJK + ASCII words (split_words keeps ASCII runs as one word; unknown -> <unk>)
+    "long": 260,            # > 200 tokens: several mini-sentences, the carried cache and the comma cut-off rule
+}
+
+
+def punc_text(name: str, n: int, vocab) -> str:
+    """Seeded text of n words from the synthetic token list (CJK tokens), with ASCII words mixed in."""
+    rng = np.random.default_rng(abs(hash(name)) % 1000 if False else {"short": 1, "mixed": 2, "long": 3}[name])
+    cjk = vocab[3:-1]
+    words = []
+    for i in range(n):
+        if name == "mixed" and i % 5 == 3:
+            words.append(" " + ["hello", "world", "FunASR", "ok", "GPU"][i % 5] + " ")
+        else:
+            words.append(cjk[int(rng.integers(len(cjk)))])
+    return "".join(words).strip()
+
+
+def save_punc():
+    """CTTransformer (tiny: 2 SAN-M blocks, vocab 4000, widths of the released model) goldens: the
+    reference inference() text / punc_array for seeded texts, and every punc_forward call it made
+    (mini-sentence ids -> argmax punctuation ids, logits)."""
+    import funasr.models.ct_transformer.model as ctm
+    import funasr.models.sanm.encoder  # noqa: F401
+    from funasr.tokenizer.char_tokenizer import CharTokenizer
+    from funasr_amd.config import ct_transformer_tiny
+    cfg = ct_transformer_tiny()
+    m = tables.model_classes["CTTransformer"](**cfg.reference_kwargs())
+    w = make_weights(cfg, 0)
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in w.items()}, strict=True)
+    m.eval()
+    vocab = token_list(cfg.vocab_size)
+    tok = CharTokenizer(token_list=vocab, unk_symbol="<unk>")
+    calls = []
+    pf = m.punc_forward
+
+    def rec(text, text_lengths, **kw):
+        y, h = pf(text, text_lengths, **kw)
+        calls.append((text[0].numpy().astype(np.int32).copy(), y[0].detach().numpy().copy()))
+        return y, h
+
+    m.punc_forward = rec
+    out = {}
+    arrays = {}
+    for name, n in PUNC_TEXTS.items():
+        text = punc_text(name, n, vocab)
+        calls.clear()
+        with torch.no_grad():
+            res, _ = m.inference([text], key=[name], tokenizer=tok, device="cpu")
+        out[name] = {"text_in": text, "text": res[0]["text"], "punc_array": res[0]["punc_array"].tolist(),
+                     "n_calls": len(calls)}
+        arrays[f"{name}_ids"] = np.concatenate([c[0] for c in calls])
+        arrays[f"{name}_off"] = np.cumsum([0] + [len(c[0]) for c in calls]).astype(np.int32)
+        arrays[f"{name}_logits"] = np.concatenate([c[1] for c in calls]).astype(np.float32)
+        print(name, len(calls), res[0]["text"][:60])
+    with open(f"{HERE}/punc.json", "w", encoding="utf-8") as f:
+        json.dump(out, f, ensure_ascii=False, indent=1)
+    np.savez_compressed(f"{HERE}/punc_tiny.npz", **arrays)
+
+
 if __name__ == "__main__" and len(sys.argv) > 1:
     torch.manual_seed(0)
     for part in sys.argv[1:]:

@@ -208,3 +208,50 @@ def test_streaming_waveform_vs_reference(stream_tiny):
             sr.FrontendOnline.__call__ = orig
         assert [f.shape[0] for f in feats] == gw["feat_rows"], tag
         np.testing.assert_allclose(np.concatenate(feats), np.load(f"{GOLD}/stream_{tag}_feats.npy"), atol=1e-5)
+
+
+# ---------------------------------------------------------------- CT-Transformer punctuation (§8f row 2)
+def test_punc_oracle_vs_reference():
+    """oracle/punc_ref.punc_forward vs every punc_forward call of the reference inference(): logits to
+    1e-5 and the argmax punctuation ids exactly."""
+    from funasr_amd.config import ct_transformer_tiny
+    from oracle.punc_ref import punc_forward
+    cfg = ct_transformer_tiny()
+    w = make_weights(cfg, seed=0)
+    g = np.load(f"{GOLD}/punc_tiny.npz")
+    for name in ("short", "mixed", "long"):
+        ids, off, lg = g[f"{name}_ids"], g[f"{name}_off"], g[f"{name}_logits"]
+        for i in range(len(off) - 1):
+            x = ids[off[i]:off[i + 1]]
+            got = punc_forward(x[None], [len(x)], w, cfg)[0].numpy()
+            ref = lg[off[i]:off[i + 1]]
+            np.testing.assert_allclose(got, ref, atol=1e-5, rtol=1e-5)
+            assert np.array_equal(got.argmax(-1), ref.argmax(-1)), (name, i)
+
+
+def test_punc_text_pipeline_vs_reference():
+    """funasr_amd.punc text logic (split_words, mini-sentences of 20 words, the carried sentence cache,
+    capitalisation / ASCII punctuation, the closing period, punc_array) driven by the reference's own
+    per-call argmax ids reproduces the reference inference() text and punc_array."""
+    import json
+    from funasr_amd.config import ct_transformer_tiny
+    from funasr_amd.punc import punc_inference
+    from funasr_amd.text import CharTokenizer
+    from tests.golden.inputs import token_list
+    cfg = ct_transformer_tiny()
+    tok = CharTokenizer(token_list=token_list(cfg.vocab_size), unk_symbol="<unk>")
+    gold = json.load(open(f"{GOLD}/punc.json", encoding="utf-8"))
+    g = np.load(f"{GOLD}/punc_tiny.npz")
+    for name, gj in gold.items():
+        ids, off, lg = g[f"{name}_ids"], g[f"{name}_off"], g[f"{name}_logits"]
+        calls = [(ids[off[i]:off[i + 1]], lg[off[i]:off[i + 1]].argmax(-1)) for i in range(len(off) - 1)]
+        seen = []
+
+        def forward(x):
+            seen.append(np.asarray(x).copy())
+            return calls[len(seen) - 1][1]
+
+        text, punc_array = punc_inference(gj["text_in"], tok, forward, cfg.punc_list, cfg.sentence_end_id)
+        assert [s.tolist() for s in seen] == [c[0].tolist() for c in calls], name
+        assert text == gj["text"], name
+        assert list(punc_array) == gj["punc_array"], name
