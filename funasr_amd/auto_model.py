@@ -26,6 +26,7 @@ import torch
 from . import model as _model  # noqa: F401  (registers "Paraformer")
 from . import sense_voice as _sense_voice  # noqa: F401  (registers "SenseVoiceSmall")
 from . import streaming as _streaming  # noqa: F401  (registers "ParaformerStreaming")
+from . import punc as _punc  # noqa: F401  (registers "CTTransformer")
 from .frontend import WavFrontend, WavFrontendOnline
 from .register import tables
 from .text import CharTokenizer, SentencepiecesTokenizer

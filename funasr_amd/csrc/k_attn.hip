@@ -635,11 +635,18 @@ __global__ __launch_bounds__(512) void attn_bf16_pp_kernel(AttnArgs a) {
 
 // q/k/v: head-concatenated rows (head h at column h*128). o: f32 [B*Tq, ldo] (may be null in
 // bf16 mode when only o2 is wanted). heads*128 columns per row.
+hipError_t pfm_attention_small(int dtype, const void* q, RowMap qmap, const void* k, RowMap kmap, const void* v,
+                               RowMap vmap, float* o, void* o2, long long ldo, const int* klen, int B, int Tq, int Tk,
+                               int heads, int dk, float scale, hipStream_t st);
+
 hipError_t pfm_attention_fsmn(int dtype, const void* q, RowMap qmap, const void* k, RowMap kmap, const void* v,
                               RowMap vmap, float* o, long long ldo, void* o2, const int* klen, int B, int Tq,
                               int Tk, int heads, int dk, float scale, const float* fsmn_wT, bf16* fsmn_out,
                               long long fsmn_ld, hipStream_t st) {
-    if (dk != DK) return hipErrorInvalidValue;
+    if (dk != DK) {   // 32 / 64-wide heads (CT-Transformer): k_punc.hip; no fused FSMN there
+        if (fsmn_out) return hipErrorInvalidValue;
+        return pfm_attention_small(dtype, q, qmap, k, kmap, v, vmap, o, o2, ldo, klen, B, Tq, Tk, heads, dk, scale, st);
+    }
     if (B <= 0 || Tq <= 0) return hipSuccess;
     AttnArgs a;
     a.q = q; a.qmap = qmap; a.k = k; a.kmap = kmap; a.v = v; a.vmap = vmap;

@@ -68,6 +68,10 @@ bool pfm_gemm_skinny_ok(const void* A, RowMap amap, const void* W, long long ldw
                         const GemmEpi& e);
 hipError_t pfm_gemm_skinny(const void* A, RowMap amap, const void* W, long long ldw, int M, int N, int K,
                            const GemmEpi& e, hipStream_t st);
+hipError_t pfm_punc_embed(const int* ids, const int* lens, int B, int T, const float* embed, int n_embed,
+                          const float* pe, int D, float scale, float* X, hipStream_t st);
+hipError_t pfm_punc_head(const float* x, int B, int T, const int* lens, const float* W, const float* bias, int NP,
+                         int D, int* punc, float* logits, hipStream_t st);
 hipError_t pfm_fbank_raw_launch(const float* wav, const int* nsamp, int B, int S_max, const unsigned char* tables,
                                 float* fb, int N_cap, hipStream_t st);
 hipError_t pfm_lfr_gather_launch(const float* frames, const int* idx, int rows, int m, const float* cmvn, float* out,
@@ -208,6 +212,7 @@ void build_registry(pfm_handle* h) {
     const pfm_config& c = h->cfg;
     const int D = c.d_model, F = c.ffn, K = c.kernel_size, I = c.input_size, V = c.vocab_size;
     const bool sv = c.arch == PFM_ARCH_SENSEVOICE;
+    const bool punc = c.arch == PFM_ARCH_PUNC;
     const int n_enc = c.enc_blocks + (sv ? c.tp_blocks : 0);
     for (int l = 0; l < n_enc; ++l) {
         const std::string p = l == 0 ? "encoder.encoders0.0"
@@ -233,6 +238,12 @@ void build_registry(pfm_handle* h) {
     }
     h->an_g = add_entry(h, "encoder.after_norm.weight", {D});
     h->an_b = add_entry(h, "encoder.after_norm.bias", {D});
+    if (punc) {   // ct_transformer/model.py:63-68: word embedding + punctuation head
+        h->embed = add_entry(h, "embed.weight", {c.n_embed, I});
+        h->ctc_w = add_entry(h, "decoder.weight", {V, D});
+        h->ctc_b = add_entry(h, "decoder.bias", {V});
+        return;
+    }
     if (sv) {   // sense_voice/model.py:542-548, ctc/ctc.py:33, model.py:646-648
         h->tp_g = add_entry(h, "encoder.tp_norm.weight", {D});
         h->tp_b = add_entry(h, "encoder.tp_norm.bias", {D});
@@ -362,7 +373,7 @@ int reserve(pfm_handle* h, int B, int T) {
     B = std::max(B, h->capB);
     T = std::max(T, h->capT);
     const pfm_config& c = h->cfg;
-    const bool sv = c.arch == PFM_ARCH_SENSEVOICE;
+    const bool sv = c.arch == PFM_ARCH_SENSEVOICE || c.arch == PFM_ARCH_PUNC;   // encoder-only families
     const size_t D = c.d_model, F = c.ffn, I = c.input_size;
     const size_t M = (size_t)B * T, Lc = (size_t)T + 1, Ml = (size_t)B * Lc;
     const size_t nkv = (size_t)c.dec_blocks * 2 * D;
@@ -838,19 +849,29 @@ void pfm_config_sensevoice(pfm_config* c) {
     c->ln_eps = 1e-5f;
 }
 
+void pfm_config_punc(pfm_config* c) {
+    pfm_config_default(c);
+    c->arch = PFM_ARCH_PUNC; c->input_size = 256; c->d_model = 256; c->heads = 8; c->ffn = 1024; c->enc_blocks = 4;
+    c->dec_blocks = 0; c->tp_blocks = 0; c->vocab_size = 6; c->n_embed = 272727; c->ln_eps = 1e-12f;
+}
+
 const char* pfm_last_error(void) { return g_err.c_str(); }
 
 int pfm_create(const pfm_config* cfg, int device, pfm_handle** out) {
     if (!cfg || !out) return fail(PFM_E_ARG, "pfm_create: null argument");
     *out = nullptr;
-    if (cfg->d_model % cfg->heads != 0 || cfg->d_model / cfg->heads != 128)
-        return fail(PFM_E_ARG, "pfm_create: head dim must be 128");
+    if (cfg->heads < 1 || cfg->d_model % cfg->heads != 0 ||
+        (cfg->arch == PFM_ARCH_PUNC ? (cfg->d_model / cfg->heads != 32 && cfg->d_model / cfg->heads != 64)
+                                    : cfg->d_model / cfg->heads != 128))
+        return fail(PFM_E_ARG, "pfm_create: head dim must be 128 (32 or 64 for the punctuation model)");
     if (cfg->input_size % 8 || cfg->d_model % 8 || cfg->ffn % 8 || cfg->input_size > 2048 || cfg->ffn > 2048)
         return fail(PFM_E_ARG, "pfm_create: dims must be multiples of 8 and <= 2048");
     if (cfg->enc_blocks < 1 || cfg->dec_blocks < 0 || cfg->kernel_size < 1 || cfg->vocab_size < 1)
         return fail(PFM_E_ARG, "pfm_create: bad block counts");
-    if (cfg->arch != PFM_ARCH_PARAFORMER && cfg->arch != PFM_ARCH_SENSEVOICE)
+    if (cfg->arch != PFM_ARCH_PARAFORMER && cfg->arch != PFM_ARCH_SENSEVOICE && cfg->arch != PFM_ARCH_PUNC)
         return fail(PFM_E_ARG, "pfm_create: unknown arch");
+    if (cfg->arch == PFM_ARCH_PUNC && (cfg->n_embed < 1 || cfg->vocab_size > 64 || cfg->dec_blocks != 0))
+        return fail(PFM_E_ARG, "pfm_create: punctuation model needs n_embed >= 1, <= 64 classes, no decoder");
     if (cfg->arch == PFM_ARCH_PARAFORMER && (cfg->cif_l_order != 1 || cfg->cif_r_order != 1))
         return fail(PFM_E_ARG, "pfm_create: CIF conv must be l_order = r_order = 1");
     if (cfg->arch == PFM_ARCH_SENSEVOICE && (cfg->tp_blocks < 0 || cfg->n_embed < 1))
@@ -1225,6 +1246,36 @@ int pfm_run_ctc(pfm_handle* h, void* stream, int mode, const float* feats, const
                               st));
     // unique_consecutive + drop blank (model.py:894-906)
     HIP_TRY(pfm_ctc_collapse(fid, Tq, olen, B, 0, L_cap, tokens, ntok_out, st));
+    return PFM_OK;
+}
+
+int pfm_run_punc(pfm_handle* h, void* stream, int mode, const int32_t* ids, const int32_t* lens, int B, int T,
+                 int32_t* punc, float* logits) {
+    if (!h || !ids || !lens || !punc) return fail(PFM_E_ARG, "pfm_run_punc: null argument");
+    if (h->cfg.arch != PFM_ARCH_PUNC) return fail(PFM_E_STATE, "pfm_run_punc: handle is not a punctuation model");
+    if (B < 1 || T < 1) return fail(PFM_E_ARG, "pfm_run_punc: bad sizes");
+    if (mode != PFM_MODE_EXACT && mode != PFM_MODE_FAST) return fail(PFM_E_ARG, "pfm_run_punc: bad mode");
+    if (h->missing) return fail(PFM_E_STATE, "pfm_run_punc: weights not set");
+    const pfm_config& c = h->cfg;
+    HIP_TRY(hipSetDevice(h->device));
+    hipStream_t st = (hipStream_t)stream;
+    const bool fast = mode == PFM_MODE_FAST;
+    int rc = reserve(h, B, T);
+    if (rc) return rc;
+    if (fast) { rc = ensure_bf16(h, st); if (rc) return rc; }
+    const int D = c.d_model;
+    float* X = h->X.as<float>();
+    // X = embed[ids] * sqrt(d) + PE: the encoder input AND layer 0's residual (input_size == d_model)
+    HIP_TRY(pfm_punc_embed(ids, lens, B, T, h->w(h->embed), c.n_embed, h->pe.as<float>(), D, sqrtf((float)D), X, st));
+    Run run(h, st, fast);
+    run.fuse_fsmn = false;   // 32-wide heads: the fused FSMN epilogue lives in the d_k = 128 kernel
+    run.raw_input = true;
+    const FinalLN fin = {h->an_g, h->an_b, h->Xf.as<float>(), rowmap_plain(D), DT_F32, nullptr, rowmap_plain(D),
+                         DT_BF16};
+    rc = encoder_stack(run, X, lens, B, T, 0, c.enc_blocks, X, fin, enc_ws(h, 0));
+    if (rc) return rc;
+    HIP_TRY(pfm_punc_head(h->Xf.as<float>(), B, T, lens, h->w(h->ctc_w), h->w(h->ctc_b), c.vocab_size, D, punc,
+                          logits, st));
     return PFM_OK;
 }
 

@@ -12,13 +12,13 @@ from typing import Dict, Optional
 
 import numpy as np
 
-from .config import ParaformerConfig, SenseVoiceConfig
+from .config import CTTransformerConfig, ParaformerConfig, SenseVoiceConfig
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("PFM_LIB", os.path.join(_HERE, "_lib", "libpfm_hip.so"))
 
 PFM_F32, PFM_BF16 = 0, 1
-ARCH_PARAFORMER, ARCH_SENSEVOICE = 0, 1
+ARCH_PARAFORMER, ARCH_SENSEVOICE, ARCH_PUNC = 0, 1, 2
 MODE_EXACT, MODE_FAST = 0, 1
 MODES = {"exact": MODE_EXACT, "fp32": MODE_EXACT, "fast": MODE_FAST, "bf16": MODE_FAST}
 
@@ -27,7 +27,7 @@ ABI_SYMBOLS = ("pfm_config_default", "pfm_config_sensevoice", "pfm_create", "pfm
                "pfm_missing_weights", "pfm_reserve", "pfm_run", "pfm_run_ctc", "pfm_op_ctc_collapse", "pfm_fbank", "pfm_lfr_frames", "pfm_last_error", "pfm_destroy", "pfm_op_gemm",
                "pfm_op_attention", "pfm_op_layernorm", "pfm_op_fsmn", "pfm_op_cif", "pfm_profile", "pfm_op_gemm_layernorm", "pfm_op_fsmn_bf16", "pfm_op_layernorm_bf16",
                "pfm_profile_read", "pfm_streams_create", "pfm_streams_reset", "pfm_stream_step",
-               "pfm_streams_destroy", "pfm_fbank_raw", "pfm_lfr_gather")
+               "pfm_streams_destroy", "pfm_fbank_raw", "pfm_lfr_gather", "pfm_config_punc", "pfm_run_punc")
 
 
 class PfmError(RuntimeError):
@@ -44,6 +44,9 @@ class PfmConfig(ctypes.Structure):
 
     @classmethod
     def from_config(cls, c) -> "PfmConfig":
+        if isinstance(c, CTTransformerConfig):
+            return cls(c.input_size, c.d_model, c.heads, c.ffn, c.enc_blocks, 0, c.kernel_size, c.enc_sanm_shift, 0,
+                       c.n_punc, 1, 1, 1.0, 0.45, 1.0, 0.0, c.ln_eps, ARCH_PUNC, 0, c.vocab_size)
         if isinstance(c, SenseVoiceConfig):
             return cls(c.input_size, c.d_model, c.heads, c.ffn, c.enc_blocks, 0, c.kernel_size, c.enc_sanm_shift, 0,
                        c.vocab_size, 1, 1, 1.0, 0.45, 1.0, 0.0, c.ln_eps, ARCH_SENSEVOICE, c.tp_blocks, c.n_embed)
@@ -103,6 +106,9 @@ def load_library(path: Optional[str] = None) -> ctypes.CDLL:
                                     f32p, f32p]
     lib.pfm_fbank_raw.argtypes = [vp, vp, f32p, i32p, i32, i32, f32p, i32]
     lib.pfm_lfr_gather.argtypes = [vp, f32p, i32p, i32, i32, f32p, f32p]
+    lib.pfm_config_punc.argtypes = [ctypes.POINTER(PfmConfig)]
+    lib.pfm_config_punc.restype = None
+    lib.pfm_run_punc.argtypes = [vp, vp, i32, i32p, i32p, i32, i32, i32p, f32p]
     lib.pfm_streams_destroy.argtypes = [vp]
     lib.pfm_streams_destroy.restype = None
     for name in ABI_SYMBOLS:
@@ -209,6 +215,27 @@ class PfmEngine:
         check(self.lib.pfm_run(self.h, _stream_ptr(torch, dev), m, _ptr(feats), _ptr(lens), B, T, _ptr(tokens),
                                L_cap, _ptr(ntok), _ptr(enc), _ptr(alphas), _ptr(peaks)), "pfm_run")
         return dict(tokens=tokens, ntok=ntok, enc=enc, alphas=alphas, peaks=peaks)
+
+    def run_punc(self, ids, lens, mode="exact", want_logits=False):
+        """CT-Transformer: word ids [B,T] int32 cuda, lens [B] -> dict(punc [B,T] int32 (-1 beyond lens),
+        logits [B,T,classes] on request)."""
+        torch = self.torch
+        if not isinstance(self.cfg, CTTransformerConfig):
+            raise PfmError("run_punc needs a CT-Transformer engine")
+        dev = torch.device("cuda", self.device)
+        ids = ids.to(device=dev, dtype=torch.int32).contiguous()
+        if ids.dim() != 2:
+            raise PfmError("ids must be [B, T]")
+        lens = lens.reshape(-1).to(device=dev, dtype=torch.int32).contiguous()
+        B, T = ids.shape
+        if lens.numel() != B:
+            raise PfmError("lens must have one entry per sequence")
+        punc = torch.empty((B, T), dtype=torch.int32, device=dev)
+        logits = torch.empty((B, T, self.cfg.n_punc), dtype=torch.float32, device=dev) if want_logits else None
+        m = MODES[mode] if isinstance(mode, str) else int(mode)
+        check(self.lib.pfm_run_punc(self.h, _stream_ptr(torch, dev), m, _ptr(ids), _ptr(lens), B, T, _ptr(punc),
+                                    _ptr(logits)), "pfm_run_punc")
+        return dict(punc=punc, logits=logits)
 
     def run_ctc(self, feats, lens, query, mode="exact", ban_token: int = -1, L_cap: Optional[int] = None,
                 want_enc=False, want_frames=False):

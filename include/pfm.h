@@ -50,7 +50,7 @@ enum pfm_mode { PFM_MODE_EXACT = 0, PFM_MODE_FAST = 1 };
  *  PARAFORMER : SAN-M encoder + CIF predictor + SAN-M NAR decoder (funasr/models/paraformer/model.py)
  *  SENSEVOICE : SenseVoiceSmall — 4 query rows + SAN-M encoder + tp encoder + CTC head
  *               (funasr/models/sense_voice/model.py:445-950); decoder / predictor fields ignored */
-enum pfm_arch { PFM_ARCH_PARAFORMER = 0, PFM_ARCH_SENSEVOICE = 1 };
+enum pfm_arch { PFM_ARCH_PARAFORMER = 0, PFM_ARCH_SENSEVOICE = 1, PFM_ARCH_PUNC = 2 };
 
 /* Model dimensions; mirrors encoder_conf / decoder_conf / predictor_conf of
  * funasr/models/paraformer/template.yaml:8-66 (Paraformer-large defaults via
@@ -139,6 +139,20 @@ int pfm_run(pfm_handle* h, void* stream, int mode, const float* feats, const int
 int pfm_run_ctc(pfm_handle* h, void* stream, int mode, const float* feats, const int32_t* lens,
                 int B, int T, const int32_t* query, int ban_token, int32_t* tokens, int L_cap,
                 int32_t* ntok, float* enc_out, int32_t* frame_ids);
+
+/* ---- CT-Transformer punctuation (PFM_ARCH_PUNC; funasr/models/ct_transformer/model.py:81-93) ----
+ * Config: input_size = embed_unit, d_model = att_unit, heads (head width 32 or 64), ffn, enc_blocks,
+ * kernel_size, vocab_size = number of punctuation classes (<= 64), n_embed = word vocabulary rows,
+ * ln_eps. Weights: "embed.weight" [n_embed, input_size], the SANMEncoder keys "encoder.*",
+ * "decoder.weight" [vocab_size, d_model], "decoder.bias". */
+void pfm_config_punc(pfm_config* c);   /* the released punc_ct-transformer (vocab 272727, 4 x 256-wide) */
+
+/* punc_forward + topk(1) for B word sequences (the reference runs one mini-sentence at a time):
+ *   ids    [B, T] int32 device word ids; lens [B] int32 device
+ *   punc   [B, T] int32 out: argmax punctuation class per word (-1 beyond lens)
+ *   logits optional [B, T, vocab_size] f32 out (NULL to skip) */
+int pfm_run_punc(pfm_handle* h, void* stream, int mode, const int32_t* ids, const int32_t* lens, int B, int T,
+                 int32_t* punc, float* logits);
 
 /* ---- Streaming Paraformer (ParaformerStreaming, paraformer_streaming/model.py:435-656) ----
  * A pfm_streams object holds `slots` independent streams whose chunk caches live in HBM:

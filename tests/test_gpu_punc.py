@@ -1,0 +1,126 @@
+"""CT-Transformer punctuation through the C-ABI (pfm_run_punc) vs the reference
+CTTransformer goldens (tests/golden/punc_tiny.npz / punc.json) and the oracle (oracle/punc_ref.py).
+
+EXACT mode: logits of every reference punc_forward call within 1e-4, argmax ids identical; AutoModel
+text / punc_array identical to the reference inference(). FAST mode: argmax agreement floor.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from funasr_amd.config import ct_transformer, ct_transformer_tiny  # noqa: E402
+from funasr_amd.runtime import PfmEngine, PfmError  # noqa: E402
+from funasr_amd.weights import make_weights  # noqa: E402
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+@pytest.fixture(scope="module")
+def tiny():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    cfg = ct_transformer_tiny()
+    w = make_weights(cfg, seed=0)
+    e = PfmEngine(cfg, 0)
+    e.load_state_dict(w)
+    return cfg, e, w
+
+
+def _calls(name):
+    g = np.load(f"{GOLD}/punc_tiny.npz")
+    ids, off, lg = g[f"{name}_ids"], g[f"{name}_off"], g[f"{name}_logits"]
+    return [(ids[off[i]:off[i + 1]], lg[off[i]:off[i + 1]]) for i in range(len(off) - 1)]
+
+
+@pytest.mark.parametrize("name", ["short", "mixed", "long"])
+def test_punc_exact_vs_reference_calls(tiny, name):
+    cfg, e, _ = tiny
+    for x, ref in _calls(name):
+        r = e.run_punc(torch.from_numpy(x[None].astype(np.int32)).cuda(),
+                       torch.tensor([len(x)], dtype=torch.int32).cuda(), mode="exact", want_logits=True)
+        torch.cuda.synchronize()
+        lg = r["logits"][0].cpu().numpy()
+        np.testing.assert_allclose(lg, ref, atol=1e-4, rtol=1e-4)
+        assert np.array_equal(r["punc"][0].cpu().numpy(), ref.argmax(-1))
+
+
+def test_punc_batched_ragged_vs_oracle(tiny):
+    """Three word sequences of different lengths in one call (padded rows -> -1, keys masked)."""
+    from oracle.punc_ref import punc_forward
+    cfg, e, w = tiny
+    rng = np.random.default_rng(9)
+    lens = [37, 5, 120]
+    T = max(lens)
+    ids = np.zeros((3, T), np.int32)
+    for b, n in enumerate(lens):
+        ids[b, :n] = rng.integers(3, cfg.vocab_size, n)
+    r = e.run_punc(torch.from_numpy(ids).cuda(), torch.tensor(lens, dtype=torch.int32).cuda(), mode="exact",
+                   want_logits=True)
+    torch.cuda.synchronize()
+    punc, lg = r["punc"].cpu().numpy(), r["logits"].cpu().numpy()
+    for b, n in enumerate(lens):
+        ref = punc_forward(ids[b:b + 1, :n], [n], w, cfg)[0].numpy()
+        np.testing.assert_allclose(lg[b, :n], ref, atol=1e-4, rtol=1e-4)
+        assert np.array_equal(punc[b, :n], ref.argmax(-1))
+        assert np.all(punc[b, n:] == -1)
+
+
+def test_punc_fast_mode_agreement(tiny):
+    cfg, e, _ = tiny
+    agree = total = 0
+    for name in ("short", "mixed", "long"):
+        for x, ref in _calls(name):
+            r = e.run_punc(torch.from_numpy(x[None].astype(np.int32)).cuda(),
+                           torch.tensor([len(x)], dtype=torch.int32).cuda(), mode="fast")
+            torch.cuda.synchronize()
+            agree += int((r["punc"][0].cpu().numpy() == ref.argmax(-1)).sum())
+            total += len(x)
+    assert agree / total >= 0.8, (agree, total)
+
+
+def test_punc_released_dims_vs_oracle():
+    """The released model's dimensions (4 blocks, 272,727-word embedding): argmax ids exact vs the oracle."""
+    from oracle.punc_ref import punc_forward
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    cfg = ct_transformer()
+    w = make_weights(cfg, seed=0)
+    e = PfmEngine(cfg, 0)
+    e.load_state_dict(w)
+    ids = np.random.default_rng(4).integers(3, cfg.vocab_size, (1, 217)).astype(np.int32)
+    r = e.run_punc(torch.from_numpy(ids).cuda(), torch.tensor([217], dtype=torch.int32).cuda(), mode="exact",
+                   want_logits=True)
+    torch.cuda.synchronize()
+    ref = punc_forward(ids, [217], w, cfg)[0].numpy()
+    np.testing.assert_allclose(r["logits"][0].cpu().numpy(), ref, atol=1e-4, rtol=1e-4)
+    assert np.array_equal(r["punc"][0].cpu().numpy(), ref.argmax(-1))
+
+
+def test_automodel_punc_generate_vs_reference():
+    """AutoModel(model="CTTransformer").generate(input=text): text and punc_array of the reference."""
+    from funasr_amd.auto_model import AutoModel
+    from tests.golden.inputs import token_list
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    cfg = ct_transformer_tiny()
+    am = AutoModel(model="CTTransformer", model_conf={}, synthetic_seed=0, device="cuda", mode="exact",
+                   tokenizer="CharTokenizer", tokenizer_conf=dict(token_list=token_list(cfg.vocab_size),
+                                                                  unk_symbol="<unk>"),
+                   **cfg.reference_kwargs())
+    gold = json.load(open(f"{GOLD}/punc.json", encoding="utf-8"))
+    for name, gj in gold.items():
+        res = am.generate(input=gj["text_in"], key=name)
+        assert res[0]["key"] == name
+        assert res[0]["text"] == gj["text"], name
+        assert res[0]["punc_array"].tolist() == gj["punc_array"], name
+
+
+def test_punc_bad_args(tiny):
+    cfg, e, _ = tiny
+    with pytest.raises(PfmError):
+        e.run_punc(torch.zeros((2, 4), dtype=torch.int32).cuda(), torch.tensor([4], dtype=torch.int32).cuda())
