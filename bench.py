@@ -122,6 +122,43 @@ def stream_leg(args, dev, torch, make_weights) -> dict:
     return res
 
 
+def punc_leg(args, dev, torch, make_weights) -> dict:
+    from funasr_amd.config import ct_transformer
+    from funasr_amd.runtime import PfmEngine
+    cfg = ct_transformer()
+    w = make_weights(cfg, args.seed)
+    eng = PfmEngine(cfg, dev.index or 0)
+    eng.load_state_dict(w)
+    B, T = 64, 200
+    g = torch.Generator(device=dev)
+    g.manual_seed(3000)
+    ids = torch.randint(3, cfg.vocab_size, (B, T), generator=g, device=dev, dtype=torch.int32)
+    lens = torch.full((B,), T, dtype=torch.int32, device=dev)
+    for _ in range(2):
+        eng.run_punc(ids, lens, mode=args.mode)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.punc_steps):
+        eng.run_punc(ids, lens, mode=args.mode)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / args.punc_steps
+    res = {"workload": f"CT-Transformer punctuation (released dims: 4 x 256-wide SAN-M, 272,727-word embedding), "
+                       f"{B} sequences x {T} words per pfm_run_punc", "value": round(B * T / dt, 1),
+           "unit": "words/sec", "ms_per_call": round(dt * 1e3, 3), "dtype": "bf16" if args.mode == "fast" else "f32"}
+    if args.cpu_utts > 0:
+        from oracle.punc_ref import punc_forward
+        torch.set_num_threads(int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)))
+        x = ids[:8].cpu().numpy()
+        tc = time.perf_counter()
+        punc_forward(x, [T] * 8, w, cfg)
+        dtc = time.perf_counter() - tc
+        res["cpu_baseline"] = {"value": round(8 * T / dtc, 1), "unit": "words/sec", "cores": torch.get_num_threads(),
+                               "kind": "port", "sample": f"8 sequences x {T} words through oracle/punc_ref.punc_forward "
+                                                         f"(torch-CPU fp32), {dtc:.2f} s on {cpu_model()}"}
+    del eng
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -137,6 +174,7 @@ def main():
     ap.add_argument("--stream-chunks", type=int, default=50,
                     help="600 ms chunks per stream in the streaming (config C5) leg (0 = skip)")
     ap.add_argument("--stream-batch", type=int, default=64, help="concurrent streams of the C5 serving line")
+    ap.add_argument("--punc-steps", type=int, default=5, help="timed CT-Transformer punctuation calls (0 = skip)")
     args = ap.parse_args()
 
     import torch
@@ -311,6 +349,10 @@ def main():
     # (the reference's batch 1: per-chunk latency) and S concurrent streams (serving throughput), rank 0
     if rank == 0 and world == 1 and args.stream_chunks > 0:
         out["streaming"] = stream_leg(args, dev, torch, make_weights)
+
+    # ---- CT-Transformer punctuation: 64 word sequences x 200 words per pfm_run_punc
+    if rank == 0 and world == 1 and args.punc_steps > 0:
+        out["punctuation"] = punc_leg(args, dev, torch, make_weights)
 
     # ---- CPU baseline: the oracle torch-CPU restatement on a bounded sample (rank 0, N=1 only)
     if rank == 0 and world == 1 and args.cpu_utts > 0:
