@@ -27,6 +27,7 @@ from . import model as _model  # noqa: F401  (registers "Paraformer")
 from . import sense_voice as _sense_voice  # noqa: F401  (registers "SenseVoiceSmall")
 from . import streaming as _streaming  # noqa: F401  (registers "ParaformerStreaming")
 from . import punc as _punc  # noqa: F401  (registers "CTTransformer")
+from . import vad as _vad  # noqa: F401  (registers "FsmnVADStreaming")
 from .frontend import WavFrontend, WavFrontendOnline
 from .register import tables
 from .text import CharTokenizer, SentencepiecesTokenizer
@@ -158,7 +159,7 @@ class AutoModel:
         tokenizer, vocab = build_tokenizer(tok_name, kwargs.get("tokenizer_conf"))
         kwargs["tokenizer"] = tokenizer
         fconf = kwargs.get("frontend_conf") or {}
-        online = kwargs.get("frontend") == "WavFrontendOnline" or name == "ParaformerStreaming"
+        online = kwargs.get("frontend") == "WavFrontendOnline" or name in ("ParaformerStreaming", "FsmnVADStreaming")
         kwargs["frontend"] = (WavFrontendOnline if online else WavFrontend)(**fconf)
         if tokenizer is None:
             vocab = kwargs.get("vocab_size", -1)

@@ -323,3 +323,64 @@ def ct_transformer() -> CTTransformerConfig:
 def ct_transformer_tiny(enc_blocks: int = 2, vocab_size: int = 4000) -> CTTransformerConfig:
     """Reduced CT-Transformer for full-tensor goldens (same widths as the released model)."""
     return CTTransformerConfig(enc_blocks=enc_blocks, vocab_size=vocab_size)
+
+
+@dataclass
+class FsmnVADConfig:
+    """FSMN-VAD (funasr/models/fsmn_vad_streaming/template.yaml; encoder.py:200-279): frames of the online
+    frontend with LFR (5, 1) -> in_linear1 (400 -> 140) -> in_linear2 (-> 250) -> ReLU -> 4 x [linear (250 ->
+    128, no bias) -> causal FSMN memory (lorder 20, x + sum of 20 taps) -> affine (-> 250) -> ReLU] ->
+    out_linear1 (-> 140) -> out_linear2 (-> 248) -> softmax. vad_opts: VADXOptions (model.py:49-117)."""
+    input_dim: int = 400
+    input_affine_dim: int = 140
+    fsmn_layers: int = 4
+    linear_dim: int = 250
+    proj_dim: int = 128
+    lorder: int = 20
+    rorder: int = 0
+    lstride: int = 1
+    output_affine_dim: int = 140
+    output_dim: int = 248
+    lfr_m: int = 5
+    lfr_n: int = 1
+    vad_opts: Dict[str, Any] = field(default_factory=lambda: dict(
+        sample_rate=16000, detect_mode=1, snr_mode=0, max_end_silence_time=800, max_start_silence_time=3000,
+        do_start_point_detection=True, do_end_point_detection=True, window_size_ms=200,
+        sil_to_speech_time_thres=150, speech_to_sil_time_thres=150, speech_2_noise_ratio=1.0, do_extend=1,
+        lookback_time_start_point=200, lookahead_time_end_point=100, max_single_segment_time=60000,
+        snr_thres=-100.0, noise_frame_num_used_for_snr=100, decibel_thres=-100.0, speech_noise_thres=0.6,
+        fe_prior_thres=1e-4, silence_pdf_num=1, sil_pdf_ids=[0], speech_noise_thresh_low=-0.1,
+        speech_noise_thresh_high=0.3, output_frame_probs=False, frame_in_ms=10, frame_length_ms=25))
+
+    def to_dict(self) -> Dict[str, Any]:
+        return dataclasses.asdict(self)
+
+    @classmethod
+    def from_kwargs(cls, **kw) -> "FsmnVADConfig":
+        c = cls()
+        if kw.get("encoder", "FSMN") != "FSMN":
+            raise ValueError("the HIP FSMN-VAD path implements encoder FSMN")
+        enc = kw.get("encoder_conf") or {}
+        for k in ("input_dim", "input_affine_dim", "fsmn_layers", "linear_dim", "proj_dim", "lorder", "rorder",
+                  "lstride", "output_affine_dim", "output_dim"):
+            if k in enc:
+                setattr(c, k, int(enc[k]))
+        if c.rorder != 0 or c.lstride != 1:
+            raise ValueError("the HIP FSMN-VAD path implements rorder 0, lstride 1 (the released model)")
+        fc = kw.get("frontend_conf") or {}
+        c.lfr_m, c.lfr_n = int(fc.get("lfr_m", c.lfr_m)), int(fc.get("lfr_n", c.lfr_n))
+        for k in list(c.vad_opts):
+            if k in kw and kw[k] is not None:
+                c.vad_opts[k] = kw[k]
+        return c
+
+    def reference_kwargs(self) -> Dict[str, Any]:
+        return dict(encoder="FSMN", encoder_conf=dict(
+            input_dim=self.input_dim, input_affine_dim=self.input_affine_dim, fsmn_layers=self.fsmn_layers,
+            linear_dim=self.linear_dim, proj_dim=self.proj_dim, lorder=self.lorder, rorder=self.rorder,
+            lstride=self.lstride, rstride=0, output_affine_dim=self.output_affine_dim, output_dim=self.output_dim),
+            **self.vad_opts)
+
+
+def fsmn_vad() -> FsmnVADConfig:
+    return FsmnVADConfig()

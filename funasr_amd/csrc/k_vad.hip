@@ -1,0 +1,115 @@
+// FSMN-VAD encoder kernels (funasr/models/fsmn_vad_streaming/encoder.py:12-279): the per-frame speech /
+// silence posteriors that the VAD state machine (fsmn_vad_streaming/model.py:493-546, host side) consumes.
+//
+//   vad_dense_kernel   Y[t, n] = act(X[t, :] . W[n, :] + b[n]) for the Affine / Linear transforms
+//                      (K = 400, 140, 250, 128: any K; f32 FMA chain per output, one thread per output,
+//                      the weight matrices (<= 56k floats) stay L2-resident)
+//   vad_fsmn_kernel    causal memory block (FSMNBlock.forward with its cache, rorder 0): y[t] = x[t] +
+//                      sum_j w[c][j] * x[t - (L-1) + j], rows before the chunk from the per-layer cache
+//                      (zeros at the start of a stream); the cache then keeps the chunk's last L-1 rows
+//   vad_softmax_kernel softmax over the output pdfs per frame (one wave per frame); writes p[t][0] (the
+//                      silence pdf, sil_pdf_ids = [0]) and optionally every posterior
+#include <math.h>
+
+#include "pfm_common.h"
+
+namespace {
+
+__global__ __launch_bounds__(256) void vad_dense_kernel(const float* __restrict__ X, int ldx, int M, int K,
+                                                        const float* __restrict__ W, const float* __restrict__ b,
+                                                        int N, int relu, float* __restrict__ Y, int ldy) {
+    const long long gid = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (gid >= (long long)M * N) return;
+    const int n = (int)(gid % N);
+    const long long m = gid / N;
+    const float* x = X + m * ldx;
+    const float* w = W + (long long)n * K;
+    float s = 0.f;
+    for (int k = 0; k < K; ++k) s = fmaf(x[k], w[k], s);
+    if (b) s += b[n];
+    if (relu) s = fmaxf(s, 0.f);
+    Y[m * ldy + n] = s;
+}
+
+// x [T, D] (this chunk), cache [L-1, D] (previous rows), w [D, L] (conv_left taps, tap j multiplies row
+// t - (L-1) + j). One thread per (row, channel). The cache update runs in a second launch (rows must be
+// read before they are replaced).
+__global__ __launch_bounds__(256) void vad_fsmn_kernel(const float* __restrict__ x, int T, int D,
+                                                       const float* __restrict__ cache, const float* __restrict__ w,
+                                                       int L, float* __restrict__ y) {
+    const long long gid = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (gid >= (long long)T * D) return;
+    const int c = (int)(gid % D);
+    const int t = (int)(gid / D);
+    float s = 0.f;
+    for (int j = 0; j < L; ++j) {
+        const int r = t - (L - 1) + j;   // row of the chunk; < 0 -> cache row L-1+r
+        const float v = r >= 0 ? x[(long long)r * D + c] : cache[(long long)(L - 1 + r) * D + c];
+        s = fmaf(w[c * L + j], v, s);
+    }
+    y[(long long)t * D + c] = x[(long long)t * D + c] + s;
+}
+
+// new cache = last L-1 rows of [cache ; x]
+__global__ __launch_bounds__(256) void vad_fsmn_cache_kernel(const float* __restrict__ x, int T, int D,
+                                                             const float* __restrict__ cache_old, int L,
+                                                             float* __restrict__ cache_new) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= (L - 1) * D) return;
+    const int r = i / D, c = i % D;
+    const int src = T - (L - 1) + r;   // row index into [cache ; x] minus (L-1)
+    cache_new[i] = src >= 0 ? x[(long long)src * D + c] : cache_old[(long long)(L - 1 + src) * D + c];
+}
+
+__global__ __launch_bounds__(256) void vad_softmax_kernel(const float* __restrict__ logits, int M, int N,
+                                                          float* __restrict__ p_sil, float* __restrict__ probs) {
+    const int lane = threadIdx.x & 63;
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= M) return;
+    const float* l = logits + (long long)row * N;
+    float mx = -INFINITY;
+    for (int j = lane; j < N; j += 64) mx = fmaxf(mx, l[j]);
+    mx = wave_max(mx);
+    float s = 0.f;
+    for (int j = lane; j < N; j += 64) s += expf(l[j] - mx);
+    s = wave_sum(s);
+    if (probs)
+        for (int j = lane; j < N; j += 64) probs[(long long)row * N + j] = expf(l[j] - mx) / s;
+    if (lane == 0) p_sil[row] = expf(l[0] - mx) / s;
+}
+
+}  // namespace
+
+hipError_t pfm_vad_dense(const float* X, int ldx, int M, int K, const float* W, const float* b, int N, int relu,
+                         float* Y, int ldy, hipStream_t st) {
+    const long long n = (long long)M * N;
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(vad_dense_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, X, ldx, M, K, W, b, N,
+                       relu, Y, ldy);
+    PFM_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+hipError_t pfm_vad_fsmn(const float* x, int T, int D, float* cache, float* cache_tmp, const float* w, int L, float* y,
+                        hipStream_t st) {
+    if (T <= 0) return hipSuccess;
+    const long long n = (long long)T * D;
+    hipLaunchKernelGGL(vad_fsmn_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, x, T, D, cache, w, L, y);
+    PFM_LAUNCH_CHECK();
+    if (L > 1) {
+        const int nc = (L - 1) * D;
+        hipLaunchKernelGGL(vad_fsmn_cache_kernel, dim3((nc + 255) / 256), dim3(256), 0, st, x, T, D, cache, L,
+                           cache_tmp);
+        PFM_LAUNCH_CHECK();
+        const hipError_t e = hipMemcpyAsync(cache, cache_tmp, (size_t)nc * 4, hipMemcpyDeviceToDevice, st);
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
+hipError_t pfm_vad_softmax(const float* logits, int M, int N, float* p_sil, float* probs, hipStream_t st) {
+    if (M <= 0) return hipSuccess;
+    hipLaunchKernelGGL(vad_softmax_kernel, dim3((M + 3) / 4), dim3(256), 0, st, logits, M, N, p_sil, probs);
+    PFM_LAUNCH_CHECK();
+    return hipSuccess;
+}

@@ -72,6 +72,11 @@ hipError_t pfm_punc_embed(const int* ids, const int* lens, int B, int T, const f
                           const float* pe, int D, float scale, float* X, hipStream_t st);
 hipError_t pfm_punc_head(const float* x, int B, int T, const int* lens, const float* W, const float* bias, int NP,
                          int D, int* punc, float* logits, hipStream_t st);
+hipError_t pfm_vad_dense(const float* X, int ldx, int M, int K, const float* W, const float* b, int N, int relu,
+                         float* Y, int ldy, hipStream_t st);
+hipError_t pfm_vad_fsmn(const float* x, int T, int D, float* cache, float* cache_tmp, const float* w, int L, float* y,
+                        hipStream_t st);
+hipError_t pfm_vad_softmax(const float* logits, int M, int N, float* p_sil, float* probs, hipStream_t st);
 hipError_t pfm_fbank_raw_launch(const float* wav, const int* nsamp, int B, int S_max, const unsigned char* tables,
                                 float* fb, int N_cap, hipStream_t st);
 hipError_t pfm_lfr_gather_launch(const float* frames, const int* idx, int rows, int m, const float* cmvn, float* out,
@@ -1279,6 +1284,19 @@ int pfm_run_punc(pfm_handle* h, void* stream, int mode, const int32_t* ids, cons
     return PFM_OK;
 }
 
+static int fbank_tables_build(DevBuf& dst) {
+    std::vector<unsigned char> tab(pfm_fbank_table_bytes(), 0);
+    float* melw = (float*)tab.data();
+    int* lo = (int*)(tab.data() + 80 * 256 * 4);
+    int* hi = lo + 80;
+    float* window = (float*)(hi + 80);
+    double* tw = (double*)(tab.data() + pfm_fbank_twoff());
+    pfm_fbank_tables(melw, lo, hi, window, tw);
+    HIP_TRY(dst.ensure(tab.size()));
+    HIP_TRY(hipMemcpy(dst.p, tab.data(), tab.size(), hipMemcpyHostToDevice));
+    return PFM_OK;
+}
+
 static int fbank_tables_ready(pfm_handle* h) {
     if (h->fb_tab_ready) return PFM_OK;
     std::vector<unsigned char> tab(pfm_fbank_table_bytes(), 0);
@@ -1880,6 +1898,180 @@ void pfm_streams_destroy(pfm_streams* s) {
     (void)hipDeviceSynchronize();
     if (s->hntok) (void)hipHostFree(s->hntok);
     delete s;
+}
+
+}  // extern "C"
+
+// ============================================================================================
+// FSMN-VAD encoder (include/pfm.h, pfm_vad_*): one stream, per-layer memory caches in HBM.
+// ============================================================================================
+struct pfm_vad {
+    pfm_vad_config cfg;
+    int device = 0;
+    struct W { std::vector<int64_t> shape; size_t off = 0, numel = 0; bool set = false; };
+    std::unordered_map<std::string, W> reg;
+    size_t elems = 0;
+    int missing = 0;
+    DevBuf arena, cache, ctmp, h1, h2, pa, pb, o1, lg;
+    DevBuf fb_tab;        // fbank tables of the object's own online frontend (pfm_vad_fbank_raw)
+    bool fb_ready = false;
+    int capT = 0;
+    size_t add(const std::string& n, std::vector<int64_t> shape) {
+        W w;
+        w.shape = shape;
+        w.numel = 1;
+        for (auto d : shape) w.numel *= (size_t)d;
+        w.off = elems;
+        elems += (w.numel + 63) & ~size_t(63);
+        reg[n] = w;
+        ++missing;
+        return w.off;
+    }
+    float* p(const std::string& n) { return arena.as<float>() + reg[n].off; }
+};
+
+extern "C" {
+
+void pfm_vad_config_default(pfm_vad_config* c) {
+    c->input_dim = 400; c->input_affine_dim = 140; c->fsmn_layers = 4; c->linear_dim = 250; c->proj_dim = 128;
+    c->lorder = 20; c->output_affine_dim = 140; c->output_dim = 248;
+}
+
+int pfm_vad_create(const pfm_vad_config* c, int device, pfm_vad** out) {
+    if (!c || !out) return fail(PFM_E_ARG, "pfm_vad_create: null argument");
+    *out = nullptr;
+    if (c->input_dim < 1 || c->input_affine_dim < 1 || c->fsmn_layers < 0 || c->linear_dim < 1 || c->proj_dim < 1 ||
+        c->lorder < 1 || c->output_affine_dim < 1 || c->output_dim < 1)
+        return fail(PFM_E_ARG, "pfm_vad_create: bad dims");
+    int ndev = 0;
+    HIP_TRY(hipGetDeviceCount(&ndev));
+    if (device < 0 || device >= ndev) return fail(PFM_E_ARG, "pfm_vad_create: bad device index");
+    HIP_TRY(hipSetDevice(device));
+    std::unique_ptr<pfm_vad> v(new pfm_vad());
+    v->cfg = *c;
+    v->device = device;
+    const int64_t I = c->input_dim, A = c->input_affine_dim, Lin = c->linear_dim, P = c->proj_dim, L = c->lorder,
+                  OA = c->output_affine_dim, O = c->output_dim;
+    v->add("encoder.in_linear1.linear.weight", {A, I});
+    v->add("encoder.in_linear1.linear.bias", {A});
+    v->add("encoder.in_linear2.linear.weight", {Lin, A});
+    v->add("encoder.in_linear2.linear.bias", {Lin});
+    for (int i = 0; i < c->fsmn_layers; ++i) {
+        const std::string p = "encoder.fsmn." + std::to_string(i);
+        v->add(p + ".linear.linear.weight", {P, Lin});
+        v->add(p + ".fsmn_block.conv_left.weight", {P, 1, L, 1});
+        v->add(p + ".affine.linear.weight", {Lin, P});
+        v->add(p + ".affine.linear.bias", {Lin});
+    }
+    v->add("encoder.out_linear1.linear.weight", {OA, Lin});
+    v->add("encoder.out_linear1.linear.bias", {OA});
+    v->add("encoder.out_linear2.linear.weight", {O, OA});
+    v->add("encoder.out_linear2.linear.bias", {O});
+    HIP_TRY(v->arena.ensure(v->elems * 4));
+    HIP_TRY(hipMemset(v->arena.p, 0, v->arena.bytes));
+    const size_t nc = (size_t)std::max(c->fsmn_layers, 1) * std::max(L - 1, (int64_t)1) * P;
+    HIP_TRY(v->cache.ensure(nc * 4));
+    HIP_TRY(v->ctmp.ensure((size_t)std::max(L - 1, (int64_t)1) * P * 4));
+    HIP_TRY(hipMemset(v->cache.p, 0, v->cache.bytes));
+    *out = v.release();
+    return PFM_OK;
+}
+
+int pfm_vad_set_weight(pfm_vad* v, const char* name, const void* host_ptr, int dtype, const int64_t* shape, int ndim) {
+    if (!v || !name || !host_ptr || (ndim > 0 && !shape)) return fail(PFM_E_ARG, "pfm_vad_set_weight: null argument");
+    if (dtype != PFM_F32) return fail(PFM_E_ARG, "pfm_vad_set_weight: weights are f32");
+    auto it = v->reg.find(name);
+    if (it == v->reg.end()) return fail(PFM_E_ARG, std::string("pfm_vad_set_weight: unknown key ") + name);
+    auto& w = it->second;
+    if ((int)w.shape.size() != ndim) return fail(PFM_E_ARG, std::string("pfm_vad_set_weight: rank of ") + name);
+    for (int i = 0; i < ndim; ++i)
+        if (shape[i] != w.shape[i]) return fail(PFM_E_ARG, std::string("pfm_vad_set_weight: shape of ") + name);
+    HIP_TRY(hipSetDevice(v->device));
+    HIP_TRY(hipMemcpy(v->arena.as<float>() + w.off, host_ptr, w.numel * 4, hipMemcpyHostToDevice));
+    if (!w.set) { w.set = true; --v->missing; }
+    return PFM_OK;
+}
+
+int pfm_vad_missing_weights(pfm_vad* v) { return v ? v->missing : -1; }
+
+int pfm_vad_reset(pfm_vad* v, void* stream) {
+    if (!v) return fail(PFM_E_ARG, "pfm_vad_reset: null argument");
+    HIP_TRY(hipSetDevice(v->device));
+    HIP_TRY(hipMemsetAsync(v->cache.p, 0, v->cache.bytes, (hipStream_t)stream));
+    return PFM_OK;
+}
+
+int pfm_vad_run(pfm_vad* v, void* stream, const float* feats, int T, float* p_sil, float* probs) {
+    if (!v || (T > 0 && (!feats || !p_sil))) return fail(PFM_E_ARG, "pfm_vad_run: null argument");
+    if (T < 0) return fail(PFM_E_ARG, "pfm_vad_run: bad T");
+    if (v->missing) return fail(PFM_E_STATE, "pfm_vad_run: weights not set");
+    if (T == 0) return PFM_OK;
+    const pfm_vad_config& c = v->cfg;
+    HIP_TRY(hipSetDevice(v->device));
+    hipStream_t st = (hipStream_t)stream;
+    if (T > v->capT) {
+        HIP_TRY(hipStreamSynchronize(st));
+        const size_t t = (size_t)T;
+        HIP_TRY(v->h1.ensure(t * std::max(c.input_affine_dim, c.output_affine_dim) * 4));
+        HIP_TRY(v->h2.ensure(t * c.linear_dim * 4));
+        HIP_TRY(v->pa.ensure(t * c.proj_dim * 4));
+        HIP_TRY(v->pb.ensure(t * c.proj_dim * 4));
+        HIP_TRY(v->o1.ensure(t * c.linear_dim * 4));
+        HIP_TRY(v->lg.ensure(t * c.output_dim * 4));
+        v->capT = T;
+    }
+    float* h1 = v->h1.as<float>();
+    float* h2 = v->h2.as<float>();
+    float* pa = v->pa.as<float>();
+    float* pb = v->pb.as<float>();
+    float* o1 = v->o1.as<float>();
+    // in_linear1 -> in_linear2 -> ReLU (encoder.py:264-266)
+    HIP_TRY(pfm_vad_dense(feats, c.input_dim, T, c.input_dim, v->p("encoder.in_linear1.linear.weight"),
+                          v->p("encoder.in_linear1.linear.bias"), c.input_affine_dim, 0, h1, c.input_affine_dim, st));
+    HIP_TRY(pfm_vad_dense(h1, c.input_affine_dim, T, c.input_affine_dim, v->p("encoder.in_linear2.linear.weight"),
+                          v->p("encoder.in_linear2.linear.bias"), c.linear_dim, 1, h2, c.linear_dim, st));
+    // FSMN stack: linear (no bias) -> memory block with cache -> affine -> ReLU (BasicBlock.forward :105-117)
+    const int Lm1 = std::max(c.lorder - 1, 1);
+    for (int i = 0; i < c.fsmn_layers; ++i) {
+        const std::string p = "encoder.fsmn." + std::to_string(i);
+        HIP_TRY(pfm_vad_dense(h2, c.linear_dim, T, c.linear_dim, v->p(p + ".linear.linear.weight"), nullptr, c.proj_dim,
+                              0, pa, c.proj_dim, st));
+        HIP_TRY(pfm_vad_fsmn(pa, T, c.proj_dim, v->cache.as<float>() + (size_t)i * Lm1 * c.proj_dim, v->ctmp.as<float>(),
+                             v->p(p + ".fsmn_block.conv_left.weight"), c.lorder, pb, st));
+        HIP_TRY(pfm_vad_dense(pb, c.proj_dim, T, c.proj_dim, v->p(p + ".affine.linear.weight"),
+                              v->p(p + ".affine.linear.bias"), c.linear_dim, 1, o1, c.linear_dim, st));
+        std::swap(h2, o1);
+    }
+    // out_linear1 -> out_linear2 -> softmax (encoder.py:268-272)
+    HIP_TRY(pfm_vad_dense(h2, c.linear_dim, T, c.linear_dim, v->p("encoder.out_linear1.linear.weight"),
+                          v->p("encoder.out_linear1.linear.bias"), c.output_affine_dim, 0, h1, c.output_affine_dim, st));
+    HIP_TRY(pfm_vad_dense(h1, c.output_affine_dim, T, c.output_affine_dim, v->p("encoder.out_linear2.linear.weight"),
+                          v->p("encoder.out_linear2.linear.bias"), c.output_dim, 0, v->lg.as<float>(), c.output_dim,
+                          st));
+    HIP_TRY(pfm_vad_softmax(v->lg.as<float>(), T, c.output_dim, p_sil, probs, st));
+    return PFM_OK;
+}
+
+int pfm_vad_fbank_raw(pfm_vad* v, void* stream, const float* wav, const int32_t* nsamp, int B, int S_max, float* fb,
+                      int N_cap) {
+    if (!v || !wav || !nsamp || !fb) return fail(PFM_E_ARG, "pfm_vad_fbank_raw: null argument");
+    if (B < 1 || S_max < 1 || N_cap < 1) return fail(PFM_E_ARG, "pfm_vad_fbank_raw: bad sizes");
+    if (pfm_fbank_nframes(S_max) > N_cap) return fail(PFM_E_ARG, "pfm_vad_fbank_raw: N_cap smaller than frames of S_max");
+    HIP_TRY(hipSetDevice(v->device));
+    if (!v->fb_ready) {
+        int rc = fbank_tables_build(v->fb_tab);
+        if (rc) return rc;
+        v->fb_ready = true;
+    }
+    HIP_TRY(pfm_fbank_raw_launch(wav, nsamp, B, S_max, v->fb_tab.as<unsigned char>(), fb, N_cap, (hipStream_t)stream));
+    return PFM_OK;
+}
+
+void pfm_vad_destroy(pfm_vad* v) {
+    if (!v) return;
+    (void)hipSetDevice(v->device);
+    (void)hipDeviceSynchronize();
+    delete v;
 }
 
 }  // extern "C"

@@ -106,15 +106,24 @@ class WavFrontendOnline(WavFrontend):
     """
     FL, FS = 400, 160
 
-    def __init__(self, cmvn_file: Optional[str] = None, **kwargs):
+    def __init__(self, cmvn_file: Optional[str] = None, lfr_m: int = 7, lfr_n: int = 6, **kwargs):
+        # the fbank options are checked by WavFrontend; LFR (m, n) is free here (ASR 7/6, FSMN-VAD 5/1)
         super().__init__(cmvn_file=cmvn_file, **kwargs)
-        self.lfr_m = 7
+        if lfr_m < 1 or lfr_n < 1:
+            raise ValueError("lfr_m / lfr_n must be >= 1")
+        self.lfr_m, self.lfr_n = int(lfr_m), int(lfr_n)
         self._cmvn_dev = {}
+
+    def output_size(self) -> int:
+        return 80 * self.lfr_m
 
     @staticmethod
     def init_cache(cache: dict) -> dict:
+        """init_cache (wav_frontend.py:468-476): carried samples, reserve_waveforms, splice frames; `waveforms`
+        = the samples of the last call's frames (cache["waveforms"], read by the VAD's decibel pass)."""
         cache.clear()
-        cache.update(input_cache=np.zeros((0,), np.float32), reserve_len=0, splice=None)
+        cache.update(input_cache=np.zeros((0,), np.float32), reserve=np.zeros((0,), np.float32), splice=None,
+                     waveforms=None)
         return cache
 
     def _cmvn_on(self, torch, dev):
@@ -177,26 +186,29 @@ class WavFrontendOnline(WavFrontend):
             rows_k = 0
             if nfr:
                 fbk = fb[k, :nfr]
-                waves_len = cache["reserve_len"] + len(used)
+                waves = np.concatenate([cache["reserve"], used])          # (:424)
+                cache["waveforms"] = waves
                 if cache["splice"] is None:
                     cache["splice"] = fbk[:1].repeat((self.lfr_m - 1) // 2, 1)
                 if nfr + cache["splice"].shape[0] >= self.lfr_m:
                     feats = torch.cat([cache["splice"], fbk])
                     idx, sidx = self._lfr_index(feats.shape[0], is_final)
-                    from_w = int((waves_len - self.FL) / self.FS + 1)
-                    minus = (self.lfr_m - 1) // 2 if cache["reserve_len"] == 0 else 0
-                    lo = min(max((sidx - minus) * self.FS, 0), waves_len)
-                    hi = min(max(from_w * self.FS, 0), waves_len)
-                    cache["reserve_len"] = max(0, hi - lo)
+                    from_w = int((len(waves) - self.FL) / self.FS + 1)
+                    minus = (self.lfr_m - 1) // 2 if cache["reserve"].size == 0 else 0
+                    lo = (sidx - minus) * self.FS
+                    cache["reserve"] = waves[lo:from_w * self.FS]                              # (:447-452)
+                    cache["waveforms"] = waves[:(from_w - 1) * self.FS + self.FL]               # (:453-456)
                     cache["splice"] = feats[sidx:].clone()
                     srcs.append(feats)
                     idxs.append(idx + offs)
                     offs += feats.shape[0]
                     rows_k = idx.shape[0]
                 else:
-                    cache["reserve_len"] = max(0, waves_len - (self.FL - self.FS))
+                    cache["reserve"] = waves[:-(self.FL - self.FS)]                              # (:458-461)
                     cache["splice"] = torch.cat([cache["splice"], fbk])
             elif is_final and cache["splice"] is not None:
+                # (:474-483): the frames of the call are the reserve (or none)
+                cache["waveforms"] = cache["reserve"] if cache["reserve"].size else np.zeros((0,), np.float32)
                 idx, _ = self._lfr_index(cache["splice"].shape[0], True)
                 srcs.append(cache["splice"])
                 idxs.append(idx + offs)

@@ -27,7 +27,8 @@ ABI_SYMBOLS = ("pfm_config_default", "pfm_config_sensevoice", "pfm_create", "pfm
                "pfm_missing_weights", "pfm_reserve", "pfm_run", "pfm_run_ctc", "pfm_op_ctc_collapse", "pfm_fbank", "pfm_lfr_frames", "pfm_last_error", "pfm_destroy", "pfm_op_gemm",
                "pfm_op_attention", "pfm_op_layernorm", "pfm_op_fsmn", "pfm_op_cif", "pfm_profile", "pfm_op_gemm_layernorm", "pfm_op_fsmn_bf16", "pfm_op_layernorm_bf16",
                "pfm_profile_read", "pfm_streams_create", "pfm_streams_reset", "pfm_stream_step",
-               "pfm_streams_destroy", "pfm_fbank_raw", "pfm_lfr_gather", "pfm_config_punc", "pfm_run_punc")
+               "pfm_streams_destroy", "pfm_fbank_raw", "pfm_lfr_gather", "pfm_config_punc", "pfm_run_punc", "pfm_vad_config_default", "pfm_vad_create",
+               "pfm_vad_set_weight", "pfm_vad_missing_weights", "pfm_vad_reset", "pfm_vad_run", "pfm_vad_destroy", "pfm_vad_fbank_raw")
 
 
 class PfmError(RuntimeError):
@@ -54,6 +55,11 @@ class PfmConfig(ctypes.Structure):
                    c.enc_sanm_shift, c.dec_sanm_shift, c.vocab_size, c.cif_l_order, c.cif_r_order,
                    c.cif_threshold, c.tail_threshold, c.smooth_factor, c.noise_threshold, c.ln_eps,
                    ARCH_PARAFORMER, 0, 0)
+
+
+class PfmVadConfig(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int32) for n in ("input_dim", "input_affine_dim", "fsmn_layers", "linear_dim", "proj_dim",
+                                               "lorder", "output_affine_dim", "output_dim")]
 
 
 _lib = None
@@ -109,6 +115,16 @@ def load_library(path: Optional[str] = None) -> ctypes.CDLL:
     lib.pfm_config_punc.argtypes = [ctypes.POINTER(PfmConfig)]
     lib.pfm_config_punc.restype = None
     lib.pfm_run_punc.argtypes = [vp, vp, i32, i32p, i32p, i32, i32, i32p, f32p]
+    lib.pfm_vad_config_default.argtypes = [ctypes.POINTER(PfmVadConfig)]
+    lib.pfm_vad_config_default.restype = None
+    lib.pfm_vad_create.argtypes = [ctypes.POINTER(PfmVadConfig), i32, ctypes.POINTER(vp)]
+    lib.pfm_vad_set_weight.argtypes = [vp, ctypes.c_char_p, vp, i32, ctypes.POINTER(ctypes.c_int64), i32]
+    lib.pfm_vad_missing_weights.argtypes = [vp]
+    lib.pfm_vad_reset.argtypes = [vp, vp]
+    lib.pfm_vad_run.argtypes = [vp, vp, f32p, i32, f32p, f32p]
+    lib.pfm_vad_fbank_raw.argtypes = [vp, vp, f32p, i32p, i32, i32, f32p, i32]
+    lib.pfm_vad_destroy.argtypes = [vp]
+    lib.pfm_vad_destroy.restype = None
     lib.pfm_streams_destroy.argtypes = [vp]
     lib.pfm_streams_destroy.restype = None
     for name in ABI_SYMBOLS:
@@ -487,3 +503,73 @@ def op_ctc_collapse(ids, olen, blank=0, L_cap=None):
     check(lib.pfm_op_ctc_collapse(_stream_ptr(torch, ids.device), _ptr(ids), T, _ptr(olen.to(torch.int32).contiguous()),
                                   B, int(blank), _ptr(tokens), L_cap, _ptr(ntok)), "pfm_op_ctc_collapse")
     return tokens, ntok
+
+
+class PfmVad:
+    """A pfm_vad object: the FSMN-VAD encoder of one stream (memory caches in HBM) on one device."""
+
+    def __init__(self, cfg, device: int = 0):   # FsmnVADConfig
+        import torch
+        if not torch.cuda.is_available():
+            raise PfmError("PfmVad needs a ROCm GPU; there is no CPU fallback")
+        self.torch, self.cfg, self.device = torch, cfg, int(device)
+        self.lib = load_library()
+        c = PfmVadConfig(cfg.input_dim, cfg.input_affine_dim, cfg.fsmn_layers, cfg.linear_dim, cfg.proj_dim,
+                         cfg.lorder, cfg.output_affine_dim, cfg.output_dim)
+        h = ctypes.c_void_p()
+        check(self.lib.pfm_vad_create(ctypes.byref(c), self.device, ctypes.byref(h)), "pfm_vad_create")
+        self.h = h
+
+    def __del__(self):
+        h = getattr(self, "h", None)
+        if h is not None and h.value:
+            try:
+                self.lib.pfm_vad_destroy(h)
+            except Exception:
+                pass
+            self.h = None
+
+    @property
+    def missing_weights(self) -> int:
+        return int(self.lib.pfm_vad_missing_weights(self.h))
+
+    def load_state_dict(self, sd):
+        for k, v in sd.items():
+            a = v.detach().cpu().float().numpy() if hasattr(v, "detach") else np.asarray(v, np.float32)
+            a = np.ascontiguousarray(a, dtype=np.float32)
+            shape = (ctypes.c_int64 * max(a.ndim, 1))(*a.shape)
+            check(self.lib.pfm_vad_set_weight(self.h, k.encode(), a.ctypes.data, PFM_F32, shape, a.ndim),
+                  f"pfm_vad_set_weight({k})")
+
+    def reset(self):
+        dev = self.torch.device("cuda", self.device)
+        check(self.lib.pfm_vad_reset(self.h, _stream_ptr(self.torch, dev)), "pfm_vad_reset")
+
+    def fbank_raw(self, wav, nsamp_host):
+        """Raw fbank frames [B, N_cap, 80] of the VAD's online frontend (pfm_vad_fbank_raw)."""
+        torch = self.torch
+        dev = torch.device("cuda", self.device)
+        wav = wav.to(device=dev, dtype=torch.float32).contiguous()
+        B, S = wav.shape
+        ns = torch.tensor([int(x) for x in nsamp_host], dtype=torch.int32).to(dev)
+        N_cap = max(1, 1 + (S - 400) // 160 if S >= 400 else 1)
+        fb = torch.empty((B, N_cap, 80), dtype=torch.float32, device=dev)
+        check(self.lib.pfm_vad_fbank_raw(self.h, _stream_ptr(torch, dev), _ptr(wav), _ptr(ns), B, S, _ptr(fb), N_cap),
+              "pfm_vad_fbank_raw")
+        return fb
+
+    lfr_gather = PfmEngine.lfr_gather
+
+    def run(self, feats, want_probs=False):
+        """feats [T, input_dim] f32 cuda -> p_sil [T] cuda (and probs [T, output_dim] on request)."""
+        torch = self.torch
+        dev = torch.device("cuda", self.device)
+        feats = feats.to(device=dev, dtype=torch.float32).contiguous()
+        if feats.dim() != 2 or feats.shape[1] != self.cfg.input_dim:
+            raise PfmError(f"feats must be [T, {self.cfg.input_dim}]")
+        T = feats.shape[0]
+        p = torch.empty((T,), dtype=torch.float32, device=dev)
+        probs = torch.empty((T, self.cfg.output_dim), dtype=torch.float32, device=dev) if want_probs else None
+        check(self.lib.pfm_vad_run(self.h, _stream_ptr(torch, dev), _ptr(feats), T, _ptr(p), _ptr(probs)),
+              "pfm_vad_run")
+        return (p, probs) if want_probs else p

@@ -21,7 +21,7 @@ from typing import Dict, Iterator, List, Tuple
 
 import numpy as np
 
-from .config import CTTransformerConfig, ParaformerConfig, SenseVoiceConfig
+from .config import CTTransformerConfig, FsmnVADConfig, ParaformerConfig, SenseVoiceConfig
 
 Shape = Tuple[int, ...]
 
@@ -35,6 +35,8 @@ def param_layout(cfg) -> List[Tuple[str, Shape, int]]:
         return sense_voice_layout(cfg)
     if isinstance(cfg, CTTransformerConfig):
         return ct_transformer_layout(cfg)
+    if isinstance(cfg, FsmnVADConfig):
+        return fsmn_vad_layout(cfg)
     D, F, K, I, V = cfg.d_model, cfg.ffn, cfg.kernel_size, cfg.input_size, cfg.vocab_size
     out: List[Tuple[str, Shape, int]] = []
 
@@ -131,6 +133,26 @@ def ct_transformer_layout(cfg: CTTransformerConfig) -> List[Tuple[str, Shape, in
     return out
 
 
+def fsmn_vad_layout(cfg: FsmnVADConfig) -> List[Tuple[str, Shape, int]]:
+    """FsmnVADStreaming state_dict keys (fsmn_vad_streaming/encoder.py:200-241): the FSMN encoder only."""
+    out: List[Tuple[str, Shape, int]] = []
+
+    def aff(name, o, i, bias=True):
+        out.append((f"{name}.linear.weight", (o, i), i))
+        if bias:
+            out.append((f"{name}.linear.bias", (o,), i))
+
+    aff("encoder.in_linear1", cfg.input_affine_dim, cfg.input_dim)
+    aff("encoder.in_linear2", cfg.linear_dim, cfg.input_affine_dim)
+    for i in range(cfg.fsmn_layers):
+        aff(f"encoder.fsmn.{i}.linear", cfg.proj_dim, cfg.linear_dim, bias=False)
+        out.append((f"encoder.fsmn.{i}.fsmn_block.conv_left.weight", (cfg.proj_dim, 1, cfg.lorder, 1), cfg.lorder))
+        aff(f"encoder.fsmn.{i}.affine", cfg.linear_dim, cfg.proj_dim)
+    aff("encoder.out_linear1", cfg.output_affine_dim, cfg.linear_dim)
+    aff("encoder.out_linear2", cfg.output_dim, cfg.output_affine_dim)
+    return out
+
+
 def _stream(seed: int, key: str) -> np.random.Generator:
     return np.random.Generator(np.random.PCG64([seed & 0xFFFFFFFF, zlib.crc32(key.encode())]))
 
@@ -162,3 +184,16 @@ def make_weights(cfg, seed: int = 0) -> Dict[str, np.ndarray]:
 
 def num_params(cfg) -> int:
     return int(sum(int(np.prod(s)) for _, s, _ in param_layout(cfg)))
+
+
+def vad_test_weights(cfg: FsmnVADConfig, seed: int = 0, sil_scale: float = -2000.0, sil_bias: float = 0.0):
+    """Synthetic FSMN-VAD weights for segment tests: the silence-pdf row of out_linear2 scaled (and its bias
+    shifted) so p(sil) follows the signal level across the speech/noise threshold; with plain random
+    weights p(sil) ~ 1/248 for every frame and the detector sees one all-speech segment."""
+    w = make_weights(cfg, seed)
+    wk, bk = "encoder.out_linear2.linear.weight", "encoder.out_linear2.linear.bias"
+    w[wk] = w[wk].copy()
+    w[wk][0] *= np.float32(sil_scale)
+    w[bk] = w[bk].copy()
+    w[bk][0] += np.float32(sil_bias)
+    return w

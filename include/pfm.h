@@ -154,6 +154,28 @@ void pfm_config_punc(pfm_config* c);   /* the released punc_ct-transformer (voca
 int pfm_run_punc(pfm_handle* h, void* stream, int mode, const int32_t* ids, const int32_t* lens, int B, int T,
                  int32_t* punc, float* logits);
 
+/* ---- FSMN-VAD (fsmn_vad_streaming/encoder.py:200-279; model.py:350-360 ComputeScores) ----
+ * One pfm_vad object = the FSMN encoder of one stream with its per-layer memory caches in HBM
+ * (cache["encoder"]); the VAD state machine (model.py:493-916) runs on the host over the posteriors. */
+typedef struct pfm_vad pfm_vad;
+typedef struct pfm_vad_config {
+    int32_t input_dim, input_affine_dim, fsmn_layers, linear_dim, proj_dim, lorder, output_affine_dim, output_dim;
+} pfm_vad_config;
+void pfm_vad_config_default(pfm_vad_config* c);   /* the released fsmn-vad: 400/140/4/250/128/20/140/248 */
+int pfm_vad_create(const pfm_vad_config* c, int device, pfm_vad** out);
+/* reference state_dict keys ("encoder.in_linear1.linear.weight", ...), f32 host data */
+int pfm_vad_set_weight(pfm_vad* v, const char* name, const void* host_ptr, int dtype, const int64_t* shape, int ndim);
+int pfm_vad_missing_weights(pfm_vad* v);
+/* zero the FSMN caches: a new stream (init_cache) */
+int pfm_vad_reset(pfm_vad* v, void* stream);
+/* One chunk: feats [T, input_dim] f32 device (WavFrontendOnline LFR rows) -> p_sil [T] f32 device (softmax
+ * posterior of pdf 0), probs optional [T, output_dim] (NULL to skip). The caches advance by the chunk. */
+int pfm_vad_run(pfm_vad* v, void* stream, const float* feats, int T, float* p_sil, float* probs);
+/* pfm_fbank_raw on the VAD object (its online frontend runs without a model handle). */
+int pfm_vad_fbank_raw(pfm_vad* v, void* stream, const float* wav, const int32_t* nsamp, int B, int S_max,
+                      float* fb, int N_cap);
+void pfm_vad_destroy(pfm_vad* v);
+
 /* ---- Streaming Paraformer (ParaformerStreaming, paraformer_streaming/model.py:435-656) ----
  * A pfm_streams object holds `slots` independent streams whose chunk caches live in HBM:
  * the encoder input overlap (cache["encoder"]["feats"]), the per-layer encoder K/V look-back

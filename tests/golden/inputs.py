@@ -30,3 +30,14 @@ def waveform(seed: int, n: int, fs: int = 16000):
 def token_list(vocab: int):
     """Synthetic CharTokenizer vocabulary: <blank>,<s>,</s>, CJK chars, <unk>."""
     return ["<blank>", "<s>", "</s>"] + [chr(0x4E00 + i) for i in range(vocab - 4)] + ["<unk>"]
+
+
+def vad_waveform(seed: int, seconds: float, gaps):
+    """Seeded 16 kHz signal for the VAD goldens: the tone+noise test signal with quiet gaps (N(0, 0.002),
+    s16-quantised) at `gaps` [(beg_s, end_s)]."""
+    x = waveform(seed=seed, n=int(seconds * 16000)).copy()
+    rng = np.random.default_rng(seed + 100)
+    for b, e in gaps:
+        i0, i1 = int(b * 16000), int(e * 16000)
+        x[i0:i1] = np.round(rng.normal(0.0, 0.002, i1 - i0) * 32768.0).clip(-32768, 32767) / 32768.0
+    return x.astype(np.float32)

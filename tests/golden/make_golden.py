@@ -617,6 +617,97 @@ def save_punc():
     np.savez_compressed(f"{HERE}/punc_tiny.npz", **arrays)
 
 
+VAD_SIL_BIAS = 0.0      # added to out_linear2.bias[0] (the silence pdf) of the synthetic VAD weights
+VAD_SIL_SCALE = -2000.0  # out_linear2.weight[0] scale
+
+
+def vad_weights(cfg, seed=0, sil_bias=None, sil_scale=None):
+    """Synthetic FSMN-VAD weights whose silence logit is amplified (row 0 of out_linear2 x VAD_SIL_SCALE) so
+    that p(sil) separates the loud and quiet parts of the test signal around the speech/noise threshold
+    (plain random weights give p(sil) ~ 1/248 everywhere: one all-speech segment)."""
+    from funasr_amd.weights import vad_test_weights
+    return vad_test_weights(cfg, seed, VAD_SIL_SCALE if sil_scale is None else sil_scale,
+                            VAD_SIL_BIAS if sil_bias is None else sil_bias)
+
+
+VAD_CASES = {   # name: (seed, seconds, gaps, calls (samples per inference call; None = one call))
+    "v1": (51, 12.0, [(2.0, 4.0), (6.5, 7.7), (10.0, 12.0)], None),
+    "v2": (52, 70.0, [(0.0, 1.5), (20.0, 23.0), (50.0, 52.5), (61.0, 62.0)], None),
+}
+
+
+def build_vad_ref(cfg, sil_bias=None, sil_scale=None):
+    import funasr.models.fsmn_vad_streaming.encoder  # noqa: F401
+    import funasr.models.fsmn_vad_streaming.model  # noqa: F401
+    m = tables.model_classes["FsmnVADStreaming"](**cfg.reference_kwargs())
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in vad_weights(cfg, 0, sil_bias, sil_scale).items()}, strict=True)
+    m.eval()
+    return m
+
+
+def vad_frontend():
+    import funasr.frontends.wav_frontend as wf
+    from oracle import fbank_ref
+
+    def kfbank(w, **kw):
+        return torch.from_numpy(fbank_ref.fbank(w[0].numpy().astype(np.float32) / np.float32(32768.0)))
+
+    sys.modules["torchaudio.compliance.kaldi"].fbank = kfbank
+    wf.kaldi.fbank = kfbank
+    return wf.WavFrontendOnline(cmvn_file=None, fs=16000, window="hamming", n_mels=80, frame_length=25,
+                                frame_shift=10, lfr_m=5, lfr_n=1, dither=0.0)
+
+
+def run_vad_ref(m, front, wav, calls=None):
+    """FsmnVADStreaming.inference (offline: chunk_size 60000 ms) -> (segments, silence posteriors, decibels)."""
+    scores, decib = [], []
+    cs, cd = m.ComputeScores, m.ComputeDecibel
+
+    def cscores(feats, cache={}):
+        cs(feats, cache=cache)
+        scores.append(cache["stats"].scores[0, -feats.shape[1]:, 0].numpy().copy())
+
+    def cdecib(cache={}):
+        n0 = len(cache["stats"].decibel)
+        cd(cache=cache)
+        decib.append(np.asarray(cache["stats"].decibel[n0:], np.float64))
+
+    m.ComputeScores, m.ComputeDecibel = cscores, cdecib
+    try:
+        cache = {}
+        with torch.no_grad():
+            res, _ = m.inference([torch.from_numpy(wav.copy())], key=["v"], frontend=front, cache=cache,
+                                 device="cpu", data_type="sound")
+    finally:
+        m.ComputeScores, m.ComputeDecibel = cs, cd
+    return (res[0]["value"], np.concatenate(scores), np.concatenate(decib),
+            np.cumsum([0] + [len(x) for x in scores]).astype(np.int32),
+            np.cumsum([0] + [len(x) for x in decib]).astype(np.int32))
+
+
+def save_vad():
+    """FsmnVADStreaming goldens (released FSMN dims, synthetic weights, silence bias VAD_SIL_BIAS): the
+    reference inference() segments [[beg_ms, end_ms], ...] of seeded waveforms with quiet gaps, plus the
+    per-frame silence posteriors and decibels its state machine consumed."""
+    from funasr_amd.config import fsmn_vad
+    cfg = fsmn_vad()
+    m = build_vad_ref(cfg)
+    front = vad_frontend()
+    out, arrays = {}, {}
+    for name, (seed, sec, gaps, calls) in VAD_CASES.items():
+        from tests.golden.inputs import vad_waveform
+        wav = vad_waveform(seed, sec, gaps)
+        segs, p0, db, p_off, d_off = run_vad_ref(m, front, wav, calls)
+        arrays[f"{name}_p0_off"], arrays[f"{name}_db_off"] = p_off, d_off
+        out[name] = dict(seed=seed, seconds=sec, gaps=gaps, segments=segs, sil_bias=VAD_SIL_BIAS)
+        arrays[f"{name}_p0"] = p0.astype(np.float32)
+        arrays[f"{name}_db"] = db.astype(np.float64)
+        print(name, segs, "p0 mean", float(p0.mean()), "frames", len(p0))
+    with open(f"{HERE}/vad.json", "w") as f:
+        json.dump(out, f, indent=1)
+    np.savez_compressed(f"{HERE}/vad.npz", **arrays)
+
+
 if __name__ == "__main__" and len(sys.argv) > 1:
     torch.manual_seed(0)
     for part in sys.argv[1:]:

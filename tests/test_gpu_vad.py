@@ -1,0 +1,95 @@
+"""FSMN-VAD on the GPU: pfm_vad_run (the FSMN encoder with HBM memory caches) vs the
+oracle (oracle/vad_ref.py, pinned to the reference posteriors), the online frontend at LFR (5, 1) vs the
+oracle frontend, and FsmnVADStreaming.inference / AutoModel segments vs the reference inference() goldens.
+
+Tolerances: posteriors on identical features within 1e-4 (the test weights amplify the silence logit
+x2000, see funasr_amd.weights.vad_test_weights); frontend rows within 2e-4 (log-mel, as
+tests/test_gpu_frontend.py); segments exact.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from funasr_amd.config import fsmn_vad  # noqa: E402
+from funasr_amd.weights import vad_test_weights  # noqa: E402
+from tests.golden.inputs import vad_waveform  # noqa: E402
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+@pytest.fixture(scope="module")
+def vad():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from funasr_amd.runtime import PfmEngine, PfmVad
+    from funasr_amd.config import paraformer_tiny
+    cfg = fsmn_vad()
+    w = vad_test_weights(cfg, 0)
+    v = PfmVad(cfg, 0)
+    v.load_state_dict(w)
+    eng = PfmEngine(paraformer_tiny(), 0)   # any handle serves the frontend ops
+    return cfg, v, w, eng
+
+
+def test_vad_encoder_chunks_vs_oracle(vad):
+    """Three chunks through one stream (caches carried across chunks, including a 7-row chunk shorter
+    than the memory order 20)."""
+    from oracle.vad_ref import vad_forward
+    cfg, v, w, _ = vad
+    rng = np.random.default_rng(2)
+    v.reset()
+    cache = None
+    for T in (300, 7, 129):
+        x = (rng.standard_normal((T, cfg.input_dim)) * 3).astype(np.float32)
+        p, probs = v.run(torch.from_numpy(x).cuda(), want_probs=True)
+        torch.cuda.synchronize()
+        ref, cache = vad_forward(x, w, cfg, cache)
+        np.testing.assert_allclose(probs.cpu().numpy(), ref.numpy(), atol=1e-4, rtol=0)
+        np.testing.assert_allclose(p.cpu().numpy(), ref[:, 0].numpy(), atol=1e-4, rtol=0)
+
+
+@pytest.mark.parametrize("name", ["v1", "v2"])
+def test_vad_frontend_and_posteriors(vad, name):
+    """Online frontend (LFR 5/1) rows vs the oracle frontend; posteriors of those rows vs the oracle."""
+    from funasr_amd.frontend import WavFrontendOnline
+    from oracle.streaming_ref import FrontendOnline
+    from oracle.vad_ref import vad_forward
+    cfg, v, w, eng = vad
+    gj = json.load(open(f"{GOLD}/vad.json"))[name]
+    wav = vad_waveform(gj["seed"], gj["seconds"], gj["gaps"])
+    fe, fo = WavFrontendOnline(cmvn_file=None, lfr_m=5, lfr_n=1), FrontendOnline(None, lfr_m=5, lfr_n=1)
+    stride = 60000 * 16
+    n = len(wav) // stride + 1
+    cache, fc = None, {}
+    v.reset()
+    for i in range(n):
+        seg, fin = wav[i * stride:(i + 1) * stride], i == n - 1
+        got = fe.step(eng, [(seg, fin, fc)])[0]
+        ref = fo(seg, fin)
+        assert got.shape[0] == ref.shape[0]
+        assert np.abs(got.cpu().numpy() - ref).max() < 2e-4
+        p = v.run(got)
+        torch.cuda.synchronize()
+        pr, cache = vad_forward(got.cpu().numpy(), w, cfg, cache)
+        np.testing.assert_allclose(p.cpu().numpy(), pr[:, 0].numpy(), atol=1e-4, rtol=0)
+
+
+@pytest.mark.parametrize("name", ["v1", "v2"])
+def test_automodel_vad_segments_vs_reference(name):
+    from funasr_amd.auto_model import AutoModel
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    cfg = fsmn_vad()
+    am = AutoModel(model="FsmnVADStreaming", model_conf={}, device="cuda", mode="exact",
+                   frontend_conf=dict(lfr_m=5, lfr_n=1), **cfg.reference_kwargs())
+    am.model.load_state_dict(vad_test_weights(cfg, 0))
+    gj = json.load(open(f"{GOLD}/vad.json"))[name]
+    wav = vad_waveform(gj["seed"], gj["seconds"], gj["gaps"])
+    res = am.generate(input=wav, key=name)
+    assert res[0]["key"] == name
+    assert res[0]["value"] == gj["segments"]

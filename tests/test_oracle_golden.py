@@ -255,3 +255,68 @@ def test_punc_text_pipeline_vs_reference():
         assert [s.tolist() for s in seen] == [c[0].tolist() for c in calls], name
         assert text == gj["text"], name
         assert list(punc_array) == gj["punc_array"], name
+
+
+# ---------------------------------------------------------------- FSMN-VAD (§8f row 1)
+@pytest.mark.parametrize("name", ["v1", "v2"])
+def test_vad_state_machine_vs_reference(name):
+    """funasr_amd.vad.VadDetector (the host state machine of FsmnVADStreaming) fed the reference's own
+    per-chunk silence posteriors and decibels reproduces the reference inference() segments exactly."""
+    import json
+    from funasr_amd.config import fsmn_vad
+    from funasr_amd.vad import VadDetector
+    gj = json.load(open(f"{GOLD}/vad.json"))[name]
+    g = np.load(f"{GOLD}/vad.npz")
+    p0, po = g[f"{name}_p0"], g[f"{name}_p0_off"]
+    db, do = g[f"{name}_db"], g[f"{name}_db_off"]
+    det = VadDetector(fsmn_vad().vad_opts)
+    segs = []
+    for c in range(len(po) - 1):
+        fin = c == len(po) - 2
+        det.decibel.extend(db[do[c]:do[c + 1]].tolist())
+        det.add_scores(p0[po[c]:po[c + 1]])
+        det.detect_chunk(int(po[c + 1] - po[c]), fin)
+        segs.extend(det.segments(fin, False))
+    assert segs == gj["segments"]
+
+
+def test_vad_decibels_vs_reference():
+    """VadDetector.add_waveform (ComputeDecibel) on the v1 signal's frontend waveform: the reference's
+    per-frame decibels (one call covers the whole 12 s: waveforms = the samples of its frames)."""
+    import json
+    from funasr_amd.config import fsmn_vad
+    from funasr_amd.vad import VadDetector
+    from tests.golden.inputs import vad_waveform
+    gj = json.load(open(f"{GOLD}/vad.json"))["v1"]
+    g = np.load(f"{GOLD}/vad.npz")
+    wav = vad_waveform(gj["seed"], gj["seconds"], gj["gaps"])
+    n = len(g["v1_db"])
+    det = VadDetector(fsmn_vad().vad_opts)
+    det.add_waveform(wav[:(n - 1) * 160 + 400])
+    np.testing.assert_allclose(np.asarray(det.decibel), g["v1_db"], rtol=0, atol=1e-9)
+
+
+@pytest.mark.parametrize("name", ["v1", "v2"])
+def test_vad_oracle_vs_reference(name):
+    """oracle/vad_ref.vad_forward on oracle online-frontend features (LFR 5/1, 60 s chunks, carried FSMN
+    caches) reproduces the reference's silence posteriors of every frame."""
+    import json
+    from funasr_amd.config import fsmn_vad
+    from funasr_amd.weights import vad_test_weights
+    from oracle.streaming_ref import FrontendOnline
+    from oracle.vad_ref import vad_forward
+    from tests.golden.inputs import vad_waveform
+    cfg = fsmn_vad()
+    gj = json.load(open(f"{GOLD}/vad.json"))[name]
+    g = np.load(f"{GOLD}/vad.npz")
+    wav = vad_waveform(gj["seed"], gj["seconds"], gj["gaps"])
+    w = vad_test_weights(cfg, 0)
+    fe = FrontendOnline(None, lfr_m=5, lfr_n=1)
+    stride = 60000 * 16
+    n = len(wav) // stride + 1
+    cache, p0 = None, []
+    for i in range(n):
+        f = fe(wav[i * stride:(i + 1) * stride], i == n - 1)
+        pr, cache = vad_forward(f, w, cfg, cache)
+        p0.append(pr[:, 0].numpy())
+    np.testing.assert_allclose(np.concatenate(p0), g[f"{name}_p0"], atol=2e-5, rtol=0)
