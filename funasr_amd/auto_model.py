@@ -55,6 +55,15 @@ _CHARS = string.ascii_letters + string.digits
 _LIST_EXT = (".scp", ".txt", ".json", ".jsonl", ".text")
 
 
+def _load_audio(item) -> np.ndarray:
+    if isinstance(item, str):
+        from .frontend import read_wav
+        return read_wav(item)
+    if hasattr(item, "detach"):
+        item = item.detach().cpu().numpy()
+    return np.asarray(item, dtype=np.float32).reshape(-1)
+
+
 def _rand_key() -> str:
     return "rand_key_" + "".join(random.choice(_CHARS) for _ in range(13))
 
@@ -134,12 +143,47 @@ def load_pretrained_state(path: str) -> Dict[str, torch.Tensor]:
     return src
 
 
+def merge_vad(vad_result, max_length=15000, min_length=0):
+    """utils/vad_utils.py merge_vad (SenseVoice `merge_vad=True`): join consecutive VAD segments up to
+    max_length ms."""
+    if len(vad_result) <= 1:
+        return vad_result
+    steps = sorted(set([t[0] for t in vad_result] + [t[1] for t in vad_result]))
+    if not steps:
+        return []
+    out, bg = [], 0
+    for i in range(len(steps) - 1):
+        t = steps[i]
+        if steps[i + 1] - bg < max_length:
+            continue
+        if t - bg > min_length:
+            out.append([bg, t])
+        bg = t
+    out.append([bg, steps[-1]])
+    return out
+
+
 class AutoModel:
+    """funasr.auto.auto_model.AutoModel on the HIP path: model / vad_model / punc_model are built from
+    registered names or local model dirs (auto_model.py:110-170); generate() runs inference_with_vad when
+    a VAD model is present (:300-306)."""
+
     def __init__(self, **kwargs):
-        if kwargs.get("vad_model") or kwargs.get("punc_model") or kwargs.get("spk_model"):
-            raise NotImplementedError("VAD / punctuation / speaker pipelines are SURVEY §8f next rows")
+        if kwargs.get("spk_model"):
+            raise NotImplementedError("speaker diarisation (spk_model) is out of scope (SURVEY §7)")
         self.model, self.kwargs = self.build_model(**kwargs)
-        self.vad_model = None
+        self.vad_model, self.vad_kwargs = self._sub_model(kwargs, "vad")
+        self.punc_model, self.punc_kwargs = self._sub_model(kwargs, "punc")
+
+    def _sub_model(self, kwargs, kind):
+        name = kwargs.get(f"{kind}_model")
+        if name is None:
+            return None, {}
+        sub = dict(kwargs.get(f"{kind}_kwargs") or {})
+        sub["model"] = name
+        sub["device"] = self.kwargs["device"]
+        sub.setdefault("mode", kwargs.get("mode", "exact"))
+        return self.build_model(**sub)
 
     @staticmethod
     def build_model(**kwargs):
@@ -183,7 +227,85 @@ class AutoModel:
         return self.model(*args, kwargs)
 
     def generate(self, input, input_len=None, **cfg):
-        return self.inference(input, input_len=input_len, **cfg)
+        if self.vad_model is None:
+            return self.inference(input, input_len=input_len, **cfg)
+        return self.inference_with_vad(input, input_len=input_len, **cfg)
+
+    def inference_with_vad(self, input, input_len=None, **cfg):
+        """auto_model.py:378-673 without the speaker branch: VAD segments per input -> segments sorted by
+        duration and packed into batches of <= batch_size_s seconds of audio (segments longer than
+        batch_size_threshold_s go alone) -> ASR -> original order restored -> texts joined with " ",
+        timestamps shifted by the segment start, other fields summed -> punctuation of the joined text."""
+        kwargs = dict(self.kwargs)
+        kwargs.update(cfg)
+        vad_kw = dict(self.vad_kwargs)
+        vad_kw.update(cfg)
+        res = self.inference(input, input_len=input_len, model=self.vad_model, kwargs=vad_kw)
+        if cfg.get("merge_vad", False):
+            for r in res:
+                r["value"] = merge_vad(r["value"], kwargs.get("merge_length_s", 15) * 1000)
+        batch_ms = max(int(kwargs.get("batch_size_s", 300)) * 1000, 1)
+        thres_ms = int(kwargs.get("batch_size_threshold_s", 60)) * 1000
+        keys, items = prepare_data_iterator(input, input_len=input_len, data_type=kwargs.get("data_type"))
+        asr_kw = dict(kwargs)
+        asr_kw.pop("batch_size_s", None)
+        asr_kw["dp"] = False   # the segment batches of one input stay on this rank
+        out = []
+        for i, r in enumerate(res):
+            key, segs = r["key"], r["value"]
+            speech = _load_audio(items[i])
+            n = len(segs)
+            order = sorted(range(n), key=lambda j: segs[j][1] - segs[j][0])
+            if n == 0:
+                out.append({"key": key, "text": "", "timestamp": []})
+                continue
+            bsz = max(batch_ms, segs[order[0]][1] - segs[order[0]][0])
+            results_sorted, beg, end, max_len = [], 0, 1, 0
+            for j in range(n):
+                slen = segs[order[j]][1] - segs[order[j]][0]
+                if j < n - 1 and slen < thres_ms and max(max_len, slen) * (j + 1 - beg) < bsz:
+                    max_len = max(max_len, slen)
+                    end += 1
+                    continue
+                batch = []
+                for jj in order[beg:end]:   # slice_padding_audio_samples (vad_utils.py:21-32)
+                    b0 = int(segs[jj][0] * 16)
+                    b1 = min(int(segs[jj][1] * 16), len(speech))
+                    batch.append(speech[b0:b1])
+                asr_kw["batch_size"] = len(batch)
+                results_sorted.extend(self.inference(batch, input_len=None, model=self.model, kwargs=asr_kw))
+                beg, end, max_len = end, end + 1, slen
+            if len(results_sorted) != n:
+                out.append({"key": key, "text": "", "timestamp": []})
+                continue
+            restored = [None] * n
+            for j in range(n):
+                restored[order[j]] = results_sorted[j]
+            result: Dict[str, Any] = {}
+            for j in range(n):
+                for k, v in restored[j].items():
+                    if k.startswith("timestamp"):
+                        result.setdefault(k, [])
+                        for t in v:
+                            t[0] += segs[j][0]
+                            t[1] += segs[j][0]
+                        result[k].extend(v)
+                    elif "text" in k:
+                        result[k] = v if k not in result else result[k] + " " + v
+                    else:
+                        result[k] = v if k not in result else result[k] + v
+            if not len(result["text"].strip()):
+                continue
+            if self.punc_model is not None:
+                punc_kw = dict(self.punc_kwargs)
+                punc_kw.update(cfg)
+                pres = self.inference(result["text"], model=self.punc_model, kwargs=punc_kw)
+                if kwargs.get("return_raw_text", False):
+                    result["raw_text"] = result["text"]
+                result["text"] = pres[0]["text"]
+            result["key"] = key
+            out.append(result)
+        return out
 
     def inference(self, input, input_len=None, model=None, kwargs=None, key=None, **cfg):
         kwargs = dict(self.kwargs if kwargs is None else kwargs)

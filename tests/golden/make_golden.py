@@ -708,6 +708,55 @@ def save_vad():
     np.savez_compressed(f"{HERE}/vad.npz", **arrays)
 
 
+def save_vad_pipeline():
+    """Reference AutoModel(model=Paraformer tiny, vad_model=FsmnVADStreaming, punc_model=CTTransformer tiny)
+    .generate(input=waveform): inference_with_vad (VAD segments -> sorted / batched ASR -> restored order ->
+    joined text -> punctuation). Synthetic weights: make_weights seed 0 (ASR, punc), vad_test_weights (VAD)."""
+    import funasr.tokenizer.char_tokenizer  # noqa: F401
+    import funasr.frontends.wav_frontend as wf
+    import funasr.models.ct_transformer.model  # noqa: F401
+    import funasr.models.fsmn_vad_streaming.model  # noqa: F401
+    import funasr.models.fsmn_vad_streaming.encoder  # noqa: F401
+    from funasr.auto.auto_model import AutoModel
+    from funasr_amd.config import ct_transformer_tiny, fsmn_vad
+    from funasr_amd.weights import vad_test_weights
+    from oracle import fbank_ref
+    from tests.golden.inputs import vad_waveform
+
+    def kfbank(w, **kw):
+        return torch.from_numpy(fbank_ref.fbank(w[0].numpy().astype(np.float32) / np.float32(32768.0)))
+
+    sys.modules["torchaudio.compliance.kaldi"].fbank = kfbank
+    wf.kaldi.fbank = kfbank
+    cfg, pcfg, vcfg = paraformer_tiny(), ct_transformer_tiny(), fsmn_vad()
+    fconf = dict(fs=16000, window="hamming", n_mels=80, frame_length=25, frame_shift=10, dither=0.0)
+    vad_kwargs = dict(model_conf={}, frontend="WavFrontendOnline", frontend_conf=dict(fconf, lfr_m=5, lfr_n=1),
+                      disable_update=True, **vcfg.reference_kwargs())
+    punc_kwargs = dict(model_conf={}, tokenizer="CharTokenizer",
+                       tokenizer_conf=dict(token_list=token_list(pcfg.vocab_size), unk_symbol="<unk>"),
+                       disable_update=True, **pcfg.reference_kwargs())
+    am = AutoModel(model="Paraformer", model_conf=dict(ctc_weight=0.0, predictor_bias=1),
+                   device="cpu", ncpu=4, disable_update=True, disable_pbar=True, disable_log=True,
+                   tokenizer="CharTokenizer", tokenizer_conf=dict(token_list=token_list(cfg.vocab_size)),
+                   frontend="WavFrontend", frontend_conf=dict(fconf, lfr_m=7, lfr_n=6, cmvn_file=CMVN),
+                   vad_model="FsmnVADStreaming", vad_kwargs=vad_kwargs, punc_model="CTTransformer",
+                   punc_kwargs=punc_kwargs, **cfg.reference_kwargs())
+    am.model.load_state_dict({k: torch.from_numpy(v) for k, v in make_weights(cfg, 0).items()}, strict=True)
+    am.vad_model.load_state_dict({k: torch.from_numpy(v) for k, v in vad_test_weights(vcfg, 0).items()},
+                                 strict=True)
+    am.punc_model.load_state_dict({k: torch.from_numpy(v) for k, v in make_weights(pcfg, 0).items()}, strict=True)
+    out = {}
+    for name, bs in (("v1", 300), ("v1_b4", 4)):
+        gj = VAD_CASES["v1"]
+        wav = vad_waveform(gj[0], gj[1], gj[2])
+        res = am.generate(input=wav, batch_size_s=bs)   # (a key= kwarg collides inside inference_with_vad)
+        out[name] = dict(batch_size_s=bs, result=[{k: (v.tolist() if hasattr(v, "tolist") else v)
+                                                   for k, v in r.items()} for r in res])
+        print(name, out[name]["result"][0]["text"][:80])
+    with open(f"{HERE}/vad_pipeline.json", "w", encoding="utf-8") as f:
+        json.dump(out, f, ensure_ascii=False, indent=1)
+
+
 if __name__ == "__main__" and len(sys.argv) > 1:
     torch.manual_seed(0)
     for part in sys.argv[1:]:
