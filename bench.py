@@ -159,6 +159,48 @@ def punc_leg(args, dev, torch, make_weights) -> dict:
     return res
 
 
+def long_audio_leg(args, sd, cfg) -> dict:
+    """AutoModel(model=Paraformer-large, vad_model=FSMN-VAD, punc_model=CT-Transformer).generate(wav): the
+    whole file-transcription pipeline (inference_with_vad) on one synthetic long waveform with quiet gaps."""
+    import torch
+    from funasr_amd.auto_model import AutoModel
+    from funasr_amd.config import ct_transformer, fsmn_vad
+    from funasr_amd.weights import make_weights, vad_test_weights
+    from tests.golden.inputs import token_list, vad_waveform
+    S = args.long_audio_s
+    gaps = [(t + 7.0, t + 8.2) for t in range(0, S - 10, 11)]
+    wav = vad_waveform(61, float(S), gaps)
+    pcfg, vcfg = ct_transformer(), fsmn_vad()
+    am = AutoModel(model="Paraformer", model_conf=dict(ctc_weight=0.0, predictor_bias=1), device="cuda",
+                   mode=args.mode, tokenizer_conf=dict(token_list=token_list(cfg.vocab_size)),
+                   vad_model="FsmnVADStreaming", vad_kwargs=dict(model_conf={}, frontend="WavFrontendOnline",
+                                                                  frontend_conf=dict(lfr_m=5, lfr_n=1),
+                                                                  **vcfg.reference_kwargs()),
+                   punc_model="CTTransformer", punc_kwargs=dict(model_conf={}, tokenizer="CharTokenizer",
+                                                                tokenizer_conf=dict(token_list=token_list(
+                                                                    pcfg.vocab_size)), **pcfg.reference_kwargs()),
+                   batch_size_s=300, **cfg.reference_kwargs())
+    am.model.load_state_dict(sd)
+    am.vad_model.load_state_dict(vad_test_weights(vcfg, 0))
+    am.punc_model.load_state_dict(make_weights(pcfg, args.seed))
+    am.generate(input=wav[:16000 * 20])   # warmup (workspaces, first-call setup)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    res = am.generate(input=wav)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    t1 = time.perf_counter()
+    vres = am.inference(wav, model=am.vad_model, kwargs=dict(am.vad_kwargs))
+    torch.cuda.synchronize()
+    dv = time.perf_counter() - t1
+    return {"workload": f"{S} s synthetic 16 kHz waveform with quiet gaps: FSMN-VAD (synthetic weights tuned to "
+                        f"segment it) -> Paraformer-large ({args.mode}) on duration-sorted batches of <= 300 s -> "
+                        f"CT-Transformer punctuation (released dims)",
+            "value": round(S / dt, 1), "unit": "audio-sec/sec", "wall_s": round(dt, 3),
+            "segments": len(vres[0]["value"]), "vad_only_value": round(S / dv, 1),
+            "text_chars": len(res[0]["text"]) if res else 0}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -175,6 +217,8 @@ def main():
                     help="600 ms chunks per stream in the streaming (config C5) leg (0 = skip)")
     ap.add_argument("--stream-batch", type=int, default=64, help="concurrent streams of the C5 serving line")
     ap.add_argument("--punc-steps", type=int, default=5, help="timed CT-Transformer punctuation calls (0 = skip)")
+    ap.add_argument("--long-audio-s", type=int, default=300,
+                    help="seconds of synthetic audio for the VAD + ASR + punctuation leg (0 = skip)")
     args = ap.parse_args()
 
     import torch
@@ -353,6 +397,10 @@ def main():
     # ---- CT-Transformer punctuation: 64 word sequences x 200 words per pfm_run_punc
     if rank == 0 and world == 1 and args.punc_steps > 0:
         out["punctuation"] = punc_leg(args, dev, torch, make_weights)
+
+    # ---- VAD-segmented long-audio transcription: FSMN-VAD -> ASR -> punctuation
+    if rank == 0 and world == 1 and args.long_audio_s > 0:
+        out["long_audio"] = long_audio_leg(args, sd, cfg)
 
     # ---- CPU baseline: the oracle torch-CPU restatement on a bounded sample (rank 0, N=1 only)
     if rank == 0 and world == 1 and args.cpu_utts > 0:
