@@ -28,7 +28,8 @@ ABI_SYMBOLS = ("pfm_config_default", "pfm_config_sensevoice", "pfm_create", "pfm
                "pfm_op_attention", "pfm_op_layernorm", "pfm_op_fsmn", "pfm_op_cif", "pfm_profile", "pfm_op_gemm_layernorm", "pfm_op_fsmn_bf16", "pfm_op_layernorm_bf16",
                "pfm_profile_read", "pfm_streams_create", "pfm_streams_reset", "pfm_stream_step",
                "pfm_streams_destroy", "pfm_fbank_raw", "pfm_lfr_gather", "pfm_config_punc", "pfm_run_punc", "pfm_vad_config_default", "pfm_vad_create",
-               "pfm_vad_set_weight", "pfm_vad_missing_weights", "pfm_vad_reset", "pfm_vad_run", "pfm_vad_destroy", "pfm_vad_fbank_raw")
+               "pfm_vad_set_weight", "pfm_vad_missing_weights", "pfm_vad_reset", "pfm_vad_run", "pfm_vad_destroy", "pfm_vad_fbank_raw",
+               "pfm_vad_opts_default", "pfm_vad_detector_create", "pfm_vad_detector_push", "pfm_vad_detector_destroy")
 
 
 class PfmError(RuntimeError):
@@ -60,6 +61,16 @@ class PfmConfig(ctypes.Structure):
 class PfmVadConfig(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int32) for n in ("input_dim", "input_affine_dim", "fsmn_layers", "linear_dim", "proj_dim",
                                                "lorder", "output_affine_dim", "output_dim")]
+
+
+class PfmVadOpts(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int32) for n in ("detect_mode", "max_end_silence_time", "max_start_silence_time",
+                                               "window_size_ms", "sil_to_speech_time_thres",
+                                               "speech_to_sil_time_thres", "do_extend", "lookback_time_start_point",
+                                               "lookahead_time_end_point", "max_single_segment_time",
+                                               "noise_frame_num_used_for_snr", "frame_in_ms")] + \
+              [(n, ctypes.c_double) for n in ("speech_2_noise_ratio", "snr_thres", "decibel_thres",
+                                              "speech_noise_thres", "fe_prior_thres")]
 
 
 _lib = None
@@ -123,6 +134,12 @@ def load_library(path: Optional[str] = None) -> ctypes.CDLL:
     lib.pfm_vad_reset.argtypes = [vp, vp]
     lib.pfm_vad_run.argtypes = [vp, vp, f32p, i32, f32p, f32p]
     lib.pfm_vad_fbank_raw.argtypes = [vp, vp, f32p, i32p, i32, i32, f32p, i32]
+    lib.pfm_vad_opts_default.argtypes = [ctypes.POINTER(PfmVadOpts)]
+    lib.pfm_vad_opts_default.restype = None
+    lib.pfm_vad_detector_create.argtypes = [ctypes.POINTER(PfmVadOpts), ctypes.POINTER(vp)]
+    lib.pfm_vad_detector_push.argtypes = [vp, vp, i32, vp, i32, i32, i32, vp, i32, ctypes.POINTER(ctypes.c_int32)]
+    lib.pfm_vad_detector_destroy.argtypes = [vp]
+    lib.pfm_vad_detector_destroy.restype = None
     lib.pfm_vad_destroy.argtypes = [vp]
     lib.pfm_vad_destroy.restype = None
     lib.pfm_streams_destroy.argtypes = [vp]
@@ -573,3 +590,40 @@ class PfmVad:
         check(self.lib.pfm_vad_run(self.h, _stream_ptr(torch, dev), _ptr(feats), T, _ptr(p), _ptr(probs)),
               "pfm_vad_run")
         return (p, probs) if want_probs else p
+
+
+class PfmVadDetector:
+    """pfm_vad_detector: the VAD decision state machine of one stream, native host code (no GPU)."""
+
+    def __init__(self, opts: Dict):
+        self.lib = load_library()
+        o = PfmVadOpts()
+        for name, _ in PfmVadOpts._fields_:
+            v = opts[name]
+            setattr(o, name, float(v) if isinstance(getattr(o, name), float) else int(v))
+        h = ctypes.c_void_p()
+        check(self.lib.pfm_vad_detector_create(ctypes.byref(o), ctypes.byref(h)), "pfm_vad_detector_create")
+        self.h = h
+
+    def __del__(self):
+        h = getattr(self, "h", None)
+        if h is not None and h.value:
+            try:
+                self.lib.pfm_vad_detector_destroy(h)
+            except Exception:
+                pass
+            self.h = None
+
+    def push(self, decibel, p_sil, is_final: bool, streaming: bool):
+        """One forward() call: the call's frame decibels and posteriors -> the segments it outputs."""
+        db = np.ascontiguousarray(decibel, dtype=np.float64)
+        ps = np.ascontiguousarray(p_sil, dtype=np.float32)
+        self.frames = getattr(self, "frames", 0) + int(ps.size)
+        cap = self.frames + 16   # every segment covers >= 1 frame: never more segments than frames
+        segs = np.zeros((cap, 2), np.int32)
+        n = ctypes.c_int32(0)
+        check(self.lib.pfm_vad_detector_push(self.h, db.ctypes.data if db.size else None, int(db.size),
+                                             ps.ctypes.data if ps.size else None, int(ps.size), int(is_final),
+                                             int(streaming), segs.ctypes.data, cap, ctypes.byref(n)),
+              "pfm_vad_detector_push")
+        return segs[: n.value].tolist()

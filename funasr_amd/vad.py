@@ -7,9 +7,10 @@ Contract (funasr/models/fsmn_vad_streaming/model.py:281-916):
     over 60 s sample chunks (chunk_size 60000) with the online frontend (LFR 5/1) and its caches; offline
     (is_streaming_input False) segments are [beg, end] pairs.
 The FSMN encoder (the per-frame silence posteriors) runs in the HIP library (pfm_vad_run) with its
-memory caches in HBM; the frame decibels and the detection state machine below are host code over those
-per-frame values, as in the reference (E2EVadModel: GetFrameState, WindowDetector, DetectOneFrame and
-the output-buffer bookkeeping).
+memory caches in HBM; the detection state machine over those per-frame values is host code, as in the
+reference (E2EVadModel: GetFrameState, WindowDetector, DetectOneFrame and the output-buffer bookkeeping),
+native in the library (pfm_vad_detector_*). `VadDetector` below is its Python statement (frame decibels
+and the same state machine), kept as the readable specification the native one is tested against.
 """
 from __future__ import annotations
 
@@ -340,7 +341,9 @@ class FsmnVADStreaming(HipModel):
         opts = dict(self.cfg.vad_opts)
         if kwargs.get("max_end_silence_time") is not None:
             opts["max_end_silence_time"] = kwargs["max_end_silence_time"]
-        cache.update(frontend={}, prev_samples=np.zeros((0,), np.float32), detector=VadDetector(opts))
+        from .runtime import PfmVadDetector
+        cache.update(frontend={}, prev_samples=np.zeros((0,), np.float32), detector=PfmVadDetector(opts),
+                     db_calc=VadDetector(opts))
         self.engine().reset()
         return cache
 
@@ -367,19 +370,21 @@ class FsmnVADStreaming(HipModel):
         n = int(len(audio) // stride + int(is_final))
         m = int(len(audio) % stride * (1 - int(is_final)))
         eng = self.engine()
-        det: VadDetector = cache["detector"]
+        det = cache["detector"]          # native state machine (pfm_vad_detector)
+        dbc: VadDetector = cache["db_calc"]
         segments: List[List[int]] = []
         for i in range(n):
             fin = is_final and i == n - 1
             seg = audio[i * stride:(i + 1) * stride]
             feats = fe.step(eng, [(seg, fin, cache["frontend"])])[0]
             wv = cache["frontend"].get("waveforms")
+            n0 = len(dbc.decibel)
             if wv is not None:
-                det.add_waveform(wv)
+                dbc.add_waveform(wv)     # ComputeDecibel in numpy float32, as the reference
+            db_new = np.asarray(dbc.decibel[n0:], np.float64)
+            dbc.decibel = []
             p = eng.run(feats).cpu().numpy() if feats.shape[0] else np.zeros((0,), np.float32)
-            det.add_scores(p)
-            det.detect_chunk(len(p), fin)
-            segments.extend(det.segments(fin, streaming))
+            segments.extend(det.push(db_new, p, fin, streaming))
         cache["prev_samples"] = audio[:-m] if m else audio[:0]
         if is_final:
             self.init_cache(cache, **kwargs)

@@ -171,6 +171,26 @@ int pfm_vad_reset(pfm_vad* v, void* stream);
 /* One chunk: feats [T, input_dim] f32 device (WavFrontendOnline LFR rows) -> p_sil [T] f32 device (softmax
  * posterior of pdf 0), probs optional [T, output_dim] (NULL to skip). The caches advance by the chunk. */
 int pfm_vad_run(pfm_vad* v, void* stream, const float* feats, int T, float* p_sil, float* probs);
+/* The VAD detection state machine (E2EVadModel, fsmn_vad_streaming/model.py:303-916): host code over the
+ * per-frame silence posteriors (pfm_vad_run) and frame decibels; one detector per stream (init_cache).
+ * Options: VADXOptions (model.py:49-117) used by the decision loop. */
+typedef struct pfm_vad_opts {
+    int32_t detect_mode, max_end_silence_time, max_start_silence_time, window_size_ms, sil_to_speech_time_thres,
+        speech_to_sil_time_thres, do_extend, lookback_time_start_point, lookahead_time_end_point,
+        max_single_segment_time, noise_frame_num_used_for_snr, frame_in_ms;
+    double speech_2_noise_ratio, snr_thres, decibel_thres, speech_noise_thres, fe_prior_thres;
+} pfm_vad_opts;
+typedef struct pfm_vad_detector pfm_vad_detector;
+void pfm_vad_opts_default(pfm_vad_opts* o);
+int pfm_vad_detector_create(const pfm_vad_opts* o, pfm_vad_detector** out);
+/* One forward() call (model.py:548-613): append the call's frame decibels (HOST f64, ComputeDecibel) and n
+ * posteriors (HOST f32), run DetectCommonFrames / DetectLastFrames (is_final) over the n new frames and
+ * write the segments this call outputs: segs [cap][2] HOST int32 ([beg_ms, end_ms]; -1 for an open end or
+ * start when streaming), n_segs = their number (an error if > cap). No GPU work. */
+int pfm_vad_detector_push(pfm_vad_detector* d, const double* decibel, int n_db, const float* p_sil, int n,
+                          int is_final, int streaming, int32_t* segs, int cap, int32_t* n_segs);
+void pfm_vad_detector_destroy(pfm_vad_detector* d);
+
 /* pfm_fbank_raw on the VAD object (its online frontend runs without a model handle). */
 int pfm_vad_fbank_raw(pfm_vad* v, void* stream, const float* wav, const int32_t* nsamp, int B, int S_max,
                       float* fb, int N_cap);

@@ -320,3 +320,21 @@ def test_vad_oracle_vs_reference(name):
         pr, cache = vad_forward(f, w, cfg, cache)
         p0.append(pr[:, 0].numpy())
     np.testing.assert_allclose(np.concatenate(p0), g[f"{name}_p0"], atol=2e-5, rtol=0)
+
+
+@pytest.mark.parametrize("name", ["v1", "v2"])
+def test_vad_native_state_machine_vs_reference(name):
+    """The native state machine (pfm_vad_detector_*, host code in libpfm_hip.so, no GPU) fed the reference's
+    per-chunk posteriors and decibels reproduces its segments exactly."""
+    import json
+    from funasr_amd.config import fsmn_vad
+    from funasr_amd.runtime import PfmVadDetector
+    gj = json.load(open(f"{GOLD}/vad.json"))[name]
+    g = np.load(f"{GOLD}/vad.npz")
+    p0, po = g[f"{name}_p0"], g[f"{name}_p0_off"]
+    db, do = g[f"{name}_db"], g[f"{name}_db_off"]
+    det = PfmVadDetector(fsmn_vad().vad_opts)
+    segs = []
+    for c in range(len(po) - 1):
+        segs += det.push(db[do[c]:do[c + 1]], p0[po[c]:po[c + 1]], c == len(po) - 2, False)
+    assert segs == gj["segments"]
