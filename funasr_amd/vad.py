@@ -97,15 +97,20 @@ class VadDetector:
         self.last_drop = 0
 
     # ---- per-chunk inputs (ComputeDecibel :326-348, ComputeScores :350-360)
-    def add_waveform(self, w: np.ndarray):
+    def frame_decibels(self, w: np.ndarray) -> np.ndarray:
+        """ComputeDecibel (:326-348) over one chunk's waveform, float32 as the reference. The frames
+        are a strided view (no gather copy); np.square materialises the same contiguous [n, fl]
+        block the reference sums, so the values are bit-identical to its fancy-indexed frames."""
         fl = int(self.o["frame_length_ms"] * self.o["sample_rate"] / 1000)
         fs = int(self.frame_ms * self.o["sample_rate"] / 1000)
-        w = np.asarray(w, np.float32)
+        w = np.asarray(w, np.float32).reshape(-1)
         if len(w) < fl:
-            return
-        offs = np.arange(0, len(w) - fl + 1, fs)
-        frames = w[offs[:, None] + np.arange(fl)]
-        self.decibel.extend((10 * np.log10(np.sum(np.square(frames), axis=1) + 0.000001)).tolist())
+            return np.zeros((0,), np.float32)
+        frames = np.lib.stride_tricks.sliding_window_view(w, fl)[::fs]
+        return 10 * np.log10(np.sum(np.square(frames), axis=1) + 0.000001)
+
+    def add_waveform(self, w: np.ndarray):
+        self.decibel.extend(self.frame_decibels(w).tolist())
 
     def add_scores(self, p_sil: np.ndarray):
         self.p_sil.extend(float(x) for x in np.asarray(p_sil, np.float32))
@@ -378,11 +383,8 @@ class FsmnVADStreaming(HipModel):
             seg = audio[i * stride:(i + 1) * stride]
             feats = fe.step(eng, [(seg, fin, cache["frontend"])])[0]
             wv = cache["frontend"].get("waveforms")
-            n0 = len(dbc.decibel)
-            if wv is not None:
-                dbc.add_waveform(wv)     # ComputeDecibel in numpy float32, as the reference
-            db_new = np.asarray(dbc.decibel[n0:], np.float64)
-            dbc.decibel = []
+            # ComputeDecibel in numpy float32, as the reference
+            db_new = dbc.frame_decibels(wv).astype(np.float64) if wv is not None else np.zeros((0,))
             p = eng.run(feats).cpu().numpy() if feats.shape[0] else np.zeros((0,), np.float32)
             segments.extend(det.push(db_new, p, fin, streaming))
         cache["prev_samples"] = audio[:-m] if m else audio[:0]
