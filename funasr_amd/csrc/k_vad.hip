@@ -2,8 +2,8 @@
 // silence posteriors that the VAD state machine (fsmn_vad_streaming/model.py:493-546, host side) consumes.
 //
 //   vad_dense_kernel   Y[t, n] = act(X[t, :] . W[n, :] + b[n]) for the Affine / Linear transforms
-//                      (K = 400, 140, 250, 128: any K; f32 FMA chain per output, one thread per output,
-//                      the weight matrices (<= 56k floats) stay L2-resident)
+//                      (K = 400, 140, 250, 128: any K; f32 FMA chain per output in k order, 64 x 64
+//                      LDS-tiled, the weight matrices (<= 56k floats) stay L2-resident)
 //   vad_fsmn_kernel    causal memory block (FSMNBlock.forward with its cache, rorder 0): y[t] = x[t] +
 //                      sum_j w[c][j] * x[t - (L-1) + j], rows before the chunk from the per-layer cache
 //                      (zeros at the start of a stream); the cache then keeps the chunk's last L-1 rows
@@ -15,20 +15,63 @@
 
 namespace {
 
+// 64 x 64 output tile per 256-thread block, 4 x 4 outputs per thread, K staged through LDS 16 at a time
+// (X and W tiles stored k-major so a thread's 4 rows / 4 columns are contiguous). Every output keeps the
+// plain serial chain s = fma(x[k], w[k], s) for k = 0..K-1 (the k loop never pads), then + b, then ReLU,
+// so the result is bit-identical to a one-thread-per-output dot product; the tiling only removes the
+// K-strided weight reads and re-reads of X.
+constexpr int VD_TM = 64, VD_TN = 64, VD_TK = 16;
 __global__ __launch_bounds__(256) void vad_dense_kernel(const float* __restrict__ X, int ldx, int M, int K,
                                                         const float* __restrict__ W, const float* __restrict__ b,
                                                         int N, int relu, float* __restrict__ Y, int ldy) {
-    const long long gid = (long long)blockIdx.x * 256 + threadIdx.x;
-    if (gid >= (long long)M * N) return;
-    const int n = (int)(gid % N);
-    const long long m = gid / N;
-    const float* x = X + m * ldx;
-    const float* w = W + (long long)n * K;
-    float s = 0.f;
-    for (int k = 0; k < K; ++k) s = fmaf(x[k], w[k], s);
-    if (b) s += b[n];
-    if (relu) s = fmaxf(s, 0.f);
-    Y[m * ldy + n] = s;
+    __shared__ float Xs[VD_TK][VD_TM + 4];
+    __shared__ float Ws[VD_TK][VD_TN + 4];
+    const int tid = threadIdx.x;
+    const int tx = tid % 16, ty = tid / 16;          // 16 x 16 threads, each 4 cols x 4 rows
+    const int m0 = blockIdx.y * VD_TM, n0 = blockIdx.x * VD_TN;
+    const int lr = tid / 4, lk = (tid % 4) * 4;      // loader: row lr of the tile, k lk..lk+3
+    float acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = 0.f;
+    for (int k0 = 0; k0 < K; k0 += VD_TK) {
+        const int kn = min(VD_TK, K - k0);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int k = k0 + lk + q;
+            const int m = m0 + lr, n = n0 + lr;
+            Xs[lk + q][lr] = (k < K && m < M) ? X[(long long)m * ldx + k] : 0.f;
+            Ws[lk + q][lr] = (k < K && n < N) ? W[(long long)n * K + k] : 0.f;
+        }
+        __syncthreads();
+        for (int kk = 0; kk < kn; ++kk) {
+            float a[4], w[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) a[i] = Xs[kk][ty * 4 + i];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) w[j] = Ws[kk][tx * 4 + j];
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) acc[i][j] = fmaf(a[i], w[j], acc[i][j]);
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int m = m0 + ty * 4 + i;
+        if (m >= M) continue;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int n = n0 + tx * 4 + j;
+            if (n >= N) continue;
+            float s = acc[i][j];
+            if (b) s += b[n];
+            if (relu) s = fmaxf(s, 0.f);
+            Y[(long long)m * ldy + n] = s;
+        }
+    }
 }
 
 // x [T, D] (this chunk), cache [L-1, D] (previous rows), w [D, L] (conv_left taps, tap j multiplies row
@@ -84,8 +127,8 @@ hipError_t pfm_vad_dense(const float* X, int ldx, int M, int K, const float* W, 
                          float* Y, int ldy, hipStream_t st) {
     const long long n = (long long)M * N;
     if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(vad_dense_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, X, ldx, M, K, W, b, N,
-                       relu, Y, ldy);
+    hipLaunchKernelGGL(vad_dense_kernel, dim3((unsigned)((N + VD_TN - 1) / VD_TN), (unsigned)((M + VD_TM - 1) / VD_TM)),
+                       dim3(256), 0, st, X, ldx, M, K, W, b, N, relu, Y, ldy);
     PFM_LAUNCH_CHECK();
     return hipSuccess;
 }
