@@ -145,8 +145,11 @@ class CTTransformer(HipModel):
         """One mini-sentence: word ids [n] -> argmax punctuation id per word (pfm_run_punc)."""
         eng = self.engine()
         dev = torch.device("cuda", eng.device)
-        x = torch.from_numpy(np.ascontiguousarray(ids, dtype=np.int32))[None].to(dev)
-        r = eng.run_punc(x, torch.tensor([x.shape[1]], dtype=torch.int32, device=dev), mode=self.mode)
+        n = len(ids)
+        # ids and their length in ONE host->device copy (the text loop is latency-bound, one call per
+        # mini-sentence)
+        buf = torch.from_numpy(np.append(np.asarray(ids, dtype=np.int32), np.int32(n))).to(dev)
+        r = eng.run_punc(buf[:n][None], buf[n:], mode=self.mode)
         return r["punc"][0].cpu().numpy()
 
     @torch.no_grad()
