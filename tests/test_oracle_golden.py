@@ -296,6 +296,24 @@ def test_vad_decibels_vs_reference():
     np.testing.assert_allclose(np.asarray(det.decibel), g["v1_db"], rtol=0, atol=1e-9)
 
 
+@pytest.mark.parametrize("n_samples", [0, 399, 400, 401, 559, 560, 16000, 16000 * 7 + 123])
+def test_vad_frame_decibels_strided_is_bit_identical(n_samples):
+    """frame_decibels (strided-view frames) vs the reference's own formulation (ComputeDecibel,
+    fsmn_vad_streaming/model.py:341-345: fancy-indexed frames, np.sum(np.square), float32) on ragged lengths,
+    including inputs shorter than one frame (no frames)."""
+    from funasr_amd.config import fsmn_vad
+    from funasr_amd.vad import VadDetector
+    w = (np.random.default_rng(n_samples).standard_normal(n_samples) * 0.1).astype(np.float32)
+    db = VadDetector(fsmn_vad().vad_opts).frame_decibels(w)
+    if n_samples < 400:
+        assert db.shape == (0,)
+        return
+    offs = np.arange(0, n_samples - 400 + 1, 160)
+    frames = w[offs[:, None] + np.arange(400)]
+    ref = 10 * np.log10(np.sum(np.square(frames), axis=1) + 0.000001)
+    assert db.dtype == ref.dtype and np.array_equal(db, ref)
+
+
 @pytest.mark.parametrize("name", ["v1", "v2"])
 def test_vad_oracle_vs_reference(name):
     """oracle/vad_ref.vad_forward on oracle online-frontend features (LFR 5/1, 60 s chunks, carried FSMN
