@@ -176,9 +176,12 @@ class WavFrontendOnline(WavFrontend):
         fb = None
         if any(nfrs):
             S = max(len(u) for u in xs)
-            buf = np.zeros((len(xs), S), np.float32)
-            for k, u in enumerate(xs):
-                buf[k, : len(u)] = u
+            if len(xs) == 1:   # one stream (the VAD, batch 1): no padded staging copy
+                buf = np.ascontiguousarray(xs[0], dtype=np.float32)[None]
+            else:
+                buf = np.zeros((len(xs), S), np.float32)
+                for k, u in enumerate(xs):
+                    buf[k, : len(u)] = u
             fb = engine.fbank_raw(torch.from_numpy(buf).to(dev), [len(u) for u in xs])
         srcs, idxs, offs, out_rows = [], [], 0, []
         for k, (wav, is_final, cache) in enumerate(items):
