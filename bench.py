@@ -232,6 +232,11 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus != world:
+        # one process per GPU: N GPUs means N ranks launched by torch.distributed.run, never a silent 1-GPU run
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; launch N>1 as "
+                 f"python -m torch.distributed.run --nproc-per-node {args.gpus} --master-addr 127.0.0.1 "
+                 f"bench.py --gpus {args.gpus}")
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl")

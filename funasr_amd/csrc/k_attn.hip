@@ -653,9 +653,8 @@ hipError_t pfm_attention_fsmn(int dtype, const void* q, RowMap qmap, const void*
     a.o = o; a.ldo = ldo; a.o2 = o2; a.o2_dtype = DT_BF16; a.klen = klen; a.Tq = Tq; a.Tk = Tk; a.scale = scale;
     a.fw = fsmn_wT; a.fout = fsmn_out; a.fld = fsmn_ld; a.fD = heads * DK;
     if (fsmn_out) {   // fused FSMN: bf16 8-wave kernel only, self-attention, 16-B aligned rows
-        const char* e = getenv("PFM_ATTN_WAVES");
-        const char* pp = getenv("PFM_ATTN_PP");
-        if (dtype != DT_BF16 || Tq != Tk || (e && atoi(e) != 8) || (pp && pp[0] == '1') || fsmn_ld % 8 ||
+        const PfmKnobs& kn = pfm_knobs();
+        if (dtype != DT_BF16 || Tq != Tk || kn.attn_waves != 8 || kn.attn_pp || fsmn_ld % 8 ||
             vmap.ld % 8 || ((uintptr_t)fsmn_out % 16) || !fsmn_wT)
             return hipErrorInvalidValue;
     }
@@ -679,10 +678,8 @@ hipError_t pfm_attention_fsmn(int dtype, const void* q, RowMap qmap, const void*
         dim3 grid((Tq + 127) / 128, heads, B), block(256);
         hipLaunchKernelGGL(attn_f32_kernel, grid, block, LDS32, st, a);
     } else {
-        const char* e = getenv("PFM_ATTN_WAVES");
-        const int nw = e ? atoi(e) : 8;
-        const char* pp = getenv("PFM_ATTN_PP");   // ping-pong 8-wave variant (A/B)
-        if (nw == 8 && pp && pp[0] == '1') {
+        const int nw = pfm_knobs().attn_waves;
+        if (nw == 8 && pfm_knobs().attn_pp) {   // ping-pong 8-wave variant (A/B)
             dim3 grid((Tq + 255) / 256, heads, B), block(512);
             hipLaunchKernelGGL(attn_bf16_pp_kernel, grid, block, 3 * STG2, st, a);
         } else if (nw == 8) {

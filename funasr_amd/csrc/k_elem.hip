@@ -562,7 +562,8 @@ __global__ __launch_bounds__(256) void sv_input_kernel(const float* __restrict__
     const float* src = t < nq ? embed + (long long)q.id[t] * I : feats + ((long long)b * T + (t - nq)) * I;
     float* dst = x + row * I;
     for (int c = lane * 4; c < I; c += 256) *(float4*)(dst + c) = *(const float4*)(src + c);
-    if (t == 0 && lane == 0) olen[b] = lens[b] + nq;
+    // clamp like every other length consumer: the collapse kernel reads [0, olen) of a [T + nq] row
+    if (t == 0 && lane == 0) olen[b] = min(max(lens[b], 0), T) + nq;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -576,7 +577,7 @@ __global__ __launch_bounds__(64) void ctc_collapse_kernel(const int* __restrict_
                                                           int* __restrict__ ntok) {
     const int lane = threadIdx.x;
     const int b = blockIdx.x;
-    const int n = olen[b];
+    const int n = (int)min((long long)max(olen[b], 0), ld);   // never past the utterance's id row
     const int* r = ids + (long long)b * ld;
     int* out = tokens + (long long)b * Lcap;
     int cnt = 0;
@@ -741,8 +742,8 @@ hipError_t pfm_fsmn_bf16in(const bf16* v, RowMap vmap, const int* len, int B, in
     if (B <= 0 || T <= 0) return hipSuccess;
     if (D % 4 != 0 || K != 11 || left < 0 || left >= K) return hipErrorInvalidValue;
     if (vmap.rows_per_seg > 0 && vmap.rows_per_seg != T) return hipErrorInvalidValue;
-    const char* ev = getenv("PFM_FSMN_V2");   // frames per thread of the 8-channel kernel (0 = 4-channel kernel)
-    const int frw = ev ? atoi(ev) : 0;   // measured: the 4-channel kernel with static LEFT is fastest
+    // PFM_FSMN_V2: frames per thread of the 8-channel kernel (0 = 4-channel kernel);
+    const int frw = pfm_knobs().fsmn_v2;   // measured: the 4-channel kernel with static LEFT is fastest
     if (!res && D % 8 == 0 && vmap.ld % 8 == 0 && (vmap.rows_per_seg <= 0 || vmap.seg_stride % 8 == 0) &&
         ((uintptr_t)v % 16) == 0 && (!out_bf || ((uintptr_t)out_bf % 16) == 0) && (!out || ((uintptr_t)out % 16) == 0) &&
         (frw == 4 || frw == 8 || frw == 16) && 11 * D * 4 <= 64 * 1024) {

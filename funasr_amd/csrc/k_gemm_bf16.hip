@@ -1028,8 +1028,7 @@ hipError_t launch(const void* A, RowMap amap, const void* W, long long ldw, int 
     const int tiles_m = (M + C::BM - 1) / C::BM, tiles_n = (N + C::BN - 1) / C::BN;
     // grouped tile order (4 tile-rows per group) for the wide-N projections (memory K|V, vocabulary:
     // +6 % measured), row-major otherwise; PFM_GEMM_GM overrides per launch (A/B)
-    const char* eg = getenv("PFM_GEMM_GM");
-    const int gm = eg ? atoi(eg) : (tiles_n >= 16 ? 4 : 0);
+    const int gm = pfm_knobs().gemm_gm >= 0 ? pfm_knobs().gemm_gm : (tiles_n >= 16 ? 4 : 0);
     hipLaunchKernelGGL((gemm_bf16_kernel<C, LN>), dim3(tiles_m * tiles_n), dim3(C::NT), C::LDS, st, (const bf16*)A, amap,
                        (const bf16*)W, ldw, M, N, K, tiles_m, tiles_n, gm, e2);
     PFM_LAUNCH_CHECK();
@@ -1075,8 +1074,7 @@ hipError_t launch_persist(const void* A, RowMap amap, const void* W, long long l
 }
 
 int pick_cfg(int M, int N, int K, bool amax) {
-    const char* e = getenv("PFM_GEMM_CFG");   // read per launch: lets one process A/B configurations
-    const int f = e ? atoi(e) : 0;
+    const int f = pfm_knobs().gemm_cfg;   // PFM_GEMM_CFG (per call): lets one process A/B configurations
     if (f >= 1 && f <= 17) return f;
     // Default (measured on the path, tools/bench_ab.py with the two concurrent encoder groups: 24.2 vs
     // 25.0-25.3 ms/step for the policies below). Grids are counted in 256x256 tiles; each encoder group
@@ -1087,8 +1085,7 @@ int pick_cfg(int M, int N, int K, bool amax) {
     //    128x256 tiles, two blocks per CU (C4).
     // PFM_GEMM_POLICY=1: the earlier grid-size policy (C15 at >= 2 tiles / CU or K >= 1536 with >= 240
     // tiles, else C4); =2: C13 / C4 for decoder-sized M.
-    const char* pol = getenv("PFM_GEMM_POLICY");
-    const int p = pol ? atoi(pol) : 0;
+    const int p = pfm_knobs().gemm_policy;
     const long long big = (long long)((M + 255) / 256) * ((N + 255) / 256);
     if (p == 1 || p == 2) {
         if (p == 2 && M <= 16384 && !amax) return 4;
@@ -1309,19 +1306,16 @@ hipError_t pfm_gemm_bf16_256(const void* A, RowMap amap, const void* W, long lon
          (epi.ln_st_in && (!epi.ln_colsum || epi.pre_res_ok))))
         return hipErrorInvalidValue;
     {
-        const char* ev = getenv("PFM_GEMM_ST16");   // read per launch (A/B runs); default on
         const RowMap& om = epi.out_map;
         e2.st16_ok = e2.vec_ok && epi.out && epi.out_dtype == DT_BF16 && !epi.out2 && !epi.amax_val && N % 8 == 0 &&
                      om.ld % 8 == 0 && (om.rows_per_seg <= 0 || om.seg_stride % 8 == 0) &&
-                     ((uintptr_t)epi.out % 16) == 0 && !(ev && ev[0] == '0');
+                     ((uintptr_t)epi.out % 16) == 0 && pfm_knobs().gemm_st16;
     }
     {
         // residual pre-loaded into the accumulators (accumulator-layout scalar loads ahead of the main
         // loop): measured 2.2 ms/step SLOWER on the path (bf16 + f32 residual out-proj), so opt-in
-        const char* pr = getenv("PFM_GEMM_PRERES");
-        e2.pre_res_ok = pr && pr[0] == '1';
-        const char* rb = getenv("PFM_GEMM_RESBATCH");   // residual loads batched ahead of the stores
-        e2.res_batch = !(rb && rb[0] == '0');
+        e2.pre_res_ok = pfm_knobs().gemm_preres;
+        e2.res_batch = pfm_knobs().gemm_resbatch;   // residual loads batched ahead of the stores
     }
     const bool ln = e2.ln_st_in || e2.ln_st_out;
     int cfg = pick_cfg(M, N, K, epi.amax_val != nullptr);

@@ -100,19 +100,61 @@ static int fail(int code, const std::string& msg) {
             return fail(PFM_E_HIP, std::string(#expr) + ": " + hipGetErrorString(_e));           \
     } while (0)
 
+static thread_local PfmKnobs t_knobs = {0, 0, 1, 8, 0, 1, 0, 2, 1, 0, -1, 0, 0, 1, 0, 1, 1, 0};
+
+const PfmKnobs& pfm_knobs() { return t_knobs; }
+
+void pfm_knobs_refresh() {
+    auto iv = [](const char* name, int dflt) {
+        const char* e = getenv(name);
+        return (e && e[0]) ? atoi(e) : dflt;
+    };
+    PfmKnobs k;
+    k.ln_fold = iv("PFM_LN_FOLD", 0) == 1;
+    k.gemm_kernel = iv("PFM_GEMM_KERNEL", 0);
+    k.attn_fsmn = iv("PFM_ATTN_FSMN", 1) != 0;
+    k.attn_waves = iv("PFM_ATTN_WAVES", 8);
+    k.attn_pp = iv("PFM_ATTN_PP", 0) == 1;
+    k.kv_overlap = iv("PFM_KV_OVERLAP", 1) != 0;
+    k.gemm_ln = iv("PFM_GEMM_LN", 0) == 1;
+    k.subbatch = std::max(1, std::min(iv("PFM_SUBBATCH", 2), 4));
+    k.stream_graph = iv("PFM_STREAM_GRAPH", 1) != 0;
+    k.fsmn_v2 = iv("PFM_FSMN_V2", 0);
+    k.gemm_gm = iv("PFM_GEMM_GM", -1);
+    k.gemm_cfg = iv("PFM_GEMM_CFG", 0);
+    k.gemm_policy = iv("PFM_GEMM_POLICY", 0);
+    k.gemm_st16 = iv("PFM_GEMM_ST16", 1) != 0;
+    k.gemm_preres = iv("PFM_GEMM_PRERES", 0) == 1;
+    k.gemm_resbatch = iv("PFM_GEMM_RESBATCH", 1) != 0;
+    k.gemm_skinny = iv("PFM_GEMM_SKINNY", 1) != 0;
+    const int* f = &k.ln_fold;
+    unsigned long long s = 1469598103934665603ull;   // FNV-1a over the fields
+    for (int i = 0; i < 17; ++i) s = (s ^ (unsigned long long)(unsigned)f[i]) * 1099511628211ull;
+    k.sig = s;
+    t_knobs = k;
+}
+
 namespace {
 
-// Bumped whenever any DevBuf is (re)allocated: captured HIP graphs hold raw buffer addresses and are
-// valid only while this is unchanged.
-std::atomic<unsigned long long> g_buf_gen{0};
+// Workspace generation of one owner (a pfm_handle or a pfm_streams): bumped whenever one of the owner's
+// DevBufs is (re)allocated. Captured HIP graphs hold raw buffer addresses, so a graph recorded against
+// (handle gen, streams gen) is valid only while both are unchanged. The DevBuf members of an owner bind
+// to its counter at construction (GenBind as the owner's first member, GenUnbind as its last).
+thread_local std::atomic<unsigned long long>* t_bind_gen = nullptr;
+struct GenBind { explicit GenBind(std::atomic<unsigned long long>* g) { t_bind_gen = g; } };
+struct GenUnbind { GenUnbind() { t_bind_gen = nullptr; } };
 
 struct DevBuf {
     void* p = nullptr;
     size_t bytes = 0;
+    std::atomic<unsigned long long>* gen = t_bind_gen;
+    DevBuf() = default;
+    DevBuf(const DevBuf&) = delete;
+    DevBuf& operator=(const DevBuf&) = delete;
     ~DevBuf() { if (p) (void)hipFree(p); }
     hipError_t ensure(size_t n) {
         if (n <= bytes) return hipSuccess;
-        g_buf_gen.fetch_add(1);
+        if (gen) gen->fetch_add(1);
         if (p) { hipError_t e = hipFree(p); if (e != hipSuccess) return e; p = nullptr; bytes = 0; }
         hipError_t e = hipMalloc(&p, n);
         if (e == hipSuccess) bytes = n;
@@ -142,6 +184,8 @@ struct DecLayer { size_t fsmn, wq, bq, wo, bo, w1, b1, w2, ng, nb, n1g, n1b, n2g
 }  // namespace
 
 struct pfm_handle {
+    std::atomic<unsigned long long> buf_gen{0};   // workspace generation (captured streaming graphs)
+    GenBind gen_bind_{&buf_gen};                  // binds every DevBuf member below to buf_gen
     pfm_config cfg;
     int device = 0;
     std::unordered_map<std::string, WEntry> reg;
@@ -189,6 +233,8 @@ struct pfm_handle {
     size_t ev_used = 0;
     double prof_ms[3] = {0, 0, 0}, prof_fl[3] = {0, 0, 0}, prof_by[3] = {0, 0, 0};
     long long prof_n[3] = {0, 0, 0};
+
+    GenUnbind gen_unbind_;                   // last member: DevBufs created later are unbound
 
     float* w(size_t off) const { return arena.as<float>() + off; }
     bf16* wb(size_t off) const { return arena_bf.as<bf16>() + off; }
@@ -336,10 +382,7 @@ void make_pe(std::vector<float>& pe, int T, int depth) {
 // more accurate fast path (token agreement with exact mode 0.85 vs 0.73-0.79 on the goldens) but measured
 // 0.6-0.9 ms/step slower than the standalone streaming LayerNorm (the producers' extra bf16(x) write and
 // statistics reductions cost more than the two LN passes they delete).
-bool ln_fold_enabled() {
-    const char* e = getenv("PFM_LN_FOLD");
-    return e && e[0] == '1';
-}
+bool ln_fold_enabled() { return pfm_knobs().ln_fold; }
 
 int ensure_bf16(pfm_handle* h, hipStream_t st) {
     if (!h->bf_ready) {
@@ -486,11 +529,7 @@ void prof_collect(pfm_handle* h) {
 // Kernel choice: bf16 operands go to the 256x256 LDS-DMA kernel whenever its alignment
 // contract holds (K % 64 == 0, 16-B aligned rows); f32 (exact mode) and odd shapes use the
 // 128x128 register-staged kernel.
-int gemm_kernel_override() {   // PFM_GEMM_KERNEL=128 forces the 128x128 kernel (A/B experiments)
-    static int v = -1;
-    if (v < 0) { const char* e = getenv("PFM_GEMM_KERNEL"); v = e ? atoi(e) : 0; }
-    return v;
-}
+int gemm_kernel_override() { return pfm_knobs().gemm_kernel; }   // 128: force the 128x128 kernel (A/B)
 
 bool use_big_bf16(int dtype, RowMap amap, long long ldw, int K) {
     return dtype == DT_BF16 && gemm_kernel_override() != 128 && pfm_gemm_bf16_256_ok(amap, ldw, K);
@@ -506,21 +545,15 @@ hipError_t gemm_dispatch(int dtype, const void* A, RowMap amap, const void* W, l
 }
 
 bool attn_fsmn_enabled() {   // PFM_ATTN_FSMN=0: separate FSMN kernel (A/B; parity test compares both)
-    const char* e = getenv("PFM_ATTN_FSMN");
-    const char* w = getenv("PFM_ATTN_WAVES");
-    const char* p = getenv("PFM_ATTN_PP");
-    return !(e && e[0] == '0') && !(w && atoi(w) != 8) && !(p && p[0] == '1');
+    const PfmKnobs& k = pfm_knobs();
+    return k.attn_fsmn && k.attn_waves == 8 && !k.attn_pp;
 }
 
-bool kv_overlap_enabled() {   // PFM_KV_OVERLAP=0: memory K|V projection in-line on the caller's stream
-    const char* e = getenv("PFM_KV_OVERLAP");
-    return !(e && e[0] == '0');
-}
+bool kv_overlap_enabled() { return pfm_knobs().kv_overlap; }   // 0: memory K|V in-line on the caller's stream
 
-bool gemm_ln_enabled() {   // PFM_GEMM_LN=1 enables the full-row GEMM+LayerNorm fusion (measured slower
-    const char* e = getenv("PFM_GEMM_LN");   // than GEMM + standalone LN on MI355X; kept for A/B runs)
-    return e && e[0] == '1';
-}
+// PFM_GEMM_LN=1 enables the full-row GEMM+LayerNorm fusion (measured slower than GEMM + standalone LN on
+// MI355X; kept for A/B runs)
+bool gemm_ln_enabled() { return pfm_knobs().gemm_ln; }
 
 int amax_tiles(int dtype, RowMap amap, long long ldw, int N, int K) {
     return use_big_bf16(dtype, amap, ldw, K) ? pfm_gemm_bf16_256_amax_tiles(N) : pfm_gemm_amax_tiles(N);
@@ -794,8 +827,7 @@ int encoder_stack(const Run& r, const float* x_in, const int* lens, int B, int T
 
 
 int subbatch_count(pfm_handle* h, int B) {   // PFM_SUBBATCH=n (1 disables); profiling runs unsplit
-    static int v = -1;
-    if (v < 0) { const char* e = getenv("PFM_SUBBATCH"); v = e ? std::max(1, std::min(atoi(e), (int)pfm_handle::MAXSUB)) : 2; }
+    const int v = std::min(pfm_knobs().subbatch, (int)pfm_handle::MAXSUB);
     if (h->prof_on) return 1;
     return std::max(1, std::min(v, B));
 }
@@ -863,6 +895,7 @@ void pfm_config_punc(pfm_config* c) {
 const char* pfm_last_error(void) { return g_err.c_str(); }
 
 int pfm_create(const pfm_config* cfg, int device, pfm_handle** out) {
+    pfm_knobs_refresh();
     if (!cfg || !out) return fail(PFM_E_ARG, "pfm_create: null argument");
     *out = nullptr;
     if (cfg->heads < 1 || cfg->d_model % cfg->heads != 0 ||
@@ -916,6 +949,7 @@ void pfm_destroy(pfm_handle* h) {
 
 int pfm_set_weight(pfm_handle* h, const char* name, const void* host_ptr, int dtype, const int64_t* shape,
                    int ndim) {
+    pfm_knobs_refresh();
     if (!h || !name || !host_ptr || !shape) return fail(PFM_E_ARG, "pfm_set_weight: null argument");
     if (dtype != PFM_F32) return fail(PFM_E_ARG, "pfm_set_weight: only PFM_F32 host tensors are accepted");
     auto it = h->reg.find(name);
@@ -954,6 +988,7 @@ int pfm_set_weight(pfm_handle* h, const char* name, const void* host_ptr, int dt
 int pfm_missing_weights(const pfm_handle* h) { return h ? h->missing : -1; }
 
 int pfm_reserve(pfm_handle* h, int B, int T) {
+    pfm_knobs_refresh();
     if (!h || B < 1 || T < 1) return fail(PFM_E_ARG, "pfm_reserve: bad arguments");
     HIP_TRY(hipSetDevice(h->device));
     return reserve(h, B, T);
@@ -963,6 +998,7 @@ int pfm_lfr_frames(int nsamp) { return pfm_fbank_frames(nsamp); }
 
 int pfm_run(pfm_handle* h, void* stream, int mode, const float* feats, const int32_t* lens, int B, int T,
             int32_t* tokens, int L_cap, int32_t* ntok_out, float* enc_out, float* alphas_out, float* peaks_out) {
+    pfm_knobs_refresh();
     if (!h || !feats || !lens || !tokens || !ntok_out) return fail(PFM_E_ARG, "pfm_run: null argument");
     if (B < 1 || T < 1 || L_cap < 0) return fail(PFM_E_ARG, "pfm_run: bad sizes");
     if (mode != PFM_MODE_EXACT && mode != PFM_MODE_FAST) return fail(PFM_E_ARG, "pfm_run: bad mode");
@@ -1187,6 +1223,7 @@ int pfm_run(pfm_handle* h, void* stream, int mode, const float* feats, const int
 int pfm_run_ctc(pfm_handle* h, void* stream, int mode, const float* feats, const int32_t* lens, int B, int T,
                 const int32_t* query, int ban_token, int32_t* tokens, int L_cap, int32_t* ntok_out, float* enc_out,
                 int32_t* frame_ids) {
+    pfm_knobs_refresh();
     if (!h || !feats || !lens || !query || !tokens || !ntok_out) return fail(PFM_E_ARG, "pfm_run_ctc: null argument");
     if (B < 1 || T < 1 || L_cap < 0) return fail(PFM_E_ARG, "pfm_run_ctc: bad sizes");
     if (mode != PFM_MODE_EXACT && mode != PFM_MODE_FAST) return fail(PFM_E_ARG, "pfm_run_ctc: bad mode");
@@ -1256,6 +1293,7 @@ int pfm_run_ctc(pfm_handle* h, void* stream, int mode, const float* feats, const
 
 int pfm_run_punc(pfm_handle* h, void* stream, int mode, const int32_t* ids, const int32_t* lens, int B, int T,
                  int32_t* punc, float* logits) {
+    pfm_knobs_refresh();
     if (!h || !ids || !lens || !punc) return fail(PFM_E_ARG, "pfm_run_punc: null argument");
     if (h->cfg.arch != PFM_ARCH_PUNC) return fail(PFM_E_STATE, "pfm_run_punc: handle is not a punctuation model");
     if (B < 1 || T < 1) return fail(PFM_E_ARG, "pfm_run_punc: bad sizes");
@@ -1334,6 +1372,7 @@ int pfm_lfr_gather(void* stream, const float* frames, const int32_t* idx, int ro
 
 int pfm_fbank(pfm_handle* h, void* stream, const float* wav, const int32_t* nsamp, int B, int S_max,
               const float* cmvn, float* feats, int T_cap, int32_t* T_out) {
+    pfm_knobs_refresh();
     if (!h || !wav || !nsamp || !feats || !T_out) return fail(PFM_E_ARG, "pfm_fbank: null argument");
     if (B < 1 || S_max < 1 || T_cap < 1) return fail(PFM_E_ARG, "pfm_fbank: bad sizes");
     if (pfm_fbank_frames(S_max) > T_cap) return fail(PFM_E_ARG, "pfm_fbank: T_cap smaller than LFR frames of S_max");
@@ -1370,6 +1409,7 @@ int pfm_profile_read(pfm_handle* h, int kc, double* ms, double* flops, double* b
 // ---------------- single-op entry points ----------------
 int pfm_op_gemm(void* stream, int dtype, const void* A, const void* Wt, const float* bias, const float* res, float* C,
                 int M, int N, int K, int act) {
+    pfm_knobs_refresh();
     if ((act & 2) && dtype != DT_BF16) return fail(PFM_E_ARG, "pfm_op_gemm: bf16 output needs bf16 operands");
     GemmEpi e = epi_default();
     e.bias = bias; e.relu = act & 1;
@@ -1381,6 +1421,7 @@ int pfm_op_gemm(void* stream, int dtype, const void* A, const void* Wt, const fl
 
 int pfm_op_gemm_layernorm(void* stream, const void* A, const void* Wt, const float* bias, const float* res, float* C,
                           const float* gamma, const float* beta, float eps, float* Y, int M, int N, int K) {
+    pfm_knobs_refresh();
     if (!A || !Wt || !gamma || !beta || !Y || M < 0) return fail(PFM_E_ARG, "pfm_op_gemm_layernorm: null argument");
     if (N != 512 || K % 32) return fail(PFM_E_ARG, "pfm_op_gemm_layernorm: needs N == 512 and K % 32 == 0");
     GemmEpi e = epi_default();
@@ -1394,6 +1435,7 @@ int pfm_op_gemm_layernorm(void* stream, const void* A, const void* Wt, const flo
 
 int pfm_op_attention(void* stream, int dtype, const void* q, const void* k, const void* v, const int32_t* klen,
                      float* out, int B, int Tq, int Tk, int heads, float scale) {
+    pfm_knobs_refresh();
     const int D = heads * 128;
     HIP_TRY(pfm_attention(dtype, q, rowmap_plain(D), k, rowmap_plain(D), v, rowmap_plain(D), out, D, nullptr, klen, B,
                           Tq, Tk, heads, 128, scale, (hipStream_t)stream));
@@ -1402,6 +1444,7 @@ int pfm_op_attention(void* stream, int dtype, const void* q, const void* k, cons
 
 int pfm_op_layernorm(void* stream, const float* x, const float* g, const float* b, float* out, int M, int D,
                      float eps) {
+    pfm_knobs_refresh();
     HIP_TRY(pfm_layernorm(x, rowmap_plain(D), M, D, g, b, eps, nullptr, 0, 1.f, out, rowmap_plain(D), DT_F32,
                           nullptr, rowmap_plain(0), 0, (hipStream_t)stream));
     return PFM_OK;
@@ -1409,6 +1452,7 @@ int pfm_op_layernorm(void* stream, const float* x, const float* g, const float* 
 
 int pfm_op_fsmn(void* stream, const float* v, const int32_t* len, const float* w, const float* res, float* out,
                 int B, int T, int D, int K, int left) {
+    pfm_knobs_refresh();
     HIP_TRY(pfm_fsmn(v, rowmap_plain(D), len, B, T, D, w, K, left, res, out, nullptr, (hipStream_t)stream));
     return PFM_OK;
 }
@@ -1447,6 +1491,8 @@ int pfm_op_cif(void* stream, const float* alphas, const float* hidden, float* em
 // Streaming Paraformer (include/pfm.h, pfm_streams_*): per-slot chunk caches in HBM.
 // ============================================================================================
 struct pfm_streams {
+    std::atomic<unsigned long long> buf_gen{0};   // workspace generation of this object's DevBufs
+    GenBind gen_bind_{&buf_gen};
     pfm_handle* h = nullptr;
     int slots = 0, cs[3] = {0, 10, 5}, elb = 0, dlb = 0, mode = PFM_MODE_EXACT;
     int C0 = 5, Ce = 0, Cd = 0;   // overlap rows, encoder / decoder K/V cache capacities (rows)
@@ -1465,10 +1511,22 @@ struct pfm_streams {
     int hntok_cap = 0;
     DevBuf fin, tok;                    // chunk rows [n][maxn][I] (graph-stable copy), tokens [n][L_cap]
     // HIP graphs of the two launch sequences of a step (encoder + CIF; decoder), keyed by shape
-    struct Graph { hipGraphExec_t exec = nullptr; unsigned long long gen = 0; int seen = 0; bool bad = false; };
-    std::map<std::array<int, 4>, Graph> graphs;
+    // key: (phase, n, maxn, L * 4096 + L_cap, knob signature); at most MAX_GRAPHS execs are kept, the least
+    // recently replayed one is evicted (a server's active-stream and token counts vary without bound)
+    struct Graph {
+        hipGraphExec_t exec = nullptr;
+        unsigned long long gen = 0, last_use = 0;
+        int seen = 0;
+        bool bad = false;
+    };
+    static constexpr size_t MAX_GRAPHS = 64;
+    std::map<std::array<unsigned long long, 5>, Graph> graphs;
+    unsigned long long use_clock = 0;
     hipStream_t cap = nullptr;          // work stream of every step: eager launches, graph capture and replay
     hipEvent_t ev_in = nullptr;
+    GenUnbind gen_unbind_;
+    // captured graphs stay valid while neither the handle's nor this object's workspace was reallocated
+    unsigned long long gen() const { return h->buf_gen.load() + buf_gen.load(); }
     ~pfm_streams() {
         if (ev_in) (void)hipEventDestroy(ev_in);
         for (auto& kv : graphs)
@@ -1587,23 +1645,31 @@ int stream_decoder(pfm_streams* s, const Run& r, int n, int Tw, int L, const SPr
     return PFM_OK;
 }
 
-bool stream_graphs_enabled() {
-    const char* e = getenv("PFM_STREAM_GRAPH");   // 0 = eager launches (A/B, debugging)
-    return !(e && e[0] == '0');
-}
-
 // Run `body` on `st`, through a HIP graph of its launches when `use`: the first step of a shape runs eagerly
 // (one-time launcher setup happens there), the second captures on the object's capture stream and every
-// later one replays. A graph is rebuilt when any workspace buffer was reallocated since its capture.
+// later one replays. A graph is rebuilt when the handle's or the streams object's workspace was reallocated
+// since its capture; graphs are keyed by the calling thread's knob snapshot as well.
 template <class F>
-int stream_graphed(pfm_streams* s, std::array<int, 4> key, bool use, hipStream_t st, F&& body) {
+int stream_graphed(pfm_streams* s, std::array<int, 4> shape, bool use, hipStream_t st, F&& body) {
     if (!use) return body(st);
+    const std::array<unsigned long long, 5> key = {(unsigned long long)shape[0], (unsigned long long)shape[1],
+                                                   (unsigned long long)shape[2], (unsigned long long)shape[3],
+                                                   pfm_knobs().sig};
+    if (!s->graphs.count(key) && s->graphs.size() >= pfm_streams::MAX_GRAPHS) {   // evict the LRU entry
+        auto lru = s->graphs.begin();
+        for (auto it = s->graphs.begin(); it != s->graphs.end(); ++it)
+            if (it->second.last_use < lru->second.last_use) lru = it;
+        if (lru->second.exec) (void)hipGraphExecDestroy(lru->second.exec);
+        s->graphs.erase(lru);
+    }
     auto& g = s->graphs[key];
-    const unsigned long long gen = g_buf_gen.load();
+    g.last_use = ++s->use_clock;
+    const unsigned long long gen = s->gen();
     static const bool log = getenv("PFM_STREAM_GRAPH_LOG") != nullptr;
     if (log)
-        fprintf(stderr, "[stream graph] key %d/%d/%d/%d %s gen %llu/%llu seen %d\n", key[0], key[1], key[2], key[3],
-                g.exec && g.gen == gen ? "replay" : (g.bad || g.seen == 0 ? "eager" : "capture"), g.gen, gen, g.seen);
+        fprintf(stderr, "[stream graph] key %d/%d/%d/%d %s gen %llu/%llu seen %d (%zu graphs)\n", shape[0], shape[1],
+                shape[2], shape[3], g.exec && g.gen == gen ? "replay" : (g.bad || g.seen == 0 ? "eager" : "capture"),
+                g.gen, gen, g.seen, s->graphs.size());
     if (g.exec && g.gen == gen) {
         HIP_TRY(hipGraphLaunch(g.exec, st));
         return PFM_OK;
@@ -1614,7 +1680,7 @@ int stream_graphed(pfm_streams* s, std::array<int, 4> key, bool use, hipStream_t
     const int rc = body(st);
     hipGraph_t graph = nullptr;
     const hipError_t e = hipStreamEndCapture(st, &graph);
-    if (rc != PFM_OK || e != hipSuccess || g_buf_gen.load() != gen) {   // run this step eagerly instead
+    if (rc != PFM_OK || e != hipSuccess || s->gen() != gen) {   // run this step eagerly instead
         if (graph) (void)hipGraphDestroy(graph);
         (void)hipGetLastError();
         if (rc != PFM_OK) return rc;
@@ -1630,10 +1696,8 @@ int stream_graphed(pfm_streams* s, std::array<int, 4> key, bool use, hipStream_t
         return body(st);
     }
     g.gen = gen;
-    {
-        HIP_TRY(hipGraphLaunch(g.exec, st));
-        return PFM_OK;
-    }
+    HIP_TRY(hipGraphLaunch(g.exec, st));
+    return PFM_OK;
 }
 
 int streams_zero(pfm_streams* s, hipStream_t st, int slot) {
@@ -1659,6 +1723,7 @@ extern "C" {
 
 int pfm_streams_create(pfm_handle* h, int slots, const int32_t* chunk_size, int enc_look_back, int dec_look_back,
                        int mode, pfm_streams** out) {
+    pfm_knobs_refresh();
     if (!h || !chunk_size || !out) return fail(PFM_E_ARG, "pfm_streams_create: null argument");
     *out = nullptr;
     const pfm_config& c = h->cfg;
@@ -1718,6 +1783,7 @@ int pfm_streams_reset(pfm_streams* s, void* stream, const int32_t* slot_ids, int
 int pfm_stream_step(pfm_streams* s, void* stream, int n, const int32_t* slot_ids, const float* feats, int Tn,
                     const int32_t* nfeat, const int32_t* is_final, int32_t* tokens, int L_cap, int32_t* ntok_out,
                     float* enc_out, float* alphas_out) {
+    pfm_knobs_refresh();
     if (!s || !slot_ids || !nfeat || !is_final || !tokens || !ntok_out)
         return fail(PFM_E_ARG, "pfm_stream_step: null argument");
     if (n < 1 || Tn < 0 || L_cap < 0) return fail(PFM_E_ARG, "pfm_stream_step: bad sizes");
@@ -1816,7 +1882,7 @@ int pfm_stream_step(pfm_streams* s, void* stream, int n, const int32_t* slot_ids
     const RowMap encmap = rowmap_seg(Tw, (long long)(Tw + 2) * D, D);
     // HIP graphs replace the ~10 launches per encoder layer when no optional output is requested: kernels
     // read every per-step value from `prm`, so one graph per (n, maxn) replays any step of that shape
-    const bool graphs = !enc_out && !alphas_out && !h->prof_on && stream_graphs_enabled();
+    const bool graphs = !enc_out && !alphas_out && !h->prof_on && pfm_knobs().stream_graph;
 
     // ---- phase A: encoder window + SANMEncoderChunkOpt.forward_chunk (scama/encoder.py:456-499) +
     // CifPredictorV2.forward_chunk (cif_predictor.py:255-344) -> acoustic embeds, ntok on the device
@@ -2002,6 +2068,7 @@ int pfm_vad_reset(pfm_vad* v, void* stream) {
 }
 
 int pfm_vad_run(pfm_vad* v, void* stream, const float* feats, int T, float* p_sil, float* probs) {
+    pfm_knobs_refresh();
     if (!v || (T > 0 && (!feats || !p_sil))) return fail(PFM_E_ARG, "pfm_vad_run: null argument");
     if (T < 0) return fail(PFM_E_ARG, "pfm_vad_run: bad T");
     if (v->missing) return fail(PFM_E_STATE, "pfm_vad_run: weights not set");

@@ -113,3 +113,31 @@ static inline int epi_vec_ok(const GemmEpi& e, int N) {
     if (e.out2 && !rowmap_vec4(e.out2_map)) return 0;
     return 1;
 }
+
+// ---- A/B knobs (PFM_* environment variables) ------------------------------------------
+// Read once per top-level C-ABI call on the calling thread (pfm_knobs_refresh at pfm_create, pfm_run,
+// pfm_run_ctc, pfm_run_punc, pfm_stream_step, ...), never per launch. Launchers read the calling
+// thread's snapshot through pfm_knobs(). `sig` hashes every field: captured streaming graphs are keyed
+// by it, so a changed knob never replays a graph recorded under other settings.
+struct PfmKnobs {
+    int ln_fold;            // PFM_LN_FOLD=1: LayerNorm folded into QKV / FFN w1 (fast mode)
+    int gemm_kernel;        // PFM_GEMM_KERNEL=128: force the 128x128 kernel
+    int attn_fsmn;          // PFM_ATTN_FSMN (default 1): encoder FSMN fused into the attention epilogue
+    int attn_waves;         // PFM_ATTN_WAVES (default 8)
+    int attn_pp;            // PFM_ATTN_PP=1: ping-pong 8-wave attention
+    int kv_overlap;         // PFM_KV_OVERLAP (default 1): memory K|V projection on the side stream
+    int gemm_ln;            // PFM_GEMM_LN=1: full-row GEMM + LayerNorm fusion
+    int subbatch;           // PFM_SUBBATCH (default 2): concurrent encoder utterance groups
+    int stream_graph;       // PFM_STREAM_GRAPH (default 1): streaming steps through HIP graphs
+    int fsmn_v2;            // PFM_FSMN_V2: frames per thread of the 8-channel FSMN kernel (0 = 4-channel)
+    int gemm_gm;            // PFM_GEMM_GM: grouped tile order override (-1 = default)
+    int gemm_cfg;           // PFM_GEMM_CFG: forced tile configuration (0 = policy)
+    int gemm_policy;        // PFM_GEMM_POLICY: alternative tile policies (0 = default)
+    int gemm_st16;          // PFM_GEMM_ST16 (default 1): 16-B bf16 epilogue stores
+    int gemm_preres;        // PFM_GEMM_PRERES=1: residual pre-loaded into the accumulators
+    int gemm_resbatch;      // PFM_GEMM_RESBATCH (default 1): residual loads batched ahead of the stores
+    int gemm_skinny;        // PFM_GEMM_SKINNY (default 1): weight-streaming kernel for <= 64-row GEMMs
+    unsigned long long sig;
+};
+const PfmKnobs& pfm_knobs();
+void pfm_knobs_refresh();

@@ -170,15 +170,23 @@ class Paraformer(HipModel):
             ids = toks[i, :n].tolist() if n <= toks.shape[1] else []
             ids = [t for t in ids if t not in (self.eos, self.sos, self.blank_id)]
             if tokenizer is not None:
+                # model.py:567-586: text = tokens2text(ids2tokens(ids)); sentence_postprocess replaces it
+                # only for tokenizers without a `bpemodel` (a SentencepiecesTokenizer keeps tokens2text)
                 toks_i = tokenizer.ids2tokens(ids)
+                text = tokenizer.tokens2text(toks_i)
+                bpe = hasattr(tokenizer, "bpemodel")
                 if pred_ts:
+                    if bpe:   # model.py:580-582 reads time_stamp_postprocessed, which only the non-bpe branch binds
+                        raise UnboundLocalError("pred_timestamp with a bpemodel tokenizer: the reference leaves "
+                                                "time_stamp_postprocessed unbound (paraformer/model.py:580-582)")
                     # the reference passes the CIF peaks as `us_alphas` and the alphas as `us_peaks`
                     _, ts = ts_prediction_lfr6_standard(peaks_h[i], alphas_h[i], list(toks_i),
                                                         vad_offset=kwargs.get("begin_time", 0), upsample_rate=1)
                     text, ts_pp, _ = sentence_postprocess(toks_i, ts)
                     results.append({"key": key[i], "text": text, "timestamp": ts_pp})
                 else:
-                    text, _ = sentence_postprocess(toks_i)
+                    if not bpe:
+                        text, _ = sentence_postprocess(toks_i)
                     results.append({"key": key[i], "text": text})
             else:
                 results.append({"key": key[i], "token_int": ids})

@@ -424,6 +424,36 @@ def save_automodel_sv_tiny():
     print("automodel sv:", {k: [r["text"][:20] for r in v] for k, v in out.items()})
 
 
+def save_automodel_tiny_bpe():
+    """Reference AutoModel.generate() with Paraformer (tiny, vocab 300) + SentencepiecesTokenizer: pins the
+    bpemodel branch of Paraformer.inference (text = tokens2text(ids2tokens(ids)), no sentence_postprocess,
+    paraformer/model.py:567-586)."""
+    import funasr.tokenizer.sentencepiece_tokenizer  # noqa: F401
+    import funasr.frontends.wav_frontend  # noqa: F401
+    from funasr.auto.auto_model import AutoModel
+    bpe = f"{HERE}/sv_bpe.model"
+    if not os.path.exists(bpe):
+        make_sv_bpe(bpe)
+    cfg = paraformer_tiny(vocab_size=300)
+    kw = cfg.reference_kwargs()
+    am = AutoModel(model="Paraformer", model_conf=dict(ctc_weight=0.0, predictor_bias=1),
+                   device="cpu", ncpu=4, disable_update=True, disable_pbar=True, disable_log=True,
+                   tokenizer="SentencepiecesTokenizer", tokenizer_conf=dict(bpemodel=bpe),
+                   frontend="WavFrontend", frontend_conf=dict(fs=16000, window="hamming", n_mels=80,
+                                                             frame_length=25, frame_shift=10, lfr_m=7,
+                                                             lfr_n=6, dither=0.0, cmvn_file=CMVN),
+                   **kw)
+    sd = {k: torch.from_numpy(v) for k, v in make_weights(cfg, seed=0).items()}
+    am.model.load_state_dict(sd, strict=True)
+    feats, lens = fbank_input(seed=11, B=2, T=40, lens=[40, 27])
+    res = am.generate(input=torch.from_numpy(feats), input_len=torch.from_numpy(lens.astype(np.int32))[:, None],
+                      data_type="fbank", key=["uttA", "uttB"])
+    res = [{k: (v if not isinstance(v, np.ndarray) else v.tolist()) for k, v in r.items()} for r in res]
+    with open(f"{HERE}/automodel_tiny_bpe.json", "w") as f:
+        json.dump(res, f, ensure_ascii=False, indent=1)
+    print("automodel bpe:", [r["text"][:40] for r in res])
+
+
 def build_stream_ref(cfg):
     import funasr.models.scama.encoder  # noqa: F401
     import funasr.models.paraformer_streaming.model  # noqa: F401

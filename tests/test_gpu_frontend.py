@@ -122,3 +122,22 @@ def test_automodel_pred_timestamp_matches_reference_generate():
                       data_type="fbank", key=["uttA", "uttB"], pred_timestamp=True)
     want = json.load(open(f"{GOLD}/automodel_tiny_ts.json", encoding="utf-8"))
     assert res == want
+
+
+def test_automodel_bpe_tokenizer_matches_reference_generate():
+    """Paraformer with a SentencepiecesTokenizer (bpemodel): the reference keeps text =
+    tokens2text(ids2tokens(ids)) and skips sentence_postprocess (paraformer/model.py:567-586)."""
+    from funasr_amd.auto_model import AutoModel
+    cfg = paraformer_tiny(vocab_size=300)
+    kw = cfg.reference_kwargs()
+    am = AutoModel(model="Paraformer", model_conf=dict(ctc_weight=0.0, predictor_bias=1), synthetic_seed=0,
+                   tokenizer="SentencepiecesTokenizer", tokenizer_conf=dict(bpemodel=f"{GOLD}/sv_bpe.model"),
+                   device="cuda", mode="exact", **kw)
+    feats, lens = fbank_input(seed=11, B=2, T=40, lens=[40, 27])
+    res = am.generate(input=torch.from_numpy(feats), input_len=torch.from_numpy(lens)[:, None],
+                      data_type="fbank", key=["uttA", "uttB"])
+    want = json.load(open(f"{GOLD}/automodel_tiny_bpe.json", encoding="utf-8"))
+    assert res == want
+    with pytest.raises(UnboundLocalError):   # the reference's bpemodel + pred_timestamp branch
+        am.generate(input=torch.from_numpy(feats), input_len=torch.from_numpy(lens)[:, None],
+                    data_type="fbank", key=["uttA", "uttB"], pred_timestamp=True)

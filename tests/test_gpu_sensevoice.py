@@ -240,3 +240,21 @@ def test_automodel_sensevoice_waveform_path():
         want = tok.decode(want_ids)
         n = min(len(got), len(want))
         assert sum(a == b for a, b in zip(got[:n], want[:n])) >= 0.8 * max(len(got), len(want))
+
+
+def test_oversized_lengths_are_clamped(sv):
+    """fbank lengths > T (and < 0) behave as min(max(len, 0), T), as every other length consumer clamps:
+    the collapse never reads past an utterance's [T + 4] id row (pfm_run_ctc does not validate lens)."""
+    e = sv["tiny"]
+    g = np.load(f"{GOLD}/sv_tiny.npz")
+    x, l = fbank_input(int(g["seed"]), int(g["B"]), int(g["T"]), g["lens"])
+    T = x.shape[1]
+    xs = torch.from_numpy(x).cuda()
+    q = _query(e.cfg)
+    big = torch.tensor([T + 1000, T + 7][: x.shape[0]], dtype=torch.int32).cuda()
+    ok = torch.full((x.shape[0],), T, dtype=torch.int32).cuda()
+    r1 = e.run_ctc(xs, big, q, mode="exact", want_frames=True)
+    r0 = e.run_ctc(xs, ok, q, mode="exact", want_frames=True)
+    torch.cuda.synchronize()
+    assert torch.equal(r1["ntok"], r0["ntok"]) and torch.equal(r1["tokens"], r0["tokens"])
+    assert torch.equal(r1["frame_ids"], r0["frame_ids"])
