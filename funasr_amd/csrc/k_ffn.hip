@@ -1,0 +1,368 @@
+// Fused SAN-M feed-forward sub-layer of the FAST-mode encoder (gfx950), one launch per layer:
+//
+//   x  <- x + W2 . relu(W1 . LN2(x) + b1) + b2          (sanm/encoder.py:138-145,
+//                                                        transformer/positionwise_feed_forward.py:14-34)
+//   xn <- LN1_next(x)  (optional: the next layer's norm1, its QKV projection's bf16 A operand)
+//
+// d_model 512, hidden 2048. One workgroup (8 waves) owns 64 rows end to end:
+//   prologue  LN2 of its rows (f32 two-pass statistics) -> bf16 A image in LDS (64 x 512, 64 KiB)
+//   loop over 8 hidden chunks of 256:
+//     phase 1  H^T[256 x 64] = W1_c . A^T  (16 k32 steps; wave w owns hidden rows 32w..32w+31)
+//              -> relu(+ b1) -> bf16 H image in LDS (64 x 256, 32 KiB)
+//     phase 2  Y^T[512 x 64] += W2_c . H^T (8 k32 steps x two 256-row halves; wave w owns output
+//              columns 32w..32w+31 of each half; accumulators stay in registers for the whole loop)
+//   epilogue  Y^T -> LDS (f32 rows) -> x + Y + b2 (f32 out) and LN1_next -> bf16
+// The 2048-wide hidden activation never leaves the CU: per layer this deletes the H round trip
+// (M x 2048 bf16 written + read) and both standalone LayerNorm passes of the unfused path.
+//
+// Weights stream through a 4-slot LDS ring of 16 KiB tiles by global_load_lds (3 tiles in flight).
+// The tiles are pre-packed once per weight upload (ffn_pack_kernel) into the exact LDS image the
+// fragment reads expect, bank swizzle included, so every DMA is a linear 1 KiB copy per wave.
+// Per chunk: 16 W1 tiles [256 hidden x 32 k] then 16 W2 tiles [256 out x 32 hidden] (k step s,
+// half eta = tile 2s + eta). Tile rows are 64 B (4 x 16-B slots, slot XOR f2(row)).
+// Fragment reads are software-pipelined one tile ahead of the MFMAs (tile t+1's ds_reads are issued
+// right after the barrier that publishes it, while tile t's MFMAs drain).
+#include <stdint.h>
+
+#include "pfm_common.h"
+
+namespace {
+
+typedef __attribute__((address_space(3))) void lds_void;
+typedef const __attribute__((address_space(1))) void gbl_void;
+
+constexpr int FD = 512, FF = 2048, BM = 64, NTH = 512;
+constexpr int HC = 256, NCH = FF / HC;          // hidden chunk, chunks
+constexpr int TILE = 16384, TPC = 32, NTILE = NCH * TPC;
+constexpr int OFF_AN = 0, OFF_H = 65536, OFF_RING = 98304, LDS_BYTES = 163840;
+constexpr int YP = 516;                         // epilogue f32 row pitch (floats)
+
+static_assert(OFF_RING + 4 * TILE == LDS_BYTES, "LDS plan");
+static_assert(BM * YP * 4 <= LDS_BYTES, "epilogue image");
+
+// 64-B tile rows: physical 16-B slot = logical slot ^ f2(row). Conflict-free for 16x16x32 fragment
+// reads (16 consecutive rows, slot = lane >> 4): every ds_read_b128 lane group covers 16 distinct
+// bank positions.
+__device__ __forceinline__ int f2(int row) { return (row >> 2) & 2; }
+
+__device__ __forceinline__ bf16x8 ld128(const unsigned char* p) { return *(const bf16x8*)p; }
+
+__device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ float pick4(float v0, float v1, float v2, float v3, int g) {
+    return g == 0 ? v0 : (g == 1 ? v1 : (g == 2 ? v2 : v3));
+}
+
+struct Frag { bf16x8 w[2]; bf16x8 a[4]; };
+
+// VAR (diagnostic builds, PFM_FFN_VAR): 0 = the kernel; 1 = no weight DMA (stale ring); 2 = no MFMAs;
+// 3 = every tile streams ring tiles 0..3 of the layer (L2-hot 64 KiB); 4 = prologue + epilogue only (no
+// tile loop); 5 = VAR 1 without the per-tile barriers (MFMA + fragment reads alone)
+template <int VAR>
+__global__ __launch_bounds__(NTH) void ffn_fused_kernel(const float* __restrict__ X, int M, const float* __restrict__ g2,
+                                                        const float* __restrict__ be2, float eps,
+                                                        const bf16* __restrict__ Wp, const float* __restrict__ b1,
+                                                        const float* __restrict__ b2, float* Xo,
+                                                        const float* __restrict__ gn, const float* __restrict__ bn,
+                                                        bf16* __restrict__ Xn) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int g = lane >> 4, r16 = lane & 15;
+    const long long m0 = (long long)blockIdx.x * BM;
+
+    auto issue = [&](int t) {
+        if (t >= NTILE || VAR == 1 || VAR == 5) return;
+        const bf16* src = Wp + (long long)(VAR == 3 ? (t & 3) : t) * (TILE / 2) + (2 * w * 64 + lane) * 8;
+        unsigned char* dst = smem + OFF_RING + (t & 3) * TILE + 2 * w * 1024;
+        __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)dst, 16, 0, 0);
+        __builtin_amdgcn_global_load_lds((gbl_void*)(src + 512), (lds_void*)(dst + 1024), 16, 0, 0);
+    };
+    auto bar = [&]() {
+        if (VAR == 5) return;
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    // ---- prologue: LN2 of rows m0 + 8w .. + 7 -> bf16 A image (row pitch 1 KiB, slot ^ (row & 15))
+    {
+        float4 xa[8], xb[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const long long row = min(m0 + 8 * w + i, (long long)M - 1);
+            const float* xr = X + row * FD + 8 * lane;
+            xa[i] = *(const float4*)xr;
+            xb[i] = *(const float4*)(xr + 4);
+        }
+        issue(0);
+        issue(1);
+        issue(2);
+        const float4 ga = *(const float4*)(g2 + 8 * lane), gb = *(const float4*)(g2 + 8 * lane + 4);
+        const float4 ba = *(const float4*)(be2 + 8 * lane), bb = *(const float4*)(be2 + 8 * lane + 4);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            float v[8] = {xa[i].x, xa[i].y, xa[i].z, xa[i].w, xb[i].x, xb[i].y, xb[i].z, xb[i].w};
+            float s = 0.f;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) s += v[e];
+            const float mean = wave_sum(s) * (1.f / FD);
+            float q = 0.f;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) { v[e] -= mean; q += v[e] * v[e]; }
+            const float rstd = 1.f / sqrtf(wave_sum(q) * (1.f / FD) + eps);
+            const float gg[8] = {ga.x, ga.y, ga.z, ga.w, gb.x, gb.y, gb.z, gb.w};
+            const float bbv[8] = {ba.x, ba.y, ba.z, ba.w, bb.x, bb.y, bb.z, bb.w};
+            bf16x8 o;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) o[e] = f2bf(v[e] * rstd * gg[e] + bbv[e]);
+            const int m = 8 * w + i;
+            *(bf16x8*)(smem + OFF_AN + m * 1024 + ((lane ^ (m & 15)) << 4)) = o;
+        }
+    }
+
+    f32x4 acc1[2][4], acc2a[2][4], acc2b[2][4];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) { acc1[i][j][e] = 0.f; acc2a[i][j][e] = 0.f; acc2b[i][j][e] = 0.f; }
+
+    // fragment reads of tile t: weight rows of this wave (ring slot t & 3) + the activation operand
+    // (A image for W1 tiles, H image for W2 tiles)
+    auto rd_w = [&](int t, Frag& f) {
+        const unsigned char* ring = smem + OFF_RING + (t & 3) * TILE;
+#pragma unroll
+        for (int hb = 0; hb < 2; ++hb) {
+            const int row = 32 * w + 16 * hb + r16;
+            f.w[hb] = ld128(ring + row * 64 + ((g ^ f2(row)) << 4));
+        }
+    };
+    auto rd_a = [&](int t, Frag& f) {   // W1 tile t: k step j = t & 15 of the A image
+        const int j = t & 15;
+#pragma unroll
+        for (int mb = 0; mb < 4; ++mb)
+            f.a[mb] = ld128(smem + OFF_AN + (16 * mb + r16) * 1024 + (((4 * j + g) ^ r16) << 4));
+    };
+    auto rd_h = [&](int t, Frag& f) {   // W2 tile t: k step s = (t & 15) >> 1 of the H image
+        const int s2 = (t & 15) >> 1;
+#pragma unroll
+        for (int mb = 0; mb < 4; ++mb)
+            f.a[mb] = ld128(smem + OFF_H + (16 * mb + r16) * 512 + (((4 * s2 + g) ^ r16) << 4));
+    };
+    auto rd1 = [&](int t, Frag& f) { rd_w(t, f); rd_a(t, f); };
+    auto rd2 = [&](int t, Frag& f) { rd_w(t, f); rd_h(t, f); };
+    // relu(H^T + b1) of chunk c -> bf16 H image [64 rows][256 hidden] (row pitch 512 B, slot ^ (row & 15)).
+    // acc1[hb][mb][i] = H^T[hidden 32w + 16hb + 4g + i][row 16mb + r16]. The wave's 32 biases come in by
+    // scalar loads (no vector-memory op beside the in-flight LDS-DMA ring).
+    auto write_h = [&](int c) {
+        const float* bp = b1 + HC * c + 32 * w;
+        float bv[32];
+#pragma unroll
+        for (int k = 0; k < 32; ++k) bv[k] = bp[k];
+#pragma unroll
+        for (int hb = 0; hb < 2; ++hb) {
+            float bi[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                bi[i] = pick4(bv[16 * hb + i], bv[16 * hb + 4 + i], bv[16 * hb + 8 + i], bv[16 * hb + 12 + i], g);
+            const int hl = 32 * w + 16 * hb + 4 * g;
+#pragma unroll
+            for (int mb = 0; mb < 4; ++mb) {
+                const int m = 16 * mb + r16;
+                bf16x4 o;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) o[i] = f2bf(fmaxf(acc1[hb][mb][i] + bi[i], 0.f));
+                *(bf16x4*)(smem + OFF_H + m * 512 + (((hl >> 3) ^ r16) << 4) + ((hl & 7) << 1)) = o;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) acc1[hb][mb][i] = 0.f;
+            }
+        }
+    };
+    auto mm1 = [&](const Frag& f) {
+        if (VAR == 2) { asm volatile("" :: "v"(f.w[0]), "v"(f.w[1]), "v"(f.a[0]), "v"(f.a[1]), "v"(f.a[2]), "v"(f.a[3])); return; }
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int hb = 0; hb < 2; ++hb)
+#pragma unroll
+            for (int mb = 0; mb < 4; ++mb) acc1[hb][mb] = mfma16(f.w[hb], f.a[mb], acc1[hb][mb]);
+        __builtin_amdgcn_s_setprio(0);
+    };
+    auto mm2a = [&](const Frag& f) {
+        if (VAR == 2) { asm volatile("" :: "v"(f.w[0]), "v"(f.w[1]), "v"(f.a[0]), "v"(f.a[1]), "v"(f.a[2]), "v"(f.a[3])); return; }
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+            for (int mb = 0; mb < 4; ++mb) acc2a[nb][mb] = mfma16(f.w[nb], f.a[mb], acc2a[nb][mb]);
+        __builtin_amdgcn_s_setprio(0);
+    };
+    auto mm2b = [&](const Frag& f) {
+        if (VAR == 2) { asm volatile("" :: "v"(f.w[0]), "v"(f.w[1]), "v"(f.a[0]), "v"(f.a[1]), "v"(f.a[2]), "v"(f.a[3])); return; }
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+            for (int mb = 0; mb < 4; ++mb) acc2b[nb][mb] = mfma16(f.w[nb], f.a[mb], acc2b[nb][mb]);
+        __builtin_amdgcn_s_setprio(0);
+    };
+    // top of iteration t: tile t+1 landed (tile t+2 may stay in flight) and visible to every wave, then
+    // the DMA of tile t+3 into the slot of tile t-1 (whose fragments every wave consumed in iteration t-1)
+    auto top = [&](int t) {
+        if (VAR != 1 && VAR != 5) {
+            if (t + 2 < NTILE) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        bar();
+        issue(t + 3);
+    };
+
+    // Software pipeline, iteration t: top(t) -> fragment reads of tile t+1 -> MFMAs of tile t (fragments
+    // read in iteration t-1), so the ds_read latency of the next tile hides under this tile's MFMAs.
+    if (VAR != 1 && VAR != 5) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");   // tile 0 (tiles 1, 2 in flight)
+    bar();
+    Frag F0, F1;
+    rd1(0, F0);
+    for (int c = 0; c < (VAR == 4 ? 0 : NCH); ++c) {
+        const int tb = TPC * c;
+        // phase 1: 16 W1 tiles (H^T of this chunk), fragments alternate F0 / F1
+        for (int j = 0; j < 14; j += 2) {
+            top(tb + j); rd1(tb + j + 1, F1); mm1(F0);
+            top(tb + j + 1); rd1(tb + j + 2, F0); mm1(F1);
+        }
+        top(tb + 14); rd1(tb + 15, F1); mm1(F0);
+        // last W1 tile: H must be complete in LDS before tile tb+16's H fragments are read
+        top(tb + 15); rd_w(tb + 16, F0); mm1(F1); write_h(c); bar(); rd_h(tb + 16, F0);
+        // phase 2: 16 W2 tiles (k step s: half 0 -> acc2a, half 1 -> acc2b)
+        for (int s2 = 0; s2 < 7; ++s2) {
+            const int t = tb + 16 + 2 * s2;
+            top(t); rd2(t + 1, F1); mm2a(F0);
+            top(t + 1); rd2(t + 2, F0); mm2b(F1);
+        }
+        top(tb + 30); rd2(tb + 31, F1); mm2a(F0);
+        if (c + 1 < NCH) { top(tb + 31); rd1(tb + 32, F0); }
+        mm2b(F1);
+    }
+
+    if (VAR == 4) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // ---- epilogue: Y^T accumulators -> f32 row image; x + Y + b2 -> Xo; LN1_next -> Xn
+    float4 xa[8], xb[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const long long row = min(m0 + 8 * w + i, (long long)M - 1);
+        const float* xr = X + row * FD + 8 * lane;
+        xa[i] = *(const float4*)xr;
+        xb[i] = *(const float4*)(xr + 4);
+    }
+    __syncthreads();   // every wave is past its last ring / A / H read (no DMA in flight here)
+    float* Y = (float*)smem;
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+        for (int mb = 0; mb < 4; ++mb) {
+            const int m = 16 * mb + r16;
+            const int n = 32 * w + 16 * nb + 4 * g;
+            *(f32x4*)(Y + m * YP + n) = acc2a[nb][mb];
+            *(f32x4*)(Y + m * YP + 256 + n) = acc2b[nb][mb];
+        }
+    bar();
+    const float4 c2a = *(const float4*)(b2 + 8 * lane), c2b = *(const float4*)(b2 + 8 * lane + 4);
+    float4 na = {0, 0, 0, 0}, nbv = {0, 0, 0, 0}, qa = {0, 0, 0, 0}, qb = {0, 0, 0, 0};
+    if (Xn) {
+        na = *(const float4*)(gn + 8 * lane); nbv = *(const float4*)(gn + 8 * lane + 4);
+        qa = *(const float4*)(bn + 8 * lane); qb = *(const float4*)(bn + 8 * lane + 4);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int m = 8 * w + i;
+        const long long row = m0 + m;
+        const f32x4 ya = *(const f32x4*)(Y + m * YP + 8 * lane), yb = *(const f32x4*)(Y + m * YP + 8 * lane + 4);
+        float v[8] = {ya[0] + c2a.x + xa[i].x, ya[1] + c2a.y + xa[i].y, ya[2] + c2a.z + xa[i].z,
+                      ya[3] + c2a.w + xa[i].w, yb[0] + c2b.x + xb[i].x, yb[1] + c2b.y + xb[i].y,
+                      yb[2] + c2b.z + xb[i].z, yb[3] + c2b.w + xb[i].w};
+        if (row < M) {
+            float* orow = Xo + row * FD + 8 * lane;
+            *(float4*)orow = make_float4(v[0], v[1], v[2], v[3]);
+            *(float4*)(orow + 4) = make_float4(v[4], v[5], v[6], v[7]);
+        }
+        if (Xn) {
+            float s = 0.f;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) s += v[e];
+            const float mean = wave_sum(s) * (1.f / FD);
+            float q = 0.f;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) { v[e] -= mean; q += v[e] * v[e]; }
+            const float rstd = 1.f / sqrtf(wave_sum(q) * (1.f / FD) + eps);
+            const float gg[8] = {na.x, na.y, na.z, na.w, nbv.x, nbv.y, nbv.z, nbv.w};
+            const float bb[8] = {qa.x, qa.y, qa.z, qa.w, qb.x, qb.y, qb.z, qb.w};
+            bf16x8 o;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) o[e] = f2bf(v[e] * rstd * gg[e] + bb[e]);
+            if (row < M) *(bf16x8*)(Xn + row * FD + 8 * lane) = o;
+        }
+    }
+}
+
+// Pack one layer's bf16 W1 [2048][512] / W2 [512][2048] into the 256 ring tiles (16 KiB each) in
+// LDS-image order. Tile t: chunk c = t >> 5; t & 16 ? W2 tile (k step s = (t & 15) >> 1, half eta = t & 1)
+// : W1 tile (k step t & 15). Unit u (16 B) of a tile: row u >> 2, physical slot u & 3 holding logical
+// slot (u & 3) ^ f2(row), i.e. 8 consecutive k.
+__global__ __launch_bounds__(256) void ffn_pack_kernel(const bf16* __restrict__ W1, const bf16* __restrict__ W2,
+                                                       bf16* __restrict__ Wp) {
+    const int gid = blockIdx.x * 256 + threadIdx.x;   // < NTILE * 1024
+    const int t = gid >> 10, u = gid & 1023;
+    const int c = t >> 5, j = t & 15, row = u >> 2, ls = (u & 3) ^ f2(row);
+    const bf16* src;
+    if (t & 16) {
+        const int s = j >> 1, eta = j & 1;
+        src = W2 + (long long)(256 * eta + row) * FF + HC * c + 32 * s + 8 * ls;
+    } else {
+        src = W1 + (long long)(HC * c + row) * FD + 32 * j + 8 * ls;
+    }
+    *(bf16x8*)(Wp + (long long)gid * 8) = *(const bf16x8*)src;
+}
+
+}  // namespace
+
+size_t pfm_ffn_packed_elems() { return (size_t)NTILE * TILE / 2; }
+
+hipError_t pfm_ffn_pack(const bf16* W1, const bf16* W2, bf16* Wp, hipStream_t st) {
+    hipLaunchKernelGGL(ffn_pack_kernel, dim3(NTILE * 1024 / 256), dim3(256), 0, st, W1, W2, Wp);
+    PFM_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+// x [M, 512] f32 (read), xo [M, 512] f32 (may alias x: every workgroup reads its rows before writing
+// them), Wp = pfm_ffn_pack output; gn / bn / xn optional (all three or none).
+hipError_t pfm_ffn_fused(const float* x, int M, const float* g2, const float* be2, float eps, const bf16* Wp,
+                         const float* b1, const float* b2, float* xo, const float* gn, const float* bn, bf16* xn,
+                         hipStream_t st) {
+    if (M <= 0) return hipSuccess;
+    if ((xn != nullptr) != (gn != nullptr && bn != nullptr)) return hipErrorInvalidValue;
+    if (((uintptr_t)x | (uintptr_t)xo | (uintptr_t)Wp | (uintptr_t)xn) % 16) return hipErrorInvalidValue;
+    static bool attr_done = false;
+    if (!attr_done) {
+        attr_done = true;
+        (void)hipFuncSetAttribute((const void*)ffn_fused_kernel<0>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+        (void)hipFuncSetAttribute((const void*)ffn_fused_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+        (void)hipFuncSetAttribute((const void*)ffn_fused_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+        (void)hipFuncSetAttribute((const void*)ffn_fused_kernel<3>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+        (void)hipFuncSetAttribute((const void*)ffn_fused_kernel<4>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+        (void)hipFuncSetAttribute((const void*)ffn_fused_kernel<5>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+    }
+    const dim3 grid((M + BM - 1) / BM), blk(NTH);
+    switch (pfm_knobs().ffn_var) {
+        case 1: hipLaunchKernelGGL(ffn_fused_kernel<1>, grid, blk, LDS_BYTES, st, x, M, g2, be2, eps, Wp, b1, b2, xo, gn, bn, xn); break;
+        case 2: hipLaunchKernelGGL(ffn_fused_kernel<2>, grid, blk, LDS_BYTES, st, x, M, g2, be2, eps, Wp, b1, b2, xo, gn, bn, xn); break;
+        case 3: hipLaunchKernelGGL(ffn_fused_kernel<3>, grid, blk, LDS_BYTES, st, x, M, g2, be2, eps, Wp, b1, b2, xo, gn, bn, xn); break;
+        case 4: hipLaunchKernelGGL(ffn_fused_kernel<4>, grid, blk, LDS_BYTES, st, x, M, g2, be2, eps, Wp, b1, b2, xo, gn, bn, xn); break;
+        case 5: hipLaunchKernelGGL(ffn_fused_kernel<5>, grid, blk, LDS_BYTES, st, x, M, g2, be2, eps, Wp, b1, b2, xo, gn, bn, xn); break;
+        default: hipLaunchKernelGGL(ffn_fused_kernel<0>, grid, blk, LDS_BYTES, st, x, M, g2, be2, eps, Wp, b1, b2, xo, gn, bn, xn);
+    }
+    PFM_LAUNCH_CHECK();
+    return hipSuccess;
+}

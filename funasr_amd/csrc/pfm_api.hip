@@ -61,6 +61,11 @@ hipError_t pfm_sv_input(const float* feats, const int* lens, const float* embed,
 hipError_t pfm_ctc_collapse(const int* ids, long long ld, const int* olen, int B, int blank, int Lcap, int* tokens,
                             int* ntok, hipStream_t st);
 hipError_t pfm_f32_to_bf16(const float* x, bf16* y, long long n, hipStream_t st);
+size_t pfm_ffn_packed_elems();
+hipError_t pfm_ffn_pack(const bf16* W1, const bf16* W2, bf16* Wp, hipStream_t st);
+hipError_t pfm_ffn_fused(const float* x, int M, const float* g2, const float* be2, float eps, const bf16* Wp,
+                         const float* b1, const float* b2, float* xo, const float* gn, const float* bn, bf16* xn,
+                         hipStream_t st);
 hipError_t pfm_fbank_launch(const float* wav, const int* nsamp, int B, int S_max, const float* cmvn,
                             const unsigned char* tables, float* fb_ws, int N_cap, float* feats, int T_cap, int* T_out,
                             hipStream_t st);
@@ -100,7 +105,7 @@ static int fail(int code, const std::string& msg) {
             return fail(PFM_E_HIP, std::string(#expr) + ": " + hipGetErrorString(_e));           \
     } while (0)
 
-static thread_local PfmKnobs t_knobs = {0, 0, 1, 8, 0, 1, 0, 2, 1, 0, -1, 0, 0, 1, 0, 1, 1, 0};
+static thread_local PfmKnobs t_knobs = {0, 0, 1, 8, 0, 1, 0, 2, 1, 0, -1, 0, 0, 1, 0, 1, 1, 1, 0, 0};
 
 const PfmKnobs& pfm_knobs() { return t_knobs; }
 
@@ -127,9 +132,11 @@ void pfm_knobs_refresh() {
     k.gemm_preres = iv("PFM_GEMM_PRERES", 0) == 1;
     k.gemm_resbatch = iv("PFM_GEMM_RESBATCH", 1) != 0;
     k.gemm_skinny = iv("PFM_GEMM_SKINNY", 1) != 0;
+    k.ffn_fused = iv("PFM_FFN_FUSED", 1) != 0;
+    k.ffn_var = iv("PFM_FFN_VAR", 0);
     const int* f = &k.ln_fold;
     unsigned long long s = 1469598103934665603ull;   // FNV-1a over the fields
-    for (int i = 0; i < 17; ++i) s = (s ^ (unsigned long long)(unsigned)f[i]) * 1099511628211ull;
+    for (int i = 0; i < 19; ++i) s = (s ^ (unsigned long long)(unsigned)f[i]) * 1099511628211ull;
     k.sig = s;
     t_knobs = k;
 }
@@ -175,6 +182,7 @@ struct WEntry {
 struct EncLayer {
     size_t ln1g, ln1b, wqkv, bqkv, wo, bo, fsmn, ln2g, ln2b, w1, b1, w2, b2;
     int din;
+    size_t ffp = 0;   // fast mode: element offset of the packed W1 | W2 ring tiles in ffn_pack (k_ffn.hip)
     // fast mode, LayerNorm folded into QKV (norm1) and FFN w1 (norm2): bf16(W o gamma) in fold_w,
     // column sums / folded biases in fold_f (element offsets)
     size_t fq_w = 0, fq_cs = 0, fq_cb = 0, f1_w = 0, f1_cs = 0, f1_cb = 0;
@@ -194,6 +202,8 @@ struct pfm_handle {
     DevBuf arena_bf;               // bf16 copies of GEMM weights (same element offsets)
     DevBuf fold_w, fold_f;         // LayerNorm-folded projection weights (bf16) and column terms (f32)
     bool fold_ready = false;
+    DevBuf ffn_pack;               // fused-FFN weight tiles of every encoder layer (bf16, LDS-image order)
+    bool ffn_ready = false;
     std::vector<std::pair<size_t, size_t>> gemm_ranges;   // (off, numel) converted to bf16
     bool bf_ready = false;
     int missing = 0;
@@ -384,6 +394,9 @@ void make_pe(std::vector<float>& pe, int T, int depth) {
 // statistics reductions cost more than the two LN passes they delete).
 bool ln_fold_enabled() { return pfm_knobs().ln_fold; }
 
+// the fused FFN kernel is written for the Paraformer / SenseVoice encoder width (512 -> 2048 -> 512)
+bool ffn_shape_ok(const pfm_config& c) { return c.d_model == 512 && c.ffn == 2048; }
+
 int ensure_bf16(pfm_handle* h, hipStream_t st) {
     if (!h->bf_ready) {
         HIP_TRY(h->arena_bf.ensure(h->arena_elems * sizeof(bf16)));
@@ -412,6 +425,15 @@ int ensure_bf16(pfm_handle* h, hipStream_t st) {
                                 ff + L.f1_cb, st));
         }
         h->fold_ready = true;
+    }
+    if (!h->ffn_ready && ffn_shape_ok(h->cfg) && pfm_knobs().ffn_fused && !h->enc.empty()) {
+        const size_t per = pfm_ffn_packed_elems();
+        HIP_TRY(h->ffn_pack.ensure(h->enc.size() * per * sizeof(bf16)));
+        for (size_t l = 0; l < h->enc.size(); ++l) {
+            h->enc[l].ffp = l * per;
+            HIP_TRY(pfm_ffn_pack(h->wb(h->enc[l].w1), h->wb(h->enc[l].w2), h->ffn_pack.as<bf16>() + l * per, st));
+        }
+        h->ffn_ready = true;
     }
     return PFM_OK;
 }
@@ -706,6 +728,9 @@ int encoder_stack(const Run& r, const float* x_in, const int* lens, int B, int T
         e.out2 = Xn; e.out2_map = rowmap_plain(D);   // bf16(x): the folded consumer's A operand
         e.ln_st_out = st; e.ln_parts = D / 64;
     };
+    // fast mode, full-size batches: LN2 -> FFN -> residual -> next layer's LN1 as ONE kernel per layer
+    // (k_ffn.hip); chunk-sized streaming steps keep the weight-streaming GEMMs
+    const bool ffn_fused = fast && !r.fuse_ln && !fold && h->ffn_ready && pfm_knobs().ffn_fused && M >= 4096;
     for (int l = l0; l < l1; ++l) {
         const EncLayer& L = h->enc[l];
         const int din = L.din;
@@ -716,7 +741,7 @@ int encoder_stack(const Run& r, const float* x_in, const int* lens, int B, int T
             HIP_TRY(pfm_layernorm(x_in, rowmap_plain(I), (int)M, I, r.P(L.ln1g), r.P(L.ln1b), c.ln_eps,
                                   h->pe.as<float>(), T, sqrtf((float)D), Xn, rowmap_plain(I), dt, nullptr, plain, 0,
                                   st));
-        else if ((!r.fuse_ln || l == l0) && !(fold && l > l0))   // fused / folded: no standalone LN1
+        else if ((!r.fuse_ln || l == l0) && !(fold && l > l0) && !(ffn_fused && l > l0))   // fused / folded: no LN1
             HIP_TRY(pfm_layernorm(X, rowmap_plain(D), (int)M, D, r.P(L.ln1g), r.P(L.ln1b), c.ln_eps, nullptr, 0, 1.f,
                                   Xn, rowmap_plain(D), dt, nullptr, plain, 0, st));
         {   // q|k|v = LN1(x) Wqkv^T + b   (fast mode: bf16 only — attention and FSMN read bf16)
@@ -783,10 +808,20 @@ int encoder_stack(const Run& r, const float* x_in, const int* lens, int B, int T
                 if (fold) stats_out(e, ws.st2);
                 HIP_TRY(r.gemm(dt, fast ? (const void*)Ob : (const void*)O, rowmap_plain(D), r.W(L.wo), D, (int)M, D,
                                D, e));
-                if (!fold)
+                if (!fold && !ffn_fused)
                     HIP_TRY(pfm_layernorm(X, rowmap_plain(D), (int)M, D, r.P(L.ln2g), r.P(L.ln2b), c.ln_eps, nullptr,
                                           0, 1.f, Xn, rowmap_plain(D), dt, nullptr, plain, 0, st));
             }
+        }
+        if (ffn_fused) {   // x = x + W2 relu(W1 LN2(x) + b1) + b2 ; Xn = LN1_{l+1}(x)
+            const bool nxt = l + 1 < l1;
+            const double fl = 4.0 * M * (double)D * Fd;
+            const double by = (double)M * D * (4.0 + 4.0 + (nxt ? 2.0 : 0.0)) + 2.0 * 2.0 * D * Fd;
+            ProfScope ps(h, st, PFM_K_GEMM, fl, by);
+            HIP_TRY(pfm_ffn_fused(X, (int)M, r.P(L.ln2g), r.P(L.ln2b), c.ln_eps, h->ffn_pack.as<bf16>() + L.ffp,
+                                  r.P(L.b1), r.P(L.b2), X, nxt ? r.P(h->enc[l + 1].ln1g) : nullptr,
+                                  nxt ? r.P(h->enc[l + 1].ln1b) : nullptr, nxt ? (bf16*)Xn : nullptr, st));
+            continue;
         }
         {   // h = relu(LN2(x) W1^T + b1)
             GemmEpi e = epi_default();
@@ -981,6 +1016,7 @@ int pfm_set_weight(pfm_handle* h, const char* name, const void* host_ptr, int dt
     if (!e.set) { e.set = true; h->missing--; }
     h->bf_ready = false;
     h->fold_ready = false;
+    h->ffn_ready = false;
     h->ban_tok = -1;   // the banned-token bias copy follows ctc.ctc_lo.bias
     return PFM_OK;
 }
@@ -1416,6 +1452,29 @@ int pfm_op_gemm(void* stream, int dtype, const void* A, const void* Wt, const fl
     if (res) { e.res0 = res; e.ld_res0 = N; }
     e.out = C; e.out_map = rowmap_plain(N); e.out_dtype = (act & 2) ? DT_BF16 : DT_F32;
     HIP_TRY(gemm_dispatch(dtype, A, rowmap_plain(K), Wt, K, M, N, K, e, (hipStream_t)stream));
+    return PFM_OK;
+}
+
+int pfm_op_ffn(void* stream, const float* x, int M, const float* g2, const float* b2n, float eps, const float* W1,
+               const float* b1, const float* W2, const float* b2, float* xo, const float* gn, const float* bn,
+               void* xn) {
+    pfm_knobs_refresh();
+    if (!x || !xo || !W1 || !W2 || M < 0) return fail(PFM_E_ARG, "pfm_op_ffn: null operand");
+    const hipStream_t st = (hipStream_t)stream;
+    const size_t nw = (size_t)2048 * 512;
+    bf16 *w1b = nullptr, *w2b = nullptr, *wp = nullptr;
+    HIP_TRY(hipMalloc(&w1b, nw * sizeof(bf16)));
+    HIP_TRY(hipMalloc(&w2b, nw * sizeof(bf16)));
+    HIP_TRY(hipMalloc(&wp, pfm_ffn_packed_elems() * sizeof(bf16)));
+    hipError_t e = pfm_f32_to_bf16(W1, w1b, (long long)nw, st);
+    if (e == hipSuccess) e = pfm_f32_to_bf16(W2, w2b, (long long)nw, st);
+    if (e == hipSuccess) e = pfm_ffn_pack(w1b, w2b, wp, st);
+    if (e == hipSuccess) e = pfm_ffn_fused(x, M, g2, b2n, eps, wp, b1, b2, xo, gn, bn, (bf16*)xn, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    (void)hipFree(w1b);
+    (void)hipFree(w2b);
+    (void)hipFree(wp);
+    if (e != hipSuccess) return fail(PFM_E_HIP, std::string("pfm_op_ffn: ") + hipGetErrorString(e));
     return PFM_OK;
 }
 

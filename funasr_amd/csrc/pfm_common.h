@@ -137,6 +137,8 @@ struct PfmKnobs {
     int gemm_preres;        // PFM_GEMM_PRERES=1: residual pre-loaded into the accumulators
     int gemm_resbatch;      // PFM_GEMM_RESBATCH (default 1): residual loads batched ahead of the stores
     int gemm_skinny;        // PFM_GEMM_SKINNY (default 1): weight-streaming kernel for <= 64-row GEMMs
+    int ffn_fused;          // PFM_FFN_FUSED (default 1): fused LN2 + FFN + LN1_next encoder kernel (k_ffn.hip)
+    int ffn_var;            // PFM_FFN_VAR: diagnostic variants of the fused FFN kernel (0 = the kernel)
     unsigned long long sig;
 };
 const PfmKnobs& pfm_knobs();

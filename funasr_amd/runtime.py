@@ -25,7 +25,7 @@ MODES = {"exact": MODE_EXACT, "fp32": MODE_EXACT, "fast": MODE_FAST, "bf16": MOD
 # every symbol include/pfm.h declares (checked by tests/test_abi.py)
 ABI_SYMBOLS = ("pfm_config_default", "pfm_config_sensevoice", "pfm_create", "pfm_set_weight",
                "pfm_missing_weights", "pfm_reserve", "pfm_run", "pfm_run_ctc", "pfm_op_ctc_collapse", "pfm_fbank", "pfm_lfr_frames", "pfm_last_error", "pfm_destroy", "pfm_op_gemm",
-               "pfm_op_attention", "pfm_op_layernorm", "pfm_op_fsmn", "pfm_op_cif", "pfm_profile", "pfm_op_gemm_layernorm", "pfm_op_fsmn_bf16", "pfm_op_layernorm_bf16",
+               "pfm_op_attention", "pfm_op_layernorm", "pfm_op_fsmn", "pfm_op_cif", "pfm_profile", "pfm_op_gemm_layernorm", "pfm_op_ffn", "pfm_op_fsmn_bf16", "pfm_op_layernorm_bf16",
                "pfm_profile_read", "pfm_streams_create", "pfm_streams_reset", "pfm_stream_step",
                "pfm_streams_destroy", "pfm_fbank_raw", "pfm_lfr_gather", "pfm_config_punc", "pfm_run_punc", "pfm_vad_config_default", "pfm_vad_create",
                "pfm_vad_set_weight", "pfm_vad_missing_weights", "pfm_vad_reset", "pfm_vad_run", "pfm_vad_destroy", "pfm_vad_fbank_raw",
@@ -116,6 +116,8 @@ def load_library(path: Optional[str] = None) -> ctypes.CDLL:
     lib.pfm_op_fsmn_bf16.argtypes = [vp, vp, i32p, f32p, vp, i32, i32, i32, i32, i32]
     lib.pfm_op_gemm_layernorm.argtypes = [vp, vp, vp, f32p, f32p, f32p, f32p, f32p, ctypes.c_float, f32p, i32, i32,
                                           i32]
+    lib.pfm_op_ffn.argtypes = [vp, f32p, i32, f32p, f32p, ctypes.c_float, f32p, f32p, f32p, f32p, f32p, f32p, f32p,
+                               vp]
     lib.pfm_streams_create.argtypes = [vp, i32, ctypes.POINTER(ctypes.c_int32), i32, i32, i32, ctypes.POINTER(vp)]
     lib.pfm_streams_reset.argtypes = [vp, vp, ctypes.POINTER(ctypes.c_int32), i32]
     lib.pfm_stream_step.argtypes = [vp, vp, i32, ctypes.POINTER(ctypes.c_int32), f32p, i32,
@@ -438,6 +440,20 @@ def op_gemm_layernorm(A, W, gamma, beta, eps, bias=None, res=None, want_x=False)
                                     _ptr(bias), _ptr(res), _ptr(C), _ptr(gamma), _ptr(beta), ctypes.c_float(eps),
                                     _ptr(Y), M, N, K), "pfm_op_gemm_layernorm")
     return (Y, C) if want_x else Y
+
+
+def op_ffn(x, g2, b2n, eps, W1, b1, W2, b2, gn=None, bn=None):
+    """Fused encoder FFN sub-layer (pfm_op_ffn): x [M,512] f32 -> (x + W2 relu(W1 LN2(x) + b1) + b2,
+    LN_next(that) as bf16 or None)."""
+    import torch
+    lib = load_library()
+    M = x.shape[0]
+    xo = torch.empty_like(x)
+    xn = torch.empty((M, 512), dtype=torch.bfloat16, device=x.device) if gn is not None else None
+    check(lib.pfm_op_ffn(_stream_ptr(torch, x.device), _ptr(x.contiguous()), M, _ptr(g2), _ptr(b2n),
+                         ctypes.c_float(eps), _ptr(W1.contiguous()), _ptr(b1), _ptr(W2.contiguous()), _ptr(b2),
+                         _ptr(xo), _ptr(gn), _ptr(bn), _ptr(xn)), "pfm_op_ffn")
+    return xo, xn
 
 
 def op_attention(q, k, v, klen, B, Tq, Tk, heads, scale):

@@ -297,6 +297,16 @@ int pfm_op_gemm_layernorm(void* stream, const void* A, const void* W, const floa
                           float* C, const float* gamma, const float* beta, float eps, float* Y, int M, int N,
                           int K);
 
+/* Fused encoder feed-forward sub-layer (fast mode, bf16 MFMA, f32 accumulate / residual / statistics):
+ *   x  = x + W2 relu(W1 LayerNorm2(x) + b1) + b2          -> xo [M, 512] f32 (may alias x)
+ *   xn = LayerNorm_next(x) as bf16 [M, 512]               (optional: gn, bn, xn all non-null)
+ * W1 f32 [2048, 512], W2 f32 [512, 2048] (torch Linear layout; converted to bf16 and packed per call).
+ * Replaces EncoderLayerSANM's norm2 -> feed_forward -> residual (sanm/encoder.py:138-145,
+ * transformer/positionwise_feed_forward.py:14-34) followed by the next layer's norm1 (encoder.py:114). */
+int pfm_op_ffn(void* stream, const float* x, int M, const float* g2, const float* b2n, float eps, const float* W1,
+               const float* b1, const float* W2, const float* b2, float* xo, const float* gn, const float* bn,
+               void* xn);
+
 /* Masked attention per (batch, head): q [B*Tq, heads*128], k/v [B*Tk, heads*128] of dtype,
  * klen [B] int32; out f32 [B*Tq, heads*128]. */
 int pfm_op_attention(void* stream, int dtype, const void* q, const void* k, const void* v,

@@ -269,3 +269,47 @@ def test_cif_bit_exact(dev):
     L = want_emb.shape[1]
     assert torch.equal(emb.cpu()[:, :L], want_emb)
     assert float(emb.cpu()[:, L:].abs().max() if emb.shape[1] > L else 0.0) == 0.0
+
+
+def _ffn_ref(x, g2, b2n, eps, W1b, b1, W2b, b2):
+    """fp64 restatement of the fused FFN sub-layer on the kernel's bf16 operand roundings:
+    A = bf16(LN2(x)), H = bf16(relu(A W1^T + b1)), y = x + H W2^T + b2."""
+    xd = x.double()
+    mu = xd.mean(-1, keepdim=True)
+    var = ((xd - mu) ** 2).mean(-1, keepdim=True)
+    a = ((xd - mu) / torch.sqrt(var + eps) * g2.double() + b2n.double()).bfloat16().double()
+    h = torch.relu(a @ W1b.double().T + b1.double()).bfloat16().double()
+    return xd + h @ W2b.double().T + b2.double()
+
+
+@pytest.mark.parametrize("M", [64, 200, 1000])
+@pytest.mark.parametrize("with_next", [False, True])
+def test_ffn_fused(dev, M, with_next):
+    """Fused LN2 -> W1 -> relu -> W2 -> residual (-> next LN, bf16) vs fp64 torch on the same bf16 weights:
+    FFN increment (y - x) within rel-L2 5e-3 (f32 accumulation order flips a few bf16 roundings of the
+    hidden activation), y within rel 1e-4; the next-layer LayerNorm of the kernel's own y within 1.6e-2
+    abs (one bf16 ulp at |v| <= 4); rows beyond M untouched by construction (ragged M)."""
+    g = torch.Generator().manual_seed(M + 7 * with_next)
+    x = torch.randn(M, 512, generator=g) * 2
+    g2 = 1 + 0.1 * torch.randn(512, generator=g)
+    b2n = 0.1 * torch.randn(512, generator=g)
+    W1 = torch.randn(2048, 512, generator=g) / 512 ** 0.5
+    b1 = 0.1 * torch.randn(2048, generator=g)
+    W2 = torch.randn(512, 2048, generator=g) / 2048 ** 0.5
+    b2 = 0.1 * torch.randn(512, generator=g)
+    gn = 1 + 0.1 * torch.randn(512, generator=g) if with_next else None
+    bn = 0.1 * torch.randn(512, generator=g) if with_next else None
+    d = lambda t: None if t is None else t.to(dev)  # noqa: E731
+    y, xn = rt.op_ffn(d(x), d(g2), d(b2n), 1e-12, d(W1), d(b1), d(W2), d(b2), d(gn), d(bn))
+    torch.cuda.synchronize()
+    want = _ffn_ref(x, g2, b2n, 1e-12, W1.bfloat16(), b1, W2.bfloat16(), b2)
+    yc = y.double().cpu()
+    assert rel(yc - x.double(), want - x.double()) < 5e-3
+    assert rel(yc, want) < 1e-4
+    if with_next:
+        mu = yc.mean(-1, keepdim=True)
+        var = ((yc - mu) ** 2).mean(-1, keepdim=True)
+        ln = (yc - mu) / torch.sqrt(var + 1e-12) * gn.double() + bn.double()
+        assert (xn.double().cpu() - ln).abs().max().item() < 1.6e-2
+    else:
+        assert xn is None
