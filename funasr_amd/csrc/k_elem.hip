@@ -809,6 +809,75 @@ hipError_t pfm_fill_i32(int* p, long long n, int v, hipStream_t st) {
     return hipSuccess;
 }
 
+// ------------------------------------------------------------------------------------------
+// Three-way bf16 split of f32 operands for the split-bf16 emulation of EXACT-mode GEMMs:
+//   x0 = bf16(x), x1 = bf16(x - x0), x2 = bf16(x - x0 - x1)  =>  x0 + x1 + x2 == x exactly (normal range;
+// each residual is exact in f32 and has <= 8 significant bits left for x2). With these,
+//   a.w ~= a0w0 + a0w1 + a1w0 + a0w2 + a1w1 + a2w0   (dropped terms <= 2^-25 |a w|; bf16 products exact)
+// so six bf16 MFMAs with f32 accumulation reproduce the f32 product to f32 rounding.
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ void split3(float x, bf16& a, bf16& b, bf16& c) {
+    a = f2bf(x);
+    const float r1 = x - bf2f(a);
+    b = f2bf(r1);
+    c = f2bf(r1 - bf2f(b));
+}
+
+// rows of x (RowMap, K columns) -> out [M][3 Kp] = [x0 | x1 | x2], segments zero-padded to Kp >= K columns;
+// 4 columns per thread
+__global__ __launch_bounds__(256) void split3_rows_kernel(const float* __restrict__ x, RowMap xm, int M, int K, int Kp,
+                                                          bf16* __restrict__ out) {
+    const int k4 = Kp >> 2;
+    const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (i >= (long long)M * k4) return;
+    const long long row = i / k4;
+    const int c = (int)(i - row * k4) * 4;
+    const float4 v = c < K ? *(const float4*)(x + xm.off(row) + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+    const float xv[4] = {v.x, v.y, v.z, v.w};
+    bf16x4 p0, p1, p2;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        bf16 a, b, cc;
+        split3(xv[e], a, b, cc);
+        p0[e] = a;
+        p1[e] = b;
+        p2[e] = cc;
+    }
+    bf16* o = out + row * 3 * Kp + c;
+    *(bf16x4*)o = p0;
+    *(bf16x4*)(o + Kp) = p1;
+    *(bf16x4*)(o + 2 * Kp) = p2;
+}
+
+// n contiguous f32 -> planes p, p + plane, p + 2 plane (weights: plane stride = the arena size)
+__global__ __launch_bounds__(256) void split3_planes_kernel(const float* __restrict__ x, bf16* __restrict__ p,
+                                                            long long plane, long long n) {
+    const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    bf16 a, b, c;
+    split3(x[i], a, b, c);
+    p[i] = a;
+    p[plane + i] = b;
+    p[2 * plane + i] = c;
+}
+
+hipError_t pfm_split3_rows(const float* x, RowMap xm, int M, int K, int Kp, bf16* out, hipStream_t st) {
+    if (M <= 0) return hipSuccess;
+    if (K % 4 || Kp % 4 || Kp < K || !rowmap_vec4(xm) || ((uintptr_t)x % 16) || ((uintptr_t)out % 8))
+        return hipErrorInvalidValue;
+    const long long n = (long long)M * (Kp / 4);
+    hipLaunchKernelGGL(split3_rows_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, x, xm, M, K, Kp, out);
+    PFM_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+hipError_t pfm_split3_planes(const float* x, bf16* p, long long plane, long long n, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(split3_planes_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, x, p, plane, n);
+    PFM_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
 hipError_t pfm_f32_to_bf16(const float* x, bf16* y, long long n, hipStream_t st) {
     if (n <= 0) return hipSuccess;
     const long long nt = (n + 3) / 4;

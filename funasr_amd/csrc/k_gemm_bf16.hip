@@ -104,15 +104,31 @@ __global__ __launch_bounds__(C::NT) void gemm_bf16_kernel(const bf16* __restrict
             gw[j] = W + (long long)min(n0 + row, N - 1) * ldw + (slot ^ C::swz(row)) * 8;
         }
     }
+    // split-bf16 emulation of an f32 GEMM (epi.x6_k > 0): K step k0 of the K' = 6 x6_k loop reads A
+    // segment pa = {2,1,0,1,0,0}[s] and W plane pw = {0,1,2,0,1,0}[s] of segment s = k0 / x6_k (a K step
+    // never straddles segments: x6_k % BK == 0). Small products first.
+    const int xk = epi.x6_k;
+    auto koff_a = [&](int k0) -> int {
+        if (!xk) return k0;
+        const int sg = k0 / xk, kk = k0 - sg * xk;
+        return (sg == 0 ? 2 : (sg == 1 || sg == 3) ? 1 : 0) * xk + kk;
+    };
+    auto koff_w = [&](int k0) -> long long {
+        if (!xk) return k0;
+        const int sg = k0 / xk, kk = k0 - sg * xk;
+        return (long long)(sg == 1 || sg == 4 ? 1 : sg == 2 ? 2 : 0) * epi.x6_ws + kk;
+    };
     auto stage = [&](int k0, int s) {
         unsigned char* base = smem + s * C::STAGE;
+        const int ka = koff_a(k0);
+        const long long kw = koff_w(k0);
 #pragma unroll
         for (int j = 0; j < PA; ++j)
-            __builtin_amdgcn_global_load_lds((gbl_void*)(ga[j] + k0), (lds_void*)(base + (PA * wid + j) * 1024), 16,
+            __builtin_amdgcn_global_load_lds((gbl_void*)(ga[j] + ka), (lds_void*)(base + (PA * wid + j) * 1024), 16,
                                              0, 0);
 #pragma unroll
         for (int j = 0; j < PW; ++j)
-            __builtin_amdgcn_global_load_lds((gbl_void*)(gw[j] + k0),
+            __builtin_amdgcn_global_load_lds((gbl_void*)(gw[j] + kw),
                                              (lds_void*)(base + C::TA + (PW * wid + j) * 1024), 16, 0, 0);
     };
 
@@ -201,9 +217,10 @@ __global__ __launch_bounds__(C::NT) void gemm_bf16_kernel(const bf16* __restrict
         auto issue = [&](int tile, int op) -> bool {
             if (tile >= nk) return false;
             unsigned char* base = smem + (tile & 3) * C::STAGE + op * C::TA;
+            const long long ko = op ? koff_w(tile * BK) : (long long)koff_a(tile * BK);
 #pragma unroll
             for (int j = 0; j < 2; ++j)
-                __builtin_amdgcn_global_load_lds((gbl_void*)(osrc[op][j] + tile * BK),
+                __builtin_amdgcn_global_load_lds((gbl_void*)(osrc[op][j] + ko),
                                                  (lds_void*)(base + (2 * wid + j) * 1024), 16, 0, 0);
             return true;
         };
@@ -288,10 +305,10 @@ __global__ __launch_bounds__(C::NT) void gemm_bf16_kernel(const bf16* __restrict
         auto issue = [&](int tile, int hh) -> bool {
             if (tile >= nk) return false;
             unsigned char* base = smem + (tile & 1) * C::STAGE + (hh >> 1) * C::TA + (hh & 1) * 16384;
-            const int k0 = tile * BK;
+            const long long ko = (hh >> 1) ? koff_w(tile * BK) : (long long)koff_a(tile * BK);
 #pragma unroll
             for (int j = 0; j < 2; ++j)
-                __builtin_amdgcn_global_load_lds((gbl_void*)(hsrc[hh][j] + k0),
+                __builtin_amdgcn_global_load_lds((gbl_void*)(hsrc[hh][j] + ko),
                                                  (lds_void*)(base + (2 * wid + j) * 1024), 16, 0, 0);
             return true;
         };
@@ -1319,7 +1336,8 @@ hipError_t pfm_gemm_bf16_256(const void* A, RowMap amap, const void* W, long lon
     }
     const bool ln = e2.ln_st_in || e2.ln_st_out;
     int cfg = pick_cfg(M, N, K, epi.amax_val != nullptr);
-    if (ln && cfg != 4 && cfg != 15 && cfg != 17) cfg = 15;
+    if ((ln || epi.x6_k) && cfg != 4 && cfg != 15 && cfg != 17) cfg = 15;
+    if (epi.x6_k && (K != 6 * epi.x6_k || epi.x6_k % 64 || ln)) return hipErrorInvalidValue;
     switch (cfg) {
         case 2: return launch<C2>(A, amap, W, ldw, M, N, K, e2, st);
         case 3: return launch<C3>(A, amap, W, ldw, M, N, K, e2, st);

@@ -62,6 +62,8 @@ hipError_t pfm_ctc_collapse(const int* ids, long long ld, const int* olen, int B
                             int* ntok, hipStream_t st);
 hipError_t pfm_f32_to_bf16(const float* x, bf16* y, long long n, hipStream_t st);
 size_t pfm_ffn_packed_elems();
+hipError_t pfm_split3_rows(const float* x, RowMap xm, int M, int K, int Kp, bf16* out, hipStream_t st);
+hipError_t pfm_split3_planes(const float* x, bf16* p, long long plane, long long n, hipStream_t st);
 hipError_t pfm_ffn_pack(const bf16* W1, const bf16* W2, bf16* Wp, hipStream_t st);
 hipError_t pfm_ffn_fused(const float* x, int M, const float* g2, const float* be2, float eps, const bf16* Wp,
                          const float* b1, const float* b2, float* xo, const float* gn, const float* bn, bf16* xn,
@@ -105,7 +107,7 @@ static int fail(int code, const std::string& msg) {
             return fail(PFM_E_HIP, std::string(#expr) + ": " + hipGetErrorString(_e));           \
     } while (0)
 
-static thread_local PfmKnobs t_knobs = {0, 0, 1, 8, 0, 1, 0, 2, 1, 0, -1, 0, 0, 1, 0, 1, 1, 1, 0, 0};
+static thread_local PfmKnobs t_knobs = {0, 0, 1, 8, 0, 1, 0, 2, 1, 0, -1, 0, 0, 1, 0, 1, 1, 1, 0, 1, 0};
 
 const PfmKnobs& pfm_knobs() { return t_knobs; }
 
@@ -134,9 +136,10 @@ void pfm_knobs_refresh() {
     k.gemm_skinny = iv("PFM_GEMM_SKINNY", 1) != 0;
     k.ffn_fused = iv("PFM_FFN_FUSED", 1) != 0;
     k.ffn_var = iv("PFM_FFN_VAR", 0);
+    k.exact_x6 = iv("PFM_EXACT_X6", 1) != 0;
     const int* f = &k.ln_fold;
     unsigned long long s = 1469598103934665603ull;   // FNV-1a over the fields
-    for (int i = 0; i < 19; ++i) s = (s ^ (unsigned long long)(unsigned)f[i]) * 1099511628211ull;
+    for (int i = 0; i < 20; ++i) s = (s ^ (unsigned long long)(unsigned)f[i]) * 1099511628211ull;
     k.sig = s;
     t_knobs = k;
 }
@@ -204,6 +207,10 @@ struct pfm_handle {
     bool fold_ready = false;
     DevBuf ffn_pack;               // fused-FFN weight tiles of every encoder layer (bf16, LDS-image order)
     bool ffn_ready = false;
+    DevBuf arena_x6;               // EXACT mode: three bf16 planes of every GEMM weight (x = x0 + x1 + x2)
+    bool x6_ready = false;
+    std::map<hipStream_t, std::unique_ptr<DevBuf>> x6_scratch;   // split A operands, one buffer per stream
+    std::map<size_t, std::unique_ptr<DevBuf>> x6_pad;   // weights with K % 64 != 0: planes [N][round64(K)] by offset
     std::vector<std::pair<size_t, size_t>> gemm_ranges;   // (off, numel) converted to bf16
     bool bf_ready = false;
     int missing = 0;
@@ -438,6 +445,17 @@ int ensure_bf16(pfm_handle* h, hipStream_t st) {
     return PFM_OK;
 }
 
+// EXACT mode: the split-bf16 planes of every GEMM weight (emulated f32 GEMMs, k_gemm_bf16.hip x6 path)
+int ensure_x6(pfm_handle* h, hipStream_t st) {
+    if (h->x6_ready || !pfm_knobs().exact_x6) return PFM_OK;
+    const size_t n = h->arena_elems;
+    HIP_TRY(h->arena_x6.ensure(3 * n * sizeof(bf16)));
+    for (auto& r : h->gemm_ranges)
+        HIP_TRY(pfm_split3_planes(h->w(r.first), h->arena_x6.as<bf16>() + r.first, (long long)n, (long long)r.second, st));
+    h->x6_ready = true;
+    return PFM_OK;
+}
+
 int reserve(pfm_handle* h, int B, int T) {
     if (B <= h->capB && T <= h->capT) return PFM_OK;
     B = std::max(B, h->capB);
@@ -577,7 +595,16 @@ bool kv_overlap_enabled() { return pfm_knobs().kv_overlap; }   // 0: memory K|V 
 // MI355X; kept for A/B runs)
 bool gemm_ln_enabled() { return pfm_knobs().gemm_ln; }
 
-int amax_tiles(int dtype, RowMap amap, long long ldw, int N, int K) {
+// EXACT-mode GEMM on the split-bf16 path: f32 weights with ld == K inside the arena, K a multiple of 64
+bool x6_route(const pfm_handle* h, int dtype, const void* W, long long ldw, int K) {
+    if (dtype != DT_F32 || !h || !h->x6_ready || !pfm_knobs().exact_x6 || K % 4 || ldw != K) return false;
+    const float* w = (const float*)W;
+    return w >= h->arena.as<float>() && w < h->arena.as<float>() + h->arena_elems;
+}
+
+int amax_tiles(int dtype, RowMap amap, long long ldw, int N, int K, const pfm_handle* h = nullptr,
+               const void* W = nullptr) {
+    if (x6_route(h, dtype, W, ldw, K)) return pfm_gemm_bf16_256_amax_tiles(N);
     return use_big_bf16(dtype, amap, ldw, K) ? pfm_gemm_bf16_256_amax_tiles(N) : pfm_gemm_amax_tiles(N);
 }
 
@@ -591,6 +618,57 @@ GemmEpi epi_default() {
 }
 
 
+
+// f32 GEMM as split bf16 x6 MFMA: A rows -> [A0 | A1 | A2] in the stream's scratch, then the bf16 256-tile
+// kernel over K' = 6K with the weight planes (the same epilogue as every other GEMM)
+hipError_t gemm_x6(pfm_handle* h, const float* A, RowMap am, const float* W, int M, int N, int K, const GemmEpi& e,
+                   hipStream_t s) {
+    if (M <= 0 || N <= 0) return hipSuccess;
+    auto& sc = h->x6_scratch[s];
+    if (!sc) {
+        sc.reset(new DevBuf());
+        sc->gen = &h->buf_gen;   // captured streaming graphs hold its address
+    }
+    const int Kp = (K + 63) / 64 * 64;   // segments zero-padded to the kernel's K step
+    const size_t off = (size_t)(W - h->arena.as<float>());
+    const bf16* planes = h->arena_x6.as<bf16>() + off;
+    long long ws = (long long)h->arena_elems;
+    if (Kp != K) {   // padded planes of this weight, built on first use (outside any graph capture)
+        auto& pb = h->x6_pad[off];
+        if (!pb) {
+            hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+            hipError_t e0 = hipStreamIsCapturing(s, &cs);
+            if (e0 != hipSuccess) return e0;
+            if (cs != hipStreamCaptureStatusNone) return hipErrorStreamCaptureUnsupported;
+            pb.reset(new DevBuf());
+            pb->gen = &h->buf_gen;
+            e0 = pb->ensure((size_t)N * Kp * 3 * sizeof(bf16));
+            if (e0 != hipSuccess) return e0;
+            // rows of W [N][K] -> [N][3 Kp] (x0 | x1 | x2), then regroup as three [N][Kp] planes below
+            e0 = pfm_split3_rows(W, rowmap_plain(K), N, K, Kp, pb->as<bf16>(), s);
+            if (e0 != hipSuccess) return e0;
+        }
+        planes = pb->as<bf16>();
+        ws = Kp;   // plane p of row n at n * 3Kp + p * Kp: ldw = 3 Kp, plane stride Kp
+    }
+    const size_t need = (size_t)M * 3 * Kp * sizeof(bf16);
+    if (need > sc->bytes) {
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        hipError_t e0 = hipStreamIsCapturing(s, &cs);
+        if (e0 != hipSuccess) return e0;
+        if (cs != hipStreamCaptureStatusNone) return hipErrorStreamCaptureUnsupported;
+        e0 = hipStreamSynchronize(s);   // the old buffer may still be read by queued work
+        if (e0 != hipSuccess) return e0;
+        e0 = sc->ensure(need);
+        if (e0 != hipSuccess) return e0;
+    }
+    hipError_t er = pfm_split3_rows(A, am, M, K, Kp, sc->as<bf16>(), s);
+    if (er != hipSuccess) return er;
+    GemmEpi e2 = e;
+    e2.x6_k = Kp;
+    e2.x6_ws = ws;
+    return pfm_gemm_bf16_256(sc->p, rowmap_plain(3LL * Kp), planes, Kp == K ? K : 3LL * Kp, M, N, 6 * Kp, e2, s);
+}
 
 // Per-call launch context shared by the Paraformer and SenseVoice pipelines: numerics mode,
 // weight views and launch wrappers that attach algorithmic flops / bytes to every MFMA launch
@@ -628,6 +706,8 @@ struct Run {
                           (e.res0 ? (e.res0_bf16 ? 2.0 : 4.0) * Mm * N : 0.0) + (e.res1 ? 4.0 * Mm * N : 0.0) +
                           (e.out2 ? 2.0 * Mm * N : 0.0);
         ProfScope ps(h, s, PFM_K_GEMM, fl, by);
+        if (!fast && x6_route(h, dtp, Wt, ldw, Kk))
+            return gemm_x6(h, (const float*)A, am, (const float*)Wt, Mm, N, Kk, e, s);
         return gemm_dispatch(dtp, A, am, Wt, ldw, Mm, N, Kk, e, s);
     }
     hipError_t attn(int dtp, const void* q, RowMap qm, const void* k, RowMap km, const void* v, RowMap vm, float* o,
@@ -1017,6 +1097,8 @@ int pfm_set_weight(pfm_handle* h, const char* name, const void* host_ptr, int dt
     h->bf_ready = false;
     h->fold_ready = false;
     h->ffn_ready = false;
+    h->x6_ready = false;
+    h->x6_pad.clear();
     h->ban_tok = -1;   // the banned-token bias copy follows ctc.ctc_lo.bias
     return PFM_OK;
 }
@@ -1046,6 +1128,7 @@ int pfm_run(pfm_handle* h, void* stream, int mode, const float* feats, const int
     if (rc) return rc;
     const bool fast = mode == PFM_MODE_FAST;
     if (fast) { rc = ensure_bf16(h, st); if (rc) return rc; }
+    else { rc = ensure_x6(h, st); if (rc) return rc; }
     const pfm_config& c = h->cfg;
     const int D = c.d_model, Fd = c.ffn, K = c.kernel_size, nkv = c.dec_blocks * 2 * D;
     const long long M = (long long)B * T;
@@ -1104,6 +1187,8 @@ int pfm_run(pfm_handle* h, void* stream, int mode, const float* feats, const int
         const double fl = 2.0 * M * nkv * D;
         const double by = ((double)M * D + (double)nkv * D) * es + (double)M * nkv * es;
         ProfScope ps(h, s, PFM_K_GEMM, fl, by);
+        if (!fast && x6_route(h, dt, W(h->wkv_all), D, D))
+            return gemm_x6(h, (const float*)A, encmap, (const float*)W(h->wkv_all), (int)M, nkv, D, e, s);
         return gemm_dispatch(dt, A, encmap, W(h->wkv_all), D, (int)M, nkv, D, e, s);
     };
     const bool kv_async = kv_overlap_enabled() && c.dec_blocks > 0;
@@ -1243,7 +1328,7 @@ int pfm_run(pfm_handle* h, void* stream, int mode, const float* feats, const int
              Xdn, dt);
     if (rc) return rc;
     {   // output layer with fused row-argmax (logits never written)
-        const int ntl = amax_tiles(dt, rowmap_plain(D), D, c.vocab_size, D);
+        const int ntl = amax_tiles(dt, rowmap_plain(D), D, c.vocab_size, D, h, W(h->out_w));
         GemmEpi e = epi_default();
         e.bias = P(h->out_b);
         e.amax_val = h->amv.as<float>(); e.amax_idx = h->ami.as<int>(); e.n_tiles = ntl;
@@ -1277,6 +1362,7 @@ int pfm_run_ctc(pfm_handle* h, void* stream, int mode, const float* feats, const
     if (rc) return rc;
     const bool fast = mode == PFM_MODE_FAST;
     if (fast) { rc = ensure_bf16(h, st); if (rc) return rc; }
+    else { rc = ensure_x6(h, st); if (rc) return rc; }
     if (h->prof_on && h->ev_used > 4096) prof_collect(h);
     const Run run(h, st, fast);
     const int D = c.d_model, I = c.input_size, V = c.vocab_size;
@@ -1311,7 +1397,7 @@ int pfm_run_ctc(pfm_handle* h, void* stream, int mode, const float* feats, const
         }
         bias = h->ban_bias.as<float>();
     }
-    const int ntl = amax_tiles(run.dt, rowmap_plain(D), D, V, D);
+    const int ntl = amax_tiles(run.dt, rowmap_plain(D), D, V, D, h, run.W(h->ctc_w));
     {
         GemmEpi e = epi_default();
         e.bias = bias;
@@ -1342,6 +1428,7 @@ int pfm_run_punc(pfm_handle* h, void* stream, int mode, const int32_t* ids, cons
     int rc = reserve(h, B, T);
     if (rc) return rc;
     if (fast) { rc = ensure_bf16(h, st); if (rc) return rc; }
+    else { rc = ensure_x6(h, st); if (rc) return rc; }
     const int D = c.d_model;
     float* X = h->X.as<float>();
     // X = embed[ids] * sqrt(d) + PE: the encoder input AND layer 0's residual (input_size == d_model)
@@ -1692,7 +1779,7 @@ int stream_decoder(pfm_streams* s, const Run& r, int n, int Tw, int L, const SPr
     }
     int rc = ffn(Xd, h->d3n1g, h->d3n1b, h->d3w1, h->d3b1, h->d3ng, h->d3nb, h->d3w2, Xd, h->dan_g, h->dan_b, Xdn, dt);
     if (rc) return rc;
-    const int ntl = amax_tiles(dt, rowmap_plain(D), D, c.vocab_size, D);
+    const int ntl = amax_tiles(dt, rowmap_plain(D), D, c.vocab_size, D, h, r.W(h->out_w));
     GemmEpi e = epi_default();
     e.bias = r.P(h->out_b);
     e.amax_val = h->amv.as<float>(); e.amax_idx = h->ami.as<int>(); e.n_tiles = ntl;
@@ -1874,6 +1961,7 @@ int pfm_stream_step(pfm_streams* s, void* stream, int n, const int32_t* slot_ids
     int rc = reserve(h, n, Tw + 2);
     if (rc) return rc;
     if (fast) { rc = ensure_bf16(h, st); if (rc) return rc; }
+    else { rc = ensure_x6(h, st); if (rc) return rc; }
     // PE rows up to the furthest position of this step (grown by doubling)
     int need = 1;
     for (int i = 0; i < n; ++i) need = std::max(need, s->start[slot_ids[i]] + (int)nfeat[i]);

@@ -100,6 +100,11 @@ struct GemmEpi {
     const float2* ln_st_in;
     const float* ln_colsum;
     float ln_eps;
+    // three-way split bf16 emulation of an f32 GEMM (EXACT mode, bf16 256-tile kernel): A = [A0 | A1 | A2]
+    // ([M, 3 x6_k], x = x0 + x1 + x2 exactly), W = three bf16 planes x6_ws elements apart; the kernel runs
+    // K' = 6 x6_k over the segments (A2,W0) (A1,W1) (A0,W2) (A1,W0) (A0,W1) (A0,W0). 0 = plain GEMM.
+    int x6_k;
+    long long x6_ws;
 };
 
 static inline bool rowmap_vec4(const RowMap& m) {
@@ -139,6 +144,7 @@ struct PfmKnobs {
     int gemm_skinny;        // PFM_GEMM_SKINNY (default 1): weight-streaming kernel for <= 64-row GEMMs
     int ffn_fused;          // PFM_FFN_FUSED (default 1): fused LN2 + FFN + LN1_next encoder kernel (k_ffn.hip)
     int ffn_var;            // PFM_FFN_VAR: diagnostic variants of the fused FFN kernel (0 = the kernel)
+    int exact_x6;           // PFM_EXACT_X6 (default 1): EXACT-mode GEMMs as split bf16 x6 MFMA (f32 MFMA if 0)
     unsigned long long sig;
 };
 const PfmKnobs& pfm_knobs();
