@@ -170,6 +170,209 @@ __global__ __launch_bounds__(256) void attn_f32_kernel(AttnArgs a) {
         }
 }
 
+// ---- EXACT mode on bf16 MFMA: split-bf16 emulation of the f32 kernel above (same swapped products,
+// same online softmax in f32). Every f32 operand x is split as x0 + x1 + x2 (bf16, exact), and each f32
+// product a.b becomes a0b0 + a0b1 + a1b0 + a0b2 + a1b1 + a2b0 on v_mfma_f32_32x32x16_bf16 (dropped
+// terms <= 2^-25 |ab|, f32 accumulation): S^T = K.Q^T and O^T = V^T.P^T at f32 accuracy for 6x the
+// bf16 MFMA work, i.e. 2.7x the f32-MFMA ceiling. 8 waves = 256 query rows per workgroup; 32-key tiles
+// staged from f32 rows into LDS as three bf16 planes (K row-major, V transposed in the permuted key
+// order that P^T takes straight from the S^T accumulator registers), double-buffered.
+constexpr int X6_KT = 32;
+constexpr int X6_KP = DK * 2 + 16;            // K plane row pitch 272 B (32 key rows)
+constexpr int X6_VP = X6_KT * 2 + 16;         // V^T plane row pitch 80 B (128 dim rows): b128 reads conflict-free
+constexpr int X6_KPL = X6_KT * X6_KP, X6_VPL = DK * X6_VP;
+constexpr int X6_STG = 3 * (X6_KPL + X6_VPL);
+constexpr int X6_LDS = 2 * X6_STG;
+
+__device__ __forceinline__ void x6_split(float x, bf16& a, bf16& b, bf16& c) {
+    a = f2bf(x);
+    const float r = x - bf2f(a);
+    b = f2bf(r);
+    c = f2bf(r - bf2f(b));
+}
+
+__device__ __forceinline__ f32x16 mfma32(bf16x8 a, bf16x8 b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+// c += a.b with a = a0+a1+a2, b = b0+b1+b2 (small products first)
+__device__ __forceinline__ f32x16 mfma_x6(const bf16x8& a0, const bf16x8& a1, const bf16x8& a2, const bf16x8& b0,
+                                          const bf16x8& b1, const bf16x8& b2, f32x16 c) {
+    c = mfma32(a2, b0, c);
+    c = mfma32(a1, b1, c);
+    c = mfma32(a0, b2, c);
+    c = mfma32(a1, b0, c);
+    c = mfma32(a0, b1, c);
+    return mfma32(a0, b0, c);
+}
+
+__global__ __launch_bounds__(512) void attn_x6_kernel(AttnArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int qt = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int fr = lane & 31, fh = lane >> 5;
+    const int klen = min(a.klen[b], a.Tk);
+    const float* Q = (const float*)a.q;
+    const float* K = (const float*)a.k;
+    const float* V = (const float*)a.v;
+
+    // Q^T fragments (B operand): lane (q = fr) holds dims 16ks + 8fh + j, pre-scaled, split in three
+    const int qrow = qt * 256 + wid * QW + fr;
+    bf16x8 q0[8], q1[8], q2[8];
+    {
+        const bool ok = qrow < a.Tq;
+        const float* qp = Q + a.qmap.off((long long)b * a.Tq + (ok ? qrow : 0)) + h * DK;
+#pragma unroll
+        for (int ks = 0; ks < 8; ++ks) {
+            const float4 x0 = ok ? *(const float4*)(qp + ks * 16 + fh * 8) : make_float4(0, 0, 0, 0);
+            const float4 x1 = ok ? *(const float4*)(qp + ks * 16 + fh * 8 + 4) : make_float4(0, 0, 0, 0);
+            const float xv[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                bf16 u, v, w;
+                x6_split(xv[j] * a.scale, u, v, w);
+                q0[ks][j] = u; q1[ks][j] = v; q2[ks][j] = w;
+            }
+        }
+    }
+    f32x16 o[4];
+#pragma unroll
+    for (int d = 0; d < 4; ++d)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) o[d][e] = 0.f;
+    float mrun = -INFINITY, lrun = 0.f;
+    const int ntiles = (klen + X6_KT - 1) / X6_KT;
+
+    // staging of one 32-key tile: threads 0..255 take a 4-key x 4-dim block of V (written transposed,
+    // key quad at its permuted slot: P^T k-step s lane half fh holds keys 16s + 8(j>>2) + 4fh + (j&3)),
+    // threads 256..511 four 4-dim chunks of K rows; keys >= klen are zeros
+    auto stage = [&](int t, int sbuf) {
+        unsigned char* Ks = smem + sbuf * X6_STG;
+        unsigned char* Vs = Ks + 3 * X6_KPL;
+        if (tid < 256) {
+            const int kq4 = tid >> 5, dq = tid & 31;   // keys 4kq4.., dims 4dq..
+            float xv[4][4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int key = t * X6_KT + 4 * kq4 + r;
+                float4 x = make_float4(0, 0, 0, 0);
+                if (key < klen) x = *(const float4*)(V + a.vmap.off((long long)b * a.Tk + key) + h * DK + 4 * dq);
+                xv[r][0] = x.x; xv[r][1] = x.y; xv[r][2] = x.z; xv[r][3] = x.w;
+            }
+            const int s16 = kq4 >> 2, w4 = kq4 & 3, pos = ((w4 & 1) << 1) | (w4 >> 1);
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                bf16x4 p0, p1, p2;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    bf16 u, v, w;
+                    x6_split(xv[r][c], u, v, w);
+                    p0[r] = u; p1[r] = v; p2[r] = w;
+                }
+                const int off = (4 * dq + c) * X6_VP + s16 * 32 + pos * 8;
+                *(bf16x4*)(Vs + off) = p0;
+                *(bf16x4*)(Vs + X6_VPL + off) = p1;
+                *(bf16x4*)(Vs + 2 * X6_VPL + off) = p2;
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int c = (tid - 256) + 256 * i, row = c >> 5, ch = c & 31;
+                const int key = t * X6_KT + row;
+                float4 x = make_float4(0, 0, 0, 0);
+                if (key < klen) x = *(const float4*)(K + a.kmap.off((long long)b * a.Tk + key) + h * DK + ch * 4);
+                const float xv[4] = {x.x, x.y, x.z, x.w};
+                bf16x4 p0, p1, p2;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    bf16 u, v, w;
+                    x6_split(xv[e], u, v, w);
+                    p0[e] = u; p1[e] = v; p2[e] = w;
+                }
+                const int off = row * X6_KP + ch * 8;
+                *(bf16x4*)(Ks + off) = p0;
+                *(bf16x4*)(Ks + X6_KPL + off) = p1;
+                *(bf16x4*)(Ks + 2 * X6_KPL + off) = p2;
+            }
+        }
+    };
+    if (ntiles > 0) stage(0, 0);
+    __syncthreads();
+    for (int t = 0; t < ntiles; ++t) {
+        const int cur = t & 1;
+        if (t + 1 < ntiles) stage(t + 1, cur ^ 1);
+        const unsigned char* Ks = smem + cur * X6_STG;
+        const unsigned char* Vs = Ks + 3 * X6_KPL;
+        // S^T[key][q]: A = K rows (key = fr, dims 16ks + 8fh ..), B = Q^T
+        f32x16 s;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) s[e] = 0.f;
+#pragma unroll
+        for (int ks = 0; ks < 8; ++ks) {
+            const unsigned char* kp = Ks + fr * X6_KP + ks * 32 + fh * 16;
+            const bf16x8 k0 = *(const bf16x8*)kp, k1 = *(const bf16x8*)(kp + X6_KPL),
+                         k2 = *(const bf16x8*)(kp + 2 * X6_KPL);
+            s = mfma_x6(k0, k1, k2, q0[ks], q1[ks], q2[ks], s);
+        }
+        // identical masking / online softmax to attn_f32_kernel
+        float mt = -INFINITY;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+            const int key = t * X6_KT + kappa(e) + 4 * fh;
+            if (key >= klen) s[e] = -INFINITY;
+            mt = fmaxf(mt, s[e]);
+        }
+        mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+        const float mnew = fmaxf(mrun, mt);
+        const float corr = expf(mrun - mnew);
+        float ls = 0.f;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+            s[e] = expf(s[e] - mnew);
+            ls += s[e];
+        }
+        ls += __shfl_xor(ls, 32, 64);
+        lrun = lrun * corr + ls;
+        mrun = mnew;
+#pragma unroll
+        for (int d = 0; d < 4; ++d)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) o[d][e] *= corr;
+        // O^T[d][q] += V^T.P^T: k step s16 takes accumulator registers 8 s16 .. 8 s16 + 7 as P^T
+#pragma unroll
+        for (int s16 = 0; s16 < 2; ++s16) {
+            bf16x8 p0, p1, p2;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                bf16 u, v, w;
+                x6_split(s[8 * s16 + j], u, v, w);
+                p0[j] = u; p1[j] = v; p2[j] = w;
+            }
+#pragma unroll
+            for (int d = 0; d < 4; ++d) {
+                const unsigned char* vp = Vs + (32 * d + fr) * X6_VP + s16 * 32 + fh * 16;
+                const bf16x8 v0 = *(const bf16x8*)vp, v1 = *(const bf16x8*)(vp + X6_VPL),
+                             v2 = *(const bf16x8*)(vp + 2 * X6_VPL);
+                o[d] = mfma_x6(v0, v1, v2, p0, p1, p2, o[d]);
+            }
+        }
+        __syncthreads();
+    }
+    if (qrow >= a.Tq) return;
+    const float inv = (klen > 0) ? 1.f / lrun : 0.f;
+    float* op = a.o ? a.o + ((long long)b * a.Tq + qrow) * a.ldo + h * DK : nullptr;
+    bf16* op2 = a.o2 ? (bf16*)a.o2 + ((long long)b * a.Tq + qrow) * a.ldo + h * DK : nullptr;
+#pragma unroll
+    for (int d = 0; d < 4; ++d)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+            const int col = d * 32 + kappa(e) + 4 * fh;
+            const float v = o[d][e] * inv;
+            if (op) op[col] = v;
+            if (op2) op2[col] = f2bf(v);
+        }
+}
+
 // ---- bf16 kernel geometry: 64-key tiles; K row-major with a 16-B chunk XOR swizzle (conflict-free
 // ds_read_b128 of 16 distinct rows); V row-major with a 320-B pitch so the transposing
 // ds_read_b64_tr_b16 reads (4 key rows x 32 B per half-wave) hit 64 distinct banks.
@@ -662,6 +865,7 @@ hipError_t pfm_attention_fsmn(int dtype, const void* q, RowMap qmap, const void*
     if (!attr_done) {
         attr_done = true;
         (void)hipFuncSetAttribute((const void*)attn_f32_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, LDS32);
+        (void)hipFuncSetAttribute((const void*)attn_x6_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, X6_LDS);
         (void)hipFuncSetAttribute((const void*)attn_bf16_kernel<4>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   2 * STG2);
         (void)hipFuncSetAttribute((const void*)attn_bf16_kernel<8>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -674,7 +878,10 @@ hipError_t pfm_attention_fsmn(int dtype, const void* q, RowMap qmap, const void*
         return (m.rows_per_seg <= 0 || m.rows_per_seg == Tk) && (long long)Tk * m.ld * 2 < (1ll << 31);
     };
     if (dtype == DT_BF16 && (!contiguous(kmap) || !contiguous(vmap))) return hipErrorInvalidValue;
-    if (dtype == DT_F32) {
+    if (dtype == DT_F32 && pfm_knobs().exact_x6) {   // EXACT mode on split-bf16 MFMA (f32 accuracy)
+        dim3 grid((Tq + 255) / 256, heads, B), block(512);
+        hipLaunchKernelGGL(attn_x6_kernel, grid, block, X6_LDS, st, a);
+    } else if (dtype == DT_F32) {
         dim3 grid((Tq + 127) / 128, heads, B), block(256);
         hipLaunchKernelGGL(attn_f32_kernel, grid, block, LDS32, st, a);
     } else {
