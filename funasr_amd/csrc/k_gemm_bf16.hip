@@ -1336,7 +1336,8 @@ hipError_t pfm_gemm_bf16_256(const void* A, RowMap amap, const void* W, long lon
     }
     const bool ln = e2.ln_st_in || e2.ln_st_out;
     int cfg = pick_cfg(M, N, K, epi.amax_val != nullptr);
-    if ((ln || epi.x6_k) && cfg != 4 && cfg != 15 && cfg != 17) cfg = 15;
+    if (ln && cfg != 4 && cfg != 15 && cfg != 17) cfg = 15;
+    if (epi.x6_k && cfg != 1 && cfg != 4 && cfg != 13 && cfg != 15 && cfg != 16 && cfg != 17) cfg = 15;
     if (epi.x6_k && (K != 6 * epi.x6_k || epi.x6_k % 64 || ln)) return hipErrorInvalidValue;
     switch (cfg) {
         case 2: return launch<C2>(A, amap, W, ldw, M, N, K, e2, st);

@@ -3,8 +3,10 @@ vectors captured from the reference modules (tests/golden/make_golden.py).
 
 EXACT mode (f32 MFMA) must reproduce the reference token ids exactly; encoder output within
 rel-L2 1e-5 / abs 1e-4 (row slices), CIF alphas within 1e-5, token counts exact.
-FAST mode (bf16 MFMA, f32 accumulate/residual) is held to encoder rel-L2 <= 2e-2 and a token
-agreement floor (random weights have small logit margins, SURVEY §7 hard part 1).
+FAST mode (bf16 MFMA, f32 accumulate/residual) is held to encoder rel-L2 <= 2e-2 and a margin bound: a
+token may differ from the f32 reference only where the reference's top-2 log-prob margin is below
+FAST_MARGIN (random weights leave a median margin of 0.1 nat, SURVEY §7 hard part 1; measured flips
+reach 0.34 nat).
 """
 import os
 
@@ -30,6 +32,28 @@ def _tokens_from_run(r, cfg):
         ids = toks[b, : nt[b]].tolist()
         out.append([t for t in ids if t not in (cfg.eos, cfg.sos, cfg.blank_id)])
     return out
+
+
+# fast (bf16) mode: largest reference top-2 log-prob margin (nat) at which a token may still flip
+FAST_MARGIN = 0.5
+
+
+def _margin_flips(r, g, cfg):
+    """Position-wise token flips of a run vs the golden decoder argmax, over utterances whose token count
+    matches; returns (#flips, largest golden top-2 margin at a flipped position)."""
+    toks, nt = r["tokens"].cpu().numpy(), r["ntok"].cpu().numpy()
+    off = np.concatenate([[0], np.cumsum(g["ntok"])])
+    flips, worst = 0, 0.0
+    gt = _golden_tokens(g)
+    for b in range(toks.shape[0]):
+        n = int(g["ntok"][b])
+        if int(nt[b]) != n or len(gt[b]) != n:   # a changed count shifts every later position
+            continue
+        bad = np.nonzero(toks[b, :n] != np.array(gt[b]))[0]
+        flips += len(bad)
+        if len(bad):
+            worst = max(worst, float(g["margin"][off[b]:off[b + 1]][bad].max()))
+    return flips, worst
 
 
 def _golden_tokens(g):
@@ -92,7 +116,7 @@ def test_large_exact_tokens(engines, name):
     assert np.abs(a - g["alphas"]).max() < 1e-5
 
 
-@pytest.mark.parametrize("name", ["para_large_ragged", "para_large_b4"])
+@pytest.mark.parametrize("name", ["para_large_ragged", "para_large_b4", "para_large_c1"])
 def test_large_fast_agreement(engines, name):
     e = engines["large"]
     g = np.load(f"{GOLD}/{name}.npz")
@@ -109,8 +133,12 @@ def test_large_fast_agreement(engines, name):
     assert np.abs(nt - g["ntok"]).max() <= 1
     agree = [np.mean(np.array(a[: min(len(a), len(b))]) == np.array(b[: min(len(a), len(b))])) for a, b in
              zip(got, want) if min(len(a), len(b)) > 0]
-    print(f"fast-mode token agreement {name}: {np.mean(agree):.4f}, enc rows rel {relerr:.2e}")
-    assert np.mean(agree) > 0.6
+    flips, worst = _margin_flips(r, g, e.cfg)
+    print(f"fast-mode token agreement {name}: {np.mean(agree):.4f}, enc rows rel {relerr:.2e}; "
+          f"{flips} flips, largest reference top-2 margin among them {worst:.4f} nat")
+    # bf16 operands move the logits by O(1e-2): a token may differ from the f32 reference only where the
+    # reference's own top-2 log-prob margin is below FAST_MARGIN (utterances whose token count matches)
+    assert worst < FAST_MARGIN, (worst, FAST_MARGIN)
 
 
 def test_fast_fused_layernorm_matches_unfused(engines, monkeypatch):

@@ -20,7 +20,8 @@ def per_dispatch(db, counter):
 
 
 def is_gemm(name):
-    return "gemm_bf16_kernel" in name or "gemm_nt_kernelIDF16b" in name or "gemm_nt_kernel<__bf16>" in name
+    return ("gemm_bf16_kernel" in name or "gemm_nt_kernelIDF16b" in name or "gemm_nt_kernel<__bf16>" in name
+            or "ffn_fused_kernel" in name)
 
 
 def main(fdb, wdb, out):

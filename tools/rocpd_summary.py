@@ -15,7 +15,8 @@ from collections import defaultdict
 
 
 def is_gemm(k):
-    return "gemm_bf16_kernel" in k or "gemm_nt_kernelIDF16b" in k or "gemm_nt_kernel<__bf16>" in k
+    return ("gemm_bf16_kernel" in k or "gemm_nt_kernelIDF16b" in k or "gemm_nt_kernel<__bf16>" in k
+            or "ffn_fused_kernel" in k)
 
 
 def main(db, out_csv, marker="argmax_reduce_kernel", bench_log=None, warmup=None, ksteps=None):
