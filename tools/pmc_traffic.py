@@ -40,7 +40,7 @@ def main(fdb, wdb, out):
             ws.append(wb)
             shapes[(name[-60:], blocks)][2] += wb
     res = {
-        "kernel_set": "bf16 GEMM launches (gemm_bf16_kernel<Cfg> + gemm_nt_kernel<bf16>)",
+        "kernel_set": "GEMM class: gemm_bf16_kernel<Cfg> + gemm_nt_kernel<bf16> + ffn_fused_kernel",
         "launches_fetch_pass": len(fs), "launches_write_pass": len(ws),
         "fetch_bytes_per_launch": sum(fs) / max(1, len(fs)),
         "write_bytes_per_launch": sum(ws) / max(1, len(ws)),
