@@ -159,14 +159,31 @@ __global__ __launch_bounds__(256) void attn_f32_kernel(AttnArgs a) {
     const float inv = (klen > 0) ? 1.f / lrun : 0.f;
     float* op = a.o ? a.o + ((long long)b * a.Tq + qrow) * a.ldo + h * DK : nullptr;
     bf16* op2 = a.o2 ? (bf16*)a.o2 + ((long long)b * a.Tq + qrow) * a.ldo + h * DK : nullptr;
+    const bool x3 = a.o2_dtype == DT_X3;   // split output (planes a.fD apart): the out-projection's operand
 #pragma unroll
     for (int d = 0; d < 4; ++d)
 #pragma unroll
-        for (int e = 0; e < 16; ++e) {
-            const int col = d * 32 + kappa(e) + 4 * fh;
-            const float v = o[d][e] * inv;
-            if (op) op[col] = v;
-            if (op2) op2[col] = f2bf(v);
+        for (int g = 0; g < 4; ++g) {   // registers 4g..4g+3 are 4 consecutive head dims
+            const int col = d * 32 + 8 * g + 4 * fh;
+            const float v[4] = {o[d][4 * g] * inv, o[d][4 * g + 1] * inv, o[d][4 * g + 2] * inv, o[d][4 * g + 3] * inv};
+            if (op) *(float4*)(op + col) = make_float4(v[0], v[1], v[2], v[3]);
+            if (op2) {
+                if (x3) {
+                    bf16x4 p0, p1, p2;
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        bf16 u, w, z;
+                        split3_bf16(v[i], u, w, z);
+                        p0[i] = u; p1[i] = w; p2[i] = z;
+                    }
+                    *(bf16x4*)(op2 + col) = p0;
+                    *(bf16x4*)(op2 + col + a.fD) = p1;
+                    *(bf16x4*)(op2 + col + 2 * a.fD) = p2;
+                } else {
+                    bf16x4 t = {f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
+                    *(bf16x4*)(op2 + col) = t;
+                }
+            }
         }
 }
 
@@ -362,14 +379,31 @@ __global__ __launch_bounds__(512) void attn_x6_kernel(AttnArgs a) {
     const float inv = (klen > 0) ? 1.f / lrun : 0.f;
     float* op = a.o ? a.o + ((long long)b * a.Tq + qrow) * a.ldo + h * DK : nullptr;
     bf16* op2 = a.o2 ? (bf16*)a.o2 + ((long long)b * a.Tq + qrow) * a.ldo + h * DK : nullptr;
+    const bool x3 = a.o2_dtype == DT_X3;   // split output (planes a.fD apart): the out-projection's operand
 #pragma unroll
     for (int d = 0; d < 4; ++d)
 #pragma unroll
-        for (int e = 0; e < 16; ++e) {
-            const int col = d * 32 + kappa(e) + 4 * fh;
-            const float v = o[d][e] * inv;
-            if (op) op[col] = v;
-            if (op2) op2[col] = f2bf(v);
+        for (int g = 0; g < 4; ++g) {   // registers 4g..4g+3 are 4 consecutive head dims
+            const int col = d * 32 + 8 * g + 4 * fh;
+            const float v[4] = {o[d][4 * g] * inv, o[d][4 * g + 1] * inv, o[d][4 * g + 2] * inv, o[d][4 * g + 3] * inv};
+            if (op) *(float4*)(op + col) = make_float4(v[0], v[1], v[2], v[3]);
+            if (op2) {
+                if (x3) {
+                    bf16x4 p0, p1, p2;
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        bf16 u, w, z;
+                        split3_bf16(v[i], u, w, z);
+                        p0[i] = u; p1[i] = w; p2[i] = z;
+                    }
+                    *(bf16x4*)(op2 + col) = p0;
+                    *(bf16x4*)(op2 + col + a.fD) = p1;
+                    *(bf16x4*)(op2 + col + 2 * a.fD) = p2;
+                } else {
+                    bf16x4 t = {f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
+                    *(bf16x4*)(op2 + col) = t;
+                }
+            }
         }
 }
 
@@ -878,7 +912,8 @@ hipError_t pfm_attention_fsmn(int dtype, const void* q, RowMap qmap, const void*
         return (m.rows_per_seg <= 0 || m.rows_per_seg == Tk) && (long long)Tk * m.ld * 2 < (1ll << 31);
     };
     if (dtype == DT_BF16 && (!contiguous(kmap) || !contiguous(vmap))) return hipErrorInvalidValue;
-    if (dtype == DT_F32 && pfm_knobs().exact_x6) {   // EXACT mode on split-bf16 MFMA (f32 accuracy)
+    if (dtype == DT_F32 && pfm_knobs().exact_x6 && ldo % 4 == 0 && ((uintptr_t)o % 16) == 0 &&
+        ((uintptr_t)o2 % 8) == 0) {   // EXACT mode on split-bf16 MFMA (f32 accuracy; 4-column output stores)
         dim3 grid((Tq + 255) / 256, heads, B), block(512);
         hipLaunchKernelGGL(attn_x6_kernel, grid, block, X6_LDS, st, a);
     } else if (dtype == DT_F32) {
@@ -897,6 +932,28 @@ hipError_t pfm_attention_fsmn(int dtype, const void* q, RowMap qmap, const void*
             hipLaunchKernelGGL(attn_bf16_kernel<4>, grid, block, 2 * STG2, st, a);
         }
     }
+    PFM_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+// EXACT mode (split-bf16 x6 attention) with the output written as the split operand of the out-projection:
+// out3 rows of 3 x heads x 128 bf16 (x0 | x1 | x2 planes, heads x 128 apart). q/k/v f32.
+hipError_t pfm_attention_x3(const float* q, RowMap qmap, const float* k, RowMap kmap, const float* v, RowMap vmap,
+                            bf16* out3, const int* klen, int B, int Tq, int Tk, int heads, int dk, float scale,
+                            hipStream_t st) {
+    if (B <= 0 || Tq <= 0) return hipSuccess;
+    if (dk != DK || !pfm_knobs().exact_x6) return hipErrorInvalidValue;
+    AttnArgs a;
+    a.q = q; a.qmap = qmap; a.k = k; a.kmap = kmap; a.v = v; a.vmap = vmap;
+    a.o = nullptr; a.ldo = 3LL * heads * DK; a.o2 = out3; a.o2_dtype = DT_X3; a.klen = klen; a.Tq = Tq; a.Tk = Tk;
+    a.scale = scale; a.fw = nullptr; a.fout = nullptr; a.fld = 0; a.fD = heads * DK;
+    static bool attr_done = false;
+    if (!attr_done) {
+        attr_done = true;
+        (void)hipFuncSetAttribute((const void*)attn_x6_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, X6_LDS);
+    }
+    dim3 grid((Tq + 255) / 256, heads, B), block(512);
+    hipLaunchKernelGGL(attn_x6_kernel, grid, block, X6_LDS, st, a);
     PFM_LAUNCH_CHECK();
     return hipSuccess;
 }

@@ -89,6 +89,17 @@ __global__ __launch_bounds__(256) void layernorm_v8_kernel(const TIN* __restrict
             if (odt == DT_F32) {
                 *(float4*)((float*)out + ob + c) = make_float4(y[0], y[1], y[2], y[3]);
                 *(float4*)((float*)out + ob + c + 4) = make_float4(y[4], y[5], y[6], y[7]);
+            } else if (odt == DT_X3) {   // EXACT-mode split operand: planes D apart within the 3D-wide row
+                bf16x8 p0, p1, p2;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    bf16 u, w, z;
+                    split3_bf16(y[e], u, w, z);
+                    p0[e] = u; p1[e] = w; p2[e] = z;
+                }
+                *(bf16x8*)((bf16*)out + ob + c) = p0;
+                *(bf16x8*)((bf16*)out + ob + D + c) = p1;
+                *(bf16x8*)((bf16*)out + ob + 2 * D + c) = p2;
             } else {
                 bf16x8 t = {f2bf(y[0]), f2bf(y[1]), f2bf(y[2]), f2bf(y[3]), f2bf(y[4]), f2bf(y[5]), f2bf(y[6]), f2bf(y[7])};
                 *(bf16x8*)((bf16*)out + ob + c) = t;
@@ -686,6 +697,7 @@ hipError_t pfm_layernorm(const float* x, RowMap xmap, int M, int D, const float*
         PFM_LAUNCH_CHECK();
         return hipSuccess;
     }
+    if (odt == DT_X3 || o2dt == DT_X3) return hipErrorInvalidValue;   // split output: streaming kernel only
     hipLaunchKernelGGL(layernorm_kernel, dim3((M + 3) / 4), dim3(256), 0, st, x, xmap, M, D, g, b, eps, pe,
                        pe_T > 0 ? pe_T : 1, in_scale, out, omap, odt, out2, o2map, o2dt);
     PFM_LAUNCH_CHECK();

@@ -764,7 +764,19 @@ __global__ __launch_bounds__(C::NT) void gemm_bf16_kernel(const bf16* __restrict
                 if constexpr (LN == 2) ln_stats_out(v, row, c4);
                 const long long ob = epi.out_map.off(row) + col;
                 if (f32o) *(float4*)((float*)epi.out + ob) = v;
-                else {
+                else if (epi.out_dtype == DT_X3) {   // EXACT-mode split operand of the next GEMM: planes N apart
+                    const float vv[4] = {v.x, v.y, v.z, v.w};
+                    bf16x4 p0, p1, p2;
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        bf16 u, w, z;
+                        split3_bf16(vv[e], u, w, z);
+                        p0[e] = u; p1[e] = w; p2[e] = z;
+                    }
+                    *(bf16x4*)((bf16*)epi.out + ob) = p0;
+                    *(bf16x4*)((bf16*)epi.out + ob + N) = p1;
+                    *(bf16x4*)((bf16*)epi.out + ob + 2 * N) = p2;
+                } else {
                     bf16x4 t = {f2bf(v.x), f2bf(v.y), f2bf(v.z), f2bf(v.w)};
                     *(bf16x4*)((bf16*)epi.out + ob) = t;
                 }
@@ -1333,6 +1345,12 @@ hipError_t pfm_gemm_bf16_256(const void* A, RowMap amap, const void* W, long lon
         // loop): measured 2.2 ms/step SLOWER on the path (bf16 + f32 residual out-proj), so opt-in
         e2.pre_res_ok = pfm_knobs().gemm_preres;
         e2.res_batch = pfm_knobs().gemm_resbatch;   // residual loads batched ahead of the stores
+    }
+    if (epi.out && epi.out_dtype == DT_X3) {   // split output: the general vector epilogue path only
+        if (!e2.vec_ok || epi.amax_val || epi.out2 || epi.ln_st_in || epi.ln_st_out || epi.out_map.ld % 4)
+            return hipErrorInvalidValue;
+        e2.res_batch = 0;
+        e2.pre_res_ok = 0;
     }
     const bool ln = e2.ln_st_in || e2.ln_st_out;
     int cfg = pick_cfg(M, N, K, epi.amax_val != nullptr);

@@ -64,6 +64,9 @@ hipError_t pfm_f32_to_bf16(const float* x, bf16* y, long long n, hipStream_t st)
 size_t pfm_ffn_packed_elems();
 hipError_t pfm_split3_rows(const float* x, RowMap xm, int M, int K, int Kp, bf16* out, hipStream_t st);
 hipError_t pfm_split3_planes(const float* x, bf16* p, long long plane, long long n, hipStream_t st);
+hipError_t pfm_attention_x3(const float* q, RowMap qmap, const float* k, RowMap kmap, const float* v, RowMap vmap,
+                            bf16* out3, const int* klen, int B, int Tq, int Tk, int heads, int dk, float scale,
+                            hipStream_t st);
 hipError_t pfm_ffn_pack(const bf16* W1, const bf16* W2, bf16* Wp, hipStream_t st);
 hipError_t pfm_ffn_fused(const float* x, int M, const float* g2, const float* be2, float eps, const bf16* Wp,
                          const float* b1, const float* b2, float* xo, const float* gn, const float* bn, bf16* xn,
@@ -456,6 +459,11 @@ int ensure_x6(pfm_handle* h, hipStream_t st) {
     return PFM_OK;
 }
 
+// bytes per row of the encoder LN output buffer: f32 [input_size | d_model] or DT_X3 [3 d_model] bf16
+size_t xn_row_bytes(const pfm_config& c) {
+    return std::max((size_t)std::max(c.input_size, c.d_model) * 4, (size_t)c.d_model * 6);
+}
+
 int reserve(pfm_handle* h, int B, int T) {
     if (B <= h->capB && T <= h->capT) return PFM_OK;
     B = std::max(B, h->capB);
@@ -469,13 +477,13 @@ int reserve(pfm_handle* h, int B, int T) {
     HIP_TRY(hipDeviceSynchronize());
     // encoder (both families)
     HIP_TRY(h->X.ensure(M * D * 4));
-    HIP_TRY(h->Xn.ensure(M * std::max(I, D) * 4));
+    HIP_TRY(h->Xn.ensure(M * xn_row_bytes(c)));
     HIP_TRY(h->QKV.ensure(M * 3 * D * 4));
     HIP_TRY(h->QKVb.ensure(M * 3 * D * 2));
     HIP_TRY(h->F.ensure(M * D * 4));
-    HIP_TRY(h->O.ensure(M * D * 4));
+    HIP_TRY(h->O.ensure(M * D * 6));   // f32 rows, or DT_X3 rows (EXACT split operand)
     HIP_TRY(h->Ob.ensure(M * D * 2));
-    HIP_TRY(h->H.ensure(M * F * 4));
+    HIP_TRY(h->H.ensure(M * F * 6));
     HIP_TRY(h->lnst1.ensure(M * (D / 64) * 8));
     HIP_TRY(h->lnst2.ensure(M * (D / 64) * 8));
     if (sv) {   // query-prefixed input, tp residual, CTC argmax partials (rows = frames)
@@ -622,8 +630,16 @@ GemmEpi epi_default() {
 // f32 GEMM as split bf16 x6 MFMA: A rows -> [A0 | A1 | A2] in the stream's scratch, then the bf16 256-tile
 // kernel over K' = 6K with the weight planes (the same epilogue as every other GEMM)
 hipError_t gemm_x6(pfm_handle* h, const float* A, RowMap am, const float* W, int M, int N, int K, const GemmEpi& e,
-                   hipStream_t s) {
+                   hipStream_t s, const bf16* A3 = nullptr) {
     if (M <= 0 || N <= 0) return hipSuccess;
+    if (A3) {   // the producer already wrote [A0 | A1 | A2] (DT_X3 rows, am.ld = 3K)
+        if (K % 64) return hipErrorInvalidValue;
+        GemmEpi e2 = e;
+        e2.x6_k = K;
+        e2.x6_ws = (long long)h->arena_elems;
+        const size_t off = (size_t)(W - h->arena.as<float>());
+        return pfm_gemm_bf16_256(A3, am, h->arena_x6.as<bf16>() + off, K, M, N, 6 * K, e2, s);
+    }
     auto& sc = h->x6_scratch[s];
     if (!sc) {
         sc.reset(new DevBuf());
@@ -682,6 +698,7 @@ struct Run {
     float qscale;    // d_k ** -0.5
     bool fuse_fsmn;  // fast mode: encoder FSMN in the attention epilogue
     bool fuse_ln;    // opt-in (PFM_GEMM_LN=1): LayerNorm fused into the 512-wide projections
+    bool x3 = false;     // EXACT mode on split-bf16 x6: producers write GEMM operands as three bf16 planes
     bool raw_input = false;                 // streaming: the stack input is already x sqrt(d) + PE
     const struct ChunkKV* ck = nullptr;     // streaming: self-attention keys = K/V cache ++ window
 
@@ -693,6 +710,8 @@ struct Run {
         const int lenc = (c.kernel_size - 1) / 2 + (c.enc_sanm_shift > 0 ? c.enc_sanm_shift : 0);
         fuse_fsmn = fast && c.kernel_size == 11 && lenc == 5 && c.d_model / c.heads == 128 && attn_fsmn_enabled();
         fuse_ln = fast && c.d_model == 512 && c.ffn % 32 == 0 && gemm_ln_enabled();
+        x3 = !fast && h->x6_ready && pfm_knobs().exact_x6 && c.d_model % 64 == 0 && c.ffn % 64 == 0 &&
+             c.d_model / c.heads == 128;
     }
     const void* W(size_t off) const { return fast ? (const void*)h->wb(off) : (const void*)h->w(off); }
     const float* P(size_t off) const { return h->w(off); }
@@ -709,6 +728,28 @@ struct Run {
         if (!fast && x6_route(h, dtp, Wt, ldw, Kk))
             return gemm_x6(h, (const float*)A, am, (const float*)Wt, Mm, N, Kk, e, s);
         return gemm_dispatch(dtp, A, am, Wt, ldw, Mm, N, Kk, e, s);
+    }
+    // EXACT-mode GEMM whose A operand a producer wrote as DT_X3 rows (am.ld = 3K); weights f32 in the arena
+    hipError_t gemm3(const void* A3, RowMap am, const void* Wt, long long ldw, int Mm, int N, int Kk, const GemmEpi& e,
+                     hipStream_t s = nullptr) const {
+        if (!s) s = st;
+        if (!x6_route(h, DT_F32, Wt, ldw, Kk) || Kk % 64) return hipErrorInvalidValue;
+        const double fl = 2.0 * Mm * N * Kk;
+        const double by = ((double)Mm * Kk + (double)N * Kk) * 4.0 +
+                          (double)Mm * N * (e.out ? (e.out_dtype == DT_F32 ? 4.0 : e.out_dtype == DT_X3 ? 6.0 : 2.0) : 0.0) +
+                          (e.res0 ? (e.res0_bf16 ? 2.0 : 4.0) * Mm * N : 0.0) + (e.res1 ? 4.0 * Mm * N : 0.0);
+        ProfScope ps(h, s, PFM_K_GEMM, fl, by);
+        return gemm_x6(h, nullptr, am, (const float*)Wt, Mm, N, Kk, e, s, (const bf16*)A3);
+    }
+    // EXACT-mode attention writing the out-projection's split operand (out3 rows of 3 x d_model bf16)
+    hipError_t attn3(const float* q, RowMap qm, const float* k, RowMap km, const float* v, RowMap vm, bf16* out3,
+                     const int* kl, int Bb, int Tq, int Tk) const {
+        const pfm_config& c = h->cfg;
+        const double dk = c.d_model / c.heads;
+        const double fl = 4.0 * Bb * Tq * (double)Tk * dk * c.heads;
+        const double by = ((double)Bb * Tq + 2.0 * Bb * Tk) * c.d_model * 4.0 + (double)Bb * Tq * c.d_model * 6.0;
+        ProfScope ps(h, st, PFM_K_ATTN, fl, by);
+        return pfm_attention_x3(q, qm, k, km, v, vm, out3, kl, Bb, Tq, Tk, c.heads, (int)dk, qscale, st);
     }
     hipError_t attn(int dtp, const void* q, RowMap qm, const void* k, RowMap km, const void* v, RowMap vm, float* o,
                     long long ldo, void* o2, const int* kl, int Bb, int Tq, int Tk) const {
@@ -759,13 +800,13 @@ EncWs enc_ws(pfm_handle* h, long long r0) {
     const pfm_config& c = h->cfg;
     const long long D = c.d_model, I = c.input_size, Fd = c.ffn;
     EncWs w;
-    w.Xn = (char*)h->Xn.p + r0 * std::max(I, D) * 4;
+    w.Xn = (char*)h->Xn.p + r0 * (long long)xn_row_bytes(c);
     w.QKV = h->QKV.as<float>() + r0 * 3 * D;
     w.QKVb = h->QKVb.as<bf16>() + r0 * 3 * D;
     w.F = h->F.as<float>() + r0 * D;
-    w.O = h->O.as<float>() + r0 * D;
+    w.O = (float*)((char*)h->O.p + r0 * D * 6);
     w.Ob = h->Ob.as<bf16>() + r0 * D;
-    w.H = (char*)h->H.p + r0 * Fd * 4;
+    w.H = (char*)h->H.p + r0 * Fd * 6;
     w.st1 = (float2*)h->lnst1.p + r0 * (D / 64);
     w.st2 = (float2*)h->lnst2.p + r0 * (D / 64);
     return w;
@@ -811,6 +852,11 @@ int encoder_stack(const Run& r, const float* x_in, const int* lens, int B, int T
     // fast mode, full-size batches: LN2 -> FFN -> residual -> next layer's LN1 as ONE kernel per layer
     // (k_ffn.hip); chunk-sized streaming steps keep the weight-streaming GEMMs
     const bool ffn_fused = fast && !r.fuse_ln && !fold && h->ffn_ready && pfm_knobs().ffn_fused && M >= 4096;
+    // EXACT mode: LayerNorm, attention and FFN w1 write their consumer GEMM's operand in split form
+    // (three bf16 planes, DT_X3) instead of f32 + a separate split pass
+    const bool x3 = r.x3 && !r.ck;
+    const RowMap xmap3 = rowmap_plain(x3 ? 3 * D : D);
+    const int lndt = x3 ? DT_X3 : dt;
     for (int l = l0; l < l1; ++l) {
         const EncLayer& L = h->enc[l];
         const int din = L.din;
@@ -823,7 +869,7 @@ int encoder_stack(const Run& r, const float* x_in, const int* lens, int B, int T
                                   st));
         else if ((!r.fuse_ln || l == l0) && !(fold && l > l0) && !(ffn_fused && l > l0))   // fused / folded: no LN1
             HIP_TRY(pfm_layernorm(X, rowmap_plain(D), (int)M, D, r.P(L.ln1g), r.P(L.ln1b), c.ln_eps, nullptr, 0, 1.f,
-                                  Xn, rowmap_plain(D), dt, nullptr, plain, 0, st));
+                                  Xn, xmap3, lndt, nullptr, plain, 0, st));
         {   // q|k|v = LN1(x) Wqkv^T + b   (fast mode: bf16 only — attention and FSMN read bf16)
             GemmEpi e = epi_default();
             e.bias = r.P(L.bqkv);
@@ -832,6 +878,8 @@ int encoder_stack(const Run& r, const float* x_in, const int* lens, int B, int T
             if (fold && l > l0) {   // Xn holds bf16(x) from the previous FFN w2 epilogue
                 fold_in(e, ws.st1, L.fq_cs, L.fq_cb);
                 HIP_TRY(r.gemm(dt, Xn, rowmap_plain(D), fw + L.fq_w, D, (int)M, 3 * D, D, e));
+            } else if (x3 && l > 0) {
+                HIP_TRY(r.gemm3(Xn, xmap3, r.W(L.wqkv), din, (int)M, 3 * D, din, e));
             } else {
                 HIP_TRY(r.gemm(dt, Xn, rowmap_plain(din), r.W(L.wqkv), din, (int)M, 3 * D, din, e));
             }
@@ -872,8 +920,12 @@ int encoder_stack(const Run& r, const float* x_in, const int* lens, int B, int T
         } else {
             HIP_TRY(pfm_fsmn(QKV + 2 * D, rowmap_plain(3 * D), lens, B, T, D, r.P(L.fsmn), K, lenc, nullptr, Fm,
                              nullptr, st));
-            HIP_TRY(r.attn(DT_F32, QKV, rowmap_plain(3 * D), QKV + D, rowmap_plain(3 * D), QKV + 2 * D,
-                           rowmap_plain(3 * D), O, D, nullptr, lens, B, T, T));
+            if (x3)
+                HIP_TRY(r.attn3(QKV, rowmap_plain(3 * D), QKV + D, rowmap_plain(3 * D), QKV + 2 * D, rowmap_plain(3 * D),
+                                (bf16*)O, lens, B, T, T));
+            else
+                HIP_TRY(r.attn(DT_F32, QKV, rowmap_plain(3 * D), QKV + D, rowmap_plain(3 * D), QKV + 2 * D,
+                               rowmap_plain(3 * D), O, D, nullptr, lens, B, T, T));
         }
         {   // x = (x +) linear_out(att) + fsmn   (encoder.py:120-137: no residual when in != out)
             GemmEpi e = epi_default();
@@ -886,11 +938,14 @@ int encoder_stack(const Run& r, const float* x_in, const int* lens, int B, int T
                                   rowmap_plain(D), DT_BF16, nullptr, plain));
             } else {
                 if (fold) stats_out(e, ws.st2);
-                HIP_TRY(r.gemm(dt, fast ? (const void*)Ob : (const void*)O, rowmap_plain(D), r.W(L.wo), D, (int)M, D,
-                               D, e));
+                if (x3)
+                    HIP_TRY(r.gemm3(O, xmap3, r.W(L.wo), D, (int)M, D, D, e));
+                else
+                    HIP_TRY(r.gemm(dt, fast ? (const void*)Ob : (const void*)O, rowmap_plain(D), r.W(L.wo), D, (int)M,
+                                   D, D, e));
                 if (!fold && !ffn_fused)
                     HIP_TRY(pfm_layernorm(X, rowmap_plain(D), (int)M, D, r.P(L.ln2g), r.P(L.ln2b), c.ln_eps, nullptr,
-                                          0, 1.f, Xn, rowmap_plain(D), dt, nullptr, plain, 0, st));
+                                          0, 1.f, Xn, xmap3, lndt, nullptr, plain, 0, st));
             }
         }
         if (ffn_fused) {   // x = x + W2 relu(W1 LN2(x) + b1) + b2 ; Xn = LN1_{l+1}(x)
@@ -910,6 +965,9 @@ int encoder_stack(const Run& r, const float* x_in, const int* lens, int B, int T
             if (fold) {
                 fold_in(e, ws.st2, L.f1_cs, L.f1_cb);
                 HIP_TRY(r.gemm(dt, Xn, rowmap_plain(D), fw + L.f1_w, D, (int)M, Fd, D, e));
+            } else if (x3) {   // h written as w2's split operand
+                e.out_map = rowmap_plain(3 * Fd); e.out_dtype = DT_X3;
+                HIP_TRY(r.gemm3(Xn, xmap3, r.W(L.w1), D, (int)M, Fd, D, e));
             } else {
                 HIP_TRY(r.gemm(dt, Xn, rowmap_plain(D), r.W(L.w1), D, (int)M, Fd, D, e));
             }
@@ -919,7 +977,9 @@ int encoder_stack(const Run& r, const float* x_in, const int* lens, int B, int T
             e.bias = r.P(L.b2);
             e.res0 = X; e.ld_res0 = D;
             e.out = X; e.out_map = rowmap_plain(D); e.out_dtype = DT_F32;
-            if (!r.fuse_ln) {
+            if (x3) {
+                HIP_TRY(r.gemm3(Hh, rowmap_plain(3 * Fd), r.W(L.w2), Fd, (int)M, D, Fd, e));
+            } else if (!r.fuse_ln) {
                 if (fold && l + 1 < l1) stats_out(e, ws.st1);   // feeds the next layer's folded norm1
                 HIP_TRY(r.gemm(dt, Hh, rowmap_plain(Fd), r.W(L.w2), Fd, (int)M, D, Fd, e));
             } else if (l + 1 < l1) {   // ... and Xn = LN1_{l+1}(x)

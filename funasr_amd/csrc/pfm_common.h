@@ -13,7 +13,17 @@ typedef __bf16 bf16;
 #define PFM_WAVE 64
 
 // dtype codes shared with include/pfm.h
-enum { DT_F32 = 0, DT_BF16 = 1 };
+enum { DT_F32 = 0, DT_BF16 = 1,
+       // internal: three bf16 planes x0 | x1 | x2 (x = x0 + x1 + x2 exactly) per row, plane stride = the
+       // row's logical width; the A operand layout of the EXACT-mode split-bf16 x6 GEMM
+       DT_X3 = 2 };
+
+__device__ __forceinline__ void split3_bf16(float x, bf16& a, bf16& b, bf16& c) {
+    a = (bf16)x;
+    const float r = x - (float)a;
+    b = (bf16)r;
+    c = (bf16)(r - (float)b);
+}
 
 __device__ __forceinline__ float bf2f(bf16 x) { return (float)x; }
 __device__ __forceinline__ bf16 f2bf(float x) { return (bf16)x; }   // RNE, v_cvt_pk_bf16_f32 on gfx950
