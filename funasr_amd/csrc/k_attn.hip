@@ -475,7 +475,9 @@ __device__ __forceinline__ void fsmn_epilogue(const AttnArgs& a, unsigned char* 
     }
 }
 
-template <int NWV>
+// VAR (diagnostics, PFM_ATTN_VAR, timing only — results are wrong): 1 no K/V loads after tile 0,
+// 2 no softmax (P = S), 3 no PV products, 4 no QK products, 5 no key loop (prologue + epilogue only)
+template <int NWV, int VAR = 0>
 __global__ __launch_bounds__(NWV * 64, 8 / NWV) void attn_bf16_kernel(AttnArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr int NT = NWV * 64, QBLK = NWV * QW;
@@ -571,6 +573,7 @@ __global__ __launch_bounds__(NWV * 64, 8 / NWV) void attn_bf16_kernel(AttnArgs a
         for (int kb = 0; kb < 2; ++kb) {
 #pragma unroll
             for (int e = 0; e < 16; ++e) s[kb][e] = 0.f;
+            if constexpr (VAR == 4) continue;
             const int row = kb * 32 + fr;
 #pragma unroll
             for (int kq = 0; kq < 8; ++kq) {
@@ -579,6 +582,7 @@ __global__ __launch_bounds__(NWV * 64, 8 / NWV) void attn_bf16_kernel(AttnArgs a
             }
         }
         // lane holds S^T[key = t*64 + kb*32 + kappa(e) + 4fh][q = fr]
+        if constexpr (VAR != 2) {
         if ((t + 1) * KT2 > klen) {   // only the last tile can hold keys past klen
 #pragma unroll
             for (int kb = 0; kb < 2; ++kb)
@@ -613,6 +617,10 @@ __global__ __launch_bounds__(NWV * 64, 8 / NWV) void attn_bf16_kernel(AttnArgs a
             }
         ls += __shfl_xor(ls, 32, 64);
         lrun += ls;
+        } else {
+            lrun = 1.f;
+        }
+        if constexpr (VAR == 3) return;
         // O^T[d][q] += sum_key V[key][d] P[q][key]; P^T from the accumulator registers (k-step st of
         // key block kb = registers 8st..8st+7: key 16st + 8(j>>2) + 4fh + (j&3)), V^T by tr reads
 #pragma unroll
@@ -641,10 +649,11 @@ __global__ __launch_bounds__(NWV * 64, 8 / NWV) void attn_bf16_kernel(AttnArgs a
     // the other LDS buffer after them (that buffer's last reader, tile t-1, finished before the
     // previous barrier), so the fetch has one tile of compute to land. The fetch index is clamped so
     // every iteration issues the same loads (the last one is unused).
-    if (ntiles > 0) sstore(0, gload(0));
+    const Stg first = gload(0);
+    if (ntiles > 0) sstore(0, first);
     __syncthreads();
-    for (int t = 0; t < ntiles; ++t) {
-        const Stg nx = gload(min(t + 1, ntiles - 1));
+    for (int t = 0; t < (VAR == 5 ? 0 : ntiles); ++t) {
+        const Stg nx = VAR == 1 ? first : gload(min(t + 1, ntiles - 1));
         compute(t);
         if (t + 1 < ntiles) sstore((t + 1) & 1, nx);
         __syncthreads();
@@ -904,6 +913,11 @@ hipError_t pfm_attention_fsmn(int dtype, const void* q, RowMap qmap, const void*
                                   2 * STG2);
         (void)hipFuncSetAttribute((const void*)attn_bf16_kernel<8>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   LDS8);
+        (void)hipFuncSetAttribute((const void*)attn_bf16_kernel<8, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS8);
+        (void)hipFuncSetAttribute((const void*)attn_bf16_kernel<8, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS8);
+        (void)hipFuncSetAttribute((const void*)attn_bf16_kernel<8, 3>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS8);
+        (void)hipFuncSetAttribute((const void*)attn_bf16_kernel<8, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS8);
+        (void)hipFuncSetAttribute((const void*)attn_bf16_kernel<8, 5>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS8);
         (void)hipFuncSetAttribute((const void*)attn_bf16_pp_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   3 * STG2);
     }
@@ -926,7 +940,15 @@ hipError_t pfm_attention_fsmn(int dtype, const void* q, RowMap qmap, const void*
             hipLaunchKernelGGL(attn_bf16_pp_kernel, grid, block, 3 * STG2, st, a);
         } else if (nw == 8) {
             dim3 grid((Tq + 255) / 256, heads, B), block(512);
-            hipLaunchKernelGGL(attn_bf16_kernel<8>, grid, block, a.fout ? LDS8 : 2 * STG2, st, a);
+            const int lds = a.fout ? LDS8 : 2 * STG2;
+            switch (pfm_knobs().attn_var) {
+            case 1: hipLaunchKernelGGL((attn_bf16_kernel<8, 1>), grid, block, lds, st, a); break;
+            case 2: hipLaunchKernelGGL((attn_bf16_kernel<8, 2>), grid, block, lds, st, a); break;
+            case 3: hipLaunchKernelGGL((attn_bf16_kernel<8, 3>), grid, block, lds, st, a); break;
+            case 4: hipLaunchKernelGGL((attn_bf16_kernel<8, 4>), grid, block, lds, st, a); break;
+            case 5: hipLaunchKernelGGL((attn_bf16_kernel<8, 5>), grid, block, lds, st, a); break;
+            default: hipLaunchKernelGGL((attn_bf16_kernel<8>), grid, block, lds, st, a);
+            }
         } else {
             dim3 grid((Tq + 127) / 128, heads, B), block(256);
             hipLaunchKernelGGL(attn_bf16_kernel<4>, grid, block, 2 * STG2, st, a);

@@ -1113,7 +1113,9 @@ int pick_cfg(int M, int N, int K, bool amax) {
     //  - everything else (out-projections, decoder-sized M, the fused-argmax vocabulary GEMM) on
     //    128x256 tiles, two blocks per CU (C4).
     // PFM_GEMM_POLICY=1: the earlier grid-size policy (C15 at >= 2 tiles / CU or K >= 1536 with >= 240
-    // tiles, else C4); =2: C13 / C4 for decoder-sized M.
+    // tiles, else C4); =2: C13 / C4 for decoder-sized M; =3: C4 instead of C3 for the 512-wide GEMMs of
+    // fewer than 120 256x256 tiles (decoder projections: C3 measured 10.9 vs 13.3 us at M = 7392, K = 512;
+    // 26.0 vs 35.5 us at K = 2048).
     const int p = pfm_knobs().gemm_policy;
     const long long big = (long long)((M + 255) / 256) * ((N + 255) / 256);
     if (p == 1 || p == 2) {
@@ -1124,6 +1126,7 @@ int pick_cfg(int M, int N, int K, bool amax) {
     if (amax) return big >= 512 ? 15 : 4;
     if (N <= 512 && K % 128 == 0 && K >= 1024 && big >= 120) return 17;
     if (big >= 256) return 15;
+    if (N <= 512 && big < 120 && p != 3) return 3;   // decoder-sized M: 128x128 tiles fill more CUs
     return 4;
 }
 
@@ -1355,6 +1358,7 @@ hipError_t pfm_gemm_bf16_256(const void* A, RowMap amap, const void* W, long lon
     const bool ln = e2.ln_st_in || e2.ln_st_out;
     int cfg = pick_cfg(M, N, K, epi.amax_val != nullptr);
     if (ln && cfg != 4 && cfg != 15 && cfg != 17) cfg = 15;
+    if (epi.x6_k && cfg == 3) cfg = 4;   // EXACT mode keeps its measured tiles
     if (epi.x6_k && cfg != 1 && cfg != 4 && cfg != 13 && cfg != 15 && cfg != 16 && cfg != 17) cfg = 15;
     if (epi.x6_k && (K != 6 * epi.x6_k || epi.x6_k % 64 || ln)) return hipErrorInvalidValue;
     switch (cfg) {

@@ -110,7 +110,7 @@ static int fail(int code, const std::string& msg) {
             return fail(PFM_E_HIP, std::string(#expr) + ": " + hipGetErrorString(_e));           \
     } while (0)
 
-static thread_local PfmKnobs t_knobs = {0, 0, 1, 8, 0, 1, 0, 2, 1, 0, -1, 0, 0, 1, 0, 1, 1, 1, 0, 1, 0};
+static thread_local PfmKnobs t_knobs = {0, 0, 1, 8, 0, 1, 0, 2, 1, 0, -1, 0, 0, 1, 0, 1, 1, 1, 0, 1, 0, 0, 1};
 
 const PfmKnobs& pfm_knobs() { return t_knobs; }
 
@@ -140,9 +140,11 @@ void pfm_knobs_refresh() {
     k.ffn_fused = iv("PFM_FFN_FUSED", 1) != 0;
     k.ffn_var = iv("PFM_FFN_VAR", 0);
     k.exact_x6 = iv("PFM_EXACT_X6", 1) != 0;
+    k.attn_var = iv("PFM_ATTN_VAR", 0);
+    k.dec_subbatch = std::max(1, iv("PFM_DEC_SUBBATCH", 1));
     const int* f = &k.ln_fold;
     unsigned long long s = 1469598103934665603ull;   // FNV-1a over the fields
-    for (int i = 0; i < 20; ++i) s = (s ^ (unsigned long long)(unsigned)f[i]) * 1099511628211ull;
+    for (int i = 0; i < 22; ++i) s = (s ^ (unsigned long long)(unsigned)f[i]) * 1099511628211ull;
     k.sig = s;
     t_knobs = k;
 }
@@ -1296,109 +1298,152 @@ int pfm_run(pfm_handle* h, void* stream, int mode, const float* feats, const int
 
     // ---------------- decoder (paraformer/decoder.py:359-411) ----------------
     const long long Ml = (long long)B * L;
-    float* Xd = h->Xd.as<float>();
-    void* Xdn = h->Xdn.p;
-    float* Hd = h->Hd.as<float>();
-    void* Hdn = h->Hdn.p;
-    float* Td = h->Td.as<float>();
-    float* Tdn = h->Tdn.as<float>();
-    void* Qd = h->Qd.p;
-    float* Od = h->Od.as<float>();
-    bf16* Odb = h->Odb.as<bf16>();
     // compact CIF embeddings [B][T+1][D] -> decoder rows [B][L][D] (acoustic_embeds[:, :L])
-    HIP_TRY(hipMemcpy2DAsync(Xd, (size_t)L * D * 4, h->emb.p, (size_t)Lc * D * 4, (size_t)L * D * 4, B,
+    HIP_TRY(hipMemcpy2DAsync(h->Xd.p, (size_t)L * D * 4, h->emb.p, (size_t)Lc * D * 4, (size_t)L * D * 4, B,
                              hipMemcpyDeviceToDevice, st));
     if (!kv_async) HIP_TRY(launch_kv(st));
-    auto ffn = [&](const float* x, bool xdn_ready, size_t lng, size_t lnb, size_t w1, size_t b1, size_t fng,
-                   size_t fnb, size_t w2, float* out, size_t pg, size_t pb, void* pout, int pdt) -> int {
-        // out = W2 . LN_F(relu(W1 . LN(x) + b1)); pout = LN_P(out)   (sanm/positionwise_feed_forward.py:26-33)
-        if (!xdn_ready)
-            HIP_TRY(pfm_layernorm(x, rowmap_plain(D), (int)Ml, D, P(lng), P(lnb), c.ln_eps, nullptr, 0, 1.f, Xdn,
-                                  rowmap_plain(D), dt, nullptr, plain, 0, st));
-        GemmEpi e = epi_default();
-        e.bias = P(b1); e.relu = 1;
-        e.out = Hd; e.out_map = rowmap_plain(Fd); e.out_dtype = fast ? DT_BF16 : DT_F32;   // fast: bf16 hidden
-        HIP_TRY(GEMM(dt, Xdn, rowmap_plain(D), W(w1), D, (int)Ml, Fd, D, e));
-        if (fast)
-            HIP_TRY(pfm_layernorm_bf16in((const bf16*)Hd, rowmap_plain(Fd), (int)Ml, Fd, P(fng), P(fnb), c.ln_eps, Hdn,
-                                         rowmap_plain(Fd), dt, st));
-        else
-            HIP_TRY(pfm_layernorm(Hd, rowmap_plain(Fd), (int)Ml, Fd, P(fng), P(fnb), c.ln_eps, nullptr, 0, 1.f, Hdn,
-                                  rowmap_plain(Fd), dt, nullptr, plain, 0, st));
-        GemmEpi e2 = epi_default();
-        if (fuse_ln) {   // out itself is dead; only LN_P(out) is consumed
-            HIP_TRY(GEMM_LN(Hdn, rowmap_plain(Fd), W(w2), Fd, (int)Ml, Fd, e2, pg, pb, pout, rowmap_plain(D), pdt,
-                            nullptr, plain));
-        } else {
-            e2.out = out; e2.out_map = rowmap_plain(D); e2.out_dtype = DT_F32;
-            HIP_TRY(GEMM(dt, Hdn, rowmap_plain(Fd), W(w2), Fd, (int)Ml, D, Fd, e2));
-            HIP_TRY(pfm_layernorm(out, rowmap_plain(D), (int)Ml, D, P(pg), P(pb), c.ln_eps, nullptr, 0, 1.f, pout,
-                                  rowmap_plain(D), pdt, nullptr, plain, 0, st));
+    // One utterance group [b0, b0 + nb) of the decoder on rg.st: every buffer is row-addressed (rows b*L + t,
+    // memory K|V rows b*T + t), so a group is the same launch sequence over offset pointers.
+    auto dec_group = [&](const Run& rg, int b0, int nb) -> int {
+        hipStream_t s = rg.st;
+        const size_t esz = fast ? 2 : 4;
+        const long long r0 = (long long)b0 * L;
+        const int Mg = (int)((long long)nb * L);
+        float* Xd = h->Xd.as<float>() + r0 * D;
+        void* Xdn = h->Xdn.as<char>() + r0 * D * esz;
+        void* Hd = h->Hd.as<char>() + r0 * Fd * esz;   // fast: bf16 hidden, exact: f32
+        void* Hdn = h->Hdn.as<char>() + r0 * Fd * esz;
+        float* Td = h->Td.as<float>() + r0 * D;
+        void* Tdn = h->Tdn.as<char>() + r0 * D * esz;
+        void* Qd = h->Qd.as<char>() + r0 * D * esz;
+        float* Od = h->Od.as<float>() + r0 * D;
+        bf16* Odb = h->Odb.as<bf16>() + r0 * D;
+        const int* ntg = ntok + b0;
+        const int* lg = lens + b0;
+        const char* KVg = (const char*)KV + (size_t)b0 * T * nkv * esz;
+        auto ffn = [&](bool xdn_ready, size_t lng, size_t lnb, size_t w1, size_t b1, size_t fng, size_t fnb, size_t w2,
+                       float* out, size_t pg, size_t pb, void* pout, int pdt) -> int {
+            // out = W2 . LN_F(relu(W1 . LN(x) + b1)); pout = LN_P(out)   (sanm/positionwise_feed_forward.py:26-33)
+            if (!xdn_ready)
+                HIP_TRY(pfm_layernorm(Xd, rowmap_plain(D), Mg, D, P(lng), P(lnb), c.ln_eps, nullptr, 0, 1.f, Xdn,
+                                      rowmap_plain(D), dt, nullptr, plain, 0, s));
+            GemmEpi e = epi_default();
+            e.bias = P(b1); e.relu = 1;
+            e.out = Hd; e.out_map = rowmap_plain(Fd); e.out_dtype = fast ? DT_BF16 : DT_F32;   // fast: bf16 hidden
+            HIP_TRY(rg.gemm(dt, Xdn, rowmap_plain(D), W(w1), D, Mg, Fd, D, e));
+            if (fast)
+                HIP_TRY(pfm_layernorm_bf16in((const bf16*)Hd, rowmap_plain(Fd), Mg, Fd, P(fng), P(fnb), c.ln_eps, Hdn,
+                                             rowmap_plain(Fd), dt, s));
+            else
+                HIP_TRY(pfm_layernorm((const float*)Hd, rowmap_plain(Fd), Mg, Fd, P(fng), P(fnb), c.ln_eps, nullptr, 0,
+                                      1.f, Hdn, rowmap_plain(Fd), dt, nullptr, plain, 0, s));
+            GemmEpi e2 = epi_default();
+            if (fuse_ln) {   // out itself is dead; only LN_P(out) is consumed
+                HIP_TRY(rg.gemm_ln(Hdn, rowmap_plain(Fd), W(w2), Fd, Mg, Fd, e2, pg, pb, pout, rowmap_plain(D), pdt,
+                                   nullptr, plain));
+            } else {
+                e2.out = out; e2.out_map = rowmap_plain(D); e2.out_dtype = DT_F32;
+                HIP_TRY(rg.gemm(dt, Hdn, rowmap_plain(Fd), W(w2), Fd, Mg, D, Fd, e2));
+                HIP_TRY(pfm_layernorm(out, rowmap_plain(D), Mg, D, P(pg), P(pb), c.ln_eps, nullptr, 0, 1.f, pout,
+                                      rowmap_plain(D), pdt, nullptr, plain, 0, s));
+            }
+            return PFM_OK;
+        };
+        bool xdn_ready = false;   // Xdn already holds LN1(x) of the next block (fused out-proj epilogue)
+        for (int l = 0; l < c.dec_blocks; ++l) {
+            const DecLayer& Lr = h->dec[l];
+            // t = FFN(LN1(x)); x = x + FSMN(LN2(t))   (decoder.py:97-107)
+            // fast mode: LN2(t) in bf16 feeding the bf16-input FSMN (x += FSMN(LN2(t)) stays f32)
+            int rc2 = ffn(xdn_ready, Lr.n1g, Lr.n1b, Lr.w1, Lr.b1, Lr.ng, Lr.nb, Lr.w2, Td, Lr.n2g, Lr.n2b, Tdn,
+                          fast ? DT_BF16 : DT_F32);
+            if (rc2) return rc2;
+            if (fast)
+                HIP_TRY(pfm_fsmn_bf16in((const bf16*)Tdn, rowmap_plain(D), ntg, nb, L, D, P(Lr.fsmn), K, ldec, Xd, Xd,
+                                        nullptr, s));
+            else
+                HIP_TRY(pfm_fsmn((const float*)Tdn, rowmap_plain(D), ntg, nb, L, D, P(Lr.fsmn), K, ldec, Xd, Xd, nullptr,
+                                 s));
+            // x = x + CrossAtt(LN3(x), memory)   (decoder.py:109-119)
+            HIP_TRY(pfm_layernorm(Xd, rowmap_plain(D), Mg, D, P(Lr.n3g), P(Lr.n3b), c.ln_eps, nullptr, 0, 1.f, Xdn,
+                                  rowmap_plain(D), dt, nullptr, plain, 0, s));
+            {
+                GemmEpi e = epi_default();
+                e.bias = P(Lr.bq);
+                e.out = Qd; e.out_map = rowmap_plain(D); e.out_dtype = dt;
+                HIP_TRY(rg.gemm(dt, Xdn, rowmap_plain(D), W(Lr.wq), D, Mg, D, D, e));
+            }
+            if (l == 0 && kv_async) HIP_TRY(hipStreamWaitEvent(s, h->ev_kv, 0));   // join the side stream
+            {
+                const char* kvb = KVg + (size_t)l * 2 * D * esz;
+                HIP_TRY(rg.attn(dt, Qd, rowmap_plain(D), kvb, rowmap_plain(nkv), kvb + (size_t)D * esz,
+                                rowmap_plain(nkv), fast ? nullptr : Od, D, fast ? (void*)Odb : nullptr, lg, nb, L, T));
+            }
+            {
+                GemmEpi e = epi_default();
+                e.bias = P(Lr.bo);
+                e.res0 = Xd; e.ld_res0 = D;
+                e.out = Xd; e.out_map = rowmap_plain(D); e.out_dtype = DT_F32;
+                if (fuse_ln) {   // ... and Xdn = LN1 of the next block (decoders[l+1] or decoders3)
+                    const size_t ng = l + 1 < c.dec_blocks ? h->dec[l + 1].n1g : h->d3n1g;
+                    const size_t nbb = l + 1 < c.dec_blocks ? h->dec[l + 1].n1b : h->d3n1b;
+                    HIP_TRY(rg.gemm_ln(Odb, rowmap_plain(D), W(Lr.wo), D, Mg, D, e, ng, nbb, Xdn, rowmap_plain(D), dt,
+                                       nullptr, plain));
+                    xdn_ready = true;
+                } else {
+                    HIP_TRY(rg.gemm(dt, fast ? (const void*)Odb : (const void*)Od, rowmap_plain(D), W(Lr.wo), D, Mg, D,
+                                    D, e));
+                }
+            }
+        }
+        // decoders3: x = FFN(LN1(x)), no residual (decoder.py:97-100 with self_attn = src_attn = None)
+        int rc3 = ffn(xdn_ready, h->d3n1g, h->d3n1b, h->d3w1, h->d3b1, h->d3ng, h->d3nb, h->d3w2, Xd, h->dan_g,
+                      h->dan_b, Xdn, dt);
+        if (rc3) return rc3;
+        {   // output layer with fused row-argmax (logits never written)
+            const int ntl = amax_tiles(dt, rowmap_plain(D), D, c.vocab_size, D, h, W(h->out_w));
+            GemmEpi e = epi_default();
+            e.bias = P(h->out_b);
+            e.amax_val = h->amv.as<float>() + r0 * ntl; e.amax_idx = h->ami.as<int>() + r0 * ntl; e.n_tiles = ntl;
+            e.out = nullptr;
+            HIP_TRY(rg.gemm(dt, Xdn, rowmap_plain(D), W(h->out_w), D, Mg, c.vocab_size, D, e));
         }
         return PFM_OK;
     };
-    bool xdn_ready = false;   // Xdn already holds LN1(x) of the next block (fused out-proj epilogue)
-    for (int l = 0; l < c.dec_blocks; ++l) {
-        const DecLayer& Lr = h->dec[l];
-        // t = FFN(LN1(x)); x = x + FSMN(LN2(t))   (decoder.py:97-107)
-        // fast mode: LN2(t) in bf16 feeding the bf16-input FSMN (x += FSMN(LN2(t)) stays f32)
-        rc = ffn(Xd, xdn_ready, Lr.n1g, Lr.n1b, Lr.w1, Lr.b1, Lr.ng, Lr.nb, Lr.w2, Td, Lr.n2g, Lr.n2b, Tdn,
-                 fast ? DT_BF16 : DT_F32);
-        if (rc) return rc;
-        if (fast)
-            HIP_TRY(pfm_fsmn_bf16in((const bf16*)Tdn, rowmap_plain(D), ntok, B, L, D, P(Lr.fsmn), K, ldec, Xd, Xd,
-                                    nullptr, st));
-        else
-            HIP_TRY(pfm_fsmn(Tdn, rowmap_plain(D), ntok, B, L, D, P(Lr.fsmn), K, ldec, Xd, Xd, nullptr, st));
-        // x = x + CrossAtt(LN3(x), memory)   (decoder.py:109-119)
-        HIP_TRY(pfm_layernorm(Xd, rowmap_plain(D), (int)Ml, D, P(Lr.n3g), P(Lr.n3b), c.ln_eps, nullptr, 0, 1.f, Xdn,
-                              rowmap_plain(D), dt, nullptr, plain, 0, st));
-        {
-            GemmEpi e = epi_default();
-            e.bias = P(Lr.bq);
-            e.out = Qd; e.out_map = rowmap_plain(D); e.out_dtype = dt;
-            HIP_TRY(GEMM(dt, Xdn, rowmap_plain(D), W(Lr.wq), D, (int)Ml, D, D, e));
-        }
-        if (l == 0 && kv_async) HIP_TRY(hipStreamWaitEvent(st, h->ev_kv, 0));   // join the side stream
-        {
-            const size_t es = fast ? 2 : 4;
-            const char* kvb = (const char*)KV + (size_t)l * 2 * D * es;
-            HIP_TRY(ATTN(dt, Qd, rowmap_plain(D), kvb, rowmap_plain(nkv), kvb + (size_t)D * es,
-                                  rowmap_plain(nkv), fast ? nullptr : Od, D, fast ? (void*)Odb : nullptr, lens, B, L, T));
-        }
-        {
-            GemmEpi e = epi_default();
-            e.bias = P(Lr.bo);
-            e.res0 = Xd; e.ld_res0 = D;
-            e.out = Xd; e.out_map = rowmap_plain(D); e.out_dtype = DT_F32;
-            if (fuse_ln) {   // ... and Xdn = LN1 of the next block (decoders[l+1] or decoders3)
-                const size_t ng = l + 1 < c.dec_blocks ? h->dec[l + 1].n1g : h->d3n1g;
-                const size_t nb = l + 1 < c.dec_blocks ? h->dec[l + 1].n1b : h->d3n1b;
-                HIP_TRY(GEMM_LN(Odb, rowmap_plain(D), W(Lr.wo), D, (int)Ml, D, e, ng, nb, Xdn, rowmap_plain(D), dt,
-                                nullptr, plain));
-                xdn_ready = true;
-            } else {
-                HIP_TRY(GEMM(dt, fast ? (const void*)Odb : (const void*)Od, rowmap_plain(D), W(Lr.wo), D, (int)Ml, D,
-                             D, e));
-            }
-        }
-    }
-    // decoders3: x = FFN(LN1(x)), no residual (decoder.py:97-100 with self_attn = src_attn = None)
-    rc = ffn(Xd, xdn_ready, h->d3n1g, h->d3n1b, h->d3w1, h->d3b1, h->d3ng, h->d3nb, h->d3w2, Xd, h->dan_g, h->dan_b,
-             Xdn, dt);
-    if (rc) return rc;
-    {   // output layer with fused row-argmax (logits never written)
-        const int ntl = amax_tiles(dt, rowmap_plain(D), D, c.vocab_size, D, h, W(h->out_w));
-        GemmEpi e = epi_default();
-        e.bias = P(h->out_b);
-        e.amax_val = h->amv.as<float>(); e.amax_idx = h->ami.as<int>(); e.n_tiles = ntl;
-        e.out = nullptr;
-        HIP_TRY(GEMM(dt, Xdn, rowmap_plain(D), W(h->out_w), D, (int)Ml, c.vocab_size, D, e));
-        if (L_cap > 0)
+    // the per-tile row maxima of every group -> token ids, one launch on the caller's stream after the join
+    auto finish = [&]() -> int {
+        if (L_cap > 0) {
+            const int ntl = amax_tiles(dt, rowmap_plain(D), D, c.vocab_size, D, h, W(h->out_w));
             HIP_TRY(pfm_argmax_reduce(h->amv.as<float>(), h->ami.as<int>(), ntl, (c.vocab_size + 63) / 64, B, L, ntok,
                                       L_cap, tokens, nullptr, st));
+        }
+        return PFM_OK;
+    };
+    // PFM_DEC_SUBBATCH=n: utterance groups on concurrent streams (default 1: two groups measured equal to
+    // one, 23.5-24.0 ms/step either way, tools/bench_ab.py)
+    const int ng = std::max(1, std::min({pfm_knobs().dec_subbatch, (int)pfm_handle::MAXSUB, B, h->prof_on ? 1 : 64}));
+    (void)Ml;
+    if (ng == 1) {
+        rc = dec_group(run, 0, B);
+        return rc ? rc : finish();
     }
-    return PFM_OK;
+    if (!h->ev_fork) HIP_TRY(hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming));
+    HIP_TRY(hipEventRecord(h->ev_fork, st));
+    for (int k = 0; k < ng; ++k) {
+        if (!h->sub_st[k]) {
+            HIP_TRY(hipStreamCreateWithFlags(&h->sub_st[k], hipStreamNonBlocking));
+            HIP_TRY(hipEventCreateWithFlags(&h->ev_join[k], hipEventDisableTiming));
+        }
+        const int b0 = (int)((long long)B * k / ng), b1 = (int)((long long)B * (k + 1) / ng);
+        if (b1 <= b0) continue;
+        HIP_TRY(hipStreamWaitEvent(h->sub_st[k], h->ev_fork, 0));
+        Run rk = run;
+        rk.st = h->sub_st[k];
+        rc = dec_group(rk, b0, b1 - b0);
+        if (rc) return rc;
+        HIP_TRY(hipEventRecord(h->ev_join[k], h->sub_st[k]));
+        HIP_TRY(hipStreamWaitEvent(st, h->ev_join[k], 0));
+    }
+    return finish();
 }
 
 int pfm_run_ctc(pfm_handle* h, void* stream, int mode, const float* feats, const int32_t* lens, int B, int T,

@@ -155,6 +155,8 @@ struct PfmKnobs {
     int ffn_fused;          // PFM_FFN_FUSED (default 1): fused LN2 + FFN + LN1_next encoder kernel (k_ffn.hip)
     int ffn_var;            // PFM_FFN_VAR: diagnostic variants of the fused FFN kernel (0 = the kernel)
     int exact_x6;           // PFM_EXACT_X6 (default 1): EXACT-mode GEMMs as split bf16 x6 MFMA (f32 MFMA if 0)
+    int attn_var;           // PFM_ATTN_VAR: diagnostic variants of the 8-wave bf16 attention kernel (0 = the kernel)
+    int dec_subbatch;       // PFM_DEC_SUBBATCH (default 1): decoder utterance groups on concurrent streams
     unsigned long long sig;
 };
 const PfmKnobs& pfm_knobs();

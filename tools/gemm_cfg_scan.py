@@ -10,7 +10,8 @@ from funasr_amd import runtime as rt  # noqa: E402
 from tools.gemm_bench import tm  # noqa: E402
 
 SHAPES = [("dq", 14784, 512, 512), ("dffn1", 14784, 2048, 512), ("dffn2", 14784, 512, 2048),
-          ("out", 32000, 512, 512), ("qkv", 32000, 1536, 512)]
+          ("out", 32000, 512, 512), ("qkv", 32000, 1536, 512),
+          ("dq/2", 7392, 512, 512), ("dffn1/2", 7392, 2048, 512), ("dffn2/2", 7392, 512, 2048)]
 
 
 def main():
