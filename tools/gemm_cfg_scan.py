@@ -12,6 +12,11 @@ from tools.gemm_bench import tm  # noqa: E402
 SHAPES = [("dq", 14784, 512, 512), ("dffn1", 14784, 2048, 512), ("dffn2", 14784, 512, 2048),
           ("out", 32000, 512, 512), ("qkv", 32000, 1536, 512),
           ("dq/2", 7392, 512, 512), ("dffn1/2", 7392, 2048, 512), ("dffn2/2", 7392, 512, 2048)]
+# EXACT mode (split-bf16 x6) GEMMs of one encoder group: K' = 6K
+X6_SHAPES = [("x6qkv", 16000, 1536, 3072), ("x6w1", 16000, 2048, 3072), ("x6out", 16000, 512, 3072),
+             ("x6w2", 16000, 512, 12288), ("x6kv", 32000, 16384, 3072)]
+if os.environ.get("SCAN_X6"):
+    SHAPES = X6_SHAPES
 
 
 def main():
