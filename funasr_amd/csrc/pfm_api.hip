@@ -110,7 +110,7 @@ static int fail(int code, const std::string& msg) {
             return fail(PFM_E_HIP, std::string(#expr) + ": " + hipGetErrorString(_e));           \
     } while (0)
 
-static thread_local PfmKnobs t_knobs = {0, 0, 1, 8, 0, 1, 0, 2, 1, 0, -1, 0, 0, 1, 0, 1, 1, 1, 0, 1, 0, 0, 1, 0};
+static thread_local PfmKnobs t_knobs = {0, 0, 1, 8, 0, 1, 0, 2, 1, 0, -1, 0, 0, 1, 0, 1, 1, 1, 0, 1, 0, 0, 1};
 
 const PfmKnobs& pfm_knobs() { return t_knobs; }
 
@@ -142,10 +142,9 @@ void pfm_knobs_refresh() {
     k.exact_x6 = iv("PFM_EXACT_X6", 1) != 0;
     k.attn_var = iv("PFM_ATTN_VAR", 0);
     k.dec_subbatch = std::max(1, iv("PFM_DEC_SUBBATCH", 1));
-    k.cu_split = iv("PFM_CU_SPLIT", 0);
     const int* f = &k.ln_fold;
     unsigned long long s = 1469598103934665603ull;   // FNV-1a over the fields
-    for (int i = 0; i < 23; ++i) s = (s ^ (unsigned long long)(unsigned)f[i]) * 1099511628211ull;
+    for (int i = 0; i < 22; ++i) s = (s ^ (unsigned long long)(unsigned)f[i]) * 1099511628211ull;
     k.sig = s;
     t_knobs = k;
 }
@@ -1004,23 +1003,6 @@ int encoder_stack(const Run& r, const float* x_in, const int* lens, int B, int T
 }
 
 
-// Utterance-group stream k of n. PFM_CU_SPLIT (read when the handle first creates the stream): 0 = all
-// CUs; 1 = CU k*n_cu/n .. (k+1)*n_cu/n - 1 of the mask; 2 = every n-th CU starting at k (a CU-masked
-// stream is created blocking; the groups still fork from / join into the caller's stream by events)
-hipError_t sub_stream_create(pfm_handle* h, int k, int n) {
-    const int mode = pfm_knobs().cu_split;
-    if (mode == 0 || n < 2) return hipStreamCreateWithFlags(&h->sub_st[k], hipStreamNonBlocking);
-    int ncu = 0;
-    hipError_t e = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, h->device);
-    if (e != hipSuccess) return e;
-    std::vector<uint32_t> m((size_t)(ncu + 31) / 32, 0u);
-    for (int i = 0; i < ncu; ++i) {
-        const bool mine = mode == 1 ? ((long long)i * n / ncu) == k : (i % n) == k;
-        if (mine) m[(size_t)i / 32] |= 1u << (i % 32);
-    }
-    return hipExtStreamCreateWithCUMask(&h->sub_st[k], (uint32_t)m.size(), m.data());
-}
-
 int subbatch_count(pfm_handle* h, int B) {   // PFM_SUBBATCH=n (1 disables); profiling runs unsplit
     const int v = std::min(pfm_knobs().subbatch, (int)pfm_handle::MAXSUB);
     if (h->prof_on) return 1;
@@ -1041,7 +1023,7 @@ int encoder_split(pfm_handle* h, const Run& r, const float* x_in, const int* len
     HIP_TRY(hipEventRecord(h->ev_fork, r.st));
     for (int k = 0; k < ns; ++k) {
         if (!h->sub_st[k]) {
-            HIP_TRY(sub_stream_create(h, k, ns));
+            HIP_TRY(hipStreamCreateWithFlags(&h->sub_st[k], hipStreamNonBlocking));
             HIP_TRY(hipEventCreateWithFlags(&h->ev_join[k], hipEventDisableTiming));
         }
         const int b0 = (int)((long long)B * k / ns), b1 = (int)((long long)B * (k + 1) / ns);
@@ -1448,7 +1430,7 @@ int pfm_run(pfm_handle* h, void* stream, int mode, const float* feats, const int
     HIP_TRY(hipEventRecord(h->ev_fork, st));
     for (int k = 0; k < ng; ++k) {
         if (!h->sub_st[k]) {
-            HIP_TRY(sub_stream_create(h, k, ng));
+            HIP_TRY(hipStreamCreateWithFlags(&h->sub_st[k], hipStreamNonBlocking));
             HIP_TRY(hipEventCreateWithFlags(&h->ev_join[k], hipEventDisableTiming));
         }
         const int b0 = (int)((long long)B * k / ng), b1 = (int)((long long)B * (k + 1) / ng);

@@ -157,7 +157,6 @@ struct PfmKnobs {
     int exact_x6;           // PFM_EXACT_X6 (default 1): EXACT-mode GEMMs as split bf16 x6 MFMA (f32 MFMA if 0)
     int attn_var;           // PFM_ATTN_VAR: diagnostic variants of the 8-wave bf16 attention kernel (0 = the kernel)
     int dec_subbatch;       // PFM_DEC_SUBBATCH (default 1): decoder utterance groups on concurrent streams
-    int cu_split;           // PFM_CU_SPLIT: utterance-group streams on disjoint CU sets (1 blocks, 2 interleaved)
     unsigned long long sig;
 };
 const PfmKnobs& pfm_knobs();

@@ -116,6 +116,21 @@ def test_large_exact_tokens(engines, name):
     assert np.abs(a - g["alphas"]).max() < 1e-5
 
 
+@pytest.mark.parametrize("name", ["para_large_ragged", "para_large_b4"])
+@pytest.mark.parametrize("env", [{"PFM_DEC_SUBBATCH": "2"}, {"PFM_SUBBATCH": "1", "PFM_DEC_SUBBATCH": "2"}])
+def test_large_exact_tokens_grouped_decoder(engines, monkeypatch, name, env):
+    """The decoder as utterance groups on concurrent streams (offset row pointers, one argmax reduction
+    after the join) stays token-exact."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    e = engines["large"]
+    g = np.load(f"{GOLD}/{name}.npz")
+    r = _run(e, g, "exact")
+    torch.cuda.synchronize()
+    assert np.array_equal(r["ntok"].cpu().numpy(), g["ntok"])
+    assert _tokens_from_run(r, e.cfg) == _golden_tokens(g)
+
+
 @pytest.mark.parametrize("name", ["para_large_ragged", "para_large_b4", "para_large_c1"])
 def test_large_fast_agreement(engines, name):
     e = engines["large"]
