@@ -1361,8 +1361,7 @@ hipError_t pfm_gemm_bf16_256(const void* A, RowMap amap, const void* W, long lon
     // (EXACT mode x6 GEMMs keep the fast-mode tiles: C17 for N >= 1024 and C16 for 512-wide x6 GEMMs were
     // faster in isolation — tools/gemm_cfg_scan.py SCAN_X6=1 — but slower on the two-group path, 99.3 and
     // 104.8 vs 98.0 ms/step; unsplit, C17 for the wide ones 100.9 vs 101.3, both 111.6)
-    if (epi.x6_k && cfg == 3) cfg = 4;
-    if (epi.x6_k && cfg != 1 && cfg != 4 && cfg != 13 && cfg != 15 && cfg != 16 && cfg != 17) cfg = 15;
+    if (epi.x6_k && cfg != 1 && cfg != 3 && cfg != 4 && cfg != 13 && cfg != 15 && cfg != 16 && cfg != 17) cfg = 15;
     if (epi.x6_k && (K != 6 * epi.x6_k || epi.x6_k % 64 || ln)) return hipErrorInvalidValue;
     switch (cfg) {
         case 2: return launch<C2>(A, amap, W, ldw, M, N, K, e2, st);
