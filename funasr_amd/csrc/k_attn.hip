@@ -39,6 +39,7 @@ struct AttnArgs {
     // optional fused FSMN memory block (encoder self-attention, fast mode): fout[b*Tq + t][h*DK + c] =
     // mask * (sum_k fw[k][h*DK + c] * vm[t - 5 + k] + vm[t]), vm = V rows masked by klen (K = 11, left 5)
     const float* fw; bf16* fout; long long fld; int fD;
+    float* fout32 = nullptr;      // EXACT mode (x6 kernel): the same FSMN block in f32 (fout's row stride fld)
 };
 
 // ---- f32 tile geometry (bytes)
@@ -223,6 +224,57 @@ __device__ __forceinline__ f32x16 mfma_x6(const bf16x8& a0, const bf16x8& a1, co
     return mfma32(a0, b0, c);
 }
 
+// Fused FSMN memory block, EXACT mode (f32 V in, f32 out): the arithmetic of fsmn_win_kernel<11, float, 5>
+// (fma chain over the 11 taps ascending from 0, then + x[t]; rows t >= klen are 0). Thread = 4 channels x
+// 8 rows of the block's QB rows x this head's 128 channels; the window comes from global memory (V was just
+// streamed by the key loop). No barriers: threads past Tq simply stop.
+template <int QB, int NTH>
+__device__ __forceinline__ void fsmn_epilogue_f32(const AttnArgs& a, int qt, int h, int b, int klen) {
+    constexpr int FK = 11, FL = 5, CQ = DK / 4, RPT = 8, RG = NTH / CQ;
+    static_assert(QB % (RG * RPT) == 0, "whole passes of RG x RPT rows");
+    const int cq = threadIdx.x % CQ, rg = threadIdx.x / CQ;
+    const int c = h * DK + cq * 4;
+    const float* V = (const float*)a.v;
+    float4 w[FK];
+#pragma unroll
+    for (int k = 0; k < FK; ++k) w[k] = *(const float4*)(a.fw + (long long)k * a.fD + c);
+#pragma unroll 1
+    for (int pass = 0; pass < QB / (RG * RPT); ++pass) {
+        const int t0 = qt * QB + (pass * RG + rg) * RPT;
+        if (t0 >= a.Tq) break;
+        float4 x[RPT + FK - 1];
+#pragma unroll
+        for (int i = 0; i < RPT + FK - 1; ++i) {
+            const int tc = min(max(t0 - FL + i, 0), a.Tk - 1);
+            x[i] = *(const float4*)(V + a.vmap.off((long long)b * a.Tk + tc) + c);
+        }
+#pragma unroll
+        for (int i = 0; i < RPT + FK - 1; ++i) {
+            const int tt = t0 - FL + i;
+            if (!(tt >= 0 && tt < klen)) x[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (int i = 0; i < RPT; ++i) {
+            const int t = t0 + i;
+            if (t >= a.Tq) break;
+            float4 y = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (t < klen) {
+                float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+                for (int k = 0; k < FK; ++k) {
+                    acc.x = fmaf(w[k].x, x[i + k].x, acc.x);
+                    acc.y = fmaf(w[k].y, x[i + k].y, acc.y);
+                    acc.z = fmaf(w[k].z, x[i + k].z, acc.z);
+                    acc.w = fmaf(w[k].w, x[i + k].w, acc.w);
+                }
+                const float4 self = x[i + FL];
+                y = make_float4(acc.x + self.x, acc.y + self.y, acc.z + self.z, acc.w + self.w);
+            }
+            *(float4*)(a.fout32 + ((long long)b * a.Tq + t) * a.fld + c) = y;
+        }
+    }
+}
+
 __global__ __launch_bounds__(512) void attn_x6_kernel(AttnArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int qt = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
@@ -375,7 +427,7 @@ __global__ __launch_bounds__(512) void attn_x6_kernel(AttnArgs a) {
         }
         __syncthreads();
     }
-    if (qrow >= a.Tq) return;
+    if (qrow < a.Tq) {
     const float inv = (klen > 0) ? 1.f / lrun : 0.f;
     float* op = a.o ? a.o + ((long long)b * a.Tq + qrow) * a.ldo + h * DK : nullptr;
     bf16* op2 = a.o2 ? (bf16*)a.o2 + ((long long)b * a.Tq + qrow) * a.ldo + h * DK : nullptr;
@@ -405,6 +457,8 @@ __global__ __launch_bounds__(512) void attn_x6_kernel(AttnArgs a) {
                 }
             }
         }
+    }
+    if (a.fout32) fsmn_epilogue_f32<256, 512>(a, qt, h, b, klen);
 }
 
 // ---- bf16 kernel geometry: 64-key tiles; K row-major with a 16-B chunk XOR swizzle (conflict-free
@@ -960,15 +1014,22 @@ hipError_t pfm_attention_fsmn(int dtype, const void* q, RowMap qmap, const void*
 
 // EXACT mode (split-bf16 x6 attention) with the output written as the split operand of the out-projection:
 // out3 rows of 3 x heads x 128 bf16 (x0 | x1 | x2 planes, heads x 128 apart). q/k/v f32.
+// fsmn_wT / fsmn_out (optional, both or neither): the encoder's FSMN memory block (K 11, left 5) on v in
+// the epilogue, f32 rows of fsmn_ld floats (self-attention only: Tq == Tk).
 hipError_t pfm_attention_x3(const float* q, RowMap qmap, const float* k, RowMap kmap, const float* v, RowMap vmap,
                             bf16* out3, const int* klen, int B, int Tq, int Tk, int heads, int dk, float scale,
-                            hipStream_t st) {
+                            const float* fsmn_wT, float* fsmn_out, long long fsmn_ld, hipStream_t st) {
     if (B <= 0 || Tq <= 0) return hipSuccess;
     if (dk != DK || !pfm_knobs().exact_x6) return hipErrorInvalidValue;
+    if ((fsmn_out != nullptr) != (fsmn_wT != nullptr)) return hipErrorInvalidValue;
+    if (fsmn_out && (Tq != Tk || fsmn_ld % 4 || vmap.ld % 4 || vmap.rows_per_seg > 0 || ((uintptr_t)fsmn_out % 16) ||
+                     ((uintptr_t)v % 16) || ((uintptr_t)fsmn_wT % 16)))
+        return hipErrorInvalidValue;
     AttnArgs a;
     a.q = q; a.qmap = qmap; a.k = k; a.kmap = kmap; a.v = v; a.vmap = vmap;
     a.o = nullptr; a.ldo = 3LL * heads * DK; a.o2 = out3; a.o2_dtype = DT_X3; a.klen = klen; a.Tq = Tq; a.Tk = Tk;
-    a.scale = scale; a.fw = nullptr; a.fout = nullptr; a.fld = 0; a.fD = heads * DK;
+    a.scale = scale; a.fw = fsmn_wT; a.fout = nullptr; a.fld = fsmn_ld; a.fD = heads * DK;
+    a.fout32 = fsmn_out;
     static bool attr_done = false;
     if (!attr_done) {
         attr_done = true;

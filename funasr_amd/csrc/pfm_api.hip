@@ -66,7 +66,7 @@ hipError_t pfm_split3_rows(const float* x, RowMap xm, int M, int K, int Kp, bf16
 hipError_t pfm_split3_planes(const float* x, bf16* p, long long plane, long long n, hipStream_t st);
 hipError_t pfm_attention_x3(const float* q, RowMap qmap, const float* k, RowMap kmap, const float* v, RowMap vmap,
                             bf16* out3, const int* klen, int B, int Tq, int Tk, int heads, int dk, float scale,
-                            hipStream_t st);
+                            const float* fsmn_wT, float* fsmn_out, long long fsmn_ld, hipStream_t st);
 hipError_t pfm_ffn_pack(const bf16* W1, const bf16* W2, bf16* Wp, hipStream_t st);
 hipError_t pfm_ffn_fused(const float* x, int M, const float* g2, const float* be2, float eps, const bf16* Wp,
                          const float* b1, const float* b2, float* xo, const float* gn, const float* bn, bf16* xn,
@@ -699,6 +699,7 @@ struct Run {
     double es;       // operand element size
     float qscale;    // d_k ** -0.5
     bool fuse_fsmn;  // fast mode: encoder FSMN in the attention epilogue
+    bool fuse_fsmn_x6 = false;   // EXACT mode (x3): the f32 FSMN in the x6 attention epilogue
     bool fuse_ln;    // opt-in (PFM_GEMM_LN=1): LayerNorm fused into the 512-wide projections
     bool x3 = false;     // EXACT mode on split-bf16 x6: producers write GEMM operands as three bf16 planes
     bool raw_input = false;                 // streaming: the stack input is already x sqrt(d) + PE
@@ -714,6 +715,7 @@ struct Run {
         fuse_ln = fast && c.d_model == 512 && c.ffn % 32 == 0 && gemm_ln_enabled();
         x3 = !fast && h->x6_ready && pfm_knobs().exact_x6 && c.d_model % 64 == 0 && c.ffn % 64 == 0 &&
              c.d_model / c.heads == 128;
+        fuse_fsmn_x6 = x3 && c.kernel_size == 11 && lenc == 5 && pfm_knobs().attn_fsmn;
     }
     const void* W(size_t off) const { return fast ? (const void*)h->wb(off) : (const void*)h->w(off); }
     const float* P(size_t off) const { return h->w(off); }
@@ -744,14 +746,17 @@ struct Run {
         return gemm_x6(h, nullptr, am, (const float*)Wt, Mm, N, Kk, e, s, (const bf16*)A3);
     }
     // EXACT-mode attention writing the out-projection's split operand (out3 rows of 3 x d_model bf16)
+    // (fsmn_wT / fsmn_out: the encoder FSMN block fused into the epilogue, f32 rows of d_model)
     hipError_t attn3(const float* q, RowMap qm, const float* k, RowMap km, const float* v, RowMap vm, bf16* out3,
-                     const int* kl, int Bb, int Tq, int Tk) const {
+                     const int* kl, int Bb, int Tq, int Tk, const float* fsmn_wT = nullptr,
+                     float* fsmn_out = nullptr) const {
         const pfm_config& c = h->cfg;
         const double dk = c.d_model / c.heads;
         const double fl = 4.0 * Bb * Tq * (double)Tk * dk * c.heads;
         const double by = ((double)Bb * Tq + 2.0 * Bb * Tk) * c.d_model * 4.0 + (double)Bb * Tq * c.d_model * 6.0;
         ProfScope ps(h, st, PFM_K_ATTN, fl, by);
-        return pfm_attention_x3(q, qm, k, km, v, vm, out3, kl, Bb, Tq, Tk, c.heads, (int)dk, qscale, st);
+        return pfm_attention_x3(q, qm, k, km, v, vm, out3, kl, Bb, Tq, Tk, c.heads, (int)dk, qscale, fsmn_wT,
+                                fsmn_out, c.d_model, st);
     }
     hipError_t attn(int dtp, const void* q, RowMap qm, const void* k, RowMap km, const void* v, RowMap vm, float* o,
                     long long ldo, void* o2, const int* kl, int Bb, int Tq, int Tk) const {
@@ -919,6 +924,9 @@ int encoder_stack(const Run& r, const float* x_in, const int* lens, int B, int T
                                     nullptr, Fb, st));
             HIP_TRY(r.attn(DT_BF16, QKVb, rowmap_plain(3 * D), QKVb + D, rowmap_plain(3 * D), QKVb + 2 * D,
                            rowmap_plain(3 * D), nullptr, D, Ob, lens, B, T, T));
+        } else if (x3 && r.fuse_fsmn_x6) {   // EXACT mode: the f32 FSMN in the x6 attention epilogue
+            HIP_TRY(r.attn3(QKV, rowmap_plain(3 * D), QKV + D, rowmap_plain(3 * D), QKV + 2 * D, rowmap_plain(3 * D),
+                            (bf16*)O, lens, B, T, T, r.P(L.fsmn), Fm));
         } else {
             HIP_TRY(pfm_fsmn(QKV + 2 * D, rowmap_plain(3 * D), lens, B, T, D, r.P(L.fsmn), K, lenc, nullptr, Fm,
                              nullptr, st));

@@ -180,16 +180,17 @@ def test_fast_fused_layernorm_matches_unfused(engines, monkeypatch):
     assert np.mean(agree) > 0.9, np.mean(agree)
 
 
-def test_fast_fused_fsmn_is_bit_identical(engines, monkeypatch):
-    """Fast mode computes the encoder FSMN in the attention kernel's epilogue; PFM_ATTN_FSMN=0 runs the
-    standalone FSMN kernel. Same bf16 inputs, same f32 operation order -> identical encoder output,
-    alphas and tokens."""
+@pytest.mark.parametrize("mode", ["fast", "exact"])
+def test_fused_fsmn_is_bit_identical(engines, monkeypatch, mode):
+    """Both modes compute the encoder FSMN in the attention kernel's epilogue (fast: bf16 8-wave kernel,
+    exact: f32 in the split-bf16 x6 kernel); PFM_ATTN_FSMN=0 runs the standalone FSMN kernel. Same inputs,
+    same f32 operation order -> identical encoder output, alphas and tokens."""
     e = engines["large"]
     g = np.load(f"{GOLD}/para_large_ragged.npz")
-    r1 = _run(e, g, "fast")
+    r1 = _run(e, g, mode)
     torch.cuda.synchronize()
     monkeypatch.setenv("PFM_ATTN_FSMN", "0")
-    r0 = _run(e, g, "fast")
+    r0 = _run(e, g, mode)
     torch.cuda.synchronize()
     assert torch.equal(r1["enc"], r0["enc"])
     assert torch.equal(r1["alphas"], r0["alphas"])
