@@ -507,13 +507,13 @@ int reserve(pfm_handle* h, int B, int T) {
         HIP_TRY(h->emb.ensure(Ml * D * 4));
         HIP_TRY(h->KV.ensure(M * nkv * 4));
         HIP_TRY(h->Xd.ensure(Ml * D * 4));
-        HIP_TRY(h->Xdn.ensure(Ml * D * 4));
+        HIP_TRY(h->Xdn.ensure(Ml * D * 6));   // EXACT mode: split operands (three bf16 planes)
         HIP_TRY(h->Hd.ensure(Ml * F * 4));
-        HIP_TRY(h->Hdn.ensure(Ml * F * 4));
+        HIP_TRY(h->Hdn.ensure(Ml * F * 6));
         HIP_TRY(h->Td.ensure(Ml * D * 4));
         HIP_TRY(h->Tdn.ensure(Ml * D * 4));
         HIP_TRY(h->Qd.ensure(Ml * D * 4));
-        HIP_TRY(h->Od.ensure(Ml * D * 4));
+        HIP_TRY(h->Od.ensure(Ml * D * 6));
         HIP_TRY(h->Odb.ensure(Ml * D * 2));
         HIP_TRY(h->amv.ensure(Ml * nt * 4));
         HIP_TRY(h->ami.ensure(Ml * nt * 4));
@@ -1315,16 +1315,27 @@ int pfm_run(pfm_handle* h, void* stream, int mode, const float* feats, const int
     auto dec_group = [&](const Run& rg, int b0, int nb) -> int {
         hipStream_t s = rg.st;
         const size_t esz = fast ? 2 : 4;
+        // EXACT mode on split-bf16 x6: the LayerNorms feeding a GEMM (LN1, LN3, LN_F, after_norm) and the
+        // cross-attention write that GEMM's A operand as three bf16 planes (DT_X3, 6 B per element)
+        const bool x3d = rg.x3;
+        const size_t xsz = x3d ? 6 : esz;
+        const int ndt = x3d ? DT_X3 : dt;
+        const RowMap xdm = rowmap_plain(x3d ? 3 * D : D), hdm = rowmap_plain(x3d ? 3 * Fd : Fd);
         const long long r0 = (long long)b0 * L;
         const int Mg = (int)((long long)nb * L);
         float* Xd = h->Xd.as<float>() + r0 * D;
-        void* Xdn = h->Xdn.as<char>() + r0 * D * esz;
+        void* Xdn = h->Xdn.as<char>() + r0 * D * xsz;
         void* Hd = h->Hd.as<char>() + r0 * Fd * esz;   // fast: bf16 hidden, exact: f32
-        void* Hdn = h->Hdn.as<char>() + r0 * Fd * esz;
+        void* Hdn = h->Hdn.as<char>() + r0 * Fd * xsz;
         float* Td = h->Td.as<float>() + r0 * D;
         void* Tdn = h->Tdn.as<char>() + r0 * D * esz;
         void* Qd = h->Qd.as<char>() + r0 * D * esz;
-        float* Od = h->Od.as<float>() + r0 * D;
+        float* Od = (float*)(h->Od.as<char>() + r0 * D * (x3d ? 6 : 4));
+        // a GEMM whose A operand a producer wrote as rows of xdm / hdm
+        auto gemmA = [&](const void* A, bool wide, const void* Wt, int N, int Kk, const GemmEpi& e) -> hipError_t {
+            if (x3d) return rg.gemm3(A, wide ? hdm : xdm, Wt, Kk, Mg, N, Kk, e);
+            return rg.gemm(dt, A, rowmap_plain(Kk), Wt, Kk, Mg, N, Kk, e);
+        };
         bf16* Odb = h->Odb.as<bf16>() + r0 * D;
         const int* ntg = ntok + b0;
         const int* lg = lens + b0;
@@ -1333,27 +1344,27 @@ int pfm_run(pfm_handle* h, void* stream, int mode, const float* feats, const int
                        float* out, size_t pg, size_t pb, void* pout, int pdt) -> int {
             // out = W2 . LN_F(relu(W1 . LN(x) + b1)); pout = LN_P(out)   (sanm/positionwise_feed_forward.py:26-33)
             if (!xdn_ready)
-                HIP_TRY(pfm_layernorm(Xd, rowmap_plain(D), Mg, D, P(lng), P(lnb), c.ln_eps, nullptr, 0, 1.f, Xdn,
-                                      rowmap_plain(D), dt, nullptr, plain, 0, s));
+                HIP_TRY(pfm_layernorm(Xd, rowmap_plain(D), Mg, D, P(lng), P(lnb), c.ln_eps, nullptr, 0, 1.f, Xdn, xdm,
+                                      ndt, nullptr, plain, 0, s));
             GemmEpi e = epi_default();
             e.bias = P(b1); e.relu = 1;
             e.out = Hd; e.out_map = rowmap_plain(Fd); e.out_dtype = fast ? DT_BF16 : DT_F32;   // fast: bf16 hidden
-            HIP_TRY(rg.gemm(dt, Xdn, rowmap_plain(D), W(w1), D, Mg, Fd, D, e));
+            HIP_TRY(gemmA(Xdn, false, W(w1), Fd, D, e));
             if (fast)
                 HIP_TRY(pfm_layernorm_bf16in((const bf16*)Hd, rowmap_plain(Fd), Mg, Fd, P(fng), P(fnb), c.ln_eps, Hdn,
                                              rowmap_plain(Fd), dt, s));
             else
                 HIP_TRY(pfm_layernorm((const float*)Hd, rowmap_plain(Fd), Mg, Fd, P(fng), P(fnb), c.ln_eps, nullptr, 0,
-                                      1.f, Hdn, rowmap_plain(Fd), dt, nullptr, plain, 0, s));
+                                      1.f, Hdn, hdm, ndt, nullptr, plain, 0, s));
             GemmEpi e2 = epi_default();
             if (fuse_ln) {   // out itself is dead; only LN_P(out) is consumed
                 HIP_TRY(rg.gemm_ln(Hdn, rowmap_plain(Fd), W(w2), Fd, Mg, Fd, e2, pg, pb, pout, rowmap_plain(D), pdt,
                                    nullptr, plain));
             } else {
                 e2.out = out; e2.out_map = rowmap_plain(D); e2.out_dtype = DT_F32;
-                HIP_TRY(rg.gemm(dt, Hdn, rowmap_plain(Fd), W(w2), Fd, Mg, D, Fd, e2));
+                HIP_TRY(gemmA(Hdn, true, W(w2), D, Fd, e2));
                 HIP_TRY(pfm_layernorm(out, rowmap_plain(D), Mg, D, P(pg), P(pb), c.ln_eps, nullptr, 0, 1.f, pout,
-                                      rowmap_plain(D), pdt, nullptr, plain, 0, s));
+                                      rowmap_plain(pdt == DT_X3 ? 3 * D : D), pdt, nullptr, plain, 0, s));
             }
             return PFM_OK;
         };
@@ -1372,19 +1383,23 @@ int pfm_run(pfm_handle* h, void* stream, int mode, const float* feats, const int
                 HIP_TRY(pfm_fsmn((const float*)Tdn, rowmap_plain(D), ntg, nb, L, D, P(Lr.fsmn), K, ldec, Xd, Xd, nullptr,
                                  s));
             // x = x + CrossAtt(LN3(x), memory)   (decoder.py:109-119)
-            HIP_TRY(pfm_layernorm(Xd, rowmap_plain(D), Mg, D, P(Lr.n3g), P(Lr.n3b), c.ln_eps, nullptr, 0, 1.f, Xdn,
-                                  rowmap_plain(D), dt, nullptr, plain, 0, s));
+            HIP_TRY(pfm_layernorm(Xd, rowmap_plain(D), Mg, D, P(Lr.n3g), P(Lr.n3b), c.ln_eps, nullptr, 0, 1.f, Xdn, xdm,
+                                  ndt, nullptr, plain, 0, s));
             {
                 GemmEpi e = epi_default();
                 e.bias = P(Lr.bq);
                 e.out = Qd; e.out_map = rowmap_plain(D); e.out_dtype = dt;
-                HIP_TRY(rg.gemm(dt, Xdn, rowmap_plain(D), W(Lr.wq), D, Mg, D, D, e));
+                HIP_TRY(gemmA(Xdn, false, W(Lr.wq), D, D, e));
             }
             if (l == 0 && kv_async) HIP_TRY(hipStreamWaitEvent(s, h->ev_kv, 0));   // join the side stream
             {
                 const char* kvb = KVg + (size_t)l * 2 * D * esz;
-                HIP_TRY(rg.attn(dt, Qd, rowmap_plain(D), kvb, rowmap_plain(nkv), kvb + (size_t)D * esz,
-                                rowmap_plain(nkv), fast ? nullptr : Od, D, fast ? (void*)Odb : nullptr, lg, nb, L, T));
+                if (x3d)
+                    HIP_TRY(rg.attn3((const float*)Qd, rowmap_plain(D), (const float*)kvb, rowmap_plain(nkv),
+                                     (const float*)(kvb + (size_t)D * esz), rowmap_plain(nkv), (bf16*)Od, lg, nb, L, T));
+                else
+                    HIP_TRY(rg.attn(dt, Qd, rowmap_plain(D), kvb, rowmap_plain(nkv), kvb + (size_t)D * esz,
+                                    rowmap_plain(nkv), fast ? nullptr : Od, D, fast ? (void*)Odb : nullptr, lg, nb, L, T));
             }
             {
                 GemmEpi e = epi_default();
@@ -1398,14 +1413,13 @@ int pfm_run(pfm_handle* h, void* stream, int mode, const float* feats, const int
                                        nullptr, plain));
                     xdn_ready = true;
                 } else {
-                    HIP_TRY(rg.gemm(dt, fast ? (const void*)Odb : (const void*)Od, rowmap_plain(D), W(Lr.wo), D, Mg, D,
-                                    D, e));
+                    HIP_TRY(gemmA(fast ? (const void*)Odb : (const void*)Od, false, W(Lr.wo), D, D, e));
                 }
             }
         }
         // decoders3: x = FFN(LN1(x)), no residual (decoder.py:97-100 with self_attn = src_attn = None)
         int rc3 = ffn(xdn_ready, h->d3n1g, h->d3n1b, h->d3w1, h->d3b1, h->d3ng, h->d3nb, h->d3w2, Xd, h->dan_g,
-                      h->dan_b, Xdn, dt);
+                      h->dan_b, Xdn, ndt);
         if (rc3) return rc3;
         {   // output layer with fused row-argmax (logits never written)
             const int ntl = amax_tiles(dt, rowmap_plain(D), D, c.vocab_size, D, h, W(h->out_w));
@@ -1413,7 +1427,7 @@ int pfm_run(pfm_handle* h, void* stream, int mode, const float* feats, const int
             e.bias = P(h->out_b);
             e.amax_val = h->amv.as<float>() + r0 * ntl; e.amax_idx = h->ami.as<int>() + r0 * ntl; e.n_tiles = ntl;
             e.out = nullptr;
-            HIP_TRY(rg.gemm(dt, Xdn, rowmap_plain(D), W(h->out_w), D, Mg, c.vocab_size, D, e));
+            HIP_TRY(gemmA(Xdn, false, W(h->out_w), c.vocab_size, D, e));
         }
         return PFM_OK;
     };
