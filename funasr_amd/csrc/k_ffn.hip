@@ -34,6 +34,7 @@ typedef const __attribute__((address_space(1))) void gbl_void;
 constexpr int FD = 512, FF = 2048, BM = 64, NTH = 512;
 constexpr int HC = 256, NCH = FF / HC;          // hidden chunk, chunks
 constexpr int TILE = 16384, TPC = 32, NTILE = NCH * TPC;
+constexpr int OP_TILES = 32;                    // out-projection Wo [512][512]: 16 k steps x 2 halves (W2 format)
 constexpr int OFF_AN = 0, OFF_H = 65536, OFF_RING = 98304, LDS_BYTES = 163840;
 constexpr int YP = 516;                         // epilogue f32 row pitch (floats)
 
@@ -60,21 +61,32 @@ struct Frag { bf16x8 w[2]; bf16x8 a[4]; };
 // VAR (diagnostic builds, PFM_FFN_VAR): 0 = the kernel; 1 = no weight DMA (stale ring); 2 = no MFMAs;
 // 3 = every tile streams ring tiles 0..3 of the layer (L2-hot 64 KiB); 4 = prologue + epilogue only (no
 // tile loop); 5 = VAR 1 without the per-tile barriers (MFMA + fragment reads alone)
-template <int VAR>
+//
+// OP (the attention sub-layer's out-projection folded in front): the block starts from the attention output
+// O and the FSMN output F (bf16 rows) instead of x:
+//   phase 0   Y0^T[512 x 64] = Wo . O^T   (O image in the A slot; 32 Wo tiles in W2 format lead the ring)
+//   x1 = ((Y0 + bo) + F) + x  (x optional: layer 0 has no residual)  kept in the phase-2 accumulators,
+//   LN2(x1) -> bf16 A image (row statistics reduced across the 8 waves through LDS), accumulators += b2,
+//   then the FFN loop above accumulates W2 . H on top: the epilogue stores x2 = accumulators directly.
+// x1 never leaves the CU (one kernel and one HBM round trip of the residual stream less per layer).
+template <int VAR, bool OP = false>
 __global__ __launch_bounds__(NTH) void ffn_fused_kernel(const float* __restrict__ X, int M, const float* __restrict__ g2,
                                                         const float* __restrict__ be2, float eps,
                                                         const bf16* __restrict__ Wp, const float* __restrict__ b1,
                                                         const float* __restrict__ b2, float* Xo,
                                                         const float* __restrict__ gn, const float* __restrict__ bn,
-                                                        bf16* __restrict__ Xn) {
+                                                        bf16* __restrict__ Xn, const bf16* __restrict__ O,
+                                                        const bf16* __restrict__ Fr, const float* __restrict__ bo) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int g = lane >> 4, r16 = lane & 15;
     const long long m0 = (long long)blockIdx.x * BM;
+    constexpr int T0 = OP ? OP_TILES : 0;      // FFN tiles start after the Wo tiles
+    constexpr int NT_ALL = NTILE + T0;
 
     auto issue = [&](int t) {
-        if (t >= NTILE || VAR == 1 || VAR == 5) return;
+        if (t >= NT_ALL || VAR == 1 || VAR == 5) return;
         const bf16* src = Wp + (long long)(VAR == 3 ? (t & 3) : t) * (TILE / 2) + (2 * w * 64 + lane) * 8;
         unsigned char* dst = smem + OFF_RING + (t & 3) * TILE + 2 * w * 1024;
         __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)dst, 16, 0, 0);
@@ -88,7 +100,19 @@ __global__ __launch_bounds__(NTH) void ffn_fused_kernel(const float* __restrict_
         __builtin_amdgcn_sched_barrier(0);
     };
     // ---- prologue: LN2 of rows m0 + 8w .. + 7 -> bf16 A image (row pitch 1 KiB, slot ^ (row & 15))
-    {
+    //      (OP: the attention output rows go to the A image instead; LN2 follows phase 0)
+    if constexpr (OP) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int m = 8 * w + i;
+            const long long row = min(m0 + m, (long long)M - 1);
+            const bf16x8 v = *(const bf16x8*)(O + row * FD + 8 * lane);
+            *(bf16x8*)(smem + OFF_AN + m * 1024 + ((lane ^ (m & 15)) << 4)) = v;
+        }
+        issue(0);
+        issue(1);
+        issue(2);
+    } else {
         float4 xa[8], xb[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
@@ -213,7 +237,7 @@ __global__ __launch_bounds__(NTH) void ffn_fused_kernel(const float* __restrict_
     // the DMA of tile t+3 into the slot of tile t-1 (whose fragments every wave consumed in iteration t-1)
     auto top = [&](int t) {
         if (VAR != 1 && VAR != 5) {
-            if (t + 2 < NTILE) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+            if (t + 2 < NT_ALL) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
             else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
         bar();
@@ -225,9 +249,100 @@ __global__ __launch_bounds__(NTH) void ffn_fused_kernel(const float* __restrict_
     if (VAR != 1 && VAR != 5) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");   // tile 0 (tiles 1, 2 in flight)
     bar();
     Frag F0, F1;
-    rd1(0, F0);
+    if constexpr (OP) {
+        // phase 0: Wo tile t = k step t >> 1 (of the O image in the A slot), half t & 1
+        auto rd0 = [&](int t, Frag& f) {
+            rd_w(t, f);
+            const int j = t >> 1;
+#pragma unroll
+            for (int mb = 0; mb < 4; ++mb)
+                f.a[mb] = ld128(smem + OFF_AN + (16 * mb + r16) * 1024 + (((4 * j + g) ^ r16) << 4));
+        };
+        rd0(0, F0);
+        for (int s2 = 0; s2 < OP_TILES / 2 - 1; ++s2) {
+            top(2 * s2); rd0(2 * s2 + 1, F1); mm2a(F0);
+            top(2 * s2 + 1); rd0(2 * s2 + 2, F0); mm2b(F1);
+        }
+        top(OP_TILES - 2); rd0(OP_TILES - 1, F1); mm2a(F0);
+        top(OP_TILES - 1); mm2b(F1);
+        // x1 = ((Y0 + bo) + F) + x in the accumulator layout: acc2{a,b}[nb][mb][e] = x1[row 16mb + r16]
+        // [col 32w + 16nb + 4g + e (+256 for b)]; LN2 row statistics: lane partials -> 4 g lanes -> 8 waves
+        float* red = (float*)(smem + OFF_H);   // [2][8 waves][64 rows] (the H image is free until chunk 0)
+        float part[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int mb = 0; mb < 4; ++mb) {
+            const long long row = min(m0 + 16 * mb + r16, (long long)M - 1);
+#pragma unroll
+            for (int hf = 0; hf < 2; ++hf)
+#pragma unroll
+                for (int nb = 0; nb < 2; ++nb) {
+                    const int n = 256 * hf + 32 * w + 16 * nb + 4 * g;
+                    f32x4& a = hf ? acc2b[nb][mb] : acc2a[nb][mb];
+                    const float4 bb4 = *(const float4*)(bo + n);
+                    const bf16x4 f4 = *(const bf16x4*)(Fr + row * FD + n);
+                    float4 x4 = make_float4(0.f, 0.f, 0.f, 0.f);
+                    if (X) x4 = *(const float4*)(X + row * FD + n);
+                    a[0] = ((a[0] + bb4.x) + bf2f(f4[0])) + x4.x;
+                    a[1] = ((a[1] + bb4.y) + bf2f(f4[1])) + x4.y;
+                    a[2] = ((a[2] + bb4.z) + bf2f(f4[2])) + x4.z;
+                    a[3] = ((a[3] + bb4.w) + bf2f(f4[3])) + x4.w;
+                    part[mb] += (a[0] + a[1]) + (a[2] + a[3]);
+                }
+        }
+        auto row_reduce = [&](float (&v)[4], int slot) {
+#pragma unroll
+            for (int mb = 0; mb < 4; ++mb) {
+                v[mb] += __shfl_xor(v[mb], 16, 64);
+                v[mb] += __shfl_xor(v[mb], 32, 64);
+                if (g == 0) red[slot * 512 + w * 64 + 16 * mb + r16] = v[mb];
+            }
+            bar();
+#pragma unroll
+            for (int mb = 0; mb < 4; ++mb) {
+                float t = 0.f;
+#pragma unroll
+                for (int ww = 0; ww < 8; ++ww) t += red[slot * 512 + ww * 64 + 16 * mb + r16];
+                v[mb] = t;
+            }
+        };
+        row_reduce(part, 0);   // its barrier also retires every wave's phase-0 reads of the O image
+        float mean[4], q[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int mb = 0; mb < 4; ++mb) mean[mb] = part[mb] * (1.f / FD);
+#pragma unroll
+        for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+            for (int hf = 0; hf < 2; ++hf)
+#pragma unroll
+                for (int nb = 0; nb < 2; ++nb) {
+                    const f32x4& a = hf ? acc2b[nb][mb] : acc2a[nb][mb];
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) { const float d = a[e] - mean[mb]; q[mb] += d * d; }
+                }
+        row_reduce(q, 1);
+#pragma unroll
+        for (int mb = 0; mb < 4; ++mb) {
+            const int m = 16 * mb + r16;
+            const float rstd = 1.f / sqrtf(q[mb] * (1.f / FD) + eps);
+#pragma unroll
+            for (int hf = 0; hf < 2; ++hf)
+#pragma unroll
+                for (int nb = 0; nb < 2; ++nb) {
+                    const int n = 256 * hf + 32 * w + 16 * nb + 4 * g;
+                    f32x4& a = hf ? acc2b[nb][mb] : acc2a[nb][mb];
+                    const float4 gg = *(const float4*)(g2 + n), be = *(const float4*)(be2 + n);
+                    const float4 c2 = *(const float4*)(b2 + n);
+                    bf16x4 o = {f2bf((a[0] - mean[mb]) * rstd * gg.x + be.x), f2bf((a[1] - mean[mb]) * rstd * gg.y + be.y),
+                                f2bf((a[2] - mean[mb]) * rstd * gg.z + be.z), f2bf((a[3] - mean[mb]) * rstd * gg.w + be.w)};
+                    *(bf16x4*)(smem + OFF_AN + m * 1024 + (((n >> 3) ^ (m & 15)) << 4) + ((n & 7) << 1)) = o;
+                    a[0] += c2.x; a[1] += c2.y; a[2] += c2.z; a[3] += c2.w;   // x2 = (x1 + b2) + W2 . H
+                }
+        }
+        bar();   // the LN2 image is complete before chunk 0's first fragment reads
+    }
+    rd1(T0, F0);
     for (int c = 0; c < (VAR == 4 ? 0 : NCH); ++c) {
-        const int tb = TPC * c;
+        const int tb = T0 + TPC * c;
         // phase 1: 16 W1 tiles (H^T of this chunk), fragments alternate F0 / F1
         for (int j = 0; j < 14; j += 2) {
             top(tb + j); rd1(tb + j + 1, F1); mm1(F0);
@@ -249,13 +364,19 @@ __global__ __launch_bounds__(NTH) void ffn_fused_kernel(const float* __restrict_
 
     if (VAR == 4) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     // ---- epilogue: Y^T accumulators -> f32 row image; x + Y + b2 -> Xo; LN1_next -> Xn
+    //      (OP: the accumulators already hold x1 + b2 + W2 . H)
     float4 xa[8], xb[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-        const long long row = min(m0 + 8 * w + i, (long long)M - 1);
-        const float* xr = X + row * FD + 8 * lane;
-        xa[i] = *(const float4*)xr;
-        xb[i] = *(const float4*)(xr + 4);
+        if constexpr (OP) {
+            xa[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+            xb[i] = xa[i];
+        } else {
+            const long long row = min(m0 + 8 * w + i, (long long)M - 1);
+            const float* xr = X + row * FD + 8 * lane;
+            xa[i] = *(const float4*)xr;
+            xb[i] = *(const float4*)(xr + 4);
+        }
     }
     __syncthreads();   // every wave is past its last ring / A / H read (no DMA in flight here)
     float* Y = (float*)smem;
@@ -269,7 +390,11 @@ __global__ __launch_bounds__(NTH) void ffn_fused_kernel(const float* __restrict_
             *(f32x4*)(Y + m * YP + 256 + n) = acc2b[nb][mb];
         }
     bar();
-    const float4 c2a = *(const float4*)(b2 + 8 * lane), c2b = *(const float4*)(b2 + 8 * lane + 4);
+    float4 c2a = *(const float4*)(b2 + 8 * lane), c2b = *(const float4*)(b2 + 8 * lane + 4);
+    if constexpr (OP) {
+        c2a = make_float4(0.f, 0.f, 0.f, 0.f);
+        c2b = c2a;
+    }
     float4 na = {0, 0, 0, 0}, nbv = {0, 0, 0, 0}, qa = {0, 0, 0, 0}, qb = {0, 0, 0, 0};
     if (Xn) {
         na = *(const float4*)(gn + 8 * lane); nbv = *(const float4*)(gn + 8 * lane + 4);
@@ -326,9 +451,26 @@ __global__ __launch_bounds__(256) void ffn_pack_kernel(const bf16* __restrict__ 
     *(bf16x8*)(Wp + (long long)gid * 8) = *(const bf16x8*)src;
 }
 
+// Wo [512 out][512 in] -> 32 tiles in the W2 tile format: tile t = k step t >> 1, half t & 1 (rows
+// 256 (t & 1) + row), so phase 0 reads them exactly like phase 2 reads a chunk's W2 tiles.
+__global__ __launch_bounds__(256) void ffn_pack_o_kernel(const bf16* __restrict__ Wo, bf16* __restrict__ Wp) {
+    const int gid = blockIdx.x * 256 + threadIdx.x;   // < OP_TILES * 1024
+    const int t = gid >> 10, u = gid & 1023;
+    const int row = u >> 2, ls = (u & 3) ^ f2(row);
+    const bf16* src = Wo + (long long)(256 * (t & 1) + row) * FD + 32 * (t >> 1) + 8 * ls;
+    *(bf16x8*)(Wp + (long long)gid * 8) = *(const bf16x8*)src;
+}
+
 }  // namespace
 
 size_t pfm_ffn_packed_elems() { return (size_t)NTILE * TILE / 2; }
+size_t pfm_ffn_packed_o_elems() { return (size_t)OP_TILES * TILE / 2; }
+
+hipError_t pfm_ffn_pack_o(const bf16* Wo, bf16* Wp, hipStream_t st) {
+    hipLaunchKernelGGL(ffn_pack_o_kernel, dim3(OP_TILES * 1024 / 256), dim3(256), 0, st, Wo, Wp);
+    PFM_LAUNCH_CHECK();
+    return hipSuccess;
+}
 
 hipError_t pfm_ffn_pack(const bf16* W1, const bf16* W2, bf16* Wp, hipStream_t st) {
     hipLaunchKernelGGL(ffn_pack_kernel, dim3(NTILE * 1024 / 256), dim3(256), 0, st, W1, W2, Wp);
@@ -355,14 +497,39 @@ hipError_t pfm_ffn_fused(const float* x, int M, const float* g2, const float* be
         (void)hipFuncSetAttribute((const void*)ffn_fused_kernel<5>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
     }
     const dim3 grid((M + BM - 1) / BM), blk(NTH);
+    const bf16* z = nullptr;
+    const float* zf = nullptr;
     switch (pfm_knobs().ffn_var) {
-        case 1: hipLaunchKernelGGL(ffn_fused_kernel<1>, grid, blk, LDS_BYTES, st, x, M, g2, be2, eps, Wp, b1, b2, xo, gn, bn, xn); break;
-        case 2: hipLaunchKernelGGL(ffn_fused_kernel<2>, grid, blk, LDS_BYTES, st, x, M, g2, be2, eps, Wp, b1, b2, xo, gn, bn, xn); break;
-        case 3: hipLaunchKernelGGL(ffn_fused_kernel<3>, grid, blk, LDS_BYTES, st, x, M, g2, be2, eps, Wp, b1, b2, xo, gn, bn, xn); break;
-        case 4: hipLaunchKernelGGL(ffn_fused_kernel<4>, grid, blk, LDS_BYTES, st, x, M, g2, be2, eps, Wp, b1, b2, xo, gn, bn, xn); break;
-        case 5: hipLaunchKernelGGL(ffn_fused_kernel<5>, grid, blk, LDS_BYTES, st, x, M, g2, be2, eps, Wp, b1, b2, xo, gn, bn, xn); break;
-        default: hipLaunchKernelGGL(ffn_fused_kernel<0>, grid, blk, LDS_BYTES, st, x, M, g2, be2, eps, Wp, b1, b2, xo, gn, bn, xn);
+        case 1: hipLaunchKernelGGL(ffn_fused_kernel<1>, grid, blk, LDS_BYTES, st, x, M, g2, be2, eps, Wp, b1, b2, xo, gn, bn, xn, z, z, zf); break;
+        case 2: hipLaunchKernelGGL(ffn_fused_kernel<2>, grid, blk, LDS_BYTES, st, x, M, g2, be2, eps, Wp, b1, b2, xo, gn, bn, xn, z, z, zf); break;
+        case 3: hipLaunchKernelGGL(ffn_fused_kernel<3>, grid, blk, LDS_BYTES, st, x, M, g2, be2, eps, Wp, b1, b2, xo, gn, bn, xn, z, z, zf); break;
+        case 4: hipLaunchKernelGGL(ffn_fused_kernel<4>, grid, blk, LDS_BYTES, st, x, M, g2, be2, eps, Wp, b1, b2, xo, gn, bn, xn, z, z, zf); break;
+        case 5: hipLaunchKernelGGL(ffn_fused_kernel<5>, grid, blk, LDS_BYTES, st, x, M, g2, be2, eps, Wp, b1, b2, xo, gn, bn, xn, z, z, zf); break;
+        default: hipLaunchKernelGGL(ffn_fused_kernel<0>, grid, blk, LDS_BYTES, st, x, M, g2, be2, eps, Wp, b1, b2, xo, gn, bn, xn, z, z, zf);
     }
+    PFM_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+// The attention sub-layer's out-projection folded in front of the FFN (see ffn_fused_kernel, OP):
+//   x1 = O Wo^T + bo + f (+ x)   (x optional)
+//   xo = x1 + W2 relu(W1 LN2(x1) + b1) + b2 ;  xn = LN_next(xo) (optional, as pfm_ffn_fused)
+// o, f: bf16 [M, 512]; Wop: pfm_ffn_pack_o output immediately followed by the layer's pfm_ffn_pack tiles.
+hipError_t pfm_ffn_fused_op(const bf16* o, const bf16* f, const float* bo, const float* x, int M, const float* g2,
+                            const float* be2, float eps, const bf16* Wop, const float* b1, const float* b2, float* xo,
+                            const float* gn, const float* bn, bf16* xn, hipStream_t st) {
+    if (M <= 0) return hipSuccess;
+    if ((xn != nullptr) != (gn != nullptr && bn != nullptr) || !o || !f || !bo) return hipErrorInvalidValue;
+    if (((uintptr_t)x | (uintptr_t)xo | (uintptr_t)Wop | (uintptr_t)xn | (uintptr_t)o | (uintptr_t)f | (uintptr_t)bo) % 16)
+        return hipErrorInvalidValue;
+    static bool attr_done = false;
+    if (!attr_done) {
+        attr_done = true;
+        (void)hipFuncSetAttribute((const void*)ffn_fused_kernel<0, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  LDS_BYTES);
+    }
+    hipLaunchKernelGGL((ffn_fused_kernel<0, true>), dim3((M + BM - 1) / BM), dim3(NTH), LDS_BYTES, st, x, M, g2, be2, eps,
+                       Wop, b1, b2, xo, gn, bn, xn, o, f, bo);
     PFM_LAUNCH_CHECK();
     return hipSuccess;
 }

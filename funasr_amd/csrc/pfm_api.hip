@@ -68,6 +68,11 @@ hipError_t pfm_attention_x3(const float* q, RowMap qmap, const float* k, RowMap 
                             bf16* out3, const int* klen, int B, int Tq, int Tk, int heads, int dk, float scale,
                             const float* fsmn_wT, float* fsmn_out, long long fsmn_ld, hipStream_t st);
 hipError_t pfm_ffn_pack(const bf16* W1, const bf16* W2, bf16* Wp, hipStream_t st);
+size_t pfm_ffn_packed_o_elems();
+hipError_t pfm_ffn_pack_o(const bf16* Wo, bf16* Wp, hipStream_t st);
+hipError_t pfm_ffn_fused_op(const bf16* o, const bf16* f, const float* bo, const float* x, int M, const float* g2,
+                            const float* be2, float eps, const bf16* Wop, const float* b1, const float* b2, float* xo,
+                            const float* gn, const float* bn, bf16* xn, hipStream_t st);
 hipError_t pfm_ffn_fused(const float* x, int M, const float* g2, const float* be2, float eps, const bf16* Wp,
                          const float* b1, const float* b2, float* xo, const float* gn, const float* bn, bf16* xn,
                          hipStream_t st);
@@ -110,7 +115,7 @@ static int fail(int code, const std::string& msg) {
             return fail(PFM_E_HIP, std::string(#expr) + ": " + hipGetErrorString(_e));           \
     } while (0)
 
-static thread_local PfmKnobs t_knobs = {0, 0, 1, 8, 0, 1, 0, 2, 1, 0, -1, 0, 0, 1, 0, 1, 1, 1, 0, 1, 0, 0, 1};
+static thread_local PfmKnobs t_knobs = {0, 0, 1, 8, 0, 1, 0, 2, 1, 0, -1, 0, 0, 1, 0, 1, 1, 1, 0, 1, 0, 0, 1, 1};
 
 const PfmKnobs& pfm_knobs() { return t_knobs; }
 
@@ -142,9 +147,10 @@ void pfm_knobs_refresh() {
     k.exact_x6 = iv("PFM_EXACT_X6", 1) != 0;
     k.attn_var = iv("PFM_ATTN_VAR", 0);
     k.dec_subbatch = std::max(1, iv("PFM_DEC_SUBBATCH", 1));
+    k.ffn_op = iv("PFM_FFN_OP", 1) != 0;
     const int* f = &k.ln_fold;
     unsigned long long s = 1469598103934665603ull;   // FNV-1a over the fields
-    for (int i = 0; i < 22; ++i) s = (s ^ (unsigned long long)(unsigned)f[i]) * 1099511628211ull;
+    for (int i = 0; i < 23; ++i) s = (s ^ (unsigned long long)(unsigned)f[i]) * 1099511628211ull;
     k.sig = s;
     t_knobs = k;
 }
@@ -439,11 +445,13 @@ int ensure_bf16(pfm_handle* h, hipStream_t st) {
         h->fold_ready = true;
     }
     if (!h->ffn_ready && ffn_shape_ok(h->cfg) && pfm_knobs().ffn_fused && !h->enc.empty()) {
-        const size_t per = pfm_ffn_packed_elems();
+        // per layer: the out-projection's 32 tiles, then the FFN's 256 (ffp = the FFN tiles)
+        const size_t po = pfm_ffn_packed_o_elems(), per = po + pfm_ffn_packed_elems();
         HIP_TRY(h->ffn_pack.ensure(h->enc.size() * per * sizeof(bf16)));
         for (size_t l = 0; l < h->enc.size(); ++l) {
-            h->enc[l].ffp = l * per;
-            HIP_TRY(pfm_ffn_pack(h->wb(h->enc[l].w1), h->wb(h->enc[l].w2), h->ffn_pack.as<bf16>() + l * per, st));
+            h->enc[l].ffp = l * per + po;
+            HIP_TRY(pfm_ffn_pack_o(h->wb(h->enc[l].wo), h->ffn_pack.as<bf16>() + l * per, st));
+            HIP_TRY(pfm_ffn_pack(h->wb(h->enc[l].w1), h->wb(h->enc[l].w2), h->ffn_pack.as<bf16>() + l * per + po, st));
         }
         h->ffn_ready = true;
     }
@@ -937,7 +945,9 @@ int encoder_stack(const Run& r, const float* x_in, const int* lens, int B, int T
                 HIP_TRY(r.attn(DT_F32, QKV, rowmap_plain(3 * D), QKV + D, rowmap_plain(3 * D), QKV + 2 * D,
                                rowmap_plain(3 * D), O, D, nullptr, lens, B, T, T));
         }
-        {   // x = (x +) linear_out(att) + fsmn   (encoder.py:120-137: no residual when in != out)
+        // fast mode, full batches: the out-projection runs inside the fused FFN kernel (its phase 0)
+        const bool ffn_op = ffn_fused && !r.ck && pfm_knobs().ffn_op;
+        if (!ffn_op) {   // x = (x +) linear_out(att) + fsmn   (encoder.py:120-137: no residual when in != out)
             GemmEpi e = epi_default();
             e.bias = r.P(L.bo);
             e.res0 = fast ? (const float*)Fb : Fm; e.ld_res0 = D; e.res0_bf16 = fast ? 1 : 0;
@@ -962,6 +972,16 @@ int encoder_stack(const Run& r, const float* x_in, const int* lens, int B, int T
             const bool nxt = l + 1 < l1;
             const double fl = 4.0 * M * (double)D * Fd;
             const double by = (double)M * D * (4.0 + 4.0 + (nxt ? 2.0 : 0.0)) + 2.0 * 2.0 * D * Fd;
+            if (ffn_op) {   // x1 = (x +) O Wo^T + bo + fsmn, then the FFN on x1 (encoder.py:120-145)
+                const double flo = fl + 2.0 * M * (double)D * D;
+                const double byo = by + (double)M * D * 2.0 * 2.0 + 2.0 * D * D - (din == D ? 0.0 : 4.0 * M * D);
+                ProfScope ps(h, st, PFM_K_GEMM, flo, byo);
+                HIP_TRY(pfm_ffn_fused_op(Ob, Fb, r.P(L.bo), din == D ? X : nullptr, (int)M, r.P(L.ln2g), r.P(L.ln2b),
+                                         c.ln_eps, h->ffn_pack.as<bf16>() + L.ffp - pfm_ffn_packed_o_elems(), r.P(L.b1),
+                                         r.P(L.b2), X, nxt ? r.P(h->enc[l + 1].ln1g) : nullptr,
+                                         nxt ? r.P(h->enc[l + 1].ln1b) : nullptr, nxt ? (bf16*)Xn : nullptr, st));
+                continue;
+            }
             ProfScope ps(h, st, PFM_K_GEMM, fl, by);
             HIP_TRY(pfm_ffn_fused(X, (int)M, r.P(L.ln2g), r.P(L.ln2b), c.ln_eps, h->ffn_pack.as<bf16>() + L.ffp,
                                   r.P(L.b1), r.P(L.b2), X, nxt ? r.P(h->enc[l + 1].ln1g) : nullptr,

@@ -157,6 +157,7 @@ struct PfmKnobs {
     int exact_x6;           // PFM_EXACT_X6 (default 1): EXACT-mode GEMMs as split bf16 x6 MFMA (f32 MFMA if 0)
     int attn_var;           // PFM_ATTN_VAR: diagnostic variants of the 8-wave bf16 attention kernel (0 = the kernel)
     int dec_subbatch;       // PFM_DEC_SUBBATCH (default 1): decoder utterance groups on concurrent streams
+    int ffn_op;             // PFM_FFN_OP (default 1): encoder out-projection folded into the fused FFN kernel
     unsigned long long sig;
 };
 const PfmKnobs& pfm_knobs();

@@ -237,6 +237,29 @@ def test_fast_folded_layernorm_matches_unfused(engines, monkeypatch):
     assert a1 >= a0 - 0.02 and a1 > 0.6
 
 
+def test_fast_folded_outproj_matches_separate(engines, monkeypatch):
+    """PFM_FFN_OP=1 (default) runs the encoder out-projection as phase 0 of the fused FFN kernel (x1 kept in
+    the accumulators, LN2 reduced across waves); PFM_FFN_OP=0 launches it as a GEMM before the fused FFN.
+    bf16 operands either way: the encoders agree to bf16 rounding, and both stay as close to EXACT mode."""
+    e = engines["large"]
+    g = np.load(f"{GOLD}/para_large_b4.npz")
+    # a batch large enough for the fused FFN path (M >= 4096 rows)
+    x, l = fbank_input(int(g["seed"]), 24, int(g["T"]), [int(g["T"])] * 24)
+    xs, ls = torch.from_numpy(x).cuda(), torch.from_numpy(l).cuda()
+    r1 = e.run(xs, ls, mode="fast", want_enc=True)
+    monkeypatch.setenv("PFM_FFN_OP", "0")
+    r0 = e.run(xs, ls, mode="fast", want_enc=True)
+    monkeypatch.delenv("PFM_FFN_OP")
+    rx = e.run(xs, ls, mode="exact", want_enc=True)
+    torch.cuda.synchronize()
+    a1, a0, ax = r1["enc"].double().cpu(), r0["enc"].double().cpu(), rx["enc"].double().cpu()
+    relerr = float((a1 - a0).norm() / a0.norm())
+    e1, e0 = float((a1 - ax).norm() / ax.norm()), float((a0 - ax).norm() / ax.norm())
+    print(f"folded vs separate out-projection: encoder rel-L2 {relerr:.2e}; vs exact: {e1:.2e}, {e0:.2e}")
+    assert relerr < 1e-2
+    assert e1 <= 1.1 * e0
+
+
 def test_fast_fused_ffn_matches_unfused(engines, monkeypatch):
     """Fast mode runs each encoder layer's LN2 -> FFN -> residual -> next LN1 as one kernel (k_ffn.hip);
     PFM_FFN_FUSED=0 runs LN / GEMM / GEMM / LN launches. Same bf16 operand roundings, different f32
