@@ -36,10 +36,11 @@ constexpr int HC = 256, NCH = FF / HC;          // hidden chunk, chunks
 constexpr int TILE = 16384, TPC = 32, NTILE = NCH * TPC;
 constexpr int OP_TILES = 32;                    // out-projection Wo [512][512]: 16 k steps x 2 halves (W2 format)
 constexpr int OFF_AN = 0, OFF_H = 65536, OFF_RING = 98304, LDS_BYTES = 163840;
+constexpr int OFF_RED = LDS_BYTES - 4096, OFF_STATS = OFF_RED - 512;   // DEC epilogue (above the Y image)
 constexpr int YP = 516;                         // epilogue f32 row pitch (floats)
 
 static_assert(OFF_RING + 4 * TILE == LDS_BYTES, "LDS plan");
-static_assert(BM * YP * 4 <= LDS_BYTES, "epilogue image");
+static_assert(BM * YP * 4 <= OFF_STATS, "epilogue image below the DEC statistics");
 
 // 64-B tile rows: physical 16-B slot = logical slot ^ f2(row). Conflict-free for 16x16x32 fragment
 // reads (16 consecutive rows, slot = lane >> 4): every ds_read_b128 lane group covers 16 distinct
@@ -69,7 +70,14 @@ struct Frag { bf16x8 w[2]; bf16x8 a[4]; };
 //   LN2(x1) -> bf16 A image (row statistics reduced across the 8 waves through LDS), accumulators += b2,
 //   then the FFN loop above accumulates W2 . H on top: the epilogue stores x2 = accumulators directly.
 // x1 never leaves the CU (one kernel and one HBM round trip of the residual stream less per layer).
-template <int VAR, bool OP = false>
+//
+// DEC (Paraformer decoder feed-forward, sanm/positionwise_feed_forward.py:12-33): y = W2 . LN_F(relu(W1 x' + b1)),
+// x' = LN1(x) (the prologue), w2 without bias. LN_F over the 2048-wide hidden is folded through W2:
+//   y = rstd . (W2g . h - mu . c1) + c2,   W2g = W2 diag(gamma_F) (packed bf16), c1 = rowsum(W2g), c2 = W2 beta_F,
+// with mu / rstd of the bf16 hidden h accumulated chunk by chunk (sum, sum of squares) and reduced across the
+// 8 waves in the epilogue. Outputs: xn = LN_next(y) (bf16; the decoder's LN2 or after_norm), xo = y (optional).
+// In DEC mode the arguments bo / b2 carry c1 / c2.
+template <int VAR, int MODE = 0>
 __global__ __launch_bounds__(NTH) void ffn_fused_kernel(const float* __restrict__ X, int M, const float* __restrict__ g2,
                                                         const float* __restrict__ be2, float eps,
                                                         const bf16* __restrict__ Wp, const float* __restrict__ b1,
@@ -82,7 +90,9 @@ __global__ __launch_bounds__(NTH) void ffn_fused_kernel(const float* __restrict_
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int g = lane >> 4, r16 = lane & 15;
     const long long m0 = (long long)blockIdx.x * BM;
+    constexpr bool OP = MODE == 1, DEC = MODE == 2;
     constexpr int T0 = OP ? OP_TILES : 0;      // FFN tiles start after the Wo tiles
+    float rs[4] = {0.f, 0.f, 0.f, 0.f}, rq[4] = {0.f, 0.f, 0.f, 0.f};   // DEC: hidden row sums / sums of squares
     constexpr int NT_ALL = NTILE + T0;
 
     auto issue = [&](int t) {
@@ -200,6 +210,14 @@ __global__ __launch_bounds__(NTH) void ffn_fused_kernel(const float* __restrict_
                 bf16x4 o;
 #pragma unroll
                 for (int i = 0; i < 4; ++i) o[i] = f2bf(fmaxf(acc1[hb][mb][i] + bi[i], 0.f));
+                if constexpr (DEC) {
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const float f = bf2f(o[i]);
+                        rs[mb] += f;
+                        rq[mb] += f * f;
+                    }
+                }
                 *(bf16x4*)(smem + OFF_H + m * 512 + (((hl >> 3) ^ r16) << 4) + ((hl & 7) << 1)) = o;
 #pragma unroll
                 for (int i = 0; i < 4; ++i) acc1[hb][mb][i] = 0.f;
@@ -368,7 +386,7 @@ __global__ __launch_bounds__(NTH) void ffn_fused_kernel(const float* __restrict_
     float4 xa[8], xb[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-        if constexpr (OP) {
+        if constexpr (OP || DEC) {
             xa[i] = make_float4(0.f, 0.f, 0.f, 0.f);
             xb[i] = xa[i];
         } else {
@@ -379,6 +397,30 @@ __global__ __launch_bounds__(NTH) void ffn_fused_kernel(const float* __restrict_
         }
     }
     __syncthreads();   // every wave is past its last ring / A / H read (no DMA in flight here)
+    float2* stats = (float2*)(smem + OFF_STATS);   // DEC: per row (mu, rstd) of the hidden
+    if constexpr (DEC) {
+        float* red = (float*)(smem + OFF_RED);
+#pragma unroll
+        for (int mb = 0; mb < 4; ++mb) {
+            rs[mb] += __shfl_xor(rs[mb], 16, 64);
+            rs[mb] += __shfl_xor(rs[mb], 32, 64);
+            rq[mb] += __shfl_xor(rq[mb], 16, 64);
+            rq[mb] += __shfl_xor(rq[mb], 32, 64);
+            if (g == 0) {
+                red[w * 64 + 16 * mb + r16] = rs[mb];
+                red[512 + w * 64 + 16 * mb + r16] = rq[mb];
+            }
+        }
+        __syncthreads();
+        if (tid < BM) {
+            float sm = 0.f, sq = 0.f;
+#pragma unroll
+            for (int ww = 0; ww < 8; ++ww) { sm += red[ww * 64 + tid]; sq += red[512 + ww * 64 + tid]; }
+            const float mu = sm * (1.f / FF);
+            const float var = fmaxf(sq * (1.f / FF) - mu * mu, 0.f);
+            stats[tid] = make_float2(mu, 1.f / sqrtf(var + eps));
+        }
+    }
     float* Y = (float*)smem;
 #pragma unroll
     for (int nb = 0; nb < 2; ++nb)
@@ -395,6 +437,11 @@ __global__ __launch_bounds__(NTH) void ffn_fused_kernel(const float* __restrict_
         c2a = make_float4(0.f, 0.f, 0.f, 0.f);
         c2b = c2a;
     }
+    float4 c1a = make_float4(0.f, 0.f, 0.f, 0.f), c1b = c1a;
+    if constexpr (DEC) {
+        c1a = *(const float4*)(bo + 8 * lane);
+        c1b = *(const float4*)(bo + 8 * lane + 4);
+    }
     float4 na = {0, 0, 0, 0}, nbv = {0, 0, 0, 0}, qa = {0, 0, 0, 0}, qb = {0, 0, 0, 0};
     if (Xn) {
         na = *(const float4*)(gn + 8 * lane); nbv = *(const float4*)(gn + 8 * lane + 4);
@@ -408,7 +455,15 @@ __global__ __launch_bounds__(NTH) void ffn_fused_kernel(const float* __restrict_
         float v[8] = {ya[0] + c2a.x + xa[i].x, ya[1] + c2a.y + xa[i].y, ya[2] + c2a.z + xa[i].z,
                       ya[3] + c2a.w + xa[i].w, yb[0] + c2b.x + xb[i].x, yb[1] + c2b.y + xb[i].y,
                       yb[2] + c2b.z + xb[i].z, yb[3] + c2b.w + xb[i].w};
-        if (row < M) {
+        if constexpr (DEC) {
+            const float2 st = stats[m];
+            const float c1v[8] = {c1a.x, c1a.y, c1a.z, c1a.w, c1b.x, c1b.y, c1b.z, c1b.w};
+            const float c2v[8] = {c2a.x, c2a.y, c2a.z, c2a.w, c2b.x, c2b.y, c2b.z, c2b.w};
+            const float yv[8] = {ya[0], ya[1], ya[2], ya[3], yb[0], yb[1], yb[2], yb[3]};
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = st.y * (yv[e] - st.x * c1v[e]) + c2v[e];
+        }
+        if (row < M && Xo) {
             float* orow = Xo + row * FD + 8 * lane;
             *(float4*)orow = make_float4(v[0], v[1], v[2], v[3]);
             *(float4*)(orow + 4) = make_float4(v[4], v[5], v[6], v[7]);
@@ -461,9 +516,78 @@ __global__ __launch_bounds__(256) void ffn_pack_o_kernel(const bf16* __restrict_
     *(bf16x8*)(Wp + (long long)gid * 8) = *(const bf16x8*)src;
 }
 
+// DEC packing: W1 tiles as ffn_pack_kernel; W2 tiles from f32 W2 scaled by gamma_F along k (W2g = bf16(W2 g)).
+__global__ __launch_bounds__(256) void ffn_pack_dec_kernel(const bf16* __restrict__ W1, const float* __restrict__ W2,
+                                                           const float* __restrict__ gF, bf16* __restrict__ Wp) {
+    const int gid = blockIdx.x * 256 + threadIdx.x;   // < NTILE * 1024
+    const int t = gid >> 10, u = gid & 1023;
+    const int c = t >> 5, j = t & 15, row = u >> 2, ls = (u & 3) ^ f2(row);
+    bf16x8 o;
+    if (t & 16) {
+        const int s = j >> 1, eta = j & 1, k0 = HC * c + 32 * s + 8 * ls;
+        const float* src = W2 + (long long)(256 * eta + row) * FF + k0;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = f2bf(src[e] * gF[k0 + e]);
+    } else {
+        o = *(const bf16x8*)(W1 + (long long)(HC * c + row) * FD + 32 * j + 8 * ls);
+    }
+    *(bf16x8*)(Wp + (long long)gid * 8) = o;
+}
+
+// c1[o] = sum_k bf16(W2[o][k] g[k]) (the packed values), c2[o] = sum_k W2[o][k] b[k]; one block per output row
+__global__ __launch_bounds__(256) void ffn_dec_consts_kernel(const float* __restrict__ W2, const float* __restrict__ gF,
+                                                             const float* __restrict__ bF, float* __restrict__ c1,
+                                                             float* __restrict__ c2) {
+    __shared__ float r1[256], r2[256];
+    const int o = blockIdx.x, t = threadIdx.x;
+    float s1 = 0.f, s2 = 0.f;
+    for (int k = t; k < FF; k += 256) {
+        const float wv = W2[(long long)o * FF + k];
+        s1 += bf2f(f2bf(wv * gF[k]));
+        s2 += wv * bF[k];
+    }
+    r1[t] = s1; r2[t] = s2;
+    __syncthreads();
+    for (int n = 128; n > 0; n >>= 1) {
+        if (t < n) { r1[t] += r1[t + n]; r2[t] += r2[t + n]; }
+        __syncthreads();
+    }
+    if (t == 0) { c1[o] = r1[0]; c2[o] = r2[0]; }
+}
+
 }  // namespace
 
 size_t pfm_ffn_packed_elems() { return (size_t)NTILE * TILE / 2; }
+
+hipError_t pfm_ffn_pack_dec(const bf16* W1, const float* W2, const float* gF, const float* bF, bf16* Wp, float* c1,
+                            float* c2, hipStream_t st) {
+    hipLaunchKernelGGL(ffn_pack_dec_kernel, dim3(NTILE * 1024 / 256), dim3(256), 0, st, W1, W2, gF, Wp);
+    PFM_LAUNCH_CHECK();
+    hipLaunchKernelGGL(ffn_dec_consts_kernel, dim3(FD), dim3(256), 0, st, W2, gF, bF, c1, c2);
+    PFM_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+// Fused decoder feed-forward (ffn_fused_kernel DEC): x f32 [M, 512] -> xn = LN_next(W2 LN_F(relu(W1 LN1(x) + b1)))
+// bf16 [M, 512] (+ the f32 FFN output in xo when non-null). Wp / c1 / c2 from pfm_ffn_pack_dec.
+hipError_t pfm_ffn_fused_dec(const float* x, int M, const float* g1, const float* be1, float eps, const bf16* Wp,
+                             const float* b1, const float* c1, const float* c2, float* xo, const float* gn,
+                             const float* bn, bf16* xn, hipStream_t st) {
+    if (M <= 0) return hipSuccess;
+    if (!xn || !gn || !bn || !c1 || !c2) return hipErrorInvalidValue;
+    if (((uintptr_t)x | (uintptr_t)xo | (uintptr_t)Wp | (uintptr_t)xn | (uintptr_t)c1 | (uintptr_t)c2) % 16)
+        return hipErrorInvalidValue;
+    static bool attr_done = false;
+    if (!attr_done) {
+        attr_done = true;
+        (void)hipFuncSetAttribute((const void*)ffn_fused_kernel<0, 2>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  LDS_BYTES);
+    }
+    hipLaunchKernelGGL((ffn_fused_kernel<0, 2>), dim3((M + BM - 1) / BM), dim3(NTH), LDS_BYTES, st, x, M, g1, be1, eps,
+                       Wp, b1, c2, xo, gn, bn, xn, (const bf16*)nullptr, (const bf16*)nullptr, c1);
+    PFM_LAUNCH_CHECK();
+    return hipSuccess;
+}
 size_t pfm_ffn_packed_o_elems() { return (size_t)OP_TILES * TILE / 2; }
 
 hipError_t pfm_ffn_pack_o(const bf16* Wo, bf16* Wp, hipStream_t st) {
@@ -525,10 +649,10 @@ hipError_t pfm_ffn_fused_op(const bf16* o, const bf16* f, const float* bo, const
     static bool attr_done = false;
     if (!attr_done) {
         attr_done = true;
-        (void)hipFuncSetAttribute((const void*)ffn_fused_kernel<0, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+        (void)hipFuncSetAttribute((const void*)ffn_fused_kernel<0, 1>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   LDS_BYTES);
     }
-    hipLaunchKernelGGL((ffn_fused_kernel<0, true>), dim3((M + BM - 1) / BM), dim3(NTH), LDS_BYTES, st, x, M, g2, be2, eps,
+    hipLaunchKernelGGL((ffn_fused_kernel<0, 1>), dim3((M + BM - 1) / BM), dim3(NTH), LDS_BYTES, st, x, M, g2, be2, eps,
                        Wop, b1, b2, xo, gn, bn, xn, o, f, bo);
     PFM_LAUNCH_CHECK();
     return hipSuccess;

@@ -69,6 +69,11 @@ hipError_t pfm_attention_x3(const float* q, RowMap qmap, const float* k, RowMap 
                             const float* fsmn_wT, float* fsmn_out, long long fsmn_ld, hipStream_t st);
 hipError_t pfm_ffn_pack(const bf16* W1, const bf16* W2, bf16* Wp, hipStream_t st);
 size_t pfm_ffn_packed_o_elems();
+hipError_t pfm_ffn_pack_dec(const bf16* W1, const float* W2, const float* gF, const float* bF, bf16* Wp, float* c1,
+                            float* c2, hipStream_t st);
+hipError_t pfm_ffn_fused_dec(const float* x, int M, const float* g1, const float* be1, float eps, const bf16* Wp,
+                             const float* b1, const float* c1, const float* c2, float* xo, const float* gn,
+                             const float* bn, bf16* xn, hipStream_t st);
 hipError_t pfm_ffn_pack_o(const bf16* Wo, bf16* Wp, hipStream_t st);
 hipError_t pfm_ffn_fused_op(const bf16* o, const bf16* f, const float* bo, const float* x, int M, const float* g2,
                             const float* be2, float eps, const bf16* Wop, const float* b1, const float* b2, float* xo,
@@ -115,7 +120,7 @@ static int fail(int code, const std::string& msg) {
             return fail(PFM_E_HIP, std::string(#expr) + ": " + hipGetErrorString(_e));           \
     } while (0)
 
-static thread_local PfmKnobs t_knobs = {0, 0, 1, 8, 0, 1, 0, 2, 1, 0, -1, 0, 0, 1, 0, 1, 1, 1, 0, 1, 0, 0, 1, 1};
+static thread_local PfmKnobs t_knobs = {0, 0, 1, 8, 0, 1, 0, 2, 1, 0, -1, 0, 0, 1, 0, 1, 1, 1, 0, 1, 0, 0, 1, 1, 1};
 
 const PfmKnobs& pfm_knobs() { return t_knobs; }
 
@@ -148,9 +153,10 @@ void pfm_knobs_refresh() {
     k.attn_var = iv("PFM_ATTN_VAR", 0);
     k.dec_subbatch = std::max(1, iv("PFM_DEC_SUBBATCH", 1));
     k.ffn_op = iv("PFM_FFN_OP", 1) != 0;
+    k.dec_ffn_fused = iv("PFM_DEC_FFN_FUSED", 1) != 0;
     const int* f = &k.ln_fold;
     unsigned long long s = 1469598103934665603ull;   // FNV-1a over the fields
-    for (int i = 0; i < 23; ++i) s = (s ^ (unsigned long long)(unsigned)f[i]) * 1099511628211ull;
+    for (int i = 0; i < 24; ++i) s = (s ^ (unsigned long long)(unsigned)f[i]) * 1099511628211ull;
     k.sig = s;
     t_knobs = k;
 }
@@ -218,6 +224,8 @@ struct pfm_handle {
     bool fold_ready = false;
     DevBuf ffn_pack;               // fused-FFN weight tiles of every encoder layer (bf16, LDS-image order)
     bool ffn_ready = false;
+    DevBuf dffn_pack, dffn_c;      // decoder FFNs (16 blocks + decoders3): W1 | W2 diag(gamma_F) tiles; c1 | c2
+    bool dffn_ready = false;
     DevBuf arena_x6;               // EXACT mode: three bf16 planes of every GEMM weight (x = x0 + x1 + x2)
     bool x6_ready = false;
     std::map<hipStream_t, std::unique_ptr<DevBuf>> x6_scratch;   // split A operands, one buffer per stream
@@ -454,6 +462,22 @@ int ensure_bf16(pfm_handle* h, hipStream_t st) {
             HIP_TRY(pfm_ffn_pack(h->wb(h->enc[l].w1), h->wb(h->enc[l].w2), h->ffn_pack.as<bf16>() + l * per + po, st));
         }
         h->ffn_ready = true;
+    }
+    const int ndf = h->cfg.dec_blocks > 0 ? h->cfg.dec_blocks + 1 : 0;
+    if (!h->dffn_ready && ffn_shape_ok(h->cfg) && pfm_knobs().dec_ffn_fused && ndf > 0 && !h->dec.empty()) {
+        const size_t per = pfm_ffn_packed_elems();
+        const int D = h->cfg.d_model;
+        HIP_TRY(h->dffn_pack.ensure((size_t)ndf * per * sizeof(bf16)));
+        HIP_TRY(h->dffn_c.ensure((size_t)ndf * 2 * D * sizeof(float)));
+        for (int j = 0; j < ndf; ++j) {
+            const bool d3 = j == ndf - 1;
+            const size_t w1 = d3 ? h->d3w1 : h->dec[j].w1, w2 = d3 ? h->d3w2 : h->dec[j].w2;
+            const size_t gF = d3 ? h->d3ng : h->dec[j].ng, bF = d3 ? h->d3nb : h->dec[j].nb;
+            float* cc = h->dffn_c.as<float>() + (size_t)j * 2 * D;
+            HIP_TRY(pfm_ffn_pack_dec(h->wb(w1), h->w(w2), h->w(gF), h->w(bF), h->dffn_pack.as<bf16>() + (size_t)j * per,
+                                     cc, cc + D, st));
+        }
+        h->dffn_ready = true;
     }
     return PFM_OK;
 }
@@ -1187,6 +1211,7 @@ int pfm_set_weight(pfm_handle* h, const char* name, const void* host_ptr, int dt
     h->bf_ready = false;
     h->fold_ready = false;
     h->ffn_ready = false;
+    h->dffn_ready = false;
     h->x6_ready = false;
     h->x6_pad.clear();
     h->ban_tok = -1;   // the banned-token bias copy follows ctc.ctc_lo.bias
@@ -1360,9 +1385,21 @@ int pfm_run(pfm_handle* h, void* stream, int mode, const float* feats, const int
         const int* ntg = ntok + b0;
         const int* lg = lens + b0;
         const char* KVg = (const char*)KV + (size_t)b0 * T * nkv * esz;
-        auto ffn = [&](bool xdn_ready, size_t lng, size_t lnb, size_t w1, size_t b1, size_t fng, size_t fnb, size_t w2,
-                       float* out, size_t pg, size_t pb, void* pout, int pdt) -> int {
+        // fast mode: each decoder FFN (+ its LN1 before, + the LN after) as one fused kernel (k_ffn.hip DEC)
+        const bool dffn = fast && !fuse_ln && h->dffn_ready && pfm_knobs().dec_ffn_fused && Mg >= 2048;
+        auto ffn = [&](int fi, bool xdn_ready, size_t lng, size_t lnb, size_t w1, size_t b1, size_t fng, size_t fnb,
+                       size_t w2, float* out, size_t pg, size_t pb, void* pout, int pdt) -> int {
             // out = W2 . LN_F(relu(W1 . LN(x) + b1)); pout = LN_P(out)   (sanm/positionwise_feed_forward.py:26-33)
+            if (dffn && pdt == DT_BF16) {   // out itself is dead in the decoder: only LN_P(out) is consumed
+                const double flo = 4.0 * Mg * (double)D * Fd;
+                const double byo = (double)Mg * D * (4.0 + 2.0) + 2.0 * 2.0 * D * Fd;
+                ProfScope ps(h, s, PFM_K_GEMM, flo, byo);
+                const float* cc = h->dffn_c.as<float>() + (size_t)fi * 2 * D;
+                HIP_TRY(pfm_ffn_fused_dec(Xd, Mg, P(lng), P(lnb), c.ln_eps,
+                                          h->dffn_pack.as<bf16>() + (size_t)fi * pfm_ffn_packed_elems(), P(b1), cc,
+                                          cc + D, nullptr, P(pg), P(pb), (bf16*)pout, s));
+                return PFM_OK;
+            }
             if (!xdn_ready)
                 HIP_TRY(pfm_layernorm(Xd, rowmap_plain(D), Mg, D, P(lng), P(lnb), c.ln_eps, nullptr, 0, 1.f, Xdn, xdm,
                                       ndt, nullptr, plain, 0, s));
@@ -1393,7 +1430,7 @@ int pfm_run(pfm_handle* h, void* stream, int mode, const float* feats, const int
             const DecLayer& Lr = h->dec[l];
             // t = FFN(LN1(x)); x = x + FSMN(LN2(t))   (decoder.py:97-107)
             // fast mode: LN2(t) in bf16 feeding the bf16-input FSMN (x += FSMN(LN2(t)) stays f32)
-            int rc2 = ffn(xdn_ready, Lr.n1g, Lr.n1b, Lr.w1, Lr.b1, Lr.ng, Lr.nb, Lr.w2, Td, Lr.n2g, Lr.n2b, Tdn,
+            int rc2 = ffn(l, xdn_ready, Lr.n1g, Lr.n1b, Lr.w1, Lr.b1, Lr.ng, Lr.nb, Lr.w2, Td, Lr.n2g, Lr.n2b, Tdn,
                           fast ? DT_BF16 : DT_F32);
             if (rc2) return rc2;
             if (fast)
@@ -1438,7 +1475,7 @@ int pfm_run(pfm_handle* h, void* stream, int mode, const float* feats, const int
             }
         }
         // decoders3: x = FFN(LN1(x)), no residual (decoder.py:97-100 with self_attn = src_attn = None)
-        int rc3 = ffn(xdn_ready, h->d3n1g, h->d3n1b, h->d3w1, h->d3b1, h->d3ng, h->d3nb, h->d3w2, Xd, h->dan_g,
+        int rc3 = ffn(c.dec_blocks, xdn_ready, h->d3n1g, h->d3n1b, h->d3w1, h->d3b1, h->d3ng, h->d3nb, h->d3w2, Xd, h->dan_g,
                       h->dan_b, Xdn, ndt);
         if (rc3) return rc3;
         {   // output layer with fused row-argmax (logits never written)

@@ -158,6 +158,7 @@ struct PfmKnobs {
     int attn_var;           // PFM_ATTN_VAR: diagnostic variants of the 8-wave bf16 attention kernel (0 = the kernel)
     int dec_subbatch;       // PFM_DEC_SUBBATCH (default 1): decoder utterance groups on concurrent streams
     int ffn_op;             // PFM_FFN_OP (default 1): encoder out-projection folded into the fused FFN kernel
+    int dec_ffn_fused;      // PFM_DEC_FFN_FUSED (default 1): decoder LN1-FFN(LN_F folded)-LN kernel (fast mode)
     unsigned long long sig;
 };
 const PfmKnobs& pfm_knobs();

@@ -260,6 +260,32 @@ def test_fast_folded_outproj_matches_separate(engines, monkeypatch):
     assert e1 <= 1.1 * e0
 
 
+def test_fast_fused_decoder_ffn_matches_unfused(engines, monkeypatch):
+    """Fast mode runs each decoder FFN (LN1 -> W1 -> relu -> LN_F -> W2 -> LN2) as one kernel with LN_F folded
+    through W2 (k_ffn.hip DEC); PFM_DEC_FFN_FUSED=0 launches LN / GEMM / LN / GEMM / LN. Tokens of a batch large
+    enough for the fused path agree between the two, and the fused path agrees with EXACT mode at least as
+    well as the unfused one (within one percent of the tokens)."""
+    e = engines["large"]
+    g = np.load(f"{GOLD}/para_large_b4.npz")
+    x, l = fbank_input(int(g["seed"]), 24, int(g["T"]), [int(g["T"])] * 24)   # B x L ~ 5,500 decoder rows
+    xs, ls = torch.from_numpy(x).cuda(), torch.from_numpy(l).cuda()
+    r1 = e.run(xs, ls, mode="fast")
+    monkeypatch.setenv("PFM_DEC_FFN_FUSED", "0")
+    r0 = e.run(xs, ls, mode="fast")
+    monkeypatch.delenv("PFM_DEC_FFN_FUSED")
+    rx = e.run(xs, ls, mode="exact")
+    torch.cuda.synchronize()
+    assert torch.equal(r1["ntok"], r0["ntok"])
+    def agree(a, b):
+        ta, tb = _tokens_from_run(a, e.cfg), _tokens_from_run(b, e.cfg)
+        same = sum(int(x == y) for p, q in zip(ta, tb) for x, y in zip(p, q))
+        return same / max(1, sum(max(len(p), len(q)) for p, q in zip(ta, tb)))
+    a10, a1x, a0x = agree(r1, r0), agree(r1, rx), agree(r0, rx)
+    print(f"fused vs unfused decoder FFN: token agreement {a10:.4f}; vs exact: fused {a1x:.4f}, unfused {a0x:.4f}")
+    assert a10 > 0.95
+    assert a1x >= a0x - 0.01
+
+
 def test_fast_fused_ffn_matches_unfused(engines, monkeypatch):
     """Fast mode runs each encoder layer's LN2 -> FFN -> residual -> next LN1 as one kernel (k_ffn.hip);
     PFM_FFN_FUSED=0 runs LN / GEMM / GEMM / LN launches. Same bf16 operand roundings, different f32
