@@ -84,13 +84,14 @@ __global__ __launch_bounds__(NTH) void ffn_fused_kernel(const float* __restrict_
                                                         const float* __restrict__ b2, float* Xo,
                                                         const float* __restrict__ gn, const float* __restrict__ bn,
                                                         bf16* __restrict__ Xn, const bf16* __restrict__ O,
-                                                        const bf16* __restrict__ Fr, const float* __restrict__ bo) {
+                                                        const bf16* __restrict__ Fr, const float* __restrict__ bo,
+                                                        const float* __restrict__ c1) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int g = lane >> 4, r16 = lane & 15;
     const long long m0 = (long long)blockIdx.x * BM;
-    constexpr bool OP = MODE == 1, DEC = MODE == 2;
+    constexpr bool OP = MODE == 1 || MODE == 3, DEC = MODE == 2 || MODE == 3;
     constexpr int T0 = OP ? OP_TILES : 0;      // FFN tiles start after the Wo tiles
     float rs[4] = {0.f, 0.f, 0.f, 0.f}, rq[4] = {0.f, 0.f, 0.f, 0.f};   // DEC: hidden row sums / sums of squares
     constexpr int NT_ALL = NTILE + T0;
@@ -297,13 +298,17 @@ __global__ __launch_bounds__(NTH) void ffn_fused_kernel(const float* __restrict_
                     const int n = 256 * hf + 32 * w + 16 * nb + 4 * g;
                     f32x4& a = hf ? acc2b[nb][mb] : acc2a[nb][mb];
                     const float4 bb4 = *(const float4*)(bo + n);
-                    const bf16x4 f4 = *(const bf16x4*)(Fr + row * FD + n);
                     float4 x4 = make_float4(0.f, 0.f, 0.f, 0.f);
                     if (X) x4 = *(const float4*)(X + row * FD + n);
-                    a[0] = ((a[0] + bb4.x) + bf2f(f4[0])) + x4.x;
-                    a[1] = ((a[1] + bb4.y) + bf2f(f4[1])) + x4.y;
-                    a[2] = ((a[2] + bb4.z) + bf2f(f4[2])) + x4.z;
-                    a[3] = ((a[3] + bb4.w) + bf2f(f4[3])) + x4.w;
+                    a[0] += bb4.x; a[1] += bb4.y; a[2] += bb4.z; a[3] += bb4.w;
+                    if (Fr) {
+                        const bf16x4 f4 = *(const bf16x4*)(Fr + row * FD + n);
+                        a[0] += bf2f(f4[0]); a[1] += bf2f(f4[1]); a[2] += bf2f(f4[2]); a[3] += bf2f(f4[3]);
+                    }
+                    a[0] += x4.x; a[1] += x4.y; a[2] += x4.z; a[3] += x4.w;
+                    if constexpr (MODE == 3) {   // the decoder keeps x1 (the FSMN step adds it back)
+                        if (m0 + 16 * mb + r16 < M) *(float4*)(Xo + row * FD + n) = make_float4(a[0], a[1], a[2], a[3]);
+                    }
                     part[mb] += (a[0] + a[1]) + (a[2] + a[3]);
                 }
         }
@@ -349,11 +354,15 @@ __global__ __launch_bounds__(NTH) void ffn_fused_kernel(const float* __restrict_
                     const int n = 256 * hf + 32 * w + 16 * nb + 4 * g;
                     f32x4& a = hf ? acc2b[nb][mb] : acc2a[nb][mb];
                     const float4 gg = *(const float4*)(g2 + n), be = *(const float4*)(be2 + n);
-                    const float4 c2 = *(const float4*)(b2 + n);
                     bf16x4 o = {f2bf((a[0] - mean[mb]) * rstd * gg.x + be.x), f2bf((a[1] - mean[mb]) * rstd * gg.y + be.y),
                                 f2bf((a[2] - mean[mb]) * rstd * gg.z + be.z), f2bf((a[3] - mean[mb]) * rstd * gg.w + be.w)};
                     *(bf16x4*)(smem + OFF_AN + m * 1024 + (((n >> 3) ^ (m & 15)) << 4) + ((n & 7) << 1)) = o;
-                    a[0] += c2.x; a[1] += c2.y; a[2] += c2.z; a[3] += c2.w;   // x2 = (x1 + b2) + W2 . H
+                    if constexpr (MODE == 1) {   // encoder: x2 = (x1 + b2) + W2 . H
+                        const float4 c2 = *(const float4*)(b2 + n);
+                        a[0] += c2.x; a[1] += c2.y; a[2] += c2.z; a[3] += c2.w;
+                    } else {                      // decoder: the FFN output has no residual
+                        a[0] = 0.f; a[1] = 0.f; a[2] = 0.f; a[3] = 0.f;
+                    }
                 }
         }
         bar();   // the LN2 image is complete before chunk 0's first fragment reads
@@ -433,14 +442,14 @@ __global__ __launch_bounds__(NTH) void ffn_fused_kernel(const float* __restrict_
         }
     bar();
     float4 c2a = *(const float4*)(b2 + 8 * lane), c2b = *(const float4*)(b2 + 8 * lane + 4);
-    if constexpr (OP) {
+    if constexpr (MODE == 1) {
         c2a = make_float4(0.f, 0.f, 0.f, 0.f);
         c2b = c2a;
     }
     float4 c1a = make_float4(0.f, 0.f, 0.f, 0.f), c1b = c1a;
     if constexpr (DEC) {
-        c1a = *(const float4*)(bo + 8 * lane);
-        c1b = *(const float4*)(bo + 8 * lane + 4);
+        c1a = *(const float4*)(c1 + 8 * lane);
+        c1b = *(const float4*)(c1 + 8 * lane + 4);
     }
     float4 na = {0, 0, 0, 0}, nbv = {0, 0, 0, 0}, qa = {0, 0, 0, 0}, qb = {0, 0, 0, 0};
     if (Xn) {
@@ -463,7 +472,7 @@ __global__ __launch_bounds__(NTH) void ffn_fused_kernel(const float* __restrict_
 #pragma unroll
             for (int e = 0; e < 8; ++e) v[e] = st.y * (yv[e] - st.x * c1v[e]) + c2v[e];
         }
-        if (row < M && Xo) {
+        if (row < M && Xo && MODE != 3) {
             float* orow = Xo + row * FD + 8 * lane;
             *(float4*)orow = make_float4(v[0], v[1], v[2], v[3]);
             *(float4*)(orow + 4) = make_float4(v[4], v[5], v[6], v[7]);
@@ -570,21 +579,32 @@ hipError_t pfm_ffn_pack_dec(const bf16* W1, const float* W2, const float* gF, co
 
 // Fused decoder feed-forward (ffn_fused_kernel DEC): x f32 [M, 512] -> xn = LN_next(W2 LN_F(relu(W1 LN1(x) + b1)))
 // bf16 [M, 512] (+ the f32 FFN output in xo when non-null). Wp / c1 / c2 from pfm_ffn_pack_dec.
+// With o (bf16 [M, 512], the previous block's cross-attention output) and bo: that block's out-projection runs
+// first (mode 3): x1 = x + o Wo^T + bo is written to xo (f32, may alias x) and the FFN runs on x1; Wp then
+// points at the 32 Wo tiles that precede the FFN tiles.
 hipError_t pfm_ffn_fused_dec(const float* x, int M, const float* g1, const float* be1, float eps, const bf16* Wp,
                              const float* b1, const float* c1, const float* c2, float* xo, const float* gn,
-                             const float* bn, bf16* xn, hipStream_t st) {
+                             const float* bn, bf16* xn, const bf16* o, const float* bo, hipStream_t st) {
     if (M <= 0) return hipSuccess;
-    if (!xn || !gn || !bn || !c1 || !c2) return hipErrorInvalidValue;
-    if (((uintptr_t)x | (uintptr_t)xo | (uintptr_t)Wp | (uintptr_t)xn | (uintptr_t)c1 | (uintptr_t)c2) % 16)
+    if (!xn || !gn || !bn || !c1 || !c2 || (o && (!bo || !xo || !x))) return hipErrorInvalidValue;
+    if (((uintptr_t)x | (uintptr_t)xo | (uintptr_t)Wp | (uintptr_t)xn | (uintptr_t)c1 | (uintptr_t)c2 | (uintptr_t)o |
+         (uintptr_t)bo) % 16)
         return hipErrorInvalidValue;
     static bool attr_done = false;
     if (!attr_done) {
         attr_done = true;
         (void)hipFuncSetAttribute((const void*)ffn_fused_kernel<0, 2>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   LDS_BYTES);
+        (void)hipFuncSetAttribute((const void*)ffn_fused_kernel<0, 3>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  LDS_BYTES);
     }
-    hipLaunchKernelGGL((ffn_fused_kernel<0, 2>), dim3((M + BM - 1) / BM), dim3(NTH), LDS_BYTES, st, x, M, g1, be1, eps,
-                       Wp, b1, c2, xo, gn, bn, xn, (const bf16*)nullptr, (const bf16*)nullptr, c1);
+    if (o)
+        hipLaunchKernelGGL((ffn_fused_kernel<0, 3>), dim3((M + BM - 1) / BM), dim3(NTH), LDS_BYTES, st, x, M, g1, be1,
+                           eps, Wp, b1, c2, xo, gn, bn, xn, o, (const bf16*)nullptr, bo, c1);
+    else
+        hipLaunchKernelGGL((ffn_fused_kernel<0, 2>), dim3((M + BM - 1) / BM), dim3(NTH), LDS_BYTES, st, x, M, g1, be1,
+                           eps, Wp, b1, c2, xo, gn, bn, xn, (const bf16*)nullptr, (const bf16*)nullptr,
+                           (const float*)nullptr, c1);
     PFM_LAUNCH_CHECK();
     return hipSuccess;
 }
@@ -624,12 +644,12 @@ hipError_t pfm_ffn_fused(const float* x, int M, const float* g2, const float* be
     const bf16* z = nullptr;
     const float* zf = nullptr;
     switch (pfm_knobs().ffn_var) {
-        case 1: hipLaunchKernelGGL(ffn_fused_kernel<1>, grid, blk, LDS_BYTES, st, x, M, g2, be2, eps, Wp, b1, b2, xo, gn, bn, xn, z, z, zf); break;
-        case 2: hipLaunchKernelGGL(ffn_fused_kernel<2>, grid, blk, LDS_BYTES, st, x, M, g2, be2, eps, Wp, b1, b2, xo, gn, bn, xn, z, z, zf); break;
-        case 3: hipLaunchKernelGGL(ffn_fused_kernel<3>, grid, blk, LDS_BYTES, st, x, M, g2, be2, eps, Wp, b1, b2, xo, gn, bn, xn, z, z, zf); break;
-        case 4: hipLaunchKernelGGL(ffn_fused_kernel<4>, grid, blk, LDS_BYTES, st, x, M, g2, be2, eps, Wp, b1, b2, xo, gn, bn, xn, z, z, zf); break;
-        case 5: hipLaunchKernelGGL(ffn_fused_kernel<5>, grid, blk, LDS_BYTES, st, x, M, g2, be2, eps, Wp, b1, b2, xo, gn, bn, xn, z, z, zf); break;
-        default: hipLaunchKernelGGL(ffn_fused_kernel<0>, grid, blk, LDS_BYTES, st, x, M, g2, be2, eps, Wp, b1, b2, xo, gn, bn, xn, z, z, zf);
+        case 1: hipLaunchKernelGGL(ffn_fused_kernel<1>, grid, blk, LDS_BYTES, st, x, M, g2, be2, eps, Wp, b1, b2, xo, gn, bn, xn, z, z, zf, zf); break;
+        case 2: hipLaunchKernelGGL(ffn_fused_kernel<2>, grid, blk, LDS_BYTES, st, x, M, g2, be2, eps, Wp, b1, b2, xo, gn, bn, xn, z, z, zf, zf); break;
+        case 3: hipLaunchKernelGGL(ffn_fused_kernel<3>, grid, blk, LDS_BYTES, st, x, M, g2, be2, eps, Wp, b1, b2, xo, gn, bn, xn, z, z, zf, zf); break;
+        case 4: hipLaunchKernelGGL(ffn_fused_kernel<4>, grid, blk, LDS_BYTES, st, x, M, g2, be2, eps, Wp, b1, b2, xo, gn, bn, xn, z, z, zf, zf); break;
+        case 5: hipLaunchKernelGGL(ffn_fused_kernel<5>, grid, blk, LDS_BYTES, st, x, M, g2, be2, eps, Wp, b1, b2, xo, gn, bn, xn, z, z, zf, zf); break;
+        default: hipLaunchKernelGGL(ffn_fused_kernel<0>, grid, blk, LDS_BYTES, st, x, M, g2, be2, eps, Wp, b1, b2, xo, gn, bn, xn, z, z, zf, zf);
     }
     PFM_LAUNCH_CHECK();
     return hipSuccess;
@@ -653,7 +673,7 @@ hipError_t pfm_ffn_fused_op(const bf16* o, const bf16* f, const float* bo, const
                                   LDS_BYTES);
     }
     hipLaunchKernelGGL((ffn_fused_kernel<0, 1>), dim3((M + BM - 1) / BM), dim3(NTH), LDS_BYTES, st, x, M, g2, be2, eps,
-                       Wop, b1, b2, xo, gn, bn, xn, o, f, bo);
+                       Wop, b1, b2, xo, gn, bn, xn, o, f, bo, (const float*)nullptr);
     PFM_LAUNCH_CHECK();
     return hipSuccess;
 }

@@ -73,7 +73,7 @@ hipError_t pfm_ffn_pack_dec(const bf16* W1, const float* W2, const float* gF, co
                             float* c2, hipStream_t st);
 hipError_t pfm_ffn_fused_dec(const float* x, int M, const float* g1, const float* be1, float eps, const bf16* Wp,
                              const float* b1, const float* c1, const float* c2, float* xo, const float* gn,
-                             const float* bn, bf16* xn, hipStream_t st);
+                             const float* bn, bf16* xn, const bf16* o, const float* bo, hipStream_t st);
 hipError_t pfm_ffn_pack_o(const bf16* Wo, bf16* Wp, hipStream_t st);
 hipError_t pfm_ffn_fused_op(const bf16* o, const bf16* f, const float* bo, const float* x, int M, const float* g2,
                             const float* be2, float eps, const bf16* Wop, const float* b1, const float* b2, float* xo,
@@ -465,7 +465,9 @@ int ensure_bf16(pfm_handle* h, hipStream_t st) {
     }
     const int ndf = h->cfg.dec_blocks > 0 ? h->cfg.dec_blocks + 1 : 0;
     if (!h->dffn_ready && ffn_shape_ok(h->cfg) && pfm_knobs().dec_ffn_fused && ndf > 0 && !h->dec.empty()) {
-        const size_t per = pfm_ffn_packed_elems();
+        // per FFN j: the 32 out-projection tiles of decoder block j - 1 (folded in front; none for j = 0),
+        // then the FFN's 256 tiles
+        const size_t po = pfm_ffn_packed_o_elems(), per = po + pfm_ffn_packed_elems();
         const int D = h->cfg.d_model;
         HIP_TRY(h->dffn_pack.ensure((size_t)ndf * per * sizeof(bf16)));
         HIP_TRY(h->dffn_c.ensure((size_t)ndf * 2 * D * sizeof(float)));
@@ -474,8 +476,9 @@ int ensure_bf16(pfm_handle* h, hipStream_t st) {
             const size_t w1 = d3 ? h->d3w1 : h->dec[j].w1, w2 = d3 ? h->d3w2 : h->dec[j].w2;
             const size_t gF = d3 ? h->d3ng : h->dec[j].ng, bF = d3 ? h->d3nb : h->dec[j].nb;
             float* cc = h->dffn_c.as<float>() + (size_t)j * 2 * D;
-            HIP_TRY(pfm_ffn_pack_dec(h->wb(w1), h->w(w2), h->w(gF), h->w(bF), h->dffn_pack.as<bf16>() + (size_t)j * per,
-                                     cc, cc + D, st));
+            if (j > 0) HIP_TRY(pfm_ffn_pack_o(h->wb(h->dec[j - 1].wo), h->dffn_pack.as<bf16>() + (size_t)j * per, st));
+            HIP_TRY(pfm_ffn_pack_dec(h->wb(w1), h->w(w2), h->w(gF), h->w(bF),
+                                     h->dffn_pack.as<bf16>() + (size_t)j * per + po, cc, cc + D, st));
         }
         h->dffn_ready = true;
     }
@@ -1387,6 +1390,7 @@ int pfm_run(pfm_handle* h, void* stream, int mode, const float* feats, const int
         const char* KVg = (const char*)KV + (size_t)b0 * T * nkv * esz;
         // fast mode: each decoder FFN (+ its LN1 before, + the LN after) as one fused kernel (k_ffn.hip DEC)
         const bool dffn = fast && !fuse_ln && h->dffn_ready && pfm_knobs().dec_ffn_fused && Mg >= 2048;
+        int op_from = -1;   // fused path: the decoder block whose out-projection runs inside the next FFN launch
         auto ffn = [&](int fi, bool xdn_ready, size_t lng, size_t lnb, size_t w1, size_t b1, size_t fng, size_t fnb,
                        size_t w2, float* out, size_t pg, size_t pb, void* pout, int pdt) -> int {
             // out = W2 . LN_F(relu(W1 . LN(x) + b1)); pout = LN_P(out)   (sanm/positionwise_feed_forward.py:26-33)
@@ -1395,9 +1399,16 @@ int pfm_run(pfm_handle* h, void* stream, int mode, const float* feats, const int
                 const double byo = (double)Mg * D * (4.0 + 2.0) + 2.0 * 2.0 * D * Fd;
                 ProfScope ps(h, s, PFM_K_GEMM, flo, byo);
                 const float* cc = h->dffn_c.as<float>() + (size_t)fi * 2 * D;
-                HIP_TRY(pfm_ffn_fused_dec(Xd, Mg, P(lng), P(lnb), c.ln_eps,
-                                          h->dffn_pack.as<bf16>() + (size_t)fi * pfm_ffn_packed_elems(), P(b1), cc,
-                                          cc + D, nullptr, P(pg), P(pb), (bf16*)pout, s));
+                const size_t po = pfm_ffn_packed_o_elems();
+                const bf16* blk = h->dffn_pack.as<bf16>() + (size_t)fi * (po + pfm_ffn_packed_elems());
+                if (op_from >= 0) {   // x = x + O Wo^T + bo of block op_from, then the FFN on it
+                    HIP_TRY(pfm_ffn_fused_dec(Xd, Mg, P(lng), P(lnb), c.ln_eps, blk, P(b1), cc, cc + D, Xd, P(pg),
+                                              P(pb), (bf16*)pout, Odb, P(h->dec[op_from].bo), s));
+                    op_from = -1;
+                } else {
+                    HIP_TRY(pfm_ffn_fused_dec(Xd, Mg, P(lng), P(lnb), c.ln_eps, blk + po, P(b1), cc, cc + D, nullptr,
+                                              P(pg), P(pb), (bf16*)pout, nullptr, nullptr, s));
+                }
                 return PFM_OK;
             }
             if (!xdn_ready)
@@ -1469,6 +1480,8 @@ int pfm_run(pfm_handle* h, void* stream, int mode, const float* feats, const int
                     HIP_TRY(rg.gemm_ln(Odb, rowmap_plain(D), W(Lr.wo), D, Mg, D, e, ng, nbb, Xdn, rowmap_plain(D), dt,
                                        nullptr, plain));
                     xdn_ready = true;
+                } else if (dffn) {   // runs as phase 0 of the next FFN launch
+                    op_from = l;
                 } else {
                     HIP_TRY(gemmA(fast ? (const void*)Odb : (const void*)Od, false, W(Lr.wo), D, D, e));
                 }
