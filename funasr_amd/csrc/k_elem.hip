@@ -455,12 +455,16 @@ __global__ __launch_bounds__(64) void cif_fire_kernel(const float* __restrict__ 
     double ph = 0.0, P = 0.0;
     float pph = 0.f, prh = 0.f, prevfl = 0.f;
     int k = 0;
+    // an utterance's T + 1 rows are ld apart within one segment (plain map or one segment per utterance:
+    // launcher check), so the row address is a base plus t * ld (no per-frame RowMap division)
+    const float* hb = h + hmap.off((long long)b * (T + 1)) + cc;
+    const long long hld = hmap.ld;
     auto fetch = [&](int t0, float (&hv)[CIF_PF], float (&av)[CIF_PF]) {
 #pragma unroll
         for (int i = 0; i < CIF_PF; ++i) {
             const int t = min(t0 + i, T);
             av[i] = al[t];
-            hv[i] = h[hmap.off((long long)b * (T + 1) + t) + cc];
+            hv[i] = hb[(long long)t * hld];
         }
     };
     auto scan = [&](int t0, const float (&hv)[CIF_PF], const float (&av)[CIF_PF]) {
@@ -500,11 +504,9 @@ __global__ __launch_bounds__(64) void cif_fire_kernel(const float* __restrict__ 
     }
     if (act)
         for (int kk = k; kk < Lcap; ++kk) emb[((long long)b * Lcap + kk) * D + c] = 0.f;
-    if (lead) {
+    if (lead) {   // P is the f64 running sum of alpha[0..T] in order: token_num = floor(sum(alphas))
         n_fire[b] = k;
-        double s = 0.0;
-        for (int t = 0; t <= T; ++t) s += (double)al[t];
-        ntok[b] = (int)floor(s);
+        ntok[b] = (int)floor(P);
     }
 }
 
@@ -796,6 +798,7 @@ hipError_t pfm_cif_alpha(const float* hc, int D, const float* wout, const float*
 hipError_t pfm_cif_fire(const float* alphas, const float* h, RowMap hmap, int B, int T, int D, int Lcap,
                         float* emb, float* peaks, int* n_fire, int* ntok, hipStream_t st) {
     if (B <= 0 || D <= 0) return hipSuccess;
+    if (hmap.rows_per_seg > 0 && hmap.rows_per_seg != T + 1) return hipErrorInvalidValue;
     hipLaunchKernelGGL(cif_fire_kernel, dim3((D + 63) / 64, B), dim3(64), 0, st, alphas, h, hmap, T, D, Lcap, emb,
                        peaks, n_fire, ntok);
     PFM_LAUNCH_CHECK();
