@@ -222,6 +222,7 @@ struct pfm_handle {
     DevBuf arena_bf;               // bf16 copies of GEMM weights (same element offsets)
     DevBuf fold_w, fold_f;         // LayerNorm-folded projection weights (bf16) and column terms (f32)
     bool fold_ready = false;
+    DevBuf qkv0_pad;               // fast mode: layer 0's bf16 QKV weights with K padded to a multiple of 64
     DevBuf ffn_pack;               // fused-FFN weight tiles of every encoder layer (bf16, LDS-image order)
     bool ffn_ready = false;
     DevBuf dffn_pack, dffn_c;      // decoder FFNs (16 blocks + decoders3): W1 | W2 diag(gamma_F) tiles; c1 | c2
@@ -428,6 +429,15 @@ int ensure_bf16(pfm_handle* h, hipStream_t st) {
         HIP_TRY(h->arena_bf.ensure(h->arena_elems * sizeof(bf16)));
         for (auto& r : h->gemm_ranges)
             HIP_TRY(pfm_f32_to_bf16(h->w(r.first), h->wb(r.first), (long long)r.second, st));
+        // layer 0's QKV weights (K = input_size, e.g. 560) zero-padded to a multiple of 64, so the first
+        // projection runs on the 256x256 LDS-DMA kernel (K % 64 == 0) instead of the odd-K fallback
+        if (!h->enc.empty() && h->enc[0].din % 64) {
+            const int din = h->enc[0].din, Kp = (din + 63) / 64 * 64, N = 3 * h->cfg.d_model;
+            HIP_TRY(h->qkv0_pad.ensure((size_t)N * Kp * sizeof(bf16)));
+            HIP_TRY(hipMemsetAsync(h->qkv0_pad.p, 0, (size_t)N * Kp * sizeof(bf16), st));
+            HIP_TRY(hipMemcpy2DAsync(h->qkv0_pad.p, (size_t)Kp * 2, h->wb(h->enc[0].wqkv), (size_t)din * 2,
+                                     (size_t)din * 2, N, hipMemcpyDeviceToDevice, st));
+        }
         h->bf_ready = true;
     }
     if (!h->fold_ready && h->cfg.d_model == 512 && ln_fold_enabled()) {
@@ -898,6 +908,9 @@ int encoder_stack(const Run& r, const float* x_in, const int* lens, int B, int T
     // (three bf16 planes, DT_X3) instead of f32 + a separate split pass
     const bool x3 = r.x3 && !r.ck;
     const RowMap xmap3 = rowmap_plain(x3 ? 3 * D : D);
+    // fast mode, offline: layer 0's K = input_size padded to a multiple of 64 (zero columns, qkv0_pad)
+    const int Kp0 = (I + 63) / 64 * 64;
+    const bool pad0 = fast && !r.raw_input && !r.ck && I % 64 && h->qkv0_pad.p && l0 == 0;
     const int lndt = x3 ? DT_X3 : dt;
     for (int l = l0; l < l1; ++l) {
         const EncLayer& L = h->enc[l];
@@ -905,7 +918,12 @@ int encoder_stack(const Run& r, const float* x_in, const int* lens, int B, int T
         if (l == 0 && r.raw_input)   // streaming: the window already holds x sqrt(d) + PE
             HIP_TRY(pfm_layernorm(x_in, rowmap_plain(I), (int)M, I, r.P(L.ln1g), r.P(L.ln1b), c.ln_eps, nullptr, 0,
                                   1.f, Xn, rowmap_plain(I), dt, nullptr, plain, 0, st));
-        else if (l == 0)   // x = x_in * sqrt(d_model) + PE ; LN1
+        else if (l == 0 && pad0) {   // ... into rows of Kp0 columns whose tail stays zero (padded K)
+            HIP_TRY(hipMemset2DAsync((char*)Xn + (size_t)I * 2, (size_t)Kp0 * 2, 0, (size_t)(Kp0 - I) * 2, M, st));
+            HIP_TRY(pfm_layernorm(x_in, rowmap_plain(I), (int)M, I, r.P(L.ln1g), r.P(L.ln1b), c.ln_eps,
+                                  h->pe.as<float>(), T, sqrtf((float)D), Xn, rowmap_plain(Kp0), dt, nullptr, plain, 0,
+                                  st));
+        } else if (l == 0)   // x = x_in * sqrt(d_model) + PE ; LN1
             HIP_TRY(pfm_layernorm(x_in, rowmap_plain(I), (int)M, I, r.P(L.ln1g), r.P(L.ln1b), c.ln_eps,
                                   h->pe.as<float>(), T, sqrtf((float)D), Xn, rowmap_plain(I), dt, nullptr, plain, 0,
                                   st));
@@ -922,6 +940,8 @@ int encoder_stack(const Run& r, const float* x_in, const int* lens, int B, int T
                 HIP_TRY(r.gemm(dt, Xn, rowmap_plain(D), fw + L.fq_w, D, (int)M, 3 * D, D, e));
             } else if (x3 && l > 0) {
                 HIP_TRY(r.gemm3(Xn, xmap3, r.W(L.wqkv), din, (int)M, 3 * D, din, e));
+            } else if (l == 0 && pad0) {
+                HIP_TRY(r.gemm(dt, Xn, rowmap_plain(Kp0), h->qkv0_pad.p, Kp0, (int)M, 3 * D, Kp0, e));
             } else {
                 HIP_TRY(r.gemm(dt, Xn, rowmap_plain(din), r.W(L.wqkv), din, (int)M, 3 * D, din, e));
             }
