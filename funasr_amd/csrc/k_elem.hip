@@ -317,6 +317,98 @@ __global__ __launch_bounds__(256) void fsmn_win_kernel(const TIN* __restrict__ v
     }
 }
 
+// fsmn_win_kernel<11, TIN, 5> with the following LayerNorm fused (D = 512: a 256-thread block is two
+// 8-row blocks x all 128 channel quads): y = res + FSMN(v) as there -> out (f32); then per row
+// mean / centred variance over the 512 channels (wave sums, the row's two waves joined through LDS)
+// -> ln_out = bf16(LN(y) * g + b). Used by the fast decoder: x += FSMN(LN2(t)) then LN3(x) (decoder.py:104-110).
+template <typename TIN>
+__global__ __launch_bounds__(256) void fsmn_ln_kernel(const TIN* __restrict__ v, RowMap vmap, const int* __restrict__ len,
+                                                      int B, int T, const float* __restrict__ wT,
+                                                      const float* __restrict__ res, float* __restrict__ out,
+                                                      const float* __restrict__ g, const float* __restrict__ bb,
+                                                      float eps, bf16* __restrict__ ln_out) {
+    constexpr int KK = 11, LEFT = 5, D = 512, QPR = D / 4;
+    __shared__ float red[2][2][FR];   // [row block][wave of the row block][row]
+    const int nblk = (T + FR - 1) / FR;
+    const long long rbg = (long long)blockIdx.x * 2 + (threadIdx.x >> 7);   // global row block
+    const bool valid = rbg < (long long)B * nblk;
+    const int q = threadIdx.x & (QPR - 1), c = q * 4;
+    const int half = threadIdx.x >> 7, wv = (threadIdx.x >> 6) & 1;
+    const int b = valid ? (int)(rbg / nblk) : 0, t0 = valid ? (int)(rbg % nblk) * FR : 0;
+    const int L = min(len[b], T);
+    float4 w[KK];
+#pragma unroll
+    for (int k = 0; k < KK; ++k) w[k] = *(const float4*)(wT + (long long)k * D + c);
+    const long long ubase = vmap.rows_per_seg > 0 ? (long long)b * vmap.seg_stride : (long long)b * T * vmap.ld;
+    float4 x[FR + KK - 1];
+#pragma unroll
+    for (int i = 0; i < FR + KK - 1; ++i) {
+        const int tc = min(max(t0 - LEFT + i, 0), T - 1);
+        x[i] = load4<TIN>(v + ubase + (long long)tc * vmap.ld + c);
+    }
+#pragma unroll
+    for (int i = 0; i < FR + KK - 1; ++i) {
+        const int tt = t0 - LEFT + i;
+        if (!(tt >= 0 && tt < L)) x[i] = make_float4(0, 0, 0, 0);
+    }
+    float4 rv[FR];
+#pragma unroll
+    for (int i = 0; i < FR; ++i) rv[i] = *(const float4*)(res + ((long long)b * T + min(t0 + i, T - 1)) * D + c);
+    float4 y[FR];
+    float ps[FR];
+#pragma unroll
+    for (int i = 0; i < FR; ++i) {
+        const int t = t0 + i;
+        float4 f = make_float4(0, 0, 0, 0);
+        if (t < L) {
+            float4 acc = make_float4(0, 0, 0, 0);
+#pragma unroll
+            for (int k = 0; k < KK; ++k) {
+                acc.x = fmaf(w[k].x, x[i + k].x, acc.x);
+                acc.y = fmaf(w[k].y, x[i + k].y, acc.y);
+                acc.z = fmaf(w[k].z, x[i + k].z, acc.z);
+                acc.w = fmaf(w[k].w, x[i + k].w, acc.w);
+            }
+            const float4 self = x[i + LEFT];
+            f = make_float4(acc.x + self.x, acc.y + self.y, acc.z + self.z, acc.w + self.w);
+        }
+        const float4 r = rv[i];
+        y[i] = make_float4(r.x + f.x, r.y + f.y, r.z + f.z, r.w + f.w);
+        ps[i] = (y[i].x + y[i].y) + (y[i].z + y[i].w);
+        if (valid && t < T) *(float4*)(out + ((long long)b * T + t) * D + c) = y[i];
+    }
+    // row means: 64-lane sums, then the row block's two waves
+#pragma unroll
+    for (int i = 0; i < FR; ++i) ps[i] = wave_sum(ps[i]);
+    if ((threadIdx.x & 63) == 0)
+#pragma unroll
+        for (int i = 0; i < FR; ++i) red[half][wv][i] = ps[i];
+    __syncthreads();
+    float mean[FR], pq[FR];
+#pragma unroll
+    for (int i = 0; i < FR; ++i) {
+        mean[i] = (red[half][0][i] + red[half][1][i]) * (1.f / D);
+        const float dx = y[i].x - mean[i], dy = y[i].y - mean[i], dz = y[i].z - mean[i], dw = y[i].w - mean[i];
+        pq[i] = (dx * dx + dy * dy) + (dz * dz + dw * dw);
+    }
+    __syncthreads();   // every thread read red[] before it is reused
+#pragma unroll
+    for (int i = 0; i < FR; ++i) pq[i] = wave_sum(pq[i]);
+    if ((threadIdx.x & 63) == 0)
+#pragma unroll
+        for (int i = 0; i < FR; ++i) red[half][wv][i] = pq[i];
+    __syncthreads();
+    const float4 gg = *(const float4*)(g + c), be = *(const float4*)(bb + c);
+#pragma unroll
+    for (int i = 0; i < FR; ++i) {
+        const int t = t0 + i;
+        const float rstd = 1.f / sqrtf((red[half][0][i] + red[half][1][i]) * (1.f / D) + eps);
+        bf16x4 o = {f2bf((y[i].x - mean[i]) * rstd * gg.x + be.x), f2bf((y[i].y - mean[i]) * rstd * gg.y + be.y),
+                    f2bf((y[i].z - mean[i]) * rstd * gg.z + be.z), f2bf((y[i].w - mean[i]) * rstd * gg.w + be.w)};
+        if (valid && t < T) *(bf16x4*)(ln_out + ((long long)b * T + t) * D + c) = o;
+    }
+}
+
 __device__ __forceinline__ float bf_lo(unsigned u) { return __uint_as_float(u << 16); }
 __device__ __forceinline__ float bf_hi(unsigned u) { return __uint_as_float(u & 0xffff0000u); }
 __device__ __forceinline__ void fma8(float4 a, float4 b, uint4 u, float (&y)[8]) {
@@ -751,6 +843,20 @@ hipError_t pfm_fsmn(const float* v, RowMap vmap, const int* len, int B, int T, i
 }
 
 // bf16 input V (fast mode): out_bf only (f32 out optional)
+// x_out = res + FSMN(v) (K 11, left 5, D 512; f32) and ln_out = bf16(LayerNorm(x_out) g + b) in one pass
+hipError_t pfm_fsmn_ln_bf16in(const bf16* v, RowMap vmap, const int* len, int B, int T, int D, const float* wT,
+                              int K, int left, const float* res, float* out, const float* g, const float* b, float eps,
+                              bf16* ln_out, hipStream_t st) {
+    if (B <= 0 || T <= 0) return hipSuccess;
+    if (D != 512 || K != 11 || left != 5 || !res || !out || !ln_out) return hipErrorInvalidValue;
+    if (vmap.rows_per_seg > 0 && vmap.rows_per_seg != T) return hipErrorInvalidValue;
+    const long long nrb = (long long)B * ((T + FR - 1) / FR);
+    hipLaunchKernelGGL(fsmn_ln_kernel<bf16>, dim3((unsigned)((nrb + 1) / 2)), dim3(256), 0, st, v, vmap, len, B, T, wT,
+                       res, out, g, b, eps, ln_out);
+    PFM_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
 hipError_t pfm_fsmn_bf16in(const bf16* v, RowMap vmap, const int* len, int B, int T, int D, const float* wT, int K,
                            int left, const float* res, float* out, bf16* out_bf, hipStream_t st) {
     if (B <= 0 || T <= 0) return hipSuccess;

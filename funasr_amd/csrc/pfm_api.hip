@@ -45,6 +45,9 @@ hipError_t pfm_layernorm_bf16in(const bf16* x, RowMap xmap, int M, int D, const 
                                 void* out, RowMap omap, int odt, hipStream_t st);
 hipError_t pfm_fsmn(const float* v, RowMap vmap, const int* len, int B, int T, int D, const float* w, int K,
                     int left, const float* res, float* out, bf16* out_bf, hipStream_t st);
+hipError_t pfm_fsmn_ln_bf16in(const bf16* v, RowMap vmap, const int* len, int B, int T, int D, const float* wT,
+                              int K, int left, const float* res, float* out, const float* g, const float* b, float eps,
+                              bf16* ln_out, hipStream_t st);
 hipError_t pfm_fsmn_bf16in(const bf16* v, RowMap vmap, const int* len, int B, int T, int D, const float* wT, int K,
                            int left, const float* res, float* out, bf16* out_bf, hipStream_t st);
 hipError_t pfm_cif_alpha(const float* hc, int D, const float* wout, const float* bout, const int* len, int B,
@@ -1464,15 +1467,20 @@ int pfm_run(pfm_handle* h, void* stream, int mode, const float* feats, const int
             int rc2 = ffn(l, xdn_ready, Lr.n1g, Lr.n1b, Lr.w1, Lr.b1, Lr.ng, Lr.nb, Lr.w2, Td, Lr.n2g, Lr.n2b, Tdn,
                           fast ? DT_BF16 : DT_F32);
             if (rc2) return rc2;
-            if (fast)
-                HIP_TRY(pfm_fsmn_bf16in((const bf16*)Tdn, rowmap_plain(D), ntg, nb, L, D, P(Lr.fsmn), K, ldec, Xd, Xd,
-                                        nullptr, s));
-            else
-                HIP_TRY(pfm_fsmn((const float*)Tdn, rowmap_plain(D), ntg, nb, L, D, P(Lr.fsmn), K, ldec, Xd, Xd, nullptr,
-                                 s));
-            // x = x + CrossAtt(LN3(x), memory)   (decoder.py:109-119)
-            HIP_TRY(pfm_layernorm(Xd, rowmap_plain(D), Mg, D, P(Lr.n3g), P(Lr.n3b), c.ln_eps, nullptr, 0, 1.f, Xdn, xdm,
-                                  ndt, nullptr, plain, 0, s));
+            // x = x + CrossAtt(LN3(x), memory)   (decoder.py:109-119); fused path: LN3 in the FSMN kernel
+            if (dffn && D == 512 && K == 11 && ldec == 5) {
+                HIP_TRY(pfm_fsmn_ln_bf16in((const bf16*)Tdn, rowmap_plain(D), ntg, nb, L, D, P(Lr.fsmn), K, ldec, Xd, Xd,
+                                           P(Lr.n3g), P(Lr.n3b), c.ln_eps, (bf16*)Xdn, s));
+            } else {
+                if (fast)
+                    HIP_TRY(pfm_fsmn_bf16in((const bf16*)Tdn, rowmap_plain(D), ntg, nb, L, D, P(Lr.fsmn), K, ldec, Xd,
+                                            Xd, nullptr, s));
+                else
+                    HIP_TRY(pfm_fsmn((const float*)Tdn, rowmap_plain(D), ntg, nb, L, D, P(Lr.fsmn), K, ldec, Xd, Xd,
+                                     nullptr, s));
+                HIP_TRY(pfm_layernorm(Xd, rowmap_plain(D), Mg, D, P(Lr.n3g), P(Lr.n3b), c.ln_eps, nullptr, 0, 1.f, Xdn,
+                                      xdm, ndt, nullptr, plain, 0, s));
+            }
             {
                 GemmEpi e = epi_default();
                 e.bias = P(Lr.bq);
