@@ -1114,6 +1114,7 @@ int pick_cfg(int M, int N, int K, bool amax) {
     //    128x256 tiles, two blocks per CU (C4).
     // PFM_GEMM_POLICY=1: the earlier grid-size policy (C15 at >= 2 tiles / CU or K >= 1536 with >= 240
     // tiles, else C4); =2: C13 / C4 for decoder-sized M; =3: C4 instead of C3 for the 512-wide GEMMs of
+    // (measured on the two-group path and not kept: 256x128 tiles for the one-group QKV, 22.08 vs 21.68 ms)
     // fewer than 120 256x256 tiles (decoder projections: C3 measured 10.9 vs 13.3 us at M = 7392, K = 512;
     // 26.0 vs 35.5 us at K = 2048).
     const int p = pfm_knobs().gemm_policy;

@@ -17,6 +17,8 @@ X6_SHAPES = [("x6qkv", 16000, 1536, 3072), ("x6w1", 16000, 2048, 3072), ("x6out"
              ("x6w2", 16000, 512, 12288), ("x6kv", 32000, 16384, 3072)]
 if os.environ.get("SCAN_X6"):
     SHAPES = X6_SHAPES
+if os.environ.get("SCAN_GROUP"):   # fast-mode GEMMs of one encoder group (two groups run concurrently)
+    SHAPES = [("qkv/2", 16000, 1536, 512), ("kv", 32000, 16384, 512), ("qkv0/2", 16000, 1536, 576)]
 
 
 def main():

@@ -12,6 +12,8 @@ from funasr_amd import runtime as rt
 
 SHAPES = [("enc out+res", 32000, 512, True), ("enc ffn2+res", 32000, 2048, True),
           ("dec w2", 14784, 2048, False), ("dec out+res", 14784, 512, True)]
+if os.environ.get("SCAN_X6"):   # EXACT-mode (x6) K' = 6K shapes of one encoder group
+    SHAPES = [("x6 out+res", 16000, 3072, True), ("x6 ffn2+res", 16000, 12288, True)]
 
 
 def main():
