@@ -31,7 +31,7 @@ namespace {
 typedef __attribute__((address_space(3))) void lds_void;
 typedef const __attribute__((address_space(1))) void gbl_void;
 
-constexpr int FD = 512, FF = 2048, BM = 64, NTH = 512;
+constexpr int FD = 512, FF = 2048, BM = 64;
 constexpr int HC = 256, NCH = FF / HC;          // hidden chunk, chunks
 constexpr int TILE = 16384, TPC = 32, NTILE = NCH * TPC;
 constexpr int OP_TILES = 32;                    // out-projection Wo [512][512]: 16 k steps x 2 halves (W2 format)
@@ -57,7 +57,17 @@ __device__ __forceinline__ float pick4(float v0, float v1, float v2, float v3, i
     return g == 0 ? v0 : (g == 1 ? v1 : (g == 2 ? v2 : v3));
 }
 
-struct Frag { bf16x8 w[2]; bf16x8 a[4]; };
+template <int N> __device__ __forceinline__ void vm_wait() {
+    if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else if constexpr (N == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if constexpr (N == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+    else static_assert(N < 0, "vm_wait: unsupported count");
+}
+
+template <int HB> struct Frag { bf16x8 w[HB]; bf16x8 a[4]; };
 
 // VAR (diagnostic builds, PFM_FFN_VAR): 0 = the kernel; 1 = no weight DMA (stale ring); 2 = no MFMAs;
 // 3 = every tile streams ring tiles 0..3 of the layer (L2-hot 64 KiB); 4 = prologue + epilogue only (no
@@ -77,8 +87,19 @@ struct Frag { bf16x8 w[2]; bf16x8 a[4]; };
 // with mu / rstd of the bf16 hidden h accumulated chunk by chunk (sum, sum of squares) and reduced across the
 // 8 waves in the epilogue. Outputs: xn = LN_next(y) (bf16; the decoder's LN2 or after_norm), xo = y (optional).
 // In DEC mode the arguments bo / b2 carry c1 / c2.
-template <int VAR, int MODE = 0>
-__global__ __launch_bounds__(NTH) void ffn_fused_kernel(const float* __restrict__ X, int M, const float* __restrict__ g2,
+//
+// NW (waves per workgroup): 8 = wave w owns 32 weight rows of every 256-row tile (2 fragments), the kernel;
+// 4 = one wave per SIMD owning 64 weight rows (4 fragments, 192 accumulator registers; each tile's A / H
+// fragments read by half as many waves: 32 instead of 48 KiB of LDS reads per tile) measured 16 % slower
+// (207 vs 178 us at M = 32,000; bench 24.6 vs 21.6 ms/step) and is not instantiated.
+// HR: phase 2 (and phase 0) reads a k step's activation fragments once for both 256-row halves (odd tiles
+// copy them from the even tile's registers) instead of re-reading them from LDS (PFM_FFN_HR A/B).
+// PD: ring tiles in flight behind the one being published (2: tile t+3 issued at the top of iteration t, 3:
+// tile t+4 — the slot of tile t is free as soon as the barrier retires everyone's fragment reads of it, so
+// all 4 ring slots can be streaming; PFM_FFN_PD A/B: 3 is the default, bench 21.6 -> 20.1 ms/step).
+// The non-default combinations (HR = false, PD = 2) are instantiated for VAR 0 only.
+template <int VAR, int MODE = 0, int NW = 8, bool HR = true, int PD = 3>
+__global__ __launch_bounds__(64 * NW) void ffn_fused_kernel(const float* __restrict__ X, int M, const float* __restrict__ g2,
                                                         const float* __restrict__ be2, float eps,
                                                         const bf16* __restrict__ Wp, const float* __restrict__ b1,
                                                         const float* __restrict__ b2, float* Xo,
@@ -91,6 +112,8 @@ __global__ __launch_bounds__(NTH) void ffn_fused_kernel(const float* __restrict_
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int g = lane >> 4, r16 = lane & 15;
     const long long m0 = (long long)blockIdx.x * BM;
+    constexpr int WR = 256 / NW, HB = WR / 16, RPW = BM / NW, LPW = TILE / (1024 * NW);
+    using FragT = Frag<HB>;
     constexpr bool OP = MODE == 1 || MODE == 3, DEC = MODE == 2 || MODE == 3;
     constexpr int T0 = OP ? OP_TILES : 0;      // FFN tiles start after the Wo tiles
     float rs[4] = {0.f, 0.f, 0.f, 0.f}, rq[4] = {0.f, 0.f, 0.f, 0.f};   // DEC: hidden row sums / sums of squares
@@ -98,10 +121,11 @@ __global__ __launch_bounds__(NTH) void ffn_fused_kernel(const float* __restrict_
 
     auto issue = [&](int t) {
         if (t >= NT_ALL || VAR == 1 || VAR == 5) return;
-        const bf16* src = Wp + (long long)(VAR == 3 ? (t & 3) : t) * (TILE / 2) + (2 * w * 64 + lane) * 8;
-        unsigned char* dst = smem + OFF_RING + (t & 3) * TILE + 2 * w * 1024;
-        __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)dst, 16, 0, 0);
-        __builtin_amdgcn_global_load_lds((gbl_void*)(src + 512), (lds_void*)(dst + 1024), 16, 0, 0);
+        const bf16* src = Wp + (long long)(VAR == 3 ? (t & 3) : t) * (TILE / 2) + (LPW * w * 64 + lane) * 8;
+        unsigned char* dst = smem + OFF_RING + (t & 3) * TILE + LPW * w * 1024;
+#pragma unroll
+        for (int i = 0; i < LPW; ++i)
+            __builtin_amdgcn_global_load_lds((gbl_void*)(src + 512 * i), (lds_void*)(dst + 1024 * i), 16, 0, 0);
     };
     auto bar = [&]() {
         if (VAR == 5) return;
@@ -114,8 +138,8 @@ __global__ __launch_bounds__(NTH) void ffn_fused_kernel(const float* __restrict_
     //      (OP: the attention output rows go to the A image instead; LN2 follows phase 0)
     if constexpr (OP) {
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const int m = 8 * w + i;
+        for (int i = 0; i < RPW; ++i) {
+            const int m = RPW * w + i;
             const long long row = min(m0 + m, (long long)M - 1);
             const bf16x8 v = *(const bf16x8*)(O + row * FD + 8 * lane);
             *(bf16x8*)(smem + OFF_AN + m * 1024 + ((lane ^ (m & 15)) << 4)) = v;
@@ -123,11 +147,12 @@ __global__ __launch_bounds__(NTH) void ffn_fused_kernel(const float* __restrict_
         issue(0);
         issue(1);
         issue(2);
+        if constexpr (PD == 3) issue(3);
     } else {
-        float4 xa[8], xb[8];
+        float4 xa[RPW], xb[RPW];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const long long row = min(m0 + 8 * w + i, (long long)M - 1);
+        for (int i = 0; i < RPW; ++i) {
+            const long long row = min(m0 + RPW * w + i, (long long)M - 1);
             const float* xr = X + row * FD + 8 * lane;
             xa[i] = *(const float4*)xr;
             xb[i] = *(const float4*)(xr + 4);
@@ -135,10 +160,11 @@ __global__ __launch_bounds__(NTH) void ffn_fused_kernel(const float* __restrict_
         issue(0);
         issue(1);
         issue(2);
+        if constexpr (PD == 3) issue(3);
         const float4 ga = *(const float4*)(g2 + 8 * lane), gb = *(const float4*)(g2 + 8 * lane + 4);
         const float4 ba = *(const float4*)(be2 + 8 * lane), bb = *(const float4*)(be2 + 8 * lane + 4);
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
+        for (int i = 0; i < RPW; ++i) {
             float v[8] = {xa[i].x, xa[i].y, xa[i].z, xa[i].w, xb[i].x, xb[i].y, xb[i].z, xb[i].w};
             float s = 0.f;
 #pragma unroll
@@ -153,14 +179,14 @@ __global__ __launch_bounds__(NTH) void ffn_fused_kernel(const float* __restrict_
             bf16x8 o;
 #pragma unroll
             for (int e = 0; e < 8; ++e) o[e] = f2bf(v[e] * rstd * gg[e] + bbv[e]);
-            const int m = 8 * w + i;
+            const int m = RPW * w + i;
             *(bf16x8*)(smem + OFF_AN + m * 1024 + ((lane ^ (m & 15)) << 4)) = o;
         }
     }
 
-    f32x4 acc1[2][4], acc2a[2][4], acc2b[2][4];
+    f32x4 acc1[HB][4], acc2a[HB][4], acc2b[HB][4];
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < HB; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
 #pragma unroll
@@ -168,43 +194,61 @@ __global__ __launch_bounds__(NTH) void ffn_fused_kernel(const float* __restrict_
 
     // fragment reads of tile t: weight rows of this wave (ring slot t & 3) + the activation operand
     // (A image for W1 tiles, H image for W2 tiles)
-    auto rd_w = [&](int t, Frag& f) {
+    auto rd_w = [&](int t, FragT& f) {
         const unsigned char* ring = smem + OFF_RING + (t & 3) * TILE;
 #pragma unroll
-        for (int hb = 0; hb < 2; ++hb) {
-            const int row = 32 * w + 16 * hb + r16;
+        for (int hb = 0; hb < HB; ++hb) {
+            const int row = WR * w + 16 * hb + r16;
             f.w[hb] = ld128(ring + row * 64 + ((g ^ f2(row)) << 4));
         }
     };
-    auto rd_a = [&](int t, Frag& f) {   // W1 tile t: k step j = t & 15 of the A image
+    auto rd_a = [&](int t, FragT& f) {   // W1 tile t: k step j = t & 15 of the A image
         const int j = t & 15;
 #pragma unroll
         for (int mb = 0; mb < 4; ++mb)
             f.a[mb] = ld128(smem + OFF_AN + (16 * mb + r16) * 1024 + (((4 * j + g) ^ r16) << 4));
     };
-    auto rd_h = [&](int t, Frag& f) {   // W2 tile t: k step s = (t & 15) >> 1 of the H image
+    auto rd_h = [&](int t, FragT& f) {   // W2 tile t: k step s = (t & 15) >> 1 of the H image
         const int s2 = (t & 15) >> 1;
 #pragma unroll
         for (int mb = 0; mb < 4; ++mb)
             f.a[mb] = ld128(smem + OFF_H + (16 * mb + r16) * 512 + (((4 * s2 + g) ^ r16) << 4));
     };
-    auto rd1 = [&](int t, Frag& f) { rd_w(t, f); rd_a(t, f); };
-    auto rd2 = [&](int t, Frag& f) { rd_w(t, f); rd_h(t, f); };
+    auto rd1 = [&](int t, FragT& f) { rd_w(t, f); rd_a(t, f); };
+    auto rd2 = [&](int t, FragT& f) { rd_w(t, f); rd_h(t, f); };
+    // the second half of a k step (odd tile) reuses the first half's activation fragments
+    auto rd_w2 = [&](int t, FragT& f, const FragT& prev) {
+        rd_w(t, f);
+        if constexpr (HR) {
+#pragma unroll
+            for (int mb = 0; mb < 4; ++mb) f.a[mb] = prev.a[mb];
+        } else if constexpr (OP) {
+            if (t < OP_TILES) {
+                const int j = t >> 1;
+#pragma unroll
+                for (int mb = 0; mb < 4; ++mb)
+                    f.a[mb] = ld128(smem + OFF_AN + (16 * mb + r16) * 1024 + (((4 * j + g) ^ r16) << 4));
+            } else {
+                rd_h(t, f);
+            }
+        } else {
+            rd_h(t, f);
+        }
+    };
     // relu(H^T + b1) of chunk c -> bf16 H image [64 rows][256 hidden] (row pitch 512 B, slot ^ (row & 15)).
     // acc1[hb][mb][i] = H^T[hidden 32w + 16hb + 4g + i][row 16mb + r16]. The wave's 32 biases come in by
     // scalar loads (no vector-memory op beside the in-flight LDS-DMA ring).
     auto write_h = [&](int c) {
-        const float* bp = b1 + HC * c + 32 * w;
-        float bv[32];
+        const float* bp = b1 + HC * c + WR * w;
 #pragma unroll
-        for (int k = 0; k < 32; ++k) bv[k] = bp[k];
+        for (int hb = 0; hb < HB; ++hb) {
+            float bv[16];
 #pragma unroll
-        for (int hb = 0; hb < 2; ++hb) {
+            for (int k = 0; k < 16; ++k) bv[k] = bp[16 * hb + k];
             float bi[4];
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
-                bi[i] = pick4(bv[16 * hb + i], bv[16 * hb + 4 + i], bv[16 * hb + 8 + i], bv[16 * hb + 12 + i], g);
-            const int hl = 32 * w + 16 * hb + 4 * g;
+            for (int i = 0; i < 4; ++i) bi[i] = pick4(bv[i], bv[4 + i], bv[8 + i], bv[12 + i], g);
+            const int hl = WR * w + 16 * hb + 4 * g;
 #pragma unroll
             for (int mb = 0; mb < 4; ++mb) {
                 const int m = 16 * mb + r16;
@@ -225,52 +269,62 @@ __global__ __launch_bounds__(NTH) void ffn_fused_kernel(const float* __restrict_
             }
         }
     };
-    auto mm1 = [&](const Frag& f) {
-        if (VAR == 2) { asm volatile("" :: "v"(f.w[0]), "v"(f.w[1]), "v"(f.a[0]), "v"(f.a[1]), "v"(f.a[2]), "v"(f.a[3])); return; }
+    auto mm1 = [&](const FragT& f) {
+        if (VAR == 2) { asm volatile("" :: "v"(f.w[0]), "v"(f.w[HB - 1]), "v"(f.a[0]), "v"(f.a[1]), "v"(f.a[2]), "v"(f.a[3])); return; }
         __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-        for (int hb = 0; hb < 2; ++hb)
+        for (int hb = 0; hb < HB; ++hb)
 #pragma unroll
             for (int mb = 0; mb < 4; ++mb) acc1[hb][mb] = mfma16(f.w[hb], f.a[mb], acc1[hb][mb]);
         __builtin_amdgcn_s_setprio(0);
     };
-    auto mm2a = [&](const Frag& f) {
-        if (VAR == 2) { asm volatile("" :: "v"(f.w[0]), "v"(f.w[1]), "v"(f.a[0]), "v"(f.a[1]), "v"(f.a[2]), "v"(f.a[3])); return; }
+    auto mm2a = [&](const FragT& f) {
+        if (VAR == 2) { asm volatile("" :: "v"(f.w[0]), "v"(f.w[HB - 1]), "v"(f.a[0]), "v"(f.a[1]), "v"(f.a[2]), "v"(f.a[3])); return; }
         __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-        for (int nb = 0; nb < 2; ++nb)
+        for (int nb = 0; nb < HB; ++nb)
 #pragma unroll
             for (int mb = 0; mb < 4; ++mb) acc2a[nb][mb] = mfma16(f.w[nb], f.a[mb], acc2a[nb][mb]);
         __builtin_amdgcn_s_setprio(0);
     };
-    auto mm2b = [&](const Frag& f) {
-        if (VAR == 2) { asm volatile("" :: "v"(f.w[0]), "v"(f.w[1]), "v"(f.a[0]), "v"(f.a[1]), "v"(f.a[2]), "v"(f.a[3])); return; }
+    auto mm2b = [&](const FragT& f) {
+        if (VAR == 2) { asm volatile("" :: "v"(f.w[0]), "v"(f.w[HB - 1]), "v"(f.a[0]), "v"(f.a[1]), "v"(f.a[2]), "v"(f.a[3])); return; }
         __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-        for (int nb = 0; nb < 2; ++nb)
+        for (int nb = 0; nb < HB; ++nb)
 #pragma unroll
             for (int mb = 0; mb < 4; ++mb) acc2b[nb][mb] = mfma16(f.w[nb], f.a[mb], acc2b[nb][mb]);
         __builtin_amdgcn_s_setprio(0);
     };
-    // top of iteration t: tile t+1 landed (tile t+2 may stay in flight) and visible to every wave, then
-    // the DMA of tile t+3 into the slot of tile t-1 (whose fragments every wave consumed in iteration t-1)
+    // top of iteration t: tile t+1 landed (tiles t+2 .. t+PD may stay in flight) and visible to every wave,
+    // then the DMA of tile t+1+PD into the slot of tile t+PD-3 (PD = 3: tile t, PD = 2: tile t-1), whose
+    // fragments every wave read before this barrier
     auto top = [&](int t) {
         if (VAR != 1 && VAR != 5) {
-            if (t + 2 < NT_ALL) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            // tile t+1 landed; tiles t+2 .. t+PD (those that exist) may stay in flight
+            if constexpr (PD == 3) {
+                if (t + 3 < NT_ALL) vm_wait<2 * LPW>();
+                else if (t + 2 < NT_ALL) vm_wait<LPW>();
+                else vm_wait<0>();
+            } else {
+                if (t + 2 < NT_ALL) vm_wait<LPW>();
+                else vm_wait<0>();
+            }
         }
         bar();
-        issue(t + 3);
+        issue(t + 1 + PD);
     };
 
     // Software pipeline, iteration t: top(t) -> fragment reads of tile t+1 -> MFMAs of tile t (fragments
     // read in iteration t-1), so the ds_read latency of the next tile hides under this tile's MFMAs.
-    if (VAR != 1 && VAR != 5) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");   // tile 0 (tiles 1, 2 in flight)
+    if (VAR != 1 && VAR != 5) {   // tile 0 (tiles 1, 2 in flight)
+        vm_wait<PD * LPW>();
+    }
     bar();
-    Frag F0, F1;
+    FragT F0, F1;
     if constexpr (OP) {
         // phase 0: Wo tile t = k step t >> 1 (of the O image in the A slot), half t & 1
-        auto rd0 = [&](int t, Frag& f) {
+        auto rd0 = [&](int t, FragT& f) {
             rd_w(t, f);
             const int j = t >> 1;
 #pragma unroll
@@ -279,10 +333,10 @@ __global__ __launch_bounds__(NTH) void ffn_fused_kernel(const float* __restrict_
         };
         rd0(0, F0);
         for (int s2 = 0; s2 < OP_TILES / 2 - 1; ++s2) {
-            top(2 * s2); rd0(2 * s2 + 1, F1); mm2a(F0);
+            top(2 * s2); rd_w2(2 * s2 + 1, F1, F0); mm2a(F0);
             top(2 * s2 + 1); rd0(2 * s2 + 2, F0); mm2b(F1);
         }
-        top(OP_TILES - 2); rd0(OP_TILES - 1, F1); mm2a(F0);
+        top(OP_TILES - 2); rd_w2(OP_TILES - 1, F1, F0); mm2a(F0);
         top(OP_TILES - 1); mm2b(F1);
         // x1 = ((Y0 + bo) + F) + x in the accumulator layout: acc2{a,b}[nb][mb][e] = x1[row 16mb + r16]
         // [col 32w + 16nb + 4g + e (+256 for b)]; LN2 row statistics: lane partials -> 4 g lanes -> 8 waves
@@ -294,8 +348,8 @@ __global__ __launch_bounds__(NTH) void ffn_fused_kernel(const float* __restrict_
 #pragma unroll
             for (int hf = 0; hf < 2; ++hf)
 #pragma unroll
-                for (int nb = 0; nb < 2; ++nb) {
-                    const int n = 256 * hf + 32 * w + 16 * nb + 4 * g;
+                for (int nb = 0; nb < HB; ++nb) {
+                    const int n = 256 * hf + WR * w + 16 * nb + 4 * g;
                     f32x4& a = hf ? acc2b[nb][mb] : acc2a[nb][mb];
                     const float4 bb4 = *(const float4*)(bo + n);
                     float4 x4 = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -324,7 +378,7 @@ __global__ __launch_bounds__(NTH) void ffn_fused_kernel(const float* __restrict_
             for (int mb = 0; mb < 4; ++mb) {
                 float t = 0.f;
 #pragma unroll
-                for (int ww = 0; ww < 8; ++ww) t += red[slot * 512 + ww * 64 + 16 * mb + r16];
+                for (int ww = 0; ww < NW; ++ww) t += red[slot * 512 + ww * 64 + 16 * mb + r16];
                 v[mb] = t;
             }
         };
@@ -337,7 +391,7 @@ __global__ __launch_bounds__(NTH) void ffn_fused_kernel(const float* __restrict_
 #pragma unroll
             for (int hf = 0; hf < 2; ++hf)
 #pragma unroll
-                for (int nb = 0; nb < 2; ++nb) {
+                for (int nb = 0; nb < HB; ++nb) {
                     const f32x4& a = hf ? acc2b[nb][mb] : acc2a[nb][mb];
 #pragma unroll
                     for (int e = 0; e < 4; ++e) { const float d = a[e] - mean[mb]; q[mb] += d * d; }
@@ -350,8 +404,8 @@ __global__ __launch_bounds__(NTH) void ffn_fused_kernel(const float* __restrict_
 #pragma unroll
             for (int hf = 0; hf < 2; ++hf)
 #pragma unroll
-                for (int nb = 0; nb < 2; ++nb) {
-                    const int n = 256 * hf + 32 * w + 16 * nb + 4 * g;
+                for (int nb = 0; nb < HB; ++nb) {
+                    const int n = 256 * hf + WR * w + 16 * nb + 4 * g;
                     f32x4& a = hf ? acc2b[nb][mb] : acc2a[nb][mb];
                     const float4 gg = *(const float4*)(g2 + n), be = *(const float4*)(be2 + n);
                     bf16x4 o = {f2bf((a[0] - mean[mb]) * rstd * gg.x + be.x), f2bf((a[1] - mean[mb]) * rstd * gg.y + be.y),
@@ -381,10 +435,10 @@ __global__ __launch_bounds__(NTH) void ffn_fused_kernel(const float* __restrict_
         // phase 2: 16 W2 tiles (k step s: half 0 -> acc2a, half 1 -> acc2b)
         for (int s2 = 0; s2 < 7; ++s2) {
             const int t = tb + 16 + 2 * s2;
-            top(t); rd2(t + 1, F1); mm2a(F0);
+            top(t); rd_w2(t + 1, F1, F0); mm2a(F0);
             top(t + 1); rd2(t + 2, F0); mm2b(F1);
         }
-        top(tb + 30); rd2(tb + 31, F1); mm2a(F0);
+        top(tb + 30); rd_w2(tb + 31, F1, F0); mm2a(F0);
         if (c + 1 < NCH) { top(tb + 31); rd1(tb + 32, F0); }
         mm2b(F1);
     }
@@ -392,14 +446,14 @@ __global__ __launch_bounds__(NTH) void ffn_fused_kernel(const float* __restrict_
     if (VAR == 4) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     // ---- epilogue: Y^T accumulators -> f32 row image; x + Y + b2 -> Xo; LN1_next -> Xn
     //      (OP: the accumulators already hold x1 + b2 + W2 . H)
-    float4 xa[8], xb[8];
+    float4 xa[RPW], xb[RPW];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
+    for (int i = 0; i < RPW; ++i) {
         if constexpr (OP || DEC) {
             xa[i] = make_float4(0.f, 0.f, 0.f, 0.f);
             xb[i] = xa[i];
         } else {
-            const long long row = min(m0 + 8 * w + i, (long long)M - 1);
+            const long long row = min(m0 + RPW * w + i, (long long)M - 1);
             const float* xr = X + row * FD + 8 * lane;
             xa[i] = *(const float4*)xr;
             xb[i] = *(const float4*)(xr + 4);
@@ -424,7 +478,7 @@ __global__ __launch_bounds__(NTH) void ffn_fused_kernel(const float* __restrict_
         if (tid < BM) {
             float sm = 0.f, sq = 0.f;
 #pragma unroll
-            for (int ww = 0; ww < 8; ++ww) { sm += red[ww * 64 + tid]; sq += red[512 + ww * 64 + tid]; }
+            for (int ww = 0; ww < NW; ++ww) { sm += red[ww * 64 + tid]; sq += red[512 + ww * 64 + tid]; }
             const float mu = sm * (1.f / FF);
             const float var = fmaxf(sq * (1.f / FF) - mu * mu, 0.f);
             stats[tid] = make_float2(mu, 1.f / sqrtf(var + eps));
@@ -432,11 +486,11 @@ __global__ __launch_bounds__(NTH) void ffn_fused_kernel(const float* __restrict_
     }
     float* Y = (float*)smem;
 #pragma unroll
-    for (int nb = 0; nb < 2; ++nb)
+    for (int nb = 0; nb < HB; ++nb)
 #pragma unroll
         for (int mb = 0; mb < 4; ++mb) {
             const int m = 16 * mb + r16;
-            const int n = 32 * w + 16 * nb + 4 * g;
+            const int n = WR * w + 16 * nb + 4 * g;
             *(f32x4*)(Y + m * YP + n) = acc2a[nb][mb];
             *(f32x4*)(Y + m * YP + 256 + n) = acc2b[nb][mb];
         }
@@ -457,8 +511,8 @@ __global__ __launch_bounds__(NTH) void ffn_fused_kernel(const float* __restrict_
         qa = *(const float4*)(bn + 8 * lane); qb = *(const float4*)(bn + 8 * lane + 4);
     }
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        const int m = 8 * w + i;
+    for (int i = 0; i < RPW; ++i) {
+        const int m = RPW * w + i;
         const long long row = m0 + m;
         const f32x4 ya = *(const f32x4*)(Y + m * YP + 8 * lane), yb = *(const f32x4*)(Y + m * YP + 8 * lane + 4);
         float v[8] = {ya[0] + c2a.x + xa[i].x, ya[1] + c2a.y + xa[i].y, ya[2] + c2a.z + xa[i].z,
@@ -582,6 +636,38 @@ hipError_t pfm_ffn_pack_dec(const bf16* W1, const float* W2, const float* gF, co
 // With o (bf16 [M, 512], the previous block's cross-attention output) and bo: that block's out-projection runs
 // first (mode 3): x1 = x + o Wo^T + bo is written to xo (f32, may alias x) and the FFN runs on x1; Wp then
 // points at the 32 Wo tiles that precede the FFN tiles.
+template <int VAR, int MODE, int NW, bool HR, int PD>
+static void ffn_launch(hipStream_t st, int M, const float* x, const float* g, const float* be, float eps, const bf16* Wp,
+                const float* b1, const float* b2, float* xo, const float* gn, const float* bn, bf16* xn, const bf16* o,
+                const bf16* f, const float* bo, const float* c1) {
+    static bool attr_done = false;   // one flag per instantiation
+    if (!attr_done) {
+        attr_done = true;
+        (void)hipFuncSetAttribute((const void*)ffn_fused_kernel<VAR, MODE, NW, HR, PD>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+    }
+    hipLaunchKernelGGL((ffn_fused_kernel<VAR, MODE, NW, HR, PD>), dim3((M + BM - 1) / BM), dim3(64 * NW), LDS_BYTES, st, x, M,
+                       g, be, eps, Wp, b1, b2, xo, gn, bn, xn, o, f, bo, c1);
+}
+
+template <int VAR, int MODE>
+static void ffn_launch_nw(hipStream_t st, int M, const float* x, const float* g, const float* be, float eps, const bf16* Wp,
+                   const float* b1, const float* b2, float* xo, const float* gn, const float* bn, bf16* xn, const bf16* o,
+                   const bf16* f, const float* bo, const float* c1) {
+    const PfmKnobs& k = pfm_knobs();
+    if (VAR == 0 && !k.ffn_hr)
+        ffn_launch<VAR, MODE, 8, false, 3>(st, M, x, g, be, eps, Wp, b1, b2, xo, gn, bn, xn, o, f, bo, c1);
+    else if (VAR == 0 && k.ffn_pd == 2)
+        ffn_launch<VAR, MODE, 8, true, 2>(st, M, x, g, be, eps, Wp, b1, b2, xo, gn, bn, xn, o, f, bo, c1);
+    else
+        ffn_launch<VAR, MODE, 8, true, 3>(st, M, x, g, be, eps, Wp, b1, b2, xo, gn, bn, xn, o, f, bo, c1);
+}
+
+// Fused decoder feed-forward (ffn_fused_kernel DEC): x f32 [M, 512] -> xn = LN_next(W2 LN_F(relu(W1 LN1(x) + b1)))
+// bf16 [M, 512] (+ the f32 FFN output in xo when non-null). Wp / c1 / c2 from pfm_ffn_pack_dec.
+// With o (bf16 [M, 512], the previous block's cross-attention output) and bo: that block's out-projection runs
+// first (mode 3): x1 = x + o Wo^T + bo is written to xo (f32, may alias x) and the FFN runs on x1; Wp then
+// points at the 32 Wo tiles that precede the FFN tiles.
 hipError_t pfm_ffn_fused_dec(const float* x, int M, const float* g1, const float* be1, float eps, const bf16* Wp,
                              const float* b1, const float* c1, const float* c2, float* xo, const float* gn,
                              const float* bn, bf16* xn, const bf16* o, const float* bo, hipStream_t st) {
@@ -590,21 +676,10 @@ hipError_t pfm_ffn_fused_dec(const float* x, int M, const float* g1, const float
     if (((uintptr_t)x | (uintptr_t)xo | (uintptr_t)Wp | (uintptr_t)xn | (uintptr_t)c1 | (uintptr_t)c2 | (uintptr_t)o |
          (uintptr_t)bo) % 16)
         return hipErrorInvalidValue;
-    static bool attr_done = false;
-    if (!attr_done) {
-        attr_done = true;
-        (void)hipFuncSetAttribute((const void*)ffn_fused_kernel<0, 2>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  LDS_BYTES);
-        (void)hipFuncSetAttribute((const void*)ffn_fused_kernel<0, 3>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  LDS_BYTES);
-    }
     if (o)
-        hipLaunchKernelGGL((ffn_fused_kernel<0, 3>), dim3((M + BM - 1) / BM), dim3(NTH), LDS_BYTES, st, x, M, g1, be1,
-                           eps, Wp, b1, c2, xo, gn, bn, xn, o, (const bf16*)nullptr, bo, c1);
+        ffn_launch_nw<0, 3>(st, M, x, g1, be1, eps, Wp, b1, c2, xo, gn, bn, xn, o, nullptr, bo, c1);
     else
-        hipLaunchKernelGGL((ffn_fused_kernel<0, 2>), dim3((M + BM - 1) / BM), dim3(NTH), LDS_BYTES, st, x, M, g1, be1,
-                           eps, Wp, b1, c2, xo, gn, bn, xn, (const bf16*)nullptr, (const bf16*)nullptr,
-                           (const float*)nullptr, c1);
+        ffn_launch_nw<0, 2>(st, M, x, g1, be1, eps, Wp, b1, c2, xo, gn, bn, xn, nullptr, nullptr, nullptr, c1);
     PFM_LAUNCH_CHECK();
     return hipSuccess;
 }
@@ -630,26 +705,15 @@ hipError_t pfm_ffn_fused(const float* x, int M, const float* g2, const float* be
     if (M <= 0) return hipSuccess;
     if ((xn != nullptr) != (gn != nullptr && bn != nullptr)) return hipErrorInvalidValue;
     if (((uintptr_t)x | (uintptr_t)xo | (uintptr_t)Wp | (uintptr_t)xn) % 16) return hipErrorInvalidValue;
-    static bool attr_done = false;
-    if (!attr_done) {
-        attr_done = true;
-        (void)hipFuncSetAttribute((const void*)ffn_fused_kernel<0>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
-        (void)hipFuncSetAttribute((const void*)ffn_fused_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
-        (void)hipFuncSetAttribute((const void*)ffn_fused_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
-        (void)hipFuncSetAttribute((const void*)ffn_fused_kernel<3>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
-        (void)hipFuncSetAttribute((const void*)ffn_fused_kernel<4>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
-        (void)hipFuncSetAttribute((const void*)ffn_fused_kernel<5>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
-    }
-    const dim3 grid((M + BM - 1) / BM), blk(NTH);
     const bf16* z = nullptr;
     const float* zf = nullptr;
     switch (pfm_knobs().ffn_var) {
-        case 1: hipLaunchKernelGGL(ffn_fused_kernel<1>, grid, blk, LDS_BYTES, st, x, M, g2, be2, eps, Wp, b1, b2, xo, gn, bn, xn, z, z, zf, zf); break;
-        case 2: hipLaunchKernelGGL(ffn_fused_kernel<2>, grid, blk, LDS_BYTES, st, x, M, g2, be2, eps, Wp, b1, b2, xo, gn, bn, xn, z, z, zf, zf); break;
-        case 3: hipLaunchKernelGGL(ffn_fused_kernel<3>, grid, blk, LDS_BYTES, st, x, M, g2, be2, eps, Wp, b1, b2, xo, gn, bn, xn, z, z, zf, zf); break;
-        case 4: hipLaunchKernelGGL(ffn_fused_kernel<4>, grid, blk, LDS_BYTES, st, x, M, g2, be2, eps, Wp, b1, b2, xo, gn, bn, xn, z, z, zf, zf); break;
-        case 5: hipLaunchKernelGGL(ffn_fused_kernel<5>, grid, blk, LDS_BYTES, st, x, M, g2, be2, eps, Wp, b1, b2, xo, gn, bn, xn, z, z, zf, zf); break;
-        default: hipLaunchKernelGGL(ffn_fused_kernel<0>, grid, blk, LDS_BYTES, st, x, M, g2, be2, eps, Wp, b1, b2, xo, gn, bn, xn, z, z, zf, zf);
+        case 1: ffn_launch_nw<1, 0>(st, M, x, g2, be2, eps, Wp, b1, b2, xo, gn, bn, xn, z, z, zf, zf); break;
+        case 2: ffn_launch_nw<2, 0>(st, M, x, g2, be2, eps, Wp, b1, b2, xo, gn, bn, xn, z, z, zf, zf); break;
+        case 3: ffn_launch_nw<3, 0>(st, M, x, g2, be2, eps, Wp, b1, b2, xo, gn, bn, xn, z, z, zf, zf); break;
+        case 4: ffn_launch_nw<4, 0>(st, M, x, g2, be2, eps, Wp, b1, b2, xo, gn, bn, xn, z, z, zf, zf); break;
+        case 5: ffn_launch_nw<5, 0>(st, M, x, g2, be2, eps, Wp, b1, b2, xo, gn, bn, xn, z, z, zf, zf); break;
+        default: ffn_launch_nw<0, 0>(st, M, x, g2, be2, eps, Wp, b1, b2, xo, gn, bn, xn, z, z, zf, zf);
     }
     PFM_LAUNCH_CHECK();
     return hipSuccess;
@@ -666,14 +730,7 @@ hipError_t pfm_ffn_fused_op(const bf16* o, const bf16* f, const float* bo, const
     if ((xn != nullptr) != (gn != nullptr && bn != nullptr) || !o || !f || !bo) return hipErrorInvalidValue;
     if (((uintptr_t)x | (uintptr_t)xo | (uintptr_t)Wop | (uintptr_t)xn | (uintptr_t)o | (uintptr_t)f | (uintptr_t)bo) % 16)
         return hipErrorInvalidValue;
-    static bool attr_done = false;
-    if (!attr_done) {
-        attr_done = true;
-        (void)hipFuncSetAttribute((const void*)ffn_fused_kernel<0, 1>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  LDS_BYTES);
-    }
-    hipLaunchKernelGGL((ffn_fused_kernel<0, 1>), dim3((M + BM - 1) / BM), dim3(NTH), LDS_BYTES, st, x, M, g2, be2, eps,
-                       Wop, b1, b2, xo, gn, bn, xn, o, f, bo, (const float*)nullptr);
+    ffn_launch_nw<0, 1>(st, M, x, g2, be2, eps, Wop, b1, b2, xo, gn, bn, xn, o, f, bo, nullptr);
     PFM_LAUNCH_CHECK();
     return hipSuccess;
 }

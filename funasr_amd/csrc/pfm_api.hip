@@ -157,9 +157,11 @@ void pfm_knobs_refresh() {
     k.dec_subbatch = std::max(1, iv("PFM_DEC_SUBBATCH", 1));
     k.ffn_op = iv("PFM_FFN_OP", 1) != 0;
     k.dec_ffn_fused = iv("PFM_DEC_FFN_FUSED", 1) != 0;
+    k.ffn_hr = iv("PFM_FFN_HR", 1) != 0;
+    k.ffn_pd = iv("PFM_FFN_PD", 3) == 2 ? 2 : 3;
     const int* f = &k.ln_fold;
     unsigned long long s = 1469598103934665603ull;   // FNV-1a over the fields
-    for (int i = 0; i < 24; ++i) s = (s ^ (unsigned long long)(unsigned)f[i]) * 1099511628211ull;
+    for (int i = 0; i < 26; ++i) s = (s ^ (unsigned long long)(unsigned)f[i]) * 1099511628211ull;
     k.sig = s;
     t_knobs = k;
 }

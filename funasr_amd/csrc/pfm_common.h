@@ -159,6 +159,8 @@ struct PfmKnobs {
     int dec_subbatch;       // PFM_DEC_SUBBATCH (default 1): decoder utterance groups on concurrent streams
     int ffn_op;             // PFM_FFN_OP (default 1): encoder out-projection folded into the fused FFN kernel
     int dec_ffn_fused;      // PFM_DEC_FFN_FUSED (default 1): decoder LN1-FFN(LN_F folded)-LN kernel (fast mode)
+    int ffn_hr;             // PFM_FFN_HR (default 1): fused FFN phase 0/2 activation fragments read once per k step
+    int ffn_pd;             // PFM_FFN_PD (default 3): fused FFN weight tiles in flight behind the published one (2 or 3)
     unsigned long long sig;
 };
 const PfmKnobs& pfm_knobs();

@@ -284,11 +284,14 @@ def _ffn_ref(x, g2, b2n, eps, W1b, b1, W2b, b2):
 
 @pytest.mark.parametrize("M", [64, 200, 1000])
 @pytest.mark.parametrize("with_next", [False, True])
-def test_ffn_fused(dev, M, with_next):
+@pytest.mark.parametrize("hr", ["1", "0"])
+def test_ffn_fused(dev, M, with_next, hr, monkeypatch):
     """Fused LN2 -> W1 -> relu -> W2 -> residual (-> next LN, bf16) vs fp64 torch on the same bf16 weights:
     FFN increment (y - x) within rel-L2 5e-3 (f32 accumulation order flips a few bf16 roundings of the
     hidden activation), y within rel 1e-4; the next-layer LayerNorm of the kernel's own y within 1.6e-2
-    abs (one bf16 ulp at |v| <= 4); rows beyond M untouched by construction (ragged M)."""
+    abs (one bf16 ulp at |v| <= 4); rows beyond M untouched by construction (ragged M). With and without
+    the phase-2 activation-fragment reuse (PFM_FFN_HR)."""
+    monkeypatch.setenv("PFM_FFN_HR", hr)
     g = torch.Generator().manual_seed(M + 7 * with_next)
     x = torch.randn(M, 512, generator=g) * 2
     g2 = 1 + 0.1 * torch.randn(512, generator=g)

@@ -310,3 +310,24 @@ def test_fast_fused_ffn_matches_unfused(engines, monkeypatch):
     print(f"fused vs unfused FFN: encoder rel-L2 {relerr:.2e}; vs exact: fused {e1:.2e}, unfused {e0:.2e}")
     assert relerr < 1e-2
     assert e1 <= 1.1 * e0
+
+
+def test_fast_ffn_schedule_variants_are_bit_identical(engines, monkeypatch):
+    """PFM_FFN_HR=1 (default) lets the second 256-row half of each phase-0 / phase-2 k step reuse the first
+    half's activation fragments from registers instead of re-reading the same LDS bytes; PFM_FFN_PD=3
+    (default) keeps all four weight-ring slots streaming instead of three. Both change only the schedule:
+    the MFMAs see identical operands in identical order, so encoder output and tokens are bit-identical."""
+    e = engines["large"]
+    g = np.load(f"{GOLD}/para_large_b4.npz")
+    x, l = fbank_input(int(g["seed"]), 24, int(g["T"]), [int(g["T"])] * 24)   # M = 12,000 rows: fused path
+    xs, ls = torch.from_numpy(x).cuda(), torch.from_numpy(l).cuda()
+    r1 = e.run(xs, ls, mode="fast", want_enc=True)
+    torch.cuda.synchronize()
+    for knob in ("PFM_FFN_HR", "PFM_FFN_PD"):   # fragment reuse off; ring prefetch depth 2 instead of 3
+        monkeypatch.setenv(knob, "0" if knob == "PFM_FFN_HR" else "2")
+        r0 = e.run(xs, ls, mode="fast", want_enc=True)
+        torch.cuda.synchronize()
+        monkeypatch.delenv(knob)
+        assert torch.equal(r1["enc"], r0["enc"]), knob
+        assert torch.equal(r1["ntok"], r0["ntok"]), knob
+        assert _tokens_from_run(r1, e.cfg) == _tokens_from_run(r0, e.cfg), knob
