@@ -319,11 +319,12 @@ def main():
     # HBM bytes per launch of the same kernel set from the committed PMC passes (rocprofv3 --pmc FETCH_SIZE /
     # WRITE_SIZE, separate runs of this bench, gfx950-corrected by tools/pmc_traffic.py); null when absent
     traffic, traffic_src = None, None
-    tpath = os.path.join(ROOT, "profiles", "r02_gemm_traffic.json")
-    if args.mode == "fast" and os.path.exists(tpath):
-        with open(tpath) as f:
+    tname = next((n for n in ("r02b_gemm_traffic.json", "r02_gemm_traffic.json")
+                  if os.path.exists(os.path.join(ROOT, "profiles", n))), None)
+    if args.mode == "fast" and tname:
+        with open(os.path.join(ROOT, "profiles", tname)) as f:
             traffic = round(json.load(f)["hbm_bytes_per_launch"])
-        traffic_src = ("profiles/r02_gemm_traffic.json (PMC FETCH_SIZE x2 + WRITE_SIZE per launch of the GEMM "
+        traffic_src = (f"profiles/{tname} (PMC FETCH_SIZE x2 + WRITE_SIZE per launch of the GEMM "
                        "class: bf16 GEMMs + fused FFN)")
     roofline = {"bound": "mfma",
                 "kernel": ("gemm_bf16_kernel (QKV / out-proj / decoder / vocabulary) + ffn_fused_kernel (encoder "

@@ -1126,6 +1126,9 @@ int pick_cfg(int M, int N, int K, bool amax) {
     }
     if (amax) return big >= 512 ? 15 : 4;
     if (N <= 512 && K % 128 == 0 && K >= 1024 && big >= 120) return 17;
+    // =4 / =5: the 8-phase schedule (C17 on 16x16x32 / C13 on 32x32x16) also for the >= 256-tile grids
+    // (QKV, memory K|V) — A/B of the one-barrier kernel's 1.48-round QKV grid
+    if ((p == 4 || p == 5) && big >= 256 && K % 128 == 0) return p == 4 ? 17 : 13;
     if (big >= 256) return 15;
     if (N <= 512 && big < 120 && p != 3) return 3;   // decoder-sized M: 128x128 tiles fill more CUs
     return 4;

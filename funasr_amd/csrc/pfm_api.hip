@@ -154,7 +154,7 @@ void pfm_knobs_refresh() {
     k.ffn_var = iv("PFM_FFN_VAR", 0);
     k.exact_x6 = iv("PFM_EXACT_X6", 1) != 0;
     k.attn_var = iv("PFM_ATTN_VAR", 0);
-    k.dec_subbatch = std::max(1, iv("PFM_DEC_SUBBATCH", 1));
+    k.dec_subbatch = std::max(1, iv("PFM_DEC_SUBBATCH", 2));
     k.ffn_op = iv("PFM_FFN_OP", 1) != 0;
     k.dec_ffn_fused = iv("PFM_DEC_FFN_FUSED", 1) != 0;
     k.ffn_hr = iv("PFM_FFN_HR", 1) != 0;
@@ -1540,8 +1540,9 @@ int pfm_run(pfm_handle* h, void* stream, int mode, const float* feats, const int
         }
         return PFM_OK;
     };
-    // PFM_DEC_SUBBATCH=n: utterance groups on concurrent streams (default 1: two groups measured equal to
-    // one, 23.5-24.0 ms/step either way, tools/bench_ab.py)
+    // PFM_DEC_SUBBATCH=n: utterance groups on concurrent streams (default 2: with the fused decoder FFN kernels
+    // the two groups overlap, 19.74 vs 19.90 ms/step in three interleaved rounds of tools/bench_ab.py; before
+    // the FFN fusion they measured equal, 23.5-24.0 ms/step either way)
     const int ng = std::max(1, std::min({pfm_knobs().dec_subbatch, (int)pfm_handle::MAXSUB, B, h->prof_on ? 1 : 64}));
     (void)Ml;
     if (ng == 1) {

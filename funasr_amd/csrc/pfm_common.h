@@ -156,7 +156,7 @@ struct PfmKnobs {
     int ffn_var;            // PFM_FFN_VAR: diagnostic variants of the fused FFN kernel (0 = the kernel)
     int exact_x6;           // PFM_EXACT_X6 (default 1): EXACT-mode GEMMs as split bf16 x6 MFMA (f32 MFMA if 0)
     int attn_var;           // PFM_ATTN_VAR: diagnostic variants of the 8-wave bf16 attention kernel (0 = the kernel)
-    int dec_subbatch;       // PFM_DEC_SUBBATCH (default 1): decoder utterance groups on concurrent streams
+    int dec_subbatch;       // PFM_DEC_SUBBATCH (default 2): decoder utterance groups on concurrent streams
     int ffn_op;             // PFM_FFN_OP (default 1): encoder out-projection folded into the fused FFN kernel
     int dec_ffn_fused;      // PFM_DEC_FFN_FUSED (default 1): decoder LN1-FFN(LN_F folded)-LN kernel (fast mode)
     int ffn_hr;             // PFM_FFN_HR (default 1): fused FFN phase 0/2 activation fragments read once per k step

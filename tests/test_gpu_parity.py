@@ -117,10 +117,11 @@ def test_large_exact_tokens(engines, name):
 
 
 @pytest.mark.parametrize("name", ["para_large_ragged", "para_large_b4"])
-@pytest.mark.parametrize("env", [{"PFM_DEC_SUBBATCH": "2"}, {"PFM_SUBBATCH": "1", "PFM_DEC_SUBBATCH": "2"}])
+@pytest.mark.parametrize("env", [{"PFM_DEC_SUBBATCH": "1"}, {"PFM_SUBBATCH": "1", "PFM_DEC_SUBBATCH": "1"},
+                                 {"PFM_SUBBATCH": "1", "PFM_DEC_SUBBATCH": "2"}])
 def test_large_exact_tokens_grouped_decoder(engines, monkeypatch, name, env):
     """The decoder as utterance groups on concurrent streams (offset row pointers, one argmax reduction
-    after the join) stays token-exact."""
+    after the join; the default, PFM_DEC_SUBBATCH=2) and as one group stays token-exact."""
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     e = engines["large"]

@@ -6,7 +6,7 @@ set -o pipefail
 out=$1
 R=$(pwd)
 mkdir -p "$R/gpurun_out/pmc_traffic"
-export PFM_SUBBATCH=1
+export PFM_SUBBATCH=1 PFM_DEC_SUBBATCH=1   # the roofline pass runs single-stream (profiling on)
 cd /tmp && export TMPDIR=/tmp
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d "$R/gpurun_out/pmc_traffic/f" -o run -- \
   python3 "$R/bench.py" --steps 3 --warmup 1 --exact-steps 0 --cpu-utts 0 --sv-steps 0 --stream-chunks 0 --punc-steps 0 --long-audio-s 0 > "$R/gpurun_out/pmc_traffic/f.log" 2>&1 &&
