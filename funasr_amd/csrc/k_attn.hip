@@ -489,15 +489,34 @@ __device__ __forceinline__ void fsmn_epilogue(const AttnArgs& a, unsigned char* 
     const bf16* V = (const bf16*)a.v;
     unsigned char* xs = smem;
     float* ws = (float*)(smem + FR * RB);
-    for (int i = threadIdx.x; i < FR * (DK / 8); i += NTH) {
+    // every V-window and tap load of the thread is issued before its first LDS store (one memory latency
+    // for the whole staging instead of one per loop trip)
+    constexpr int NV = FR * (DK / 8), ITV = (NV + NTH - 1) / NTH;
+    constexpr int NW4 = FK * (DK / 4), ITW = (NW4 + NTH - 1) / NTH;
+    uint4 vv[ITV];
+    float4 wv[ITW];
+#pragma unroll
+    for (int j = 0; j < ITV; ++j) {
+        const int i = threadIdx.x + j * NTH;
         const int r = i / (DK / 8), ch = i % (DK / 8), t = t0 - FL + r;
-        uint4 v = make_uint4(0, 0, 0, 0);
-        if (t >= 0 && t < klen) v = *(const uint4*)(V + a.vmap.off((long long)b * a.Tk + t) + h * DK + ch * 8);
-        *(uint4*)(xs + r * RB + ch * 16) = v;
+        vv[j] = make_uint4(0, 0, 0, 0);
+        if (i < NV && t >= 0 && t < klen) vv[j] = *(const uint4*)(V + a.vmap.off((long long)b * a.Tk + t) + h * DK + ch * 8);
     }
-    for (int i = threadIdx.x; i < FK * (DK / 4); i += NTH) {
+#pragma unroll
+    for (int j = 0; j < ITW; ++j) {
+        const int i = threadIdx.x + j * NTH;
         const int k = i / (DK / 4), c4 = i % (DK / 4);
-        *(float4*)(ws + k * DK + c4 * 4) = *(const float4*)(a.fw + (long long)k * a.fD + h * DK + c4 * 4);
+        if (i < NW4) wv[j] = *(const float4*)(a.fw + (long long)k * a.fD + h * DK + c4 * 4);
+    }
+#pragma unroll
+    for (int j = 0; j < ITV; ++j) {
+        const int i = threadIdx.x + j * NTH;
+        if (i < NV) *(uint4*)(xs + (i / (DK / 8)) * RB + (i % (DK / 8)) * 16) = vv[j];
+    }
+#pragma unroll
+    for (int j = 0; j < ITW; ++j) {
+        const int i = threadIdx.x + j * NTH;
+        if (i < NW4) *(float4*)(ws + (i / (DK / 4)) * DK + (i % (DK / 4)) * 4) = wv[j];
     }
     __syncthreads();
     const int rb = threadIdx.x / (DK / 8), c8 = (threadIdx.x % (DK / 8)) * 8;
