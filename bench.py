@@ -238,10 +238,14 @@ def main():
         sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; launch N>1 as "
                  f"python -m torch.distributed.run --nproc-per-node {args.gpus} --master-addr 127.0.0.1 "
                  f"bench.py --gpus {args.gpus}")
+    # one rank per GPU over RCCL ("nccl"). PFM_DIST_BACKEND=gloo with more ranks than GPUs (ranks share a device:
+    # local rank mod device count) rehearses the N > 1 code path on a one-GPU box; it is never a measurement.
+    backend = os.environ.get("PFM_DIST_BACKEND", "nccl")
+    gpu = local % max(1, torch.cuda.device_count()) if backend == "gloo" else local
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
-    dev = torch.device("cuda", local)
+        torch.cuda.set_device(gpu)
+        dist.init_process_group(backend)
+    dev = torch.device("cuda", gpu)
     cfg = paraformer_large()
     B, T = args.batch, args.frames
 
@@ -251,7 +255,7 @@ def main():
         sd = broadcast_state_dict(param_layout(cfg), make_weights(cfg, args.seed) if rank == 0 else None, device=dev)
     else:
         sd = make_weights(cfg, args.seed)
-    eng = PfmEngine(cfg, local)
+    eng = PfmEngine(cfg, gpu)
     eng.load_state_dict(sd)
     eng.reserve(B, T)
     t_setup = time.time() - t0
@@ -395,7 +399,7 @@ def main():
     if rank == 0 and args.sv_steps > 0:
         from funasr_amd.config import sense_voice_small
         scfg = sense_voice_small()
-        seng = PfmEngine(scfg, local)
+        seng = PfmEngine(scfg, gpu)
         seng.load_state_dict(make_weights(scfg, args.seed))
         seng.reserve(B, T + 4)
         q = [0, 1, 2, 15]   # language auto, event, emotion, woitn
