@@ -1044,6 +1044,7 @@ using C14 = Cfg<256, 256, 2, 4, 32, 4, 3>;  // k-step phases, BK 32 x 4 buffers
 using C15 = Cfg<256, 256, 2, 4, 64, 2, 0, 1>;  // C1 on v_mfma_f32_16x16x32_bf16
 using C16 = Cfg<128, 256, 2, 4, 32, 3, 0, 1>;  // C4 on v_mfma_f32_16x16x32_bf16
 using C17 = Cfg<256, 256, 2, 4, 64, 2, 2, 1>;  // 8-phase schedule on v_mfma_f32_16x16x32_bf16 (K % 128 == 0)
+using C18 = Cfg<256, 256, 2, 4, 32, 4, 0, 1>;  // C15 as BK 32 x 4 stages: two 32-deep stages in flight behind the read one
 
 template <class C, int LN = 0>
 hipError_t launch(const void* A, RowMap amap, const void* W, long long ldw, int M, int N, int K, const GemmEpi& e2,
@@ -1104,7 +1105,7 @@ hipError_t launch_persist(const void* A, RowMap amap, const void* W, long long l
 
 int pick_cfg(int M, int N, int K, bool amax) {
     const int f = pfm_knobs().gemm_cfg;   // PFM_GEMM_CFG (per call): lets one process A/B configurations
-    if (f >= 1 && f <= 17) return f;
+    if (f >= 1 && f <= 18) return f;
     // Default (measured on the path, tools/bench_ab.py with the two concurrent encoder groups: 24.2 vs
     // 25.0-25.3 ms/step for the policies below). Grids are counted in 256x256 tiles; each encoder group
     // sees half the batch's rows:
@@ -1365,7 +1366,10 @@ hipError_t pfm_gemm_bf16_256(const void* A, RowMap amap, const void* W, long lon
     // (EXACT mode x6 GEMMs keep the fast-mode tiles: C17 for N >= 1024 and C16 for 512-wide x6 GEMMs were
     // faster in isolation — tools/gemm_cfg_scan.py SCAN_X6=1 — but slower on the two-group path, 99.3 and
     // 104.8 vs 98.0 ms/step; unsplit, C17 for the wide ones 100.9 vs 101.3, both 111.6)
-    if (epi.x6_k && cfg != 1 && cfg != 3 && cfg != 4 && cfg != 13 && cfg != 15 && cfg != 16 && cfg != 17) cfg = 15;
+    // PFM_GEMM_POLICY=6: C18 wherever the policy picks C15 (deeper LDS-DMA prefetch A/B)
+    if (pfm_knobs().gemm_policy == 6 && cfg == 15 && !ln) cfg = 18;
+    if (epi.x6_k && cfg != 1 && cfg != 3 && cfg != 4 && cfg != 13 && cfg != 15 && cfg != 16 && cfg != 17 && cfg != 18)
+        cfg = 15;
     if (epi.x6_k && (K != 6 * epi.x6_k || epi.x6_k % 64 || ln)) return hipErrorInvalidValue;
     switch (cfg) {
         case 2: return launch<C2>(A, amap, W, ldw, M, N, K, e2, st);
@@ -1386,6 +1390,7 @@ hipError_t pfm_gemm_bf16_256(const void* A, RowMap amap, const void* W, long lon
                  return launch<C1>(A, amap, W, ldw, M, N, K, e2, st);
         case 14: return launch<C14>(A, amap, W, ldw, M, N, K, e2, st);
         case 16: return launch<C16>(A, amap, W, ldw, M, N, K, e2, st);
+        case 18: return launch<C18>(A, amap, W, ldw, M, N, K, e2, st);
         case 17: if (K % 128 == 0) return launch_ln<C17>(A, amap, W, ldw, M, N, K, e2, st);
                  return launch_ln<C15>(A, amap, W, ldw, M, N, K, e2, st);
         case 1: return launch<C1>(A, amap, W, ldw, M, N, K, e2, st);

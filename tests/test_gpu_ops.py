@@ -41,7 +41,7 @@ def test_gemm_f32(dev, M, N, K):
     assert err < 1e-4
 
 
-@pytest.mark.parametrize("cfg", ["0", "1", "2", "3", "4", "5", "6", "7", "8", "9", "10", "11", "12", "13", "14", "15", "16", "17"])
+@pytest.mark.parametrize("cfg", ["0", "1", "2", "3", "4", "5", "6", "7", "8", "9", "10", "11", "12", "13", "14", "15", "16", "17", "18"])
 @pytest.mark.parametrize("M,N,K", [(300, 1536, 560), (77, 8404, 512), (1000, 512, 2048), (513, 1024, 1536),
                                    (256, 256, 64), (4000, 2048, 512), (2000, 768, 96), (600, 256, 32)])
 @pytest.mark.parametrize("epi", ["none", "bias_res", "bias_res_pre", "bias_res_nobatch", "bias_relu_res",
