@@ -342,29 +342,58 @@ __global__ __launch_bounds__(64 * NW) void ffn_fused_kernel(const float* __restr
         // [col 32w + 16nb + 4g + e (+256 for b)]; LN2 row statistics: lane partials -> 4 g lanes -> 8 waves
         float* red = (float*)(smem + OFF_H);   // [2][8 waves][64 rows] (the H image is free until chunk 0)
         float part[4] = {0.f, 0.f, 0.f, 0.f};
+        // Addend loads are branch-free (a null X / Fr reads a valid stand-in and is selected away) and issued
+        // in two batches of 8 row fragments, so a batch costs one memory latency: with the loads behind
+        // per-fragment `if`s the compiler drained vmcnt(0) before every one (16 serial round trips).
+        const bool hx = X != nullptr, hf_ = Fr != nullptr;
+        const float* xs = hx ? X : bo;
+        const long long xst = hx ? FD : 0;
+        const bf16* fs = hf_ ? Fr : O;
+        float4 bv[2][HB];
 #pragma unroll
-        for (int mb = 0; mb < 4; ++mb) {
-            const long long row = min(m0 + 16 * mb + r16, (long long)M - 1);
+        for (int hf = 0; hf < 2; ++hf)
 #pragma unroll
-            for (int hf = 0; hf < 2; ++hf)
+            for (int nb = 0; nb < HB; ++nb) bv[hf][nb] = *(const float4*)(bo + 256 * hf + WR * w + 16 * nb + 4 * g);
 #pragma unroll
-                for (int nb = 0; nb < HB; ++nb) {
-                    const int n = 256 * hf + WR * w + 16 * nb + 4 * g;
-                    f32x4& a = hf ? acc2b[nb][mb] : acc2a[nb][mb];
-                    const float4 bb4 = *(const float4*)(bo + n);
-                    float4 x4 = make_float4(0.f, 0.f, 0.f, 0.f);
-                    if (X) x4 = *(const float4*)(X + row * FD + n);
-                    a[0] += bb4.x; a[1] += bb4.y; a[2] += bb4.z; a[3] += bb4.w;
-                    if (Fr) {
-                        const bf16x4 f4 = *(const bf16x4*)(Fr + row * FD + n);
-                        a[0] += bf2f(f4[0]); a[1] += bf2f(f4[1]); a[2] += bf2f(f4[2]); a[3] += bf2f(f4[3]);
+        for (int mh = 0; mh < 2; ++mh) {
+            float4 xv[2][2][HB];
+            bf16x4 fv[2][2][HB];
+#pragma unroll
+            for (int mi = 0; mi < 2; ++mi) {
+                const long long row = min(m0 + 16 * (2 * mh + mi) + r16, (long long)M - 1);
+#pragma unroll
+                for (int hf = 0; hf < 2; ++hf)
+#pragma unroll
+                    for (int nb = 0; nb < HB; ++nb) {
+                        const int n = 256 * hf + WR * w + 16 * nb + 4 * g;
+                        xv[mi][hf][nb] = *(const float4*)(xs + row * xst + n);
+                        fv[mi][hf][nb] = *(const bf16x4*)(fs + row * FD + n);
                     }
-                    a[0] += x4.x; a[1] += x4.y; a[2] += x4.z; a[3] += x4.w;
-                    if constexpr (MODE == 3) {   // the decoder keeps x1 (the FSMN step adds it back)
-                        if (m0 + 16 * mb + r16 < M) *(float4*)(Xo + row * FD + n) = make_float4(a[0], a[1], a[2], a[3]);
+            }
+#pragma unroll
+            for (int mi = 0; mi < 2; ++mi) {
+                const int mb = 2 * mh + mi;
+                const long long row = min(m0 + 16 * mb + r16, (long long)M - 1);
+#pragma unroll
+                for (int hf = 0; hf < 2; ++hf)
+#pragma unroll
+                    for (int nb = 0; nb < HB; ++nb) {
+                        const int n = 256 * hf + WR * w + 16 * nb + 4 * g;
+                        f32x4& a = hf ? acc2b[nb][mb] : acc2a[nb][mb];
+                        const float4 bb4 = bv[hf][nb];
+                        const float4 x4 = hx ? xv[mi][hf][nb] : make_float4(0.f, 0.f, 0.f, 0.f);
+                        const bf16x4 f4 = fv[mi][hf][nb];
+                        a[0] += bb4.x; a[1] += bb4.y; a[2] += bb4.z; a[3] += bb4.w;
+                        if (hf_) {
+                            a[0] += bf2f(f4[0]); a[1] += bf2f(f4[1]); a[2] += bf2f(f4[2]); a[3] += bf2f(f4[3]);
+                        }
+                        a[0] += x4.x; a[1] += x4.y; a[2] += x4.z; a[3] += x4.w;
+                        if constexpr (MODE == 3) {   // the decoder keeps x1 (the FSMN step adds it back)
+                            if (m0 + 16 * mb + r16 < M) *(float4*)(Xo + row * FD + n) = make_float4(a[0], a[1], a[2], a[3]);
+                        }
+                        part[mb] += (a[0] + a[1]) + (a[2] + a[3]);
                     }
-                    part[mb] += (a[0] + a[1]) + (a[2] + a[3]);
-                }
+            }
         }
         auto row_reduce = [&](float (&v)[4], int slot) {
 #pragma unroll
@@ -397,6 +426,16 @@ __global__ __launch_bounds__(64 * NW) void ffn_fused_kernel(const float* __restr
                     for (int e = 0; e < 4; ++e) { const float d = a[e] - mean[mb]; q[mb] += d * d; }
                 }
         row_reduce(q, 1);
+        float4 gv[2][HB], bev[2][HB], c2v[2][HB];   // per-column constants, loaded once (not per row block)
+#pragma unroll
+        for (int hf = 0; hf < 2; ++hf)
+#pragma unroll
+            for (int nb = 0; nb < HB; ++nb) {
+                const int n = 256 * hf + WR * w + 16 * nb + 4 * g;
+                gv[hf][nb] = *(const float4*)(g2 + n);
+                bev[hf][nb] = *(const float4*)(be2 + n);
+                c2v[hf][nb] = MODE == 1 ? *(const float4*)(b2 + n) : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
 #pragma unroll
         for (int mb = 0; mb < 4; ++mb) {
             const int m = 16 * mb + r16;
@@ -407,12 +446,12 @@ __global__ __launch_bounds__(64 * NW) void ffn_fused_kernel(const float* __restr
                 for (int nb = 0; nb < HB; ++nb) {
                     const int n = 256 * hf + WR * w + 16 * nb + 4 * g;
                     f32x4& a = hf ? acc2b[nb][mb] : acc2a[nb][mb];
-                    const float4 gg = *(const float4*)(g2 + n), be = *(const float4*)(be2 + n);
+                    const float4 gg = gv[hf][nb], be = bev[hf][nb];
                     bf16x4 o = {f2bf((a[0] - mean[mb]) * rstd * gg.x + be.x), f2bf((a[1] - mean[mb]) * rstd * gg.y + be.y),
                                 f2bf((a[2] - mean[mb]) * rstd * gg.z + be.z), f2bf((a[3] - mean[mb]) * rstd * gg.w + be.w)};
                     *(bf16x4*)(smem + OFF_AN + m * 1024 + (((n >> 3) ^ (m & 15)) << 4) + ((n & 7) << 1)) = o;
                     if constexpr (MODE == 1) {   // encoder: x2 = (x1 + b2) + W2 . H
-                        const float4 c2 = *(const float4*)(b2 + n);
+                        const float4 c2 = c2v[hf][nb];
                         a[0] += c2.x; a[1] += c2.y; a[2] += c2.z; a[3] += c2.w;
                     } else {                      // decoder: the FFN output has no residual
                         a[0] = 0.f; a[1] = 0.f; a[2] = 0.f; a[3] = 0.f;
