@@ -123,9 +123,17 @@ static int fail(int code, const std::string& msg) {
             return fail(PFM_E_HIP, std::string(#expr) + ": " + hipGetErrorString(_e));           \
     } while (0)
 
-static thread_local PfmKnobs t_knobs = {0, 0, 1, 8, 0, 1, 0, 2, 1, 0, -1, 0, 0, 1, 0, 1, 1, 1, 0, 1, 0, 0, 1, 1, 1};
+// Every field is an int; the FNV hash below walks them all. A thread that reads the knobs before any
+// C-ABI entry point refreshed them gets the documented defaults (lazy first refresh), never zero-fill.
+static_assert(sizeof(PfmKnobs) == (PFM_KNOB_FIELDS * sizeof(int) + 7) / 8 * 8 + sizeof(unsigned long long),
+              "PfmKnobs: PFM_KNOB_FIELDS int fields + sig");
+static thread_local PfmKnobs t_knobs;
+static thread_local bool t_knobs_set = false;
 
-const PfmKnobs& pfm_knobs() { return t_knobs; }
+const PfmKnobs& pfm_knobs() {
+    if (!t_knobs_set) pfm_knobs_refresh();
+    return t_knobs;
+}
 
 void pfm_knobs_refresh() {
     auto iv = [](const char* name, int dflt) {
@@ -161,9 +169,10 @@ void pfm_knobs_refresh() {
     k.ffn_pd = iv("PFM_FFN_PD", 3) == 2 ? 2 : 3;
     const int* f = &k.ln_fold;
     unsigned long long s = 1469598103934665603ull;   // FNV-1a over the fields
-    for (int i = 0; i < 26; ++i) s = (s ^ (unsigned long long)(unsigned)f[i]) * 1099511628211ull;
+    for (int i = 0; i < PFM_KNOB_FIELDS; ++i) s = (s ^ (unsigned long long)(unsigned)f[i]) * 1099511628211ull;
     k.sig = s;
     t_knobs = k;
+    t_knobs_set = true;
 }
 
 namespace {
@@ -507,6 +516,23 @@ int ensure_x6(pfm_handle* h, hipStream_t st) {
     HIP_TRY(h->arena_x6.ensure(3 * n * sizeof(bf16)));
     for (auto& r : h->gemm_ranges)
         HIP_TRY(pfm_split3_planes(h->w(r.first), h->arena_x6.as<bf16>() + r.first, (long long)n, (long long)r.second, st));
+    // weights whose K is not a multiple of the kernel's 64-deep step (the input_size-wide layer-0 QKV): zero-padded
+    // planes [N][3 Kp], built here on the caller's stream BEFORE any utterance-group stream forks from it (the
+    // fork event orders every group after them). The buffers are kept across weight reloads and re-split in
+    // place, so their addresses (held by captured streaming graphs) stay valid.
+    for (auto& L : h->enc) {
+        const int K = L.din, N = 3 * h->cfg.d_model;
+        if (K % 64 == 0) continue;
+        const int Kp = (K + 63) / 64 * 64;
+        auto& pb = h->x6_pad[L.wqkv];
+        if (!pb) {
+            pb.reset(new DevBuf());
+            pb->gen = &h->buf_gen;
+        }
+        HIP_TRY(pb->ensure((size_t)N * Kp * 3 * sizeof(bf16)));
+        // rows of W [N][K] -> [N][3 Kp] (x0 | x1 | x2), read by gemm_x6 as three [N][Kp] planes
+        HIP_TRY(pfm_split3_rows(h->w(L.wqkv), rowmap_plain(K), N, K, Kp, pb->as<bf16>(), st));
+    }
     h->x6_ready = true;
     return PFM_OK;
 }
@@ -701,22 +727,11 @@ hipError_t gemm_x6(pfm_handle* h, const float* A, RowMap am, const float* W, int
     const size_t off = (size_t)(W - h->arena.as<float>());
     const bf16* planes = h->arena_x6.as<bf16>() + off;
     long long ws = (long long)h->arena_elems;
-    if (Kp != K) {   // padded planes of this weight, built on first use (outside any graph capture)
-        auto& pb = h->x6_pad[off];
-        if (!pb) {
-            hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-            hipError_t e0 = hipStreamIsCapturing(s, &cs);
-            if (e0 != hipSuccess) return e0;
-            if (cs != hipStreamCaptureStatusNone) return hipErrorStreamCaptureUnsupported;
-            pb.reset(new DevBuf());
-            pb->gen = &h->buf_gen;
-            e0 = pb->ensure((size_t)N * Kp * 3 * sizeof(bf16));
-            if (e0 != hipSuccess) return e0;
-            // rows of W [N][K] -> [N][3 Kp] (x0 | x1 | x2), then regroup as three [N][Kp] planes below
-            e0 = pfm_split3_rows(W, rowmap_plain(K), N, K, Kp, pb->as<bf16>(), s);
-            if (e0 != hipSuccess) return e0;
-        }
-        planes = pb->as<bf16>();
+    if (Kp != K) {   // padded planes of this weight (ensure_x6 built them on the caller's stream)
+        auto it = h->x6_pad.find(off);
+        if (it == h->x6_pad.end() || !it->second || it->second->bytes < (size_t)N * Kp * 3 * sizeof(bf16))
+            return hipErrorInvalidValue;
+        planes = it->second->as<bf16>();
         ws = Kp;   // plane p of row n at n * 3Kp + p * Kp: ldw = 3 Kp, plane stride Kp
     }
     const size_t need = (size_t)M * 3 * Kp * sizeof(bf16);
@@ -1240,8 +1255,7 @@ int pfm_set_weight(pfm_handle* h, const char* name, const void* host_ptr, int dt
     h->fold_ready = false;
     h->ffn_ready = false;
     h->dffn_ready = false;
-    h->x6_ready = false;
-    h->x6_pad.clear();
+    h->x6_ready = false;   // ensure_x6 re-splits arena_x6 and the padded planes in place (stable addresses)
     h->ban_tok = -1;   // the banned-token bias copy follows ctc.ctc_lo.bias
     return PFM_OK;
 }
@@ -1770,26 +1784,113 @@ int pfm_op_gemm(void* stream, int dtype, const void* A, const void* Wt, const fl
     return PFM_OK;
 }
 
+}  // extern "C"
+
+// scratch device buffers of one single-op call, freed on every return path
+struct OpScratch {
+    std::vector<void*> ptrs;
+    OpScratch() = default;
+    OpScratch(const OpScratch&) = delete;
+    OpScratch& operator=(const OpScratch&) = delete;
+    ~OpScratch() { for (void* p : ptrs) (void)hipFree(p); }
+    template <typename T> hipError_t alloc(T** p, size_t n) {
+        void* q = nullptr;
+        hipError_t e = hipMalloc(&q, n * sizeof(T));
+        if (e == hipSuccess) { ptrs.push_back(q); *p = (T*)q; }
+        return e;
+    }
+};
+
+static bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+static bool all_aligned16(std::initializer_list<const void*> ps) {
+    for (const void* p : ps) if (!aligned16(p)) return false;
+    return true;
+}
+
+extern "C" {
+
 int pfm_op_ffn(void* stream, const float* x, int M, const float* g2, const float* b2n, float eps, const float* W1,
                const float* b1, const float* W2, const float* b2, float* xo, const float* gn, const float* bn,
                void* xn) {
     pfm_knobs_refresh();
-    if (!x || !xo || !W1 || !W2 || M < 0) return fail(PFM_E_ARG, "pfm_op_ffn: null operand");
+    if (!x || !xo || !W1 || !W2 || !g2 || !b2n || !b1 || !b2 || M < 0) return fail(PFM_E_ARG, "pfm_op_ffn: null operand");
+    if ((xn != nullptr) != (gn != nullptr && bn != nullptr)) return fail(PFM_E_ARG, "pfm_op_ffn: xn needs gn and bn");
+    if (!all_aligned16({x, xo, g2, b2n, b1, b2, xn, gn, bn})) return fail(PFM_E_ARG, "pfm_op_ffn: operands must be 16-B aligned");
     const hipStream_t st = (hipStream_t)stream;
     const size_t nw = (size_t)2048 * 512;
-    bf16 *w1b = nullptr, *w2b = nullptr, *wp = nullptr;
-    HIP_TRY(hipMalloc(&w1b, nw * sizeof(bf16)));
-    HIP_TRY(hipMalloc(&w2b, nw * sizeof(bf16)));
-    HIP_TRY(hipMalloc(&wp, pfm_ffn_packed_elems() * sizeof(bf16)));
-    hipError_t e = pfm_f32_to_bf16(W1, w1b, (long long)nw, st);
-    if (e == hipSuccess) e = pfm_f32_to_bf16(W2, w2b, (long long)nw, st);
-    if (e == hipSuccess) e = pfm_ffn_pack(w1b, w2b, wp, st);
-    if (e == hipSuccess) e = pfm_ffn_fused(x, M, g2, b2n, eps, wp, b1, b2, xo, gn, bn, (bf16*)xn, st);
-    if (e == hipSuccess) e = hipStreamSynchronize(st);
-    (void)hipFree(w1b);
-    (void)hipFree(w2b);
-    (void)hipFree(wp);
-    if (e != hipSuccess) return fail(PFM_E_HIP, std::string("pfm_op_ffn: ") + hipGetErrorString(e));
+    OpScratch sc;
+    bf16 *w1b, *w2b, *wp;
+    HIP_TRY(sc.alloc(&w1b, nw));
+    HIP_TRY(sc.alloc(&w2b, nw));
+    HIP_TRY(sc.alloc(&wp, pfm_ffn_packed_elems()));
+    HIP_TRY(pfm_f32_to_bf16(W1, w1b, (long long)nw, st));
+    HIP_TRY(pfm_f32_to_bf16(W2, w2b, (long long)nw, st));
+    HIP_TRY(pfm_ffn_pack(w1b, w2b, wp, st));
+    HIP_TRY(pfm_ffn_fused(x, M, g2, b2n, eps, wp, b1, b2, xo, gn, bn, (bf16*)xn, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    return PFM_OK;
+}
+
+int pfm_op_ffn_op(void* stream, const void* o, const void* f, const float* Wo, const float* bo, const float* x, int M,
+                  const float* g2, const float* b2n, float eps, const float* W1, const float* b1, const float* W2,
+                  const float* b2, float* xo, const float* gn, const float* bn, void* xn) {
+    pfm_knobs_refresh();
+    if (!o || !f || !Wo || !bo || !xo || !W1 || !W2 || !g2 || !b2n || !b1 || !b2 || M < 0)
+        return fail(PFM_E_ARG, "pfm_op_ffn_op: null operand");
+    if ((xn != nullptr) != (gn != nullptr && bn != nullptr)) return fail(PFM_E_ARG, "pfm_op_ffn_op: xn needs gn and bn");
+    if (!all_aligned16({o, f, bo, x, xo, g2, b2n, b1, b2, xn, gn, bn}))
+        return fail(PFM_E_ARG, "pfm_op_ffn_op: operands must be 16-B aligned");
+    const hipStream_t st = (hipStream_t)stream;
+    const size_t nw = (size_t)2048 * 512, no = (size_t)512 * 512, po = pfm_ffn_packed_o_elems();
+    OpScratch sc;
+    bf16 *w1b, *w2b, *wob, *wp;
+    HIP_TRY(sc.alloc(&w1b, nw));
+    HIP_TRY(sc.alloc(&w2b, nw));
+    HIP_TRY(sc.alloc(&wob, no));
+    HIP_TRY(sc.alloc(&wp, po + pfm_ffn_packed_elems()));
+    HIP_TRY(pfm_f32_to_bf16(W1, w1b, (long long)nw, st));
+    HIP_TRY(pfm_f32_to_bf16(W2, w2b, (long long)nw, st));
+    HIP_TRY(pfm_f32_to_bf16(Wo, wob, (long long)no, st));
+    HIP_TRY(pfm_ffn_pack_o(wob, wp, st));
+    HIP_TRY(pfm_ffn_pack(w1b, w2b, wp + po, st));
+    HIP_TRY(pfm_ffn_fused_op((const bf16*)o, (const bf16*)f, bo, x, M, g2, b2n, eps, wp, b1, b2, xo, gn, bn, (bf16*)xn,
+                             st));
+    HIP_TRY(hipStreamSynchronize(st));
+    return PFM_OK;
+}
+
+int pfm_op_ffn_dec(void* stream, const float* x, int M, const float* g1, const float* b1n, float eps, const float* W1,
+                   const float* b1, const float* W2, const float* gF, const float* bF, float* xo, const float* gn,
+                   const float* bn, void* xn, const void* o, const float* Wo, const float* bo) {
+    pfm_knobs_refresh();
+    if (!x || !W1 || !W2 || !g1 || !b1n || !b1 || !gF || !bF || !gn || !bn || !xn || M < 0)
+        return fail(PFM_E_ARG, "pfm_op_ffn_dec: null operand");
+    if (o && (!Wo || !bo || !xo)) return fail(PFM_E_ARG, "pfm_op_ffn_dec: o needs Wo, bo and xo");
+    if (!all_aligned16({x, g1, b1n, b1, gF, bF, xo, gn, bn, xn, o, bo}))
+        return fail(PFM_E_ARG, "pfm_op_ffn_dec: operands must be 16-B aligned");
+    const hipStream_t st = (hipStream_t)stream;
+    const size_t nw = (size_t)2048 * 512, no = (size_t)512 * 512, po = pfm_ffn_packed_o_elems();
+    OpScratch sc;
+    bf16 *w1b, *wob, *wp;
+    float* cc;
+    HIP_TRY(sc.alloc(&w1b, nw));
+    HIP_TRY(sc.alloc(&wob, no));
+    HIP_TRY(sc.alloc(&wp, po + pfm_ffn_packed_elems()));
+    HIP_TRY(sc.alloc(&cc, (size_t)2 * 512));
+    HIP_TRY(pfm_f32_to_bf16(W1, w1b, (long long)nw, st));
+    if (o) {
+        HIP_TRY(pfm_f32_to_bf16(Wo, wob, (long long)no, st));
+        HIP_TRY(pfm_ffn_pack_o(wob, wp, st));
+    }
+    HIP_TRY(pfm_ffn_pack_dec(w1b, W2, gF, bF, wp + po, cc, cc + 512, st));
+    if (o) {   // mode 3: x1 = x + o Wo^T + bo -> xo, then the FFN on x1 (x may alias xo)
+        HIP_TRY(pfm_ffn_fused_dec(x, M, g1, b1n, eps, wp, b1, cc, cc + 512, xo, gn, bn, (bf16*)xn, (const bf16*)o, bo,
+                                  st));
+    } else {
+        HIP_TRY(pfm_ffn_fused_dec(x, M, g1, b1n, eps, wp + po, b1, cc, cc + 512, xo, gn, bn, (bf16*)xn, nullptr,
+                                  nullptr, st));
+    }
+    HIP_TRY(hipStreamSynchronize(st));
     return PFM_OK;
 }
 

@@ -163,5 +163,6 @@ struct PfmKnobs {
     int ffn_pd;             // PFM_FFN_PD (default 3): fused FFN weight tiles in flight behind the published one (2 or 3)
     unsigned long long sig;
 };
-const PfmKnobs& pfm_knobs();
+#define PFM_KNOB_FIELDS 26
+const PfmKnobs& pfm_knobs();   // the calling thread's snapshot (refreshed lazily if no entry point did yet)
 void pfm_knobs_refresh();

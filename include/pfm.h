@@ -307,6 +307,27 @@ int pfm_op_ffn(void* stream, const float* x, int M, const float* g2, const float
                const float* b1, const float* W2, const float* b2, float* xo, const float* gn, const float* bn,
                void* xn);
 
+/* Fused encoder sub-layer tail as the fast path runs it (k_ffn.hip, out-projection folded in front):
+ *   x1 = o Wo^T + bo + f (+ x; x may be NULL: layer 0 has no residual)
+ *   xo = x1 + W2 relu(W1 LN2(x1) + b1) + b2 ;  xn = LN_next(xo) as bf16 (optional: gn, bn, xn all or none)
+ * o, f: bf16 [M, 512] (attention output, FSMN memory); x, xo: f32 [M, 512] (xo may alias x).
+ * Replaces sanm/encoder.py:120-145 (linear_out + fsmn + residual, norm2, feed_forward, residual) and
+ * transformer/positionwise_feed_forward.py:32-34. Weights f32 host layout [out][in] on the device; synchronous. */
+int pfm_op_ffn_op(void* stream, const void* o, const void* f, const float* Wo, const float* bo, const float* x,
+                  int M, const float* g2, const float* b2n, float eps, const float* W1, const float* b1,
+                  const float* W2, const float* b2, float* xo, const float* gn, const float* bn, void* xn);
+
+/* Fused decoder feed-forward as the fast path runs it (k_ffn.hip DEC, LN_F folded through W2):
+ *   x1 = x, or x + o Wo^T + bo when o is non-NULL (the previous block's cross-attention out-projection)
+ *   y  = W2 LN_F(relu(W1 LN1(x1) + b1))  (w_2 has no bias) ;  xn = LN_next(y) bf16
+ *   xo = x1 when o is non-NULL (may alias x), else y (optional)
+ * Replaces sanm/positionwise_feed_forward.py:12-33 with paraformer/decoder.py:97-101 (norm1 -> feed_forward ->
+ * norm2) and decoder.py:113-119 (src_attn linear_out + residual). Synchronous. */
+int pfm_op_ffn_dec(void* stream, const float* x, int M, const float* g1, const float* b1n, float eps,
+                   const float* W1, const float* b1, const float* W2, const float* gF, const float* bF,
+                   float* xo, const float* gn, const float* bn, void* xn, const void* o, const float* Wo,
+                   const float* bo);
+
 /* Masked attention per (batch, head): q [B*Tq, heads*128], k/v [B*Tk, heads*128] of dtype,
  * klen [B] int32; out f32 [B*Tq, heads*128]. */
 int pfm_op_attention(void* stream, int dtype, const void* q, const void* k, const void* v,

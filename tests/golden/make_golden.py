@@ -148,6 +148,37 @@ def save_large(m, name, seed, B, T, lens):
     print(name, "ntok", r["ntok"], "min margin", top2_margin(r["logp"], r["ntok"]).min())
 
 
+HEADLINE = {   # name: (seed, B, T, lens) — batches whose per-group row counts engage the fast path's fused
+    # encoder FFN (OP mode), fused decoder FFN and the two-group concurrent dispatch (bench config C2 = b64)
+    "para_large_b24": (6, 24, 500, [500 - 9 * i for i in range(24)]),
+    "para_large_b64": (7, 64, 500, None),
+}
+
+
+def save_headline():
+    """Paraformer-large reference run at the bench configuration (B=64 x T=500) and a B=24 ragged batch:
+    token ids, the per-position decoder argmax (incl. special ids) and top-2 log-prob margins, token counts,
+    alphas, three encoder rows per utterance and per-utterance encoder checksums."""
+    m = build_ref(paraformer_large())
+    for name, (seed, B, T, ln) in HEADLINE.items():
+        feats, lens = fbank_input(seed=seed, B=B, T=T, lens=ln)
+        r = run_ref(m, feats, lens)
+        flat, off = pack_tokens(r["tokens"])
+        enc = r["enc"]
+        rows = np.stack([enc[b, [0, int(lens[b]) // 2, int(lens[b]) - 1]] for b in range(B)])
+        valid = np.arange(T)[None, :] < lens[:, None]
+        csum = np.array([enc[b][valid[b]].astype(np.float64).sum() for b in range(B)])
+        csq = np.array([(enc[b][valid[b]].astype(np.float64) ** 2).sum() for b in range(B)])
+        am = np.concatenate([r["logp"][b, : r["ntok"][b]].argmax(-1) for b in range(B)]).astype(np.int32)
+        np.savez_compressed(f"{HERE}/{name}.npz", seed=seed, B=B, T=T, lens=lens, enc_rows=rows, enc_sum=csum,
+                            enc_sumsq=csq, enc_lens=r["enc_lens"], token_num=r["token_num"], alphas=r["alphas"],
+                            ntok=r["ntok"], tokens=flat, tokens_off=off, argmax=am,
+                            margin=top2_margin(r["logp"], r["ntok"]))
+        mg = top2_margin(r["logp"], r["ntok"])
+        print(name, "ntok mean", r["ntok"].mean(), "positions", len(mg), "min margin", mg.min(),
+              "margins < 1e-3:", int((mg < 1e-3).sum()))
+
+
 def save_lfr_cmvn():
     from funasr.frontends.wav_frontend import apply_cmvn, apply_lfr, load_cmvn
     cmvn = load_cmvn(CMVN).numpy()

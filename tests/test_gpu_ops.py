@@ -316,3 +316,97 @@ def test_ffn_fused(dev, M, with_next, hr, monkeypatch):
         assert (xn.double().cpu() - ln).abs().max().item() < 1.6e-2
     else:
         assert xn is None
+
+
+def _ln64(x, g, b, eps):
+    mu = x.mean(-1, keepdim=True)
+    var = ((x - mu) ** 2).mean(-1, keepdim=True)
+    return (x - mu) / torch.sqrt(var + eps) * g.double() + b.double()
+
+
+def _ffn_params(g, dec=False):
+    p = dict(W1=torch.randn(2048, 512, generator=g) / 512 ** 0.5, b1=0.1 * torch.randn(2048, generator=g),
+             W2=torch.randn(512, 2048, generator=g) / 2048 ** 0.5, g2=1 + 0.1 * torch.randn(512, generator=g),
+             b2n=0.1 * torch.randn(512, generator=g), gn=1 + 0.1 * torch.randn(512, generator=g),
+             bn=0.1 * torch.randn(512, generator=g), Wo=torch.randn(512, 512, generator=g) / 512 ** 0.5,
+             bo=0.1 * torch.randn(512, generator=g))
+    if dec:
+        p.update(gF=1 + 0.1 * torch.randn(2048, generator=g), bF=0.1 * torch.randn(2048, generator=g))
+    else:
+        p.update(b2=0.1 * torch.randn(512, generator=g))
+    return p
+
+
+@pytest.mark.parametrize("M", [64, 200, 1000, 4100])
+@pytest.mark.parametrize("resid", [True, False])
+def test_ffn_fused_outproj(dev, M, resid):
+    """The encoder sub-layer tail exactly as the fast path's default dispatch runs it (ffn_fused_kernel OP mode:
+    out-projection as phase 0, x1 in the accumulators, LN2 reduced across waves, FFN, next LN1) vs an fp64
+    restatement of sanm/encoder.py:120-145 on the kernel's bf16 operand roundings:
+      x1 = x + (o Wo^T + bo + f)   (layer 0: no x),  a = bf16(LN2(x1)),  h = bf16(relu(a W1^T + b1)),
+      x2 = x1 + h W2^T + b2,  xn = LN1_next(x2).
+    Tolerances: the FFN increment x2 - x1 rel-L2 < 5e-3 (f32 accumulation order flips a few bf16 roundings of
+    a / h), x2 rel < 1e-4, xn within 1.6e-2 abs of LN1_next of the kernel's own x2 (one bf16 ulp at |v| <= 4)."""
+    g = torch.Generator().manual_seed(31 * M + resid)
+    p = _ffn_params(g)
+    x = torch.randn(M, 512, generator=g) * 2 if resid else None
+    o = torch.randn(M, 512, generator=g).bfloat16()
+    f = (0.5 * torch.randn(M, 512, generator=g)).bfloat16()
+    d = lambda t: None if t is None else t.to(dev)  # noqa: E731
+    x2, xn = rt.op_ffn_op(d(o), d(f), d(p["Wo"]), d(p["bo"]), d(x), d(p["g2"]), d(p["b2n"]), 1e-12, d(p["W1"]),
+                          d(p["b1"]), d(p["W2"]), d(p["b2"]), d(p["gn"]), d(p["bn"]))
+    torch.cuda.synchronize()
+    x1 = o.double() @ p["Wo"].bfloat16().double().T + p["bo"].double() + f.double()
+    if resid:
+        x1 = x1 + x.double()
+    want = _ffn_ref(x1, p["g2"], p["b2n"], 1e-12, p["W1"].bfloat16(), p["b1"], p["W2"].bfloat16(), p["b2"])
+    yc = x2.double().cpu()
+    assert rel(yc - x1, want - x1) < 5e-3
+    assert rel(yc, want) < 1e-4
+    ln = _ln64(yc, p["gn"], p["bn"], 1e-12)
+    assert (xn.double().cpu() - ln).abs().max().item() < 1.6e-2
+
+
+def _dec_ffn_ref(x1, p, eps=1e-12):
+    """fp64 sanm/positionwise_feed_forward.py:26-33 on the kernel's roundings: a = bf16(LN1(x1)),
+    h = bf16(relu(a W1^T + b1)); LN_F over the 2048 hidden folded through W2 with W2g = bf16(W2 diag(gamma_F)):
+    y = rstd (h W2g^T - mu rowsum(W2g)) + W2 beta_F (= W2 LN_F(h) up to the rounding of W2 gamma_F)."""
+    a = _ln64(x1, p["g2"], p["b2n"], eps).bfloat16().double()
+    h = torch.relu(a @ p["W1"].bfloat16().double().T + p["b1"].double()).bfloat16().double()
+    mu = h.mean(-1, keepdim=True)
+    rstd = 1.0 / torch.sqrt(((h - mu) ** 2).mean(-1, keepdim=True) + eps)
+    w2g = (p["W2"] * p["gF"][None, :]).bfloat16().double()
+    y = rstd * (h @ w2g.T - mu * w2g.sum(-1)[None, :]) + (p["W2"].double() @ p["bF"].double())[None, :]
+    exact = (_ln64(h, p["gF"], p["bF"], eps)) @ p["W2"].double().T   # no W2 / gamma rounding
+    return y, exact
+
+
+@pytest.mark.parametrize("M", [64, 200, 1000, 4100])
+@pytest.mark.parametrize("outproj", [False, True])
+def test_ffn_fused_decoder(dev, M, outproj):
+    """The decoder FFN exactly as the fast path runs it (ffn_fused_kernel DEC: LN1 prologue, LN_F folded through
+    W2, next LayerNorm epilogue; with outproj the previous block's cross-attention out-projection as phase 0,
+    x1 = x + o Wo^T + bo written back) vs fp64 on the kernel's bf16 roundings: y rel-L2 < 5e-3 (and < 2e-2 vs
+    the unrounded W2 LN_F(h)), xn within 1.6e-2 of LN_next of the fp64 y plus the y error; x1 rel < 1e-6."""
+    g = torch.Generator().manual_seed(17 * M + outproj)
+    p = _ffn_params(g, dec=True)
+    x = torch.randn(M, 512, generator=g) * 2
+    o = torch.randn(M, 512, generator=g).bfloat16() if outproj else None
+    d = lambda t: None if t is None else t.to(dev)  # noqa: E731
+    xo, xn = rt.op_ffn_dec(d(x), d(p["g2"]), d(p["b2n"]), 1e-12, d(p["W1"]), d(p["b1"]), d(p["W2"]), d(p["gF"]),
+                           d(p["bF"]), d(p["gn"]), d(p["bn"]), d(o), d(p["Wo"] if outproj else None),
+                           d(p["bo"] if outproj else None))
+    torch.cuda.synchronize()
+    x1 = x.double()
+    if outproj:
+        x1 = x1 + o.double() @ p["Wo"].bfloat16().double().T + p["bo"].double()
+        assert rel(xo.double().cpu(), x1) < 1e-6
+        x1 = xo.double().cpu()   # the FFN runs on the kernel's own f32 x1
+    y, exact = _dec_ffn_ref(x1, p)
+    if not outproj:
+        yc = xo.double().cpu()
+        assert rel(yc, y) < 5e-3
+        assert rel(yc, exact) < 2e-2
+    ln = _ln64(y, p["gn"], p["bn"], 1e-12)
+    assert rel(xn.double().cpu(), ln) < 1e-2
+    assert (xn.double().cpu() - ln).abs().max().item() < 0.1

@@ -40,20 +40,26 @@ FAST_MARGIN = 0.5
 
 def _margin_flips(r, g, cfg):
     """Position-wise token flips of a run vs the golden decoder argmax, over utterances whose token count
-    matches; returns (#flips, largest golden top-2 margin at a flipped position)."""
+    matches; returns (#flips, largest golden top-2 margin at a flipped position, #positions compared,
+    fraction of utterances compared)."""
     toks, nt = r["tokens"].cpu().numpy(), r["ntok"].cpu().numpy()
     off = np.concatenate([[0], np.cumsum(g["ntok"])])
-    flips, worst = 0, 0.0
-    gt = _golden_tokens(g)
+    flips, worst, compared, utts = 0, 0.0, 0, 0
+    if "argmax" in g:   # the per-position decoder argmax (special ids included)
+        gt = [g["argmax"][off[b]:off[b + 1]].tolist() for b in range(len(off) - 1)]
+    else:
+        gt = _golden_tokens(g)
     for b in range(toks.shape[0]):
         n = int(g["ntok"][b])
         if int(nt[b]) != n or len(gt[b]) != n:   # a changed count shifts every later position
             continue
+        utts += 1
+        compared += n
         bad = np.nonzero(toks[b, :n] != np.array(gt[b]))[0]
         flips += len(bad)
         if len(bad):
             worst = max(worst, float(g["margin"][off[b]:off[b + 1]][bad].max()))
-    return flips, worst
+    return flips, worst, compared, utts / max(1, toks.shape[0])
 
 
 def _golden_tokens(g):
@@ -149,11 +155,67 @@ def test_large_fast_agreement(engines, name):
     assert np.abs(nt - g["ntok"]).max() <= 1
     agree = [np.mean(np.array(a[: min(len(a), len(b))]) == np.array(b[: min(len(a), len(b))])) for a, b in
              zip(got, want) if min(len(a), len(b)) > 0]
-    flips, worst = _margin_flips(r, g, e.cfg)
+    flips, worst, compared, frac = _margin_flips(r, g, e.cfg)
     print(f"fast-mode token agreement {name}: {np.mean(agree):.4f}, enc rows rel {relerr:.2e}; "
           f"{flips} flips, largest reference top-2 margin among them {worst:.4f} nat")
     # bf16 operands move the logits by O(1e-2): a token may differ from the f32 reference only where the
     # reference's own top-2 log-prob margin is below FAST_MARGIN (utterances whose token count matches)
+    assert worst < FAST_MARGIN, (worst, FAST_MARGIN)
+    assert frac >= 0.5 and compared > 0, (frac, compared)   # the bound must compare something
+    assert np.mean(agree) > 0.6
+
+
+# ---------------------------------------------------------------- the bench configuration (C2) itself
+# para_large_b64 is the bench's shape (B=64 x T=500); para_large_b24 a ragged 24-utterance batch. Both are
+# reference runs (make_golden.py save_headline). At these sizes the DEFAULT fast dispatch engages every
+# kernel of the headline step: the fused encoder out-projection + FFN (OP mode, group rows >= 4096), the
+# fused decoder FFN (mode 2 / 3, group rows >= 2048) and the two concurrent encoder / decoder groups.
+HEADLINE = ["para_large_b24", "para_large_b64"]
+
+
+@pytest.mark.parametrize("name", HEADLINE)
+def test_headline_exact_tokens(engines, name):
+    """EXACT mode at the bench configuration: token ids and counts identical to the reference; encoder rows,
+    checksums and alphas at f32 accuracy."""
+    e = engines["large"]
+    g = np.load(f"{GOLD}/{name}.npz")
+    r = _run(e, g, "exact")
+    torch.cuda.synchronize()
+    assert np.array_equal(r["ntok"].cpu().numpy(), g["ntok"])
+    got, want = _tokens_from_run(r, e.cfg), _golden_tokens(g)
+    bad = [(b, i) for b in range(len(want)) for i, (p, q) in enumerate(zip(got[b], want[b])) if p != q]
+    assert got == want, f"{len(bad)} token differences, first {bad[:5]}"
+    enc = r["enc"].cpu().numpy()
+    lens = g["lens"]
+    rows = np.stack([enc[b, [0, int(lens[b]) // 2, int(lens[b]) - 1]] for b in range(len(lens))])
+    assert np.abs(rows - g["enc_rows"]).max() < 1e-4
+    assert np.linalg.norm(rows - g["enc_rows"]) / np.linalg.norm(g["enc_rows"]) < 1e-5
+    for b in range(len(lens)):
+        s = enc[b, : int(lens[b])].astype(np.float64)
+        assert abs((s ** 2).sum() - g["enc_sumsq"][b]) < 1e-5 * g["enc_sumsq"][b]
+    assert np.abs(r["alphas"].cpu().numpy() - g["alphas"]).max() < 1e-5
+
+
+@pytest.mark.parametrize("name", HEADLINE)
+def test_headline_fast_default_dispatch(engines, name):
+    """FAST mode, default dispatch, at the bench configuration: encoder rows within bf16 tolerance of the
+    reference (rel-L2 < 2e-2), token counts within +-1, and every token flip (utterances whose count matches)
+    at a reference top-2 log-prob margin below FAST_MARGIN; at least half the utterances compared."""
+    e = engines["large"]
+    g = np.load(f"{GOLD}/{name}.npz")
+    r = _run(e, g, "fast")
+    torch.cuda.synchronize()
+    enc = r["enc"].cpu().numpy()
+    lens = g["lens"]
+    rows = np.stack([enc[b, [0, int(lens[b]) // 2, int(lens[b]) - 1]] for b in range(len(lens))])
+    relerr = np.linalg.norm(rows - g["enc_rows"]) / np.linalg.norm(g["enc_rows"])
+    nt = r["ntok"].cpu().numpy()
+    flips, worst, compared, frac = _margin_flips(r, g, e.cfg)
+    print(f"{name} fast: enc rows rel-L2 {relerr:.2e}, ntok equal {np.mean(nt == g['ntok']):.3f}, "
+          f"{flips}/{compared} flips, largest reference margin among them {worst:.4f} nat")
+    assert relerr < 2e-2, relerr
+    assert np.abs(nt - g["ntok"]).max() <= 1
+    assert frac >= 0.5 and compared > 0, (frac, compared)
     assert worst < FAST_MARGIN, (worst, FAST_MARGIN)
 
 
@@ -332,3 +394,24 @@ def test_fast_ffn_schedule_variants_are_bit_identical(engines, monkeypatch):
         assert torch.equal(r1["enc"], r0["enc"]), knob
         assert torch.equal(r1["ntok"], r0["ntok"]), knob
         assert _tokens_from_run(r1, e.cfg) == _tokens_from_run(r0, e.cfg), knob
+
+
+@pytest.mark.parametrize("sub", ["1", "2"])
+def test_exact_first_run_after_reload(monkeypatch, sub):
+    """A fresh engine (and a weight reload) rebuilds the EXACT split planes, including layer 0's K-padded QKV
+    planes, on the caller's stream before the utterance groups fork: the first run after loading, with two
+    concurrent encoder groups, is token-exact on the ragged golden."""
+    monkeypatch.setenv("PFM_SUBBATCH", sub)
+    cfg = paraformer_large()
+    w = make_weights(cfg, seed=0)
+    e = PfmEngine(cfg, 0)
+    e.load_state_dict(w)
+    g = np.load(f"{GOLD}/para_large_ragged.npz")
+    r = _run(e, g, "exact")
+    torch.cuda.synchronize()
+    assert _tokens_from_run(r, e.cfg) == _golden_tokens(g)
+    key = "encoder.encoders0.0.self_attn.linear_q_k_v.weight"
+    e.set_weight(key, w[key])   # reload: planes re-split in place, then immediately a two-group run
+    r = _run(e, g, "exact")
+    torch.cuda.synchronize()
+    assert _tokens_from_run(r, e.cfg) == _golden_tokens(g)

@@ -310,3 +310,39 @@ def test_stream_graph_replay_matches_eager(tiny, mode, monkeypatch):
     eager, graphed = run("0"), run("1")
     assert graphed == eager
     assert sum(sum(n) for n, _ in eager) > 0
+
+
+
+def test_stream_graph_replay_after_weight_reload():
+    """EXACT-mode streaming graphs hold the addresses of layer 0's padded split planes (K = 560): a weight
+    reload after a graph was captured re-splits them in place (same buffers), so later replays see the new
+    weights. The same streams object runs one schedule before a reload (graphs captured at step 2, replayed
+    after), with layer 0's QKV scaled, and with the original weights back: the first and last runs equal a fresh
+    engine's run and the scaled interlude differs."""
+    cfg = paraformer_streaming_tiny()
+    e, w = _eng(cfg)
+    rng = np.random.default_rng(5)
+    xs = [torch.from_numpy(rng.standard_normal((2, 10, cfg.input_size), dtype=np.float32)).cuda() for _ in range(6)]
+
+    def run(s):
+        s.reset([0, 1])
+        out = []
+        for j, x in enumerate(xs):
+            r = s.step([0, 1], x, [10, 10], [j == len(xs) - 1] * 2)
+            torch.cuda.synchronize()
+            rc = {k: v.cpu() for k, v in r.items() if v is not None}
+            out.append([_toks(rc, i) for i in range(2)])
+        return out
+
+    s = PfmStreams(e, 2, (0, 10, 5), 4, 1, "exact")
+    base = run(s)
+    key = "encoder.encoders0.0.self_attn.linear_q_k_v.weight"
+    e.set_weight(key, w[key] * 3.0)
+    scaled = run(s)
+    e.set_weight(key, w[key])
+    again = run(s)
+    e2, _ = _eng(cfg)
+    fresh = run(PfmStreams(e2, 2, (0, 10, 5), 4, 1, "exact"))
+    assert again == base == fresh
+    assert scaled != base
+    assert sum(len(t) for step in base for t in step) > 0
