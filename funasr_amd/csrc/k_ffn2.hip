@@ -1,0 +1,681 @@
+// Fused SAN-M feed-forward sub-layer, 128 rows per workgroup (gfx950, fast mode). Same four modes and the
+// same arithmetic as k_ffn.hip (see there for the reference citations):
+//   MODE 0  encoder:       x2 = x + W2 relu(W1 LN2(x) + b1) + b2                 (sanm/encoder.py:138-145)
+//   MODE 1  encoder + OP:  x1 = O Wo^T + bo + F (+ x), then MODE 0 on x1          (sanm/encoder.py:120-145)
+//   MODE 2  decoder FFN:   y = W2 LN_F(relu(W1 LN1(x) + b1)), LN_F folded through W2
+//                          (sanm/positionwise_feed_forward.py:12-33)
+//   MODE 3  decoder + OP:  x1 = x + O Wo^T + bo -> xo, then MODE 2 on x1         (paraformer/decoder.py:97-119)
+// with the next LayerNorm of the result as a bf16 output (the consumer GEMM's operand).
+//
+// Why a second kernel: k_ffn.hip owns 64 rows per workgroup, so every workgroup streams all 4.5 MB of the
+// layer's weights through L2 -> LDS for 64 rows (64 FLOP per weight byte), and its A / H images fill the LDS
+// beside the weight ring. Here a workgroup owns 128 rows with 4 waves (one per SIMD, up to 512 VGPRs each) on
+// v_mfma_f32_32x32x16_bf16; each wave owns 32 rows and keeps EVERYTHING of them in registers:
+//   act[32]  the B operand fragments of its rows (O in phase 0, then LN(x1)): 128 VGPRs
+//   acc[16]  the 512-wide f32 output rows Y^T[512 x 32] (x1 + b2 + W2 H): 256 AGPRs
+//   acc1     one hidden chunk H^T[32 x 32] of phase 1, converted in registers into phase 2's B operand
+// The 32x32 accumulator has the row (lane) as its column and the features in registers, so the next
+// product that sums over features takes it with no lane movement (cdna_hip_programming.md §3 "an
+// accumulator tile as the next MFMA's operand"); the k order inside each 16-deep step is permuted
+// (element j of lane half h <-> feature 16s + 8(j>>2) + 4h + (j&3) of its 32-block) and the weights are
+// packed in that order. The LDS holds only the weight ring (8 x 16 KiB tiles, one 1 KiB MFMA fragment per
+// 32x16 weight block, read lane-linearly: conflict-free) and the per-column vectors. Weight bytes per row
+// halve against k_ffn.hip and no activation ever goes through LDS.
+//
+// Weight stream (pfm_ffn2_pack*): [OP: Wo fragments (ob, ks) ob-major] then per hidden chunk c of 32:
+// 32 W1 fragments (k steps of the 512 inputs) then 32 W2 fragments (16 output blocks x 2 k steps).
+// Fragment f feeds MFMA f; its ds_read is issued PD MFMAs ahead. Tile t is published (landed + every wave
+// done with tile t-1) by one barrier placed PD fragments before its first read; that barrier also frees
+// tile t-1's slot, which receives tile t-1+RS at once (RS-1 tiles in flight).
+#include <stdint.h>
+
+#include "pfm_common.h"
+
+namespace {
+
+typedef __attribute__((address_space(3))) void lds_void;
+typedef const __attribute__((address_space(1))) void gbl_void;
+
+constexpr int FD = 512, FF = 2048, BM = 128, NW = 4, HC = 32, NCH = FF / HC;   // 64 hidden chunks
+constexpr int FE = 512;                  // bf16 elements per fragment (32 rows x 16 k)
+constexpr int TF = 16;                   // fragments per ring tile (16 KiB)
+constexpr int RS = 8;                    // ring slots
+constexpr int GW = TF / NW;              // LDS-DMA pieces (1 KiB) per wave per tile
+constexpr int RING = RS * TF * 1024;     // 128 KiB
+constexpr int OPF = 16 * 32;             // phase-0 fragments: Wo = 16 output blocks x 32 k steps
+constexpr int CHF = 64;                  // fragments per hidden chunk: 32 W1 k steps + 16 x 2 W2
+constexpr int PD = 6;                    // fragment reads in flight ahead of their MFMA
+constexpr int NB = 8;                    // fragment register slots (divides TF, CHF and OPF)
+// per-column vectors staged in LDS behind the ring (float offsets)
+constexpr int V_G = 0, V_B = 512, V_C2 = 1024, V_GN = 1536, V_BN = 2048, V_BO = 2560, V_C1 = 3072, V_B1 = 3584;
+constexpr int NVEC = V_B1 + FF;
+constexpr int LDS_BYTES = RING + NVEC * 4;   // 153,600 B
+static_assert(LDS_BYTES <= 163840, "LDS plan");
+static_assert(PD < TF && TF % NB == 0 && CHF % NB == 0 && OPF % NB == 0 && PD < NB, "stream plan");
+
+__device__ __forceinline__ f32x16 mfma32(bf16x8 a, bf16x8 b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+// Every MFMA of the kernel is an asm statement with an explicit register file, so the allocator cannot trade
+// the 16 output blocks (acc[16] = all 256 AGPRs, "a") against phase 1's accumulator (acc1, 16 VGPRs, "v"):
+// with the builtin, acc1 claimed an AGPR block and one output block bounced through scratch every chunk.
+// hipcc pads no hazards around inline asm (cdna_hip_programming.md §5.7 item 2), so the kernel keeps them:
+//   * the first MFMA of a chain takes the inline constant 0 as C; later ones accumulate back to back into the
+//     same registers (XDL D -> the next XDL's whole C: 0 wait states);
+//   * D -> any other reader: 24 wait states (covers the 16-pass XDL distance of 19; xdl_drain(), fenced by
+//     sched_barrier, before the transition / epilogue VALU reads the accumulators; mfma_v_drain() before the relu
+//     of acc1 — 13 states measured too few: the next-LayerNorm output read stale accumulators);
+//   * a VALU-written operand -> MFMA: s_nop 1 (valu_to_mfma(), after the relu writes phase 2's B operand and
+//     after the transition writes act).
+// A comes from ds_read (ordered by lgkmcnt), B from act / hf.
+__device__ __forceinline__ void mfma_a0(f32x16& d, const bf16x8& a, const bf16x8& b) {
+    asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=&a"(d) : "v"(a), "v"(b));
+}
+__device__ __forceinline__ void mfma_a(f32x16& d, const bf16x8& a, const bf16x8& b) {
+    asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(d) : "v"(a), "v"(b));
+}
+__device__ __forceinline__ void mfma32_v0(f32x16& d, const bf16x8& a, const bf16x8& b) {
+    asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=&v"(d) : "v"(a), "v"(b));
+}
+__device__ __forceinline__ void mfma32_v(f32x16& d, const bf16x8& a, const bf16x8& b) {
+    asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(d) : "v"(a), "v"(b));
+}
+__device__ __forceinline__ void mfma_v_drain(f32x16& d) { asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" : "+v"(d)); }
+// The drain names every output block ("+a"): the compiler's copies of an accumulator into VGPRs (it keeps some
+// blocks there for the epilogue) can then only come after the wait states — a nop without operands let the
+// allocator place the copy of the last-written block right behind its MFMA, before the nops (stale values).
+__device__ __forceinline__ void xdl_drain(f32x16 (&a)[16]) {
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7"
+                 : "+a"(a[0]), "+a"(a[1]), "+a"(a[2]), "+a"(a[3]), "+a"(a[4]), "+a"(a[5]), "+a"(a[6]), "+a"(a[7]),
+                   "+a"(a[8]), "+a"(a[9]), "+a"(a[10]), "+a"(a[11]), "+a"(a[12]), "+a"(a[13]), "+a"(a[14]),
+                   "+a"(a[15])::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+}
+__device__ __forceinline__ void valu_to_mfma() {
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_nop 1" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+}
+
+template <int N> __device__ __forceinline__ void vm_wait() {
+    if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else if constexpr (N == 20) asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
+    else static_assert(N < 0, "vm_wait: unsupported count");
+}
+static_assert((RS - 3) * GW == 20, "vm_wait counts");
+
+// the hidden chunk's biases (4 x 16 B of this lane) by asm ds_reads: hipcc would precede a plain LDS read of
+// the staging area with vmcnt(0) (draining the in-flight ring DMA), and a scalar load would turn every counted
+// LDS wait of the chunk into lgkmcnt(0). hipcc does not count these reads: b1_wait() orders them (LDS returns
+// in order, and at the point of use only the PD younger fragment reads may still be outstanding).
+__device__ __forceinline__ void b1_read(f32x4& d, const void* lds) {
+    asm volatile("ds_read_b128 %0, %1" : "=v"(d) : "v"((unsigned)(uintptr_t)lds) : "memory");
+}
+// the per-column vectors of the VALU phases, by the same asm reads: a plain LDS read makes hipcc wait vmcnt(0)
+// first (it cannot tell the vector area from the LDS-DMA ring), which in the epilogue serialised every group of
+// output stores behind the next vector read. vec_wait() retires all LDS reads issued so far.
+__device__ __forceinline__ f32x4 vec_read(const float* lds) {
+    f32x4 d;
+    asm volatile("ds_read_b128 %0, %1" : "=v"(d) : "v"((unsigned)(uintptr_t)lds) : "memory");
+    return d;
+}
+
+// feature index (within its 32-block) of register reg of a 32x32 accumulator in lane half h
+__device__ __forceinline__ int acc_col(int reg, int h) { return (reg & 3) + 8 * (reg >> 2) + 4 * h; }
+
+// VAR (diagnostic builds of tools/ffn2_bench.hip only; the library instantiates VAR 0): 1 = no weight DMA and no
+// DMA waits (stale ring), 2 = no MFMAs, 3 = neither DMA nor barriers (MFMA + fragment reads alone), 5 = the
+// prologue / transition / epilogue alone (no stream: zero chunks, no phase-0 MFMAs), 4 = every tile streamed from
+// the same L2-hot 64 KiB (wrong math; prices L2 misses of the weight stream), 6 = the kernel with s_memtime
+// stamps at its phase boundaries (wave 0 of each block -> ffn2_stamps; cdna_hip_programming.md §7 in-kernel stamps)
+#ifdef PFM_FFN2_STAMPS
+__device__ unsigned long long ffn2_stamps[4096 * 16];
+#endif
+template <int MODE, int VAR = 0>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void ffn2_kernel(
+    const float* __restrict__ X, int M, const float* __restrict__ g, const float* __restrict__ be, float eps,
+    const bf16* __restrict__ Wp, const float* __restrict__ b1, const float* __restrict__ b2, float* Xo,
+    const float* __restrict__ gn, const float* __restrict__ bn, bf16* __restrict__ Xn, const bf16* __restrict__ O,
+    const bf16* __restrict__ Fr, const float* __restrict__ bo, const float* __restrict__ c1) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    float* vec = (float*)(smem + RING);
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int r = lane & 31, h = lane >> 5;
+    constexpr bool OP = MODE == 1 || MODE == 3, DEC = MODE == 2 || MODE == 3;
+    constexpr int F0 = OP ? OPF : 0, NF = F0 + NCH * CHF, NT = NF / TF;
+    const long long rg = (long long)blockIdx.x * BM + 32 * w + r;   // this lane's row
+    const bool live = rg < M;
+    const long long rc = live ? rg : (long long)M - 1;               // clamped for loads
+    auto stamp = [&](int k) {
+#ifdef PFM_FFN2_STAMPS
+        if constexpr (VAR == 6) {
+            unsigned long long t;
+            __builtin_amdgcn_sched_barrier(0);
+            asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+            __builtin_amdgcn_sched_barrier(0);
+            if (tid == 0 && blockIdx.x < 4096) ffn2_stamps[blockIdx.x * 16 + k] = t;
+        }
+#endif
+    };
+    stamp(0);
+
+    // ---- per-column vectors -> LDS (before any LDS-DMA is in flight: their waits drain nothing)
+    for (int i = tid; i < FD; i += 256) {
+        vec[V_G + i] = g[i];
+        vec[V_B + i] = be[i];
+        vec[V_C2 + i] = b2[i];
+        if (Xn) { vec[V_GN + i] = gn[i]; vec[V_BN + i] = bn[i]; }
+        if constexpr (OP) vec[V_BO + i] = bo[i];
+        if constexpr (DEC) vec[V_C1 + i] = c1[i];
+    }
+    for (int i = tid; i < FF; i += 256) vec[V_B1 + i] = b1[i];
+    __syncthreads();
+
+    // ---- weight ring: tile t -> slot t % RS; this wave moves fragments GW w .. GW w + GW - 1 of each tile
+    const bf16* wsrc = Wp + (long long)GW * w * FE + lane * 8;
+    auto issue = [&](int t) {
+        if (t >= NT || VAR == 1 || VAR == 3 || VAR == 5) return;
+        const bf16* src = wsrc + (long long)(VAR == 4 ? (t & 3) : t) * TF * FE;   // VAR 4: an L2-hot 64 KiB stream
+        unsigned char* dst = smem + (t % RS) * (TF * 1024) + GW * w * 1024;
+        // one address and one M0 per tile: the pieces are 1 KiB apart in both spaces, so they differ only in the
+        // instruction's immediate offset (applied to the global and the LDS address alike)
+        static_assert(GW == 4, "LDS-DMA pieces per tile");
+        __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)dst, 16, 0, 0);
+        __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)dst, 16, 1024, 0);
+        __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)dst, 16, 2048, 0);
+        __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)dst, 16, 3072, 0);
+    };
+    auto bar = [&]() {
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    // publish tile t: it landed (RS-3 newer tiles may stay in flight). The same barrier retires tile t-2: every
+    // wave consumed its last fragment (the MFMA waited for the read) before reaching this barrier, so its slot
+    // takes tile t-2+RS at once — no LDS wait at the barrier, the PD fragment reads of tile t stay in flight.
+    auto top = [&](int t) {
+        if (t >= NT || VAR == 3 || VAR == 5) return;
+        if (VAR == 1) {}
+        else if (t + RS - 3 < NT) vm_wait<(RS - 3) * GW>();
+        else vm_wait<0>();
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        issue(t - 2 + RS);
+    };
+    // Fragment reads are asm ds_reads with hand-counted waits (the compiler's wait analysis lost count across the
+    // asm MFMAs and the loop back edge and drained every read in flight ~10 times per chunk). LDS reads return in
+    // order: before MFMA f, the reads of fragments f+1 .. f+PD are the only younger ones, so lgkmcnt(PD) covers
+    // fragment f. The wait statement names the destination ("+v"),
+    // so no consumer of it is scheduled above the wait.
+    bf16x8 wf[NB];
+    const unsigned ring_lane = (unsigned)(uintptr_t)smem + lane * 16;
+    auto rd = [&](int f, int fs, bf16x8& dst) {   // fs = f mod TF at compile time (the immediate offset)
+        const unsigned a = ring_lane + ((f / TF) % RS) * (TF * 1024);
+        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(dst) : "v"(a), "i"((fs % TF) * 1024));
+    };
+    auto frag_wait = [&](bf16x8& d) { asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(d) : "i"(PD)); };
+#pragma unroll
+    for (int t = 0; t < RS - 1; ++t) issue(t);
+
+    // ---- prologue: B-operand fragments of this lane's row (phase 0: O rows; else LN(x)) and the accumulator
+    bf16x8 act[32];
+    f32x16 acc[16];
+    // LayerNorm statistics of a 512-wide row split over lanes r, r+32 (256 features each)
+    // (two-pass: mean, then the centred sum of squares, like the unfused LayerNorm kernels)
+    auto half_mean = [&](float s) { return (s + __shfl_xor(s, 32, 64)) * (1.f / FD); };
+    auto half_rstd = [&](float q) { return 1.f / sqrtf((q + __shfl_xor(q, 32, 64)) * (1.f / FD) + eps); };
+    // The VALU phases (prologue, transition, epilogue) touch the accumulators one output block at a time: the
+    // block is copied to VGPRs, used / updated and written back between scheduling fences, so at most one block
+    // (plus a batch of loads) is in VGPRs at once — left to itself the allocator pulled the whole array into
+    // VGPRs and spilled it to scratch.
+    auto fence = [&]() { __builtin_amdgcn_sched_barrier(0); };
+    auto acc_get = [&](int ob) {
+        f32x16 t = acc[ob];
+        asm volatile("" : "+v"(t));
+        return t;
+    };
+    auto acc_put = [&](int ob, f32x16 t) {
+        acc[ob] = t;
+        asm volatile("" : "+a"(acc[ob]));
+    };
+    auto acc_stats = [&](float& mean, float& rstd) {
+        float s = 0.f;
+#pragma unroll
+        for (int ob = 0; ob < 16; ++ob) {
+            fence();
+            const f32x16 t = acc_get(ob);
+#pragma unroll
+            for (int e = 0; e < 16; ++e) s += t[e];
+        }
+        fence();
+        mean = half_mean(s);
+        float q = 0.f;
+#pragma unroll
+        for (int ob = 0; ob < 16; ++ob) {
+            fence();
+            const f32x16 t = acc_get(ob);
+#pragma unroll
+            for (int e = 0; e < 16; ++e) { const float d = t[e] - mean; q += d * d; }
+        }
+        fence();
+        rstd = half_rstd(q);
+    };
+    // LN of block ob (values t, register e = feature 8(e>>2) + 4h + (e&3) of the block) with the vectors at
+    // vg / vb -> the B fragments of k steps 2 ob, 2 ob + 1 (the permuted order the W1 fragments are packed in)
+    // four column vectors (vector areas va, vb of block ob: register groups q = 0..3) by asm reads, one wait
+    auto vec_block = [&](int va, int vb, int ob, f32x4 (&A)[4], f32x4 (&B)[4]) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            A[q] = vec_read(vec + va + 32 * ob + 8 * q + 4 * h);
+            B[q] = vec_read(vec + vb + 32 * ob + 8 * q + 4 * h);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(A[0]), "+v"(A[1]), "+v"(A[2]), "+v"(A[3]), "+v"(B[0]), "+v"(B[1]),
+                     "+v"(B[2]), "+v"(B[3]));
+    };
+    auto ln_block = [&](int ob, const f32x16& t, float mean, float rstd) {
+        f32x4 G[4], Bt[4];
+        vec_block(V_G, V_B, ob, G, Bt);
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                act[2 * ob + (q >> 1)][4 * (q & 1) + i] = f2bf((t[4 * q + i] - mean) * rstd * G[q][i] + Bt[q][i]);
+    };
+    // acc[ob] = (keep ? acc[ob] + vector at V_C2 : 0) for every block (the accumulator start of the FFN)
+    auto acc_c2 = [&](int ob, f32x16 t, bool keep) {
+        if (keep) {
+            f32x4 C[4], Cd[4];
+            vec_block(V_C2, V_C2, ob, C, Cd);
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) t[4 * q + i] += C[q][i];
+        } else {
+#pragma unroll
+            for (int e = 0; e < 16; ++e) t[e] = 0.f;
+        }
+        acc_put(ob, t);
+    };
+    // acc = ((acc or 0) + bias) + f) + hx * x over the row, in four batches of 4 output blocks whose loads
+    // (16 float4 of x, 16 x 8 B of f) are all issued before the first use: one memory round trip per batch (loads
+    // interleaved with their uses were serialised, each wait also draining the in-flight weight DMA)
+    auto add_rows = [&](bool from_zero, const float* xp, long long xst, float hx, const bf16* fp, int vb) {
+        constexpr int NBT = 4, KB = 64 / NBT;
+#pragma unroll
+        for (int bt = 0; bt < NBT; ++bt) {
+            fence();
+            float4 xv[KB];
+            bf16x4 fv[KB];
+#pragma unroll
+            for (int k = 0; k < KB; ++k) {
+                const int kk = KB * bt + k, col = 32 * (kk / 4) + 8 * (kk % 4) + 4 * h;
+                xv[k] = *(const float4*)(xp + rc * xst + col);
+                if (fp) fv[k] = *(const bf16x4*)(fp + rc * FD + col);
+            }
+            fence();
+#pragma unroll
+            for (int j = 0; j < KB / 4; ++j) {
+                const int ob = (KB / 4) * bt + j;
+                f32x16 t;
+                if (from_zero) {
+#pragma unroll
+                    for (int e = 0; e < 16; ++e) t[e] = 0.f;
+                } else {
+                    t = acc_get(ob);
+                }
+                f32x4 Bv[4], Bd[4];
+                if (vb >= 0) {
+                    vec_block(vb, vb, ob, Bv, Bd);
+                } else {
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) Bv[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+                }
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int k = 4 * j + q;
+                    const float xs[4] = {xv[k].x, xv[k].y, xv[k].z, xv[k].w};
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const float fvi = fp ? bf2f(fv[k][i]) : 0.f;
+                        t[4 * q + i] = ((t[4 * q + i] + Bv[q][i]) + fvi) + hx * xs[i];
+                    }
+                }
+                acc_put(ob, t);
+                fence();
+            }
+        }
+    };
+    if constexpr (OP) {
+#pragma unroll
+        for (int ks = 0; ks < 32; ++ks) act[ks] = *(const bf16x8*)(O + rc * FD + 16 * ks + 8 * h);
+    } else {
+        // the row into the accumulators (batched loads), its LayerNorm -> act, then the accumulator start
+        // (MODE 0: x + b2, the residual the FFN output lands on; DEC: 0)
+        add_rows(true, X, FD, 1.f, nullptr, -1);
+        float mean, rstd;
+        acc_stats(mean, rstd);
+#pragma unroll
+        for (int ob = 0; ob < 16; ++ob) {
+            fence();
+            const f32x16 t = acc_get(ob);
+            ln_block(ob, t, mean, rstd);
+            acc_c2(ob, t, MODE == 0);
+        }
+        fence();
+    }
+
+    stamp(1);
+    // ---- tile 0 landed everywhere (the compiler's wait for the activation loads drained the ring DMA too)
+    vm_wait<0>();
+    bar();
+#pragma unroll
+    for (int f = 0; f < PD; ++f) rd(f, f, wf[f]);
+
+    // one stream step: fragment f (compile-time position fs within the stream's unrolled body): publish the next
+    // tile when its first read is due, read fragment f+PD, wait for fragment f (then its MFMA)
+    // (past the stream's end the read-ahead keeps going: in-bounds reads of stale ring slots nobody consumes,
+    // so every step has the same wait)
+    auto step_pre = [&](int f, int fs) {
+        __builtin_amdgcn_sched_barrier(0);
+        if (fs % TF == TF - PD) top(f / TF + 1);
+        rd(f + PD, fs + PD, wf[(fs + PD) % NB]);
+        frag_wait(wf[fs % NB]);
+        __builtin_amdgcn_sched_barrier(0);
+    };
+
+    if constexpr (OP) {   // phase 0: Y0^T += Wo . O^T  (fragment 32 ob + ks)
+#pragma unroll
+        for (int ob = 0; ob < 16; ++ob)
+#pragma unroll
+            for (int ks = 0; ks < 32; ++ks) {
+                const int f = 32 * ob + ks;
+                step_pre(f, f);
+                if (VAR == 2 || VAR == 5) asm volatile("" :: "v"(wf[f % NB]));
+                else if (ks == 0) mfma_a0(acc[ob], wf[f % NB], act[0]);
+                else mfma_a(acc[ob], wf[f % NB], act[ks]);
+            }
+        xdl_drain(acc);
+        stamp(2);
+        // x1 = ((Y0 + bo) + F) + x (the separate GEMM epilogue's order; layer 0: no x, the decoder: no F)
+        add_rows(false, X ? X : bo, X ? FD : 0, X ? 1.f : 0.f, MODE == 1 ? Fr : nullptr, V_BO);
+        stamp(6);
+        if constexpr (MODE == 3) {   // the decoder keeps x1 (its FSMN step adds to it)
+            if (live) {
+#pragma unroll
+                for (int ob = 0; ob < 16; ++ob) {
+                    fence();
+                    const f32x16 t = acc_get(ob);
+#pragma unroll
+                    for (int q = 0; q < 4; ++q)
+                        *(float4*)(Xo + rg * FD + 32 * ob + 8 * q + 4 * h) =
+                            make_float4(t[4 * q], t[4 * q + 1], t[4 * q + 2], t[4 * q + 3]);
+                }
+                fence();
+            }
+        }
+        float mean, rstd;
+        acc_stats(mean, rstd);
+        stamp(7);
+#pragma unroll
+        for (int ob = 0; ob < 16; ++ob) {   // LN2(x1) -> act; accumulators: x1 + b2 (encoder) / 0 (decoder)
+            fence();
+            const f32x16 t = acc_get(ob);
+            ln_block(ob, t, mean, rstd);
+            acc_c2(ob, t, MODE == 1);
+        }
+        fence();
+    }
+    valu_to_mfma();
+
+    stamp(3);
+    float rs = 0.f, rq = 0.f;   // DEC: sum / sum of squares of this lane's bf16 hidden values
+    f32x16 acc1;
+    for (int c = 0; c < (VAR == 5 ? 0 : NCH); ++c) {
+        const int fb = F0 + CHF * c;
+        f32x4 bq[4];   // b1 of the chunk's features 8q + 4h .. +3 (the accumulator's register groups)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) b1_read(bq[q], vec + V_B1 + HC * c + 8 * q + 4 * h);
+        // phase 1: H^T[32 hidden x 32 rows] = W1_c . A^T over the 32 k steps
+#pragma unroll
+        for (int i = 0; i < 32; ++i) {
+            step_pre(fb + i, i);
+            if (VAR == 2) asm volatile("" :: "v"(wf[i % NB]));
+            else if (VAR == 7) mfma_a(acc[i & 15], wf[i % NB], act[i]);   // diagnostic: AGPR chain, wrong math
+            else if (i == 0) mfma32_v0(acc1, wf[0], act[0]);
+            else mfma32_v(acc1, wf[i % NB], act[i]);
+        }
+        mfma_v_drain(acc1);
+        // relu(H + b1) -> bf16 -> phase 2's B operand (registers 8s .. 8s+7 = k step s)
+        bf16x8 hf[2];
+        if constexpr (VAR == 8) {   // diagnostic: no relu / bias / drain between the phases
+            hf[0] = act[0];
+            hf[1] = act[1];
+        } else {
+            static_assert(PD == 6, "b1 wait count");
+            __builtin_amdgcn_sched_barrier(0);
+            asm volatile("s_waitcnt lgkmcnt(6)" : "+v"(bq[0]), "+v"(bq[1]), "+v"(bq[2]), "+v"(bq[3]));
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const float bv4[4] = {bq[q][0], bq[q][1], bq[q][2], bq[q][3]};
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const float bv = bv4[i];
+                    const bf16 v = f2bf(fmaxf(acc1[4 * q + i] + bv, 0.f));
+                    hf[q >> 1][4 * (q & 1) + i] = v;
+                    if constexpr (DEC) {
+                        const float fv = bf2f(v);
+                        rs += fv;
+                        rq += fv * fv;
+                    }
+                }
+            }
+        }
+        valu_to_mfma();
+        // phase 2: Y^T[512 x 32] += W2_c . H^T  (fragment 32 + 2 ob + s)
+#pragma unroll
+        for (int j = 0; j < 32; ++j) {
+            step_pre(fb + 32 + j, 32 + j);
+            if (VAR == 2) asm volatile("" :: "v"(wf[(32 + j) % NB]), "v"(hf[j & 1]));
+            else mfma_a(acc[j >> 1], wf[(32 + j) % NB], hf[j & 1]);
+        }
+    }
+    xdl_drain(acc);
+
+    stamp(4);
+    // ---- epilogue (no DMA in flight: the last tiles were waited for by their tops)
+    if constexpr (DEC) {   // y = rstd_h (W2g h - mu_h c1) + c2 ; the hidden's statistics over both lane halves
+        rs += __shfl_xor(rs, 32, 64);
+        rq += __shfl_xor(rq, 32, 64);
+        const float mu = rs * (1.f / FF);
+        const float var = fmaxf(rq * (1.f / FF) - mu * mu, 0.f);
+        const float rh = 1.f / sqrtf(var + eps);
+#pragma unroll
+        for (int ob = 0; ob < 16; ++ob) {
+            fence();
+            f32x16 t = acc_get(ob);
+            f32x4 C1[4], C2[4];
+            vec_block(V_C1, V_C2, ob, C1, C2);
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) t[4 * q + i] = rh * (t[4 * q + i] - mu * C1[q][i]) + C2[q][i];
+            acc_put(ob, t);
+        }
+        fence();
+    }
+    if (live && Xo && MODE != 3) {
+#pragma unroll
+        for (int ob = 0; ob < 16; ++ob) {
+            fence();
+            const f32x16 t = acc_get(ob);
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                *(float4*)(Xo + rg * FD + 32 * ob + 8 * q + 4 * h) = make_float4(t[4 * q], t[4 * q + 1], t[4 * q + 2], t[4 * q + 3]);
+        }
+        fence();
+    }
+    stamp(8);
+    if (Xn) {
+        float mean, rstd;
+        acc_stats(mean, rstd);
+        stamp(9);
+        if (live) {
+#pragma unroll
+            for (int ob = 0; ob < 16; ++ob) {
+                fence();
+                const f32x16 t = acc_get(ob);
+                f32x4 G[4], Bt[4];
+                vec_block(V_GN, V_BN, ob, G, Bt);
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    bf16x4 o;
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) o[i] = f2bf((t[4 * q + i] - mean) * rstd * G[q][i] + Bt[q][i]);
+                    *(bf16x4*)(Xn + rg * FD + 32 * ob + 8 * q + 4 * h) = o;
+                }
+            }
+            fence();
+        }
+    }
+    stamp(5);
+}
+
+// ---- packing: one thread per 16-B piece (fragment f, lane l = 32 hh + m) in stream order
+// within-block feature of element j of lane half hh in k step s (the accumulator's register order)
+__device__ __forceinline__ int perm_k(int s, int hh, int j) { return 16 * s + 8 * (j >> 2) + 4 * hh + (j & 3); }
+
+// hidden chunk c: fragments 0..31 = W1 rows [32c, 32c+32) x k step ks (permuted k of the 512 inputs),
+// fragments 32 + 2 ob + s = W2 rows [32 ob, 32 ob + 32) x k step s of the chunk's 32 hidden (permuted).
+// DEC: the W2 fragments hold bf16(W2 gamma_F) from the f32 W2 (W2b unused).
+__global__ __launch_bounds__(256) void ffn2_pack_kernel(const bf16* __restrict__ W1, const bf16* __restrict__ W2b,
+                                                        const float* __restrict__ W2f, const float* __restrict__ gF,
+                                                        bf16* __restrict__ Wp) {
+    const int gid = blockIdx.x * 256 + threadIdx.x;   // < NCH * CHF * 64
+    const int f = gid >> 6, l = gid & 63, m = l & 31, hh = l >> 5;
+    const int c = f / CHF, i = f % CHF;
+    bf16x8 o;
+    if (i < 32) {
+        const int kb = i >> 1, s = i & 1;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = W1[(long long)(HC * c + m) * FD + 32 * kb + perm_k(s, hh, j)];
+    } else {
+        const int ob = (i - 32) >> 1, s = (i - 32) & 1;
+        const long long rowb = (long long)(32 * ob + m) * FF + HC * c;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int k = perm_k(s, hh, j);
+            o[j] = W2f ? f2bf(W2f[rowb + k] * gF[HC * c + k]) : W2b[rowb + k];
+        }
+    }
+    *(bf16x8*)(Wp + (long long)gid * 8) = o;
+}
+
+// Wo [512 out][512 in] -> fragments (ob, ks) ob-major, natural k (the O rows are loaded in natural order)
+__global__ __launch_bounds__(256) void ffn2_pack_o_kernel(const bf16* __restrict__ Wo, bf16* __restrict__ Wp) {
+    const int gid = blockIdx.x * 256 + threadIdx.x;   // < OPF * 64
+    const int f = gid >> 6, l = gid & 63, m = l & 31, hh = l >> 5;
+    const int ob = f >> 5, ks = f & 31;
+    *(bf16x8*)(Wp + (long long)gid * 8) = *(const bf16x8*)(Wo + (long long)(32 * ob + m) * FD + 16 * ks + 8 * hh);
+}
+
+// c1[o] = sum_k bf16(W2[o][k] g[k]) (the packed values), c2[o] = sum_k W2[o][k] b[k]; one block per output row
+__global__ __launch_bounds__(256) void ffn2_dec_consts_kernel(const float* __restrict__ W2, const float* __restrict__ gF,
+                                                              const float* __restrict__ bF, float* __restrict__ c1,
+                                                              float* __restrict__ c2) {
+    __shared__ float r1[256], r2[256];
+    const int o = blockIdx.x, t = threadIdx.x;
+    float s1 = 0.f, s2 = 0.f;
+    for (int k = t; k < FF; k += 256) {
+        const float wv = W2[(long long)o * FF + k];
+        s1 += bf2f(f2bf(wv * gF[k]));
+        s2 += wv * bF[k];
+    }
+    r1[t] = s1; r2[t] = s2;
+    __syncthreads();
+    for (int n = 128; n > 0; n >>= 1) {
+        if (t < n) { r1[t] += r1[t + n]; r2[t] += r2[t + n]; }
+        __syncthreads();
+    }
+    if (t == 0) { c1[o] = r1[0]; c2[o] = r2[0]; }
+}
+
+template <int MODE>
+hipError_t ffn2_launch(hipStream_t st, int M, const float* x, const float* g, const float* be, float eps, const bf16* Wp,
+                       const float* b1, const float* b2, float* xo, const float* gn, const float* bn, bf16* xn,
+                       const bf16* o, const bf16* f, const float* bo, const float* c1) {
+    static bool attr_done = false;   // one flag per instantiation
+    if (!attr_done) {
+        attr_done = true;
+        (void)hipFuncSetAttribute((const void*)ffn2_kernel<MODE>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+    }
+    hipLaunchKernelGGL(ffn2_kernel<MODE>, dim3((M + BM - 1) / BM), dim3(64 * NW), LDS_BYTES, st, x, M, g, be, eps, Wp,
+                       b1, b2, xo, gn, bn, xn, o, f, bo, c1);
+    PFM_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+}  // namespace
+
+// packed sizes equal k_ffn.hip's (pfm_ffn_packed_elems / pfm_ffn_packed_o_elems): the buffers are shared
+static_assert((size_t)NCH * CHF * FE == (size_t)2048 * 1024, "FFN pack size");
+static_assert((size_t)OPF * FE == (size_t)512 * 512, "Wo pack size");
+
+hipError_t pfm_ffn2_pack(const bf16* W1, const bf16* W2, bf16* Wp, hipStream_t st) {
+    hipLaunchKernelGGL(ffn2_pack_kernel, dim3(NCH * CHF * 64 / 256), dim3(256), 0, st, W1, W2, nullptr, nullptr, Wp);
+    PFM_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+hipError_t pfm_ffn2_pack_o(const bf16* Wo, bf16* Wp, hipStream_t st) {
+    hipLaunchKernelGGL(ffn2_pack_o_kernel, dim3(OPF * 64 / 256), dim3(256), 0, st, Wo, Wp);
+    PFM_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+hipError_t pfm_ffn2_pack_dec(const bf16* W1, const float* W2, const float* gF, const float* bF, bf16* Wp, float* c1,
+                             float* c2, hipStream_t st) {
+    hipLaunchKernelGGL(ffn2_pack_kernel, dim3(NCH * CHF * 64 / 256), dim3(256), 0, st, W1, nullptr, W2, gF, Wp);
+    PFM_LAUNCH_CHECK();
+    hipLaunchKernelGGL(ffn2_dec_consts_kernel, dim3(FD), dim3(256), 0, st, W2, gF, bF, c1, c2);
+    PFM_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+// Same contracts as pfm_ffn_fused / pfm_ffn_fused_op / pfm_ffn_fused_dec (k_ffn.hip), pfm_ffn2_pack* weights.
+hipError_t pfm_ffn2_fused(const float* x, int M, const float* g2, const float* be2, float eps, const bf16* Wp,
+                          const float* b1, const float* b2, float* xo, const float* gn, const float* bn, bf16* xn,
+                          hipStream_t st) {
+    if (M <= 0) return hipSuccess;
+    if ((xn != nullptr) != (gn != nullptr && bn != nullptr) || !x || !b1 || !b2 || !g2 || !be2) return hipErrorInvalidValue;
+    if (!al16(x) || !al16(xo) || !al16(Wp) || !al16(xn) || !al16(b1) || !al16(b2)) return hipErrorInvalidValue;
+    return ffn2_launch<0>(st, M, x, g2, be2, eps, Wp, b1, b2, xo, gn, bn, xn, nullptr, nullptr, nullptr, nullptr);
+}
+
+hipError_t pfm_ffn2_fused_op(const bf16* o, const bf16* f, const float* bo, const float* x, int M, const float* g2,
+                             const float* be2, float eps, const bf16* Wop, const float* b1, const float* b2, float* xo,
+                             const float* gn, const float* bn, bf16* xn, hipStream_t st) {
+    if (M <= 0) return hipSuccess;
+    if ((xn != nullptr) != (gn != nullptr && bn != nullptr) || !o || !f || !bo || !xo || !b1 || !b2)
+        return hipErrorInvalidValue;
+    if (!al16(x) || !al16(xo) || !al16(Wop) || !al16(xn) || !al16(o) || !al16(f) || !al16(bo)) return hipErrorInvalidValue;
+    return ffn2_launch<1>(st, M, x, g2, be2, eps, Wop, b1, b2, xo, gn, bn, xn, o, f, bo, nullptr);
+}
+
+hipError_t pfm_ffn2_fused_dec(const float* x, int M, const float* g1, const float* be1, float eps, const bf16* Wp,
+                              const float* b1, const float* c1, const float* c2, float* xo, const float* gn,
+                              const float* bn, bf16* xn, const bf16* o, const float* bo, hipStream_t st) {
+    if (M <= 0) return hipSuccess;
+    if (!xn || !gn || !bn || !c1 || !c2 || !x || (o && (!bo || !xo))) return hipErrorInvalidValue;
+    if (!al16(x) || !al16(xo) || !al16(Wp) || !al16(xn) || !al16(c1) || !al16(c2) || !al16(o) || !al16(bo))
+        return hipErrorInvalidValue;
+    if (o) return ffn2_launch<3>(st, M, x, g1, be1, eps, Wp, b1, c2, xo, gn, bn, xn, o, nullptr, bo, c1);
+    return ffn2_launch<2>(st, M, x, g1, be1, eps, Wp, b1, c2, xo, gn, bn, xn, nullptr, nullptr, nullptr, c1);
+}

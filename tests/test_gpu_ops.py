@@ -284,14 +284,18 @@ def _ffn_ref(x, g2, b2n, eps, W1b, b1, W2b, b2):
 
 @pytest.mark.parametrize("M", [64, 200, 1000])
 @pytest.mark.parametrize("with_next", [False, True])
-@pytest.mark.parametrize("hr", ["1", "0"])
+@pytest.mark.parametrize("hr", ["1", "0", "k2"])
 def test_ffn_fused(dev, M, with_next, hr, monkeypatch):
     """Fused LN2 -> W1 -> relu -> W2 -> residual (-> next LN, bf16) vs fp64 torch on the same bf16 weights:
     FFN increment (y - x) within rel-L2 5e-3 (f32 accumulation order flips a few bf16 roundings of the
     hidden activation), y within rel 1e-4; the next-layer LayerNorm of the kernel's own y within 1.6e-2
     abs (one bf16 ulp at |v| <= 4); rows beyond M untouched by construction (ragged M). With and without
     the phase-2 activation-fragment reuse (PFM_FFN_HR)."""
-    monkeypatch.setenv("PFM_FFN_HR", hr)
+    if hr == "k2":   # the 128-row kernel (k_ffn2.hip)
+        monkeypatch.setenv("PFM_FFN_KERNEL", "2")
+    else:
+        monkeypatch.setenv("PFM_FFN_KERNEL", "1")
+        monkeypatch.setenv("PFM_FFN_HR", hr)
     g = torch.Generator().manual_seed(M + 7 * with_next)
     x = torch.randn(M, 512, generator=g) * 2
     g2 = 1 + 0.1 * torch.randn(512, generator=g)
@@ -337,16 +341,19 @@ def _ffn_params(g, dec=False):
     return p
 
 
+@pytest.mark.parametrize("kern", ["1", "2"])
 @pytest.mark.parametrize("M", [64, 200, 1000, 4100])
 @pytest.mark.parametrize("resid", [True, False])
-def test_ffn_fused_outproj(dev, M, resid):
+def test_ffn_fused_outproj(dev, M, resid, kern, monkeypatch):
     """The encoder sub-layer tail exactly as the fast path's default dispatch runs it (ffn_fused_kernel OP mode:
     out-projection as phase 0, x1 in the accumulators, LN2 reduced across waves, FFN, next LN1) vs an fp64
     restatement of sanm/encoder.py:120-145 on the kernel's bf16 operand roundings:
       x1 = x + (o Wo^T + bo + f)   (layer 0: no x),  a = bf16(LN2(x1)),  h = bf16(relu(a W1^T + b1)),
       x2 = x1 + h W2^T + b2,  xn = LN1_next(x2).
     Tolerances: the FFN increment x2 - x1 rel-L2 < 5e-3 (f32 accumulation order flips a few bf16 roundings of
-    a / h), x2 rel < 1e-4, xn within 1.6e-2 abs of LN1_next of the kernel's own x2 (one bf16 ulp at |v| <= 4)."""
+    a / h), x2 rel < 1e-4, xn within 1.6e-2 abs of LN1_next of the kernel's own x2 (one bf16 ulp at |v| <= 4).
+    Both fused kernels: k_ffn.hip (64 rows per workgroup, PFM_FFN_KERNEL=1) and k_ffn2.hip (128, the default)."""
+    monkeypatch.setenv("PFM_FFN_KERNEL", kern)
     g = torch.Generator().manual_seed(31 * M + resid)
     p = _ffn_params(g)
     x = torch.randn(M, 512, generator=g) * 2 if resid else None
@@ -381,13 +388,16 @@ def _dec_ffn_ref(x1, p, eps=1e-12):
     return y, exact
 
 
+@pytest.mark.parametrize("kern", ["1", "2"])
 @pytest.mark.parametrize("M", [64, 200, 1000, 4100])
 @pytest.mark.parametrize("outproj", [False, True])
-def test_ffn_fused_decoder(dev, M, outproj):
+def test_ffn_fused_decoder(dev, M, outproj, kern, monkeypatch):
     """The decoder FFN exactly as the fast path runs it (ffn_fused_kernel DEC: LN1 prologue, LN_F folded through
     W2, next LayerNorm epilogue; with outproj the previous block's cross-attention out-projection as phase 0,
     x1 = x + o Wo^T + bo written back) vs fp64 on the kernel's bf16 roundings: y rel-L2 < 5e-3 (and < 2e-2 vs
-    the unrounded W2 LN_F(h)), xn within 1.6e-2 of LN_next of the fp64 y plus the y error; x1 rel < 1e-6."""
+    the unrounded W2 LN_F(h)), xn within 1.6e-2 of LN_next of the fp64 y plus the y error; x1 rel < 1e-6.
+    Both fused kernels (PFM_FFN_KERNEL 1 / 2)."""
+    monkeypatch.setenv("PFM_FFN_KERNEL", kern)
     g = torch.Generator().manual_seed(17 * M + outproj)
     p = _ffn_params(g, dec=True)
     x = torch.randn(M, 512, generator=g) * 2

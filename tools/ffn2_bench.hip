@@ -1,0 +1,119 @@
+// Standalone timing of the 128-row fused FFN kernel (k_ffn2.hip) and its diagnostic variants (VAR 1: no weight
+// DMA, 2: no MFMA, 3: no DMA and no barriers) on random data, HIP events, one process.
+//   hipcc -O3 -std=c++17 --offload-arch=gfx950 -I include tools/ffn2_bench.hip -o tools/ffn2_bench
+//   ./tools/ffn2_bench [M ...]
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+#include <algorithm>
+
+#define PFM_FFN2_STAMPS
+#include "../funasr_amd/csrc/k_ffn2.hip"
+
+#define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e_)); exit(1); } } while (0)
+
+__global__ void fill_bf16(bf16* p, long long n, unsigned seed, float scale) {
+    long long i = blockIdx.x * 256LL + threadIdx.x;
+    if (i >= n) return;
+    unsigned x = (unsigned)i * 2654435761u ^ seed;
+    x ^= x >> 13; x *= 0x5bd1e995u; x ^= x >> 15;
+    p[i] = (bf16)(((x & 0xffff) / 65536.f - 0.5f) * scale);
+}
+__global__ void fill_f32(float* p, long long n, unsigned seed, float scale, float off) {
+    long long i = blockIdx.x * 256LL + threadIdx.x;
+    if (i >= n) return;
+    unsigned x = (unsigned)i * 2246822519u ^ seed;
+    x ^= x >> 13; x *= 0x5bd1e995u; x ^= x >> 15;
+    p[i] = off + ((x & 0xffff) / 65536.f - 0.5f) * scale;
+}
+
+template <int MODE, int VAR>
+float run(int M, int reps, const float* X, const float* g, const float* be, const bf16* Wp, const float* b1, const float* b2,
+          float* Xo, const float* gn, const float* bn, bf16* Xn, const bf16* O, const bf16* Fr, const float* bo,
+          const float* c1) {
+    CK(hipFuncSetAttribute((const void*)ffn2_kernel<MODE, VAR>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES));
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    for (int i = 0; i < 3; ++i)
+        hipLaunchKernelGGL((ffn2_kernel<MODE, VAR>), dim3((M + BM - 1) / BM), dim3(256), LDS_BYTES, 0, X, M, g, be, 1e-12f,
+                           Wp, b1, b2, Xo, gn, bn, Xn, O, Fr, bo, c1);
+    CK(hipEventRecord(a, 0));
+    for (int i = 0; i < reps; ++i)
+        hipLaunchKernelGGL((ffn2_kernel<MODE, VAR>), dim3((M + BM - 1) / BM), dim3(256), LDS_BYTES, 0, X, M, g, be, 1e-12f,
+                           Wp, b1, b2, Xo, gn, bn, Xn, O, Fr, bo, c1);
+    CK(hipEventRecord(b, 0));
+    CK(hipEventSynchronize(b));
+    float ms = 0;
+    CK(hipEventElapsedTime(&ms, a, b));
+    CK(hipGetLastError());
+    return ms * 1000.f / reps;
+}
+
+int main(int argc, char** argv) {
+    std::vector<int> Ms;
+    for (int i = 1; i < argc; ++i) Ms.push_back(atoi(argv[i]));
+    if (Ms.empty()) Ms = {16000, 32000};
+    const int Mmax = 32768;
+    const long long nx = (long long)Mmax * 512, nw = 262144 + 2097152;
+    float *X, *Xo, *vecs;
+    bf16 *Wp, *O, *Fr, *Xn;
+    CK(hipMalloc(&X, nx * 4));
+    CK(hipMalloc(&Xo, nx * 4));
+    CK(hipMalloc(&O, nx * 2));
+    CK(hipMalloc(&Fr, nx * 2));
+    CK(hipMalloc(&Xn, nx * 2));
+    CK(hipMalloc(&Wp, nw * 2));
+    CK(hipMalloc(&vecs, 16 * 2048 * 4));
+    hipLaunchKernelGGL(fill_f32, dim3((nx + 255) / 256), dim3(256), 0, 0, X, nx, 1u, 4.f, 0.f);
+    hipLaunchKernelGGL(fill_bf16, dim3((nx + 255) / 256), dim3(256), 0, 0, O, nx, 2u, 2.f);
+    hipLaunchKernelGGL(fill_bf16, dim3((nx + 255) / 256), dim3(256), 0, 0, Fr, nx, 3u, 1.f);
+    hipLaunchKernelGGL(fill_bf16, dim3((nw + 255) / 256), dim3(256), 0, 0, Wp, nw, 4u, 0.09f);
+    hipLaunchKernelGGL(fill_f32, dim3(16 * 2048 / 256), dim3(256), 0, 0, vecs, 16LL * 2048, 5u, 0.2f, 0.f);
+    CK(hipDeviceSynchronize());
+    const float *g = vecs, *be = vecs + 2048, *b1 = vecs + 4096, *b2 = vecs + 6144, *gn = vecs + 8192, *bn = vecs + 10240,
+                *bo = vecs + 12288, *c1 = vecs + 14336;
+    for (int M : Ms) {
+        const double fl1 = 2.0 * M * (2.0 * 512 * 2048 + 512.0 * 512), fl0 = 2.0 * M * 2.0 * 512 * 2048;
+        const int reps = 20;
+        float t;
+        t = run<1, 0>(M, reps, X, g, be, Wp, b1, b2, Xo, gn, bn, Xn, O, Fr, bo, c1);
+        printf("M=%6d OP   full        %8.1f us  %7.1f TF/s\n", M, t, fl1 / t / 1e6);
+        t = run<1, 1>(M, reps, X, g, be, Wp, b1, b2, Xo, gn, bn, Xn, O, Fr, bo, c1);
+        printf("M=%6d OP   no DMA      %8.1f us\n", M, t);
+        t = run<1, 4>(M, reps, X, g, be, Wp, b1, b2, Xo, gn, bn, Xn, O, Fr, bo, c1);
+        printf("M=%6d OP   L2-hot W    %8.1f us\n", M, t);
+        t = run<1, 2>(M, reps, X, g, be, Wp, b1, b2, Xo, gn, bn, Xn, O, Fr, bo, c1);
+        printf("M=%6d OP   no MFMA     %8.1f us\n", M, t);
+        t = run<1, 3>(M, reps, X, g, be, Wp, b1, b2, Xo, gn, bn, Xn, O, Fr, bo, c1);
+        printf("M=%6d OP   no DMA/bar  %8.1f us  %7.1f TF/s\n", M, t, fl1 / t / 1e6);
+        t = run<1, 7>(M, reps, X, g, be, Wp, b1, b2, Xo, gn, bn, Xn, O, Fr, bo, c1);
+        printf("M=%6d OP   AGPR phase1 %8.1f us\n", M, t);
+        t = run<1, 8>(M, reps, X, g, be, Wp, b1, b2, Xo, gn, bn, Xn, O, Fr, bo, c1);
+        printf("M=%6d OP   no H conv   %8.1f us\n", M, t);
+        t = run<1, 5>(M, reps, X, g, be, Wp, b1, b2, Xo, gn, bn, Xn, O, Fr, bo, c1);
+        printf("M=%6d OP   pro/epi     %8.1f us\n", M, t);
+        t = run<1, 6>(M, 5, X, g, be, Wp, b1, b2, Xo, gn, bn, Xn, O, Fr, bo, c1);
+        {
+            std::vector<unsigned long long> st(4096 * 16);
+            CK(hipMemcpyFromSymbol(st.data(), HIP_SYMBOL(ffn2_stamps), st.size() * 8));
+            const int nb = std::min(4096, (M + BM - 1) / BM);
+            // stamp ids in time order: 0 start, 1 prologue end, 2 phase-0 end, 6 x1 added, 7 LN2 stats, 3 transition end,
+            // 4 stream end, 8 outputs stored, 9 next-LN stats, 5 end
+            const int ord[10] = {0, 1, 2, 6, 7, 3, 4, 8, 9, 5};
+            const char* nm[9] = {"prologue", "phase0", "x1-add", "ln2-stats", "ln2-act", "chunks", "store-xo", "ln-stats",
+                                 "ln-store"};
+            double seg[9] = {0};
+            for (int b = 0; b < nb; ++b)
+                for (int k = 0; k < 9; ++k) seg[k] += (double)(st[b * 16 + ord[k + 1]] - st[b * 16 + ord[k]]);
+            printf("M=%6d OP   stamps (cycles/block):", M);
+            for (int k = 0; k < 9; ++k) printf(" %s %.0f", nm[k], seg[k] / nb);
+            printf("  (%.1f us kernel)\n", t);
+        }
+        t = run<0, 0>(M, reps, X, g, be, Wp + 262144, b1, b2, Xo, gn, bn, Xn, O, Fr, bo, c1);
+        printf("M=%6d FFN  full        %8.1f us  %7.1f TF/s\n", M, t, fl0 / t / 1e6);
+        t = run<2, 0>(M, reps, X, g, be, Wp + 262144, b1, b2, Xo, gn, bn, Xn, O, Fr, bo, c1);
+        printf("M=%6d DEC  full        %8.1f us  %7.1f TF/s\n", M, t, fl0 / t / 1e6);
+    }
+    return 0;
+}
