@@ -181,7 +181,8 @@ void pfm_knobs_refresh() {
     k.dec_ffn_fused = iv("PFM_DEC_FFN_FUSED", 1) != 0;
     k.ffn_hr = iv("PFM_FFN_HR", 1) != 0;
     k.ffn_pd = iv("PFM_FFN_PD", 3) == 2 ? 2 : 3;
-    k.ffn_kernel = iv("PFM_FFN_KERNEL", 2) == 1 ? 1 : 2;
+    k.ffn_kernel = iv("PFM_FFN_KERNEL", 1) == 2 ? 2 : 1;
+    k.dec_ffn_kernel = iv("PFM_DEC_FFN_KERNEL", 1) == 2 ? 2 : 1;
     const int* f = &k.ln_fold;
     unsigned long long s = 1469598103934665603ull;   // FNV-1a over the fields
     for (int i = 0; i < PFM_KNOB_FIELDS; ++i) s = (s ^ (unsigned long long)(unsigned)f[i]) * 1099511628211ull;
@@ -254,7 +255,8 @@ struct pfm_handle {
     DevBuf qkv0_pad;               // fast mode: layer 0's bf16 QKV weights with K padded to a multiple of 64
     DevBuf ffn_pack;               // fused-FFN weight tiles of every encoder layer (bf16, LDS-image order)
     bool ffn_ready = false;
-    int ffn_kind = 0;              // which fused-FFN kernel the packed weights (ffn_pack, dffn_pack) are ordered for
+    int ffn_kind = 0;              // which fused-FFN kernel the packed encoder weights (ffn_pack) are ordered for
+    int dffn_kind = 0;             // ... and the packed decoder weights (dffn_pack)
     DevBuf dffn_pack, dffn_c;      // decoder FFNs (16 blocks + decoders3): W1 | W2 diag(gamma_F) tiles; c1 | c2
     bool dffn_ready = false;
     DevBuf arena_x6;               // EXACT mode: three bf16 planes of every GEMM weight (x = x0 + x1 + x2)
@@ -492,17 +494,19 @@ int ensure_bf16(pfm_handle* h, hipStream_t st) {
         }
         h->fold_ready = true;
     }
-    const int fk = pfm_knobs().ffn_kernel;   // k_ffn.hip (1) and k_ffn2.hip (2) order their fragments differently
-    if (h->ffn_kind != fk) { h->ffn_ready = false; h->dffn_ready = false; h->ffn_kind = fk; }
+    // k_ffn.hip (1) and k_ffn2.hip (2) order their fragments differently; encoder and decoder choose separately
+    const int fk = pfm_knobs().ffn_kernel, dk = pfm_knobs().dec_ffn_kernel;
+    if (h->ffn_kind != fk) { h->ffn_ready = false; h->ffn_kind = fk; }
+    if (h->dffn_kind != dk) { h->dffn_ready = false; h->dffn_kind = dk; }
     auto pack = [&](const bf16* w1, const bf16* w2, bf16* wp) { return fk == 2 ? pfm_ffn2_pack(w1, w2, wp, st) : pfm_ffn_pack(w1, w2, wp, st); };
-    auto pack_o = [&](const bf16* wo, bf16* wp) { return fk == 2 ? pfm_ffn2_pack_o(wo, wp, st) : pfm_ffn_pack_o(wo, wp, st); };
+    auto pack_o = [&](int kind, const bf16* wo, bf16* wp) { return kind == 2 ? pfm_ffn2_pack_o(wo, wp, st) : pfm_ffn_pack_o(wo, wp, st); };
     if (!h->ffn_ready && ffn_shape_ok(h->cfg) && pfm_knobs().ffn_fused && !h->enc.empty()) {
         // per layer: the out-projection's 32 tiles, then the FFN's 256 (ffp = the FFN tiles)
         const size_t po = pfm_ffn_packed_o_elems(), per = po + pfm_ffn_packed_elems();
         HIP_TRY(h->ffn_pack.ensure(h->enc.size() * per * sizeof(bf16)));
         for (size_t l = 0; l < h->enc.size(); ++l) {
             h->enc[l].ffp = l * per + po;
-            HIP_TRY(pack_o(h->wb(h->enc[l].wo), h->ffn_pack.as<bf16>() + l * per));
+            HIP_TRY(pack_o(fk, h->wb(h->enc[l].wo), h->ffn_pack.as<bf16>() + l * per));
             HIP_TRY(pack(h->wb(h->enc[l].w1), h->wb(h->enc[l].w2), h->ffn_pack.as<bf16>() + l * per + po));
         }
         h->ffn_ready = true;
@@ -520,8 +524,8 @@ int ensure_bf16(pfm_handle* h, hipStream_t st) {
             const size_t w1 = d3 ? h->d3w1 : h->dec[j].w1, w2 = d3 ? h->d3w2 : h->dec[j].w2;
             const size_t gF = d3 ? h->d3ng : h->dec[j].ng, bF = d3 ? h->d3nb : h->dec[j].nb;
             float* cc = h->dffn_c.as<float>() + (size_t)j * 2 * D;
-            if (j > 0) HIP_TRY(pack_o(h->wb(h->dec[j - 1].wo), h->dffn_pack.as<bf16>() + (size_t)j * per));
-            HIP_TRY((fk == 2 ? pfm_ffn2_pack_dec : pfm_ffn_pack_dec)(h->wb(w1), h->w(w2), h->w(gF), h->w(bF),
+            if (j > 0) HIP_TRY(pack_o(dk, h->wb(h->dec[j - 1].wo), h->dffn_pack.as<bf16>() + (size_t)j * per));
+            HIP_TRY((dk == 2 ? pfm_ffn2_pack_dec : pfm_ffn_pack_dec)(h->wb(w1), h->w(w2), h->w(gF), h->w(bF),
                                      h->dffn_pack.as<bf16>() + (size_t)j * per + po, cc, cc + D, st));
         }
         h->dffn_ready = true;
@@ -1461,11 +1465,11 @@ int pfm_run(pfm_handle* h, void* stream, int mode, const float* feats, const int
                 const size_t po = pfm_ffn_packed_o_elems();
                 const bf16* blk = h->dffn_pack.as<bf16>() + (size_t)fi * (po + pfm_ffn_packed_elems());
                 if (op_from >= 0) {   // x = x + O Wo^T + bo of block op_from, then the FFN on it
-                    HIP_TRY((h->ffn_kind == 2 ? pfm_ffn2_fused_dec : pfm_ffn_fused_dec)(Xd, Mg, P(lng), P(lnb), c.ln_eps, blk, P(b1), cc, cc + D, Xd, P(pg),
+                    HIP_TRY((h->dffn_kind == 2 ? pfm_ffn2_fused_dec : pfm_ffn_fused_dec)(Xd, Mg, P(lng), P(lnb), c.ln_eps, blk, P(b1), cc, cc + D, Xd, P(pg),
                                               P(pb), (bf16*)pout, Odb, P(h->dec[op_from].bo), s));
                     op_from = -1;
                 } else {
-                    HIP_TRY((h->ffn_kind == 2 ? pfm_ffn2_fused_dec : pfm_ffn_fused_dec)(Xd, Mg, P(lng), P(lnb), c.ln_eps, blk + po, P(b1), cc, cc + D, nullptr,
+                    HIP_TRY((h->dffn_kind == 2 ? pfm_ffn2_fused_dec : pfm_ffn_fused_dec)(Xd, Mg, P(lng), P(lnb), c.ln_eps, blk + po, P(b1), cc, cc + D, nullptr,
                                               P(pg), P(pb), (bf16*)pout, nullptr, nullptr, s));
                 }
                 return PFM_OK;
@@ -1899,7 +1903,7 @@ int pfm_op_ffn_dec(void* stream, const float* x, int M, const float* g1, const f
     HIP_TRY(sc.alloc(&wob, no));
     HIP_TRY(sc.alloc(&wp, po + pfm_ffn_packed_elems()));
     HIP_TRY(sc.alloc(&cc, (size_t)2 * 512));
-    const bool k2 = pfm_knobs().ffn_kernel == 2;
+    const bool k2 = pfm_knobs().dec_ffn_kernel == 2;
     HIP_TRY(pfm_f32_to_bf16(W1, w1b, (long long)nw, st));
     if (o) {
         HIP_TRY(pfm_f32_to_bf16(Wo, wob, (long long)no, st));

@@ -161,9 +161,11 @@ struct PfmKnobs {
     int dec_ffn_fused;      // PFM_DEC_FFN_FUSED (default 1): decoder LN1-FFN(LN_F folded)-LN kernel (fast mode)
     int ffn_hr;             // PFM_FFN_HR (default 1): fused FFN phase 0/2 activation fragments read once per k step
     int ffn_pd;             // PFM_FFN_PD (default 3): fused FFN weight tiles in flight behind the published one (2 or 3)
-    int ffn_kernel;         // PFM_FFN_KERNEL (default 2): fused FFN as 128-row workgroups (k_ffn2.hip); 1 = k_ffn.hip
+    int ffn_kernel;         // PFM_FFN_KERNEL (default 1): encoder fused FFN as 64-row workgroups (k_ffn.hip);
+                            // 2 = 128-row workgroups (k_ffn2.hip; pays only when M / 128 fills the chip)
+    int dec_ffn_kernel;     // PFM_DEC_FFN_KERNEL (default 1): the same choice for the decoder FFN
     unsigned long long sig;
 };
-#define PFM_KNOB_FIELDS 27
+#define PFM_KNOB_FIELDS 28
 const PfmKnobs& pfm_knobs();   // the calling thread's snapshot (refreshed lazily if no entry point did yet)
 void pfm_knobs_refresh();

@@ -40,8 +40,10 @@ enum pfm_status {
 enum pfm_dtype { PFM_F32 = 0, PFM_BF16 = 1 };
 
 /* Numerics mode of pfm_run.
- *  EXACT: every contraction on v_mfma_f32_32x32x2_f32 (exact f32 FMA chains), softmax /
- *         LayerNorm / CIF in f32 (f64 reductions) — the token-ID parity mode.
+ *  EXACT: every GEMM and the attention as split-bf16 x6 MFMA (each f32 operand split into
+ *         three bf16 planes x = x0+x1+x2, the six products above 2^-24 relative summed in
+ *         f32 — f32-equivalent contractions; PFM_EXACT_X6=0 selects v_mfma_f32_32x32x2_f32),
+ *         softmax / LayerNorm / CIF in f32 (f64 reductions) — the token-ID parity mode.
  *  FAST : bf16 MFMA operands with f32 accumulation; f32 residual stream, LayerNorm,
  *         softmax statistics and CIF — the throughput mode.                              */
 enum pfm_mode { PFM_MODE_EXACT = 0, PFM_MODE_FAST = 1 };

@@ -352,7 +352,7 @@ def test_ffn_fused_outproj(dev, M, resid, kern, monkeypatch):
       x2 = x1 + h W2^T + b2,  xn = LN1_next(x2).
     Tolerances: the FFN increment x2 - x1 rel-L2 < 5e-3 (f32 accumulation order flips a few bf16 roundings of
     a / h), x2 rel < 1e-4, xn within 1.6e-2 abs of LN1_next of the kernel's own x2 (one bf16 ulp at |v| <= 4).
-    Both fused kernels: k_ffn.hip (64 rows per workgroup, PFM_FFN_KERNEL=1) and k_ffn2.hip (128, the default)."""
+    Both fused kernels: k_ffn.hip (64 rows per workgroup, PFM_FFN_KERNEL=1, the default) and k_ffn2.hip (128)."""
     monkeypatch.setenv("PFM_FFN_KERNEL", kern)
     g = torch.Generator().manual_seed(31 * M + resid)
     p = _ffn_params(g)
@@ -396,8 +396,8 @@ def test_ffn_fused_decoder(dev, M, outproj, kern, monkeypatch):
     W2, next LayerNorm epilogue; with outproj the previous block's cross-attention out-projection as phase 0,
     x1 = x + o Wo^T + bo written back) vs fp64 on the kernel's bf16 roundings: y rel-L2 < 5e-3 (and < 2e-2 vs
     the unrounded W2 LN_F(h)), xn within 1.6e-2 of LN_next of the fp64 y plus the y error; x1 rel < 1e-6.
-    Both fused kernels (PFM_FFN_KERNEL 1 / 2)."""
-    monkeypatch.setenv("PFM_FFN_KERNEL", kern)
+    Both fused kernels (PFM_DEC_FFN_KERNEL 1 / 2)."""
+    monkeypatch.setenv("PFM_DEC_FFN_KERNEL", kern)
     g = torch.Generator().manual_seed(17 * M + outproj)
     p = _ffn_params(g, dec=True)
     x = torch.randn(M, 512, generator=g) * 2
