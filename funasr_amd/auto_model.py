@@ -8,8 +8,9 @@ Mirrors funasr/auto/auto_model.py:
                                      speed stats, results in input order
 Differences (by design): device defaults to the GPU and there is no CPU path; hub names are
 not fetched (no network); VAD/punctuation/speaker pipelines are not built.
-Multi-GPU: when torch.distributed is initialised with world > 1, inference() shards the
-utterances over ranks (funasr_amd.distributed.shard_range) and all-gathers the results.
+Multi-GPU: when torch.distributed is initialised with world > 1, inference() deals the
+utterances over ranks longest-first (funasr_amd.distributed.length_sorted_shards) and all-gathers
+the results back into input order.
 """
 from __future__ import annotations
 
@@ -317,29 +318,32 @@ class AutoModel:
         world, rank = 1, 0
         if torch.distributed.is_available() and torch.distributed.is_initialized() and kwargs.get("dp", True):
             world, rank = torch.distributed.get_world_size(), torch.distributed.get_rank()
-        lo, hi = 0, len(items)
-        if world > 1 and len(items) > 1:
-            from .distributed import shard_range
-            lo, hi = shard_range(len(items), world, rank)
+        dp = world > 1 and len(items) > 1
+        mine = list(range(len(items)))
+        if dp:   # longest-first round-robin: balanced padded work per rank
+            from .distributed import item_lengths, length_sorted_shards
+            mine = length_sorted_shards(item_lengths(items), world)[rank]
         results = []
         speech_s, wall_s = 0.0, 0.0
-        for beg in range(lo, hi, batch_size):
-            end = min(hi, beg + batch_size)
-            batch = {"data_in": items[beg:end], "key": keys[beg:end]}
-            if end - beg == 1 and kwargs.get("data_type") == "fbank":
-                batch["data_in"] = items[beg]
+        for beg in range(0, len(mine), batch_size):
+            idx = mine[beg:beg + batch_size]
+            batch = {"data_in": [items[i] for i in idx], "key": [keys[i] for i in idx]}
+            if len(idx) == 1 and kwargs.get("data_type") == "fbank":
+                batch["data_in"] = items[idx[0]]
                 batch["data_lengths"] = input_len
             t1 = time.perf_counter()
             with torch.no_grad():
                 res = model.inference(**batch, **{k: v for k, v in kwargs.items() if k not in ("key",)})
             t2 = time.perf_counter()
             out, meta = (res[0], res[1]) if isinstance(res, (list, tuple)) and len(res) > 1 else (res, {})
-            results.extend(out)
+            if dp and len(out) != len(idx):
+                raise RuntimeError(f"data-parallel inference: {len(out)} results for {len(idx)} inputs")
+            results.extend(zip(idx, out) if dp else out)
             bt = meta.get("batch_data_time", -1)
             speech_s += bt if bt > 0 else 0.0
             wall_s += t2 - t1
         self.last_speed = {"rtf": (wall_s / speech_s) if speech_s > 0 else None, "forward_s": wall_s}
-        if world > 1 and len(items) > 1:
+        if dp:   # (input index, result) pairs from every rank -> input order
             from .distributed import gather_results
-            results = gather_results(results)
+            results = [r for _, r in sorted(gather_results(results), key=lambda p: p[0])]
         return results

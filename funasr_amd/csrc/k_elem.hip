@@ -731,6 +731,16 @@ __global__ __launch_bounds__(256) void ln_fold_kernel(const float* __restrict__ 
     }
 }
 
+// [A][Bd][C] -> [A][C][Bd] (weight re-layout of device-resident state_dict tensors: Conv1d [O][I][k] -> [O][k][I],
+// depthwise taps [D][1][K] -> [K][D]); one thread per output element, coalesced stores
+__global__ void swap_last2_kernel(const float* __restrict__ x, float* __restrict__ y, long long A, long long Bd,
+                                  long long C) {
+    const long long i = blockIdx.x * 256LL + threadIdx.x, n = A * Bd * C;
+    if (i >= n) return;
+    const long long b = i % Bd, c = (i / Bd) % C, a = i / (Bd * C);
+    y[i] = x[(a * Bd + b) * C + c];
+}
+
 }  // namespace
 
 hipError_t pfm_ln_fold(const float* W, int N, int K, const float* gamma, const float* beta, const float* bias, bf16* Wf,
@@ -1003,6 +1013,14 @@ hipError_t pfm_f32_to_bf16(const float* x, bf16* y, long long n, hipStream_t st)
     if (n <= 0) return hipSuccess;
     const long long nt = (n + 3) / 4;
     hipLaunchKernelGGL(f32_to_bf16_kernel, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, st, x, y, n);
+    PFM_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+hipError_t pfm_swap_last2(const float* x, float* y, long long A, long long Bd, long long C, hipStream_t st) {
+    const long long n = A * Bd * C;
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(swap_last2_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, x, y, A, Bd, C);
     PFM_LAUNCH_CHECK();
     return hipSuccess;
 }

@@ -107,15 +107,16 @@ __global__ __launch_bounds__(C::NT) void gemm_bf16_kernel(const bf16* __restrict
     // split-bf16 emulation of an f32 GEMM (epi.x6_k > 0): K step k0 of the K' = 6 x6_k loop reads A
     // segment pa = {2,1,0,1,0,0}[s] and W plane pw = {0,1,2,0,1,0}[s] of segment s = k0 / x6_k (a K step
     // never straddles segments: x6_k % BK == 0). Small products first.
-    const int xk = epi.x6_k;
+    // bf16x3 (x6_terms 3): segments 3..5 only.
+    const int xk = epi.x6_k, sg0 = epi.x6_terms == 3 ? 3 : 0;
     auto koff_a = [&](int k0) -> int {
         if (!xk) return k0;
-        const int sg = k0 / xk, kk = k0 - sg * xk;
+        const int s0 = k0 / xk, kk = k0 - s0 * xk, sg = s0 + sg0;
         return (sg == 0 ? 2 : (sg == 1 || sg == 3) ? 1 : 0) * xk + kk;
     };
     auto koff_w = [&](int k0) -> long long {
         if (!xk) return k0;
-        const int sg = k0 / xk, kk = k0 - sg * xk;
+        const int s0 = k0 / xk, kk = k0 - s0 * xk, sg = s0 + sg0;
         return (long long)(sg == 1 || sg == 4 ? 1 : sg == 2 ? 2 : 0) * epi.x6_ws + kk;
     };
     auto stage = [&](int k0, int s) {
@@ -1370,7 +1371,7 @@ hipError_t pfm_gemm_bf16_256(const void* A, RowMap amap, const void* W, long lon
     if (pfm_knobs().gemm_policy == 6 && cfg == 15 && !ln) cfg = 18;
     if (epi.x6_k && cfg != 1 && cfg != 3 && cfg != 4 && cfg != 13 && cfg != 15 && cfg != 16 && cfg != 17 && cfg != 18)
         cfg = 15;
-    if (epi.x6_k && (K != 6 * epi.x6_k || epi.x6_k % 64 || ln)) return hipErrorInvalidValue;
+    if (epi.x6_k && (K != (epi.x6_terms == 3 ? 3 : 6) * epi.x6_k || epi.x6_k % 64 || ln)) return hipErrorInvalidValue;
     switch (cfg) {
         case 2: return launch<C2>(A, amap, W, ldw, M, N, K, e2, st);
         case 3: return launch<C3>(A, amap, W, ldw, M, N, K, e2, st);

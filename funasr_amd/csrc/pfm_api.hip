@@ -64,6 +64,7 @@ hipError_t pfm_sv_input(const float* feats, const int* lens, const float* embed,
 hipError_t pfm_ctc_collapse(const int* ids, long long ld, const int* olen, int B, int blank, int Lcap, int* tokens,
                             int* ntok, hipStream_t st);
 hipError_t pfm_f32_to_bf16(const float* x, bf16* y, long long n, hipStream_t st);
+hipError_t pfm_swap_last2(const float* x, float* y, long long A, long long Bd, long long C, hipStream_t st);
 size_t pfm_ffn_packed_elems();
 hipError_t pfm_split3_rows(const float* x, RowMap xm, int M, int K, int Kp, bf16* out, hipStream_t st);
 hipError_t pfm_split3_planes(const float* x, bf16* p, long long plane, long long n, hipStream_t st);
@@ -183,6 +184,7 @@ void pfm_knobs_refresh() {
     k.ffn_pd = iv("PFM_FFN_PD", 3) == 2 ? 2 : 3;
     k.ffn_kernel = iv("PFM_FFN_KERNEL", 1) == 2 ? 2 : 1;
     k.dec_ffn_kernel = iv("PFM_DEC_FFN_KERNEL", 1) == 2 ? 2 : 1;
+    k.exact_terms = iv("PFM_EXACT_TERMS", 6) == 3 ? 3 : 6;
     const int* f = &k.ln_fold;
     unsigned long long s = 1469598103934665603ull;   // FNV-1a over the fields
     for (int i = 0; i < PFM_KNOB_FIELDS; ++i) s = (s ^ (unsigned long long)(unsigned)f[i]) * 1099511628211ull;
@@ -734,13 +736,15 @@ GemmEpi epi_default() {
 hipError_t gemm_x6(pfm_handle* h, const float* A, RowMap am, const float* W, int M, int N, int K, const GemmEpi& e,
                    hipStream_t s, const bf16* A3 = nullptr) {
     if (M <= 0 || N <= 0) return hipSuccess;
+    const int terms = pfm_knobs().exact_terms;   // 6 (f32-equivalent) or 3 (bf16x3)
     if (A3) {   // the producer already wrote [A0 | A1 | A2] (DT_X3 rows, am.ld = 3K)
         if (K % 64) return hipErrorInvalidValue;
         GemmEpi e2 = e;
         e2.x6_k = K;
         e2.x6_ws = (long long)h->arena_elems;
+        e2.x6_terms = terms;
         const size_t off = (size_t)(W - h->arena.as<float>());
-        return pfm_gemm_bf16_256(A3, am, h->arena_x6.as<bf16>() + off, K, M, N, 6 * K, e2, s);
+        return pfm_gemm_bf16_256(A3, am, h->arena_x6.as<bf16>() + off, K, M, N, terms * K, e2, s);
     }
     auto& sc = h->x6_scratch[s];
     if (!sc) {
@@ -774,7 +778,8 @@ hipError_t gemm_x6(pfm_handle* h, const float* A, RowMap am, const float* W, int
     GemmEpi e2 = e;
     e2.x6_k = Kp;
     e2.x6_ws = ws;
-    return pfm_gemm_bf16_256(sc->p, rowmap_plain(3LL * Kp), planes, Kp == K ? K : 3LL * Kp, M, N, 6 * Kp, e2, s);
+    e2.x6_terms = terms;
+    return pfm_gemm_bf16_256(sc->p, rowmap_plain(3LL * Kp), planes, Kp == K ? K : 3LL * Kp, M, N, terms * Kp, e2, s);
 }
 
 // Per-call launch context shared by the Paraformer and SenseVoice pipelines: numerics mode,
@@ -1243,6 +1248,17 @@ void pfm_destroy(pfm_handle* h) {
     delete h;
 }
 
+// a weight changed: every derived copy (bf16 arena, LN folds, packed FFN tiles, x6 planes, banned-token bias) is stale
+static void weight_written(pfm_handle* h, WEntry& e) {
+    if (!e.set) { e.set = true; h->missing--; }
+    h->bf_ready = false;
+    h->fold_ready = false;
+    h->ffn_ready = false;
+    h->dffn_ready = false;
+    h->x6_ready = false;   // ensure_x6 re-splits arena_x6 and the padded planes in place (stable addresses)
+    h->ban_tok = -1;   // the banned-token bias copy follows ctc.ctc_lo.bias
+}
+
 int pfm_set_weight(pfm_handle* h, const char* name, const void* host_ptr, int dtype, const int64_t* shape,
                    int ndim) {
     pfm_knobs_refresh();
@@ -1274,13 +1290,36 @@ int pfm_set_weight(pfm_handle* h, const char* name, const void* host_ptr, int dt
         src = tmp.data();
     }
     HIP_TRY(hipMemcpy(h->w(e.off), src, e.numel * 4, hipMemcpyHostToDevice));
-    if (!e.set) { e.set = true; h->missing--; }
-    h->bf_ready = false;
-    h->fold_ready = false;
-    h->ffn_ready = false;
-    h->dffn_ready = false;
-    h->x6_ready = false;   // ensure_x6 re-splits arena_x6 and the padded planes in place (stable addresses)
-    h->ban_tok = -1;   // the banned-token bias copy follows ctc.ctc_lo.bias
+    weight_written(h, e);
+    return PFM_OK;
+}
+
+int pfm_set_weight_device(pfm_handle* h, const char* name, const void* dev_ptr, int dtype, const int64_t* shape,
+                          int ndim, void* stream) {
+    pfm_knobs_refresh();
+    if (!h || !name || !dev_ptr || !shape) return fail(PFM_E_ARG, "pfm_set_weight_device: null argument");
+    if (dtype != PFM_F32) return fail(PFM_E_ARG, "pfm_set_weight_device: only PFM_F32 tensors are accepted");
+    if ((uintptr_t)dev_ptr % 4) return fail(PFM_E_ARG, "pfm_set_weight_device: source must be 4-B aligned");
+    auto it = h->reg.find(name);
+    if (it == h->reg.end()) return fail(PFM_E_NAME, std::string("pfm_set_weight_device: unknown key ") + name);
+    WEntry& e = it->second;
+    if ((int)e.shape.size() != ndim)
+        return fail(PFM_E_ARG, std::string("pfm_set_weight_device: rank mismatch for ") + name);
+    for (int i = 0; i < ndim; ++i)
+        if (e.shape[i] != shape[i])
+            return fail(PFM_E_ARG, std::string("pfm_set_weight_device: shape mismatch for ") + name);
+    if (e.kind == 2) return PFM_OK;
+    HIP_TRY(hipSetDevice(h->device));
+    const hipStream_t st = (hipStream_t)stream;
+    const float* src = (const float*)dev_ptr;
+    if (e.kind == 1)        // Conv1d [O][I][k] -> [O][k][I] (as pfm_set_weight, on the device)
+        HIP_TRY(pfm_swap_last2(src, h->w(e.off), e.shape[0], e.shape[1], e.shape[2], st));
+    else if (e.kind == 3)   // depthwise taps [D][1][K] -> [K][D]
+        HIP_TRY(pfm_swap_last2(src, h->w(e.off), 1, e.shape[0], e.shape[2], st));
+    else
+        HIP_TRY(hipMemcpyAsync(h->w(e.off), src, e.numel * 4, hipMemcpyDeviceToDevice, st));
+    HIP_TRY(hipStreamSynchronize(st));   // the caller may free / reuse its buffer on return
+    weight_written(h, e);
     return PFM_OK;
 }
 

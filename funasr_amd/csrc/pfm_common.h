@@ -113,8 +113,11 @@ struct GemmEpi {
     // three-way split bf16 emulation of an f32 GEMM (EXACT mode, bf16 256-tile kernel): A = [A0 | A1 | A2]
     // ([M, 3 x6_k], x = x0 + x1 + x2 exactly), W = three bf16 planes x6_ws elements apart; the kernel runs
     // K' = 6 x6_k over the segments (A2,W0) (A1,W1) (A0,W2) (A1,W0) (A0,W1) (A0,W0). 0 = plain GEMM.
+    // x6_terms 3 (bf16x3): only the last three segments (A1,W0) (A0,W1) (A0,W0), K' = 3 x6_k (relative
+    // error ~2^-16 instead of ~2^-24); 0 / 6 = all six.
     int x6_k;
     long long x6_ws;
+    int x6_terms;
 };
 
 static inline bool rowmap_vec4(const RowMap& m) {
@@ -164,8 +167,9 @@ struct PfmKnobs {
     int ffn_kernel;         // PFM_FFN_KERNEL (default 1): encoder fused FFN as 64-row workgroups (k_ffn.hip);
                             // 2 = 128-row workgroups (k_ffn2.hip; pays only when M / 128 fills the chip)
     int dec_ffn_kernel;     // PFM_DEC_FFN_KERNEL (default 1): the same choice for the decoder FFN
+    int exact_terms;        // PFM_EXACT_TERMS (default 6): products per EXACT-mode split-bf16 GEMM; 3 = bf16x3
     unsigned long long sig;
 };
-#define PFM_KNOB_FIELDS 28
+#define PFM_KNOB_FIELDS 29
 const PfmKnobs& pfm_knobs();   // the calling thread's snapshot (refreshed lazily if no entry point did yet)
 void pfm_knobs_refresh();

@@ -9,6 +9,9 @@ independent. So the only collectives are
 The timed benchmark step has no collective at all: each rank decodes its own shard.
 The reference's only multi-GPU inference is one process per GPU over a split scp list
 (examples/aishell/paraformer/run.sh:136-170); `shard_range` is that split, in-process.
+AutoModel.inference deals utterances longest-first round-robin instead (`length_sorted_shards`
+over `item_lengths`), so every rank gets a similar amount of padded audio, and all-gathers
+(index, result) pairs to restore the input order.
 """
 from __future__ import annotations
 
@@ -30,12 +33,33 @@ def length_sorted_shards(lengths: Sequence[int], world: int) -> List[List[int]]:
     return [order[r::world].tolist() for r in range(world)]
 
 
-def broadcast_state_dict(layout, sd: Optional[Dict[str, np.ndarray]], device=None, src: int = 0):
+def item_lengths(items: Sequence) -> List[int]:
+    """Cheap per-item work estimate for sharding without decoding anything: samples / frames of
+    in-memory arrays, the byte size of files and byte strings, 0 when unknown."""
+    import os
+    out = []
+    for x in items:
+        if hasattr(x, "shape") and len(getattr(x, "shape", ())) > 0:
+            out.append(int(x.shape[0]))
+        elif isinstance(x, (bytes, bytearray)):
+            out.append(len(x))
+        elif isinstance(x, str) and os.path.isfile(x):
+            out.append(int(os.path.getsize(x)))
+        elif isinstance(x, (list, tuple)):
+            out.append(len(x))
+        else:
+            out.append(0)
+    return out
+
+
+def broadcast_state_dict(layout, sd: Optional[Dict[str, np.ndarray]], device=None, src: int = 0,
+                         keep_on_device: bool = False):
     """Broadcast a state_dict from `src` as ONE flat fp32 tensor; returns it on every rank.
 
     layout: [(key, shape, ...)] in a fixed order known to all ranks (weights.param_layout).
     sd: the dict on `src` (ignored elsewhere). device: torch device of the collective
-    (cuda for RCCL, cpu for gloo).
+    (cuda for RCCL, cpu for gloo). keep_on_device: return the flat tensor itself (for
+    PfmEngine.load_flat_device: no device -> host -> device round trip) instead of a host dict.
     """
     import torch
     import torch.distributed as dist
@@ -52,6 +76,8 @@ def broadcast_state_dict(layout, sd: Optional[Dict[str, np.ndarray]], device=Non
             off += n
         flat.copy_(torch.from_numpy(host))
     dist.broadcast(flat, src)
+    if keep_on_device:
+        return flat
     host = flat.cpu().numpy() if dev.type != "cpu" else flat.numpy()
     out, off = {}, 0
     for (k, s, *_), n in zip(layout, sizes):

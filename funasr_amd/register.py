@@ -37,6 +37,8 @@ def install_into_funasr() -> bool:
         from funasr.register import tables as ref_tables  # type: ignore
     except Exception:
         return False
+    # the model modules register themselves on import (lazy in funasr_amd/__init__.py)
+    from . import model, punc, sense_voice, streaming, vad  # noqa: F401
     for table in ("model_classes", "frontend_classes", "tokenizer_classes"):
         for k, cls in getattr(tables, table).items():
             ref_tables.register(table, k)(cls)

@@ -23,7 +23,7 @@ MODE_EXACT, MODE_FAST = 0, 1
 MODES = {"exact": MODE_EXACT, "fp32": MODE_EXACT, "fast": MODE_FAST, "bf16": MODE_FAST}
 
 # every symbol include/pfm.h declares (checked by tests/test_abi.py)
-ABI_SYMBOLS = ("pfm_config_default", "pfm_config_sensevoice", "pfm_create", "pfm_set_weight",
+ABI_SYMBOLS = ("pfm_config_default", "pfm_config_sensevoice", "pfm_create", "pfm_set_weight", "pfm_set_weight_device",
                "pfm_missing_weights", "pfm_reserve", "pfm_run", "pfm_run_ctc", "pfm_op_ctc_collapse", "pfm_fbank", "pfm_lfr_frames", "pfm_last_error", "pfm_destroy", "pfm_op_gemm",
                "pfm_op_attention", "pfm_op_layernorm", "pfm_op_fsmn", "pfm_op_cif", "pfm_profile", "pfm_op_gemm_layernorm", "pfm_op_ffn", "pfm_op_ffn_op", "pfm_op_ffn_dec", "pfm_op_fsmn_bf16", "pfm_op_layernorm_bf16",
                "pfm_profile_read", "pfm_streams_create", "pfm_streams_reset", "pfm_stream_step",
@@ -95,6 +95,7 @@ def load_library(path: Optional[str] = None) -> ctypes.CDLL:
     lib.pfm_op_ctc_collapse.argtypes = [vp, i32p, ctypes.c_int64, i32p, i32, i32, i32p, i32, i32p]
     lib.pfm_create.argtypes = [ctypes.POINTER(PfmConfig), i32, ctypes.POINTER(vp)]
     lib.pfm_set_weight.argtypes = [vp, ctypes.c_char_p, vp, i32, ctypes.POINTER(ctypes.c_int64), i32]
+    lib.pfm_set_weight_device.argtypes = [vp, ctypes.c_char_p, vp, i32, ctypes.POINTER(ctypes.c_int64), i32, vp]
     lib.pfm_missing_weights.argtypes = [vp]
     lib.pfm_reserve.argtypes = [vp, i32, i32]
     lib.pfm_run.argtypes = [vp, vp, i32, f32p, i32p, i32, i32, i32p, i32, i32p, f32p, f32p, f32p]
@@ -212,6 +213,30 @@ class PfmEngine:
         miss = self.lib.pfm_missing_weights(self.h)
         if strict and miss:
             raise PfmError(f"{miss} required weights missing after load_state_dict")
+
+    def load_flat_device(self, flat, layout, strict: bool = True) -> None:
+        """Weights from ONE flat f32 device tensor on this engine's GPU, packed in `layout` order
+        ([(key, shape, ...)], weights.param_layout) — e.g. the buffer a data-parallel rank received by
+        RCCL broadcast (distributed.broadcast_state_dict(keep_on_device=True)). pfm_set_weight_device per
+        key: device-to-device copies, nothing round-trips through the host."""
+        torch = self.torch
+        if flat.device.type != "cuda" or flat.device.index != self.device or flat.dtype != torch.float32:
+            raise PfmError(f"load_flat_device: need an f32 tensor on cuda:{self.device}, got {flat.dtype} on {flat.device}")
+        flat = flat.contiguous()
+        stream = torch.cuda.current_stream(flat.device).cuda_stream
+        off = 0
+        for k, shp, *_ in layout:
+            n = int(np.prod(shp))
+            if off + n > flat.numel():
+                raise PfmError(f"load_flat_device: buffer of {flat.numel()} floats ends inside {k}")
+            shape = (ctypes.c_int64 * len(shp))(*shp)
+            check(self.lib.pfm_set_weight_device(self.h, k.encode(), ctypes.c_void_p(flat.data_ptr() + 4 * off),
+                                                 PFM_F32, shape, len(shp), ctypes.c_void_p(stream)),
+                  f"pfm_set_weight_device({k})")
+            off += n
+        miss = self.lib.pfm_missing_weights(self.h)
+        if strict and miss:
+            raise PfmError(f"{miss} required weights missing after load_flat_device")
 
     @property
     def missing_weights(self) -> int:

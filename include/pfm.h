@@ -100,6 +100,13 @@ int pfm_create(const pfm_config* cfg, int device, pfm_handle** out);
 int pfm_set_weight(pfm_handle* h, const char* name, const void* host_ptr, int dtype,
                    const int64_t* shape, int ndim);
 
+/* Same contract as pfm_set_weight with the tensor already in device memory of the handle's GPU
+ * (e.g. a slice of the flat buffer a data-parallel rank received by RCCL broadcast, so the weights
+ * never round-trip through the host). Copies on `stream` (a hipStream_t; NULL = default stream) and
+ * returns after the copy completed, so the caller may reuse its buffer. */
+int pfm_set_weight_device(pfm_handle* h, const char* name, const void* dev_ptr, int dtype,
+                          const int64_t* shape, int ndim, void* stream);
+
 /* Number of required weights still missing (0 when pfm_run may be called). */
 int pfm_missing_weights(const pfm_handle* h);
 

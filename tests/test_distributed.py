@@ -76,3 +76,54 @@ def test_gloo_world2_broadcast_and_gather():
         assert sd == want
         assert [r["key"] for r in allres] == [f"u{i}" for i in range(11)]
         assert [r["rank"] for r in allres] == [0] * 6 + [1] * 5
+
+
+class _EchoModel:
+    """Stands in for the HIP model inside AutoModel.inference: one result per input, tagged with the rank."""
+
+    def eval(self):
+        return self
+
+    def inference(self, data_in, key=None, **kw):
+        rank = dist.get_rank() if dist.is_initialized() else 0
+        return [{"key": k, "n": int(len(x)), "rank": rank} for k, x in zip(key, data_in)], {}
+
+
+def _infer_worker(rank, world, port, items, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from funasr_amd.auto_model import AutoModel
+        am = AutoModel.__new__(AutoModel)
+        am.kwargs, am.model = {"batch_size": 2}, _EchoModel()
+        q.put((rank, am.inference(items, key=None)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world2_automodel_inference_length_sorted_order_restored():
+    """AutoModel.inference under world 2: longest-first round-robin shards (both ranks get similar padded
+    work), results all-gathered back into input order; identical to the one-process run minus the rank tag."""
+    from funasr_amd.auto_model import AutoModel
+    lens = [500, 83, 431, 500, 120, 300, 222, 17, 260]
+    items = [np.zeros(n, np.float32) for n in lens]
+    single = AutoModel.__new__(AutoModel)
+    single.kwargs, single.model = {"batch_size": 2}, _EchoModel()
+    want = [{k: v for k, v in r.items() if k != "rank"} for r in single.inference(items)]
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_infer_worker, args=(r, world, port, items, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, res in out:
+        assert [r["n"] for r in res] == lens
+        assert [{k: v for k, v in r.items() if k not in ("rank", "key")} for r in res] == \
+            [{k: v for k, v in r.items() if k != "key"} for r in want]
+        per_rank = [sum(r["n"] for r in res if r["rank"] == k) for k in range(world)]
+        assert abs(per_rank[0] - per_rank[1]) <= max(lens)
+        assert {r["rank"] for r in res if r["n"] == 500} == {0, 1}   # the two longest go to different ranks

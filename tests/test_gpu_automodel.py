@@ -1,0 +1,210 @@
+"""AutoModel on the HIP path, end to end:
+  * waveform input: the model alone is token-exact against the oracle fed the GPU's own pfm_fbank features,
+    and the frontend's <= 2e-4 log-mel difference from knf is priced separately (token flips only where the
+    oracle's own top-2 margin is small);
+  * a local model dir (config.yaml + model.pt + tokens.json + am.mvn; download_model_from_hub.py:60-79,
+    load_pretrained_model.py:44-47) decodes exactly like the same weights given by seed;
+  * data parallel: two gloo ranks sharing cuda:0 (spawned, so no GPU state is inherited) decode a ragged
+    list of wav files with length-sorted sharding, and the gathered results equal the one-rank run.
+"""
+import json
+import os
+import socket
+import wave
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from funasr_amd.config import paraformer_tiny  # noqa: E402
+from oracle import fbank_ref  # noqa: E402
+from tests.golden.inputs import token_list, waveform  # noqa: E402
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+FLIP_MARGIN = 0.5   # nat: a frontend-induced token flip must sit at an oracle top-2 log-prob margin below this
+
+
+def _automodel(**extra):
+    from funasr_amd.auto_model import AutoModel
+    kw = paraformer_tiny().reference_kwargs()
+    kw.update(extra)
+    return AutoModel(model="Paraformer", model_conf=dict(ctc_weight=0.0, predictor_bias=1), synthetic_seed=0,
+                     device="cuda", mode="exact", **kw)
+
+
+def _write_wav(path, x):
+    q = np.clip(np.round(x * 32768.0), -32768, 32767).astype("<i2")
+    with wave.open(str(path), "wb") as w:
+        w.setnchannels(1)
+        w.setsampwidth(2)
+        w.setframerate(16000)
+        w.writeframes(q.tobytes())
+
+
+WAV_SPECS = [(41, 16000 * 2 + 311), (42, 16000 * 6), (43, 16000 * 1 + 5), (44, 16000 * 4 + 777),
+             (45, 16000 * 3), (46, 16000 * 5 + 4000), (47, 9000)]
+
+
+def _wav_files(d):
+    paths = []
+    for i, (seed, n) in enumerate(WAV_SPECS):
+        p = os.path.join(str(d), f"utt{i}.wav")
+        _write_wav(p, waveform(seed, n))
+        paths.append(p)
+    return paths
+
+
+def test_waveform_model_alone_token_exact():
+    from funasr_amd.weights import make_weights
+    from oracle.paraformer_ref import paraformer_infer
+    cfg = paraformer_tiny()
+    am = _automodel()                       # no tokenizer -> token_int results
+    wavs = [waveform(31, 16000 * 3), waveform(32, 16000 * 5 + 123), waveform(33, 16000 * 2 + 7)]
+    res = am.generate(input=wavs, batch_size=3, key=["a", "b", "c"])
+    got = [r["token_int"] for r in res]
+
+    eng = am.model.engine()
+    S = max(len(w) for w in wavs)
+    buf = np.zeros((len(wavs), S), np.float32)
+    for i, w in enumerate(wavs):
+        buf[i, : len(w)] = w
+    feats, tout = eng.fbank(torch.from_numpy(buf).cuda(), torch.tensor([len(w) for w in wavs], dtype=torch.int32))
+    torch.cuda.synchronize()
+    feats, tout = feats.cpu().numpy(), tout.cpu().numpy()
+    w = make_weights(cfg)
+    # (1) the model alone: oracle on the GPU's own features == the HIP path, token for token
+    r_gpu = paraformer_infer(feats[:, : int(tout.max())], tout, w, cfg, keep_logits=True)
+    assert got == r_gpu["tokens"]
+
+    # (2) the frontend alone: oracle on knf-equivalent features (oracle/fbank_ref) vs on the GPU features
+    ref_feats = [fbank_ref.frontend(x) for x in wavs]
+    T = max(f.shape[0] for f in ref_feats)
+    x = np.zeros((len(wavs), T, 560), np.float32)
+    for i, f in enumerate(ref_feats):
+        x[i, : f.shape[0]] = f
+    assert [f.shape[0] for f in ref_feats] == tout.tolist()
+    r_ref = paraformer_infer(x, tout, w, cfg)
+    lp = torch.log_softmax(r_gpu["logits"].double(), -1)
+    top2 = lp.topk(2, -1).values
+    margin = (top2[..., 0] - top2[..., 1]).numpy()
+    flips, worst, ntok_diff = 0, 0.0, 0
+    for b in range(len(wavs)):
+        na, nb = int(r_gpu["ntok"][b]), int(r_ref["ntok"][b])
+        ntok_diff = max(ntok_diff, abs(na - nb))
+        if na != nb:
+            continue
+        a_ids, b_ids = r_gpu["argmax"][b, :na].numpy(), r_ref["argmax"][b, :nb].numpy()
+        for t in np.nonzero(a_ids != b_ids)[0]:
+            flips += 1
+            worst = max(worst, float(margin[b, t]))
+    ntot = int(r_gpu["ntok"].sum())
+    print(f"frontend-only effect: {flips}/{ntot} token flips, ntok diff <= {ntok_diff}, largest margin at a flip "
+          f"{worst:.4f} nat")
+    assert ntok_diff <= 1
+    assert worst < FLIP_MARGIN, (flips, worst)
+
+
+def test_model_dir_matches_synthetic_seed(tmp_path):
+    """A model dir written the way the hub layout stores it (config.yaml, model.pt {"state_dict"}, tokens.json,
+    am.mvn) decodes exactly like AutoModel(model="Paraformer", synthetic_seed=0) with the same token list and
+    CMVN."""
+    import yaml
+    from funasr_amd.weights import make_weights
+    cfg = paraformer_tiny()
+    toks = token_list(cfg.vocab_size)
+    cmvn = np.load(f"{GOLD}/lfr_cmvn.npz")["cmvn"]
+    d = tmp_path / "paraformer_tiny"
+    d.mkdir()
+    conf = cfg.reference_kwargs()
+    conf.pop("vocab_size")
+    conf.update(model="Paraformer", model_conf=dict(ctc_weight=0.0, predictor_bias=1), frontend="WavFrontend",
+                frontend_conf=dict(fs=16000, window="hamming", n_mels=80, frame_length=25, frame_shift=10,
+                                   lfr_m=7, lfr_n=6),
+                tokenizer="CharTokenizer", tokenizer_conf=dict(unk_symbol="<unk>", split_with_space=True))
+    (d / "config.yaml").write_text(yaml.safe_dump(conf, allow_unicode=True), encoding="utf-8")
+    torch.save({"state_dict": {k: torch.from_numpy(v) for k, v in make_weights(cfg, 0).items()}}, d / "model.pt")
+    (d / "tokens.json").write_text(json.dumps(toks, ensure_ascii=False), encoding="utf-8")
+    with open(d / "am.mvn", "w") as f:
+        f.write("<Nnet>\n<Splice> 560 560\n[ 0 ]\n<AddShift> 560 560\n<LearnRateCoef> 0 [ "
+                + " ".join(repr(float(v)) for v in cmvn[0]) + " ]\n<Rescale> 560 560\n<LearnRateCoef> 0 [ "
+                + " ".join(repr(float(v)) for v in cmvn[1]) + " ]\n</Nnet>\n")
+    from funasr_amd.auto_model import AutoModel
+    am_dir = AutoModel(model=str(d), device="cuda", mode="exact")
+    am_seed = _automodel(tokenizer_conf=dict(token_list=toks), frontend_conf=dict(cmvn_file=str(d / "am.mvn")))
+    wavs = [waveform(51, 16000 * 4), waveform(52, 16000 * 2 + 900)]
+    a = am_dir.generate(input=wavs, batch_size=2, key=["x", "y"])
+    b = am_seed.generate(input=wavs, batch_size=2, key=["x", "y"])
+    assert a == b
+    assert all(r["text"] for r in a)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _dp_worker(rank, world, port, paths, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.cuda.set_device(0)   # both ranks share the one card of the box
+        am = _automodel()
+        res = am.generate(input=paths, batch_size=2)
+        from funasr_amd.distributed import item_lengths, length_sorted_shards
+        mine = length_sorted_shards(item_lengths(paths), world)[rank]
+        q.put((rank, res, mine))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_dp_world2_shared_device_matches_single_rank(tmp_path):
+    import torch.multiprocessing as mp
+    paths = _wav_files(tmp_path)
+    one = _automodel().generate(input=paths, batch_size=2)
+    assert [r["key"] for r in one] == [f"utt{i}" for i in range(len(paths))]
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_dp_worker, args=(r, world, port, paths, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = sorted([q.get(timeout=240) for _ in range(world)], key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    shards = [m for _, _, m in out]
+    assert sorted(shards[0] + shards[1]) == list(range(len(paths)))
+    assert min(len(s) for s in shards) >= len(paths) // world
+    for rank, res, _ in out:
+        assert res == one, rank   # gathered in input order, token for token
+
+
+def test_load_flat_device_matches_host_load():
+    """pfm_set_weight_device (the DP ranks' path: weights stay in HBM after the RCCL broadcast) gives the same
+    decode as pfm_set_weight from host memory, including the Conv1d / depthwise-tap re-layouts."""
+    from funasr_amd.runtime import PfmEngine
+    from funasr_amd.weights import make_weights, param_layout
+    from tests.golden.inputs import fbank_input
+    cfg = paraformer_tiny()
+    sd = make_weights(cfg, 5)
+    a = PfmEngine(cfg, 0)
+    a.load_state_dict(sd)
+    lay = param_layout(cfg)
+    flat = torch.cat([torch.from_numpy(np.ascontiguousarray(sd[k], np.float32)).reshape(-1) for k, *_ in lay]).cuda()
+    b = PfmEngine(cfg, 0)
+    b.load_flat_device(flat, lay)
+    assert b.missing_weights == 0
+    feats, lens = fbank_input(seed=12, B=3, T=60, lens=[60, 41, 17])
+    x, ln = torch.from_numpy(feats).cuda(), torch.from_numpy(lens).cuda()
+    ra, rb = a.run(x, ln, mode="exact"), b.run(x, ln, mode="exact")
+    torch.cuda.synchronize()
+    for k in ("tokens", "ntok"):
+        assert torch.equal(ra[k], rb[k]), k
+    with pytest.raises(Exception):
+        b.load_flat_device(flat[:100], lay)
