@@ -548,8 +548,9 @@ __device__ __forceinline__ void fsmn_epilogue(const AttnArgs& a, unsigned char* 
     }
 }
 
-// VAR (diagnostics, PFM_ATTN_VAR, timing only — results are wrong): 1 no K/V loads after tile 0,
-// 2 no softmax (P = S), 3 no PV products, 4 no QK products, 5 no key loop (prologue + epilogue only)
+// VAR (diagnostic instantiations for standalone timing — results are wrong; the library instantiates
+// VAR 0 only): 1 no K/V loads after tile 0, 2 no softmax (P = S), 3 no PV products, 4 no QK products,
+// 5 no key loop (prologue + epilogue only)
 template <int NWV, int VAR = 0>
 __global__ __launch_bounds__(NWV * 64, 8 / NWV) void attn_bf16_kernel(AttnArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -754,202 +755,6 @@ __global__ __launch_bounds__(NWV * 64, 8 / NWV) void attn_bf16_kernel(AttnArgs a
     }
 }
 
-// ------------------------------------------------------------------------------------------
-// Ping-pong variant (8 waves, 256 query rows per block). Waves 0-3 (group 0) and 4-7 (group 1) share
-// every SIMD; per key tile each wave runs
-//   phase A(t): QK^T of tile t (16 MFMA) + PV of tile t-1 (16 MFMA)         -> barrier
-//   phase B(t): softmax of tile t (VALU: max, lazy rescale, exp2, row sum, P -> bf16) -> barrier
-// and group 1 runs one barrier behind group 0, so one wave's MFMAs overlap its partner's VALU.
-// Common barrier numbering (b0 = prologue): G0 ends A(t) at b(2t+1), B(t) at b(2t+2); G1 ends A(t) at
-// b(2t+2), B(t) at b(2t+3). Tile t+1 is written to LDS stage (t+1)%3 by G0 in B(t) and by G1 in A(t),
-// i.e. before b(2t+2), and first read after b(2t+2) (G0's A(t+1)). 3 stages: the buffer a write
-// targets last held tile t-2, whose final read (G1's PV(t-2) in A(t-1)) ended at b(2t).
-// Register staging fetches tile t+2 at the start of A(t) (two named sets in flight).
-__global__ __launch_bounds__(512) void attn_bf16_pp_kernel(AttnArgs a) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    constexpr int NT = 512, QBLK = 8 * QW, NSTG = 3;
-    const int qt = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
-    const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int grp = wid >> 2;
-    const int fr = lane & 31, fh = lane >> 5;
-    const int klen = min(a.klen[b], a.Tk);
-    const bf16* Q = (const bf16*)a.q;
-    const bf16* K = (const bf16*)a.k;
-    const bf16* V = (const bf16*)a.v;
-    const int qrow = qt * QBLK + wid * QW + fr;
-    const float qs = a.scale * 1.4426950408889634f;   // scores in log2 units
-    bf16x8 qf[8];
-    {
-        const bool ok = qrow < a.Tq;
-        const bf16* qp = Q + a.qmap.off((long long)b * a.Tq + (ok ? qrow : 0)) + h * DK;
-#pragma unroll
-        for (int kq = 0; kq < 8; ++kq) {
-            bf16x8 x = *(const bf16x8*)(qp + kq * 16 + fh * 8);
-#pragma unroll
-            for (int j = 0; j < 8; ++j) x[j] = ok ? f2bf(bf2f(x[j]) * qs) : (bf16)0.f;
-            qf[kq] = x;
-        }
-    }
-    f32x16 o[4];
-#pragma unroll
-    for (int d = 0; d < 4; ++d)
-#pragma unroll
-        for (int e = 0; e < 16; ++e) o[d][e] = 0.f;
-    float mused = -INFINITY, lrun = 0.f;
-    const int ntiles = (klen + KT2 - 1) / KT2;
-
-    struct Stg { uint4 k0, k1, v0, v1; };
-    auto ld1 = [&](int t, int c, uint4& kk, uint4& vv) {
-        const long long m = (long long)b * a.Tk + min(t * KT2 + (c >> 4), max(klen - 1, 0));
-        kk = *(const uint4*)(K + a.kmap.off(m) + h * DK + (c & 15) * 8);
-        vv = *(const uint4*)(V + a.vmap.off(m) + h * DK + (c & 15) * 8);
-    };
-    auto gload = [&](int t) -> Stg {
-        Stg r;
-        ld1(t, tid, r.k0, r.v0);
-        ld1(t, tid + NT, r.k1, r.v1);
-        return r;
-    };
-    auto st1 = [&](unsigned char* Ks, unsigned char* Vs, int c, const uint4& kk, const uint4& vv) {
-        const int row = c >> 4, ch = c & 15;
-        *(uint4*)(Ks + row * KROW + ((ch ^ (row & 15)) << 4)) = kk;
-        *(uint4*)(Vs + row * VROW + ch * 16) = vv;
-    };
-    auto sstore = [&](int t, const Stg& r) {
-        unsigned char* Ks = smem + (t % NSTG) * STG2;
-        st1(Ks, Ks + KTILE, tid, r.k0, r.v0);
-        st1(Ks, Ks + KTILE, tid + NT, r.k1, r.v1);
-    };
-    const int tg = lane >> 4, ti = lane & 15;
-    const int tr_key = 4 * (tg >> 1) + (ti >> 2);
-    const int tr_col = 16 * (tg & 1) + 4 * (ti & 3);
-
-    auto qk = [&](int t, f32x16 (&sc)[2]) {
-        const unsigned char* Ks = smem + (t % NSTG) * STG2;
-#pragma unroll
-        for (int kb = 0; kb < 2; ++kb) {
-#pragma unroll
-            for (int e = 0; e < 16; ++e) sc[kb][e] = 0.f;
-            const int row = kb * 32 + fr;
-#pragma unroll
-            for (int kq = 0; kq < 8; ++kq) {
-                const bf16x8 kx = *(const bf16x8*)(Ks + row * KROW + (((2 * kq + fh) ^ (row & 15)) << 4));
-                sc[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kx, qf[kq], sc[kb], 0, 0, 0);
-            }
-        }
-    };
-    auto pv = [&](int t, const bf16x8 (&pb)[4]) {
-        const unsigned char* Vs = smem + (t % NSTG) * STG2 + KTILE;
-#pragma unroll
-        for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-            for (int st = 0; st < 2; ++st) {
-                const int key0 = kb * 32 + 16 * st + tr_key;
-#pragma unroll
-                for (int d = 0; d < 4; ++d) {
-                    const unsigned char* vp = Vs + key0 * VROW + (d * 32 + tr_col) * 2;
-                    const v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)vp);
-                    const v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(vp + 8 * VROW));
-                    bf16x8 va;
-                    __builtin_memcpy(&va, &lo, 8);
-                    __builtin_memcpy(((char*)&va) + 8, &hi, 8);
-                    o[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va, pb[2 * kb + st], o[d], 0, 0, 0);
-                }
-            }
-    };
-    auto softmax = [&](int t, f32x16 (&sc)[2], bf16x8 (&pb)[4]) {
-        if ((t + 1) * KT2 > klen) {
-#pragma unroll
-            for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-                for (int e = 0; e < 16; ++e)
-                    if (t * KT2 + kb * 32 + kappa(e) + 4 * fh >= klen) sc[kb][e] = -INFINITY;
-        }
-        float mt = -INFINITY;
-#pragma unroll
-        for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-            for (int e = 0; e < 16; ++e) mt = fmaxf(mt, sc[kb][e]);
-        mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
-        if (mt > mused + RESCALE_THR * 1.4426950408889634f) {   // PV(t-1) is complete (phase A)
-            const float corr = __builtin_amdgcn_exp2f(mused - mt);
-            lrun *= corr;
-#pragma unroll
-            for (int d = 0; d < 4; ++d)
-#pragma unroll
-                for (int e = 0; e < 16; ++e) o[d][e] *= corr;
-            mused = mt;
-        }
-        float ls = 0.f;
-#pragma unroll
-        for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-            for (int e = 0; e < 16; ++e) {
-                sc[kb][e] = __builtin_amdgcn_exp2f(sc[kb][e] - mused);
-                ls += sc[kb][e];
-            }
-        ls += __shfl_xor(ls, 32, 64);
-        lrun += ls;
-#pragma unroll
-        for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-            for (int st = 0; st < 2; ++st)
-#pragma unroll
-                for (int j = 0; j < 8; ++j) pb[2 * kb + st][j] = f2bf(sc[kb][8 * st + j]);
-    };
-    auto bar = [&]() {
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_sched_barrier(0);
-        __builtin_amdgcn_s_barrier();
-        __builtin_amdgcn_sched_barrier(0);
-    };
-
-    Stg nxt = {}, nxt2 = {};
-    if (ntiles > 0) sstore(0, gload(0));
-    if (ntiles > 1) nxt = gload(1);
-    __syncthreads();                                  // b0
-    if (grp == 1) bar();                              // stagger: group 1 one phase behind
-    f32x16 sc[2];
-    bf16x8 pb[4];
-    for (int t = 0; t < ntiles; ++t) {
-        // ---- phase A(t): MFMA
-        if (t + 2 < ntiles) nxt2 = gload(t + 2);
-        qk(t, sc);
-        if (t > 0) pv(t - 1, pb);
-        if (grp == 1) {
-            if (t + 1 < ntiles) sstore(t + 1, nxt);
-            nxt = nxt2;
-        }
-        bar();
-        // ---- phase B(t): softmax (VALU)
-        softmax(t, sc, pb);
-        if (grp == 0) {
-            if (t + 1 < ntiles) sstore(t + 1, nxt);
-            nxt = nxt2;
-        }
-        bar();
-    }
-    if (ntiles > 0) pv(ntiles - 1, pb);
-    if (grp == 0) bar();                              // match group 1's stagger barrier
-    if (qrow >= a.Tq) return;
-    const float inv = (klen > 0) ? 1.f / lrun : 0.f;
-    float* op = a.o ? a.o + ((long long)b * a.Tq + qrow) * a.ldo + h * DK : nullptr;
-    bf16* op2 = a.o2 ? (bf16*)a.o2 + ((long long)b * a.Tq + qrow) * a.ldo + h * DK : nullptr;
-#pragma unroll
-    for (int d = 0; d < 4; ++d)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            const int col = d * 32 + 8 * g + 4 * fh;
-            const float v0 = o[d][4 * g] * inv, v1 = o[d][4 * g + 1] * inv;
-            const float v2 = o[d][4 * g + 2] * inv, v3 = o[d][4 * g + 3] * inv;
-            if (op) *(float4*)(op + col) = make_float4(v0, v1, v2, v3);
-            if (op2) {
-                bf16x4 t4 = {f2bf(v0), f2bf(v1), f2bf(v2), f2bf(v3)};
-                *(bf16x4*)(op2 + col) = t4;
-            }
-        }
-}
-
 }  // namespace
 
 // q/k/v: head-concatenated rows (head h at column h*128). o: f32 [B*Tq, ldo] (may be null in
@@ -973,7 +778,7 @@ hipError_t pfm_attention_fsmn(int dtype, const void* q, RowMap qmap, const void*
     a.fw = fsmn_wT; a.fout = fsmn_out; a.fld = fsmn_ld; a.fD = heads * DK;
     if (fsmn_out) {   // fused FSMN: bf16 8-wave kernel only, self-attention, 16-B aligned rows
         const PfmKnobs& kn = pfm_knobs();
-        if (dtype != DT_BF16 || Tq != Tk || kn.attn_waves != 8 || kn.attn_pp || fsmn_ld % 8 ||
+        if (dtype != DT_BF16 || Tq != Tk || kn.attn_waves != 8 || fsmn_ld % 8 ||
             vmap.ld % 8 || ((uintptr_t)fsmn_out % 16) || !fsmn_wT)
             return hipErrorInvalidValue;
     }
@@ -986,13 +791,6 @@ hipError_t pfm_attention_fsmn(int dtype, const void* q, RowMap qmap, const void*
                                   2 * STG2);
         (void)hipFuncSetAttribute((const void*)attn_bf16_kernel<8>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   LDS8);
-        (void)hipFuncSetAttribute((const void*)attn_bf16_kernel<8, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS8);
-        (void)hipFuncSetAttribute((const void*)attn_bf16_kernel<8, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS8);
-        (void)hipFuncSetAttribute((const void*)attn_bf16_kernel<8, 3>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS8);
-        (void)hipFuncSetAttribute((const void*)attn_bf16_kernel<8, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS8);
-        (void)hipFuncSetAttribute((const void*)attn_bf16_kernel<8, 5>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS8);
-        (void)hipFuncSetAttribute((const void*)attn_bf16_pp_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  3 * STG2);
     }
     // bf16 kernels address an utterance's key rows as base + t * ld (32-bit offsets)
     auto contiguous = [&](const RowMap& m) {
@@ -1008,20 +806,9 @@ hipError_t pfm_attention_fsmn(int dtype, const void* q, RowMap qmap, const void*
         hipLaunchKernelGGL(attn_f32_kernel, grid, block, LDS32, st, a);
     } else {
         const int nw = pfm_knobs().attn_waves;
-        if (nw == 8 && pfm_knobs().attn_pp) {   // ping-pong 8-wave variant (A/B)
+        if (nw == 8) {
             dim3 grid((Tq + 255) / 256, heads, B), block(512);
-            hipLaunchKernelGGL(attn_bf16_pp_kernel, grid, block, 3 * STG2, st, a);
-        } else if (nw == 8) {
-            dim3 grid((Tq + 255) / 256, heads, B), block(512);
-            const int lds = a.fout ? LDS8 : 2 * STG2;
-            switch (pfm_knobs().attn_var) {
-            case 1: hipLaunchKernelGGL((attn_bf16_kernel<8, 1>), grid, block, lds, st, a); break;
-            case 2: hipLaunchKernelGGL((attn_bf16_kernel<8, 2>), grid, block, lds, st, a); break;
-            case 3: hipLaunchKernelGGL((attn_bf16_kernel<8, 3>), grid, block, lds, st, a); break;
-            case 4: hipLaunchKernelGGL((attn_bf16_kernel<8, 4>), grid, block, lds, st, a); break;
-            case 5: hipLaunchKernelGGL((attn_bf16_kernel<8, 5>), grid, block, lds, st, a); break;
-            default: hipLaunchKernelGGL((attn_bf16_kernel<8>), grid, block, lds, st, a);
-            }
+            hipLaunchKernelGGL((attn_bf16_kernel<8>), grid, block, a.fout ? LDS8 : 2 * STG2, st, a);
         } else {
             dim3 grid((Tq + 127) / 128, heads, B), block(256);
             hipLaunchKernelGGL(attn_bf16_kernel<4>, grid, block, 2 * STG2, st, a);

@@ -702,35 +702,6 @@ __global__ __launch_bounds__(64) void ctc_collapse_kernel(const int* __restrict_
 
 
 // ------------------------------------------------------------------------------------------
-// LayerNorm folded into the following projection (fast mode): for LN(x) W^T + b with
-// LN(x) = (x - mean) rstd gamma + beta,
-//   Wf[n][k] = bf16(W[n][k] gamma[k]),  colsum[n] = sum_k Wf[n][k] (of the rounded values, as the MFMA
-//   sees them),  colbias[n] = b[n] + sum_k beta[k] W[n][k]
-// so that LN(x) W^T + b = rstd (bf16(x) Wf^T - mean colsum) + colbias. One wave per output row.
-// ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void ln_fold_kernel(const float* __restrict__ W, int N, int K,
-                                                      const float* __restrict__ gamma, const float* __restrict__ beta,
-                                                      const float* __restrict__ bias, bf16* __restrict__ Wf,
-                                                      float* __restrict__ colsum, float* __restrict__ colbias) {
-    const int lane = threadIdx.x & 63;
-    const int n = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (n >= N) return;
-    double s = 0.0, c = 0.0;
-    for (int k = lane; k < K; k += 64) {
-        const float w = W[(long long)n * K + k];
-        const bf16 wf = f2bf(w * gamma[k]);
-        Wf[(long long)n * K + k] = wf;
-        s += (double)bf2f(wf);
-        c += (double)beta[k] * (double)w;
-    }
-    s = wave_sum_d(s);
-    c = wave_sum_d(c);
-    if (lane == 0) {
-        colsum[n] = (float)s;
-        colbias[n] = (float)((double)(bias ? bias[n] : 0.f) + c);
-    }
-}
-
 // [A][Bd][C] -> [A][C][Bd] (weight re-layout of device-resident state_dict tensors: Conv1d [O][I][k] -> [O][k][I],
 // depthwise taps [D][1][K] -> [K][D]); one thread per output element, coalesced stores
 __global__ void swap_last2_kernel(const float* __restrict__ x, float* __restrict__ y, long long A, long long Bd,
@@ -742,15 +713,6 @@ __global__ void swap_last2_kernel(const float* __restrict__ x, float* __restrict
 }
 
 }  // namespace
-
-hipError_t pfm_ln_fold(const float* W, int N, int K, const float* gamma, const float* beta, const float* bias, bf16* Wf,
-                       float* colsum, float* colbias, hipStream_t st) {
-    if (N <= 0) return hipSuccess;
-    hipLaunchKernelGGL(ln_fold_kernel, dim3((unsigned)((N + 3) / 4)), dim3(256), 0, st, W, N, K, gamma, beta, bias, Wf,
-                       colsum, colbias);
-    PFM_LAUNCH_CHECK();
-    return hipSuccess;
-}
 
 hipError_t pfm_sv_input(const float* feats, const int* lens, const float* embed, const int* qid, int nq, int B, int T,
                         int I, float* x, int* olen, hipStream_t st) {

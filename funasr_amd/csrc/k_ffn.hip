@@ -69,7 +69,7 @@ template <int N> __device__ __forceinline__ void vm_wait() {
 
 template <int HB> struct Frag { bf16x8 w[HB]; bf16x8 a[4]; };
 
-// VAR (diagnostic builds, PFM_FFN_VAR): 0 = the kernel; 1 = no weight DMA (stale ring); 2 = no MFMAs;
+// VAR (diagnostic instantiations for standalone timing; the library instantiates VAR 0 only): 0 = the kernel; 1 = no weight DMA (stale ring); 2 = no MFMAs;
 // 3 = every tile streams ring tiles 0..3 of the layer (L2-hot 64 KiB); 4 = prologue + epilogue only (no
 // tile loop); 5 = VAR 1 without the per-tile barriers (MFMA + fragment reads alone)
 //
@@ -93,11 +93,11 @@ template <int HB> struct Frag { bf16x8 w[HB]; bf16x8 a[4]; };
 // fragments read by half as many waves: 32 instead of 48 KiB of LDS reads per tile) measured 16 % slower
 // (207 vs 178 us at M = 32,000; bench 24.6 vs 21.6 ms/step) and is not instantiated.
 // HR: phase 2 (and phase 0) reads a k step's activation fragments once for both 256-row halves (odd tiles
-// copy them from the even tile's registers) instead of re-reading them from LDS (PFM_FFN_HR A/B).
+// copy them from the even tile's registers) instead of re-reading them from LDS.
 // PD: ring tiles in flight behind the one being published (2: tile t+3 issued at the top of iteration t, 3:
 // tile t+4 — the slot of tile t is free as soon as the barrier retires everyone's fragment reads of it, so
-// all 4 ring slots can be streaming; PFM_FFN_PD A/B: 3 is the default, bench 21.6 -> 20.1 ms/step).
-// The non-default combinations (HR = false, PD = 2) are instantiated for VAR 0 only.
+// all 4 ring slots can be streaming; A/B: bench 21.6 (PD 2) -> 20.1 ms/step (PD 3)). The library
+// instantiates HR = true, PD = 3 only (the measured-slower combinations were A/B knobs until round 3).
 template <int VAR, int MODE = 0, int NW = 8, bool HR = true, int PD = 3>
 __global__ __launch_bounds__(64 * NW) void ffn_fused_kernel(const float* __restrict__ X, int M, const float* __restrict__ g2,
                                                         const float* __restrict__ be2, float eps,
@@ -693,13 +693,7 @@ template <int VAR, int MODE>
 static void ffn_launch_nw(hipStream_t st, int M, const float* x, const float* g, const float* be, float eps, const bf16* Wp,
                    const float* b1, const float* b2, float* xo, const float* gn, const float* bn, bf16* xn, const bf16* o,
                    const bf16* f, const float* bo, const float* c1) {
-    const PfmKnobs& k = pfm_knobs();
-    if (VAR == 0 && !k.ffn_hr)
-        ffn_launch<VAR, MODE, 8, false, 3>(st, M, x, g, be, eps, Wp, b1, b2, xo, gn, bn, xn, o, f, bo, c1);
-    else if (VAR == 0 && k.ffn_pd == 2)
-        ffn_launch<VAR, MODE, 8, true, 2>(st, M, x, g, be, eps, Wp, b1, b2, xo, gn, bn, xn, o, f, bo, c1);
-    else
-        ffn_launch<VAR, MODE, 8, true, 3>(st, M, x, g, be, eps, Wp, b1, b2, xo, gn, bn, xn, o, f, bo, c1);
+    ffn_launch<VAR, MODE, 8, true, 3>(st, M, x, g, be, eps, Wp, b1, b2, xo, gn, bn, xn, o, f, bo, c1);
 }
 
 // Fused decoder feed-forward (ffn_fused_kernel DEC): x f32 [M, 512] -> xn = LN_next(W2 LN_F(relu(W1 LN1(x) + b1)))
@@ -746,14 +740,7 @@ hipError_t pfm_ffn_fused(const float* x, int M, const float* g2, const float* be
     if (((uintptr_t)x | (uintptr_t)xo | (uintptr_t)Wp | (uintptr_t)xn) % 16) return hipErrorInvalidValue;
     const bf16* z = nullptr;
     const float* zf = nullptr;
-    switch (pfm_knobs().ffn_var) {
-        case 1: ffn_launch_nw<1, 0>(st, M, x, g2, be2, eps, Wp, b1, b2, xo, gn, bn, xn, z, z, zf, zf); break;
-        case 2: ffn_launch_nw<2, 0>(st, M, x, g2, be2, eps, Wp, b1, b2, xo, gn, bn, xn, z, z, zf, zf); break;
-        case 3: ffn_launch_nw<3, 0>(st, M, x, g2, be2, eps, Wp, b1, b2, xo, gn, bn, xn, z, z, zf, zf); break;
-        case 4: ffn_launch_nw<4, 0>(st, M, x, g2, be2, eps, Wp, b1, b2, xo, gn, bn, xn, z, z, zf, zf); break;
-        case 5: ffn_launch_nw<5, 0>(st, M, x, g2, be2, eps, Wp, b1, b2, xo, gn, bn, xn, z, z, zf, zf); break;
-        default: ffn_launch_nw<0, 0>(st, M, x, g2, be2, eps, Wp, b1, b2, xo, gn, bn, xn, z, z, zf, zf);
-    }
+    ffn_launch_nw<0, 0>(st, M, x, g2, be2, eps, Wp, b1, b2, xo, gn, bn, xn, z, z, zf, zf);
     PFM_LAUNCH_CHECK();
     return hipSuccess;
 }

@@ -60,9 +60,7 @@ template <int P> __device__ __forceinline__ void wait_vm(int rem) {
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-// LN: 0 plain epilogue; 1 folded-LayerNorm consumer; 2 LayerNorm-statistics producer (compile-time, so the
-// plain kernels carry none of the extra epilogue state: the runtime-flag version spilled to scratch)
-template <class C, int LN = 0>
+template <class C>
 __global__ __launch_bounds__(C::NT) void gemm_bf16_kernel(const bf16* __restrict__ A, RowMap amap,
                                                           const bf16* __restrict__ W, long long ldw, int M, int N,
                                                           int K, int tiles_m, int tiles_n, int gm, GemmEpi epi) {
@@ -133,11 +131,6 @@ __global__ __launch_bounds__(C::NT) void gemm_bf16_kernel(const bf16* __restrict
                                              (lds_void*)(base + C::TA + (PW * wid + j) * 1024), 16, 0, 0);
     };
 
-    // Residual GEMMs (alpha 1, no activation): the accumulators start from res0 + res1, read here in
-    // the accumulator layout (32 lanes = 128 contiguous bytes per row) ahead of the prologue DMA, so
-    // the epilogue carries no loads. vmcnt retires in order: an epilogue load issued after stores
-    // waits for them, which serialised one HBM round trip per 4 rows before.
-    const bool pre_res = C::MF == 0 && epi.pre_res_ok && (epi.res0 || epi.res1) && epi.alpha == 1.f && !epi.relu;
     f32x16 acc[MI][NI];
     // MF 1: 16x16 blocks, block (i4, j4) = rows 16 i4.., cols 16 j4.. of the wave tile;
     // C/D map col = lane & 15, row = 4 (lane >> 4) + reg
@@ -156,24 +149,6 @@ __global__ __launch_bounds__(C::NT) void gemm_bf16_kernel(const bf16* __restrict
             for (int j = 0; j < 2 * NI; ++j)
 #pragma unroll
                 for (int e = 0; e < 4; ++e) acc4[i][j][e] = 0.f;
-    }
-    if (pre_res) {
-#pragma unroll
-        for (int i = 0; i < MI; ++i)
-#pragma unroll
-            for (int e = 0; e < 16; ++e) {
-                const long long row = min(m0 + wm * C::WTM + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * fh, M - 1);
-#pragma unroll
-                for (int j = 0; j < NI; ++j) {
-                    const int col = min(n0 + wn * C::WTN + j * 32 + fr, N - 1);
-                    float v = 0.f;
-                    if (epi.res0)
-                        v = epi.res0_bf16 ? bf2f(((const bf16*)epi.res0)[row * epi.ld_res0 + col])
-                                          : epi.res0[row * epi.ld_res0 + col];
-                    if (epi.res1) v += epi.res1[row * epi.ld_res1 + col];
-                    acc[i][j][e] = v;
-                }
-            }
     }
     int aoff[MI], asw[MI], woff[NI], wsw[NI];
 #pragma unroll
@@ -545,52 +520,17 @@ __global__ __launch_bounds__(C::NT) void gemm_bf16_kernel(const bf16* __restrict
         float* ep = (float*)(smem + wid * C::EPW);
         const bool f32o = epi.out_dtype == DT_F32;
         // a lane's output columns are the same for every row it writes: one bias load, before any store
-        const bool st16 = epi.st16_ok && (pre_res || !(epi.res0 || epi.res1));
+        const bool st16 = epi.st16_ok && !(epi.res0 || epi.res1);
         const int colv = n0 + wn * 64 + (st16 ? (lane & 7) * 8 : (lane & 15) * 4);
         float4 bb = make_float4(0.f, 0.f, 0.f, 0.f), bb2 = bb;
         if (epi.out && epi.bias && colv < N) {
             bb = *(const float4*)(epi.bias + colv);
             if (st16) bb2 = *(const float4*)(epi.bias + colv + 4);
         }
-        // LayerNorm folded into this projection: column sums of bf16(W o gamma) for the lane's columns
-        constexpr bool lnf = LN == 1;
-        float4 lc = make_float4(0.f, 0.f, 0.f, 0.f), lc2 = lc;
-        if (lnf && epi.out && colv < N) {
-            lc = *(const float4*)(epi.ln_colsum + colv);
-            if (st16) lc2 = *(const float4*)(epi.ln_colsum + colv + 4);
-        }
         // consume it here, before any store: otherwise paths that skip rows leave it "pending" and the
         // compiler re-waits vmcnt(0) (draining the stores issued since) at every use below
         asm volatile("" ::"v"(bb.x), "v"(bb.y), "v"(bb.z), "v"(bb.w), "v"(bb2.x), "v"(bb2.y), "v"(bb2.z),
                      "v"(bb2.w));
-        asm volatile("" ::"v"(lc.x), "v"(lc.y), "v"(lc.z), "v"(lc.w), "v"(lc2.x), "v"(lc2.y), "v"(lc2.z),
-                     "v"(lc2.w));
-        // folded LayerNorm: the producer's partials of row (lane & 31) of 32-row group ig; group i+1's are
-        // loaded while group i is processed (their latency stays off the store stream)
-        auto ln_load = [&](int ig, float2 (&d)[8]) {
-            const long long row = min(m0 + wm * C::WTM + ig * 32 + (lane & 31), M - 1);
-            const float2* sp = epi.ln_st_in + row * epi.ln_parts;
-#pragma unroll
-            for (int p = 0; p < 8; ++p) d[p] = p < epi.ln_parts ? sp[p] : make_float2(0.f, 0.f);
-        };
-        float2 ln_cur[8], ln_nxt[8];
-        if constexpr (lnf) ln_load(0, ln_cur);
-        // producer statistics of a 16-lane row group's 64 values (4 per lane): (mean, M2) of the slice
-        auto ln_stats_out = [&](const float4& v, long long row, int c4) {
-            float sm = (v.x + v.y) + (v.z + v.w);
-            sm += __shfl_xor(sm, 1, 64);
-            sm += __shfl_xor(sm, 2, 64);
-            sm += __shfl_xor(sm, 4, 64);
-            sm += __shfl_xor(sm, 8, 64);
-            const float mu = sm * (1.f / 64.f);
-            const float dx = v.x - mu, dy = v.y - mu, dz = v.z - mu, dw = v.w - mu;
-            float q = (dx * dx + dy * dy) + (dz * dz + dw * dw);
-            q += __shfl_xor(q, 1, 64);
-            q += __shfl_xor(q, 2, 64);
-            q += __shfl_xor(q, 4, 64);
-            q += __shfl_xor(q, 8, 64);
-            if (c4 == 0) epi.ln_st_out[row * epi.ln_parts + (n0 + wn * 64) / 64] = make_float2(mu, q);
-        };
 #pragma unroll
         for (int i = 0; i < MI; ++i) {
             if constexpr (C::MF == 0) {
@@ -610,23 +550,6 @@ __global__ __launch_bounds__(C::NT) void gemm_bf16_kernel(const bf16* __restrict
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            // folded LayerNorm: lane l holds (mean, rstd) of row (l & 31) of this 32-row group, combined
-            // from the producer's per-slice partials (Chan: M2 = sum M2_p + 64 sum (m_p - mean)^2)
-            float g_mean = 0.f, g_rstd = 0.f;
-            if constexpr (lnf) {
-                if (i + 1 < MI) ln_load(i + 1, ln_nxt);
-                const int P = epi.ln_parts;
-                float msum = 0.f;
-#pragma unroll
-                for (int p = 0; p < 8; ++p) msum += ln_cur[p].x;
-                const float mean = msum / (float)P;
-                float m2 = 0.f;
-#pragma unroll
-                for (int p = 0; p < 8; ++p)
-                    if (p < P) m2 += ln_cur[p].y + 64.f * (ln_cur[p].x - mean) * (ln_cur[p].x - mean);
-                g_mean = mean;
-                g_rstd = 1.f / sqrtf(m2 / (64.f * (float)P) + epi.ln_eps);
-            }
             if (epi.amax_val) {
                 // fused row-argmax of the output layer over this wave's 64 columns: 2 lanes per staged
                 // row scan 32 columns each in order (first index wins ties, like torch.argmax)
@@ -657,22 +580,13 @@ __global__ __launch_bounds__(C::NT) void gemm_bf16_kernel(const bf16* __restrict
                     const int f = lane + 64 * sidx, rr = f >> 3, c8 = f & 7;
                     const int row = m0 + wm * C::WTM + i * 32 + rr;
                     const int col = n0 + wn * 64 + c8 * 8;
-                    const float mr = lnf ? __shfl(g_mean, rr, 64) : 0.f;   // every lane active here
-                    const float rs = lnf ? __shfl(g_rstd, rr, 64) : 0.f;
                     if (row >= M || col >= N) continue;
                     float4 v = *(const float4*)(ep + rr * EP + c8 * 8);
                     float4 u = *(const float4*)(ep + rr * EP + c8 * 8 + 4);
-                    if (lnf) {
-                        v.x = rs * (v.x - mr * lc.x) + bb.x; v.y = rs * (v.y - mr * lc.y) + bb.y;
-                        v.z = rs * (v.z - mr * lc.z) + bb.z; v.w = rs * (v.w - mr * lc.w) + bb.w;
-                        u.x = rs * (u.x - mr * lc2.x) + bb2.x; u.y = rs * (u.y - mr * lc2.y) + bb2.y;
-                        u.z = rs * (u.z - mr * lc2.z) + bb2.z; u.w = rs * (u.w - mr * lc2.w) + bb2.w;
-                    } else {
-                        v.x = v.x * epi.alpha + bb.x; v.y = v.y * epi.alpha + bb.y;
-                        v.z = v.z * epi.alpha + bb.z; v.w = v.w * epi.alpha + bb.w;
-                        u.x = u.x * epi.alpha + bb2.x; u.y = u.y * epi.alpha + bb2.y;
-                        u.z = u.z * epi.alpha + bb2.z; u.w = u.w * epi.alpha + bb2.w;
-                    }
+                    v.x = v.x * epi.alpha + bb.x; v.y = v.y * epi.alpha + bb.y;
+                    v.z = v.z * epi.alpha + bb.z; v.w = v.w * epi.alpha + bb.w;
+                    u.x = u.x * epi.alpha + bb2.x; u.y = u.y * epi.alpha + bb2.y;
+                    u.z = u.z * epi.alpha + bb2.z; u.w = u.w * epi.alpha + bb2.w;
                     if (epi.relu) {
                         v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
                         u.x = fmaxf(u.x, 0.f); u.y = fmaxf(u.y, 0.f); u.z = fmaxf(u.z, 0.f); u.w = fmaxf(u.w, 0.f);
@@ -680,7 +594,7 @@ __global__ __launch_bounds__(C::NT) void gemm_bf16_kernel(const bf16* __restrict
                     bf16x8 t = {f2bf(v.x), f2bf(v.y), f2bf(v.z), f2bf(v.w), f2bf(u.x), f2bf(u.y), f2bf(u.z), f2bf(u.w)};
                     *(bf16x8*)((bf16*)epi.out + epi.out_map.off(row) + col) = t;
                 }
-            } else if (C::MI <= 2 && epi.res_batch && !pre_res && (epi.res0 || epi.res1) && epi.out) {
+            } else if (C::MI <= 2 && epi.res_batch && (epi.res0 || epi.res1) && epi.out) {
                 // (64-row wave tiles only: with 128-row tiles the extra registers spill)
                 // residual loads of 4 row groups first, then their stores (vmcnt retires in order: a load
                 // queued behind a store waits for it)
@@ -716,7 +630,6 @@ __global__ __launch_bounds__(C::NT) void gemm_bf16_kernel(const bf16* __restrict
                         if (epi.relu) { v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f); }
                         v.x += r0[q].x + r1[q].x; v.y += r0[q].y + r1[q].y;
                         v.z += r0[q].z + r1[q].z; v.w += r0[q].w + r1[q].w;
-                        if constexpr (LN == 2) ln_stats_out(v, row, c4);
                         const long long ob = epi.out_map.off(row) + col;
                         if (f32o) *(float4*)((float*)epi.out + ob) = v;
                         else {
@@ -736,19 +649,12 @@ __global__ __launch_bounds__(C::NT) void gemm_bf16_kernel(const bf16* __restrict
                 const int f = lane + 64 * sidx, rr = f >> 4, c4 = f & 15;
                 const int row = m0 + wm * C::WTM + i * 32 + rr;
                 const int col = n0 + wn * 64 + c4 * 4;
-                const float mr = lnf ? __shfl(g_mean, rr, 64) : 0.f;   // every lane active here
-                const float rs = lnf ? __shfl(g_rstd, rr, 64) : 0.f;
                 if (row >= M || col >= N) continue;
                 float4 v = *(const float4*)(ep + rr * EP + c4 * 4);
-                if (lnf) {
-                    v.x = rs * (v.x - mr * lc.x) + bb.x; v.y = rs * (v.y - mr * lc.y) + bb.y;
-                    v.z = rs * (v.z - mr * lc.z) + bb.z; v.w = rs * (v.w - mr * lc.w) + bb.w;
-                } else {
-                    v.x = v.x * epi.alpha + bb.x; v.y = v.y * epi.alpha + bb.y;
-                    v.z = v.z * epi.alpha + bb.z; v.w = v.w * epi.alpha + bb.w;
-                }
+                v.x = v.x * epi.alpha + bb.x; v.y = v.y * epi.alpha + bb.y;
+                v.z = v.z * epi.alpha + bb.z; v.w = v.w * epi.alpha + bb.w;
                 if (epi.relu) { v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f); }
-                if (epi.res0 && !pre_res) {
+                if (epi.res0) {
                     float4 r0;
                     if (epi.res0_bf16) {
                         const bf16x4 rb = *(const bf16x4*)((const bf16*)epi.res0 + (long long)row * epi.ld_res0 + col);
@@ -758,11 +664,10 @@ __global__ __launch_bounds__(C::NT) void gemm_bf16_kernel(const bf16* __restrict
                     }
                     v.x += r0.x; v.y += r0.y; v.z += r0.z; v.w += r0.w;
                 }
-                if (epi.res1 && !pre_res) {
+                if (epi.res1) {
                     const float4 r1 = *(const float4*)(epi.res1 + (long long)row * epi.ld_res1 + col);
                     v.x += r1.x; v.y += r1.y; v.z += r1.z; v.w += r1.w;
                 }
-                if constexpr (LN == 2) ln_stats_out(v, row, c4);
                 const long long ob = epi.out_map.off(row) + col;
                 if (f32o) *(float4*)((float*)epi.out + ob) = v;
                 else if (epi.out_dtype == DT_X3) {   // EXACT-mode split operand of the next GEMM: planes N apart
@@ -789,11 +694,6 @@ __global__ __launch_bounds__(C::NT) void gemm_bf16_kernel(const bf16* __restrict
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            if constexpr (lnf) {
-                if (i + 1 < MI)
-#pragma unroll
-                    for (int p = 0; p < 8; ++p) ln_cur[p] = ln_nxt[p];
-            }
         }
         return;
     }
@@ -842,10 +742,10 @@ __global__ __launch_bounds__(C::NT) void gemm_bf16_kernel(const bf16* __restrict
                 float v = acc[i][j][e] * epi.alpha;
                 if (epi.bias) v += epi.bias[col];
                 if (epi.relu) v = fmaxf(v, 0.f);
-                if (epi.res0 && !pre_res)
+                if (epi.res0)
                     v += epi.res0_bf16 ? bf2f(((const bf16*)epi.res0)[(long long)row * epi.ld_res0 + col])
                                        : epi.res0[(long long)row * epi.ld_res0 + col];
-                if (epi.res1 && !pre_res) v += epi.res1[(long long)row * epi.ld_res1 + col];
+                if (epi.res1) v += epi.res1[(long long)row * epi.ld_res1 + col];
                 if (epi.out_dtype == DT_F32) ((float*)epi.out)[ob + col] = v;
                 else ((bf16*)epi.out)[ob + col] = f2bf(v);
                 if (epi.out2) ((bf16*)epi.out2)[epi.out2_map.off(row) + col] = f2bf(v);
@@ -1045,34 +945,24 @@ using C14 = Cfg<256, 256, 2, 4, 32, 4, 3>;  // k-step phases, BK 32 x 4 buffers
 using C15 = Cfg<256, 256, 2, 4, 64, 2, 0, 1>;  // C1 on v_mfma_f32_16x16x32_bf16
 using C16 = Cfg<128, 256, 2, 4, 32, 3, 0, 1>;  // C4 on v_mfma_f32_16x16x32_bf16
 using C17 = Cfg<256, 256, 2, 4, 64, 2, 2, 1>;  // 8-phase schedule on v_mfma_f32_16x16x32_bf16 (K % 128 == 0)
-using C18 = Cfg<256, 256, 2, 4, 32, 4, 0, 1>;  // C15 as BK 32 x 4 stages: two 32-deep stages in flight behind the read one
 
-template <class C, int LN = 0>
+template <class C>
 hipError_t launch(const void* A, RowMap amap, const void* W, long long ldw, int M, int N, int K, const GemmEpi& e2,
                   hipStream_t st) {
     static bool attr_done = false;
     if (!attr_done) {
         attr_done = true;
-        (void)hipFuncSetAttribute((const void*)gemm_bf16_kernel<C, LN>, hipFuncAttributeMaxDynamicSharedMemorySize,
+        (void)hipFuncSetAttribute((const void*)gemm_bf16_kernel<C>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   C::LDS);
     }
     const int tiles_m = (M + C::BM - 1) / C::BM, tiles_n = (N + C::BN - 1) / C::BN;
     // grouped tile order (4 tile-rows per group) for the wide-N projections (memory K|V, vocabulary:
     // +6 % measured), row-major otherwise; PFM_GEMM_GM overrides per launch (A/B)
     const int gm = pfm_knobs().gemm_gm >= 0 ? pfm_knobs().gemm_gm : (tiles_n >= 16 ? 4 : 0);
-    hipLaunchKernelGGL((gemm_bf16_kernel<C, LN>), dim3(tiles_m * tiles_n), dim3(C::NT), C::LDS, st, (const bf16*)A, amap,
+    hipLaunchKernelGGL((gemm_bf16_kernel<C>), dim3(tiles_m * tiles_n), dim3(C::NT), C::LDS, st, (const bf16*)A, amap,
                        (const bf16*)W, ldw, M, N, K, tiles_m, tiles_n, gm, e2);
     PFM_LAUNCH_CHECK();
     return hipSuccess;
-}
-
-// the configurations the path uses (C4, C15, C17) carry the LayerNorm epilogue variants
-template <class C>
-hipError_t launch_ln(const void* A, RowMap amap, const void* W, long long ldw, int M, int N, int K, const GemmEpi& e2,
-                     hipStream_t st) {
-    if (e2.ln_st_in) return launch<C, 1>(A, amap, W, ldw, M, N, K, e2, st);
-    if (e2.ln_st_out) return launch<C, 2>(A, amap, W, ldw, M, N, K, e2, st);
-    return launch<C, 0>(A, amap, W, ldw, M, N, K, e2, st);
 }
 
 int num_cus() {
@@ -1106,7 +996,7 @@ hipError_t launch_persist(const void* A, RowMap amap, const void* W, long long l
 
 int pick_cfg(int M, int N, int K, bool amax) {
     const int f = pfm_knobs().gemm_cfg;   // PFM_GEMM_CFG (per call): lets one process A/B configurations
-    if (f >= 1 && f <= 18) return f;
+    if (f >= 1 && f <= 17) return f;
     // Default (measured on the path, tools/bench_ab.py with the two concurrent encoder groups: 24.2 vs
     // 25.0-25.3 ms/step for the policies below). Grids are counted in 256x256 tiles; each encoder group
     // sees half the batch's rows:
@@ -1114,212 +1004,16 @@ int pick_cfg(int M, int N, int K, bool amax) {
     //  - >= one 256x256 tile per CU (QKV, FFN w1, memory K|V) on the one-barrier 16x16x32 kernel (C15);
     //  - everything else (out-projections, decoder-sized M, the fused-argmax vocabulary GEMM) on
     //    128x256 tiles, two blocks per CU (C4).
-    // PFM_GEMM_POLICY=1: the earlier grid-size policy (C15 at >= 2 tiles / CU or K >= 1536 with >= 240
-    // tiles, else C4); =2: C13 / C4 for decoder-sized M; =3: C4 instead of C3 for the 512-wide GEMMs of
-    // (measured on the two-group path and not kept: 256x128 tiles for the one-group QKV, 22.08 vs 21.68 ms)
-    // fewer than 120 256x256 tiles (decoder projections: C3 measured 10.9 vs 13.3 us at M = 7392, K = 512;
-    // 26.0 vs 35.5 us at K = 2048).
-    const int p = pfm_knobs().gemm_policy;
+    // (alternative policies measured slower on the path and removed in round 3: the earlier grid-size
+    // policy C15 / C4, C13 for decoder-sized M, C4 for the 512-wide decoder GEMMs, the 8-phase schedules
+    // for the >= 256-tile grids; 256x128 tiles for the one-group QKV 22.08 vs 21.68 ms. C3 for the
+    // decoder projections: 10.9 vs 13.3 us at M = 7392, K = 512; 26.0 vs 35.5 us at K = 2048)
     const long long big = (long long)((M + 255) / 256) * ((N + 255) / 256);
-    if (p == 1 || p == 2) {
-        if (p == 2 && M <= 16384 && !amax) return 4;
-        if (big >= 512 || (K >= 1536 && big >= 240)) return (p == 2 && K % 128 == 0) ? 13 : 15;
-        return 4;
-    }
     if (amax) return big >= 512 ? 15 : 4;
     if (N <= 512 && K % 128 == 0 && K >= 1024 && big >= 120) return 17;
-    // =4 / =5: the 8-phase schedule (C17 on 16x16x32 / C13 on 32x32x16) also for the >= 256-tile grids
-    // (QKV, memory K|V) — A/B of the one-barrier kernel's 1.48-round QKV grid
-    if ((p == 4 || p == 5) && big >= 256 && K % 128 == 0) return p == 4 ? 17 : 13;
     if (big >= 256) return 15;
-    if (N <= 512 && big < 120 && p != 3) return 3;   // decoder-sized M: 128x128 tiles fill more CUs
+    if (N <= 512 && big < 120) return 3;   // decoder-sized M: 128x128 tiles fill more CUs
     return 4;
-}
-
-// ------------------------------------------------------------------------------------------
-// Full-row GEMM + LayerNorm epilogue (N == 512 == d_model): one block owns 128 whole rows.
-//   x = act(A.W^T + bias) (+ res0) (+ res1)          -> out (f32, optional)
-//   y = LayerNorm(x) * gamma + beta                  -> ln_out (f32/bf16), ln_out2 (bf16, optional)
-// Fuses the LN that follows every 512-wide projection on the path (encoder out-proj -> norm2,
-// FFN w2 -> next norm1 / after_norm, decoder w2 -> norm2, decoder out-proj -> next norm1),
-// removing one full HBM read+write pass of the residual stream per fused LN.
-// 8 waves as 2 x 4 (wave tile 64 x 128 = 2x4 MFMA 32x32x16 blocks: 6 LDS fragment reads per 8 MFMAs,
-// the same ratio as the 256x256 kernel), BK 32, 3-stage LDS-DMA ring (A 8 KiB + W 32 KiB per stage,
-// 5 x 1-KiB pieces per wave). Epilogue: two halves of 64 rows; the half's waves stage their f32
-// accumulators in LDS, then every wave normalises 8 whole rows (lane = 8 columns, float4 I/O).
-constexpr int LN_BM = 128, LN_N = 512, LN_BK = 32, LN_NS = 3;
-constexpr int LN_ROWB = LN_BK * 2;                          // 64 B
-constexpr int LN_TA = LN_BM * LN_ROWB, LN_TW = LN_N * LN_ROWB, LN_STAGE = LN_TA + LN_TW;   // 8K + 32K
-constexpr int LN_CP = LN_N + 8;                             // staged C row pitch (floats): rows r, r+4 on disjoint banks
-constexpr int LN_HALF = 64;
-constexpr int LN_LDS = (LN_NS * LN_STAGE > LN_HALF * LN_CP * 4) ? LN_NS * LN_STAGE : LN_HALF * LN_CP * 4;
-
-struct LnEpi {
-    const float* gamma; const float* beta; float eps;
-    void* out; RowMap map; int dtype;            // LN output (f32 or bf16)
-    void* out2; RowMap map2;                     // optional bf16 copy
-};
-
-__device__ __forceinline__ int ln_swz(int row) { return (row >> 2) & 3; }   // 64-B rows
-
-__global__ __launch_bounds__(512) void gemm_bf16_ln_kernel(const bf16* __restrict__ A, RowMap amap,
-                                                           const bf16* __restrict__ W, long long ldw, int M, int K,
-                                                           GemmEpi epi, LnEpi ln) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int m0 = blockIdx.x * LN_BM;
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const int wm = wid >> 2, wn = wid & 3;
-    const int fr = lane & 31, fh = lane >> 5;
-    const int sub = lane >> 2, slot = lane & 3;     // 16 rows x 4 chunks per 1-KiB piece
-    const int arow = 16 * wid + sub;
-    const bf16* ga = A + amap.off(min(m0 + arow, M - 1)) + (slot ^ ln_swz(arow)) * 8;
-    const bf16* gw[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const int row = 16 * (4 * wid + j) + sub;
-        gw[j] = W + (long long)row * ldw + (slot ^ ln_swz(row)) * 8;
-    }
-    auto stage = [&](int k0, int s) {
-        unsigned char* base = smem + s * LN_STAGE;
-        __builtin_amdgcn_global_load_lds((gbl_void*)(ga + k0), (lds_void*)(base + wid * 1024), 16, 0, 0);
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-            __builtin_amdgcn_global_load_lds((gbl_void*)(gw[j] + k0),
-                                             (lds_void*)(base + LN_TA + (4 * wid + j) * 1024), 16, 0, 0);
-    };
-    f32x16 acc[2][4];
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-            for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
-    int aoff[2], asw[2], woff[4], wsw[4];
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-        const int ar = wm * 64 + i * 32 + fr;
-        aoff[i] = ar * LN_ROWB; asw[i] = ln_swz(ar);
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const int wr = wn * 128 + j * 32 + fr;
-        woff[j] = LN_TA + wr * LN_ROWB; wsw[j] = ln_swz(wr);
-    }
-    const int nk = K / LN_BK;
-#pragma unroll
-    for (int s = 0; s < LN_NS - 1; ++s)
-        if (s < nk) stage(s * LN_BK, s);
-    for (int kt = 0; kt < nk; ++kt) {
-        if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");   // NS=3: one stage (5 loads) in flight
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        __builtin_amdgcn_sched_barrier(0);
-        if (kt + LN_NS - 1 < nk) stage((kt + LN_NS - 1) * LN_BK, (kt + LN_NS - 1) % LN_NS);
-        const unsigned char* sb = smem + (kt % LN_NS) * LN_STAGE;
-#pragma unroll
-        for (int kq = 0; kq < LN_BK / 16; ++kq) {
-            const int c = 2 * kq + fh;
-            bf16x8 af[2], bfr[4];
-#pragma unroll
-            for (int i = 0; i < 2; ++i) af[i] = *(const bf16x8*)(sb + aoff[i] + ((c ^ asw[i]) << 4));
-#pragma unroll
-            for (int j = 0; j < 4; ++j) bfr[j] = *(const bf16x8*)(sb + woff[j] + ((c ^ wsw[j]) << 4));
-#pragma unroll
-            for (int i = 0; i < 2; ++i)
-#pragma unroll
-                for (int j = 0; j < 4; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-        }
-    }
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    __syncthreads();
-    // (1) in the accumulator layout: x = act(alpha*acc + bias) (+ res0) (+ res1). The residual reads of a
-    // wave are independent scalar loads (32 lanes = 128 contiguous bytes), so they all overlap.
-    {
-        float bj[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) bj[j] = epi.bias ? epi.bias[wn * 128 + j * 32 + fr] : 0.f;
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int e = 0; e < 16; ++e) {
-                const long long row = min(m0 + wm * 64 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * fh, M - 1);
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const int col = wn * 128 + j * 32 + fr;
-                    float v = acc[i][j][e] * epi.alpha + bj[j];
-                    if (epi.relu) v = fmaxf(v, 0.f);
-                    if (epi.res0)
-                        v += epi.res0_bf16 ? bf2f(((const bf16*)epi.res0)[row * epi.ld_res0 + col])
-                                           : epi.res0[row * epi.ld_res0 + col];
-                    if (epi.res1) v += epi.res1[row * epi.ld_res1 + col];
-                    acc[i][j][e] = v;
-                }
-            }
-    }
-    float4 gam[2], bet[2];
-#pragma unroll
-    for (int hf = 0; hf < 2; ++hf) {
-        const int col = hf * 256 + lane * 4;
-        gam[hf] = *(const float4*)(ln.gamma + col);
-        bet[hf] = *(const float4*)(ln.beta + col);
-    }
-    // (2) per 64-row half: stage x in LDS, then each wave normalises 8 whole rows (no global reads)
-    float* ct = (float*)smem;
-#pragma unroll
-    for (int half = 0; half < 2; ++half) {
-        if (half) __syncthreads();   // previous half fully consumed
-        if (wm == half) {
-#pragma unroll
-            for (int i = 0; i < 2; ++i)
-#pragma unroll
-                for (int j = 0; j < 4; ++j)
-#pragma unroll
-                    for (int e = 0; e < 16; ++e)
-                        ct[(i * 32 + (e & 3) + 8 * (e >> 2) + 4 * fh) * LN_CP + wn * 128 + j * 32 + fr] = acc[i][j][e];
-        }
-        __syncthreads();
-        for (int rr = 0; rr < 8; ++rr) {
-            const int lr = wid * 8 + rr, row = m0 + half * LN_HALF + lr;
-            if (row >= M) break;
-            float4 x[2];
-#pragma unroll
-            for (int hf = 0; hf < 2; ++hf) {
-                const int col = hf * 256 + lane * 4;
-                x[hf] = *(const float4*)(ct + lr * LN_CP + col);
-                if (epi.out) *(float4*)((float*)epi.out + epi.out_map.off(row) + col) = x[hf];
-            }
-            float sm = x[0].x + x[0].y + x[0].z + x[0].w + x[1].x + x[1].y + x[1].z + x[1].w;
-            const float mean = wave_sum(sm) * (1.f / LN_N);
-            float q = 0.f;
-#pragma unroll
-            for (int hf = 0; hf < 2; ++hf) {
-                const float a0 = x[hf].x - mean, a1 = x[hf].y - mean, a2 = x[hf].z - mean, a3 = x[hf].w - mean;
-                q += a0 * a0 + a1 * a1 + a2 * a2 + a3 * a3;
-            }
-            const float rstd = rsqrtf(wave_sum(q) * (1.f / LN_N) + ln.eps);
-#pragma unroll
-            for (int hf = 0; hf < 2; ++hf) {
-                const int col = hf * 256 + lane * 4;
-                float4 y;
-                y.x = (x[hf].x - mean) * rstd * gam[hf].x + bet[hf].x;
-                y.y = (x[hf].y - mean) * rstd * gam[hf].y + bet[hf].y;
-                y.z = (x[hf].z - mean) * rstd * gam[hf].z + bet[hf].z;
-                y.w = (x[hf].w - mean) * rstd * gam[hf].w + bet[hf].w;
-                const long long o1 = ln.map.off(row) + col;
-                if (ln.dtype == DT_F32) *(float4*)((float*)ln.out + o1) = y;
-                else {
-                    bf16x4 t = {f2bf(y.x), f2bf(y.y), f2bf(y.z), f2bf(y.w)};
-                    *(bf16x4*)((bf16*)ln.out + o1) = t;
-                }
-                if (ln.out2) {
-                    bf16x4 t = {f2bf(y.x), f2bf(y.y), f2bf(y.z), f2bf(y.w)};
-                    *(bf16x4*)((bf16*)ln.out2 + ln.map2.off(row) + col) = t;
-                }
-            }
-        }
-    }
 }
 
 }  // namespace
@@ -1337,45 +1031,27 @@ hipError_t pfm_gemm_bf16_256(const void* A, RowMap amap, const void* W, long lon
     if (!pfm_gemm_bf16_256_ok(amap, ldw, K)) return hipErrorInvalidValue;
     GemmEpi e2 = epi;
     e2.vec_ok = epi_vec_ok(epi, N);
-    // the folded-LayerNorm consumer / statistics producer live in the vector epilogue of the tiled kernel
-    // (64-column wave slices: partial index = column / 64, at most 8 partials per row)
-    if ((epi.ln_st_in || epi.ln_st_out) &&
-        (!e2.vec_ok || epi.amax_val || epi.ln_parts < 1 || epi.ln_parts > 8 || (epi.ln_st_out && N != 64 * epi.ln_parts) ||
-         (epi.ln_st_in && (!epi.ln_colsum || epi.pre_res_ok))))
-        return hipErrorInvalidValue;
     {
         const RowMap& om = epi.out_map;
         e2.st16_ok = e2.vec_ok && epi.out && epi.out_dtype == DT_BF16 && !epi.out2 && !epi.amax_val && N % 8 == 0 &&
                      om.ld % 8 == 0 && (om.rows_per_seg <= 0 || om.seg_stride % 8 == 0) &&
                      ((uintptr_t)epi.out % 16) == 0 && pfm_knobs().gemm_st16;
     }
-    {
-        // residual pre-loaded into the accumulators (accumulator-layout scalar loads ahead of the main
-        // loop): measured 2.2 ms/step SLOWER on the path (bf16 + f32 residual out-proj), so opt-in
-        e2.pre_res_ok = pfm_knobs().gemm_preres;
-        e2.res_batch = pfm_knobs().gemm_resbatch;   // residual loads batched ahead of the stores
-    }
+    e2.res_batch = pfm_knobs().gemm_resbatch;   // residual loads batched ahead of the stores
     if (epi.out && epi.out_dtype == DT_X3) {   // split output: the general vector epilogue path only
-        if (!e2.vec_ok || epi.amax_val || epi.out2 || epi.ln_st_in || epi.ln_st_out || epi.out_map.ld % 4)
-            return hipErrorInvalidValue;
+        if (!e2.vec_ok || epi.amax_val || epi.out2 || epi.out_map.ld % 4) return hipErrorInvalidValue;
         e2.res_batch = 0;
-        e2.pre_res_ok = 0;
     }
-    const bool ln = e2.ln_st_in || e2.ln_st_out;
     int cfg = pick_cfg(M, N, K, epi.amax_val != nullptr);
-    if (ln && cfg != 4 && cfg != 15 && cfg != 17) cfg = 15;
     // (EXACT mode x6 GEMMs keep the fast-mode tiles: C17 for N >= 1024 and C16 for 512-wide x6 GEMMs were
     // faster in isolation — tools/gemm_cfg_scan.py SCAN_X6=1 — but slower on the two-group path, 99.3 and
     // 104.8 vs 98.0 ms/step; unsplit, C17 for the wide ones 100.9 vs 101.3, both 111.6)
-    // PFM_GEMM_POLICY=6: C18 wherever the policy picks C15 (deeper LDS-DMA prefetch A/B)
-    if (pfm_knobs().gemm_policy == 6 && cfg == 15 && !ln) cfg = 18;
-    if (epi.x6_k && cfg != 1 && cfg != 3 && cfg != 4 && cfg != 13 && cfg != 15 && cfg != 16 && cfg != 17 && cfg != 18)
-        cfg = 15;
-    if (epi.x6_k && (K != (epi.x6_terms == 3 ? 3 : 6) * epi.x6_k || epi.x6_k % 64 || ln)) return hipErrorInvalidValue;
+    if (epi.x6_k && cfg != 1 && cfg != 3 && cfg != 4 && cfg != 13 && cfg != 15 && cfg != 16 && cfg != 17) cfg = 15;
+    if (epi.x6_k && (K != (epi.x6_terms == 3 ? 3 : 6) * epi.x6_k || epi.x6_k % 64)) return hipErrorInvalidValue;
     switch (cfg) {
         case 2: return launch<C2>(A, amap, W, ldw, M, N, K, e2, st);
         case 3: return launch<C3>(A, amap, W, ldw, M, N, K, e2, st);
-        case 4: return launch_ln<C4>(A, amap, W, ldw, M, N, K, e2, st);
+        case 4: return launch<C4>(A, amap, W, ldw, M, N, K, e2, st);
         case 5: return launch<C5>(A, amap, W, ldw, M, N, K, e2, st);
         case 6: return launch<C6>(A, amap, W, ldw, M, N, K, e2, st);
         case 7: if (!e2.amax_val && e2.vec_ok) return launch_persist<C7, 16>(A, amap, W, ldw, M, N, K, e2, st);
@@ -1391,34 +1067,10 @@ hipError_t pfm_gemm_bf16_256(const void* A, RowMap amap, const void* W, long lon
                  return launch<C1>(A, amap, W, ldw, M, N, K, e2, st);
         case 14: return launch<C14>(A, amap, W, ldw, M, N, K, e2, st);
         case 16: return launch<C16>(A, amap, W, ldw, M, N, K, e2, st);
-        case 18: return launch<C18>(A, amap, W, ldw, M, N, K, e2, st);
-        case 17: if (K % 128 == 0) return launch_ln<C17>(A, amap, W, ldw, M, N, K, e2, st);
-                 return launch_ln<C15>(A, amap, W, ldw, M, N, K, e2, st);
+        case 17: if (K % 128 == 0) return launch<C17>(A, amap, W, ldw, M, N, K, e2, st);
+                 return launch<C15>(A, amap, W, ldw, M, N, K, e2, st);
         case 1: return launch<C1>(A, amap, W, ldw, M, N, K, e2, st);
-        default: return launch_ln<C15>(A, amap, W, ldw, M, N, K, e2, st);
+        default: return launch<C15>(A, amap, W, ldw, M, N, K, e2, st);
     }
 }
 
-// Full-row projection + LayerNorm (fast mode). N is fixed to 512; K % 32 == 0; 16-B aligned rows.
-hipError_t pfm_gemm_bf16_ln(const void* A, RowMap amap, const void* W, long long ldw, int M, int N, int K,
-                            const GemmEpi& epi, const float* gamma, const float* beta, float eps, void* ln_out,
-                            RowMap ln_map, int ln_dtype, void* ln_out2, RowMap ln_map2, hipStream_t st) {
-    if (M <= 0) return hipSuccess;
-    if (N != LN_N || K % LN_BK || ldw % 8 || amap.ld % 8 || (amap.rows_per_seg > 0 && amap.seg_stride % 8))
-        return hipErrorInvalidValue;
-    if ((epi.res0 && epi.ld_res0 % 4) || (epi.res1 && epi.ld_res1 % 4) || (epi.out && !rowmap_vec4(epi.out_map)) ||
-        !rowmap_vec4(ln_map) || (ln_out2 && !rowmap_vec4(ln_map2)))
-        return hipErrorInvalidValue;
-    static bool attr_done = false;
-    if (!attr_done) {
-        attr_done = true;
-        (void)hipFuncSetAttribute((const void*)gemm_bf16_ln_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, LN_LDS);
-    }
-    LnEpi ln;
-    ln.gamma = gamma; ln.beta = beta; ln.eps = eps; ln.out = ln_out; ln.map = ln_map; ln.dtype = ln_dtype;
-    ln.out2 = ln_out2; ln.map2 = ln_map2;
-    hipLaunchKernelGGL(gemm_bf16_ln_kernel, dim3((M + LN_BM - 1) / LN_BM), dim3(512), LN_LDS, st, (const bf16*)A, amap,
-                       (const bf16*)W, ldw, M, K, epi, ln);
-    PFM_LAUNCH_CHECK();
-    return hipSuccess;
-}

@@ -98,7 +98,7 @@ bool pfm_gemm_skinny_ok(const void* A, RowMap amap, const void* W, long long ldw
     if (M < 1 || K % 32 != 0 || ldw % 8 != 0 || amap.ld % 8 != 0) return false;
     if (amap.rows_per_seg > 0 && amap.seg_stride % 8 != 0) return false;
     if (((uintptr_t)A | (uintptr_t)W) % 16 != 0) return false;
-    if (!e.out || e.amax_val || e.ln_st_in || e.ln_st_out) return false;
+    if (!e.out || e.amax_val) return false;
     if (!pfm_knobs().gemm_skinny) return false;    // PFM_GEMM_SKINNY=0: tiled kernels for every M (A/B)
     if (pfm_knobs().gemm_cfg != 0) return false;   // a forced tile configuration wins (tile-config tests / A/B)
     // beyond 64 rows: only while the tiled kernels would launch fewer than ~64 128x256 tiles (the

@@ -27,9 +27,6 @@ bool pfm_gemm_bf16_256_ok(RowMap amap, long long ldw, int K);
 int pfm_gemm_bf16_256_amax_tiles(int N);
 hipError_t pfm_gemm_bf16_256(const void* A, RowMap amap, const void* W, long long ldw, int M, int N, int K,
                              const GemmEpi& epi, hipStream_t st);
-hipError_t pfm_gemm_bf16_ln(const void* A, RowMap amap, const void* W, long long ldw, int M, int N, int K,
-                            const GemmEpi& epi, const float* gamma, const float* beta, float eps, void* ln_out,
-                            RowMap ln_map, int ln_dtype, void* ln_out2, RowMap ln_map2, hipStream_t st);
 hipError_t pfm_attention(int dtype, const void* q, RowMap qmap, const void* k, RowMap kmap, const void* v,
                          RowMap vmap, float* o, long long ldo, void* o2, const int* klen, int B, int Tq, int Tk,
                          int heads, int dk, float scale, hipStream_t st);
@@ -57,8 +54,6 @@ hipError_t pfm_cif_fire(const float* alphas, const float* h, RowMap hmap, int B,
 hipError_t pfm_argmax_reduce(const float* val, const int* idx, int ntiles, int ncount, int B, int L, const int* ntok,
                              int Lcap, int* tokens, float* score, hipStream_t st);
 hipError_t pfm_fill_i32(int* p, long long n, int v, hipStream_t st);
-hipError_t pfm_ln_fold(const float* W, int N, int K, const float* gamma, const float* beta, const float* bias, bf16* Wf,
-                       float* colsum, float* colbias, hipStream_t st);
 hipError_t pfm_sv_input(const float* feats, const int* lens, const float* embed, const int* qid, int nq, int B, int T,
                         int I, float* x, int* olen, hipStream_t st);
 hipError_t pfm_ctc_collapse(const int* ids, long long ld, const int* olen, int B, int blank, int Lcap, int* tokens,
@@ -156,36 +151,27 @@ void pfm_knobs_refresh() {
         return (e && e[0]) ? atoi(e) : dflt;
     };
     PfmKnobs k;
-    k.ln_fold = iv("PFM_LN_FOLD", 0) == 1;
     k.gemm_kernel = iv("PFM_GEMM_KERNEL", 0);
     k.attn_fsmn = iv("PFM_ATTN_FSMN", 1) != 0;
     k.attn_waves = iv("PFM_ATTN_WAVES", 8);
-    k.attn_pp = iv("PFM_ATTN_PP", 0) == 1;
     k.kv_overlap = iv("PFM_KV_OVERLAP", 1) != 0;
-    k.gemm_ln = iv("PFM_GEMM_LN", 0) == 1;
     k.subbatch = std::max(1, std::min(iv("PFM_SUBBATCH", 2), 4));
     k.stream_graph = iv("PFM_STREAM_GRAPH", 1) != 0;
     k.fsmn_v2 = iv("PFM_FSMN_V2", 0);
     k.gemm_gm = iv("PFM_GEMM_GM", -1);
     k.gemm_cfg = iv("PFM_GEMM_CFG", 0);
-    k.gemm_policy = iv("PFM_GEMM_POLICY", 0);
     k.gemm_st16 = iv("PFM_GEMM_ST16", 1) != 0;
-    k.gemm_preres = iv("PFM_GEMM_PRERES", 0) == 1;
     k.gemm_resbatch = iv("PFM_GEMM_RESBATCH", 1) != 0;
     k.gemm_skinny = iv("PFM_GEMM_SKINNY", 1) != 0;
     k.ffn_fused = iv("PFM_FFN_FUSED", 1) != 0;
-    k.ffn_var = iv("PFM_FFN_VAR", 0);
     k.exact_x6 = iv("PFM_EXACT_X6", 1) != 0;
-    k.attn_var = iv("PFM_ATTN_VAR", 0);
     k.dec_subbatch = std::max(1, iv("PFM_DEC_SUBBATCH", 2));
     k.ffn_op = iv("PFM_FFN_OP", 1) != 0;
     k.dec_ffn_fused = iv("PFM_DEC_FFN_FUSED", 1) != 0;
-    k.ffn_hr = iv("PFM_FFN_HR", 1) != 0;
-    k.ffn_pd = iv("PFM_FFN_PD", 3) == 2 ? 2 : 3;
     k.ffn_kernel = iv("PFM_FFN_KERNEL", 1) == 2 ? 2 : 1;
     k.dec_ffn_kernel = iv("PFM_DEC_FFN_KERNEL", 1) == 2 ? 2 : 1;
     k.exact_terms = iv("PFM_EXACT_TERMS", 6) == 3 ? 3 : 6;
-    const int* f = &k.ln_fold;
+    const int* f = &k.gemm_kernel;
     unsigned long long s = 1469598103934665603ull;   // FNV-1a over the fields
     for (int i = 0; i < PFM_KNOB_FIELDS; ++i) s = (s ^ (unsigned long long)(unsigned)f[i]) * 1099511628211ull;
     k.sig = s;
@@ -235,9 +221,6 @@ struct EncLayer {
     size_t ln1g, ln1b, wqkv, bqkv, wo, bo, fsmn, ln2g, ln2b, w1, b1, w2, b2;
     int din;
     size_t ffp = 0;   // fast mode: element offset of the packed W1 | W2 ring tiles in ffn_pack (k_ffn.hip)
-    // fast mode, LayerNorm folded into QKV (norm1) and FFN w1 (norm2): bf16(W o gamma) in fold_w,
-    // column sums / folded biases in fold_f (element offsets)
-    size_t fq_w = 0, fq_cs = 0, fq_cb = 0, f1_w = 0, f1_cs = 0, f1_cb = 0;
 };
 struct DecLayer { size_t fsmn, wq, bq, wo, bo, w1, b1, w2, ng, nb, n1g, n1b, n2g, n2b, n3g, n3b; };
 
@@ -252,8 +235,6 @@ struct pfm_handle {
     size_t arena_elems = 0;
     DevBuf arena;                  // all f32 weights
     DevBuf arena_bf;               // bf16 copies of GEMM weights (same element offsets)
-    DevBuf fold_w, fold_f;         // LayerNorm-folded projection weights (bf16) and column terms (f32)
-    bool fold_ready = false;
     DevBuf qkv0_pad;               // fast mode: layer 0's bf16 QKV weights with K padded to a multiple of 64
     DevBuf ffn_pack;               // fused-FFN weight tiles of every encoder layer (bf16, LDS-image order)
     bool ffn_ready = false;
@@ -449,12 +430,6 @@ void make_pe(std::vector<float>& pe, int T, int depth) {
     }
 }
 
-// PFM_LN_FOLD=1: fast mode folds norm1 / norm2 into the QKV / FFN w1 projections. Opt-in: it is the
-// more accurate fast path (token agreement with exact mode 0.85 vs 0.73-0.79 on the goldens) but measured
-// 0.6-0.9 ms/step slower than the standalone streaming LayerNorm (the producers' extra bf16(x) write and
-// statistics reductions cost more than the two LN passes they delete).
-bool ln_fold_enabled() { return pfm_knobs().ln_fold; }
-
 // the fused FFN kernel is written for the Paraformer / SenseVoice encoder width (512 -> 2048 -> 512)
 bool ffn_shape_ok(const pfm_config& c) { return c.d_model == 512 && c.ffn == 2048; }
 
@@ -473,28 +448,6 @@ int ensure_bf16(pfm_handle* h, hipStream_t st) {
                                      (size_t)din * 2, N, hipMemcpyDeviceToDevice, st));
         }
         h->bf_ready = true;
-    }
-    if (!h->fold_ready && h->cfg.d_model == 512 && ln_fold_enabled()) {
-        // norm1 -> linear_q_k_v (512-wide layers) and norm2 -> feed_forward.w_1 (every layer)
-        const pfm_config& c = h->cfg;
-        const size_t D = c.d_model, F = c.ffn;
-        size_t nw = 0, nf = 0;
-        for (auto& L : h->enc) {
-            if (L.din == (int)D) { L.fq_w = nw; nw += 3 * D * D; L.fq_cs = nf; L.fq_cb = nf + 3 * D; nf += 6 * D; }
-            L.f1_w = nw; nw += F * D; L.f1_cs = nf; L.f1_cb = nf + F; nf += 2 * F;
-        }
-        HIP_TRY(h->fold_w.ensure(nw * sizeof(bf16)));
-        HIP_TRY(h->fold_f.ensure(nf * sizeof(float)));
-        bf16* fw = h->fold_w.as<bf16>();
-        float* ff = h->fold_f.as<float>();
-        for (auto& L : h->enc) {
-            if (L.din == (int)D)
-                HIP_TRY(pfm_ln_fold(h->w(L.wqkv), 3 * D, D, h->w(L.ln1g), h->w(L.ln1b), h->w(L.bqkv), fw + L.fq_w,
-                                    ff + L.fq_cs, ff + L.fq_cb, st));
-            HIP_TRY(pfm_ln_fold(h->w(L.w1), F, D, h->w(L.ln2g), h->w(L.ln2b), h->w(L.b1), fw + L.f1_w, ff + L.f1_cs,
-                                ff + L.f1_cb, st));
-        }
-        h->fold_ready = true;
     }
     // k_ffn.hip (1) and k_ffn2.hip (2) order their fragments differently; encoder and decoder choose separately
     const int fk = pfm_knobs().ffn_kernel, dk = pfm_knobs().dec_ffn_kernel;
@@ -698,14 +651,10 @@ hipError_t gemm_dispatch(int dtype, const void* A, RowMap amap, const void* W, l
 
 bool attn_fsmn_enabled() {   // PFM_ATTN_FSMN=0: separate FSMN kernel (A/B; parity test compares both)
     const PfmKnobs& k = pfm_knobs();
-    return k.attn_fsmn && k.attn_waves == 8 && !k.attn_pp;
+    return k.attn_fsmn && k.attn_waves == 8;
 }
 
 bool kv_overlap_enabled() { return pfm_knobs().kv_overlap; }   // 0: memory K|V in-line on the caller's stream
-
-// PFM_GEMM_LN=1 enables the full-row GEMM+LayerNorm fusion (measured slower than GEMM + standalone LN on
-// MI355X; kept for A/B runs)
-bool gemm_ln_enabled() { return pfm_knobs().gemm_ln; }
 
 // EXACT-mode GEMM on the split-bf16 path: f32 weights with ld == K inside the arena, K a multiple of 64
 bool x6_route(const pfm_handle* h, int dtype, const void* W, long long ldw, int K) {
@@ -794,7 +743,6 @@ struct Run {
     float qscale;    // d_k ** -0.5
     bool fuse_fsmn;  // fast mode: encoder FSMN in the attention epilogue
     bool fuse_fsmn_x6 = false;   // EXACT mode (x3): the f32 FSMN in the x6 attention epilogue
-    bool fuse_ln;    // opt-in (PFM_GEMM_LN=1): LayerNorm fused into the 512-wide projections
     bool x3 = false;     // EXACT mode on split-bf16 x6: producers write GEMM operands as three bf16 planes
     bool raw_input = false;                 // streaming: the stack input is already x sqrt(d) + PE
     const struct ChunkKV* ck = nullptr;     // streaming: self-attention keys = K/V cache ++ window
@@ -806,7 +754,6 @@ struct Run {
         qscale = (float)(1.0 / sqrt((double)(c.d_model / c.heads)));
         const int lenc = (c.kernel_size - 1) / 2 + (c.enc_sanm_shift > 0 ? c.enc_sanm_shift : 0);
         fuse_fsmn = fast && c.kernel_size == 11 && lenc == 5 && c.d_model / c.heads == 128 && attn_fsmn_enabled();
-        fuse_ln = fast && c.d_model == 512 && c.ffn % 32 == 0 && gemm_ln_enabled();
         x3 = !fast && h->x6_ready && pfm_knobs().exact_x6 && c.d_model % 64 == 0 && c.ffn % 64 == 0 &&
              c.d_model / c.heads == 128;
         fuse_fsmn_x6 = x3 && c.kernel_size == 11 && lenc == 5 && pfm_knobs().attn_fsmn;
@@ -860,18 +807,6 @@ struct Run {
         const double by = ((double)Bb * Tq + 2.0 * Bb * Tk) * c.d_model * es + (double)Bb * Tq * c.d_model * (o ? 4 : 2);
         ProfScope ps(h, st, PFM_K_ATTN, fl, by);
         return pfm_attention(dtp, q, qm, k, km, v, vm, o, ldo, o2, kl, Bb, Tq, Tk, c.heads, (int)dk, qscale, st);
-    }
-    // 512-wide projection with the following LayerNorm in its epilogue (opt-in fusion)
-    hipError_t gemm_ln(const void* A, RowMap am, const void* Wt, long long ldw, int Mm, int Kk, const GemmEpi& e,
-                       size_t g, size_t b, void* lo, RowMap lm, int ldt, void* lo2, RowMap lm2) const {
-        const int D = h->cfg.d_model;
-        const double fl = 2.0 * Mm * D * Kk;
-        const double by = ((double)Mm * Kk + (double)D * Kk) * 2.0 + (double)Mm * D * (e.out ? 4.0 : 0.0) +
-                          (e.res0 ? (e.res0_bf16 ? 2.0 : 4.0) * Mm * D : 0.0) + (e.res1 ? 4.0 * Mm * D : 0.0) +
-                          (double)Mm * D * (ldt == DT_F32 ? 4.0 : 2.0) + (lo2 ? 2.0 * Mm * D : 0.0);
-        ProfScope ps(h, st, PFM_K_GEMM, fl, by);
-        return pfm_gemm_bf16_ln(A, am, Wt, ldw, Mm, D, Kk, e, h->w(g), h->w(b), h->cfg.ln_eps, lo, lm, ldt, lo2, lm2,
-                                st);
     }
 };
 
@@ -936,23 +871,9 @@ int encoder_stack(const Run& r, const float* x_in, const int* lens, int B, int T
     bf16* Ob = ws.Ob;
     void* Hh = ws.H;
     const RowMap plain = rowmap_plain(0);
-    const bool fuse_last = r.fuse_ln && (!fin.out2 || fin.o2dt == DT_BF16);
-    // fast mode: norm1 / norm2 folded into the QKV / FFN w1 projections (producers write bf16(x) + row
-    // statistics partials in their epilogues; ensure_bf16 prepared the folded weights)
-    const bool fold = fast && !r.fuse_ln && D == 512 && h->fold_ready && ln_fold_enabled();
-    const bf16* fw = h->fold_w.as<bf16>();
-    const float* ff = h->fold_f.as<float>();
-    auto fold_in = [&](GemmEpi& e, const float2* st, size_t cs, size_t cb) {
-        e.bias = ff + cb;
-        e.ln_st_in = st; e.ln_colsum = ff + cs; e.ln_parts = D / 64; e.ln_eps = c.ln_eps;
-    };
-    auto stats_out = [&](GemmEpi& e, float2* st) {
-        e.out2 = Xn; e.out2_map = rowmap_plain(D);   // bf16(x): the folded consumer's A operand
-        e.ln_st_out = st; e.ln_parts = D / 64;
-    };
     // fast mode, full-size batches: LN2 -> FFN -> residual -> next layer's LN1 as ONE kernel per layer
     // (k_ffn.hip); chunk-sized streaming steps keep the weight-streaming GEMMs
-    const bool ffn_fused = fast && !r.fuse_ln && !fold && h->ffn_ready && pfm_knobs().ffn_fused && M >= 4096;
+    const bool ffn_fused = fast && h->ffn_ready && pfm_knobs().ffn_fused && M >= 4096;
     // EXACT mode: LayerNorm, attention and FFN w1 write their consumer GEMM's operand in split form
     // (three bf16 planes, DT_X3) instead of f32 + a separate split pass
     const bool x3 = r.x3 && !r.ck;
@@ -976,7 +897,7 @@ int encoder_stack(const Run& r, const float* x_in, const int* lens, int B, int T
             HIP_TRY(pfm_layernorm(x_in, rowmap_plain(I), (int)M, I, r.P(L.ln1g), r.P(L.ln1b), c.ln_eps,
                                   h->pe.as<float>(), T, sqrtf((float)D), Xn, rowmap_plain(I), dt, nullptr, plain, 0,
                                   st));
-        else if ((!r.fuse_ln || l == l0) && !(fold && l > l0) && !(ffn_fused && l > l0))   // fused / folded: no LN1
+        else if (!(ffn_fused && l > l0))   // fused FFN: the previous layer's kernel wrote LN1(x)
             HIP_TRY(pfm_layernorm(X, rowmap_plain(D), (int)M, D, r.P(L.ln1g), r.P(L.ln1b), c.ln_eps, nullptr, 0, 1.f,
                                   Xn, xmap3, lndt, nullptr, plain, 0, st));
         {   // q|k|v = LN1(x) Wqkv^T + b   (fast mode: bf16 only — attention and FSMN read bf16)
@@ -984,10 +905,7 @@ int encoder_stack(const Run& r, const float* x_in, const int* lens, int B, int T
             e.bias = r.P(L.bqkv);
             if (fast) { e.out = QKVb; e.out_map = rowmap_plain(3 * D); e.out_dtype = DT_BF16; }
             else { e.out = QKV; e.out_map = rowmap_plain(3 * D); e.out_dtype = DT_F32; }
-            if (fold && l > l0) {   // Xn holds bf16(x) from the previous FFN w2 epilogue
-                fold_in(e, ws.st1, L.fq_cs, L.fq_cb);
-                HIP_TRY(r.gemm(dt, Xn, rowmap_plain(D), fw + L.fq_w, D, (int)M, 3 * D, D, e));
-            } else if (x3 && l > 0) {
+            if (x3 && l > 0) {
                 HIP_TRY(r.gemm3(Xn, xmap3, r.W(L.wqkv), din, (int)M, 3 * D, din, e));
             } else if (l == 0 && pad0) {
                 HIP_TRY(r.gemm(dt, Xn, rowmap_plain(Kp0), h->qkv0_pad.p, Kp0, (int)M, 3 * D, Kp0, e));
@@ -1049,20 +967,14 @@ int encoder_stack(const Run& r, const float* x_in, const int* lens, int B, int T
             e.res0 = fast ? (const float*)Fb : Fm; e.ld_res0 = D; e.res0_bf16 = fast ? 1 : 0;
             if (din == D) { e.res1 = X; e.ld_res1 = D; }
             e.out = X; e.out_map = rowmap_plain(D); e.out_dtype = DT_F32;
-            if (r.fuse_ln) {   // ... and Xn = LN2(x)
-                HIP_TRY(r.gemm_ln(Ob, rowmap_plain(D), r.W(L.wo), D, (int)M, D, e, L.ln2g, L.ln2b, Xn,
-                                  rowmap_plain(D), DT_BF16, nullptr, plain));
-            } else {
-                if (fold) stats_out(e, ws.st2);
-                if (x3)
-                    HIP_TRY(r.gemm3(O, xmap3, r.W(L.wo), D, (int)M, D, D, e));
-                else
-                    HIP_TRY(r.gemm(dt, fast ? (const void*)Ob : (const void*)O, rowmap_plain(D), r.W(L.wo), D, (int)M,
-                                   D, D, e));
-                if (!fold && !ffn_fused)
-                    HIP_TRY(pfm_layernorm(X, rowmap_plain(D), (int)M, D, r.P(L.ln2g), r.P(L.ln2b), c.ln_eps, nullptr,
-                                          0, 1.f, Xn, xmap3, lndt, nullptr, plain, 0, st));
-            }
+            if (x3)
+                HIP_TRY(r.gemm3(O, xmap3, r.W(L.wo), D, (int)M, D, D, e));
+            else
+                HIP_TRY(r.gemm(dt, fast ? (const void*)Ob : (const void*)O, rowmap_plain(D), r.W(L.wo), D, (int)M, D,
+                               D, e));
+            if (!ffn_fused)
+                HIP_TRY(pfm_layernorm(X, rowmap_plain(D), (int)M, D, r.P(L.ln2g), r.P(L.ln2b), c.ln_eps, nullptr, 0,
+                                      1.f, Xn, xmap3, lndt, nullptr, plain, 0, st));
         }
         if (ffn_fused) {   // x = x + W2 relu(W1 LN2(x) + b1) + b2 ; Xn = LN1_{l+1}(x)
             const bool nxt = l + 1 < l1;
@@ -1088,10 +1000,7 @@ int encoder_stack(const Run& r, const float* x_in, const int* lens, int B, int T
             GemmEpi e = epi_default();
             e.bias = r.P(L.b1); e.relu = 1;
             e.out = Hh; e.out_map = rowmap_plain(Fd); e.out_dtype = dt;
-            if (fold) {
-                fold_in(e, ws.st2, L.f1_cs, L.f1_cb);
-                HIP_TRY(r.gemm(dt, Xn, rowmap_plain(D), fw + L.f1_w, D, (int)M, Fd, D, e));
-            } else if (x3) {   // h written as w2's split operand
+            if (x3) {   // h written as w2's split operand
                 e.out_map = rowmap_plain(3 * Fd); e.out_dtype = DT_X3;
                 HIP_TRY(r.gemm3(Xn, xmap3, r.W(L.w1), D, (int)M, Fd, D, e));
             } else {
@@ -1103,26 +1012,14 @@ int encoder_stack(const Run& r, const float* x_in, const int* lens, int B, int T
             e.bias = r.P(L.b2);
             e.res0 = X; e.ld_res0 = D;
             e.out = X; e.out_map = rowmap_plain(D); e.out_dtype = DT_F32;
-            if (x3) {
+            if (x3)
                 HIP_TRY(r.gemm3(Hh, rowmap_plain(3 * Fd), r.W(L.w2), Fd, (int)M, D, Fd, e));
-            } else if (!r.fuse_ln) {
-                if (fold && l + 1 < l1) stats_out(e, ws.st1);   // feeds the next layer's folded norm1
+            else
                 HIP_TRY(r.gemm(dt, Hh, rowmap_plain(Fd), r.W(L.w2), Fd, (int)M, D, Fd, e));
-            } else if (l + 1 < l1) {   // ... and Xn = LN1_{l+1}(x)
-                HIP_TRY(r.gemm_ln(Hh, rowmap_plain(Fd), r.W(L.w2), Fd, (int)M, Fd, e, h->enc[l + 1].ln1g,
-                                  h->enc[l + 1].ln1b, Xn, rowmap_plain(D), DT_BF16, nullptr, plain));
-            } else if (fuse_last) {   // last layer: x itself is dead; the closing LN straight into its outputs
-                e.out = nullptr;
-                HIP_TRY(r.gemm_ln(Hh, rowmap_plain(Fd), r.W(L.w2), Fd, (int)M, Fd, e, fin.g, fin.b, fin.out,
-                                  fin.omap, fin.odt, fin.out2, fin.o2map));
-            } else {
-                HIP_TRY(r.gemm(dt, Hh, rowmap_plain(Fd), r.W(L.w2), Fd, (int)M, D, Fd, e));
-            }
         }
     }
-    if (!fuse_last || l1 == l0)
-        HIP_TRY(pfm_layernorm(X, rowmap_plain(D), (int)M, D, r.P(fin.g), r.P(fin.b), c.ln_eps, nullptr, 0, 1.f, fin.out,
-                              fin.omap, fin.odt, fin.out2, fin.o2map, fin.o2dt, st));
+    HIP_TRY(pfm_layernorm(X, rowmap_plain(D), (int)M, D, r.P(fin.g), r.P(fin.b), c.ln_eps, nullptr, 0, 1.f, fin.out,
+                          fin.omap, fin.odt, fin.out2, fin.o2map, fin.o2dt, st));
     return PFM_OK;
 }
 
@@ -1252,7 +1149,6 @@ void pfm_destroy(pfm_handle* h) {
 static void weight_written(pfm_handle* h, WEntry& e) {
     if (!e.set) { e.set = true; h->missing--; }
     h->bf_ready = false;
-    h->fold_ready = false;
     h->ffn_ready = false;
     h->dffn_ready = false;
     h->x6_ready = false;   // ensure_x6 re-splits arena_x6 and the padded planes in place (stable addresses)
@@ -1357,16 +1253,11 @@ int pfm_run(pfm_handle* h, void* stream, int mode, const float* feats, const int
     if (h->prof_on && h->ev_used > 4096) prof_collect(h);
     const double es = fast ? 2.0 : 4.0;
     const Run run(h, st, fast);
-    const bool fuse_ln = run.fuse_ln;
     auto GEMM = [&](int dtp, const void* A, RowMap am, const void* Wt, long long ldw, int Mm, int N, int Kk,
                     const GemmEpi& e) -> hipError_t { return run.gemm(dtp, A, am, Wt, ldw, Mm, N, Kk, e); };
     auto ATTN = [&](int dtp, const void* q, RowMap qm, const void* k, RowMap km, const void* v, RowMap vm, float* o,
                     long long ldo, void* o2, const int* kl, int Bb, int Tq, int Tk) -> hipError_t {
         return run.attn(dtp, q, qm, k, km, v, vm, o, ldo, o2, kl, Bb, Tq, Tk);
-    };
-    auto GEMM_LN = [&](const void* A, RowMap am, const void* Wt, long long ldw, int Mm, int Kk, const GemmEpi& e,
-                       size_t g, size_t b, void* lo, RowMap lm, int ldt, void* lo2, RowMap lm2) -> hipError_t {
-        return run.gemm_ln(A, am, Wt, ldw, Mm, Kk, e, g, b, lo, lm, ldt, lo2, lm2);
     };
     auto W = [&](size_t off) -> const void* { return run.W(off); };
     auto P = [&](size_t off) -> const float* { return run.P(off); };
@@ -1491,9 +1382,9 @@ int pfm_run(pfm_handle* h, void* stream, int mode, const float* feats, const int
         const int* lg = lens + b0;
         const char* KVg = (const char*)KV + (size_t)b0 * T * nkv * esz;
         // fast mode: each decoder FFN (+ its LN1 before, + the LN after) as one fused kernel (k_ffn.hip DEC)
-        const bool dffn = fast && !fuse_ln && h->dffn_ready && pfm_knobs().dec_ffn_fused && Mg >= 2048;
+        const bool dffn = fast && h->dffn_ready && pfm_knobs().dec_ffn_fused && Mg >= 2048;
         int op_from = -1;   // fused path: the decoder block whose out-projection runs inside the next FFN launch
-        auto ffn = [&](int fi, bool xdn_ready, size_t lng, size_t lnb, size_t w1, size_t b1, size_t fng, size_t fnb,
+        auto ffn = [&](int fi, size_t lng, size_t lnb, size_t w1, size_t b1, size_t fng, size_t fnb,
                        size_t w2, float* out, size_t pg, size_t pb, void* pout, int pdt) -> int {
             // out = W2 . LN_F(relu(W1 . LN(x) + b1)); pout = LN_P(out)   (sanm/positionwise_feed_forward.py:26-33)
             if (dffn && pdt == DT_BF16) {   // out itself is dead in the decoder: only LN_P(out) is consumed
@@ -1513,9 +1404,8 @@ int pfm_run(pfm_handle* h, void* stream, int mode, const float* feats, const int
                 }
                 return PFM_OK;
             }
-            if (!xdn_ready)
-                HIP_TRY(pfm_layernorm(Xd, rowmap_plain(D), Mg, D, P(lng), P(lnb), c.ln_eps, nullptr, 0, 1.f, Xdn, xdm,
-                                      ndt, nullptr, plain, 0, s));
+            HIP_TRY(pfm_layernorm(Xd, rowmap_plain(D), Mg, D, P(lng), P(lnb), c.ln_eps, nullptr, 0, 1.f, Xdn, xdm, ndt,
+                                  nullptr, plain, 0, s));
             GemmEpi e = epi_default();
             e.bias = P(b1); e.relu = 1;
             e.out = Hd; e.out_map = rowmap_plain(Fd); e.out_dtype = fast ? DT_BF16 : DT_F32;   // fast: bf16 hidden
@@ -1527,23 +1417,17 @@ int pfm_run(pfm_handle* h, void* stream, int mode, const float* feats, const int
                 HIP_TRY(pfm_layernorm((const float*)Hd, rowmap_plain(Fd), Mg, Fd, P(fng), P(fnb), c.ln_eps, nullptr, 0,
                                       1.f, Hdn, hdm, ndt, nullptr, plain, 0, s));
             GemmEpi e2 = epi_default();
-            if (fuse_ln) {   // out itself is dead; only LN_P(out) is consumed
-                HIP_TRY(rg.gemm_ln(Hdn, rowmap_plain(Fd), W(w2), Fd, Mg, Fd, e2, pg, pb, pout, rowmap_plain(D), pdt,
-                                   nullptr, plain));
-            } else {
-                e2.out = out; e2.out_map = rowmap_plain(D); e2.out_dtype = DT_F32;
-                HIP_TRY(gemmA(Hdn, true, W(w2), D, Fd, e2));
-                HIP_TRY(pfm_layernorm(out, rowmap_plain(D), Mg, D, P(pg), P(pb), c.ln_eps, nullptr, 0, 1.f, pout,
-                                      rowmap_plain(pdt == DT_X3 ? 3 * D : D), pdt, nullptr, plain, 0, s));
-            }
+            e2.out = out; e2.out_map = rowmap_plain(D); e2.out_dtype = DT_F32;
+            HIP_TRY(gemmA(Hdn, true, W(w2), D, Fd, e2));
+            HIP_TRY(pfm_layernorm(out, rowmap_plain(D), Mg, D, P(pg), P(pb), c.ln_eps, nullptr, 0, 1.f, pout,
+                                  rowmap_plain(pdt == DT_X3 ? 3 * D : D), pdt, nullptr, plain, 0, s));
             return PFM_OK;
         };
-        bool xdn_ready = false;   // Xdn already holds LN1(x) of the next block (fused out-proj epilogue)
         for (int l = 0; l < c.dec_blocks; ++l) {
             const DecLayer& Lr = h->dec[l];
             // t = FFN(LN1(x)); x = x + FSMN(LN2(t))   (decoder.py:97-107)
             // fast mode: LN2(t) in bf16 feeding the bf16-input FSMN (x += FSMN(LN2(t)) stays f32)
-            int rc2 = ffn(l, xdn_ready, Lr.n1g, Lr.n1b, Lr.w1, Lr.b1, Lr.ng, Lr.nb, Lr.w2, Td, Lr.n2g, Lr.n2b, Tdn,
+            int rc2 = ffn(l, Lr.n1g, Lr.n1b, Lr.w1, Lr.b1, Lr.ng, Lr.nb, Lr.w2, Td, Lr.n2g, Lr.n2b, Tdn,
                           fast ? DT_BF16 : DT_F32);
             if (rc2) return rc2;
             // x = x + CrossAtt(LN3(x), memory)   (decoder.py:109-119); fused path: LN3 in the FSMN kernel
@@ -1581,13 +1465,7 @@ int pfm_run(pfm_handle* h, void* stream, int mode, const float* feats, const int
                 e.bias = P(Lr.bo);
                 e.res0 = Xd; e.ld_res0 = D;
                 e.out = Xd; e.out_map = rowmap_plain(D); e.out_dtype = DT_F32;
-                if (fuse_ln) {   // ... and Xdn = LN1 of the next block (decoders[l+1] or decoders3)
-                    const size_t ng = l + 1 < c.dec_blocks ? h->dec[l + 1].n1g : h->d3n1g;
-                    const size_t nbb = l + 1 < c.dec_blocks ? h->dec[l + 1].n1b : h->d3n1b;
-                    HIP_TRY(rg.gemm_ln(Odb, rowmap_plain(D), W(Lr.wo), D, Mg, D, e, ng, nbb, Xdn, rowmap_plain(D), dt,
-                                       nullptr, plain));
-                    xdn_ready = true;
-                } else if (dffn) {   // runs as phase 0 of the next FFN launch
+                if (dffn) {   // runs as phase 0 of the next FFN launch
                     op_from = l;
                 } else {
                     HIP_TRY(gemmA(fast ? (const void*)Odb : (const void*)Od, false, W(Lr.wo), D, D, e));
@@ -1595,7 +1473,7 @@ int pfm_run(pfm_handle* h, void* stream, int mode, const float* feats, const int
             }
         }
         // decoders3: x = FFN(LN1(x)), no residual (decoder.py:97-100 with self_attn = src_attn = None)
-        int rc3 = ffn(c.dec_blocks, xdn_ready, h->d3n1g, h->d3n1b, h->d3w1, h->d3b1, h->d3ng, h->d3nb, h->d3w2, Xd, h->dan_g,
+        int rc3 = ffn(c.dec_blocks, h->d3n1g, h->d3n1b, h->d3w1, h->d3b1, h->d3ng, h->d3nb, h->d3w2, Xd, h->dan_g,
                       h->dan_b, Xdn, ndt);
         if (rc3) return rc3;
         {   // output layer with fused row-argmax (logits never written)
@@ -1956,20 +1834,6 @@ int pfm_op_ffn_dec(void* stream, const float* x, int M, const float* g1, const f
         HIP_TRY(dec(x, M, g1, b1n, eps, wp + po, b1, cc, cc + 512, xo, gn, bn, (bf16*)xn, nullptr, nullptr, st));
     }
     HIP_TRY(hipStreamSynchronize(st));
-    return PFM_OK;
-}
-
-int pfm_op_gemm_layernorm(void* stream, const void* A, const void* Wt, const float* bias, const float* res, float* C,
-                          const float* gamma, const float* beta, float eps, float* Y, int M, int N, int K) {
-    pfm_knobs_refresh();
-    if (!A || !Wt || !gamma || !beta || !Y || M < 0) return fail(PFM_E_ARG, "pfm_op_gemm_layernorm: null argument");
-    if (N != 512 || K % 32) return fail(PFM_E_ARG, "pfm_op_gemm_layernorm: needs N == 512 and K % 32 == 0");
-    GemmEpi e = epi_default();
-    e.bias = bias;
-    if (res) { e.res0 = res; e.ld_res0 = N; }
-    if (C) { e.out = C; e.out_map = rowmap_plain(N); e.out_dtype = DT_F32; }
-    HIP_TRY(pfm_gemm_bf16_ln(A, rowmap_plain(K), Wt, K, M, N, K, e, gamma, beta, eps, Y, rowmap_plain(N), DT_F32,
-                             nullptr, rowmap_plain(0), (hipStream_t)stream));
     return PFM_OK;
 }
 

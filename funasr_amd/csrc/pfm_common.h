@@ -97,19 +97,7 @@ struct GemmEpi {
     // set by the bf16 launcher: bf16-only output with 16-B aligned rows -> 8 columns per lane,
     // one 16-B store each (halves the store-issue tail of the big bf16 outputs)
     int st16_ok;
-    // set by the bf16 launcher: residual GEMMs may start their accumulators from res0 + res1
-    int pre_res_ok;
     int res_batch;          // epilogue: residual loads of 4 row groups issued before their stores
-    // LayerNorm statistics producer (fast mode): per (output row, 64-column wave slice) the slice's
-    // (mean, M2) of the final values, at ln_st_out[row * ln_parts + col / 64]
-    float2* ln_st_out;
-    int ln_parts;
-    // LayerNorm folded into this GEMM (consumer): A = bf16(x), W = bf16(W o gamma) and
-    //   out = rstd_r * (acc - mean_r * ln_colsum[n]) + bias[n]        (bias = b + W.beta)
-    // with (mean_r, rstd_r) combined from the producer's ln_parts partials of row r
-    const float2* ln_st_in;
-    const float* ln_colsum;
-    float ln_eps;
     // three-way split bf16 emulation of an f32 GEMM (EXACT mode, bf16 256-tile kernel): A = [A0 | A1 | A2]
     // ([M, 3 x6_k], x = x0 + x1 + x2 exactly), W = three bf16 planes x6_ws elements apart; the kernel runs
     // K' = 6 x6_k over the segments (A2,W0) (A1,W1) (A0,W2) (A1,W0) (A0,W1) (A0,W0). 0 = plain GEMM.
@@ -138,38 +126,29 @@ static inline int epi_vec_ok(const GemmEpi& e, int N) {
 // thread's snapshot through pfm_knobs(). `sig` hashes every field: captured streaming graphs are keyed
 // by it, so a changed knob never replays a graph recorded under other settings.
 struct PfmKnobs {
-    int ln_fold;            // PFM_LN_FOLD=1: LayerNorm folded into QKV / FFN w1 (fast mode)
     int gemm_kernel;        // PFM_GEMM_KERNEL=128: force the 128x128 kernel
     int attn_fsmn;          // PFM_ATTN_FSMN (default 1): encoder FSMN fused into the attention epilogue
     int attn_waves;         // PFM_ATTN_WAVES (default 8)
-    int attn_pp;            // PFM_ATTN_PP=1: ping-pong 8-wave attention
     int kv_overlap;         // PFM_KV_OVERLAP (default 1): memory K|V projection on the side stream
-    int gemm_ln;            // PFM_GEMM_LN=1: full-row GEMM + LayerNorm fusion
     int subbatch;           // PFM_SUBBATCH (default 2): concurrent encoder utterance groups
     int stream_graph;       // PFM_STREAM_GRAPH (default 1): streaming steps through HIP graphs
     int fsmn_v2;            // PFM_FSMN_V2: frames per thread of the 8-channel FSMN kernel (0 = 4-channel)
     int gemm_gm;            // PFM_GEMM_GM: grouped tile order override (-1 = default)
     int gemm_cfg;           // PFM_GEMM_CFG: forced tile configuration (0 = policy)
-    int gemm_policy;        // PFM_GEMM_POLICY: alternative tile policies (0 = default)
     int gemm_st16;          // PFM_GEMM_ST16 (default 1): 16-B bf16 epilogue stores
-    int gemm_preres;        // PFM_GEMM_PRERES=1: residual pre-loaded into the accumulators
     int gemm_resbatch;      // PFM_GEMM_RESBATCH (default 1): residual loads batched ahead of the stores
     int gemm_skinny;        // PFM_GEMM_SKINNY (default 1): weight-streaming kernel for <= 64-row GEMMs
     int ffn_fused;          // PFM_FFN_FUSED (default 1): fused LN2 + FFN + LN1_next encoder kernel (k_ffn.hip)
-    int ffn_var;            // PFM_FFN_VAR: diagnostic variants of the fused FFN kernel (0 = the kernel)
     int exact_x6;           // PFM_EXACT_X6 (default 1): EXACT-mode GEMMs as split bf16 x6 MFMA (f32 MFMA if 0)
-    int attn_var;           // PFM_ATTN_VAR: diagnostic variants of the 8-wave bf16 attention kernel (0 = the kernel)
     int dec_subbatch;       // PFM_DEC_SUBBATCH (default 2): decoder utterance groups on concurrent streams
     int ffn_op;             // PFM_FFN_OP (default 1): encoder out-projection folded into the fused FFN kernel
     int dec_ffn_fused;      // PFM_DEC_FFN_FUSED (default 1): decoder LN1-FFN(LN_F folded)-LN kernel (fast mode)
-    int ffn_hr;             // PFM_FFN_HR (default 1): fused FFN phase 0/2 activation fragments read once per k step
-    int ffn_pd;             // PFM_FFN_PD (default 3): fused FFN weight tiles in flight behind the published one (2 or 3)
     int ffn_kernel;         // PFM_FFN_KERNEL (default 1): encoder fused FFN as 64-row workgroups (k_ffn.hip);
                             // 2 = 128-row workgroups (k_ffn2.hip; pays only when M / 128 fills the chip)
     int dec_ffn_kernel;     // PFM_DEC_FFN_KERNEL (default 1): the same choice for the decoder FFN
     int exact_terms;        // PFM_EXACT_TERMS (default 6): products per EXACT-mode split-bf16 GEMM; 3 = bf16x3
     unsigned long long sig;
 };
-#define PFM_KNOB_FIELDS 29
+#define PFM_KNOB_FIELDS 20
 const PfmKnobs& pfm_knobs();   // the calling thread's snapshot (refreshed lazily if no entry point did yet)
 void pfm_knobs_refresh();

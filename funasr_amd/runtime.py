@@ -25,7 +25,7 @@ MODES = {"exact": MODE_EXACT, "fp32": MODE_EXACT, "fast": MODE_FAST, "bf16": MOD
 # every symbol include/pfm.h declares (checked by tests/test_abi.py)
 ABI_SYMBOLS = ("pfm_config_default", "pfm_config_sensevoice", "pfm_create", "pfm_set_weight", "pfm_set_weight_device",
                "pfm_missing_weights", "pfm_reserve", "pfm_run", "pfm_run_ctc", "pfm_op_ctc_collapse", "pfm_fbank", "pfm_lfr_frames", "pfm_last_error", "pfm_destroy", "pfm_op_gemm",
-               "pfm_op_attention", "pfm_op_layernorm", "pfm_op_fsmn", "pfm_op_cif", "pfm_profile", "pfm_op_gemm_layernorm", "pfm_op_ffn", "pfm_op_ffn_op", "pfm_op_ffn_dec", "pfm_op_fsmn_bf16", "pfm_op_layernorm_bf16",
+               "pfm_op_attention", "pfm_op_layernorm", "pfm_op_fsmn", "pfm_op_cif", "pfm_profile", "pfm_op_ffn", "pfm_op_ffn_op", "pfm_op_ffn_dec", "pfm_op_fsmn_bf16", "pfm_op_layernorm_bf16",
                "pfm_profile_read", "pfm_streams_create", "pfm_streams_reset", "pfm_stream_step",
                "pfm_streams_destroy", "pfm_fbank_raw", "pfm_lfr_gather", "pfm_config_punc", "pfm_run_punc", "pfm_vad_config_default", "pfm_vad_create",
                "pfm_vad_set_weight", "pfm_vad_missing_weights", "pfm_vad_reset", "pfm_vad_run", "pfm_vad_destroy", "pfm_vad_fbank_raw",
@@ -115,8 +115,6 @@ def load_library(path: Optional[str] = None) -> ctypes.CDLL:
     lib.pfm_op_cif.argtypes = [vp, f32p, f32p, f32p, f32p, i32p, i32p, i32, i32, i32, i32]
     lib.pfm_op_layernorm_bf16.argtypes = [vp, vp, f32p, f32p, f32p, i32, i32, ctypes.c_float]
     lib.pfm_op_fsmn_bf16.argtypes = [vp, vp, i32p, f32p, vp, i32, i32, i32, i32, i32]
-    lib.pfm_op_gemm_layernorm.argtypes = [vp, vp, vp, f32p, f32p, f32p, f32p, f32p, ctypes.c_float, f32p, i32, i32,
-                                          i32]
     lib.pfm_op_ffn.argtypes = [vp, f32p, i32, f32p, f32p, ctypes.c_float, f32p, f32p, f32p, f32p, f32p, f32p, f32p,
                                vp]
     lib.pfm_op_ffn_op.argtypes = [vp, vp, vp, f32p, f32p, f32p, i32, f32p, f32p, ctypes.c_float, f32p, f32p, f32p,
@@ -455,20 +453,6 @@ def op_gemm(A, W, bias=None, res=None, relu=False, out_bf16=False):
     check(lib.pfm_op_gemm(_stream_ptr(torch, A.device), dt, _ptr(A.contiguous()), _ptr(W.contiguous()), _ptr(bias),
                           _ptr(res), _ptr(C), M, N, K, act), "pfm_op_gemm")
     return C
-
-
-def op_gemm_layernorm(A, W, gamma, beta, eps, bias=None, res=None, want_x=False):
-    """bf16 A [M,K] . W [512,K]^T (+bias +res) -> LayerNorm; returns Y (and x when want_x)."""
-    import torch
-    lib = load_library()
-    M, K = A.shape
-    N = W.shape[0]
-    Y = torch.empty((M, N), dtype=torch.float32, device=A.device)
-    C = torch.empty((M, N), dtype=torch.float32, device=A.device) if want_x else None
-    check(lib.pfm_op_gemm_layernorm(_stream_ptr(torch, A.device), _ptr(A.contiguous()), _ptr(W.contiguous()),
-                                    _ptr(bias), _ptr(res), _ptr(C), _ptr(gamma), _ptr(beta), ctypes.c_float(eps),
-                                    _ptr(Y), M, N, K), "pfm_op_gemm_layernorm")
-    return (Y, C) if want_x else Y
 
 
 def op_ffn(x, g2, b2n, eps, W1, b1, W2, b2, gn=None, bn=None):

@@ -298,14 +298,6 @@ int pfm_profile_read(pfm_handle* h, int kclass, double* ms, double* flops, doubl
 int pfm_op_gemm(void* stream, int dtype, const void* A, const void* W, const float* bias,
                 const float* res, float* C, int M, int N, int K, int act);
 
-/* Fused 512-wide projection + LayerNorm (bf16 operands, f32 accumulate/statistics):
- *   x = A W^T + bias (+ res) ; C = x (optional, f32) ; Y = LayerNorm(x) * gamma + beta (f32).
- * N must be 512 and K % 32 == 0. Replaces nn.Linear followed by LayerNorm
- * (e.g. sanm/encoder.py:120-137 -> norm2, positionwise_feed_forward.py:33 -> decoder norm2). */
-int pfm_op_gemm_layernorm(void* stream, const void* A, const void* W, const float* bias, const float* res,
-                          float* C, const float* gamma, const float* beta, float eps, float* Y, int M, int N,
-                          int K);
-
 /* Fused encoder feed-forward sub-layer (fast mode, bf16 MFMA, f32 accumulate / residual / statistics):
  *   x  = x + W2 relu(W1 LayerNorm2(x) + b1) + b2          -> xo [M, 512] f32 (may alias x)
  *   xn = LayerNorm_next(x) as bf16 [M, 512]               (optional: gn, bn, xn all non-null)

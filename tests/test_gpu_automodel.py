@@ -155,7 +155,7 @@ def _dp_worker(rank, world, port, paths, q):
     try:
         torch.cuda.set_device(0)   # both ranks share the one card of the box
         am = _automodel()
-        res = am.generate(input=paths, batch_size=2)
+        res = am.generate(input=paths, batch_size=1)
         from funasr_amd.distributed import item_lengths, length_sorted_shards
         mine = length_sorted_shards(item_lengths(paths), world)[rank]
         q.put((rank, res, mine))
@@ -166,7 +166,10 @@ def _dp_worker(rank, world, port, paths, q):
 def test_dp_world2_shared_device_matches_single_rank(tmp_path):
     import torch.multiprocessing as mp
     paths = _wav_files(tmp_path)
-    one = _automodel().generate(input=paths, batch_size=2)
+    # batch_size 1 on both sides: each utterance is decoded alone in either run, so the comparison is
+    # bitwise (a batch's padded length changes the GEMM tile policy, which may move an f32 rounding and
+    # flip a near-tie token of the random-weight model: that is batching, not sharding)
+    one = _automodel().generate(input=paths, batch_size=1)
     assert [r["key"] for r in one] == [f"utt{i}" for i in range(len(paths))]
     world, port = 2, _free_port()
     ctx = mp.get_context("spawn")
