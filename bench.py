@@ -341,7 +341,7 @@ def main():
     # HBM bytes per launch of the same kernel set from the committed PMC passes (rocprofv3 --pmc FETCH_SIZE /
     # WRITE_SIZE, separate runs of this bench, gfx950-corrected by tools/pmc_traffic.py); null when absent
     traffic, traffic_src = None, None
-    tname = next((n for n in ("r02b_gemm_traffic.json", "r02_gemm_traffic.json")
+    tname = next((n for n in ("r03_gemm_traffic.json", "r02b_gemm_traffic.json")
                   if os.path.exists(os.path.join(ROOT, "profiles", n))), None)
     if args.mode == "fast" and tname:
         with open(os.path.join(ROOT, "profiles", tname)) as f:
