@@ -53,6 +53,10 @@ class ParaformerConfig:
     blank_id: int = 0
     sos: int = 1
     eos: int = 2
+    # model_conf.ctc_weight: > 0 means the model carries the CTC head ctc.ctc_lo (paraformer/model.py:95-100,
+    # 147-150), which the joint CTC prefix beam search needs. The released Paraformer-large configs set 0.0;
+    # the reference constructor's own default is 0.5, so pass it explicitly when a checkpoint has the head.
+    ctc_weight: float = 0.0
 
     @property
     def d_k(self) -> int:
@@ -103,6 +107,10 @@ class ParaformerConfig:
         for k in ("blank_id", "sos", "eos"):
             if k in kw and kw[k] is not None:
                 setattr(c, k, int(kw[k]))
+        if kw.get("ctc_weight") is not None:
+            c.ctc_weight = float(kw["ctc_weight"])
+            if c.ctc_weight >= 1.0:
+                raise ValueError("ctc_weight 1.0 (a CTC-only model without decoder) is not on the HIP Paraformer path")
         return c
 
     def reference_kwargs(self) -> Dict[str, Any]:

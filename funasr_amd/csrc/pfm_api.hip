@@ -60,6 +60,13 @@ hipError_t pfm_ctc_collapse(const int* ids, long long ld, const int* olen, int B
                             int* ntok, hipStream_t st);
 hipError_t pfm_f32_to_bf16(const float* x, bf16* y, long long n, hipStream_t st);
 hipError_t pfm_swap_last2(const float* x, float* y, long long A, long long Bd, long long C, hipStream_t st);
+hipError_t pfm_logsoftmax_rows(float* x, long long rows, long long ld, int V, hipStream_t st);
+long long pfm_ctc_beam_fscratch(int K, int P, int T, int L);
+long long pfm_ctc_beam_iscratch(int K, int nbest, int L);
+hipError_t pfm_ctc_beam(const float* am, int L, const float* x, int T, const int* lens, const int* ntok, int B, int V,
+                        int K, int P, int nbest, float wctc, float pen, int use_pen, int end_detect, int sos, int eos,
+                        int blank, float* fs, int* is, int* tokens, int Lcap, int* olen, float* oscore,
+                        hipStream_t st);
 size_t pfm_ffn_packed_elems();
 hipError_t pfm_split3_rows(const float* x, RowMap xm, int M, int K, int Kp, bf16* out, hipStream_t st);
 hipError_t pfm_split3_planes(const float* x, bf16* p, long long plane, long long n, hipStream_t st);
@@ -238,6 +245,9 @@ struct pfm_handle {
     DevBuf qkv0_pad;               // fast mode: layer 0's bf16 QKV weights with K padded to a multiple of 64
     DevBuf ffn_pack;               // fused-FFN weight tiles of every encoder layer (bf16, LDS-image order)
     bool ffn_ready = false;
+    DevBuf logits, ctcx, beam_fs, beam_is;   // pfm_run_beam: decoder / CTC log-probs and the search's scratch
+    bool want_logits = false;      // set by pfm_run_beam around its pfm_run: the output layer writes logits
+    int last_L = 0;                // decoder positions of the last pfm_run (max token count)
     int ffn_kind = 0;              // which fused-FFN kernel the packed encoder weights (ffn_pack) are ordered for
     int dffn_kind = 0;             // ... and the packed decoder weights (dffn_pack)
     DevBuf dffn_pack, dffn_c;      // decoder FFNs (16 blocks + decoders3): W1 | W2 diag(gamma_F) tiles; c1 | c2
@@ -360,6 +370,10 @@ void build_registry(pfm_handle* h) {
     h->dan_b = add_entry(h, "decoder.after_norm.bias", {D});
     h->out_w = add_entry(h, "decoder.output_layer.weight", {V, D}, 0, true);
     h->out_b = add_entry(h, "decoder.output_layer.bias", {V});
+    if (c.ctc_head) {   // Paraformer trained with ctc_weight > 0 (paraformer/model.py:95-100, ctc/ctc.py:33)
+        h->ctc_w = add_entry(h, "ctc.ctc_lo.weight", {V, D}, 0, true);
+        h->ctc_b = add_entry(h, "ctc.ctc_lo.bias", {V});
+    }
     // cross-attention K/V projections of all decoder layers live in one [nL*2D, D] matrix so the
     // encoder memory is projected by ONE GEMM (N = nL*2D) instead of nL small ones.
     const size_t kv_rows = (size_t)c.dec_blocks * 2 * D;
@@ -1075,7 +1089,7 @@ void pfm_config_default(pfm_config* c) {
     c->kernel_size = 11; c->enc_sanm_shift = 0; c->dec_sanm_shift = 0; c->vocab_size = 8404;
     c->cif_l_order = 1; c->cif_r_order = 1; c->cif_threshold = 1.f; c->tail_threshold = 0.45f;
     c->smooth_factor = 1.f; c->noise_threshold = 0.f; c->ln_eps = 1e-12f;
-    c->arch = PFM_ARCH_PARAFORMER; c->tp_blocks = 0; c->n_embed = 0;
+    c->arch = PFM_ARCH_PARAFORMER; c->tp_blocks = 0; c->n_embed = 0; c->ctc_head = 0;
 }
 
 void pfm_config_sensevoice(pfm_config* c) {
@@ -1112,6 +1126,8 @@ int pfm_create(const pfm_config* cfg, int device, pfm_handle** out) {
         return fail(PFM_E_ARG, "pfm_create: CIF conv must be l_order = r_order = 1");
     if (cfg->arch == PFM_ARCH_SENSEVOICE && (cfg->tp_blocks < 0 || cfg->n_embed < 1))
         return fail(PFM_E_ARG, "pfm_create: SenseVoice needs tp_blocks >= 0 and n_embed >= 1");
+    if (cfg->ctc_head != 0 && (cfg->arch != PFM_ARCH_PARAFORMER || cfg->ctc_head != 1))
+        return fail(PFM_E_ARG, "pfm_create: ctc_head is 0 / 1 and only for Paraformer (SenseVoice always has one)");
     int ndev = 0;
     HIP_TRY(hipGetDeviceCount(&ndev));
     if (device < 0 || device >= ndev) return fail(PFM_E_ARG, "pfm_create: bad device index");
@@ -1340,10 +1356,12 @@ int pfm_run(pfm_handle* h, void* stream, int mode, const float* feats, const int
     for (int b = 0; b < B; ++b) L = std::max(L, (int)h->host_ntok[b]);
     L = std::min(L, Lc);   // ntok <= fires <= T+1 frames (+ rounding); decoder never exceeds the CIF rows
     if (L_cap > 0) HIP_TRY(pfm_fill_i32(tokens, (long long)B * L_cap, -1, st));
+    h->last_L = L;
     if (L < 1 || c.dec_blocks < 0) {   // model.py:514-515: nothing to decode
         if (kv_async) HIP_TRY(hipStreamWaitEvent(st, h->ev_kv, 0));   // the side stream still reads encp
         return PFM_OK;
     }
+    if (h->want_logits) HIP_TRY(h->logits.ensure((size_t)B * L * c.vocab_size * sizeof(float)));
 
     // ---------------- decoder (paraformer/decoder.py:359-411) ----------------
     const long long Ml = (long long)B * L;
@@ -1476,7 +1494,13 @@ int pfm_run(pfm_handle* h, void* stream, int mode, const float* feats, const int
         int rc3 = ffn(c.dec_blocks, h->d3n1g, h->d3n1b, h->d3w1, h->d3b1, h->d3ng, h->d3nb, h->d3w2, Xd, h->dan_g,
                       h->dan_b, Xdn, ndt);
         if (rc3) return rc3;
-        {   // output layer with fused row-argmax (logits never written)
+        if (h->want_logits) {   // beam search (pfm_run_beam): the f32 logits [B][L][V] themselves
+            GemmEpi e = epi_default();
+            e.bias = P(h->out_b);
+            e.out = h->logits.as<float>() + r0 * c.vocab_size; e.out_map = rowmap_plain(c.vocab_size);
+            e.out_dtype = DT_F32;
+            HIP_TRY(gemmA(Xdn, false, W(h->out_w), c.vocab_size, D, e));
+        } else {   // output layer with fused row-argmax (logits never written)
             const int ntl = amax_tiles(dt, rowmap_plain(D), D, c.vocab_size, D, h, W(h->out_w));
             GemmEpi e = epi_default();
             e.bias = P(h->out_b);
@@ -1488,7 +1512,7 @@ int pfm_run(pfm_handle* h, void* stream, int mode, const float* feats, const int
     };
     // the per-tile row maxima of every group -> token ids, one launch on the caller's stream after the join
     auto finish = [&]() -> int {
-        if (L_cap > 0) {
+        if (L_cap > 0 && !h->want_logits) {
             const int ntl = amax_tiles(dt, rowmap_plain(D), D, c.vocab_size, D, h, W(h->out_w));
             HIP_TRY(pfm_argmax_reduce(h->amv.as<float>(), h->ami.as<int>(), ntl, (c.vocab_size + 63) / 64, B, L, ntok,
                                       L_cap, tokens, nullptr, st));
@@ -1522,6 +1546,70 @@ int pfm_run(pfm_handle* h, void* stream, int mode, const float* feats, const int
         HIP_TRY(hipStreamWaitEvent(st, h->ev_join[k], 0));
     }
     return finish();
+}
+
+int pfm_run_beam(pfm_handle* h, void* stream, int mode, const float* feats, const int32_t* lens, int B, int T,
+                 int beam, float ctc_weight, float penalty, int nbest, int end_detect, int sos, int eos, int blank,
+                 int32_t* tokens, int L_cap, int32_t* ntok_out, float* scores_out) {
+    pfm_knobs_refresh();
+    if (!h || !feats || !lens || !tokens || !ntok_out || !scores_out) return fail(PFM_E_ARG, "pfm_run_beam: null argument");
+    if (h->cfg.arch != PFM_ARCH_PARAFORMER || !h->cfg.ctc_head)
+        return fail(PFM_E_STATE, "pfm_run_beam: needs a Paraformer handle with a CTC head (ctc_head = 1)");
+    const int V = h->cfg.vocab_size;
+    // BeamSearchPara(pre_beam_ratio 1.5, pre_beam_score_key "full"): pre-beam when int(1.5 beam) < V
+    const int pre = (int)(1.5 * beam), P = pre < V ? pre : V;
+    if (sos < 0 || sos >= V || eos < 0 || eos >= V || blank < 0 || blank >= V)
+        return fail(PFM_E_ARG, "pfm_run_beam: sos / eos / blank outside the vocabulary");
+    if (beam < 1 || beam > 16 || nbest < 1 || nbest > beam || P > 64 || !(ctc_weight > 1e-5f) || L_cap < 0)
+        return fail(PFM_E_ARG, "pfm_run_beam: need 1 <= nbest <= beam <= 16, ctc_weight > 1e-5, <= 64 candidates");
+    HIP_TRY(hipSetDevice(h->device));
+    hipStream_t st = (hipStream_t)stream;
+    int32_t* ntok_dev = nullptr;
+    {   // encoder -> CIF -> decoder with the output layer writing f32 logits (pfm_run, want_logits)
+        h->want_logits = true;
+        h->last_L = 0;
+        HIP_TRY(h->beam_is.ensure((size_t)B * sizeof(int32_t)));
+        ntok_dev = h->beam_is.as<int32_t>();
+        const int rc = pfm_run(h, stream, mode, feats, lens, B, T, ntok_dev, 0, ntok_dev, nullptr, nullptr, nullptr);
+        h->want_logits = false;
+        if (rc) return rc;
+    }
+    const int L = h->last_L;
+    const int D = h->cfg.d_model;
+    HIP_TRY(hipMemsetAsync(scores_out, 0, (size_t)B * nbest * sizeof(float), st));
+    if (L < 1) {   // model.py:514-515: nothing decoded -> no hypotheses
+        HIP_TRY(pfm_fill_i32(ntok_out, (long long)B * nbest, -1, st));
+        return PFM_OK;
+    }
+    const bool fast = mode == PFM_MODE_FAST;
+    const Run run(h, st, fast);
+    // CTC log-probs of the encoder output (ctc.log_softmax, ctc/ctc.py:173-185): [B*T, V] f32
+    const long long M = (long long)B * T;
+    HIP_TRY(h->ctcx.ensure((size_t)M * V * sizeof(float)));
+    {
+        GemmEpi e = epi_default();
+        e.bias = run.P(h->ctc_b);
+        e.out = h->ctcx.p; e.out_map = rowmap_plain(V); e.out_dtype = DT_F32;
+        const RowMap encmap = rowmap_seg(T, (long long)(T + 2) * D, D);
+        const void* A = fast ? (const void*)(h->encpb.as<bf16>() + D) : (const void*)(h->encp.as<float>() + D);
+        HIP_TRY(run.gemm(run.dt, A, encmap, run.W(h->ctc_w), D, (int)M, V, D, e));
+    }
+    HIP_TRY(pfm_logsoftmax_rows(h->ctcx.as<float>(), M, V, V, st));
+    HIP_TRY(pfm_logsoftmax_rows(h->logits.as<float>(), (long long)B * L, V, V, st));   // decoder log_softmax
+    // the search (ntok of the run: the device token counts behind pfm_run's ntok_out)
+    const long long fsz = pfm_ctc_beam_fscratch(beam, P, T, L), isz = pfm_ctc_beam_iscratch(beam, nbest, L);
+    // the device token counts (first B ints of beam_is) move behind the float scratch before beam_is is resized
+    HIP_TRY(hipStreamSynchronize(st));
+    HIP_TRY(h->beam_fs.ensure(((size_t)B * fsz + B) * sizeof(float)));
+    int* ntk = (int*)(h->beam_fs.as<float>() + (size_t)B * fsz);
+    HIP_TRY(hipMemcpyAsync(ntk, ntok_dev, (size_t)B * sizeof(int32_t), hipMemcpyDeviceToDevice, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    HIP_TRY(h->beam_is.ensure((size_t)B * isz * sizeof(int32_t)));
+    HIP_TRY(pfm_ctc_beam(h->logits.as<float>(), L, h->ctcx.as<float>(), T, lens, ntk, B, V, beam, P, nbest,
+                         ctc_weight, penalty, penalty != 0.f ? 1 : 0, end_detect, sos, eos, blank,
+                         h->beam_fs.as<float>(), h->beam_is.as<int>(), tokens, L_cap, ntok_out, scores_out, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    return PFM_OK;
 }
 
 int pfm_run_ctc(pfm_handle* h, void* stream, int mode, const float* feats, const int32_t* lens, int B, int T,

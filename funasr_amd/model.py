@@ -150,44 +150,62 @@ class Paraformer(HipModel):
     @torch.no_grad()
     def inference(self, data_in, data_lengths=None, key: List[str] = None, tokenizer=None, frontend=None,
                   **kwargs):
-        if kwargs.get("decoding_ctc_weight", 0.0) > 1e-5 or kwargs.get("lm_weight", 0.0) > 1e-5:
-            raise NotImplementedError("CTC / LM beam search is not on the HIP Paraformer path (greedy only)")
+        # paraformer/model.py:443-458: beam search when decoding_ctc_weight > 1e-5 and the model has a CTC head
+        # (otherwise the reference's is_use_ctc is False and it decodes greedily); LM fusion needs an LM scorer the
+        # reference does not build either (init_beam_search: "ngram is not supported now")
+        if kwargs.get("lm_weight", 0.0) > 1e-5 and kwargs.get("lm_file") is not None:
+            raise NotImplementedError("LM shallow fusion (lm_file) is not on the HIP Paraformer path")
+        use_ctc = kwargs.get("decoding_ctc_weight", 0.0) > 1e-5 and self.cfg.ctc_weight > 0.0
         eng = self.engine()
         mode = kwargs.get("mode", self.mode)
         meta = {}
         speech, lens = self._speech(eng, data_in, data_lengths, frontend, kwargs, meta)
         pred_ts = bool(kwargs.get("pred_timestamp", False))
-        r = eng.run(speech, lens, mode=mode, want_alphas=pred_ts)
-        toks = r["tokens"].cpu().numpy()           # one device->host copy for the whole batch
-        ntok = r["ntok"].cpu().numpy()
+        if use_ctc:   # joint decoder + CTC prefix beam search on the device (pfm_run_beam)
+            nbest = int(kwargs.get("nbest", 1))
+            rb = eng.run_beam(speech, lens, mode=mode, beam=int(kwargs.get("beam_size", 2)),
+                              ctc_weight=float(kwargs["decoding_ctc_weight"]), penalty=float(kwargs.get("penalty", 0.0)),
+                              nbest=nbest, end_detect=float(kwargs.get("maxlenratio", 0.0)) == 0.0)
+            btok, bn = rb["tokens"].cpu().numpy(), rb["ntok"].cpu().numpy()
+            hyps = [[btok[i, k, :bn[i, k]].tolist() for k in range(nbest) if bn[i, k] >= 0]
+                    for i in range(btok.shape[0])]
+            if pred_ts:   # the CIF outputs of the same encoder (paraformer/model.py:572-582)
+                r = eng.run(speech, lens, mode=mode, want_alphas=True)
+        else:
+            r = eng.run(speech, lens, mode=mode, want_alphas=pred_ts)
+            toks = r["tokens"].cpu().numpy()           # one device->host copy for the whole batch
+            ntok = r["ntok"].cpu().numpy()
+            hyps = []
+            for i in range(toks.shape[0]):
+                n = int(ntok[i])
+                ids = toks[i, :n].tolist() if n <= toks.shape[1] else []
+                hyps.append([[t for t in ids if t not in (self.eos, self.sos, self.blank_id)]])
         if pred_ts:   # CIF outputs for ts_prediction_lfr6_standard (paraformer/model.py:572-582)
             peaks_h, alphas_h = r["peaks"].cpu(), r["alphas"].cpu()
-        b = toks.shape[0]
+        b = len(hyps)
         key = self._keys(key, b)
         results = []
         for i in range(b):
-            n = int(ntok[i])
-            ids = toks[i, :n].tolist() if n <= toks.shape[1] else []
-            ids = [t for t in ids if t not in (self.eos, self.sos, self.blank_id)]
-            if tokenizer is not None:
-                # model.py:567-586: text = tokens2text(ids2tokens(ids)); sentence_postprocess replaces it
-                # only for tokenizers without a `bpemodel` (a SentencepiecesTokenizer keeps tokens2text)
-                toks_i = tokenizer.ids2tokens(ids)
-                text = tokenizer.tokens2text(toks_i)
-                bpe = hasattr(tokenizer, "bpemodel")
-                if pred_ts:
-                    if bpe:   # model.py:580-582 reads time_stamp_postprocessed, which only the non-bpe branch binds
-                        raise UnboundLocalError("pred_timestamp with a bpemodel tokenizer: the reference leaves "
-                                                "time_stamp_postprocessed unbound (paraformer/model.py:580-582)")
-                    # the reference passes the CIF peaks as `us_alphas` and the alphas as `us_peaks`
-                    _, ts = ts_prediction_lfr6_standard(peaks_h[i], alphas_h[i], list(toks_i),
-                                                        vad_offset=kwargs.get("begin_time", 0), upsample_rate=1)
-                    text, ts_pp, _ = sentence_postprocess(toks_i, ts)
-                    results.append({"key": key[i], "text": text, "timestamp": ts_pp})
+            for ids in hyps[i]:   # n-best hypotheses of utterance i, best first (model.py:553)
+                if tokenizer is not None:
+                    # model.py:567-586: text = tokens2text(ids2tokens(ids)); sentence_postprocess replaces it
+                    # only for tokenizers without a `bpemodel` (a SentencepiecesTokenizer keeps tokens2text)
+                    toks_i = tokenizer.ids2tokens(ids)
+                    text = tokenizer.tokens2text(toks_i)
+                    bpe = hasattr(tokenizer, "bpemodel")
+                    if pred_ts:
+                        if bpe:   # model.py:580-582 reads time_stamp_postprocessed, which only the non-bpe branch binds
+                            raise UnboundLocalError("pred_timestamp with a bpemodel tokenizer: the reference leaves "
+                                                    "time_stamp_postprocessed unbound (paraformer/model.py:580-582)")
+                        # the reference passes the CIF peaks as `us_alphas` and the alphas as `us_peaks`
+                        _, ts = ts_prediction_lfr6_standard(peaks_h[i], alphas_h[i], list(toks_i),
+                                                            vad_offset=kwargs.get("begin_time", 0), upsample_rate=1)
+                        text, ts_pp, _ = sentence_postprocess(toks_i, ts)
+                        results.append({"key": key[i], "text": text, "timestamp": ts_pp})
+                    else:
+                        if not bpe:
+                            text, _ = sentence_postprocess(toks_i)
+                        results.append({"key": key[i], "text": text})
                 else:
-                    if not bpe:
-                        text, _ = sentence_postprocess(toks_i)
-                    results.append({"key": key[i], "text": text})
-            else:
-                results.append({"key": key[i], "token_int": ids})
+                    results.append({"key": key[i], "token_int": ids})
         return results, meta

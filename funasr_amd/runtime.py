@@ -23,7 +23,7 @@ MODE_EXACT, MODE_FAST = 0, 1
 MODES = {"exact": MODE_EXACT, "fp32": MODE_EXACT, "fast": MODE_FAST, "bf16": MODE_FAST}
 
 # every symbol include/pfm.h declares (checked by tests/test_abi.py)
-ABI_SYMBOLS = ("pfm_config_default", "pfm_config_sensevoice", "pfm_create", "pfm_set_weight", "pfm_set_weight_device",
+ABI_SYMBOLS = ("pfm_config_default", "pfm_config_sensevoice", "pfm_create", "pfm_run_beam", "pfm_set_weight", "pfm_set_weight_device",
                "pfm_missing_weights", "pfm_reserve", "pfm_run", "pfm_run_ctc", "pfm_op_ctc_collapse", "pfm_fbank", "pfm_lfr_frames", "pfm_last_error", "pfm_destroy", "pfm_op_gemm",
                "pfm_op_attention", "pfm_op_layernorm", "pfm_op_fsmn", "pfm_op_cif", "pfm_profile", "pfm_op_ffn", "pfm_op_ffn_op", "pfm_op_ffn_dec", "pfm_op_fsmn_bf16", "pfm_op_layernorm_bf16",
                "pfm_profile_read", "pfm_streams_create", "pfm_streams_reset", "pfm_stream_step",
@@ -42,20 +42,20 @@ class PfmConfig(ctypes.Structure):
                                                "cif_l_order", "cif_r_order")] + \
               [(n, ctypes.c_float) for n in ("cif_threshold", "tail_threshold", "smooth_factor", "noise_threshold",
                                              "ln_eps")] + \
-              [(n, ctypes.c_int32) for n in ("arch", "tp_blocks", "n_embed")]
+              [(n, ctypes.c_int32) for n in ("arch", "tp_blocks", "n_embed", "ctc_head")]
 
     @classmethod
     def from_config(cls, c) -> "PfmConfig":
         if isinstance(c, CTTransformerConfig):
             return cls(c.input_size, c.d_model, c.heads, c.ffn, c.enc_blocks, 0, c.kernel_size, c.enc_sanm_shift, 0,
-                       c.n_punc, 1, 1, 1.0, 0.45, 1.0, 0.0, c.ln_eps, ARCH_PUNC, 0, c.vocab_size)
+                       c.n_punc, 1, 1, 1.0, 0.45, 1.0, 0.0, c.ln_eps, ARCH_PUNC, 0, c.vocab_size, 0)
         if isinstance(c, SenseVoiceConfig):
             return cls(c.input_size, c.d_model, c.heads, c.ffn, c.enc_blocks, 0, c.kernel_size, c.enc_sanm_shift, 0,
-                       c.vocab_size, 1, 1, 1.0, 0.45, 1.0, 0.0, c.ln_eps, ARCH_SENSEVOICE, c.tp_blocks, c.n_embed)
+                       c.vocab_size, 1, 1, 1.0, 0.45, 1.0, 0.0, c.ln_eps, ARCH_SENSEVOICE, c.tp_blocks, c.n_embed, 0)
         return cls(c.input_size, c.d_model, c.heads, c.ffn, c.enc_blocks, c.dec_blocks, c.kernel_size,
                    c.enc_sanm_shift, c.dec_sanm_shift, c.vocab_size, c.cif_l_order, c.cif_r_order,
                    c.cif_threshold, c.tail_threshold, c.smooth_factor, c.noise_threshold, c.ln_eps,
-                   ARCH_PARAFORMER, 0, 0)
+                   ARCH_PARAFORMER, 0, 0, 1 if getattr(c, "ctc_weight", 0.0) > 0.0 else 0)
 
 
 class PfmVadConfig(ctypes.Structure):
@@ -99,6 +99,8 @@ def load_library(path: Optional[str] = None) -> ctypes.CDLL:
     lib.pfm_missing_weights.argtypes = [vp]
     lib.pfm_reserve.argtypes = [vp, i32, i32]
     lib.pfm_run.argtypes = [vp, vp, i32, f32p, i32p, i32, i32, i32p, i32, i32p, f32p, f32p, f32p]
+    lib.pfm_run_beam.argtypes = [vp, vp, i32, f32p, i32p, i32, i32, i32, ctypes.c_float, ctypes.c_float, i32, i32,
+                                 i32, i32, i32, i32p, i32, i32p, f32p]
     lib.pfm_fbank.argtypes = [vp, vp, f32p, i32p, i32, i32, f32p, f32p, i32, i32p]
     lib.pfm_lfr_frames.argtypes = [i32]
     lib.pfm_last_error.argtypes = []
@@ -277,6 +279,29 @@ class PfmEngine:
         check(self.lib.pfm_run(self.h, _stream_ptr(torch, dev), m, _ptr(feats), _ptr(lens), B, T, _ptr(tokens),
                                L_cap, _ptr(ntok), _ptr(enc), _ptr(alphas), _ptr(peaks)), "pfm_run")
         return dict(tokens=tokens, ntok=ntok, enc=enc, alphas=alphas, peaks=peaks)
+
+    def run_beam(self, feats, lens, mode="exact", beam=2, ctc_weight=0.5, penalty=0.0, nbest=1, end_detect=True,
+                 L_cap: Optional[int] = None):
+        """Joint decoder + CTC prefix beam search (pfm_run_beam; Paraformer with a CTC head):
+        feats [B,T,in], lens [B] -> dict(tokens [B,nbest,L_cap] int32, ntok [B,nbest] (-1 = none), scores)."""
+        torch = self.torch
+        dev = torch.device("cuda", self.device)
+        feats = feats.to(device=dev, dtype=torch.float32).contiguous()
+        lens = lens.reshape(-1).to(device=dev, dtype=torch.int32).contiguous()
+        B, T, I = feats.shape
+        if I != self.cfg.input_size or lens.numel() != B:
+            raise PfmError("run_beam: feats [B, T, input_size] and lens [B] expected")
+        L_cap = T + 1 if L_cap is None else int(L_cap)
+        tokens = torch.empty((B, nbest, max(L_cap, 1)), dtype=torch.int32, device=dev)
+        ntok = torch.empty((B, nbest), dtype=torch.int32, device=dev)
+        scores = torch.empty((B, nbest), dtype=torch.float32, device=dev)
+        m = MODES[mode] if isinstance(mode, str) else int(mode)
+        c = self.cfg
+        check(self.lib.pfm_run_beam(self.h, _stream_ptr(torch, dev), m, _ptr(feats), _ptr(lens), B, T, int(beam),
+                                    float(ctc_weight), float(penalty), int(nbest), 1 if end_detect else 0,
+                                    int(c.sos), int(c.eos), int(c.blank_id), _ptr(tokens), L_cap, _ptr(ntok),
+                                    _ptr(scores)), "pfm_run_beam")
+        return dict(tokens=tokens, ntok=ntok, scores=scores)
 
     def run_punc(self, ids, lens, mode="exact", want_logits=False):
         """CT-Transformer: word ids [B,T] int32 cuda, lens [B] -> dict(punc [B,T] int32 (-1 beyond lens),

@@ -88,6 +88,8 @@ def param_layout(cfg) -> List[Tuple[str, Shape, int]]:
     out.append(("predictor.cif_conv1d.weight", (D, D, kp), D * kp))
     out.append(("predictor.cif_conv1d.bias", (D,), D * kp))
     lin("predictor.cif_output", 1, D)
+    if getattr(cfg, "ctc_weight", 0.0) > 0.0:   # ctc/ctc.py:33 (paraformer/model.py:95-100)
+        lin("ctc.ctc_lo", V, D)
     return out
 
 

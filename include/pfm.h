@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define PFM_ABI_VERSION 2
+#define PFM_ABI_VERSION 3
 
 enum pfm_status {
     PFM_OK = 0,
@@ -78,6 +78,8 @@ typedef struct pfm_config {
     int32_t arch;            /* pfm_arch */
     int32_t tp_blocks;       /* SenseVoice: 20 tp_encoders (sense_voice/model.py:529-540) */
     int32_t n_embed;         /* SenseVoice: 16 rows of the query Embedding (model.py:646-648) */
+    int32_t ctc_head;        /* Paraformer: 1 = the model carries ctc.ctc_lo (trained with ctc_weight > 0,
+                                paraformer/model.py:95-100, 147-150), needed by pfm_run_beam; else 0 */
 } pfm_config;
 
 typedef struct pfm_handle pfm_handle;
@@ -130,6 +132,24 @@ int pfm_reserve(pfm_handle* h, int B, int T);
 int pfm_run(pfm_handle* h, void* stream, int mode, const float* feats, const int32_t* lens,
             int B, int T, int32_t* tokens, int L_cap, int32_t* ntok, float* enc_out,
             float* alphas, float* peaks);
+
+/* Paraformer inference with the joint decoder + CTC prefix beam search — Paraformer.inference with
+ * decoding_ctc_weight > 0 (paraformer/model.py:396-441, 530-565): BeamSearchPara
+ * (paraformer/search.py:35-451) over the decoder log-probs with the CTCPrefixScorer
+ * (transformer/scorers/ctc.py:10-80, ctc_prefix_score.py:255-337) and the LengthBonus scorer, pre-beam
+ * int(1.5 beam) candidates, end detection (metrics/common.py:18-46) when end_detect != 0
+ * (maxlenratio == 0). Handle: Paraformer with ctc_head = 1. Runs the encoder / CIF / decoder of pfm_run,
+ * then the CTC head, both log_softmaxes and the search itself on the device (one workgroup per utterance).
+ *   beam 1..16, nbest 1..beam, ctc_weight > 1e-5 (weights["ctc"]), penalty (weights["length_bonus"]),
+ *   sos / eos / blank ids of the model (blank is also the CTC blank)
+ *   tokens    [B, nbest, L_cap] int32 out: token ids of the n-th best ended hypothesis, sos / eos / blank
+ *             removed (model.py:553-565)
+ *   ntok_out  [B, nbest] int32 out: number of those ids (may exceed L_cap: truncated), -1 = no hypothesis
+ *   scores_out[B, nbest] f32 out: the hypothesis score
+ * The call synchronises `stream`. */
+int pfm_run_beam(pfm_handle* h, void* stream, int mode, const float* feats, const int32_t* lens, int B, int T,
+                 int beam, float ctc_weight, float penalty, int nbest, int end_detect, int sos, int eos, int blank,
+                 int32_t* tokens, int L_cap, int32_t* ntok_out, float* scores_out);
 
 /* SenseVoiceSmall inference on an fbank batch — SenseVoiceSmall.inference for
  * data_type="fbank" (sense_voice/model.py:809-906) up to token_int: query rows, encoder,

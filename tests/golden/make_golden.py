@@ -179,6 +179,58 @@ def save_headline():
               "margins < 1e-3:", int((mg < 1e-3).sum()))
 
 
+BEAM_CASES = {   # name: (large?, weight seed, fbank seed, B, T, lens, decoding_ctc_weight, beam_size, penalty, nbest)
+    "beam_tiny": (False, 4, 21, 3, 40, [40, 27, 9], 0.3, 3, 0.0, 2),
+    "beam_tiny_pen": (False, 4, 22, 2, 40, [33, 40], 0.5, 4, 0.8, 3),
+    "beam_large": (True, 0, 23, 2, 500, [500, 431], 0.3, 4, 0.0, 2),
+}
+
+
+def save_beam():
+    """Paraformer with a CTC head (model_conf ctc_weight 0.3) decoded by the reference's joint decoder + CTC prefix
+    beam search (Paraformer.inference with decoding_ctc_weight > 0: BeamSearchPara + CTCPrefixScorer +
+    LengthBonus, paraformer/model.py:396-441, 530-565). Stores the n-best yseqs (sos ... eos) and scores from
+    beam_search() itself and the token_int result dicts of inference()."""
+    import dataclasses
+    models = {}
+    for name, (large, wseed, fseed, B, T, ln, wctc, beam, pen, nbest) in BEAM_CASES.items():
+        cfg = dataclasses.replace(paraformer_large() if large else paraformer_tiny(), ctc_weight=0.3)
+        kw = cfg.reference_kwargs()
+        cls = tables.model_classes["Paraformer"]
+        m = cls(encoder=kw["encoder"], encoder_conf=kw["encoder_conf"], decoder=kw["decoder"],
+                decoder_conf=kw["decoder_conf"], predictor=kw["predictor"], predictor_conf=kw["predictor_conf"],
+                input_size=cfg.input_size, vocab_size=cfg.vocab_size, ctc_weight=0.3, predictor_bias=1)
+        m.load_state_dict({k: torch.from_numpy(v) for k, v in make_weights(cfg, seed=wseed).items()}, strict=True)
+        m.eval()
+        feats, lens = fbank_input(seed=fseed, B=B, T=T, lens=ln)
+        x = torch.from_numpy(feats)
+        l64 = torch.from_numpy(lens.astype(np.int64))
+        toks = token_list(cfg.vocab_size)
+        opts = dict(decoding_ctc_weight=wctc, beam_size=beam, penalty=pen, nbest=nbest, token_list=toks)
+        with torch.no_grad():
+            res = m.inference(x, data_lengths=l64[:, None], key=[f"utt{i}" for i in range(B)], tokenizer=None,
+                              data_type="fbank", device="cpu", **opts)[0]
+            enc, olens = m.encode(x, l64)
+            embeds, token_num, alphas, peak = m.calc_predictor(enc, olens)
+            ntok = token_num.round().long()
+            logp, _ = m.cal_decoder_with_predictor(enc, olens, embeds, ntok)
+            yseq, scores, owner = [], [], []
+            for i in range(B):
+                nb = m.beam_search(x=enc[i, : olens[i]], am_scores=logp[i, : ntok[i]], maxlenratio=0.0,
+                                   minlenratio=0.0)[:nbest]
+                for h in nb:
+                    yseq.append(h.yseq.tolist())
+                    scores.append(float(h.score))
+                    owner.append(i)
+        flat, off = pack_tokens(yseq)
+        rflat, roff = pack_tokens([r["token_int"] for r in res])
+        np.savez_compressed(f"{HERE}/{name}.npz", large=large, wseed=wseed, seed=fseed, B=B, T=T, lens=lens,
+                            decoding_ctc_weight=wctc, beam_size=beam, penalty=pen, nbest=nbest, ntok=ntok.numpy(),
+                            enc_lens=olens.numpy(), yseq=flat, yseq_off=off, scores=np.array(scores, np.float32),
+                            owner=np.array(owner, np.int32), result_tokens=rflat, result_off=roff)
+        print(name, "ntok", ntok.tolist(), "hyps", len(yseq), "scores", [round(v, 3) for v in scores])
+
+
 def save_lfr_cmvn():
     from funasr.frontends.wav_frontend import apply_cmvn, apply_lfr, load_cmvn
     cmvn = load_cmvn(CMVN).numpy()

@@ -1,0 +1,141 @@
+"""Joint decoder + CTC prefix beam search on the device (pfm_run_beam, k_beam.hip) against the reference's own
+BeamSearchPara runs (tests/golden/beam_*.npz: Paraformer with a CTC head, ctc_weight 0.3, decoded with
+decoding_ctc_weight > 0; make_golden.py save_beam).
+
+EXACT mode: the n-best token sequences equal the reference's and their scores agree within 1e-5 relative
+(tiny config); at Paraformer-large scale, where the reference's two best hypotheses differ by 2 f32 ulps
+(-2223.5 vs -2223.50049), the GPU's best hypothesis must be one of the reference hypotheses within 1e-3 of the
+reference's best score and every score within 1e-3 of the reference's. AutoModel / Paraformer.inference with
+decoding_ctc_weight reproduces the reference inference() token_int dicts.
+"""
+import dataclasses
+import os
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from funasr_amd.config import paraformer_large, paraformer_tiny  # noqa: E402
+from funasr_amd.weights import make_weights  # noqa: E402
+from tests.golden.inputs import fbank_input  # noqa: E402
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def _cfg(g):
+    base = paraformer_large() if bool(g["large"]) else paraformer_tiny()
+    return dataclasses.replace(base, ctc_weight=0.3)
+
+
+def _golden(g):
+    off = g["yseq_off"]
+    hyps = [g["yseq"][off[k]:off[k + 1]].tolist() for k in range(len(off) - 1)]
+    return hyps, g["scores"], g["owner"]
+
+
+def _strip(y, cfg):
+    return [t for t in y[1:-1] if t not in (cfg.eos, cfg.sos, cfg.blank_id)]
+
+
+def _engine(g):
+    from funasr_amd.runtime import PfmEngine
+    cfg = _cfg(g)
+    e = PfmEngine(cfg, 0)
+    e.load_state_dict(make_weights(cfg, int(g["wseed"])))
+    return e, cfg
+
+
+def _run(e, g, mode="exact"):
+    feats, lens = fbank_input(int(g["seed"]), int(g["B"]), int(g["T"]), g["lens"])
+    r = e.run_beam(torch.from_numpy(feats).cuda(), torch.from_numpy(lens).cuda(), mode=mode,
+                   beam=int(g["beam_size"]), ctc_weight=float(g["decoding_ctc_weight"]), penalty=float(g["penalty"]),
+                   nbest=int(g["nbest"]))
+    torch.cuda.synchronize()
+    return r["tokens"].cpu().numpy(), r["ntok"].cpu().numpy(), r["scores"].cpu().numpy()
+
+
+@pytest.mark.parametrize("name", ["beam_tiny", "beam_tiny_pen"])
+def test_beam_exact_vs_reference(name):
+    g = np.load(f"{GOLD}/{name}.npz")
+    e, cfg = _engine(g)
+    toks, nt, sc = _run(e, g)
+    hyps, scores, owner = _golden(g)
+    nbest = int(g["nbest"])
+    k = 0
+    for i in range(int(g["B"])):
+        for n in range(nbest):
+            if k < len(owner) and owner[k] == i:
+                assert nt[i, n] >= 0
+                assert toks[i, n, : nt[i, n]].tolist() == _strip(hyps[k], cfg), (i, n)
+                assert abs(sc[i, n] - scores[k]) <= 1e-5 * abs(scores[k]), (i, n, sc[i, n], scores[k])
+                k += 1
+            else:
+                assert nt[i, n] == -1
+    assert k == len(owner)
+
+
+def test_beam_exact_large_vs_reference():
+    g = np.load(f"{GOLD}/beam_large.npz")
+    e, cfg = _engine(g)
+    toks, nt, sc = _run(e, g)
+    hyps, scores, owner = _golden(g)
+    for i in range(int(g["B"])):
+        ref = [(hyps[k], scores[k]) for k in range(len(owner)) if owner[k] == i]
+        best = max(s for _, s in ref)
+        near = [_strip(y, cfg) for y, s in ref if s >= best - 1e-3]
+        assert toks[i, 0, : nt[i, 0]].tolist() in near, i
+        for n in range(len(ref)):
+            got = toks[i, n, : nt[i, n]].tolist()
+            match = [s for y, s in ref if _strip(y, cfg) == got]
+            assert match and abs(sc[i, n] - match[0]) <= 1e-3, (i, n, sc[i, n], match)
+
+
+def test_beam_fast_mode_runs_and_is_close():
+    """fast (bf16) mode: same API; the best hypothesis shares >= 90 % of its positions with the exact one."""
+    g = np.load(f"{GOLD}/beam_tiny.npz")
+    e, _ = _engine(g)
+    te, ne, _ = _run(e, g, "exact")
+    tf, nf, sf = _run(e, g, "fast")
+    assert np.all(np.isfinite(sf[nf >= 0]))
+    for i in range(int(g["B"])):
+        a, b = te[i, 0, : ne[i, 0]], tf[i, 0, : nf[i, 0]]
+        n = min(len(a), len(b))
+        assert abs(len(a) - len(b)) <= 1 and (n == 0 or np.mean(a[:n] == b[:n]) >= 0.9)
+
+
+def test_automodel_beam_matches_reference_inference():
+    """Paraformer.inference(decoding_ctc_weight=..., beam_size, penalty, nbest) -> the reference inference()
+    result dicts (one {"key", "token_int"} per n-best hypothesis, utterance order)."""
+    from funasr_amd.model import Paraformer
+    for name in ("beam_tiny", "beam_tiny_pen"):
+        g = np.load(f"{GOLD}/{name}.npz")
+        cfg = _cfg(g)
+        kw = cfg.reference_kwargs()
+        m = Paraformer(**kw, ctc_weight=0.3, predictor_bias=1, mode="exact").cuda()
+        m.load_state_dict(make_weights(cfg, int(g["wseed"])))
+        feats, lens = fbank_input(int(g["seed"]), int(g["B"]), int(g["T"]), g["lens"])
+        res, _ = m.inference(torch.from_numpy(feats), data_lengths=torch.from_numpy(lens)[:, None],
+                             key=[f"utt{i}" for i in range(int(g["B"]))], data_type="fbank",
+                             decoding_ctc_weight=float(g["decoding_ctc_weight"]), beam_size=int(g["beam_size"]),
+                             penalty=float(g["penalty"]), nbest=int(g["nbest"]))
+        roff = g["result_off"]
+        want = [g["result_tokens"][roff[k]:roff[k + 1]].tolist() for k in range(len(roff) - 1)]
+        assert [r["token_int"] for r in res] == want, name
+        assert [r["key"] for r in res] == [f"utt{int(o)}" for o in g["owner"]]
+
+
+def test_beam_rejects_bad_arguments():
+    from funasr_amd.runtime import PfmEngine, PfmError
+    g = np.load(f"{GOLD}/beam_tiny.npz")
+    e, _ = _engine(g)
+    x, l = torch.zeros(1, 10, 560).cuda(), torch.tensor([10], dtype=torch.int32).cuda()
+    with pytest.raises(PfmError):
+        e.run_beam(x, l, beam=3, nbest=4)
+    with pytest.raises(PfmError):
+        e.run_beam(x, l, beam=3, ctc_weight=0.0)
+    plain = PfmEngine(paraformer_tiny(), 0)   # no CTC head
+    plain.load_state_dict(make_weights(paraformer_tiny(), 0))
+    with pytest.raises(PfmError):
+        plain.run_beam(x, l, beam=2)

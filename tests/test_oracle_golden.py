@@ -356,3 +356,40 @@ def test_vad_native_state_machine_vs_reference(name):
     for c in range(len(po) - 1):
         segs += det.push(db[do[c]:do[c + 1]], p0[po[c]:po[c + 1]], c == len(po) - 2, False)
     assert segs == gj["segments"]
+
+
+def _golden_hyps(g):
+    off = g["yseq_off"]
+    return [g["yseq"][off[k]:off[k + 1]].tolist() for k in range(len(off) - 1)]
+
+
+@pytest.mark.parametrize("name", ["beam_tiny", "beam_tiny_pen"])
+def test_beam_search_oracle_vs_reference(name):
+    """oracle/beam_ref.py (BeamSearchPara + CTCPrefixScore restated) on the oracle model's decoder log-probs and
+    CTC log-probs reproduces the reference beam_search() n-best: identical yseqs, scores within 1e-5 relative,
+    and the reference inference() token_int dicts (yseq minus sos / eos / blank)."""
+    import dataclasses
+    from oracle.beam_ref import beam_search, ctc_log_probs
+    g = np.load(f"{GOLD}/{name}.npz")
+    cfg = dataclasses.replace(paraformer_tiny(), ctc_weight=0.3)
+    w = make_weights(cfg, int(g["wseed"]))
+    feats, lens = fbank_input(int(g["seed"]), int(g["B"]), int(g["T"]), g["lens"])
+    r = paraformer_infer(feats, lens, w, cfg, keep_logits=True)
+    assert np.array_equal(r["ntok"].numpy(), g["ntok"])
+    logp = torch.log_softmax(r["logits"], dim=-1).numpy()
+    want, scores, owner = _golden_hyps(g), g["scores"], g["owner"]
+    nbest = int(g["nbest"])
+    got, got_scores = [], []
+    for i in range(int(g["B"])):
+        n = int(r["enc_lens"][i])
+        x = ctc_log_probs(r["enc"][i, :n], w).numpy()
+        hyps = beam_search(logp[i, : int(r["ntok"][i])], x, int(g["beam_size"]), float(g["decoding_ctc_weight"]),
+                           float(g["penalty"]), cfg.sos, cfg.eos)[:nbest]
+        got += [h.yseq for h in hyps]
+        got_scores += [float(h.score) for h in hyps]
+    assert got == want
+    np.testing.assert_allclose(got_scores, scores, rtol=1e-5)
+    roff = g["result_off"]
+    res = [g["result_tokens"][roff[k]:roff[k + 1]].tolist() for k in range(len(roff) - 1)]
+    assert res == [[t for t in y[1:-1] if t not in (cfg.eos, cfg.sos, cfg.blank_id)] for y in want]
+    del owner
