@@ -551,7 +551,7 @@ __device__ __forceinline__ void fsmn_epilogue(const AttnArgs& a, unsigned char* 
 // VAR (diagnostic instantiations for standalone timing — results are wrong; the library instantiates
 // VAR 0 only): 1 no K/V loads after tile 0, 2 no softmax (P = S), 3 no PV products, 4 no QK products,
 // 5 no key loop (prologue + epilogue only)
-template <int NWV, int VAR = 0>
+template <int NWV, int VAR = 0, int PD = 1>
 __global__ __launch_bounds__(NWV * 64, 8 / NWV) void attn_bf16_kernel(AttnArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr int NT = NWV * 64, QBLK = NWV * QW;
@@ -725,12 +725,26 @@ __global__ __launch_bounds__(NWV * 64, 8 / NWV) void attn_bf16_kernel(AttnArgs a
     // every iteration issues the same loads (the last one is unused).
     const Stg first = gload(0);
     if (ntiles > 0) sstore(0, first);
-    __syncthreads();
-    for (int t = 0; t < (VAR == 5 ? 0 : ntiles); ++t) {
-        const Stg nx = VAR == 1 ? first : gload(min(t + 1, ntiles - 1));
-        compute(t);
-        if (t + 1 < ntiles) sstore((t + 1) & 1, nx);
+    if constexpr (PD == 1) {
         __syncthreads();
+        for (int t = 0; t < (VAR == 5 ? 0 : ntiles); ++t) {
+            const Stg nx = VAR == 1 ? first : gload(min(t + 1, ntiles - 1));
+            compute(t);
+            if (t + 1 < ntiles) sstore((t + 1) & 1, nx);
+            __syncthreads();
+        }
+    } else {
+        // two tiles in flight: tile t+2 is fetched into registers while tile t+1's registers (fetched one
+        // iteration earlier, so they had a whole tile of compute to land) are written to the free LDS buffer
+        Stg nx = gload(min(1, max(ntiles - 1, 0)));
+        __syncthreads();
+        for (int t = 0; t < (VAR == 5 ? 0 : ntiles); ++t) {
+            const Stg nn = VAR == 1 ? first : gload(min(t + 2, ntiles - 1));
+            compute(t);
+            if (t + 1 < ntiles) sstore((t + 1) & 1, nx);
+            __syncthreads();
+            nx = nn;
+        }
     }
     if (qrow < a.Tq) {
         const float inv = (klen > 0) ? 1.f / lrun : 0.f;

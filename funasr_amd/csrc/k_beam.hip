@@ -32,6 +32,7 @@ constexpr int MAXP = 64;                     // pre-beam candidates (int(1.5 bea
 constexpr int MAXN = 16;                     // n-best
 
 __device__ __forceinline__ float lae(float a, float b) {
+#pragma clang fp contract(off)
     if (a == b) return a + 0.693147180559945309417232121458176568f;
     const float d = a - b;
     if (d > 0.f) return a + log1pf(expf(-d));
@@ -41,6 +42,7 @@ __device__ __forceinline__ float lae(float a, float b) {
 
 // row-wise log_softmax in place: x[r][0..V) -> x - max - log(sum exp(x - max)) (sum in f64)
 __global__ __launch_bounds__(256) void logsoftmax_rows_kernel(float* __restrict__ x, long long ld, int V) {
+#pragma clang fp contract(off)
     float* row = x + (long long)blockIdx.x * ld;
     __shared__ float smx[256];
     __shared__ double ssm[256];
@@ -86,6 +88,7 @@ struct BeamArgs {
 };
 
 __global__ __launch_bounds__(NT) void ctc_beam_kernel(BeamArgs a) {
+#pragma clang fp contract(off)   // every product rounded before its sum, as the reference's numpy / torch ops
     const int b = blockIdx.x, tid = threadIdx.x;
     const int V = a.V, K = a.K, P = a.P, Tb = min(a.lens[b], a.T), maxlen = min(a.ntok[b], a.L);
     const int S = a.L + 2;   // yseq capacity: sos + L tokens + eos
@@ -222,10 +225,10 @@ __global__ __launch_bounds__(NT) void ctc_beam_kernel(BeamArgs a) {
                 bool used[MAXP];
                 for (int j = 0; j < P; ++j) used[j] = false;
                 const int kk = min(K, P);
-                for (int r = 0; r < kk; ++r) {   // top-beam of this hypothesis, descending (equal: lower id)
+                for (int r = 0; r < kk; ++r) {   // top-beam of this hypothesis, descending
                     int bj = -1;
                     for (int j = 0; j < P; ++j)
-                        if (!used[j] && (bj < 0 || ws[j] > ws[bj] || (ws[j] == ws[bj] && cs[j] < cs[bj]))) bj = j;
+                        if (!used[j] && (bj < 0 || ws[j] > ws[bj])) bj = j;   // equal: lower pre-beam rank
                     used[bj] = true;
                     // stable insertion into the running candidate list (sorted descending)
                     int pos = nc;

@@ -68,6 +68,10 @@ hipError_t pfm_ctc_beam(const float* am, int L, const float* x, int T, const int
                         int blank, float* fs, int* is, int* tokens, int Lcap, int* olen, float* oscore,
                         hipStream_t st);
 size_t pfm_ffn_packed_elems();
+hipError_t pfm_emis_stats(const float* logits, long long rows, int V, float* mx, float* inv, int* amax, hipStream_t st);
+hipError_t pfm_ctc_align_run(const float* logits, const float* mx, const float* inv, const int* amax, int B, int Tf,
+                             int V, int blank, const int* olen, const int* tg, const int* tlen, int Lmax,
+                             unsigned char* bp, int* align, hipStream_t st);
 hipError_t pfm_split3_rows(const float* x, RowMap xm, int M, int K, int Kp, bf16* out, hipStream_t st);
 hipError_t pfm_split3_planes(const float* x, bf16* p, long long plane, long long n, hipStream_t st);
 hipError_t pfm_attention_x3(const float* q, RowMap qmap, const float* k, RowMap kmap, const float* v, RowMap vmap,
@@ -1974,6 +1978,66 @@ int pfm_op_cif(void* stream, const float* alphas, const float* hidden, float* em
                int32_t* ntok, int B, int T, int D, int L_cap) {
     HIP_TRY(pfm_cif_fire(alphas, hidden, rowmap_plain(D), B, T, D, L_cap, emb, peaks, n_fire, ntok,
                          (hipStream_t)stream));
+    return PFM_OK;
+}
+
+int pfm_ctc_align(pfm_handle* h, void* stream, const float* enc, int B, int Tq, const int32_t* olens,
+                  const int32_t* targets, int Lmax, const int32_t* tlens, int blank, int32_t* align) {
+    pfm_knobs_refresh();
+    if (!h || !enc || !olens || !align || (Lmax > 0 && (!targets || !tlens)) || B < 0 || Tq < 0 || Lmax < 0)
+        return fail(PFM_E_ARG, "pfm_ctc_align: null argument or bad sizes");
+    if (h->cfg.arch != PFM_ARCH_SENSEVOICE) return fail(PFM_E_STATE, "pfm_ctc_align: handle is not a SenseVoice model");
+    if (h->missing) return fail(PFM_E_STATE, "pfm_ctc_align: weights not set");
+    constexpr int NQ = 4;
+    const int V = h->cfg.vocab_size, D = h->cfg.d_model, Tf = Tq - NQ;
+    if (blank < 0 || blank >= V) return fail(PFM_E_ARG, "pfm_ctc_align: blank outside the vocabulary");
+    if (2 * (2 * (long long)Lmax + 3) * 4 > 64 * 1024) return fail(PFM_E_ARG, "pfm_ctc_align: Lmax too large");
+    if (B == 0 || Tf <= 0) return PFM_OK;
+    HIP_TRY(hipSetDevice(h->device));
+    const hipStream_t st = (hipStream_t)stream;
+    const long long M = (long long)B * Tf;
+    // CTC head logits of the speech frames (rows 4 .. Tq-1 of every utterance) in f32 (ctc.ctc_lo)
+    OpScratch sc;
+    float *logits, *mx, *inv;
+    int* amax;
+    unsigned char* bp;
+    HIP_TRY(sc.alloc(&logits, (size_t)M * V));
+    HIP_TRY(sc.alloc(&mx, (size_t)M));
+    HIP_TRY(sc.alloc(&inv, (size_t)M));
+    HIP_TRY(sc.alloc(&amax, (size_t)M));
+    HIP_TRY(sc.alloc(&bp, (size_t)M * (2 * Lmax + 1)));
+    GemmEpi e = epi_default();
+    e.bias = h->w(h->ctc_b);
+    e.out = logits; e.out_map = rowmap_plain(V); e.out_dtype = DT_F32;
+    HIP_TRY(gemm_dispatch(DT_F32, enc + (size_t)NQ * D, rowmap_seg(Tf, (long long)Tq * D, D), h->w(h->ctc_w), D,
+                          (int)M, V, D, e, st));
+    HIP_TRY(pfm_emis_stats(logits, M, V, mx, inv, amax, st));
+    HIP_TRY(pfm_ctc_align_run(logits, mx, inv, amax, B, Tf, V, blank, olens, targets, tlens, Lmax, bp, align, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    return PFM_OK;
+}
+
+int pfm_op_ctc_beam(void* stream, const float* am, int L, const float* x, int T, const int32_t* lens,
+                    const int32_t* ntok, int B, int V, int beam, float ctc_weight, float penalty, int nbest,
+                    int end_detect, int sos, int eos, int blank, int32_t* tokens, int L_cap, int32_t* ntok_out,
+                    float* scores_out) {
+    if (!am || !x || !lens || !ntok || !tokens || !ntok_out || !scores_out || B < 0 || L < 0 || T < 0 || V < 1)
+        return fail(PFM_E_ARG, "pfm_op_ctc_beam: null argument or bad sizes");
+    const int pre = (int)(1.5 * beam), P = pre < V ? pre : V;
+    if (sos < 0 || sos >= V || eos < 0 || eos >= V || blank < 0 || blank >= V)
+        return fail(PFM_E_ARG, "pfm_op_ctc_beam: sos / eos / blank outside the vocabulary");
+    if (beam < 1 || beam > 16 || nbest < 1 || nbest > beam || P > 64 || L_cap < 0)
+        return fail(PFM_E_ARG, "pfm_op_ctc_beam: need 1 <= nbest <= beam <= 16, <= 64 candidates");
+    if (B == 0) return PFM_OK;
+    const hipStream_t st = (hipStream_t)stream;
+    OpScratch sc;
+    float* fs;
+    int* is;
+    HIP_TRY(sc.alloc(&fs, (size_t)B * pfm_ctc_beam_fscratch(beam, P, T, L)));
+    HIP_TRY(sc.alloc(&is, (size_t)B * pfm_ctc_beam_iscratch(beam, nbest, L)));
+    HIP_TRY(pfm_ctc_beam(am, L, x, T, lens, ntok, B, V, beam, P, nbest, ctc_weight, penalty, penalty != 0.f ? 1 : 0,
+                         end_detect, sos, eos, blank, fs, is, tokens, L_cap, ntok_out, scores_out, st));
+    HIP_TRY(hipStreamSynchronize(st));
     return PFM_OK;
 }
 

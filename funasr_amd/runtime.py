@@ -24,8 +24,8 @@ MODES = {"exact": MODE_EXACT, "fp32": MODE_EXACT, "fast": MODE_FAST, "bf16": MOD
 
 # every symbol include/pfm.h declares (checked by tests/test_abi.py)
 ABI_SYMBOLS = ("pfm_config_default", "pfm_config_sensevoice", "pfm_create", "pfm_run_beam", "pfm_set_weight", "pfm_set_weight_device",
-               "pfm_missing_weights", "pfm_reserve", "pfm_run", "pfm_run_ctc", "pfm_op_ctc_collapse", "pfm_fbank", "pfm_lfr_frames", "pfm_last_error", "pfm_destroy", "pfm_op_gemm",
-               "pfm_op_attention", "pfm_op_layernorm", "pfm_op_fsmn", "pfm_op_cif", "pfm_profile", "pfm_op_ffn", "pfm_op_ffn_op", "pfm_op_ffn_dec", "pfm_op_fsmn_bf16", "pfm_op_layernorm_bf16",
+               "pfm_missing_weights", "pfm_reserve", "pfm_run", "pfm_run_ctc", "pfm_ctc_align", "pfm_op_ctc_collapse", "pfm_fbank", "pfm_lfr_frames", "pfm_last_error", "pfm_destroy", "pfm_op_gemm",
+               "pfm_op_attention", "pfm_op_layernorm", "pfm_op_fsmn", "pfm_op_cif", "pfm_op_ctc_beam", "pfm_profile", "pfm_op_ffn", "pfm_op_ffn_op", "pfm_op_ffn_dec", "pfm_op_fsmn_bf16", "pfm_op_layernorm_bf16",
                "pfm_profile_read", "pfm_streams_create", "pfm_streams_reset", "pfm_stream_step",
                "pfm_streams_destroy", "pfm_fbank_raw", "pfm_lfr_gather", "pfm_config_punc", "pfm_run_punc", "pfm_vad_config_default", "pfm_vad_create",
                "pfm_vad_set_weight", "pfm_vad_missing_weights", "pfm_vad_reset", "pfm_vad_run", "pfm_vad_destroy", "pfm_vad_fbank_raw",
@@ -93,6 +93,7 @@ def load_library(path: Optional[str] = None) -> ctypes.CDLL:
     lib.pfm_run_ctc.argtypes = [vp, vp, i32, f32p, i32p, i32, i32, ctypes.POINTER(ctypes.c_int32), i32, i32p, i32,
                                 i32p, f32p, i32p]
     lib.pfm_op_ctc_collapse.argtypes = [vp, i32p, ctypes.c_int64, i32p, i32, i32, i32p, i32, i32p]
+    lib.pfm_ctc_align.argtypes = [vp, vp, f32p, i32, i32, i32p, i32p, i32, i32p, i32, i32p]
     lib.pfm_create.argtypes = [ctypes.POINTER(PfmConfig), i32, ctypes.POINTER(vp)]
     lib.pfm_set_weight.argtypes = [vp, ctypes.c_char_p, vp, i32, ctypes.POINTER(ctypes.c_int64), i32]
     lib.pfm_set_weight_device.argtypes = [vp, ctypes.c_char_p, vp, i32, ctypes.POINTER(ctypes.c_int64), i32, vp]
@@ -115,6 +116,8 @@ def load_library(path: Optional[str] = None) -> ctypes.CDLL:
     lib.pfm_op_layernorm.argtypes = [vp, f32p, f32p, f32p, f32p, i32, i32, ctypes.c_float]
     lib.pfm_op_fsmn.argtypes = [vp, f32p, i32p, f32p, f32p, f32p, i32, i32, i32, i32, i32]
     lib.pfm_op_cif.argtypes = [vp, f32p, f32p, f32p, f32p, i32p, i32p, i32, i32, i32, i32]
+    lib.pfm_op_ctc_beam.argtypes = [vp, f32p, i32, f32p, i32, i32p, i32p, i32, i32, i32, ctypes.c_float,
+                                    ctypes.c_float, i32, i32, i32, i32, i32, i32p, i32, i32p, f32p]
     lib.pfm_op_layernorm_bf16.argtypes = [vp, vp, f32p, f32p, f32p, i32, i32, ctypes.c_float]
     lib.pfm_op_fsmn_bf16.argtypes = [vp, vp, i32p, f32p, vp, i32, i32, i32, i32, i32]
     lib.pfm_op_ffn.argtypes = [vp, f32p, i32, f32p, f32p, ctypes.c_float, f32p, f32p, f32p, f32p, f32p, f32p, f32p,
@@ -354,6 +357,27 @@ class PfmEngine:
                                    int(ban_token), _ptr(tokens), L_cap, _ptr(ntok), _ptr(enc), _ptr(frames)),
               "pfm_run_ctc")
         return dict(tokens=tokens, ntok=ntok, enc=enc, frame_ids=frames)
+
+    def ctc_align(self, enc, olens, targets, blank: int = 0):
+        """SenseVoice timestamps' forced alignment (pfm_ctc_align): enc [B, T+4, D] f32 cuda (run_ctc's enc),
+        olens [B] (lens + 4), targets: one list of token ids per utterance (token_int[4:]) -> align [B, T] int32
+        cuda (label id per speech frame, -1 beyond the utterance)."""
+        torch = self.torch
+        dev = torch.device("cuda", self.device)
+        enc = enc.to(device=dev, dtype=torch.float32).contiguous()
+        B, Tq, _ = enc.shape
+        olens = olens.reshape(-1).to(device=dev, dtype=torch.int32).contiguous()
+        Lmax = max([len(t) for t in targets] + [0])
+        tg = torch.zeros((B, max(Lmax, 1)), dtype=torch.int32)
+        for i, t in enumerate(targets):
+            if len(t):
+                tg[i, : len(t)] = torch.as_tensor(list(t), dtype=torch.int32)
+        tl = torch.as_tensor([len(t) for t in targets], dtype=torch.int32)
+        tg, tl = tg.to(dev), tl.to(dev)
+        align = torch.empty((B, max(Tq - 4, 1)), dtype=torch.int32, device=dev)
+        check(self.lib.pfm_ctc_align(self.h, _stream_ptr(torch, dev), _ptr(enc), B, Tq, _ptr(olens), _ptr(tg), Lmax,
+                                     _ptr(tl), int(blank), _ptr(align)), "pfm_ctc_align")
+        return align
 
     def fbank(self, wav, nsamp, cmvn=None):
         """wav [B,S] f32 cuda in [-1,1), nsamp [B] int32 -> (feats [B,T,560], T_out [B])."""
@@ -605,6 +629,28 @@ def op_ctc_collapse(ids, olen, blank=0, L_cap=None):
     check(lib.pfm_op_ctc_collapse(_stream_ptr(torch, ids.device), _ptr(ids), T, _ptr(olen.to(torch.int32).contiguous()),
                                   B, int(blank), _ptr(tokens), L_cap, _ptr(ntok)), "pfm_op_ctc_collapse")
     return tokens, ntok
+
+
+def op_ctc_beam(am, x, lens, ntok, beam, ctc_weight, penalty=0.0, nbest=1, sos=1, eos=2, blank=0, end_detect=True,
+                L_cap=None):
+    """Joint decoder + CTC prefix beam search alone (pfm_op_ctc_beam) on device log-probs am [B, L, V] and
+    x [B, T, V] -> (tokens [B, nbest, L_cap], ntok [B, nbest] (-1 = none), scores [B, nbest])."""
+    import torch
+    lib = load_library()
+    am = am.float().contiguous()
+    x = x.float().contiguous()
+    B, L, V = am.shape
+    T = x.shape[1]
+    L_cap = L + 1 if L_cap is None else int(L_cap)
+    tokens = torch.zeros((B, nbest, max(L_cap, 1)), dtype=torch.int32, device=am.device)
+    nt = torch.empty((B, nbest), dtype=torch.int32, device=am.device)
+    sc = torch.empty((B, nbest), dtype=torch.float32, device=am.device)
+    check(lib.pfm_op_ctc_beam(_stream_ptr(torch, am.device), _ptr(am), L, _ptr(x), T,
+                              _ptr(lens.to(torch.int32).contiguous()), _ptr(ntok.to(torch.int32).contiguous()), B, V,
+                              int(beam), float(ctc_weight), float(penalty), int(nbest), 1 if end_detect else 0,
+                              int(sos), int(eos), int(blank), _ptr(tokens), L_cap, _ptr(nt), _ptr(sc)),
+          "pfm_op_ctc_beam")
+    return tokens, nt, sc
 
 
 class PfmVad:

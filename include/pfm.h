@@ -169,6 +169,19 @@ int pfm_run_ctc(pfm_handle* h, void* stream, int mode, const float* feats, const
                 int B, int T, const int32_t* query, int ban_token, int32_t* tokens, int L_cap,
                 int32_t* ntok, float* enc_out, int32_t* frame_ids);
 
+/* SenseVoice timestamps — the CTC forced alignment of SenseVoiceSmall.inference(output_timestamp=True)
+ * (sense_voice/model.py:917-928, ctc_forced_align of sense_voice/utils/ctc_alignment.py:2-60): the CTC head's
+ * softmax over each utterance's speech frames (rows 4 .. olens[b]-1 of enc), blank probability zeroed where the
+ * blank is the frame's argmax, Viterbi over [blank, y1, blank, ..., yL, blank] summing those probabilities in
+ * f32, back-pointers from the better of the last label / final blank. Handle: PFM_ARCH_SENSEVOICE.
+ *   enc      [B, Tq, d_model] f32 device: pfm_run_ctc's enc_out (Tq = T + 4)
+ *   olens    [B] int32 device: encoder_out_lens (lens + 4)
+ *   targets  [B, Lmax] int32 device: token_int[4:] of each utterance; tlens [B] int32 device (0..Lmax)
+ *   align    [B, Tq - 4] int32 out: label id of each speech frame's state (-1 beyond olens[b] - 4)
+ * Lmax <= 8190. Synchronises `stream`. */
+int pfm_ctc_align(pfm_handle* h, void* stream, const float* enc, int B, int Tq, const int32_t* olens,
+                  const int32_t* targets, int Lmax, const int32_t* tlens, int blank, int32_t* align);
+
 /* ---- CT-Transformer punctuation (PFM_ARCH_PUNC; funasr/models/ct_transformer/model.py:81-93) ----
  * Config: input_size = embed_unit, d_model = att_unit, heads (head width 32 or 64), ffn, enc_blocks,
  * kernel_size, vocab_size = number of punctuation classes (<= 64), n_embed = word vocabulary rows,
@@ -381,6 +394,16 @@ int pfm_op_cif(void* stream, const float* alphas, const float* hidden, float* em
  * `blank` -> tokens [B, L_cap] (-1 padded), ntok [B]. Same kernel pfm_run_ctc uses. */
 int pfm_op_ctc_collapse(void* stream, const int32_t* ids, int64_t ld, const int32_t* olen, int B, int blank,
                         int32_t* tokens, int L_cap, int32_t* ntok);
+
+/* The joint decoder + CTC prefix beam search of pfm_run_beam alone (k_beam.hip; BeamSearchPara,
+ * paraformer/search.py:35-451, CTCPrefixScore, transformer/scorers/ctc_prefix_score.py:255-337) on given
+ * log-probabilities: am [B, L, V] decoder log-probs (utterance b uses its first ntok[b] rows), x [B, T, V] CTC
+ * log-probs (first lens[b] frames), device pointers. Arguments and outputs as pfm_run_beam (penalty != 0 adds
+ * the LengthBonus scorer). Synchronises `stream`. */
+int pfm_op_ctc_beam(void* stream, const float* am, int L, const float* x, int T, const int32_t* lens,
+                    const int32_t* ntok, int B, int V, int beam, float ctc_weight, float penalty, int nbest,
+                    int end_detect, int sos, int eos, int blank, int32_t* tokens, int L_cap, int32_t* ntok_out,
+                    float* scores_out);
 
 #ifdef __cplusplus
 }

@@ -507,6 +507,61 @@ def save_automodel_sv_tiny():
     print("automodel sv:", {k: [r["text"][:20] for r in v] for k, v in out.items()})
 
 
+def save_sv_timestamps():
+    """SenseVoice output_timestamp (model.py:917-945): (1) the reference ctc_forced_align on seeded emissions
+    (repeated labels, blank-zeroed softmax rows); (2) reference SenseVoiceSmall.inference(output_timestamp=True)
+    on the tiny config (vocab 300, sentencepiece tokenizer) one utterance per call, with the emission / targets /
+    alignment the reference's own ctc_forced_align call saw and the result dicts."""
+    import funasr.models.sense_voice.model as svm
+    import funasr.tokenizer.sentencepiece_tokenizer  # noqa: F401
+    from funasr.models.sense_voice.utils.ctc_alignment import ctc_forced_align
+    from funasr_amd.config import sense_voice_tiny
+    out = {}
+    rng = np.random.default_rng(7)
+    cases = [(30, 6, [3, 5, 5, 2, 4, 1]), (50, 9, [1, 2, 3, 4, 5, 6, 7, 8]), (12, 5, [4, 4, 4]), (8, 4, [2, 3, 1, 2])]
+    for k, (T, V, tg) in enumerate(cases):
+        e = torch.softmax(torch.from_numpy(rng.standard_normal((T, V)).astype(np.float32) * 2), -1)
+        e[e.argmax(-1) == 0, 0] = 0
+        a = ctc_forced_align(e[None].clone(), torch.tensor(tg)[None].long(), torch.tensor([T]).long(),
+                             torch.tensor([len(tg)]).long())
+        out[f"dp{k}_emis"], out[f"dp{k}_targets"], out[f"dp{k}_align"] = e.numpy(), np.array(tg), a[0].numpy()
+    bpe = f"{HERE}/sv_bpe.model"
+    if not os.path.exists(bpe):
+        make_sv_bpe(bpe)
+    tok = tables.tokenizer_classes["SentencepiecesTokenizer"](bpemodel=bpe)
+    cfg = sense_voice_tiny(vocab_size=300)
+    seen = []
+    orig = svm.ctc_forced_align
+
+    def spy(log_probs, targets, input_lengths, target_lengths, **kw):
+        targets = targets.clone()
+        e = log_probs[0].detach().clone().numpy()
+        r = orig(log_probs, targets, input_lengths, target_lengths, **kw)
+        seen.append((e, targets[0].numpy(), r[0].numpy()))
+        return r
+
+    svm.ctc_forced_align = spy
+    results = []
+    try:
+        for bias, seed, T in ((None, 31, 40), ({0: 2.5}, 32, 60), ({0: 1.0}, 33, 25)):
+            m = build_sv_ref(cfg, bias_boost=bias)
+            feats, lens = fbank_input(seed=seed, B=1, T=T, lens=[T])
+            res, _ = m.inference(torch.from_numpy(feats.copy()), data_lengths=torch.from_numpy(lens.astype(np.int64)),
+                                 key=[f"utt{seed}"], tokenizer=tok, data_type="fbank", device="cpu",
+                                 output_timestamp=True)
+            r = res[0]
+            results.append(dict(seed=seed, T=T, bias=bias and {str(k): v for k, v in bias.items()}, key=r["key"],
+                                text=r["text"], timestamp=[[int(a), int(b)] for a, b in r["timestamp"]]))
+    finally:
+        svm.ctc_forced_align = orig
+    for k, (e, tg, a) in enumerate(seen):
+        out[f"sv{k}_emis"], out[f"sv{k}_targets"], out[f"sv{k}_align"] = e, tg, a
+    np.savez_compressed(f"{HERE}/sv_timestamps.npz", **out)
+    with open(f"{HERE}/sv_timestamps.json", "w") as f:
+        json.dump(results, f, ensure_ascii=False, indent=1)
+    print("sv timestamps:", [(r["text"][:20], len(r["timestamp"])) for r in results])
+
+
 def save_automodel_tiny_bpe():
     """Reference AutoModel.generate() with Paraformer (tiny, vocab 300) + SentencepiecesTokenizer: pins the
     bpemodel branch of Paraformer.inference (text = tokens2text(ids2tokens(ids)), no sentence_postprocess,

@@ -76,6 +76,48 @@ def test_beam_exact_vs_reference(name):
     assert k == len(owner)
 
 
+def _oracle_logprobs(g, cfg):
+    """The oracle model's decoder log-probs [B, L, V] and CTC log-probs [B, T, V] (zero past each utterance's
+    frames) on the golden's inputs: the arrays the reference's beam search consumed (test_oracle_golden.py pins
+    the oracle search on them to the reference's n-best)."""
+    from oracle.beam_ref import ctc_log_probs
+    from oracle.paraformer_ref import paraformer_infer
+    w = make_weights(cfg, int(g["wseed"]))
+    feats, lens = fbank_input(int(g["seed"]), int(g["B"]), int(g["T"]), g["lens"])
+    r = paraformer_infer(feats, lens, w, cfg, keep_logits=True)
+    logp = torch.log_softmax(r["logits"], dim=-1)
+    B, T = int(g["B"]), int(g["T"])
+    x = torch.zeros(B, T, cfg.vocab_size)
+    for i in range(B):
+        n = int(r["enc_lens"][i])
+        x[i, :n] = ctc_log_probs(r["enc"][i, :n], w)
+    return logp, x, torch.as_tensor(r["enc_lens"]).int(), torch.as_tensor(r["ntok"]).int()
+
+
+@pytest.mark.parametrize("name", ["beam_tiny", "beam_tiny_pen"])
+def test_beam_kernel_on_reference_logprobs(name):
+    """The search kernel alone (pfm_op_ctc_beam) on the oracle model's log-probs: the reference's n-best token
+    sequences and scores (1e-5 relative) — separates the search from the model's arithmetic."""
+    from funasr_amd.runtime import op_ctc_beam
+    g = np.load(f"{GOLD}/{name}.npz")
+    cfg = _cfg(g)
+    logp, x, elens, ntok = _oracle_logprobs(g, cfg)
+    nbest = int(g["nbest"])
+    toks, nt, sc = op_ctc_beam(logp.cuda(), x.cuda(), elens.cuda(), ntok.cuda(), int(g["beam_size"]),
+                               float(g["decoding_ctc_weight"]), float(g["penalty"]), nbest, cfg.sos, cfg.eos,
+                               cfg.blank_id)
+    toks, nt, sc = toks.cpu().numpy(), nt.cpu().numpy(), sc.cpu().numpy()
+    hyps, scores, owner = _golden(g)
+    k = 0
+    for i in range(int(g["B"])):
+        for n in range(nbest):
+            if k < len(owner) and owner[k] == i:
+                assert toks[i, n, : nt[i, n]].tolist() == _strip(hyps[k], cfg), (i, n, sc[i, n], scores[k])
+                assert abs(sc[i, n] - scores[k]) <= 1e-5 * abs(scores[k]), (i, n, sc[i, n], scores[k])
+                k += 1
+    assert k == len(owner)
+
+
 def test_beam_exact_large_vs_reference():
     g = np.load(f"{GOLD}/beam_large.npz")
     e, cfg = _engine(g)

@@ -258,3 +258,72 @@ def test_oversized_lengths_are_clamped(sv):
     torch.cuda.synchronize()
     assert torch.equal(r1["ntok"], r0["ntok"]) and torch.equal(r1["tokens"], r0["tokens"])
     assert torch.equal(r1["frame_ids"], r0["frame_ids"])
+
+
+def _ts_model(bias):
+    from funasr_amd.sense_voice import SenseVoiceSmall
+    cfg = sense_voice_tiny(vocab_size=300)
+    kw = cfg.reference_kwargs()
+    m = SenseVoiceSmall(encoder=kw["encoder"], encoder_conf=kw["encoder_conf"], input_size=cfg.input_size,
+                        vocab_size=cfg.vocab_size, mode="exact").cuda()
+    m.load_state_dict(_weights(cfg, {int(k): v for k, v in (bias or {}).items()}))
+    return m
+
+
+def test_ctc_align_kernel_vs_reference():
+    """pfm_ctc_align (the forced alignment of output_timestamp) on the GPU encoder output reproduces the
+    alignments the reference's ctc_forced_align returned in inference(output_timestamp=True)
+    (tests/golden/sv_timestamps.npz, tiny config, vocab 300, one utterance per call)."""
+    import json
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    g = np.load(f"{GOLD}/sv_timestamps.npz")
+    want = json.load(open(f"{GOLD}/sv_timestamps.json", encoding="utf-8"))
+    for k, w in enumerate(want):
+        m = _ts_model(w["bias"])
+        eng = m.engine()
+        x, l = fbank_input(w["seed"], 1, w["T"], [w["T"]])
+        r = eng.run_ctc(torch.from_numpy(x).cuda(), torch.from_numpy(l).cuda(), _query(eng.cfg), mode="exact",
+                        want_enc=True)
+        ids = _tokens(r)[0]
+        assert ids[4:] == g[f"sv{k}_targets"].tolist(), k
+        align = eng.ctc_align(r["enc"], torch.from_numpy(l).cuda() + 4, [ids[4:]]).cpu().numpy()
+        assert np.array_equal(align[0, : w["T"]], g[f"sv{k}_align"]), (k, align[0, : w["T"]], g[f"sv{k}_align"])
+
+
+def test_sensevoice_output_timestamp_matches_reference():
+    """SenseVoiceSmall.inference(output_timestamp=True) returns the reference's result dicts: text and the
+    word-level [start ms, end ms] list (model.py:917-965), including a blank-heavy utterance with one word."""
+    import json
+    from funasr_amd.text import SentencepiecesTokenizer
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    tok = SentencepiecesTokenizer(bpemodel=os.path.join(GOLD, "sv_bpe.model"))
+    want = json.load(open(f"{GOLD}/sv_timestamps.json", encoding="utf-8"))
+    for w in want:
+        m = _ts_model(w["bias"])
+        x, l = fbank_input(w["seed"], 1, w["T"], [w["T"]])
+        res, _ = m.inference(torch.from_numpy(x), data_lengths=torch.from_numpy(l), key=[w["key"]], tokenizer=tok,
+                             data_type="fbank", output_timestamp=True)
+        assert res == [{"key": w["key"], "text": w["text"], "timestamp": w["timestamp"]}], w["seed"]
+
+
+def test_ctc_align_ragged_batch_equals_single_calls():
+    """A ragged batch aligns each utterance on its own frames: the same alignments as one call per utterance."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    m = _ts_model(None)
+    eng = m.engine()
+    x, l = fbank_input(51, 3, 50, [50, 33, 18])
+    r = eng.run_ctc(torch.from_numpy(x).cuda(), torch.from_numpy(l).cuda(), _query(eng.cfg), mode="exact",
+                    want_enc=True)
+    ids = _tokens(r)
+    a = eng.ctc_align(r["enc"], torch.from_numpy(l).cuda() + 4, [t[4:] for t in ids]).cpu().numpy()
+    for i in range(3):
+        n = int(l[i])
+        ri = eng.run_ctc(torch.from_numpy(x[i:i + 1, :n].copy()).cuda(), torch.from_numpy(l[i:i + 1]).cuda(),
+                         _query(eng.cfg), mode="exact", want_enc=True)
+        assert _tokens(ri)[0] == ids[i]
+        ai = eng.ctc_align(ri["enc"], torch.from_numpy(l[i:i + 1]).cuda() + 4, [ids[i][4:]]).cpu().numpy()
+        assert np.array_equal(a[i, :n], ai[0, :n]), i
+        assert np.all(a[i, n:] == -1)

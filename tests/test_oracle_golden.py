@@ -393,3 +393,55 @@ def test_beam_search_oracle_vs_reference(name):
     res = [g["result_tokens"][roff[k]:roff[k + 1]].tolist() for k in range(len(roff) - 1)]
     assert res == [[t for t in y[1:-1] if t not in (cfg.eos, cfg.sos, cfg.blank_id)] for y in want]
     del owner
+
+
+def test_ctc_forced_align_oracle_vs_reference():
+    """oracle.sensevoice_ref.ctc_forced_align on the emissions the reference's ctc_forced_align saw
+    (tests/golden/sv_timestamps.npz: seeded cases with repeated labels, and the three SenseVoice
+    inference(output_timestamp=True) calls) reproduces its alignments exactly."""
+    from oracle.sensevoice_ref import ctc_forced_align
+    g = np.load(f"{GOLD}/sv_timestamps.npz")
+    n = 0
+    for pre in ("dp0", "dp1", "dp2", "dp3", "sv0", "sv1", "sv2"):
+        got = ctc_forced_align(g[f"{pre}_emis"], g[f"{pre}_targets"].tolist())
+        assert np.array_equal(got, g[f"{pre}_align"]), pre
+        n += 1
+    assert n == 7
+
+
+def test_sensevoice_timestamps_oracle_vs_reference():
+    """The oracle's timestamp path (softmax emission with blank zeroed, forced alignment, frame groups,
+    post()) on the oracle model's CTC logits reproduces the reference inference(output_timestamp=True)
+    result dicts (tiny config, vocab 300, sentencepiece tokenizer, one utterance per call)."""
+    import json
+    import sentencepiece as spm
+    from funasr_amd.config import sense_voice_tiny
+    from oracle.sensevoice_ref import (ctc_forced_align, sensevoice_infer, timestamp_emission, timestamp_groups,
+                                       timestamp_post)
+    cfg = sense_voice_tiny(vocab_size=300)
+    sp = spm.SentencePieceProcessor(model_file=f"{GOLD}/sv_bpe.model")
+    g = np.load(f"{GOLD}/sv_timestamps.npz")
+    with open(f"{GOLD}/sv_timestamps.json") as f:
+        want = json.load(f)
+    for k, w in enumerate(want):
+        wt = make_weights(cfg, 0)
+        if w["bias"]:
+            b = wt["ctc.ctc_lo.bias"].copy()
+            for t, add in w["bias"].items():
+                b[int(t)] += add
+            wt["ctc.ctc_lo.bias"] = b
+        feats, lens = fbank_input(seed=w["seed"], B=1, T=w["T"], lens=[w["T"]])
+        r = sensevoice_infer(feats, lens, wt, cfg, keep_logits=True)
+        ids = r["tokens"][0]
+        assert sp.decode(ids) == w["text"]
+        n = int(r["enc_lens"][0])
+        logits = torch.nn.functional.linear(r["enc"][0, 4:n], torch.as_tensor(wt["ctc.ctc_lo.weight"]),
+                                            torch.as_tensor(wt["ctc.ctc_lo.bias"])).numpy()
+        emis = timestamp_emission(logits, cfg.blank_id)
+        np.testing.assert_allclose(emis, g[f"sv{k}_emis"], rtol=1e-5, atol=1e-7)
+        assert ids[4:] == g[f"sv{k}_targets"].tolist()
+        align = ctc_forced_align(emis, ids[4:], cfg.blank_id)
+        assert np.array_equal(align, g[f"sv{k}_align"]), k
+        pieces = sp.encode(w["text"], out_type=str)[4:]
+        ts = timestamp_post(timestamp_groups(align, n, n - 4, pieces))
+        assert ts == w["timestamp"], k
