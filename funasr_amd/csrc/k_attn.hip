@@ -469,56 +469,26 @@ constexpr int KROW = DK * 2;                    // 256 B
 constexpr int VROW = DK * 2 + 64;               // 320 B
 constexpr int KTILE = KT2 * KROW, VTILE = KT2 * VROW;
 constexpr int STG2 = KTILE + VTILE;             // 36 KiB per stage
-constexpr int FSMN_LDS = (256 + 10) * DK * 2 + 11 * DK * 4;   // fused FSMN epilogue staging (8-wave kernel)
-constexpr int LDS8 = (2 * STG2 > FSMN_LDS) ? 2 * STG2 : FSMN_LDS;
+constexpr int FSMN_LDS = (256 + 10) * DK * 2 + 11 * DK * 4;   // fused FSMN window + taps (8-wave kernel)
+constexpr int LDS8_FS = 2 * STG2 + FSMN_LDS;            // K/V stages + the FSMN window captured beside them
 constexpr float RESCALE_THR = 8.0f;             // lazy O rescale: only when a row max grows by > 8
 
 typedef short v4i16 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
 
 // Fused FSMN memory block for the block's QB query rows x this head's DK channels (encoder
-// self-attention: query row == key row). V rows [t0-5, t0+QB+5) of head h go to LDS (rows outside
-// [0, klen) as zeros), the 11 taps of the head's channels after them; thread = 8 rows x 8 channels.
-// Same f32 operation order as fsmn_win_kernel<11, bf16, 5> (taps ascending, then + x[t]).
+// self-attention: query row == key row). `win` holds V rows [t0-5, t0+QB+5) of head h (rows outside [0, klen)
+// as zeros; captured by the key loop) followed by the 11 taps of the head's channels; thread = 8 rows x 8
+// channels. Same f32 operation order as fsmn_win_kernel<11, bf16, 5> (taps ascending, then + x[t]).
 template <int QB, int NTH>
-__device__ __forceinline__ void fsmn_epilogue(const AttnArgs& a, unsigned char* smem, int qt, int h, int b, int klen) {
+__device__ __forceinline__ void fsmn_epilogue(const AttnArgs& a, const unsigned char* win, int qt, int h, int b,
+                                              int klen) {
     constexpr int FK = 11, FL = 5, FR = QB + FK - 1, RB = DK * 2;   // 256-B rows
     static_assert(NTH == (QB / 8) * (DK / 8), "one thread per 8 rows x 8 channels");
-    __syncthreads();                                   // every wave is past its last K/V read
+    __syncthreads();                                   // every window row and tap is in LDS
     const int t0 = qt * QB;
-    const bf16* V = (const bf16*)a.v;
-    unsigned char* xs = smem;
-    float* ws = (float*)(smem + FR * RB);
-    // every V-window and tap load of the thread is issued before its first LDS store (one memory latency
-    // for the whole staging instead of one per loop trip)
-    constexpr int NV = FR * (DK / 8), ITV = (NV + NTH - 1) / NTH;
-    constexpr int NW4 = FK * (DK / 4), ITW = (NW4 + NTH - 1) / NTH;
-    uint4 vv[ITV];
-    float4 wv[ITW];
-#pragma unroll
-    for (int j = 0; j < ITV; ++j) {
-        const int i = threadIdx.x + j * NTH;
-        const int r = i / (DK / 8), ch = i % (DK / 8), t = t0 - FL + r;
-        vv[j] = make_uint4(0, 0, 0, 0);
-        if (i < NV && t >= 0 && t < klen) vv[j] = *(const uint4*)(V + a.vmap.off((long long)b * a.Tk + t) + h * DK + ch * 8);
-    }
-#pragma unroll
-    for (int j = 0; j < ITW; ++j) {
-        const int i = threadIdx.x + j * NTH;
-        const int k = i / (DK / 4), c4 = i % (DK / 4);
-        if (i < NW4) wv[j] = *(const float4*)(a.fw + (long long)k * a.fD + h * DK + c4 * 4);
-    }
-#pragma unroll
-    for (int j = 0; j < ITV; ++j) {
-        const int i = threadIdx.x + j * NTH;
-        if (i < NV) *(uint4*)(xs + (i / (DK / 8)) * RB + (i % (DK / 8)) * 16) = vv[j];
-    }
-#pragma unroll
-    for (int j = 0; j < ITW; ++j) {
-        const int i = threadIdx.x + j * NTH;
-        if (i < NW4) *(float4*)(ws + (i / (DK / 4)) * DK + (i % (DK / 4)) * 4) = wv[j];
-    }
-    __syncthreads();
+    const unsigned char* xs = win;
+    const float* ws = (const float*)(win + FR * RB);
     const int rb = threadIdx.x / (DK / 8), c8 = (threadIdx.x % (DK / 8)) * 8;
     float y[8][8];
 #pragma unroll
@@ -551,7 +521,14 @@ __device__ __forceinline__ void fsmn_epilogue(const AttnArgs& a, unsigned char* 
 // VAR (diagnostic instantiations for standalone timing — results are wrong; the library instantiates
 // VAR 0 only): 1 no K/V loads after tile 0, 2 no softmax (P = S), 3 no PV products, 4 no QK products,
 // 5 no key loop (prologue + epilogue only)
-template <int NWV, int VAR = 0, int PD = 1>
+// Fused FSMN epilogue (8 waves): the block's V window [t0 - 5, t0 + 261) is captured into its own LDS region from
+// the staging registers as the key tiles stream through (rows < klen; the others zeroed up front), so the epilogue
+// starts from LDS (re-loading the window from global memory after the key loop: 37.8 -> 35.5 us per encoder group
+// launch, tools/attn_bench.hip). bf16-only outputs are stored 16 B per lane: permlane32 swaps pair the two
+// half-waves' 8-B pieces of a row (35.5 -> 33.5 us). Both bit-identical to the earlier forms. Measured and not
+// kept: two K/V tiles in flight (register staging two tiles ahead: +1.5 %), static priority 1 for the younger half
+// of the waves (within noise).
+template <int NWV, int VAR = 0>
 __global__ __launch_bounds__(NWV * 64, 8 / NWV) void attn_bf16_kernel(AttnArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr int NT = NWV * 64, QBLK = NWV * QW;
@@ -624,13 +601,32 @@ __global__ __launch_bounds__(NWV * 64, 8 / NWV) void attn_bf16_kernel(AttnArgs a
         *(uint4*)(base + row * KROW + ((ch ^ (row & 15)) << 4)) = kk;
         *(uint4*)(base + KTILE + row * VROW + ch * 16) = vv;
     };
-    auto sstore = [&](int s, const Stg& r) {
+    // the block's FSMN window (V rows [fw0, fw0 + QBLK + 10) of this head) lives at smem + 2 STG2
+    constexpr bool CAP = NWV == 8;
+    const bool cap = CAP && a.fout != nullptr;
+    const int fw0 = qt * QBLK - 5;
+    unsigned char* fxs = smem + 2 * STG2;
+    auto fcap = [&](int t, int c, const uint4& vv) {
+        const int row = t * KT2 + (c >> 4), r = row - fw0;
+        if (r >= 0 && r < QBLK + 10 && row < klen) *(uint4*)(fxs + r * (DK * 2) + (c & 15) * 16) = vv;
+    };
+    auto sstore = [&](int s, const Stg& r, int t) {
         unsigned char* base = smem + s * STG2;
         st1(base, tid, r.k0, r.v0);
         st1(base, tid + NT, r.k1, r.v1);
         if constexpr (CPT == 4) {
             st1(base, tid + 2 * NT, r.k2, r.v2);
             st1(base, tid + 3 * NT, r.k3, r.v3);
+        }
+        if constexpr (CAP) {
+            if (cap) {
+                fcap(t, tid, r.v0);
+                fcap(t, tid + NT, r.v1);
+                if constexpr (CPT == 4) {
+                    fcap(t, tid + 2 * NT, r.v2);
+                    fcap(t, tid + 3 * NT, r.v3);
+                }
+            }
         }
     };
     // per-lane constants of the transposed V read: lane 4q+p of its 16-lane group addresses key
@@ -724,29 +720,51 @@ __global__ __launch_bounds__(NWV * 64, 8 / NWV) void attn_bf16_kernel(AttnArgs a
     // previous barrier), so the fetch has one tile of compute to land. The fetch index is clamped so
     // every iteration issues the same loads (the last one is unused).
     const Stg first = gload(0);
-    if (ntiles > 0) sstore(0, first);
-    if constexpr (PD == 1) {
-        __syncthreads();
-        for (int t = 0; t < (VAR == 5 ? 0 : ntiles); ++t) {
-            const Stg nx = VAR == 1 ? first : gload(min(t + 1, ntiles - 1));
-            compute(t);
-            if (t + 1 < ntiles) sstore((t + 1) & 1, nx);
-            __syncthreads();
-        }
-    } else {
-        // two tiles in flight: tile t+2 is fetched into registers while tile t+1's registers (fetched one
-        // iteration earlier, so they had a whole tile of compute to land) are written to the free LDS buffer
-        Stg nx = gload(min(1, max(ntiles - 1, 0)));
-        __syncthreads();
-        for (int t = 0; t < (VAR == 5 ? 0 : ntiles); ++t) {
-            const Stg nn = VAR == 1 ? first : gload(min(t + 2, ntiles - 1));
-            compute(t);
-            if (t + 1 < ntiles) sstore((t + 1) & 1, nx);
-            __syncthreads();
-            nx = nn;
+    if constexpr (CAP) {
+        if (cap) {   // rows of the window outside [0, klen) are zeros; the taps of this head after the window
+            float4 tw = make_float4(0.f, 0.f, 0.f, 0.f);
+            constexpr int NW4 = 11 * (DK / 4);
+            if (tid < NW4) tw = *(const float4*)(a.fw + (long long)(tid / (DK / 4)) * a.fD + h * DK + (tid % (DK / 4)) * 4);
+            for (int i = tid; i < (QBLK + 10) * 16; i += NT) {
+                const int row = fw0 + (i >> 4);
+                if (row < 0 || row >= klen) *(uint4*)(fxs + (i >> 4) * (DK * 2) + (i & 15) * 16) = make_uint4(0, 0, 0, 0);
+            }
+            if (tid < NW4) *(float4*)(fxs + (QBLK + 10) * (DK * 2) + tid * 16) = tw;
         }
     }
-    if (qrow < a.Tq) {
+    if (ntiles > 0) sstore(0, first, 0);
+    __syncthreads();
+    for (int t = 0; t < (VAR == 5 ? 0 : ntiles); ++t) {
+        const Stg nx = VAR == 1 ? first : gload(min(t + 1, ntiles - 1));
+        compute(t);
+        if (t + 1 < ntiles) sstore((t + 1) & 1, nx, t + 1);
+        __syncthreads();
+    }
+    {
+        if (!a.o && a.o2) {   // bf16 rows only: 8 x 16-B stores per lane (the two half-waves hold 8-B pieces of a row)
+            const float inv = (klen > 0) ? 1.f / lrun : 0.f;
+            bf16* op2 = (bf16*)a.o2 + ((long long)b * a.Tq + (qrow < a.Tq ? qrow : 0)) * a.ldo + h * DK;
+#pragma unroll
+            for (int d = 0; d < 4; ++d)
+#pragma unroll
+                for (int g = 0; g < 4; g += 2) {
+                    uint2 pa, pb;
+                    {
+                        bf16x4 t4 = {f2bf(o[d][4 * g] * inv), f2bf(o[d][4 * g + 1] * inv), f2bf(o[d][4 * g + 2] * inv),
+                                     f2bf(o[d][4 * g + 3] * inv)};
+                        __builtin_memcpy(&pa, &t4, 8);
+                        bf16x4 u4 = {f2bf(o[d][4 * g + 4] * inv), f2bf(o[d][4 * g + 5] * inv),
+                                     f2bf(o[d][4 * g + 6] * inv), f2bf(o[d][4 * g + 7] * inv)};
+                        __builtin_memcpy(&pb, &u4, 8);
+                    }
+                    auto rx = __builtin_amdgcn_permlane32_swap(pa.x, pb.x, false, false);
+                    auto ry = __builtin_amdgcn_permlane32_swap(pa.y, pb.y, false, false);
+                    if (qrow < a.Tq)
+                        *(uint4*)(op2 + d * 32 + 8 * g + 8 * fh) = make_uint4(rx[0], ry[0], rx[1], ry[1]);
+                }
+        }
+    }
+    if (qrow < a.Tq && (a.o || !a.o2)) {
         const float inv = (klen > 0) ? 1.f / lrun : 0.f;
         float* op = a.o ? a.o + ((long long)b * a.Tq + qrow) * a.ldo + h * DK : nullptr;
         bf16* op2 = a.o2 ? (bf16*)a.o2 + ((long long)b * a.Tq + qrow) * a.ldo + h * DK : nullptr;
@@ -765,7 +783,7 @@ __global__ __launch_bounds__(NWV * 64, 8 / NWV) void attn_bf16_kernel(AttnArgs a
             }
     }
     if constexpr (NWV == 8) {
-        if (a.fout) fsmn_epilogue<QBLK, NT>(a, smem, qt, h, b, klen);
+        if (a.fout) fsmn_epilogue<QBLK, NT>(a, fxs, qt, h, b, klen);
     }
 }
 
@@ -804,7 +822,7 @@ hipError_t pfm_attention_fsmn(int dtype, const void* q, RowMap qmap, const void*
         (void)hipFuncSetAttribute((const void*)attn_bf16_kernel<4>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   2 * STG2);
         (void)hipFuncSetAttribute((const void*)attn_bf16_kernel<8>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  LDS8);
+                                  LDS8_FS);
     }
     // bf16 kernels address an utterance's key rows as base + t * ld (32-bit offsets)
     auto contiguous = [&](const RowMap& m) {
@@ -822,7 +840,7 @@ hipError_t pfm_attention_fsmn(int dtype, const void* q, RowMap qmap, const void*
         const int nw = pfm_knobs().attn_waves;
         if (nw == 8) {
             dim3 grid((Tq + 255) / 256, heads, B), block(512);
-            hipLaunchKernelGGL((attn_bf16_kernel<8>), grid, block, a.fout ? LDS8 : 2 * STG2, st, a);
+            hipLaunchKernelGGL((attn_bf16_kernel<8>), grid, block, a.fout ? LDS8_FS : 2 * STG2, st, a);
         } else {
             dim3 grid((Tq + 127) / 128, heads, B), block(256);
             hipLaunchKernelGGL(attn_bf16_kernel<4>, grid, block, 2 * STG2, st, a);

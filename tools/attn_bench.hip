@@ -1,7 +1,7 @@
-// Standalone timing of the bf16 encoder self-attention kernel (k_attn.hip attn_bf16_kernel<8, VAR, PD>, fused
+// Standalone timing of the bf16 encoder self-attention kernel (k_attn.hip attn_bf16_kernel<8, VAR>, fused
 // FSMN epilogue on, as the fast encoder launches it) on random data: one utterance group (B = 32 x 500 x 500,
 // 4 heads of 128) and the whole batch (B = 64). VAR: 0 product, 1 no K/V loads after tile 0, 2 no softmax,
-// 3 no PV products, 4 no QK products, 5 no key loop. PD: 1 or 2 tiles of K/V in flight. HIP events, one process.
+// 3 no PV products, 4 no QK products, 5 no key loop. HIP events, one process.
 //   hipcc -O3 -std=c++17 --offload-arch=gfx950 tools/attn_bench.hip -o tools/attn_bench && ./tools/attn_bench
 #include <cstdio>
 #include <cstdlib>
@@ -34,17 +34,18 @@ __global__ void fill_f32(float* p, long long n, unsigned seed, float scale) {
     p[i] = ((x & 0xffff) / 65536.f - 0.5f) * scale;
 }
 
-template <int VAR, int PD>
+template <int VAR>
 float run(const AttnArgs& a, int B, int T, int reps) {
-    auto k = attn_bf16_kernel<8, VAR, PD>;
-    CK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, LDS8));
+    auto k = attn_bf16_kernel<8, VAR>;
+    const int lds = LDS8_FS;
+    CK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
     dim3 grid((T + 255) / 256, 4, B), block(512);
-    for (int i = 0; i < 3; ++i) hipLaunchKernelGGL(k, grid, block, LDS8, 0, a);
+    for (int i = 0; i < 3; ++i) hipLaunchKernelGGL(k, grid, block, lds, 0, a);
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
     CK(hipEventRecord(e0, 0));
-    for (int i = 0; i < reps; ++i) hipLaunchKernelGGL(k, grid, block, LDS8, 0, a);
+    for (int i = 0; i < reps; ++i) hipLaunchKernelGGL(k, grid, block, lds, 0, a);
     CK(hipEventRecord(e1, 0));
     CK(hipEventSynchronize(e1));
     float ms = 0;
@@ -78,15 +79,13 @@ int main(int argc, char** argv) {
         a.scale = 1.f / sqrtf(128.f); a.fw = fw; a.fout = fb; a.fld = D; a.fD = D;
         const double fl = 4.0 * B * (double)T * T * 128 * H;
         for (int round = 0; round < 2; ++round) {
-            float t[8] = {run<0, 1>(a, B, T, reps), run<0, 2>(a, B, T, reps), run<1, 1>(a, B, T, reps),
-                          run<2, 1>(a, B, T, reps), run<3, 1>(a, B, T, reps), run<4, 1>(a, B, T, reps),
-                          run<5, 1>(a, B, T, reps), 0.f};
+            float t[8] = {run<0>(a, B, T, reps), run<1>(a, B, T, reps), run<2>(a, B, T, reps), run<3>(a, B, T, reps),
+                          run<4>(a, B, T, reps), run<5>(a, B, T, reps), 0.f, 0.f};
             AttnArgs an = a;
             an.fout = nullptr;
-            t[7] = run<0, 1>(an, B, T, reps);
-            printf("B=%d: PD1 %.1f us (%.0f TF) | PD2 %.1f (%.0f TF) | noKV %.1f | noSM %.1f | noPV %.1f | noQK %.1f | "
-                   "noLoop %.1f | PD1 no-FSMN %.1f\n",
-                   B, t[0], fl / t[0] / 1e6, t[1], fl / t[1] / 1e6, t[2], t[3], t[4], t[5], t[6], t[7]);
+            t[6] = run<0>(an, B, T, reps);
+            printf("B=%d: kernel %.1f us (%.0f TF) | noKV %.1f | noSM %.1f | noPV %.1f | noQK %.1f | noLoop %.1f | "
+                   "no FSMN %.1f\n", B, t[0], fl / t[0] / 1e6, t[1], t[2], t[3], t[4], t[5], t[6]);
         }
     }
     return 0;
