@@ -220,6 +220,9 @@ def main():
                     help="600 ms chunks per stream in the streaming (config C5) leg (0 = skip)")
     ap.add_argument("--stream-batch", type=int, default=64, help="concurrent streams of the C5 serving line")
     ap.add_argument("--punc-steps", type=int, default=5, help="timed CT-Transformer punctuation calls (0 = skip)")
+    ap.add_argument("--beam-steps", type=int, default=2,
+                    help="timed joint decoder + CTC prefix beam search steps (Paraformer-large + CTC head; 0 = skip)")
+    ap.add_argument("--beam", type=int, default=10, help="beam size of the beam-search leg")
     ap.add_argument("--long-audio-s", type=int, default=300,
                     help="seconds of synthetic audio for the VAD + ASR + punctuation leg (0 = skip)")
     args = ap.parse_args()
@@ -448,6 +451,31 @@ def main():
                              "path_tflops": round(sv_tf, 2), "path_frac": round(sv_tf / peak, 4),
                              "tokens_per_utt_mean": float(sv_last["ntok"].float().mean().item())}
         del seng
+
+    # ---- joint decoder + CTC prefix beam search (BASELINE config C5's CTC prefix-beam; Paraformer.inference with
+    # decoding_ctc_weight): Paraformer-large with a CTC head (ctc_weight 0.3), the same batch, rank 0
+    if rank == 0 and args.beam_steps > 0:
+        import dataclasses
+        bcfg = dataclasses.replace(cfg, ctc_weight=0.3)
+        beng = PfmEngine(bcfg, gpu)
+        beng.load_state_dict(make_weights(bcfg, args.seed))
+        beng.reserve(B, T)
+        bkw = dict(mode=args.mode, beam=args.beam, ctc_weight=0.3, penalty=0.0, nbest=1)
+        beng.run_beam(feats, lens, **bkw)
+        torch.cuda.synchronize()
+        tb = time.perf_counter()
+        for _ in range(args.beam_steps):
+            bl = beng.run_beam(feats, lens, **bkw)
+        torch.cuda.synchronize()
+        dtb = (time.perf_counter() - tb) / args.beam_steps
+        nb = bl["ntok"][:, 0].float()
+        out["beam_search"] = {"workload": (f"Paraformer-large + CTC head, B={B} x 30 s, joint decoder + CTC prefix beam "
+                                           f"search (beam {args.beam}, decoding_ctc_weight 0.3, pre-beam "
+                                           f"{int(1.5 * args.beam)}, end detection), one workgroup per utterance"),
+                              "value": round(B * T * FRAME_SEC / dtb, 1), "unit": "audio-sec/sec",
+                              "ms_per_step": round(dtb * 1e3, 2), "dtype": out["dtype"],
+                              "tokens_per_utt_mean": round(float(nb[nb >= 0].mean().item()), 2)}
+        del beng
 
     # ---- streaming Paraformer (BASELINE config C5): 600 ms chunks ([0, 10, 5], look-back 4 / 1) of
     # 30 s streams through pfm_stream_step, synthetic LFR+CMVN chunk rows resident in HBM; one stream

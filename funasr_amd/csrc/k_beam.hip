@@ -31,13 +31,35 @@ constexpr int MAXK = 16;                     // beam
 constexpr int MAXP = 64;                     // pre-beam candidates (int(1.5 beam), or the vocabulary without pre-beam)
 constexpr int MAXN = 16;                     // n-best
 
+// log1p(u) for u in [0, 1) (u = exp(-|a - b|) of logaddexp): 2 atanh(s), s = u / (2 + u) in [0, 1/3), as a series
+// in f64 (terms to s^17: truncation < 2^-34 relative; 1 / (2 + u) by v_rcp_f64 + two Newton steps) rounded once to
+// f32 — the correctly rounded value in all but rare halfway cases (the C library's log1pf is within 1 ulp of it),
+// at about a tenth of the f32 library routine's instructions
+__device__ __forceinline__ float log1p_unit(float u) {
+    const double x = (double)u, d = 2.0 + x;
+    double r = __builtin_amdgcn_rcp(d);
+    r = fma(fma(-d, r, 1.0), r, r);
+    r = fma(fma(-d, r, 1.0), r, r);
+    const double sd = x * r, z = sd * sd;
+    double p = 1.0 / 17.0;
+    p = fma(p, z, 1.0 / 15.0);
+    p = fma(p, z, 1.0 / 13.0);
+    p = fma(p, z, 1.0 / 11.0);
+    p = fma(p, z, 1.0 / 9.0);
+    p = fma(p, z, 1.0 / 7.0);
+    p = fma(p, z, 1.0 / 5.0);
+    p = fma(p, z, 1.0 / 3.0);
+    p = fma(p, z, 1.0);
+    return (float)(2.0 * sd * p);
+}
+
+// numpy's npy_logaddexpf (float32): equal operands -> x + ln 2, else max + log1p(exp(-|d|)); branch-free (both
+// signs of d in one wave), the same values (a NaN operand still gives NaN through the arithmetic)
 __device__ __forceinline__ float lae(float a, float b) {
 #pragma clang fp contract(off)
-    if (a == b) return a + 0.693147180559945309417232121458176568f;
-    const float d = a - b;
-    if (d > 0.f) return a + log1pf(expf(-d));
-    if (d <= 0.f) return b + log1pf(expf(d));
-    return d;   // nan
+    const float m = a > b ? a : b;
+    const float r = m + log1p_unit(expf(-fabsf(a - b)));
+    return a == b ? a + 0.693147180559945309417232121458176568f : r;
 }
 
 // row-wise log_softmax in place: x[r][0..V) -> x - max - log(sum exp(x - max)) (sum in f64)
@@ -85,54 +107,65 @@ struct BeamArgs {
     int Lcap;
     int* olen;           // [B][nbest] token count of each n-best hypothesis, -1 = none
     float* oscore;       // [B][nbest]
+    int wlds;            // the position's ws0 row staged in dynamic LDS (V floats)
 };
+
+// (value, index) order of the pre-beam: larger value first, equal values lower index first
+__device__ __forceinline__ bool beats(float w, int v, float bw, int bv) { return w > bw || (w == bw && v < bv); }
 
 __global__ __launch_bounds__(NT) void ctc_beam_kernel(BeamArgs a) {
 #pragma clang fp contract(off)   // every product rounded before its sum, as the reference's numpy / torch ops
-    const int b = blockIdx.x, tid = threadIdx.x;
+    const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int V = a.V, K = a.K, P = a.P, Tb = min(a.lens[b], a.T), maxlen = min(a.ntok[b], a.L);
     const int S = a.L + 2;   // yseq capacity: sos + L tokens + eos
+    const int kk = min(K, P), KP = K * P;
     const float* am = a.am + (long long)b * a.L * V;
     const float* x = a.x + (long long)b * a.T * V;
-    // scratch layout (floats): Rcur [K][T][2] | Rnew [K][P][T][2] | xs [T][P] | xb [T] | best_by_len [S + 1]
-    float* Rcur = a.fs + b * a.fstride;
-    float* Rnew = Rcur + (long long)K * a.T * 2;
-    float* xs = Rnew + (long long)K * P * a.T * 2;
+    // scratch (floats): Rb [2][T][K*P] float2 | xs [T][P] | xb [T] | Rs [K][T] | bylen [S + 1]
+    // The CTC states (r^n, r^b) of position i's candidates are column k*P + j of buffer i & 1 (frame-major: one
+    // recurrence step's stores are contiguous across lanes); a running hypothesis is the column it was created in,
+    // read from the other buffer at the next position, so nothing is copied between positions.
+    float2* Rb = (float2*)(a.fs + b * a.fstride);
+    float* xs = (float*)(Rb + 2LL * a.T * KP);
     float* xb = xs + (long long)a.T * P;
-    float* bylen = xb + a.T;
-    // (ints): ycur [K][S] | ynew [K][S] | yend [nbest][S] | has_len [S + 1] (ended lengths reach S)
-    int* ycur = a.is + b * a.istride;
-    int* ynew = ycur + K * S;
-    int* yend = ynew + K * S;
-    int* haslen = yend + a.nbest * S;
+    float* Rs = xb + a.T;
+    float* bylen = Rs + (long long)K * a.T;
+    // (ints): bpar [L][K] parent slot, btok [L][K] token of the hypothesis in beam slot k after position i |
+    // has_len [S + 1] (ended lengths reach S) | raw [S] (n-best output staging)
+    int* bpar = a.is + b * a.istride;
+    int* btok = bpar + (long long)a.L * K;
+    int* haslen = btok + (long long)a.L * K;
+    int* raw = haslen + S + 1;
 
     __shared__ int cs[MAXP];
     __shared__ float ws0c[MAXP];
-    __shared__ float psi[MAXK][MAXP];
+    __shared__ float psi[MAXK][MAXP], wsc[MAXK][MAXP];
     __shared__ float hscore[MAXK], hprev[MAXK];
-    __shared__ int hlen[MAXK], nlen[MAXK];
+    __shared__ int hlen[MAXK], hlast[MAXK], hcol[MAXK];   // running beam: length, last token, state column
     __shared__ float nscore[MAXK], nprev[MAXK];
-    __shared__ int nsrc[MAXK], ntokn[MAXK];            // new hypothesis: source (k * P + j), appended token
-    __shared__ float cscore[MAXK * MAXK];
-    __shared__ int cidx[MAXK * MAXK];
+    __shared__ int nsrc[MAXK], ntokn[MAXK], nlen[MAXK];
+    __shared__ float csc[MAXK * MAXK];
+    __shared__ int csrc[MAXK * MAXK];
     __shared__ float escore[MAXN];
-    __shared__ int elen[MAXN];
+    __shared__ int elen[MAXN], epos[MAXN], epar[MAXN], etok[MAXN], eeos[MAXN];   // n-best list, best first
     __shared__ int nrun, nend, stop;
     __shared__ float best_end;
-    __shared__ float redv[NT];
-    __shared__ int redi[NT];
+    __shared__ float redv[2][NT / 64];
+    __shared__ int redi[2][NT / 64];
+    extern __shared__ float ws0s[];   // [V] when a.wlds
+    const bool wlds = a.wlds != 0;
 
-    for (int s = tid; s <= S; s += NT) haslen[s] = 0;
+    for (int q = tid; q <= S; q += NT) haslen[q] = 0;
     if (tid == 0) {
         nrun = 1; nend = 0; stop = maxlen < 1; best_end = -INFINITY;
-        hscore[0] = 0.f; hprev[0] = 0.f; hlen[0] = 1;
-        ycur[0] = a.sos;
-        // CTCPrefixScore.initial_state: r^n = logzero, r^b = cumulative blank log-probs
+        hscore[0] = 0.f; hprev[0] = 0.f; hlen[0] = 1; hlast[0] = a.sos; hcol[0] = 0;
+        // CTCPrefixScore.initial_state (r^n = logzero, r^b = cumulative blank log-probs) as column 0 of buffer 1,
+        // the "previous" buffer of position 0
         float rb = 0.f;
+        float2* r0 = Rb + (long long)a.T * KP;
         for (int t = 0; t < Tb; ++t) {
             rb = t == 0 ? x[a.blank] : rb + x[(long long)t * V + a.blank];
-            Rcur[2 * t] = LOGZERO;
-            Rcur[2 * t + 1] = rb;
+            r0[(long long)t * KP] = make_float2(LOGZERO, rb);
         }
     }
     for (int t = tid; t < Tb; t += NT) xb[t] = x[(long long)t * V + a.blank];
@@ -140,142 +173,181 @@ __global__ __launch_bounds__(NT) void ctc_beam_kernel(BeamArgs a) {
 
     for (int i = 0; i < maxlen && !stop; ++i) {
         const float* ami = am + (long long)i * V;
-        // ---- pre-beam: top-P of ws0 (descending; equal values: lower id first)
-        for (int r = 0; r < P; ++r) {
+        const int nr = nrun;
+        const float2* Rprev = Rb + (long long)((i + 1) & 1) * a.T * KP;
+        float2* Rcur = Rb + (long long)(i & 1) * a.T * KP;
+        // ---- pre-beam: the top P of ws0 in (value desc, id asc) order. Each thread caches the best of its
+        // strided ids; per round the block-wide best is taken and only its owner rescans (for the best element
+        // after the taken one in that order)
+        if (P == V) {   // no pre-beam: the candidates are the whole vocabulary in id order
+            for (int v = tid; v < V; v += NT) { cs[v] = v; ws0c[v] = a.use_pen ? ami[v] + a.pen : ami[v]; }
+        } else {
+            // ws0 of this position: staged in LDS when the vocabulary fits (the owner rescans read it from there)
+            const float* wsrc = ami;
+            if (wlds) {
+                for (int v = tid; v < V; v += NT) ws0s[v] = a.use_pen ? ami[v] + a.pen : ami[v];
+                wsrc = ws0s;
+            }
+            const bool pen_in = !wlds && a.use_pen;
             float bv = -INFINITY;
             int bi = 0x7fffffff;
-            if (P == V) {   // no pre-beam: the candidates are the whole vocabulary in id order
-                if (tid == 0) { cs[r] = r; ws0c[r] = a.use_pen ? ami[r] + a.pen : ami[r]; }
-                continue;
-            }
             for (int v = tid; v < V; v += NT) {
-                bool taken = false;
-                for (int q = 0; q < r; ++q) taken |= cs[q] == v;
-                const float w = a.use_pen ? ami[v] + a.pen : ami[v];
-                if (!taken && (w > bv || (w == bv && v < bi))) { bv = w; bi = v; }
+                const float w = pen_in ? wsrc[v] + a.pen : wsrc[v];
+                if (bi == 0x7fffffff || beats(w, v, bv, bi)) { bv = w; bi = v; }
             }
-            redv[tid] = bv;
-            redi[tid] = bi;
-            __syncthreads();
-            for (int s = NT / 2; s > 0; s >>= 1) {
-                if (tid < s) {
-                    const float ov = redv[tid + s];
-                    const int oi = redi[tid + s];
-                    if (ov > redv[tid] || (ov == redv[tid] && oi < redi[tid])) { redv[tid] = ov; redi[tid] = oi; }
+            for (int r = 0; r < P; ++r) {
+                float gv = bv;
+                int gi = bi;
+#pragma unroll
+                for (int o = 32; o > 0; o >>= 1) {
+                    const float ov = __shfl_xor(gv, o, 64);
+                    const int oi = __shfl_xor(gi, o, 64);
+                    if (oi != 0x7fffffff && (gi == 0x7fffffff || beats(ov, oi, gv, gi))) { gv = ov; gi = oi; }
                 }
+                if (lane == 0) { redv[r & 1][wv] = gv; redi[r & 1][wv] = gi; }
                 __syncthreads();
+                gv = redv[r & 1][0];
+                gi = redi[r & 1][0];
+#pragma unroll
+                for (int q = 1; q < NT / 64; ++q) {
+                    const float ov = redv[r & 1][q];
+                    const int oi = redi[r & 1][q];
+                    if (oi != 0x7fffffff && (gi == 0x7fffffff || beats(ov, oi, gv, gi))) { gv = ov; gi = oi; }
+                }
+                if (tid == 0) { cs[r] = gi; ws0c[r] = gv; }
+                if (gi % NT == tid) {   // owner of the taken id: next best strictly after (gv, gi)
+                    bv = -INFINITY;
+                    bi = 0x7fffffff;
+                    for (int v = tid; v < V; v += NT) {
+                        const float w = pen_in ? wsrc[v] + a.pen : wsrc[v];
+                        if (!beats(w, v, gv, gi) && !(w == gv && v == gi) && (bi == 0x7fffffff || beats(w, v, bv, bi))) {
+                            bv = w;
+                            bi = v;
+                        }
+                    }
+                }
             }
-            if (tid == 0) { cs[r] = redi[0]; ws0c[r] = redv[0]; }
-            __syncthreads();
         }
         __syncthreads();
-        // ---- the candidates' CTC log-probs over the frames, gathered once per position
-        for (int e = tid; e < Tb * P; e += NT) {
-            const int t = e / P, j = e - t * P;
-            xs[e] = x[(long long)t * V + cs[j]];
+        // ---- the candidates' CTC log-probs over the frames, gathered once per position; r_sum of every running
+        // hypothesis (logaddexp(r^n, r^b), the log_phi of a non-repeated label)
+        {   // 8 gathers in flight per thread
+            int e = tid;
+            for (; e + 7 * NT < Tb * P; e += 8 * NT) {
+                float g8[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const int q = e + u * NT, t = q / P, j = q - t * P;
+                    g8[u] = x[(long long)t * V + cs[j]];
+                }
+#pragma unroll
+                for (int u = 0; u < 8; ++u) xs[e + u * NT] = g8[u];
+            }
+            for (; e < Tb * P; e += NT) {
+                const int t = e / P, j = e - t * P;
+                xs[e] = x[(long long)t * V + cs[j]];
+            }
+        }
+        for (int e = tid; e < nr * Tb; e += NT) {
+            const int k = e / Tb, t = e - k * Tb;
+            const float2 rp = Rprev[(long long)t * KP + hcol[k]];
+            Rs[(long long)k * a.T + t] = lae(rp.x, rp.y);
         }
         __syncthreads();
-        // ---- CTC prefix scores: one thread per (hypothesis, candidate)
-        for (int w = tid; w < nrun * P; w += NT) {
+        // ---- CTC prefix scores and weighted scores: one thread per (hypothesis, candidate)
+        for (int w = tid; w < nr * P; w += NT) {
             const int k = w / P, j = w - k * P;
             const int c = cs[j];
             const int ol = hlen[k] - 1;                 // output_length (sos ignored)
-            const int last = ycur[k * S + hlen[k] - 1];
-            const bool phi_b = ol > 0 && c == last;     // log_phi = r^b(g) for a repeated label
-            const float* rp = Rcur + (long long)k * a.T * 2;
-            float* rn = Rnew + ((long long)k * P + j) * a.T * 2;
+            const bool phi_b = ol > 0 && c == hlast[k]; // log_phi = r^b(g) for a repeated label
+            const float2* rp = Rprev + hcol[k];         // frame t at rp[t * KP]
+            const float* rsum = Rs + (long long)k * a.T;
+            float2* rn = Rcur + w;
             float r0, r1, lpsi;
             const int start = max(ol, 1);
             if (ol == 0) {
                 r0 = xs[j];
                 r1 = LOGZERO;
-                if (Tb > 0) { rn[0] = r0; rn[1] = r1; }
+                if (Tb > 0) rn[0] = make_float2(r0, r1);
             } else {
                 r0 = LOGZERO;
                 r1 = LOGZERO;
-                if (ol - 1 < Tb) { rn[2 * (ol - 1)] = r0; rn[2 * (ol - 1) + 1] = r1; }
+                if (ol - 1 < Tb) rn[(long long)(ol - 1) * KP] = make_float2(r0, r1);
             }
             lpsi = r0;   // r[start - 1, 0]
-            for (int t = start; t < Tb; ++t) {
-                const float pn = rp[2 * (t - 1)], pb = rp[2 * (t - 1) + 1];
-                const float phi = phi_b ? pb : lae(pn, pb);
+            int t = start;
+            // 8 frames per trip: the trip's inputs are loaded together (one memory latency per 8 recurrence steps)
+            for (; t + 8 <= Tb; t += 8) {
+                float ph[8], xv[8], bq[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    ph[u] = phi_b ? rp[(long long)(t + u - 1) * KP].y : rsum[t + u - 1];
+                    xv[u] = xs[(t + u) * P + j];
+                    bq[u] = xb[t + u];
+                }
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const float n0 = lae(r0, ph[u]) + xv[u];
+                    const float n1 = lae(r0, r1) + bq[u];
+                    lpsi = lae(lpsi, ph[u] + xv[u]);
+                    r0 = n0;
+                    r1 = n1;
+                    rn[(long long)(t + u) * KP] = make_float2(r0, r1);
+                }
+            }
+            for (; t < Tb; ++t) {
+                const float phi = phi_b ? rp[(long long)(t - 1) * KP].y : rsum[t - 1];
                 const float xt = xs[t * P + j];
                 const float n0 = lae(r0, phi) + xt;
                 const float n1 = lae(r0, r1) + xb[t];
                 lpsi = lae(lpsi, phi + xt);
                 r0 = n0;
                 r1 = n1;
-                rn[2 * t] = r0;
-                rn[2 * t + 1] = r1;
+                rn[(long long)t * KP] = make_float2(r0, r1);
             }
-            if (c == a.eos) lpsi = Tb > 0 ? lae(rp[2 * (Tb - 1)], rp[2 * (Tb - 1) + 1]) : LOGZERO;   // r_sum[-1]
+            if (c == a.eos) lpsi = Tb > 0 ? rsum[Tb - 1] : LOGZERO;   // r_sum[-1]
             if (c == a.blank) lpsi = LOGZERO;
             psi[k][j] = lpsi;
+            const float ts = lpsi - hprev[k];
+            wsc[k][j] = (ws0c[j] + a.wctc * ts) + hscore[k];
         }
         __syncthreads();
-        // ---- scores, per-hypothesis beam, stable global prune (thread 0: at most beam x beam candidates)
+        // ---- per-hypothesis top kk (descending, equal scores: lower pre-beam rank), appended in hypothesis order
+        for (int w = tid; w < nr * P; w += NT) {
+            const int k = w / P, j = w - k * P;
+            const float v = wsc[k][j];
+            int r = 0;
+            for (int q = 0; q < P; ++q) r += (wsc[k][q] > v || (wsc[k][q] == v && q < j)) ? 1 : 0;
+            if (r < kk) { csc[k * kk + r] = v; csrc[k * kk + r] = w; }
+        }
+        __syncthreads();
+        // ---- sort-and-prune after each hypothesis (search.py:330-332) keeps the top K of all appended candidates in
+        // (score desc, append order) order: rank every candidate by counting those before it
+        const int nall = nr * kk, nc = min(K, nall);
+        for (int q = tid; q < nall; q += NT) {
+            const float v = csc[q];
+            int g = 0;
+            for (int o = 0; o < nall; ++o) g += (csc[o] > v || (csc[o] == v && o < q)) ? 1 : 0;
+            if (g < K) {
+                const int src = csrc[q], k = src / P, j = src - k * P;
+                nscore[g] = v;
+                nprev[g] = psi[k][j];
+                nsrc[g] = src;
+                ntokn[g] = cs[j];
+                nlen[g] = hlen[k] + 1;
+            }
+        }
+        __syncthreads();
+        // ---- post_process (search.py:401-451): hypotheses ending in <eos> (all of them at the last position, where
+        // <eos> is appended) go to the n-best list, the others keep their order on the beam (back-pointers only)
         if (tid == 0) {
-            int nc = 0;
-            for (int k = 0; k < nrun; ++k) {
-                float ws[MAXP];
-                for (int j = 0; j < P; ++j) {
-                    const float ts = psi[k][j] - hprev[k];
-                    ws[j] = (ws0c[j] + a.wctc * ts) + hscore[k];
-                }
-                bool used[MAXP];
-                for (int j = 0; j < P; ++j) used[j] = false;
-                const int kk = min(K, P);
-                for (int r = 0; r < kk; ++r) {   // top-beam of this hypothesis, descending
-                    int bj = -1;
-                    for (int j = 0; j < P; ++j)
-                        if (!used[j] && (bj < 0 || ws[j] > ws[bj])) bj = j;   // equal: lower pre-beam rank
-                    used[bj] = true;
-                    // stable insertion into the running candidate list (sorted descending)
-                    int pos = nc;
-                    while (pos > 0 && cscore[pos - 1] < ws[bj]) {
-                        cscore[pos] = cscore[pos - 1];
-                        cidx[pos] = cidx[pos - 1];
-                        --pos;
-                    }
-                    cscore[pos] = ws[bj];
-                    cidx[pos] = k * P + bj;
-                    ++nc;
-                }
-                if (nc > K) nc = K;   // search.py:330-332: sort and prune after each hypothesis
-            }
-            for (int s = 0; s < nc; ++s) {
-                const int k = cidx[s] / P, j = cidx[s] - k * P;
-                nscore[s] = cscore[s];
-                nprev[s] = psi[k][j];
-                nsrc[s] = cidx[s];
-                ntokn[s] = cs[j];
-                nlen[s] = hlen[k] + 1;
-            }
-            nrun = nc;
-        }
-        __syncthreads();
-        // ---- materialise the new hypotheses: yseq = parent's + token (+ eos at the last position), CTC state
-        const bool lastpos = i == maxlen - 1;
-        for (int s = 0; s < nrun; ++s) {
-            const int k = nsrc[s] / P;
-            for (int e = tid; e < nlen[s] - 1; e += NT) ynew[s * S + e] = ycur[k * S + e];
-            if (tid == 0) {
-                ynew[s * S + nlen[s] - 1] = ntokn[s];
-                if (lastpos) ynew[s * S + nlen[s]] = a.eos;
-            }
-            const float* src = Rnew + (long long)nsrc[s] * a.T * 2;
-            float* dst = Rcur + (long long)s * a.T * 2;
-            for (int e = tid; e < 2 * Tb; e += NT) dst[e] = src[e];
-        }
-        __syncthreads();
-        // ---- post_process (search.py:401-451): ended hypotheses leave the beam; end detection
-        if (tid == 0) {
+            const bool lastpos = i == maxlen - 1;
             int keep = 0;
-            for (int s = 0; s < nrun; ++s) {
-                const int len = nlen[s] + (lastpos ? 1 : 0);
-                const int lastt = ynew[s * S + len - 1];
-                if (lastt == a.eos) {
-                    const float sc = nscore[s];
+            for (int q = 0; q < nc; ++q) {
+                const int len = nlen[q] + (lastpos ? 1 : 0);
+                const int par = nsrc[q] / P;
+                if (lastpos || ntokn[q] == a.eos) {
+                    const float sc = nscore[q];
                     if (!haslen[len] || sc > bylen[len]) bylen[len] = sc;
                     haslen[len] = 1;
                     best_end = fmaxf(best_end, sc);
@@ -283,27 +355,23 @@ __global__ __launch_bounds__(NT) void ctc_beam_kernel(BeamArgs a) {
                     int pos = nend < a.nbest ? nend : a.nbest;
                     while (pos > 0 && escore[pos - 1] < sc) --pos;
                     if (pos < a.nbest) {
-                        const int last = (nend < a.nbest ? nend : a.nbest - 1);
-                        for (int q = last; q > pos; --q) {
-                            escore[q] = escore[q - 1];
-                            elen[q] = elen[q - 1];
-                            for (int e = 0; e < elen[q]; ++e) yend[q * S + e] = yend[(q - 1) * S + e];
+                        const int last = nend < a.nbest ? nend : a.nbest - 1;
+                        for (int e = last; e > pos; --e) {
+                            escore[e] = escore[e - 1]; elen[e] = elen[e - 1]; epos[e] = epos[e - 1];
+                            epar[e] = epar[e - 1]; etok[e] = etok[e - 1]; eeos[e] = eeos[e - 1];
                         }
-                        escore[pos] = sc;
-                        elen[pos] = len;
-                        for (int e = 0; e < len; ++e) yend[pos * S + e] = ynew[s * S + e];
+                        escore[pos] = sc; elen[pos] = len; epos[pos] = i; epar[pos] = par; etok[pos] = ntokn[q];
+                        eeos[pos] = lastpos ? 1 : 0;
                         if (nend < a.nbest) ++nend;
                     }
-                } else {   // stays on the beam: compact in order (slot keep <= s)
-                    if (keep != s) {
-                        for (int e = 0; e < nlen[s]; ++e) ynew[keep * S + e] = ynew[s * S + e];
-                        float* dst = Rcur + (long long)keep * a.T * 2;
-                        const float* src = Rcur + (long long)s * a.T * 2;
-                        for (int e = 0; e < 2 * Tb; ++e) dst[e] = src[e];
-                    }
-                    hscore[keep] = nscore[s];
-                    hprev[keep] = nprev[s];
-                    hlen[keep] = nlen[s];
+                } else {
+                    hscore[keep] = nscore[q];
+                    hprev[keep] = nprev[q];
+                    hlen[keep] = nlen[q];
+                    hlast[keep] = ntokn[q];
+                    hcol[keep] = nsrc[q];
+                    bpar[(long long)i * K + keep] = par;
+                    btok[(long long)i * K + keep] = ntokn[q];
                     ++keep;
                 }
             }
@@ -316,15 +384,12 @@ __global__ __launch_bounds__(NT) void ctc_beam_kernel(BeamArgs a) {
                 }
                 if (count == 3) stop = 1;
             }
-            if (nrun == 0) stop = 1;
+            if (keep == 0) stop = 1;
         }
         __syncthreads();
-        // ynew -> ycur for the survivors
-        for (int s = 0; s < nrun; ++s)
-            for (int e = tid; e < hlen[s]; e += NT) ycur[s * S + e] = ynew[s * S + e];
-        __syncthreads();
     }
-    // ---- n-best token ids: yseq[1:-1] without eos / sos / blank
+    // ---- n-best token ids: yseq[1:-1] without eos / sos / blank; the tokens of an ended hypothesis are its own
+    // (position epos) and its parent chain's, found by walking the back-pointers
     if (tid == 0) {
         for (int n = 0; n < a.nbest; ++n) {
             int* out = a.tokens + ((long long)b * a.nbest + n) * a.Lcap;
@@ -333,9 +398,19 @@ __global__ __launch_bounds__(NT) void ctc_beam_kernel(BeamArgs a) {
                 a.oscore[b * a.nbest + n] = -INFINITY;
                 continue;
             }
+            // raw = y_0 .. y_epos (+ eos): tokens after sos; yseq[1:-1] drops its last element
+            const int p = epos[n];
+            raw[p] = etok[n];
+            int slot = epar[n];
+            for (int q = p - 1; q >= 0; --q) {
+                raw[q] = btok[(long long)q * K + slot];
+                slot = bpar[(long long)q * K + slot];
+            }
+            const int nraw = p + 1 + eeos[n] - 1;   // elen[n] - 2 elements between sos and the last one
+            if (eeos[n]) raw[p + 1] = a.eos;
             int cnt = 0;
-            for (int e = 1; e < elen[n] - 1; ++e) {
-                const int tkn = yend[n * S + e];
+            for (int e = 0; e < nraw; ++e) {
+                const int tkn = raw[e];
                 if (tkn == a.eos || tkn == a.sos || tkn == a.blank) continue;
                 if (cnt < a.Lcap) out[cnt] = tkn;
                 ++cnt;
@@ -357,9 +432,9 @@ hipError_t pfm_logsoftmax_rows(float* x, long long rows, long long ld, int V, hi
 
 // scratch sizes per utterance for pfm_ctc_beam
 long long pfm_ctc_beam_fscratch(int K, int P, int T, int L) {
-    return (long long)K * T * 2 + (long long)K * P * T * 2 + (long long)T * P + T + (L + 3);
+    return (2LL * T * K * P * 2 + (long long)T * P + T + (long long)K * T + (L + 3) + 1) & ~1LL;   // even: float2 rows
 }
-long long pfm_ctc_beam_iscratch(int K, int nbest, int L) { return (long long)(2 * K + nbest) * (L + 2) + (L + 3); }
+long long pfm_ctc_beam_iscratch(int K, int nbest, int L) { return 2LL * L * K + (L + 3) + (L + 2); }
 
 hipError_t pfm_ctc_beam(const float* am, int L, const float* x, int T, const int* lens, const int* ntok, int B, int V,
                         int K, int P, int nbest, float wctc, float pen, int use_pen, int end_detect, int sos, int eos,
@@ -374,7 +449,16 @@ hipError_t pfm_ctc_beam(const float* am, int L, const float* x, int T, const int
     a.blank = blank; a.fs = fs; a.is = is; a.fstride = pfm_ctc_beam_fscratch(K, P, T, L);
     a.istride = pfm_ctc_beam_iscratch(K, nbest, L); a.tokens = tokens; a.Lcap = Lcap; a.olen = olen;
     a.oscore = oscore;
-    hipLaunchKernelGGL(ctc_beam_kernel, dim3(B), dim3(NT), 0, st, a);
+    const size_t lds = (size_t)V * sizeof(float);
+    a.wlds = lds <= 128 * 1024 ? 1 : 0;
+    if (a.wlds) {
+        static bool attr = false;
+        if (!attr) {
+            attr = true;
+            (void)hipFuncSetAttribute((const void*)ctc_beam_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024);
+        }
+    }
+    hipLaunchKernelGGL(ctc_beam_kernel, dim3(B), dim3(NT), a.wlds ? lds : 0, st, a);
     PFM_LAUNCH_CHECK();
     return hipSuccess;
 }
