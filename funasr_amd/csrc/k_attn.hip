@@ -495,15 +495,27 @@ __device__ __forceinline__ void fsmn_epilogue(const AttnArgs& a, const unsigned 
     for (int i = 0; i < 8; ++i)
 #pragma unroll
         for (int j = 0; j < 8; ++j) y[i][j] = 0.f;
+    // every window row is read once (18 rows for 8 outputs x 11 taps) and feeds each output it touches; an output's
+    // taps still accumulate in ascending k (row r = i + k ascending), the order of fsmn_win_kernel
+    float w8[FK][8];
 #pragma unroll
     for (int k = 0; k < FK; ++k) {
         const float4 wa = *(const float4*)(ws + k * DK + c8), wb = *(const float4*)(ws + k * DK + c8 + 4);
-        const float w8[8] = {wa.x, wa.y, wa.z, wa.w, wb.x, wb.y, wb.z, wb.w};
+        w8[k][0] = wa.x; w8[k][1] = wa.y; w8[k][2] = wa.z; w8[k][3] = wa.w;
+        w8[k][4] = wb.x; w8[k][5] = wb.y; w8[k][6] = wb.z; w8[k][7] = wb.w;
+    }
+#pragma unroll
+    for (int r = 0; r < 8 + FK - 1; ++r) {
+        const bf16x8 x = *(const bf16x8*)(xs + (rb * 8 + r) * RB + c8 * 2);
+        float xf[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) xf[j] = bf2f(x[j]);
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-            const bf16x8 x = *(const bf16x8*)(xs + (rb * 8 + i + k) * RB + c8 * 2);
+            const int k = r - i;
+            if (k < 0 || k >= FK) continue;
 #pragma unroll
-            for (int j = 0; j < 8; ++j) y[i][j] = fmaf(w8[j], bf2f(x[j]), y[i][j]);
+            for (int j = 0; j < 8; ++j) y[i][j] = fmaf(w8[k][j], xf[j], y[i][j]);
         }
     }
 #pragma unroll
