@@ -181,3 +181,31 @@ def test_beam_rejects_bad_arguments():
     plain.load_state_dict(make_weights(paraformer_tiny(), 0))
     with pytest.raises(PfmError):
         plain.run_beam(x, l, beam=2)
+
+
+@pytest.mark.parametrize("seed,B,T,L,V,beam,pen", [(3, 4, 100, 40, 500, 5, 0.0), (4, 3, 64, 30, 300, 8, 0.5),
+                                                    (5, 2, 120, 50, 2000, 10, 0.0)])
+def test_beam_kernel_random_logprobs_vs_oracle(seed, B, T, L, V, beam, pen):
+    """The search kernel alone (pfm_op_ctc_beam) against the oracle restatement (oracle/beam_ref.py, pinned to the
+    reference's beam_search goldens) on identical seeded log-probs over a grid of sizes, beams and length bonuses:
+    the same n-best token sequences, scores within 1e-5 relative. Ragged frame / token counts per utterance."""
+    from funasr_amd.runtime import op_ctc_beam
+    from oracle.beam_ref import beam_search
+    g = torch.Generator().manual_seed(seed)
+    am = torch.log_softmax(torch.randn(B, L, V, generator=g) * 2.5, -1)
+    x = torch.log_softmax(torch.randn(B, T, V, generator=g) * 2.5, -1)
+    lens = torch.tensor([T - 13 * i for i in range(B)], dtype=torch.int32)
+    ntok = torch.tensor([L - 7 * i for i in range(B)], dtype=torch.int32)
+    sos, eos = V - 1, V - 2
+    nbest = min(3, beam)
+    toks, nt, sc = op_ctc_beam(am.cuda(), x.cuda(), lens.cuda(), ntok.cuda(), beam, 0.3, pen, nbest, sos, eos, 0)
+    toks, nt, sc = toks.cpu().numpy(), nt.cpu().numpy(), sc.cpu().numpy()
+    for i in range(B):
+        hyps = beam_search(am[i, : int(ntok[i])].numpy(), x[i, : int(lens[i])].numpy(), beam, 0.3, pen, sos, eos)
+        for n in range(nbest):
+            if n >= len(hyps):
+                assert nt[i, n] == -1
+                continue
+            want = [t for t in hyps[n].yseq[1:-1] if t not in (eos, sos, 0)]
+            assert toks[i, n, : nt[i, n]].tolist() == want, (i, n)
+            assert abs(sc[i, n] - float(hyps[n].score)) <= 1e-5 * abs(float(hyps[n].score)), (i, n)
