@@ -275,6 +275,9 @@ __device__ __forceinline__ void fsmn_epilogue_f32(const AttnArgs& a, int qt, int
     }
 }
 
+// VAR (diagnostic instantiations for standalone timing; the library instantiates VAR 0): 1 no staging after tile
+// 0, 2 no softmax, 3 no PV products, 4 no QK products
+template <int VAR = 0>
 __global__ __launch_bounds__(512) void attn_x6_kernel(AttnArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int qt = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
@@ -369,21 +372,24 @@ __global__ __launch_bounds__(512) void attn_x6_kernel(AttnArgs a) {
     __syncthreads();
     for (int t = 0; t < ntiles; ++t) {
         const int cur = t & 1;
-        if (t + 1 < ntiles) stage(t + 1, cur ^ 1);
-        const unsigned char* Ks = smem + cur * X6_STG;
+        if (VAR != 1 && t + 1 < ntiles) stage(t + 1, cur ^ 1);
+        const unsigned char* Ks = smem + (VAR == 1 ? 0 : cur) * X6_STG;
         const unsigned char* Vs = Ks + 3 * X6_KPL;
         // S^T[key][q]: A = K rows (key = fr, dims 16ks + 8fh ..), B = Q^T
         f32x16 s;
 #pragma unroll
         for (int e = 0; e < 16; ++e) s[e] = 0.f;
 #pragma unroll
-        for (int ks = 0; ks < 8; ++ks) {
+        for (int ks = 0; ks < (VAR == 4 ? 0 : 8); ++ks) {
             const unsigned char* kp = Ks + fr * X6_KP + ks * 32 + fh * 16;
             const bf16x8 k0 = *(const bf16x8*)kp, k1 = *(const bf16x8*)(kp + X6_KPL),
                          k2 = *(const bf16x8*)(kp + 2 * X6_KPL);
             s = mfma_x6(k0, k1, k2, q0[ks], q1[ks], q2[ks], s);
         }
         // identical masking / online softmax to attn_f32_kernel
+        if constexpr (VAR == 2) {
+            lrun = 1.f;
+        } else {
         float mt = -INFINITY;
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
@@ -407,9 +413,10 @@ __global__ __launch_bounds__(512) void attn_x6_kernel(AttnArgs a) {
         for (int d = 0; d < 4; ++d)
 #pragma unroll
             for (int e = 0; e < 16; ++e) o[d][e] *= corr;
+        }
         // O^T[d][q] += V^T.P^T: k step s16 takes accumulator registers 8 s16 .. 8 s16 + 7 as P^T
 #pragma unroll
-        for (int s16 = 0; s16 < 2; ++s16) {
+        for (int s16 = 0; s16 < (VAR == 3 ? 0 : 2); ++s16) {
             bf16x8 p0, p1, p2;
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
@@ -830,7 +837,7 @@ hipError_t pfm_attention_fsmn(int dtype, const void* q, RowMap qmap, const void*
     if (!attr_done) {
         attr_done = true;
         (void)hipFuncSetAttribute((const void*)attn_f32_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, LDS32);
-        (void)hipFuncSetAttribute((const void*)attn_x6_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, X6_LDS);
+        (void)hipFuncSetAttribute((const void*)attn_x6_kernel<0>, hipFuncAttributeMaxDynamicSharedMemorySize, X6_LDS);
         (void)hipFuncSetAttribute((const void*)attn_bf16_kernel<4>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   2 * STG2);
         (void)hipFuncSetAttribute((const void*)attn_bf16_kernel<8>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -844,7 +851,7 @@ hipError_t pfm_attention_fsmn(int dtype, const void* q, RowMap qmap, const void*
     if (dtype == DT_F32 && pfm_knobs().exact_x6 && ldo % 4 == 0 && ((uintptr_t)o % 16) == 0 &&
         ((uintptr_t)o2 % 8) == 0) {   // EXACT mode on split-bf16 MFMA (f32 accuracy; 4-column output stores)
         dim3 grid((Tq + 255) / 256, heads, B), block(512);
-        hipLaunchKernelGGL(attn_x6_kernel, grid, block, X6_LDS, st, a);
+        hipLaunchKernelGGL(attn_x6_kernel<0>, grid, block, X6_LDS, st, a);
     } else if (dtype == DT_F32) {
         dim3 grid((Tq + 127) / 128, heads, B), block(256);
         hipLaunchKernelGGL(attn_f32_kernel, grid, block, LDS32, st, a);
@@ -883,10 +890,10 @@ hipError_t pfm_attention_x3(const float* q, RowMap qmap, const float* k, RowMap 
     static bool attr_done = false;
     if (!attr_done) {
         attr_done = true;
-        (void)hipFuncSetAttribute((const void*)attn_x6_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, X6_LDS);
+        (void)hipFuncSetAttribute((const void*)attn_x6_kernel<0>, hipFuncAttributeMaxDynamicSharedMemorySize, X6_LDS);
     }
     dim3 grid((Tq + 255) / 256, heads, B), block(512);
-    hipLaunchKernelGGL(attn_x6_kernel, grid, block, X6_LDS, st, a);
+    hipLaunchKernelGGL(attn_x6_kernel<0>, grid, block, X6_LDS, st, a);
     PFM_LAUNCH_CHECK();
     return hipSuccess;
 }

@@ -53,6 +53,57 @@ float run(const AttnArgs& a, int B, int T, int reps) {
     return ms * 1e3f / reps;
 }
 
+template <int VAR>
+float run_x6(const AttnArgs& a, int B, int T, int reps) {
+    auto k = attn_x6_kernel<VAR>;
+    CK(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, X6_LDS));
+    dim3 grid((T + 255) / 256, 4, B), block(512);
+    for (int i = 0; i < 2; ++i) hipLaunchKernelGGL(k, grid, block, X6_LDS, 0, a);
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    CK(hipEventRecord(e0, 0));
+    for (int i = 0; i < reps; ++i) hipLaunchKernelGGL(k, grid, block, X6_LDS, 0, a);
+    CK(hipEventRecord(e1, 0));
+    CK(hipEventSynchronize(e1));
+    float ms = 0;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    return ms * 1e3f / reps;
+}
+
+// EXACT-mode attention (attn_x6_kernel: split-bf16 x6, f32 FSMN epilogue) as the exact encoder launches it, one group
+void bench_x6(int reps) {
+    const int T = 500, D = 512, B = 32;
+    float *qkv, *fo, *fw;
+    bf16* o3;
+    int* lens;
+    CK(hipMalloc(&qkv, (size_t)B * T * 3 * D * 4));
+    CK(hipMalloc(&o3, (size_t)B * T * 3 * D * 2));
+    CK(hipMalloc(&fo, (size_t)B * T * D * 4));
+    CK(hipMalloc(&fw, 11 * D * 4));
+    CK(hipMalloc(&lens, B * 4));
+    const long long n = (long long)B * T * 3 * D;
+    hipLaunchKernelGGL(fill_f32, dim3((n + 255) / 256), dim3(256), 0, 0, qkv, n, 7u, 4.f);
+    hipLaunchKernelGGL(fill_f32, dim3((11 * D + 255) / 256), dim3(256), 0, 0, fw, 11LL * D, 2u, 0.5f);
+    std::vector<int> hl(B, T);
+    CK(hipMemcpy(lens, hl.data(), B * 4, hipMemcpyHostToDevice));
+    AttnArgs a;
+    a.q = qkv; a.qmap = rowmap_plain(3 * D); a.k = qkv + D; a.kmap = rowmap_plain(3 * D);
+    a.v = qkv + 2 * D; a.vmap = rowmap_plain(3 * D); a.o = nullptr; a.ldo = 3 * D; a.o2 = o3; a.o2_dtype = DT_X3;
+    a.klen = lens; a.Tq = T; a.Tk = T; a.scale = 1.f / sqrtf(128.f); a.fw = fw; a.fout = nullptr; a.fld = D; a.fD = D;
+    a.fout32 = fo;
+    const double fl = 6.0 * 4.0 * B * (double)T * T * 128 * 4;   // bf16 MFMA FLOPs issued (six products)
+    for (int round = 0; round < 2; ++round) {
+        const float t0 = run_x6<0>(a, B, T, reps), t1 = run_x6<1>(a, B, T, reps), t2 = run_x6<2>(a, B, T, reps),
+                    t3 = run_x6<3>(a, B, T, reps), t4 = run_x6<4>(a, B, T, reps);
+        AttnArgs an = a;
+        an.fout32 = nullptr;
+        const float t5 = run_x6<0>(an, B, T, reps);
+        printf("x6 B=%d: kernel %.1f us (%.0f TF issued) | no staging %.1f | no softmax %.1f | no PV %.1f | no QK %.1f | "
+               "no FSMN %.1f\n", B, t0, fl / t0 / 1e6, t1, t2, t3, t4, t5);
+    }
+}
+
 int main(int argc, char** argv) {
     const int T = 500, H = 4, D = 512;
     const int Bmax = 64;
@@ -70,6 +121,7 @@ int main(int argc, char** argv) {
     std::vector<int> hl(Bmax, T);
     CK(hipMemcpy(lens, hl.data(), Bmax * 4, hipMemcpyHostToDevice));
     const int reps = argc > 1 ? atoi(argv[1]) : 20;
+    bench_x6(reps);
     for (int B : {32, 64}) {
         AttnArgs a;
         a.q = qkv; a.qmap = rowmap_plain(3 * D);
