@@ -35,6 +35,7 @@ constexpr int FD = 512, FF = 2048, BM = 64;
 constexpr int HC = 256, NCH = FF / HC;          // hidden chunk, chunks
 constexpr int TILE = 16384, TPC = 32, NTILE = NCH * TPC;
 constexpr int OP_TILES = 32;                    // out-projection Wo [512][512]: 16 k steps x 2 halves (W2 format)
+constexpr int QK_TILES = 3 * OP_TILES;          // next layer's Wqkv [1536][512]: three Wo-format passes
 constexpr int OFF_AN = 0, OFF_H = 65536, OFF_RING = 98304, LDS_BYTES = 163840;
 constexpr int OFF_RED = LDS_BYTES - 4096, OFF_STATS = OFF_RED - 512;   // DEC epilogue (above the Y image)
 constexpr int YP = 516;                         // epilogue f32 row pitch (floats)
@@ -71,7 +72,8 @@ template <int HB> struct Frag { bf16x8 w[HB]; bf16x8 a[4]; };
 
 // VAR (diagnostic instantiations for standalone timing; the library instantiates VAR 0 only): 0 = the kernel; 1 = no weight DMA (stale ring); 2 = no MFMAs;
 // 3 = every tile streams ring tiles 0..3 of the layer (L2-hot 64 KiB); 4 = prologue + epilogue only (no
-// tile loop); 5 = VAR 1 without the per-tile barriers (MFMA + fragment reads alone)
+// tile loop); 5 = VAR 1 without the per-tile barriers (MFMA + fragment reads alone); OP only: 6 = prologue, phase 0 and
+// LN2, then exit; 7 = VAR 6 without phase 0 (the I/O of the OP transition alone)
 //
 // OP (the attention sub-layer's out-projection folded in front): the block starts from the attention output
 // O and the FSMN output F (bf16 rows) instead of x:
@@ -114,10 +116,11 @@ __global__ __launch_bounds__(64 * NW) void ffn_fused_kernel(const float* __restr
     const long long m0 = (long long)blockIdx.x * BM;
     constexpr int WR = 256 / NW, HB = WR / 16, RPW = BM / NW, LPW = TILE / (1024 * NW);
     using FragT = Frag<HB>;
-    constexpr bool OP = MODE == 1 || MODE == 3, DEC = MODE == 2 || MODE == 3;
+    constexpr bool OP = MODE == 1 || MODE == 3 || MODE == 4, DEC = MODE == 2 || MODE == 3;
+    constexpr bool EOP = MODE == 1 || MODE == 4, QK = MODE == 4;
     constexpr int T0 = OP ? OP_TILES : 0;      // FFN tiles start after the Wo tiles
     float rs[4] = {0.f, 0.f, 0.f, 0.f}, rq[4] = {0.f, 0.f, 0.f, 0.f};   // DEC: hidden row sums / sums of squares
-    constexpr int NT_ALL = NTILE + T0;
+    constexpr int NT_ALL = NTILE + T0 + (QK ? QK_TILES : 0);
 
     auto issue = [&](int t) {
         if (t >= NT_ALL || VAR == 1 || VAR == 5) return;
@@ -133,6 +136,34 @@ __global__ __launch_bounds__(64 * NW) void ffn_fused_kernel(const float* __restr
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_sched_barrier(0);
+    };
+    // OP row statistics: lane partials -> the 4 g lanes -> the 8 waves through LDS ([2][8 waves][64 rows] in the
+    // H image, which is free between chunks' uses: before chunk 0 and after the last chunk)
+    float* red = (float*)(smem + OFF_H);
+    auto row_reduce = [&](float (&v)[4], int slot) {
+#pragma unroll
+        for (int mb = 0; mb < 4; ++mb) {
+            v[mb] += __shfl_xor(v[mb], 16, 64);
+            v[mb] += __shfl_xor(v[mb], 32, 64);
+            if (g == 0) red[slot * 512 + w * 64 + 16 * mb + r16] = v[mb];
+        }
+        bar();
+#pragma unroll
+        for (int mb = 0; mb < 4; ++mb) {
+            float t = 0.f;
+#pragma unroll
+            for (int ww = 0; ww < NW; ++ww) t += red[slot * 512 + ww * 64 + 16 * mb + r16];
+            v[mb] = t;
+        }
+    };
+    // the lane's 4 consecutive columns 4g .. 4g+3 of the 16 at a wave-uniform address, by scalar loads (a vector load
+    // would share vmcnt with the in-flight ring DMAs and drain the ring before its first use)
+    auto cols4 = [&](const float* p) {
+        float v[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) v[k] = p[k];
+        return make_float4(pick4(v[0], v[4], v[8], v[12], g), pick4(v[1], v[5], v[9], v[13], g),
+                           pick4(v[2], v[6], v[10], v[14], g), pick4(v[3], v[7], v[11], v[15], g));
     };
     // ---- prologue: LN2 of rows m0 + 8w .. + 7 -> bf16 A image (row pitch 1 KiB, slot ^ (row & 15))
     //      (OP: the attention output rows go to the A image instead; LN2 follows phase 0)
@@ -322,25 +353,26 @@ __global__ __launch_bounds__(64 * NW) void ffn_fused_kernel(const float* __restr
     }
     bar();
     FragT F0, F1;
-    if constexpr (OP) {
-        // phase 0: Wo tile t = k step t >> 1 (of the O image in the A slot), half t & 1
-        auto rd0 = [&](int t, FragT& f) {
-            rd_w(t, f);
-            const int j = t >> 1;
+    // phase 0 (phase 3): Wo (Wqkv) tile t = k step (t >> 1) & 15 of the O (xn) image in the A slot, half t & 1
+    auto rd0 = [&](int t, FragT& f) {
+        rd_w(t, f);
+        const int j = (t >> 1) & 15;
 #pragma unroll
-            for (int mb = 0; mb < 4; ++mb)
-                f.a[mb] = ld128(smem + OFF_AN + (16 * mb + r16) * 1024 + (((4 * j + g) ^ r16) << 4));
-        };
-        rd0(0, F0);
-        for (int s2 = 0; s2 < OP_TILES / 2 - 1; ++s2) {
-            top(2 * s2); rd_w2(2 * s2 + 1, F1, F0); mm2a(F0);
-            top(2 * s2 + 1); rd0(2 * s2 + 2, F0); mm2b(F1);
+        for (int mb = 0; mb < 4; ++mb)
+            f.a[mb] = ld128(smem + OFF_AN + (16 * mb + r16) * 1024 + (((4 * j + g) ^ r16) << 4));
+    };
+    if constexpr (OP) {
+        if constexpr (VAR != 7) {
+            rd0(0, F0);
+            for (int s2 = 0; s2 < OP_TILES / 2 - 1; ++s2) {
+                top(2 * s2); rd_w2(2 * s2 + 1, F1, F0); mm2a(F0);
+                top(2 * s2 + 1); rd0(2 * s2 + 2, F0); mm2b(F1);
+            }
+            top(OP_TILES - 2); rd_w2(OP_TILES - 1, F1, F0); mm2a(F0);
+            top(OP_TILES - 1); mm2b(F1);
         }
-        top(OP_TILES - 2); rd_w2(OP_TILES - 1, F1, F0); mm2a(F0);
-        top(OP_TILES - 1); mm2b(F1);
         // x1 = ((Y0 + bo) + F) + x in the accumulator layout: acc2{a,b}[nb][mb][e] = x1[row 16mb + r16]
         // [col 32w + 16nb + 4g + e (+256 for b)]; LN2 row statistics: lane partials -> 4 g lanes -> 8 waves
-        float* red = (float*)(smem + OFF_H);   // [2][8 waves][64 rows] (the H image is free until chunk 0)
         float part[4] = {0.f, 0.f, 0.f, 0.f};
         // Addend loads are branch-free (a null X / Fr reads a valid stand-in and is selected away) and issued
         // in two batches of 8 row fragments, so a batch costs one memory latency: with the loads behind
@@ -395,22 +427,6 @@ __global__ __launch_bounds__(64 * NW) void ffn_fused_kernel(const float* __restr
                     }
             }
         }
-        auto row_reduce = [&](float (&v)[4], int slot) {
-#pragma unroll
-            for (int mb = 0; mb < 4; ++mb) {
-                v[mb] += __shfl_xor(v[mb], 16, 64);
-                v[mb] += __shfl_xor(v[mb], 32, 64);
-                if (g == 0) red[slot * 512 + w * 64 + 16 * mb + r16] = v[mb];
-            }
-            bar();
-#pragma unroll
-            for (int mb = 0; mb < 4; ++mb) {
-                float t = 0.f;
-#pragma unroll
-                for (int ww = 0; ww < NW; ++ww) t += red[slot * 512 + ww * 64 + 16 * mb + r16];
-                v[mb] = t;
-            }
-        };
         row_reduce(part, 0);   // its barrier also retires every wave's phase-0 reads of the O image
         float mean[4], q[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -434,7 +450,7 @@ __global__ __launch_bounds__(64 * NW) void ffn_fused_kernel(const float* __restr
                 const int n = 256 * hf + WR * w + 16 * nb + 4 * g;
                 gv[hf][nb] = *(const float4*)(g2 + n);
                 bev[hf][nb] = *(const float4*)(be2 + n);
-                c2v[hf][nb] = MODE == 1 ? *(const float4*)(b2 + n) : make_float4(0.f, 0.f, 0.f, 0.f);
+                c2v[hf][nb] = EOP ? *(const float4*)(b2 + n) : make_float4(0.f, 0.f, 0.f, 0.f);
             }
 #pragma unroll
         for (int mb = 0; mb < 4; ++mb) {
@@ -450,7 +466,7 @@ __global__ __launch_bounds__(64 * NW) void ffn_fused_kernel(const float* __restr
                     bf16x4 o = {f2bf((a[0] - mean[mb]) * rstd * gg.x + be.x), f2bf((a[1] - mean[mb]) * rstd * gg.y + be.y),
                                 f2bf((a[2] - mean[mb]) * rstd * gg.z + be.z), f2bf((a[3] - mean[mb]) * rstd * gg.w + be.w)};
                     *(bf16x4*)(smem + OFF_AN + m * 1024 + (((n >> 3) ^ (m & 15)) << 4) + ((n & 7) << 1)) = o;
-                    if constexpr (MODE == 1) {   // encoder: x2 = (x1 + b2) + W2 . H
+                    if constexpr (EOP) {   // encoder: x2 = (x1 + b2) + W2 . H
                         const float4 c2 = c2v[hf][nb];
                         a[0] += c2.x; a[1] += c2.y; a[2] += c2.z; a[3] += c2.w;
                     } else {                      // decoder: the FFN output has no residual
@@ -459,6 +475,10 @@ __global__ __launch_bounds__(64 * NW) void ffn_fused_kernel(const float* __restr
                 }
         }
         bar();   // the LN2 image is complete before chunk 0's first fragment reads
+        if constexpr (VAR == 6 || VAR == 7) {
+            vm_wait<0>();
+            return;
+        }
     }
     rd1(T0, F0);
     for (int c = 0; c < (VAR == 4 ? 0 : NCH); ++c) {
@@ -480,6 +500,104 @@ __global__ __launch_bounds__(64 * NW) void ffn_fused_kernel(const float* __restr
         top(tb + 30); rd_w2(tb + 31, F1, F0); mm2a(F0);
         if (c + 1 < NCH) { top(tb + 31); rd1(tb + 32, F0); }
         mm2b(F1);
+    }
+
+    if constexpr (QK) {
+        // ---- QK epilogue: x2 (the accumulators) -> Xo straight from the accumulator layout; LN1_next(x2) -> bf16
+        //      xn image in the A slot (row statistics across the 8 waves, as LN2 after phase 0). Every wave is past
+        //      top(tb + 30) of the last chunk, hence past its last H read: the H image holds the reduction.
+        float part[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int mb = 0; mb < 4; ++mb) {
+            const long long row = m0 + 16 * mb + r16;
+#pragma unroll
+            for (int hf = 0; hf < 2; ++hf)
+#pragma unroll
+                for (int nb = 0; nb < HB; ++nb) {
+                    const int n = 256 * hf + WR * w + 16 * nb + 4 * g;
+                    const f32x4& a = hf ? acc2b[nb][mb] : acc2a[nb][mb];
+                    if (row < M) *(float4*)(Xo + row * FD + n) = make_float4(a[0], a[1], a[2], a[3]);
+                    part[mb] += (a[0] + a[1]) + (a[2] + a[3]);
+                }
+        }
+        row_reduce(part, 0);   // its barrier retires every wave's fragment reads of the last ring tile
+        constexpr int T3 = T0 + NTILE;   // tiles T3 .. T3 + 2 were issued during the last chunk
+        issue(T3 + 3);
+        float mean[4], q[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int mb = 0; mb < 4; ++mb) mean[mb] = part[mb] * (1.f / FD);
+#pragma unroll
+        for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+            for (int hf = 0; hf < 2; ++hf)
+#pragma unroll
+                for (int nb = 0; nb < HB; ++nb) {
+                    const f32x4& a = hf ? acc2b[nb][mb] : acc2a[nb][mb];
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) { const float d = a[e] - mean[mb]; q[mb] += d * d; }
+                }
+        row_reduce(q, 1);
+        float4 gv[2][HB], bev[2][HB];
+#pragma unroll
+        for (int hf = 0; hf < 2; ++hf)
+#pragma unroll
+            for (int nb = 0; nb < HB; ++nb) {
+                gv[hf][nb] = cols4(gn + 256 * hf + WR * w + 16 * nb);
+                bev[hf][nb] = cols4(bn + 256 * hf + WR * w + 16 * nb);
+            }
+#pragma unroll
+        for (int mb = 0; mb < 4; ++mb) {
+            const int m = 16 * mb + r16;
+            const float rstd = 1.f / sqrtf(q[mb] * (1.f / FD) + eps);
+#pragma unroll
+            for (int hf = 0; hf < 2; ++hf)
+#pragma unroll
+                for (int nb = 0; nb < HB; ++nb) {
+                    const int n = 256 * hf + WR * w + 16 * nb + 4 * g;
+                    f32x4& a = hf ? acc2b[nb][mb] : acc2a[nb][mb];
+                    const float4 gg = gv[hf][nb], be = bev[hf][nb];
+                    bf16x4 o = {f2bf((a[0] - mean[mb]) * rstd * gg.x + be.x), f2bf((a[1] - mean[mb]) * rstd * gg.y + be.y),
+                                f2bf((a[2] - mean[mb]) * rstd * gg.z + be.z), f2bf((a[3] - mean[mb]) * rstd * gg.w + be.w)};
+                    *(bf16x4*)(smem + OFF_AN + m * 1024 + (((n >> 3) ^ (m & 15)) << 4) + ((n & 7) << 1)) = o;
+                    a[0] = 0.f; a[1] = 0.f; a[2] = 0.f; a[3] = 0.f;
+                }
+        }
+        vm_wait<PD * LPW>();   // tile T3 landed (the x2 stores ahead of tile T3 + 3 retire with it)
+        bar();                 // ... and the xn image is complete
+        // ---- phase 3: QKV_next[64 x 1536] = xn . Wqkv^T + bqkv in three passes of 512 columns (32 Wo-format
+        //      tiles each); outputs bf16 rows of 1536 in Xn, biases in c1
+        rd0(T3, F0);
+        for (int p = 0; p < 3; ++p) {
+            const int tp = T3 + OP_TILES * p;
+            for (int s2 = 0; s2 < OP_TILES / 2 - 1; ++s2) {
+                top(tp + 2 * s2); rd_w2(tp + 2 * s2 + 1, F1, F0); mm2a(F0);
+                top(tp + 2 * s2 + 1); rd0(tp + 2 * s2 + 2, F0); mm2b(F1);
+            }
+            top(tp + OP_TILES - 2); rd_w2(tp + OP_TILES - 1, F1, F0); mm2a(F0);
+            if (p < 2) { top(tp + OP_TILES - 1); rd0(tp + OP_TILES, F0); }
+            mm2b(F1);
+            const float* bq = c1 + 512 * p;
+            float4 bv[2][HB];
+#pragma unroll
+            for (int hf = 0; hf < 2; ++hf)
+#pragma unroll
+                for (int nb = 0; nb < HB; ++nb) bv[hf][nb] = cols4(bq + 256 * hf + WR * w + 16 * nb);
+#pragma unroll
+            for (int mb = 0; mb < 4; ++mb) {
+                const long long row = m0 + 16 * mb + r16;
+#pragma unroll
+                for (int hf = 0; hf < 2; ++hf)
+#pragma unroll
+                    for (int nb = 0; nb < HB; ++nb) {
+                        f32x4& a = hf ? acc2b[nb][mb] : acc2a[nb][mb];
+                        const float4 b4 = bv[hf][nb];
+                        const bf16x4 o = {f2bf(a[0] + b4.x), f2bf(a[1] + b4.y), f2bf(a[2] + b4.z), f2bf(a[3] + b4.w)};
+                        if (row < M) *(bf16x4*)(Xn + row * (3 * FD) + 512 * p + 256 * hf + WR * w + 16 * nb + 4 * g) = o;
+                        a[0] = 0.f; a[1] = 0.f; a[2] = 0.f; a[3] = 0.f;
+                    }
+            }
+        }
+        return;
     }
 
     if (VAR == 4) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -757,6 +875,22 @@ hipError_t pfm_ffn_fused_op(const bf16* o, const bf16* f, const float* bo, const
     if (((uintptr_t)x | (uintptr_t)xo | (uintptr_t)Wop | (uintptr_t)xn | (uintptr_t)o | (uintptr_t)f | (uintptr_t)bo) % 16)
         return hipErrorInvalidValue;
     ffn_launch_nw<0, 1>(st, M, x, g2, be2, eps, Wop, b1, b2, xo, gn, bn, xn, o, f, bo, nullptr);
+    PFM_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+// pfm_ffn_fused_op followed by the next encoder layer's QKV projection (ffn_fused_kernel MODE 4, phase 3):
+//   xo = x2 as pfm_ffn_fused_op;  qkv = bf16(LN_next(x2)) Wq^T + bq  (bf16 [M, 1536]; LN_next(x2) stays in LDS)
+// Wop: the 32 Wo tiles, the layer's FFN tiles, then pfm_ffn_pack_o of Wq's three 512-row blocks (96 tiles).
+hipError_t pfm_ffn_fused_op_qkv(const bf16* o, const bf16* f, const float* bo, const float* x, int M, const float* g2,
+                                const float* be2, float eps, const bf16* Wop, const float* b1, const float* b2, float* xo,
+                                const float* gn, const float* bn, const float* bq, bf16* qkv, hipStream_t st) {
+    if (M <= 0) return hipSuccess;
+    if (!o || !f || !bo || !xo || !gn || !bn || !bq || !qkv) return hipErrorInvalidValue;
+    if (((uintptr_t)x | (uintptr_t)xo | (uintptr_t)Wop | (uintptr_t)qkv | (uintptr_t)o | (uintptr_t)f | (uintptr_t)bo |
+         (uintptr_t)bq | (uintptr_t)gn | (uintptr_t)bn) % 16)
+        return hipErrorInvalidValue;
+    ffn_launch_nw<0, 4>(st, M, x, g2, be2, eps, Wop, b1, b2, xo, gn, bn, qkv, o, f, bo, bq);
     PFM_LAUNCH_CHECK();
     return hipSuccess;
 }

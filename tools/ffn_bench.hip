@@ -1,7 +1,7 @@
 // Standalone timing of the 64-row fused FFN kernel (k_ffn.hip ffn_fused_kernel, OP mode as the fast encoder launches
 // it) and its diagnostic variants on random data: VAR 0 the kernel, 1 no weight DMA (stale ring), 2 no MFMAs, 3 every
 // tile streams ring tiles 0..3 of the layer (the weight stream L2-hot), 4 prologue + epilogue only, 5 VAR 1 without
-// the per-tile barriers. HIP events, one process.
+// the per-tile barriers; then MODE 4 (the next layer's QKV projection as phase 3). HIP events, one process.
 //   hipcc -O3 -std=c++17 --offload-arch=gfx950 tools/ffn_bench.hip -o tools/ffn_bench && ./tools/ffn_bench [M ...]
 #include <cstdio>
 #include <cstdlib>
@@ -55,14 +55,14 @@ int main(int argc, char** argv) {
     for (int i = 1; i < argc; ++i) Ms.push_back(atoi(argv[i]));
     if (Ms.empty()) Ms = {16000, 32000};
     const int Mmax = 32768;
-    const long long nx = (long long)Mmax * 512, nw = (long long)(OP_TILES + NTILE) * TILE / 2;
+    const long long nx = (long long)Mmax * 512, nw = (long long)(OP_TILES + NTILE + QK_TILES) * TILE / 2;
     float *X, *Xo, *vecs;
     bf16 *Wp, *O, *Fr, *Xn;
     CK(hipMalloc(&X, nx * 4));
     CK(hipMalloc(&Xo, nx * 4));
     CK(hipMalloc(&O, nx * 2));
     CK(hipMalloc(&Fr, nx * 2));
-    CK(hipMalloc(&Xn, nx * 2));
+    CK(hipMalloc(&Xn, nx * 2 * 3));
     CK(hipMalloc(&Wp, nw * 2));
     CK(hipMalloc(&vecs, 16 * 2048 * 4));
     hipLaunchKernelGGL(fill_f32, dim3((nx + 255) / 256), dim3(256), 0, 0, X, nx, 1u, 4.f, 0.f);
@@ -85,6 +85,17 @@ int main(int argc, char** argv) {
             const float t5 = run<5, 1>(M, reps, X, g, be, Wp, b1, b2, Xo, gn, bn, Xn, O, Fr, bo, nullptr);
             printf("M=%6d OP: kernel %.1f us (%.0f TF/s) | no DMA %.1f | no MFMA %.1f | L2-hot W %.1f | pro/epi %.1f | "
                    "no DMA/bar %.1f\n", M, t0, fl / t0 / 1e6, t1, t2, t3, t4, t5);
+            const float t6 = run<6, 1>(M, reps, X, g, be, Wp, b1, b2, Xo, gn, bn, Xn, O, Fr, bo, nullptr);
+            const float t7 = run<7, 1>(M, reps, X, g, be, Wp, b1, b2, Xo, gn, bn, Xn, O, Fr, bo, nullptr);
+            printf("M=%6d OP anatomy: O load + x1 loads + LN2 %.1f | + phase 0 %.1f | + epilogue (= pro/epi) %.1f\n", M, t7,
+                   t6, t4);
+            const float q0 = run<0, 4>(M, reps, X, g, be, Wp, b1, b2, Xo, gn, bn, Xn, O, Fr, bo, vecs + 14336);
+            const float q1 = run<1, 4>(M, reps, X, g, be, Wp, b1, b2, Xo, gn, bn, Xn, O, Fr, bo, vecs + 14336);
+            const float q2 = run<2, 4>(M, reps, X, g, be, Wp, b1, b2, Xo, gn, bn, Xn, O, Fr, bo, vecs + 14336);
+            const float q3 = run<3, 4>(M, reps, X, g, be, Wp, b1, b2, Xo, gn, bn, Xn, O, Fr, bo, vecs + 14336);
+            const double flq = fl + 2.0 * M * 512.0 * 1536;
+            printf("M=%6d OP+QKV: kernel %.1f us (%.0f TF/s; +%.1f us over OP) | no DMA %.1f | no MFMA %.1f | L2-hot W %.1f\n",
+                   M, q0, flq / q0 / 1e6, q0 - t0, q1, q2, q3);
         }
     }
     return 0;
