@@ -658,21 +658,30 @@ __global__ __launch_bounds__(NWV * 64, 8 / NWV) void attn_bf16_kernel(AttnArgs a
         const unsigned char* Ks = smem + (t & 1) * STG2;
         const unsigned char* Vs = Ks + KTILE;
         f32x16 s[2];
+        // all 16 K fragments of the tile are read before the first product (graduated lgkmcnt waits): left to
+        // the scheduler, each ds_read was followed by lgkmcnt(0) and its MFMA, one LDS latency per product
+        bf16x8 kx[2][8];
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) {
+            const int row = kb * 32 + fr;
+#pragma unroll
+            for (int kq = 0; kq < 8; ++kq) kx[kb][kq] = *(const bf16x8*)(Ks + row * KROW + (((2 * kq + fh) ^ (row & 15)) << 4));
+        }
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb) {
 #pragma unroll
             for (int e = 0; e < 16; ++e) s[kb][e] = 0.f;
             if constexpr (VAR == 4) continue;
-            const int row = kb * 32 + fr;
 #pragma unroll
-            for (int kq = 0; kq < 8; ++kq) {
-                const bf16x8 kx = *(const bf16x8*)(Ks + row * KROW + (((2 * kq + fh) ^ (row & 15)) << 4));
-                s[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kx, qf[kq], s[kb], 0, 0, 0);
-            }
+            for (int kq = 0; kq < 8; ++kq) s[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kx[kb][kq], qf[kq], s[kb], 0, 0, 0);
         }
         // lane holds S^T[key = t*64 + kb*32 + kappa(e) + 4fh][q = fr]
         if constexpr (VAR != 2) {
         if ((t + 1) * KT2 > klen) {   // only the last tile can hold keys past klen
+            // a real branch: as a plain `if` the compiler if-converted the masking onto every tile (32 compares +
+            // 32 selects per tile); the empty volatile asm keeps it out of the common path
+            asm volatile("" ::: "memory");
 #pragma unroll
             for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
