@@ -10,5 +10,5 @@ cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/$name" -o run -- \
   python3 "$R/bench.py" --exact-steps 0 --cpu-utts 0 --beam-steps 0 --steps 5 --warmup 2 "${@:3}" > "$R/gpurun_out/$name/bench.log" 2>&1
 rc=$?
-find "$R/gpurun_out/$name" -name "*kernel_trace.csv" -delete
+for f in $(find "$R/gpurun_out/$name" -name "*kernel_trace.csv"); do python3 "$R/tools/trace_busy.py" "$f" > "$R/gpurun_out/$name/busy.txt" 2>&1; rm -f "$f"; done
 exit $rc
