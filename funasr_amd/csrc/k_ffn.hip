@@ -38,6 +38,9 @@ constexpr int OP_TILES = 32;                    // out-projection Wo [512][512]:
 constexpr int QK_TILES = 3 * OP_TILES;          // next layer's Wqkv [1536][512]: three Wo-format passes
 constexpr int OFF_AN = 0, OFF_H = 65536, OFF_RING = 98304, LDS_BYTES = 163840;
 constexpr int OFF_RED = LDS_BYTES - 4096, OFF_STATS = OFF_RED - 512;   // DEC epilogue (above the Y image)
+#ifndef FFN_XB
+#define FFN_XB 2
+#endif
 constexpr int YP = 516;                         // epilogue f32 row pitch (floats)
 
 static_assert(OFF_RING + 4 * TILE == LDS_BYTES, "LDS plan");
@@ -386,13 +389,14 @@ __global__ __launch_bounds__(64 * NW) void ffn_fused_kernel(const float* __restr
         for (int hf = 0; hf < 2; ++hf)
 #pragma unroll
             for (int nb = 0; nb < HB; ++nb) bv[hf][nb] = *(const float4*)(bo + 256 * hf + WR * w + 16 * nb + 4 * g);
+        constexpr int XB = FFN_XB;   // row blocks per load batch
 #pragma unroll
-        for (int mh = 0; mh < 2; ++mh) {
-            float4 xv[2][2][HB];
-            bf16x4 fv[2][2][HB];
+        for (int mh = 0; mh < 4 / XB; ++mh) {
+            float4 xv[XB][2][HB];
+            bf16x4 fv[XB][2][HB];
 #pragma unroll
-            for (int mi = 0; mi < 2; ++mi) {
-                const long long row = min(m0 + 16 * (2 * mh + mi) + r16, (long long)M - 1);
+            for (int mi = 0; mi < XB; ++mi) {
+                const long long row = min(m0 + 16 * (XB * mh + mi) + r16, (long long)M - 1);
 #pragma unroll
                 for (int hf = 0; hf < 2; ++hf)
 #pragma unroll
@@ -403,8 +407,8 @@ __global__ __launch_bounds__(64 * NW) void ffn_fused_kernel(const float* __restr
                     }
             }
 #pragma unroll
-            for (int mi = 0; mi < 2; ++mi) {
-                const int mb = 2 * mh + mi;
+            for (int mi = 0; mi < XB; ++mi) {
+                const int mb = XB * mh + mi;
                 const long long row = min(m0 + 16 * mb + r16, (long long)M - 1);
 #pragma unroll
                 for (int hf = 0; hf < 2; ++hf)
