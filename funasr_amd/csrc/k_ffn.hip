@@ -86,6 +86,10 @@ template <int HB> struct Frag { bf16x8 w[HB]; bf16x8 a[4]; };
 //   then the FFN loop above accumulates W2 . H on top: the epilogue stores x2 = accumulators directly.
 // x1 never leaves the CU (one kernel and one HBM round trip of the residual stream less per layer).
 //
+// QK (MODE 4; diagnostic: instantiated by tools/ffn_bench.hip only, measured slower than the separate GEMM): after the
+// FFN, x2 goes out from the accumulators, LN1_next(x2) becomes the bf16 A image and phase 3 streams the next layer's Wqkv
+// as 96 more Wo-format tiles (Xn receives q|k|v rows of 1536, c1 the biases).
+//
 // DEC (Paraformer decoder feed-forward, sanm/positionwise_feed_forward.py:12-33): y = W2 . LN_F(relu(W1 x' + b1)),
 // x' = LN1(x) (the prologue), w2 without bias. LN_F over the 2048-wide hidden is folded through W2:
 //   y = rstd . (W2g . h - mu . c1) + c2,   W2g = W2 diag(gamma_F) (packed bf16), c1 = rowsum(W2g), c2 = W2 beta_F,
@@ -879,22 +883,6 @@ hipError_t pfm_ffn_fused_op(const bf16* o, const bf16* f, const float* bo, const
     if (((uintptr_t)x | (uintptr_t)xo | (uintptr_t)Wop | (uintptr_t)xn | (uintptr_t)o | (uintptr_t)f | (uintptr_t)bo) % 16)
         return hipErrorInvalidValue;
     ffn_launch_nw<0, 1>(st, M, x, g2, be2, eps, Wop, b1, b2, xo, gn, bn, xn, o, f, bo, nullptr);
-    PFM_LAUNCH_CHECK();
-    return hipSuccess;
-}
-
-// pfm_ffn_fused_op followed by the next encoder layer's QKV projection (ffn_fused_kernel MODE 4, phase 3):
-//   xo = x2 as pfm_ffn_fused_op;  qkv = bf16(LN_next(x2)) Wq^T + bq  (bf16 [M, 1536]; LN_next(x2) stays in LDS)
-// Wop: the 32 Wo tiles, the layer's FFN tiles, then pfm_ffn_pack_o of Wq's three 512-row blocks (96 tiles).
-hipError_t pfm_ffn_fused_op_qkv(const bf16* o, const bf16* f, const float* bo, const float* x, int M, const float* g2,
-                                const float* be2, float eps, const bf16* Wop, const float* b1, const float* b2, float* xo,
-                                const float* gn, const float* bn, const float* bq, bf16* qkv, hipStream_t st) {
-    if (M <= 0) return hipSuccess;
-    if (!o || !f || !bo || !xo || !gn || !bn || !bq || !qkv) return hipErrorInvalidValue;
-    if (((uintptr_t)x | (uintptr_t)xo | (uintptr_t)Wop | (uintptr_t)qkv | (uintptr_t)o | (uintptr_t)f | (uintptr_t)bo |
-         (uintptr_t)bq | (uintptr_t)gn | (uintptr_t)bn) % 16)
-        return hipErrorInvalidValue;
-    ffn_launch_nw<0, 4>(st, M, x, g2, be2, eps, Wop, b1, b2, xo, gn, bn, qkv, o, f, bo, bq);
     PFM_LAUNCH_CHECK();
     return hipSuccess;
 }

@@ -147,9 +147,8 @@ struct PfmKnobs {
                             // 2 = 128-row workgroups (k_ffn2.hip; pays only when M / 128 fills the chip)
     int dec_ffn_kernel;     // PFM_DEC_FFN_KERNEL (default 1): the same choice for the decoder FFN
     int exact_terms;        // PFM_EXACT_TERMS (default 6): products per EXACT-mode split-bf16 GEMM; 3 = bf16x3
-    int ffn_qkv;            // PFM_FFN_QKV: the next layer's QKV projection folded behind the fused FFN (k_ffn.hip)
     unsigned long long sig;
 };
-#define PFM_KNOB_FIELDS 21
+#define PFM_KNOB_FIELDS 20
 const PfmKnobs& pfm_knobs();   // the calling thread's snapshot (refreshed lazily if no entry point did yet)
 void pfm_knobs_refresh();
