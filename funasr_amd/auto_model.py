@@ -320,9 +320,9 @@ class AutoModel:
             world, rank = torch.distributed.get_world_size(), torch.distributed.get_rank()
         dp = world > 1 and len(items) > 1
         mine = list(range(len(items)))
-        if dp:   # longest-first round-robin: balanced padded work per rank
-            from .distributed import item_lengths, length_sorted_shards
-            mine = length_sorted_shards(item_lengths(items), world)[rank]
+        if dp:   # longest-first round-robin: balanced padded work per rank, decided on rank 0
+            from .distributed import shard_items
+            mine = shard_items(items, world, rank)
         results = []
         speech_s, wall_s = 0.0, 0.0
         for beg in range(0, len(mine), batch_size):
@@ -336,14 +336,23 @@ class AutoModel:
                 res = model.inference(**batch, **{k: v for k, v in kwargs.items() if k not in ("key",)})
             t2 = time.perf_counter()
             out, meta = (res[0], res[1]) if isinstance(res, (list, tuple)) and len(res) > 1 else (res, {})
-            if dp and len(out) != len(idx):
-                raise RuntimeError(f"data-parallel inference: {len(out)} results for {len(idx)} inputs")
-            results.extend(zip(idx, out) if dp else out)
+            if dp:   # (input index, result) per result; n-best models give several per input (meta "owner")
+                owner = meta.get("owner")
+                if owner is None:
+                    if len(out) != len(idx):
+                        raise RuntimeError(f"data-parallel inference: {len(out)} results for {len(idx)} inputs")
+                    owner = list(range(len(idx)))
+                results.extend((idx[o], r) for o, r in zip(owner, out))
+            else:
+                results.extend(out)
             bt = meta.get("batch_data_time", -1)
             speech_s += bt if bt > 0 else 0.0
             wall_s += t2 - t1
         self.last_speed = {"rtf": (wall_s / speech_s) if speech_s > 0 else None, "forward_s": wall_s}
-        if dp:   # (input index, result) pairs from every rank -> input order
+        if dp:   # (input index, result) pairs from every rank -> input order (stable: n-best order kept)
             from .distributed import gather_results
-            results = [r for _, r in sorted(gather_results(results), key=lambda p: p[0])]
+            pairs = gather_results(results)
+            if any(not 0 <= i < len(items) for i, _ in pairs):
+                raise RuntimeError("data-parallel inference: gathered a result for an unknown input index")
+            results = [r for _, r in sorted(pairs, key=lambda p: p[0])]
         return results

@@ -441,7 +441,7 @@ hipError_t pfm_ctc_beam(const float* am, int L, const float* x, int T, const int
                         int blank, float* fs, int* is, int* tokens, int Lcap, int* olen, float* oscore,
                         hipStream_t st) {
     if (B <= 0) return hipSuccess;
-    if (K < 1 || K > MAXK || P < 1 || P > MAXP || nbest < 1 || nbest > MAXN || nbest > K || Lcap < 0)
+    if (K < 1 || K > MAXK || P < 1 || P > MAXP || nbest < 1 || nbest > MAXN || Lcap < 0)
         return hipErrorInvalidValue;
     BeamArgs a;
     a.am = am; a.L = L; a.x = x; a.T = T; a.lens = lens; a.ntok = ntok; a.V = V; a.K = K; a.P = P; a.nbest = nbest;

@@ -22,11 +22,18 @@
 // 32x16 weight block, read lane-linearly: conflict-free) and the per-column vectors. Weight bytes per row
 // halve against k_ffn.hip and no activation ever goes through LDS.
 //
-// Weight stream (pfm_ffn2_pack*): [OP: Wo fragments (ob, ks) ob-major] then per hidden chunk c of 32:
-// 32 W1 fragments (k steps of the 512 inputs) then 32 W2 fragments (16 output blocks x 2 k steps).
-// Fragment f feeds MFMA f; its ds_read is issued PD MFMAs ahead. Tile t is published (landed + every wave
-// done with tile t-1) by one barrier placed PD fragments before its first read; that barrier also frees
-// tile t-1's slot, which receives tile t-1+RS at once (RS-1 tiles in flight).
+// Weight stream (pfm_ffn2_pack*), one 1 KiB fragment per MFMA, in MFMA issue order:
+//   [OP: Wo fragments, four output blocks interleaved per k step: (ob 4g, ks) .. (ob 4g+3, ks), then ks+1]
+//   head  P1(0): the 32 W1 fragments of hidden chunk 0 (k steps 0..31, alternating accumulator chains a / b)
+//   body c (c = 0..62), 64 fragments: slots 3m, 3m+1 = P1(c+1) k steps 2m, 2m+1 (chains a, b), slot 3m+2 = P2(c)
+//         output block m, hidden k step 0 (m < 16); slots 48..63 = P2(c) output blocks 0..15, hidden k step 1
+//   tail  P2(63): output blocks 0..15 of k step 0, then of k step 1
+// so phase 1 of chunk c+1 runs under phase 2 of chunk c (a software pipeline), and relu(H + b1) of chunk c+1 -> bf16
+// (phase 2's B operand, double-buffered) is issued
+// between the last 16 MFMAs of the body, in their VALU-issue shadow, instead of in a drain between the phases.
+// Tile t is published (landed + every wave done with tile t-2) by one barrier placed PD fragments before its
+// first read; the DMA of tile t-2+RS into the freed slot is spread over the following 16 MFMAs (one 1 KiB piece
+// per wave every 4 fragments), so no wave issues a burst of LDS-DMA beside an idle matrix pipe.
 #include <stdint.h>
 
 #include "pfm_common.h"
@@ -45,6 +52,10 @@ constexpr int RING = RS * TF * 1024;     // 128 KiB
 constexpr int OPF = 16 * 32;             // phase-0 fragments: Wo = 16 output blocks x 32 k steps
 constexpr int CHF = 64;                  // fragments per hidden chunk: 32 W1 k steps + 16 x 2 W2
 constexpr int PD = 6;                    // fragment reads in flight ahead of their MFMA
+#ifndef FFN2_OPI
+#define FFN2_OPI 4
+#endif
+constexpr int OPI = FFN2_OPI;                   // phase-0 output blocks interleaved per k step (1 = back-to-back chains)
 constexpr int NB = 8;                    // fragment register slots (divides TF, CHF and OPF)
 // per-column vectors staged in LDS behind the ring (float offsets)
 constexpr int V_G = 0, V_B = 512, V_C2 = 1024, V_GN = 1536, V_BN = 2048, V_BO = 2560, V_C1 = 3072, V_B1 = 3584;
@@ -61,8 +72,10 @@ __device__ __forceinline__ f32x16 mfma32(bf16x8 a, bf16x8 b, f32x16 c) {
 // the 16 output blocks (acc[16] = all 256 AGPRs, "a") against phase 1's accumulator (acc1, 16 VGPRs, "v"):
 // with the builtin, acc1 claimed an AGPR block and one output block bounced through scratch every chunk.
 // hipcc pads no hazards around inline asm (cdna_hip_programming.md §5.7 item 2), so the kernel keeps them:
-//   * the first MFMA of a chain takes the inline constant 0 as C; later ones accumulate back to back into the
-//     same registers (XDL D -> the next XDL's whole C: 0 wait states);
+//   * the first MFMA of a chain takes the inline constant 0 as C; later ones accumulate into the same registers,
+//     back to back (XDL D -> the next XDL's whole C: 0 wait states) or with other MFMAs in between (phase 0
+//     interleaves four output blocks, phase 1's two chains alternate; 1, 2 and 4 interleaved blocks measured
+//     bit-identical);
 //   * D -> any other reader: 24 wait states (covers the 16-pass XDL distance of 19; xdl_drain(), fenced by
 //     sched_barrier, before the transition / epilogue VALU reads the accumulators; mfma_v_drain() before the relu
 //     of acc1 — 13 states measured too few: the next-LayerNorm output read stale accumulators);
@@ -128,11 +141,8 @@ __device__ __forceinline__ int acc_col(int reg, int h) { return (reg & 3) + 8 * 
 // VAR (diagnostic builds of tools/ffn2_bench.hip only; the library instantiates VAR 0): 1 = no weight DMA and no
 // DMA waits (stale ring), 2 = no MFMAs, 3 = neither DMA nor barriers (MFMA + fragment reads alone), 5 = the
 // prologue / transition / epilogue alone (no stream: zero chunks, no phase-0 MFMAs), 4 = every tile streamed from
-// the same L2-hot 64 KiB (wrong math; prices L2 misses of the weight stream), 6 = the kernel with s_memtime
-// stamps at its phase boundaries (wave 0 of each block -> ffn2_stamps; cdna_hip_programming.md §7 in-kernel stamps)
-#ifdef PFM_FFN2_STAMPS
-__device__ unsigned long long ffn2_stamps[4096 * 16];
-#endif
+// the same L2-hot 64 KiB (wrong math; prices L2 misses of the weight stream), 6 = the DMA of a tile issued as one
+// burst at its publishing barrier (the pre-round-4 schedule)
 template <int MODE, int VAR = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void ffn2_kernel(
     const float* __restrict__ X, int M, const float* __restrict__ g, const float* __restrict__ be, float eps,
@@ -149,18 +159,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     const long long rg = (long long)blockIdx.x * BM + 32 * w + r;   // this lane's row
     const bool live = rg < M;
     const long long rc = live ? rg : (long long)M - 1;               // clamped for loads
-    auto stamp = [&](int k) {
-#ifdef PFM_FFN2_STAMPS
-        if constexpr (VAR == 6) {
-            unsigned long long t;
-            __builtin_amdgcn_sched_barrier(0);
-            asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-            __builtin_amdgcn_sched_barrier(0);
-            if (tid == 0 && blockIdx.x < 4096) ffn2_stamps[blockIdx.x * 16 + k] = t;
-        }
-#endif
-    };
-    stamp(0);
 
     // ---- per-column vectors -> LDS (before any LDS-DMA is in flight: their waits drain nothing)
     for (int i = tid; i < FD; i += 256) {
@@ -176,17 +174,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 
     // ---- weight ring: tile t -> slot t % RS; this wave moves fragments GW w .. GW w + GW - 1 of each tile
     const bf16* wsrc = Wp + (long long)GW * w * FE + lane * 8;
-    auto issue = [&](int t) {
+    // piece p (0..3) of tile t: one 1 KiB LDS-DMA per wave. The four pieces of a wave are 1 KiB apart in both
+    // spaces, so they share one address and one M0 and differ only in the instruction's immediate offset.
+    static_assert(GW == 4, "LDS-DMA pieces per tile");
+    auto piece = [&](int t, int p) {
         if (t >= NT || VAR == 1 || VAR == 3 || VAR == 5) return;
         const bf16* src = wsrc + (long long)(VAR == 4 ? (t & 3) : t) * TF * FE;   // VAR 4: an L2-hot 64 KiB stream
         unsigned char* dst = smem + (t % RS) * (TF * 1024) + GW * w * 1024;
-        // one address and one M0 per tile: the pieces are 1 KiB apart in both spaces, so they differ only in the
-        // instruction's immediate offset (applied to the global and the LDS address alike)
-        static_assert(GW == 4, "LDS-DMA pieces per tile");
-        __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)dst, 16, 0, 0);
-        __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)dst, 16, 1024, 0);
-        __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)dst, 16, 2048, 0);
-        __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)dst, 16, 3072, 0);
+        if (p == 0) __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)dst, 16, 0, 0);
+        else if (p == 1) __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)dst, 16, 1024, 0);
+        else if (p == 2) __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)dst, 16, 2048, 0);
+        else __builtin_amdgcn_global_load_lds((gbl_void*)src, (lds_void*)dst, 16, 3072, 0);
+    };
+    auto issue = [&](int t) {
+#pragma unroll
+        for (int p = 0; p < GW; ++p) piece(t, p);
     };
     auto bar = [&]() {
         __builtin_amdgcn_sched_barrier(0);
@@ -194,9 +196,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_sched_barrier(0);
     };
-    // publish tile t: it landed (RS-3 newer tiles may stay in flight). The same barrier retires tile t-2: every
-    // wave consumed its last fragment (the MFMA waited for the read) before reaching this barrier, so its slot
-    // takes tile t-2+RS at once — no LDS wait at the barrier, the PD fragment reads of tile t stay in flight.
+    // publish tile t: it landed (RS-3 newer tiles may stay in flight: every piece of tiles up to t-3+RS was issued
+    // before this point). The same barrier retires tile t-2: every wave consumed its last fragment (the MFMA waited
+    // for the read) before reaching this barrier, so its slot takes tile t-2+RS at once — no LDS wait at the
+    // barrier, the PD fragment reads of tile t stay in flight. Piece 0 goes out here, pieces 1..3 four, eight and
+    // twelve fragments later (step_pre), all before the next publishing barrier.
     auto top = [&](int t) {
         if (t >= NT || VAR == 3 || VAR == 5) return;
         if (VAR == 1) {}
@@ -205,7 +209,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         __builtin_amdgcn_sched_barrier(0);
         __builtin_amdgcn_s_barrier();
         __builtin_amdgcn_sched_barrier(0);
-        issue(t - 2 + RS);
+        if constexpr (VAR == 6) issue(t - 2 + RS);
+        else piece(t - 2 + RS, 0);
     };
     // Fragment reads are asm ds_reads with hand-counted waits (the compiler's wait analysis lost count across the
     // asm MFMAs and the loop back edge and drained every read in flight ~10 times per chunk). LDS reads return in
@@ -220,7 +225,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     };
     auto frag_wait = [&](bf16x8& d) { asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(d) : "i"(PD)); };
 #pragma unroll
-    for (int t = 0; t < RS - 1; ++t) issue(t);
+    for (int t = 0; t < RS - 2; ++t) issue(t);
+    if constexpr (VAR == 6) {
+        issue(RS - 2);
+    } else {   // pieces 2, 3 of tile RS-2 go out at positions 2 and 6 of tile 0 (step_pre's spread schedule)
+        piece(RS - 2, 0);
+        piece(RS - 2, 1);
+    }
 
     // ---- prologue: B-operand fragments of this lane's row (phase 0: O rows; else LN(x)) and the accumulator
     bf16x8 act[32];
@@ -369,41 +380,54 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         fence();
     }
 
-    stamp(1);
     // ---- tile 0 landed everywhere (the compiler's wait for the activation loads drained the ring DMA too)
     vm_wait<0>();
     bar();
 #pragma unroll
     for (int f = 0; f < PD; ++f) rd(f, f, wf[f]);
 
-    // one stream step: fragment f (compile-time position fs within the stream's unrolled body): publish the next
-    // tile when its first read is due, read fragment f+PD, wait for fragment f (then its MFMA)
+    // one stream step: fragment f (compile-time position fs within the stream's unrolled section, fs = f mod 16):
+    // publish the next tile when its first read is due, issue this wave's spread DMA pieces of the tile whose slot
+    // that barrier freed, read fragment f+PD, wait for fragment f (then its MFMA)
     // (past the stream's end the read-ahead keeps going: in-bounds reads of stale ring slots nobody consumes,
     // so every step has the same wait)
-    auto step_pre = [&](int f, int fs) {
+    static_assert(TF == 16 && PD == 6, "publish / DMA spread positions");
+    auto step_pre = [&](int f, int fs) __attribute__((always_inline)) {
         __builtin_amdgcn_sched_barrier(0);
-        if (fs % TF == TF - PD) top(f / TF + 1);
+        const int ps = fs % TF;
+        if (ps == TF - PD) top(f / TF + 1);        // position 10: publish tile f/16 + 1 (DMA piece 0 of tile f/16 + 7)
+        else if constexpr (VAR != 6) {
+            if (ps == 14) piece(f / TF - 1 + RS, 1);
+            else if (ps == 2) piece(f / TF - 2 + RS, 2);
+            else if (ps == 6) piece(f / TF - 2 + RS, 3);
+        }
         rd(f + PD, fs + PD, wf[(fs + PD) % NB]);
         frag_wait(wf[fs % NB]);
         __builtin_amdgcn_sched_barrier(0);
     };
 
-    if constexpr (OP) {   // phase 0: Y0^T += Wo . O^T  (fragment 32 ob + ks)
+    if constexpr (OP) {   // phase 0: Y0^T += Wo . O^T; fragment f -> output block 4 (f >> 7) + (f & 3), k step (f >> 2) & 31
 #pragma unroll
-        for (int ob = 0; ob < 16; ++ob)
+        for (int pp = 0; pp < 16 / OPI; ++pp)
 #pragma unroll
-            for (int ks = 0; ks < 32; ++ks) {
-                const int f = 32 * ob + ks;
-                step_pre(f, f);
-                if (VAR == 2 || VAR == 5) asm volatile("" :: "v"(wf[f % NB]));
-                else if (ks == 0) mfma_a0(acc[ob], wf[f % NB], act[0]);
-                else mfma_a(acc[ob], wf[f % NB], act[ks]);
-            }
+            for (int ks = 0; ks < 32; ++ks)
+#pragma unroll
+                for (int e = 0; e < OPI; ++e) {
+                    const int f = 32 * OPI * pp + OPI * ks + e, ob = OPI * pp + e;
+                    step_pre(f, f);
+                    if (VAR == 2 || VAR == 5) asm volatile("" :: "v"(wf[f % NB]));
+                    else if (ks == 0) mfma_a0(acc[ob], wf[f % NB], act[0]);
+                    else mfma_a(acc[ob], wf[f % NB], act[ks]);
+                }
+        // The read-ahead of the stream's first PD fragments is in flight. An asm ds_read's destination counts as
+        // written at the statement, so across the VALU-heavy transition the compiler spilled those registers to
+        // scratch before the data landed (garbage operands for the first phase-1 MFMAs on some waves): retire the
+        // reads here and issue them again after the transition.
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(wf[0]), "+v"(wf[1]), "+v"(wf[2]), "+v"(wf[3]), "+v"(wf[4]),
+                     "+v"(wf[5]), "+v"(wf[6]), "+v"(wf[7]));
         xdl_drain(acc);
-        stamp(2);
         // x1 = ((Y0 + bo) + F) + x (the separate GEMM epilogue's order; layer 0: no x, the decoder: no F)
         add_rows(false, X ? X : bo, X ? FD : 0, X ? 1.f : 0.f, MODE == 1 ? Fr : nullptr, V_BO);
-        stamp(6);
         if constexpr (MODE == 3) {   // the decoder keeps x1 (its FSMN step adds to it)
             if (live) {
 #pragma unroll
@@ -420,7 +444,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         }
         float mean, rstd;
         acc_stats(mean, rstd);
-        stamp(7);
 #pragma unroll
         for (int ob = 0; ob < 16; ++ob) {   // LN2(x1) -> act; accumulators: x1 + b2 (encoder) / 0 (decoder)
             fence();
@@ -430,64 +453,102 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         }
         fence();
     }
+    // the LayerNorm's bf16 operand materialised before the MFMAs (see relu_q: the conversions must not sink into the
+    // MFMA stream past valu_to_mfma's wait states)
+#pragma unroll
+    for (int ks = 0; ks < 32; ++ks) asm volatile("" : "+v"(act[ks]));
+    if constexpr (OP) {   // the stream's first PD fragments again (see the end of phase 0)
+#pragma unroll
+        for (int f = 0; f < PD; ++f) rd(F0 + f, f, wf[f % NB]);
+    }
     valu_to_mfma();
 
-    stamp(3);
+    // ---- the FFN stream (see the header): head P1(0), bodies c = 0..62 (P1(c+1) under P2(c)), tail P2(63)
     float rs = 0.f, rq = 0.f;   // DEC: sum / sum of squares of this lane's bf16 hidden values
-    f32x16 acc1;
-    for (int c = 0; c < (VAR == 5 ? 0 : NCH); ++c) {
-        const int fb = F0 + CHF * c;
-        f32x4 bq[4];   // b1 of the chunk's features 8q + 4h .. +3 (the accumulator's register groups)
+    f32x16 acc1a, acc1b;        // phase 1 of one chunk as two accumulator chains (even / odd k steps)
+    bf16x8 hfa[2], hfb[2];      // phase 2's B operand (hidden k steps 0, 1) of even / odd chunks
+    f32x4 bq[4];                // b1 of the chunk being activated: features 8q + 4h .. +3 (accumulator register groups)
+    auto b1_issue = [&](int c) __attribute__((always_inline)) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) b1_read(bq[q], vec + V_B1 + HC * c + 8 * q + 4 * h);
-        // phase 1: H^T[32 hidden x 32 rows] = W1_c . A^T over the 32 k steps
+    };
+    auto p1 = [&](int f, int fs, int j) __attribute__((always_inline)) {   // phase 1, k step j of a chunk (stream fragment f, position fs)
+        step_pre(f, fs);
+        if (VAR == 2) asm volatile("" :: "v"(wf[fs % NB]));
+        else if (j == 0) mfma32_v0(acc1a, wf[fs % NB], act[0]);
+        else if (j == 1) mfma32_v0(acc1b, wf[fs % NB], act[1]);
+        else if (j & 1) mfma32_v(acc1b, wf[fs % NB], act[j]);
+        else mfma32_v(acc1a, wf[fs % NB], act[j]);
+    };
+    auto p2 = [&](int f, int fs, int k, const bf16x8 (&hb)[2]) __attribute__((always_inline)) {   // phase 2: output block k & 15, hidden k step k >> 4
+        step_pre(f, fs);
+        if (VAR == 2) asm volatile("" :: "v"(wf[fs % NB]), "v"(hb[k >> 4]));
+        else mfma_a(acc[k & 15], wf[fs % NB], hb[k >> 4]);
+    };
+    // phase 1's last MFMAs drained (24 wait states before a VALU reads their results) and b1 landed (at most the PD
+    // younger fragment reads outstanding)
+    auto acc1_ready = [&]() __attribute__((always_inline)) {
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" : "+v"(acc1a), "+v"(acc1b));
+        asm volatile("s_waitcnt lgkmcnt(6)" : "+v"(bq[0]), "+v"(bq[1]), "+v"(bq[2]), "+v"(bq[3]));
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    // relu((H_a + H_b) + b1) -> bf16 for register group q (4 features) into hb; DEC: the hidden's running statistics
+    auto relu_q = [&](int q, bf16x8 (&hb)[2]) __attribute__((always_inline)) {
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int i = 0; i < 32; ++i) {
-            step_pre(fb + i, i);
-            if (VAR == 2) asm volatile("" :: "v"(wf[i % NB]));
-            else if (VAR == 7) mfma_a(acc[i & 15], wf[i % NB], act[i]);   // diagnostic: AGPR chain, wrong math
-            else if (i == 0) mfma32_v0(acc1, wf[0], act[0]);
-            else mfma32_v(acc1, wf[i % NB], act[i]);
-        }
-        mfma_v_drain(acc1);
-        // relu(H + b1) -> bf16 -> phase 2's B operand (registers 8s .. 8s+7 = k step s)
-        bf16x8 hf[2];
-        if constexpr (VAR == 8) {   // diagnostic: no relu / bias / drain between the phases
-            hf[0] = act[0];
-            hf[1] = act[1];
-        } else {
-            static_assert(PD == 6, "b1 wait count");
-            __builtin_amdgcn_sched_barrier(0);
-            asm volatile("s_waitcnt lgkmcnt(6)" : "+v"(bq[0]), "+v"(bq[1]), "+v"(bq[2]), "+v"(bq[3]));
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const float bv4[4] = {bq[q][0], bq[q][1], bq[q][2], bq[q][3]};
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const float bv = bv4[i];
-                    const bf16 v = f2bf(fmaxf(acc1[4 * q + i] + bv, 0.f));
-                    hf[q >> 1][4 * (q & 1) + i] = v;
-                    if constexpr (DEC) {
-                        const float fv = bf2f(v);
-                        rs += fv;
-                        rq += fv * fv;
-                    }
-                }
+        for (int i = 0; i < 4; ++i) {
+            const bf16 v = f2bf(fmaxf((acc1a[4 * q + i] + acc1b[4 * q + i]) + bq[q][i], 0.f));
+            hb[q >> 1][4 * (q & 1) + i] = v;
+            if constexpr (DEC) {
+                const float fv = bf2f(v);
+                rs += fv;
+                rq += fv * fv;
             }
         }
-        valu_to_mfma();
-        // phase 2: Y^T[512 x 32] += W2_c . H^T  (fragment 32 + 2 ob + s)
+        // pin the packed bf16 here: left alone, instruction selection sinks the v_cvt_pk_bf16_f32 next to the operand's
+        // first MFMA, past every scheduling fence, with no wait state between the VALU write and the MFMA read
+        asm volatile("" : "+v"(hb[q >> 1]));
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    // body c: slots 3m, 3m+1 = P1(c+1) k steps 2m, 2m+1; slot 3m+2 = P2(c) block m, hidden k step 0; slots 48..63 =
+    // P2(c) blocks 0..15, hidden k step 1, with relu(c+1) in four groups behind slots 50, 52, 54, 56
+    auto body = [&](int c, const bf16x8 (&hcur)[2], bf16x8 (&hnext)[2]) __attribute__((always_inline)) {
+        const int fb = F0 + 32 + CHF * c;
+        b1_issue(c + 1);
 #pragma unroll
-        for (int j = 0; j < 32; ++j) {
-            step_pre(fb + 32 + j, 32 + j);
-            if (VAR == 2) asm volatile("" :: "v"(wf[(32 + j) % NB]), "v"(hf[j & 1]));
-            else mfma_a(acc[j >> 1], wf[(32 + j) % NB], hf[j & 1]);
+        for (int m = 0; m < 16; ++m) {
+            p1(fb + 3 * m, 3 * m, 2 * m);
+            p1(fb + 3 * m + 1, 3 * m + 1, 2 * m + 1);
+            p2(fb + 3 * m + 2, 3 * m + 2, m, hcur);
         }
+#pragma unroll
+        for (int i = 48; i < 64; ++i) {
+            p2(fb + i, i, 16 + (i - 48), hcur);
+            if (i == 49) acc1_ready();
+            if (i >= 50 && i <= 56 && (i & 1) == 0) relu_q((i - 50) >> 1, hnext);
+        }
+        valu_to_mfma();
+    };
+    if constexpr (VAR != 5) {
+        b1_issue(0);
+#pragma unroll
+        for (int j = 0; j < 32; ++j) p1(F0 + j, j, j);   // head: P1(0)
+        acc1_ready();
+#pragma unroll
+        for (int q = 0; q < 4; ++q) relu_q(q, hfa);
+        valu_to_mfma();
+        for (int c = 0; c < NCH - 2; c += 2) {
+            body(c, hfa, hfb);
+            body(c + 1, hfb, hfa);
+        }
+        body(NCH - 2, hfa, hfb);
+        const int ft = F0 + 32 + CHF * (NCH - 1);
+#pragma unroll
+        for (int k = 0; k < 32; ++k) p2(ft + k, k, k, hfb);   // tail: P2(63)
     }
     xdl_drain(acc);
 
-    stamp(4);
     // ---- epilogue (no DMA in flight: the last tiles were waited for by their tops)
     if constexpr (DEC) {   // y = rstd_h (W2g h - mu_h c1) + c2 ; the hidden's statistics over both lane halves
         rs += __shfl_xor(rs, 32, 64);
@@ -520,11 +581,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         }
         fence();
     }
-    stamp(8);
     if (Xn) {
         float mean, rstd;
         acc_stats(mean, rstd);
-        stamp(9);
         if (live) {
 #pragma unroll
             for (int ob = 0; ob < 16; ++ob) {
@@ -543,44 +602,60 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
             fence();
         }
     }
-    stamp(5);
 }
 
 // ---- packing: one thread per 16-B piece (fragment f, lane l = 32 hh + m) in stream order
 // within-block feature of element j of lane half hh in k step s (the accumulator's register order)
 __device__ __forceinline__ int perm_k(int s, int hh, int j) { return 16 * s + 8 * (j >> 2) + 4 * hh + (j & 3); }
 
-// hidden chunk c: fragments 0..31 = W1 rows [32c, 32c+32) x k step ks (permuted k of the 512 inputs),
-// fragments 32 + 2 ob + s = W2 rows [32 ob, 32 ob + 32) x k step s of the chunk's 32 hidden (permuted).
-// DEC: the W2 fragments hold bf16(W2 gamma_F) from the f32 W2 (W2b unused).
+// FFN stream position q (0..4095, see the header) -> hidden chunk c, W1 (P1) or W2 (P2) fragment, index j:
+// P1 j = W1 rows [32c, 32c+32) x k step j of the 512 inputs (permuted k); P2 j = W2 rows [32 (j & 15), +32) x hidden
+// k step j >> 4 of the chunk's 32 hidden (permuted). DEC: the W2 fragments hold bf16(W2 gamma_F) from the f32 W2.
+__device__ __forceinline__ void ffn2_stream_frag(int q, int& c, bool& w1, int& j) {
+    constexpr int TAIL = 32 + (NCH - 1) * CHF;
+    if (q < 32) { c = 0; w1 = true; j = q; return; }
+    if (q >= TAIL) { c = NCH - 1; w1 = false; j = q - TAIL; return; }
+    const int b = (q - 32) / CHF, i = (q - 32) % CHF;
+    if (i < 48) {
+        const int m = i / 3, rr = i % 3;
+        if (rr < 2) { c = b + 1; w1 = true; j = 2 * m + rr; }
+        else { c = b; w1 = false; j = m; }
+    } else {
+        c = b; w1 = false; j = 16 + (i - 48);
+    }
+}
+
 __global__ __launch_bounds__(256) void ffn2_pack_kernel(const bf16* __restrict__ W1, const bf16* __restrict__ W2b,
                                                         const float* __restrict__ W2f, const float* __restrict__ gF,
                                                         bf16* __restrict__ Wp) {
     const int gid = blockIdx.x * 256 + threadIdx.x;   // < NCH * CHF * 64
     const int f = gid >> 6, l = gid & 63, m = l & 31, hh = l >> 5;
-    const int c = f / CHF, i = f % CHF;
+    int c, j;
+    bool w1;
+    ffn2_stream_frag(f, c, w1, j);
     bf16x8 o;
-    if (i < 32) {
-        const int kb = i >> 1, s = i & 1;
+    if (w1) {
+        const int kb = j >> 1, s = j & 1;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) o[j] = W1[(long long)(HC * c + m) * FD + 32 * kb + perm_k(s, hh, j)];
+        for (int e = 0; e < 8; ++e) o[e] = W1[(long long)(HC * c + m) * FD + 32 * kb + perm_k(s, hh, e)];
     } else {
-        const int ob = (i - 32) >> 1, s = (i - 32) & 1;
+        const int ob = j & 15, s = j >> 4;
         const long long rowb = (long long)(32 * ob + m) * FF + HC * c;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const int k = perm_k(s, hh, j);
-            o[j] = W2f ? f2bf(W2f[rowb + k] * gF[HC * c + k]) : W2b[rowb + k];
+        for (int e = 0; e < 8; ++e) {
+            const int k = perm_k(s, hh, e);
+            o[e] = W2f ? f2bf(W2f[rowb + k] * gF[HC * c + k]) : W2b[rowb + k];
         }
     }
     *(bf16x8*)(Wp + (long long)gid * 8) = o;
 }
 
-// Wo [512 out][512 in] -> fragments (ob, ks) ob-major, natural k (the O rows are loaded in natural order)
+// Wo [512 out][512 in] -> phase-0 fragments f = 128 p + 4 ks + e: output block 4p + e, k step ks (natural k: the O rows
+// are loaded in natural order)
 __global__ __launch_bounds__(256) void ffn2_pack_o_kernel(const bf16* __restrict__ Wo, bf16* __restrict__ Wp) {
     const int gid = blockIdx.x * 256 + threadIdx.x;   // < OPF * 64
     const int f = gid >> 6, l = gid & 63, m = l & 31, hh = l >> 5;
-    const int ob = f >> 5, ks = f & 31;
+    const int ob = OPI * (f / (32 * OPI)) + f % OPI, ks = (f / OPI) % 32;
     *(bf16x8*)(Wp + (long long)gid * 8) = *(const bf16x8*)(Wo + (long long)(32 * ob + m) * FD + 16 * ks + 8 * hh);
 }
 

@@ -1556,7 +1556,8 @@ int pfm_run(pfm_handle* h, void* stream, int mode, const float* feats, const int
 
 int pfm_run_beam(pfm_handle* h, void* stream, int mode, const float* feats, const int32_t* lens, int B, int T,
                  int beam, float ctc_weight, float penalty, int nbest, int end_detect, int sos, int eos, int blank,
-                 int32_t* tokens, int L_cap, int32_t* ntok_out, float* scores_out) {
+                 int32_t* tokens, int L_cap, int32_t* ntok_out, float* scores_out, float* alphas_out,
+                 float* peaks_out) {
     pfm_knobs_refresh();
     if (!h || !feats || !lens || !tokens || !ntok_out || !scores_out) return fail(PFM_E_ARG, "pfm_run_beam: null argument");
     if (h->cfg.arch != PFM_ARCH_PARAFORMER || !h->cfg.ctc_head)
@@ -1566,8 +1567,8 @@ int pfm_run_beam(pfm_handle* h, void* stream, int mode, const float* feats, cons
     const int pre = (int)(1.5 * beam), P = pre < V ? pre : V;
     if (sos < 0 || sos >= V || eos < 0 || eos >= V || blank < 0 || blank >= V)
         return fail(PFM_E_ARG, "pfm_run_beam: sos / eos / blank outside the vocabulary");
-    if (beam < 1 || beam > 16 || nbest < 1 || nbest > beam || P > 64 || !(ctc_weight > 1e-5f) || L_cap < 0)
-        return fail(PFM_E_ARG, "pfm_run_beam: need 1 <= nbest <= beam <= 16, ctc_weight > 1e-5, <= 64 candidates");
+    if (beam < 1 || beam > 16 || nbest < 1 || nbest > 16 || P > 64 || !(ctc_weight > 1e-5f) || L_cap < 0)
+        return fail(PFM_E_ARG, "pfm_run_beam: need 1 <= beam <= 16, 1 <= nbest <= 16, ctc_weight > 1e-5, <= 64 candidates");
     HIP_TRY(hipSetDevice(h->device));
     hipStream_t st = (hipStream_t)stream;
     int32_t* ntok_dev = nullptr;
@@ -1576,7 +1577,7 @@ int pfm_run_beam(pfm_handle* h, void* stream, int mode, const float* feats, cons
         h->last_L = 0;
         HIP_TRY(h->beam_is.ensure((size_t)B * sizeof(int32_t)));
         ntok_dev = h->beam_is.as<int32_t>();
-        const int rc = pfm_run(h, stream, mode, feats, lens, B, T, ntok_dev, 0, ntok_dev, nullptr, nullptr, nullptr);
+        const int rc = pfm_run(h, stream, mode, feats, lens, B, T, ntok_dev, 0, ntok_dev, nullptr, alphas_out, peaks_out);
         h->want_logits = false;
         if (rc) return rc;
     }
@@ -2028,8 +2029,8 @@ int pfm_op_ctc_beam(void* stream, const float* am, int L, const float* x, int T,
     const int pre = (int)(1.5 * beam), P = pre < V ? pre : V;
     if (sos < 0 || sos >= V || eos < 0 || eos >= V || blank < 0 || blank >= V)
         return fail(PFM_E_ARG, "pfm_op_ctc_beam: sos / eos / blank outside the vocabulary");
-    if (beam < 1 || beam > 16 || nbest < 1 || nbest > beam || P > 64 || L_cap < 0)
-        return fail(PFM_E_ARG, "pfm_op_ctc_beam: need 1 <= nbest <= beam <= 16, <= 64 candidates");
+    if (beam < 1 || beam > 16 || nbest < 1 || nbest > 16 || P > 64 || L_cap < 0)
+        return fail(PFM_E_ARG, "pfm_op_ctc_beam: need 1 <= beam <= 16, 1 <= nbest <= 16, <= 64 candidates");
     if (B == 0) return PFM_OK;
     const hipStream_t st = (hipStream_t)stream;
     OpScratch sc;

@@ -33,6 +33,19 @@ def length_sorted_shards(lengths: Sequence[int], world: int) -> List[List[int]]:
     return [order[r::world].tolist() for r in range(world)]
 
 
+def shard_items(items: Sequence, world: int, rank: int) -> List[int]:
+    """This rank's input indices: rank 0 measures the items (item_lengths) and deals them with
+    length_sorted_shards; the deal is broadcast, so every rank shards identically even where its own view of
+    the inputs differs (node-local paths, a file still being written)."""
+    import torch.distributed as dist
+    plan = [length_sorted_shards(item_lengths(items), world) if dist.get_rank() == 0 else None]
+    dist.broadcast_object_list(plan, src=0)
+    shards = plan[0]
+    if sorted(i for s in shards for i in s) != list(range(len(items))):
+        raise RuntimeError(f"data-parallel shard plan does not cover the {len(items)} inputs of rank {rank}")
+    return shards[rank]
+
+
 def item_lengths(items: Sequence) -> List[int]:
     """Cheap per-item work estimate for sharding without decoding anything: samples / frames of
     in-memory arrays, the byte size of files and byte strings, 0 when unknown."""

@@ -67,6 +67,15 @@ class HipModel(torch.nn.Module):
         want = {k: s for k, s, _ in param_layout(self.cfg)}
         missing = [k for k in want if k not in state_dict]
         unexpected = [k for k in state_dict if k not in want]
+        if "ctc.ctc_lo.weight" in unexpected and getattr(self.cfg, "ctc_weight", None) == 0.0:
+            # the reference builds ctc.ctc_lo whenever model_conf.ctc_weight > 0 (its constructor default is 0.5,
+            # paraformer/model.py:51, 95-100); a config that leaves ctc_weight out would drop the head here
+            msg = (f"{type(self).__name__}: the checkpoint carries a CTC head (ctc.ctc_lo) but the model was built "
+                   "with ctc_weight 0.0; set model_conf.ctc_weight > 0 (the reference default is 0.5) to keep it")
+            if strict:
+                raise RuntimeError(msg)
+            import warnings
+            warnings.warn(msg)
         if strict and (missing or unexpected):
             raise RuntimeError(f"{type(self).__name__}.load_state_dict: missing {missing[:5]} "
                                f"unexpected {unexpected[:5]}")
@@ -156,6 +165,10 @@ class Paraformer(HipModel):
         if kwargs.get("lm_weight", 0.0) > 1e-5 and kwargs.get("lm_file") is not None:
             raise NotImplementedError("LM shallow fusion (lm_file) is not on the HIP Paraformer path")
         use_ctc = kwargs.get("decoding_ctc_weight", 0.0) > 1e-5 and self.cfg.ctc_weight > 0.0
+        if kwargs.get("decoding_ctc_weight", 0.0) > 1e-5 and not use_ctc:
+            import warnings   # the reference decodes greedily too when self.ctc is None (model.py:443-458)
+            warnings.warn("decoding_ctc_weight > 0 on a Paraformer without a CTC head (ctc_weight 0.0): greedy "
+                          "decoding, as the reference does when the model has no ctc module")
         eng = self.engine()
         mode = kwargs.get("mode", self.mode)
         meta = {}
@@ -163,14 +176,16 @@ class Paraformer(HipModel):
         pred_ts = bool(kwargs.get("pred_timestamp", False))
         if use_ctc:   # joint decoder + CTC prefix beam search on the device (pfm_run_beam)
             nbest = int(kwargs.get("nbest", 1))
-            rb = eng.run_beam(speech, lens, mode=mode, beam=int(kwargs.get("beam_size", 2)),
-                              ctc_weight=float(kwargs["decoding_ctc_weight"]), penalty=float(kwargs.get("penalty", 0.0)),
-                              nbest=nbest, end_detect=float(kwargs.get("maxlenratio", 0.0)) == 0.0)
-            btok, bn = rb["tokens"].cpu().numpy(), rb["ntok"].cpu().numpy()
+            # the kernel's n-best list holds up to 16 ended hypotheses (sorted(ended_hyps)[:nbest], model.py:553)
+            if not 1 <= nbest <= 16:
+                raise PfmError(f"nbest {nbest}: the HIP beam search keeps at most 16 ended hypotheses")
+            r = eng.run_beam(speech, lens, mode=mode, beam=int(kwargs.get("beam_size", 2)),
+                             ctc_weight=float(kwargs["decoding_ctc_weight"]), penalty=float(kwargs.get("penalty", 0.0)),
+                             nbest=nbest, end_detect=float(kwargs.get("maxlenratio", 0.0)) == 0.0,
+                             want_alphas=pred_ts)   # with timestamps: the CIF outputs of the same encoder pass
+            btok, bn = r["tokens"].cpu().numpy(), r["ntok"].cpu().numpy()
             hyps = [[btok[i, k, :bn[i, k]].tolist() for k in range(nbest) if bn[i, k] >= 0]
                     for i in range(btok.shape[0])]
-            if pred_ts:   # the CIF outputs of the same encoder (paraformer/model.py:572-582)
-                r = eng.run(speech, lens, mode=mode, want_alphas=True)
         else:
             r = eng.run(speech, lens, mode=mode, want_alphas=pred_ts)
             toks = r["tokens"].cpu().numpy()           # one device->host copy for the whole batch
@@ -185,8 +200,10 @@ class Paraformer(HipModel):
         b = len(hyps)
         key = self._keys(key, b)
         results = []
+        owner = []   # batch index of each result (n-best gives several per utterance, an unfinished search none)
         for i in range(b):
             for ids in hyps[i]:   # n-best hypotheses of utterance i, best first (model.py:553)
+                owner.append(i)
                 if tokenizer is not None:
                     # model.py:567-586: text = tokens2text(ids2tokens(ids)); sentence_postprocess replaces it
                     # only for tokenizers without a `bpemodel` (a SentencepiecesTokenizer keeps tokens2text)
@@ -208,4 +225,5 @@ class Paraformer(HipModel):
                         results.append({"key": key[i], "text": text})
                 else:
                     results.append({"key": key[i], "token_int": ids})
+        meta["owner"] = owner
         return results, meta

@@ -101,7 +101,7 @@ def load_library(path: Optional[str] = None) -> ctypes.CDLL:
     lib.pfm_reserve.argtypes = [vp, i32, i32]
     lib.pfm_run.argtypes = [vp, vp, i32, f32p, i32p, i32, i32, i32p, i32, i32p, f32p, f32p, f32p]
     lib.pfm_run_beam.argtypes = [vp, vp, i32, f32p, i32p, i32, i32, i32, ctypes.c_float, ctypes.c_float, i32, i32,
-                                 i32, i32, i32, i32p, i32, i32p, f32p]
+                                 i32, i32, i32, i32p, i32, i32p, f32p, f32p, f32p]
     lib.pfm_fbank.argtypes = [vp, vp, f32p, i32p, i32, i32, f32p, f32p, i32, i32p]
     lib.pfm_lfr_frames.argtypes = [i32]
     lib.pfm_last_error.argtypes = []
@@ -284,9 +284,10 @@ class PfmEngine:
         return dict(tokens=tokens, ntok=ntok, enc=enc, alphas=alphas, peaks=peaks)
 
     def run_beam(self, feats, lens, mode="exact", beam=2, ctc_weight=0.5, penalty=0.0, nbest=1, end_detect=True,
-                 L_cap: Optional[int] = None):
+                 L_cap: Optional[int] = None, want_alphas: bool = False):
         """Joint decoder + CTC prefix beam search (pfm_run_beam; Paraformer with a CTC head):
-        feats [B,T,in], lens [B] -> dict(tokens [B,nbest,L_cap] int32, ntok [B,nbest] (-1 = none), scores)."""
+        feats [B,T,in], lens [B] -> dict(tokens [B,nbest,L_cap] int32, ntok [B,nbest] (-1 = none), scores, and with
+        want_alphas the CIF alphas / peaks [B,T+1] of the same encoder pass)."""
         torch = self.torch
         dev = torch.device("cuda", self.device)
         feats = feats.to(device=dev, dtype=torch.float32).contiguous()
@@ -298,13 +299,15 @@ class PfmEngine:
         tokens = torch.empty((B, nbest, max(L_cap, 1)), dtype=torch.int32, device=dev)
         ntok = torch.empty((B, nbest), dtype=torch.int32, device=dev)
         scores = torch.empty((B, nbest), dtype=torch.float32, device=dev)
+        alphas = torch.empty((B, T + 1), dtype=torch.float32, device=dev) if want_alphas else None
+        peaks = torch.empty((B, T + 1), dtype=torch.float32, device=dev) if want_alphas else None
         m = MODES[mode] if isinstance(mode, str) else int(mode)
         c = self.cfg
         check(self.lib.pfm_run_beam(self.h, _stream_ptr(torch, dev), m, _ptr(feats), _ptr(lens), B, T, int(beam),
                                     float(ctc_weight), float(penalty), int(nbest), 1 if end_detect else 0,
                                     int(c.sos), int(c.eos), int(c.blank_id), _ptr(tokens), L_cap, _ptr(ntok),
-                                    _ptr(scores)), "pfm_run_beam")
-        return dict(tokens=tokens, ntok=ntok, scores=scores)
+                                    _ptr(scores), _ptr(alphas), _ptr(peaks)), "pfm_run_beam")
+        return dict(tokens=tokens, ntok=ntok, scores=scores, alphas=alphas, peaks=peaks)
 
     def run_punc(self, ids, lens, mode="exact", want_logits=False):
         """CT-Transformer: word ids [B,T] int32 cuda, lens [B] -> dict(punc [B,T] int32 (-1 beyond lens),

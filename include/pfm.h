@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define PFM_ABI_VERSION 3
+#define PFM_ABI_VERSION 4
 
 enum pfm_status {
     PFM_OK = 0,
@@ -140,16 +140,19 @@ int pfm_run(pfm_handle* h, void* stream, int mode, const float* feats, const int
  * int(1.5 beam) candidates, end detection (metrics/common.py:18-46) when end_detect != 0
  * (maxlenratio == 0). Handle: Paraformer with ctc_head = 1. Runs the encoder / CIF / decoder of pfm_run,
  * then the CTC head, both log_softmaxes and the search itself on the device (one workgroup per utterance).
- *   beam 1..16, nbest 1..beam, ctc_weight > 1e-5 (weights["ctc"]), penalty (weights["length_bonus"]),
+ *   beam 1..16, nbest 1..16 (the reference returns sorted(ended_hyps)[:nbest], which may hold more than beam
+ *   hypotheses), ctc_weight > 1e-5 (weights["ctc"]), penalty (weights["length_bonus"]),
  *   sos / eos / blank ids of the model (blank is also the CTC blank)
  *   tokens    [B, nbest, L_cap] int32 out: token ids of the n-th best ended hypothesis, sos / eos / blank
  *             removed (model.py:553-565)
  *   ntok_out  [B, nbest] int32 out: number of those ids (may exceed L_cap: truncated), -1 = no hypothesis
  *   scores_out[B, nbest] f32 out: the hypothesis score
+ * Optional outputs (NULL to skip; ABI 4): alphas / peaks [B, T+1] f32, the CIF weights and fire values of the same
+ * encoder pass (pfm_run's; what pred_timestamp needs, model.py:572-582).
  * The call synchronises `stream`. */
 int pfm_run_beam(pfm_handle* h, void* stream, int mode, const float* feats, const int32_t* lens, int B, int T,
                  int beam, float ctc_weight, float penalty, int nbest, int end_detect, int sos, int eos, int blank,
-                 int32_t* tokens, int L_cap, int32_t* ntok_out, float* scores_out);
+                 int32_t* tokens, int L_cap, int32_t* ntok_out, float* scores_out, float* alphas, float* peaks);
 
 /* SenseVoiceSmall inference on an fbank batch — SenseVoiceSmall.inference for
  * data_type="fbank" (sense_voice/model.py:809-906) up to token_int: query rows, encoder,

@@ -179,28 +179,43 @@ def save_headline():
               "margins < 1e-3:", int((mg < 1e-3).sum()))
 
 
-BEAM_CASES = {   # name: (large?, weight seed, fbank seed, B, T, lens, decoding_ctc_weight, beam_size, penalty, nbest)
+BEAM_CASES = {   # name: (large?, weight seed, fbank seed, B, T, lens, decoding_ctc_weight, beam_size, penalty, nbest
+    #        [, + on the decoder output bias of eos: hypotheses end at many positions])
     "beam_tiny": (False, 4, 21, 3, 40, [40, 27, 9], 0.3, 3, 0.0, 2),
     "beam_tiny_pen": (False, 4, 22, 2, 40, [33, 40], 0.5, 4, 0.8, 3),
     "beam_large": (True, 0, 23, 2, 500, [500, 431], 0.3, 4, 0.0, 2),
+    # nbest > beam: sorted(ended_hyps)[:nbest] collects ended hypotheses of every position (more than beam)
+    "beam_tiny_nb": (False, 4, 24, 3, 40, [40, 31, 22], 0.01, 2, 0.0, 5, 8.0),
 }
 
 
-def save_beam():
+def save_beam_nb():
+    save_beam(["beam_tiny_nb"])
+
+
+def save_beam(only=None):
     """Paraformer with a CTC head (model_conf ctc_weight 0.3) decoded by the reference's joint decoder + CTC prefix
     beam search (Paraformer.inference with decoding_ctc_weight > 0: BeamSearchPara + CTCPrefixScorer +
     LengthBonus, paraformer/model.py:396-441, 530-565). Stores the n-best yseqs (sos ... eos) and scores from
     beam_search() itself and the token_int result dicts of inference()."""
     import dataclasses
     models = {}
-    for name, (large, wseed, fseed, B, T, ln, wctc, beam, pen, nbest) in BEAM_CASES.items():
+    for name, case in BEAM_CASES.items():
+        if only is not None and name not in only:
+            continue
+        large, wseed, fseed, B, T, ln, wctc, beam, pen, nbest = case[:10]
+        eos_boost = case[10] if len(case) > 10 else 0.0
         cfg = dataclasses.replace(paraformer_large() if large else paraformer_tiny(), ctc_weight=0.3)
         kw = cfg.reference_kwargs()
         cls = tables.model_classes["Paraformer"]
         m = cls(encoder=kw["encoder"], encoder_conf=kw["encoder_conf"], decoder=kw["decoder"],
                 decoder_conf=kw["decoder_conf"], predictor=kw["predictor"], predictor_conf=kw["predictor_conf"],
                 input_size=cfg.input_size, vocab_size=cfg.vocab_size, ctc_weight=0.3, predictor_bias=1)
-        m.load_state_dict({k: torch.from_numpy(v) for k, v in make_weights(cfg, seed=wseed).items()}, strict=True)
+        w = make_weights(cfg, seed=wseed)
+        if eos_boost:
+            w["decoder.output_layer.bias"] = w["decoder.output_layer.bias"].copy()
+            w["decoder.output_layer.bias"][cfg.eos] += eos_boost
+        m.load_state_dict({k: torch.from_numpy(v) for k, v in w.items()}, strict=True)
         m.eval()
         feats, lens = fbank_input(seed=fseed, B=B, T=T, lens=ln)
         x = torch.from_numpy(feats)
@@ -226,6 +241,7 @@ def save_beam():
         rflat, roff = pack_tokens([r["token_int"] for r in res])
         np.savez_compressed(f"{HERE}/{name}.npz", large=large, wseed=wseed, seed=fseed, B=B, T=T, lens=lens,
                             decoding_ctc_weight=wctc, beam_size=beam, penalty=pen, nbest=nbest, ntok=ntok.numpy(),
+                            eos_boost=eos_boost,
                             enc_lens=olens.numpy(), yseq=flat, yseq_off=off, scores=np.array(scores, np.float32),
                             owner=np.array(owner, np.int32), result_tokens=rflat, result_off=roff)
         print(name, "ntok", ntok.tolist(), "hyps", len(yseq), "scores", [round(v, 3) for v in scores])

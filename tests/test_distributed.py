@@ -127,3 +127,62 @@ def test_gloo_world2_automodel_inference_length_sorted_order_restored():
         per_rank = [sum(r["n"] for r in res if r["rank"] == k) for k in range(world)]
         assert abs(per_rank[0] - per_rank[1]) <= max(lens)
         assert {r["rank"] for r in res if r["n"] == 500} == {0, 1}   # the two longest go to different ranks
+
+
+class _NbestModel(_EchoModel):
+    """An n-best model: two results per input (best first), none for a 17-sample input (a search that ended no
+    hypothesis), with meta["owner"] naming each result's batch index (what Paraformer.inference returns)."""
+
+    def inference(self, data_in, key=None, **kw):
+        rank = dist.get_rank() if dist.is_initialized() else 0
+        res, owner = [], []
+        for i, (k, x) in enumerate(zip(key, data_in)):
+            if len(x) == 17:
+                continue
+            for n in range(2):
+                res.append({"key": k, "n": int(len(x)), "hyp": n, "rank": rank})
+                owner.append(i)
+        return res, {"owner": owner}
+
+
+def _nbest_worker(rank, world, port, items, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from funasr_amd.auto_model import AutoModel
+        am = AutoModel.__new__(AutoModel)
+        am.kwargs, am.model = {"batch_size": 3}, _NbestModel()
+        # rank 1 sees every input as empty: the shard plan must still be rank 0's (broadcast), not its own
+        mine = items if rank == 0 else [np.zeros(0, np.float32) for _ in items]
+        from funasr_amd.distributed import shard_items
+        q.put((rank, shard_items(mine, world, rank), am.inference(items, key=None)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world2_automodel_nbest_grouped_by_input():
+    """AutoModel.inference under world 2 with an n-best model: results are grouped by the input they belong to
+    (meta owner), inputs without a hypothesis contribute none, n-best order inside an input is kept; equal to
+    the one-process run. The shard plan is rank 0's on every rank."""
+    from funasr_amd.auto_model import AutoModel
+    from funasr_amd.distributed import item_lengths
+    lens = [500, 83, 17, 431, 500, 120, 300, 222, 260]
+    items = [np.zeros(n, np.float32) for n in lens]
+    single = AutoModel.__new__(AutoModel)
+    single.kwargs, single.model = {"batch_size": 3}, _NbestModel()
+    want = [{k: v for k, v in r.items() if k not in ("rank", "key")} for r in single.inference(items)]
+    assert len(want) == 2 * (len(lens) - 1)
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_nbest_worker, args=(r, world, port, items, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    plan = length_sorted_shards(item_lengths(items), world)
+    for rank, shard, res in out:
+        assert shard == plan[rank]
+        assert [{k: v for k, v in r.items() if k not in ("rank", "key")} for r in res] == want

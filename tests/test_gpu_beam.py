@@ -39,11 +39,21 @@ def _strip(y, cfg):
     return [t for t in y[1:-1] if t not in (cfg.eos, cfg.sos, cfg.blank_id)]
 
 
+def _weights(g, cfg):
+    """The golden's weights: seeded, plus the eos boost on the decoder output bias of beam_tiny_nb."""
+    w = make_weights(cfg, int(g["wseed"]))
+    boost = float(g["eos_boost"]) if "eos_boost" in g else 0.0
+    if boost:
+        w["decoder.output_layer.bias"] = w["decoder.output_layer.bias"].copy()
+        w["decoder.output_layer.bias"][cfg.eos] += boost
+    return w
+
+
 def _engine(g):
     from funasr_amd.runtime import PfmEngine
     cfg = _cfg(g)
     e = PfmEngine(cfg, 0)
-    e.load_state_dict(make_weights(cfg, int(g["wseed"])))
+    e.load_state_dict(_weights(g, cfg))
     return e, cfg
 
 
@@ -56,7 +66,9 @@ def _run(e, g, mode="exact"):
     return r["tokens"].cpu().numpy(), r["ntok"].cpu().numpy(), r["scores"].cpu().numpy()
 
 
-@pytest.mark.parametrize("name", ["beam_tiny", "beam_tiny_pen"])
+# beam_tiny_nb: beam 2, nbest 5, decoding_ctc_weight 0.01 and an eos-biased decoder, so hypotheses end at many
+# positions and the reference's sorted(ended_hyps)[:nbest] holds five per utterance (more than the beam)
+@pytest.mark.parametrize("name", ["beam_tiny", "beam_tiny_pen", "beam_tiny_nb"])
 def test_beam_exact_vs_reference(name):
     g = np.load(f"{GOLD}/{name}.npz")
     e, cfg = _engine(g)
@@ -82,7 +94,7 @@ def _oracle_logprobs(g, cfg):
     the oracle search on them to the reference's n-best)."""
     from oracle.beam_ref import ctc_log_probs
     from oracle.paraformer_ref import paraformer_infer
-    w = make_weights(cfg, int(g["wseed"]))
+    w = _weights(g, cfg)
     feats, lens = fbank_input(int(g["seed"]), int(g["B"]), int(g["T"]), g["lens"])
     r = paraformer_infer(feats, lens, w, cfg, keep_logits=True)
     logp = torch.log_softmax(r["logits"], dim=-1)
@@ -94,7 +106,7 @@ def _oracle_logprobs(g, cfg):
     return logp, x, torch.as_tensor(r["enc_lens"]).int(), torch.as_tensor(r["ntok"]).int()
 
 
-@pytest.mark.parametrize("name", ["beam_tiny", "beam_tiny_pen"])
+@pytest.mark.parametrize("name", ["beam_tiny", "beam_tiny_pen", "beam_tiny_nb"])
 def test_beam_kernel_on_reference_logprobs(name):
     """The search kernel alone (pfm_op_ctc_beam) on the oracle model's log-probs: the reference's n-best token
     sequences and scores (1e-5 relative) — separates the search from the model's arithmetic."""
@@ -151,12 +163,12 @@ def test_automodel_beam_matches_reference_inference():
     """Paraformer.inference(decoding_ctc_weight=..., beam_size, penalty, nbest) -> the reference inference()
     result dicts (one {"key", "token_int"} per n-best hypothesis, utterance order)."""
     from funasr_amd.model import Paraformer
-    for name in ("beam_tiny", "beam_tiny_pen"):
+    for name in ("beam_tiny", "beam_tiny_pen", "beam_tiny_nb"):
         g = np.load(f"{GOLD}/{name}.npz")
         cfg = _cfg(g)
         kw = cfg.reference_kwargs()
         m = Paraformer(**kw, ctc_weight=0.3, predictor_bias=1, mode="exact").cuda()
-        m.load_state_dict(make_weights(cfg, int(g["wseed"])))
+        m.load_state_dict(_weights(g, cfg))
         feats, lens = fbank_input(int(g["seed"]), int(g["B"]), int(g["T"]), g["lens"])
         res, _ = m.inference(torch.from_numpy(feats), data_lengths=torch.from_numpy(lens)[:, None],
                              key=[f"utt{i}" for i in range(int(g["B"]))], data_type="fbank",
@@ -174,7 +186,9 @@ def test_beam_rejects_bad_arguments():
     e, _ = _engine(g)
     x, l = torch.zeros(1, 10, 560).cuda(), torch.tensor([10], dtype=torch.int32).cuda()
     with pytest.raises(PfmError):
-        e.run_beam(x, l, beam=3, nbest=4)
+        e.run_beam(x, l, beam=3, nbest=17)   # the kernel keeps at most 16 ended hypotheses (nbest > beam is legal)
+    with pytest.raises(PfmError):
+        e.run_beam(x, l, beam=17)
     with pytest.raises(PfmError):
         e.run_beam(x, l, beam=3, ctc_weight=0.0)
     plain = PfmEngine(paraformer_tiny(), 0)   # no CTC head

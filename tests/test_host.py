@@ -133,6 +133,24 @@ def test_model_state_dict_contract():
         m.load_state_dict({"encoder.after_norm.weight": torch.zeros(3)}, strict=True)
 
 
+def test_ctc_head_checkpoint_needs_ctc_weight():
+    """A checkpoint with ctc.ctc_lo into a model built with ctc_weight 0.0 (a config.yaml that leaves it out;
+    the reference's constructor default is 0.5 and keeps the head): strict load names the fix, a non-strict load
+    warns; built with ctc_weight > 0 the same checkpoint loads strictly."""
+    import dataclasses
+    from funasr_amd.model import Paraformer
+    cfg = dataclasses.replace(paraformer_tiny(), ctc_weight=0.3)
+    sd = {k: torch.from_numpy(v) for k, v in make_weights(cfg).items()}
+    assert "ctc.ctc_lo.weight" in sd
+    m0 = Paraformer(**paraformer_tiny().reference_kwargs(), ctc_weight=0.0)
+    with pytest.raises(RuntimeError, match="ctc_weight"):
+        m0.load_state_dict(sd, strict=True)
+    with pytest.warns(UserWarning, match="ctc_weight"):
+        m0.load_state_dict(sd, strict=False)
+    m1 = Paraformer(**paraformer_tiny().reference_kwargs(), ctc_weight=0.3)
+    m1.load_state_dict(sd, strict=True)
+
+
 @pytest.mark.skipif(torch.cuda.is_available(), reason="checks the no-GPU behaviour")
 def test_no_gpu_fails_loudly():
     from funasr_amd.auto_model import AutoModel

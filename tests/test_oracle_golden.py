@@ -363,7 +363,7 @@ def _golden_hyps(g):
     return [g["yseq"][off[k]:off[k + 1]].tolist() for k in range(len(off) - 1)]
 
 
-@pytest.mark.parametrize("name", ["beam_tiny", "beam_tiny_pen"])
+@pytest.mark.parametrize("name", ["beam_tiny", "beam_tiny_pen", "beam_tiny_nb"])
 def test_beam_search_oracle_vs_reference(name):
     """oracle/beam_ref.py (BeamSearchPara + CTCPrefixScore restated) on the oracle model's decoder log-probs and
     CTC log-probs reproduces the reference beam_search() n-best: identical yseqs, scores within 1e-5 relative,
@@ -373,6 +373,9 @@ def test_beam_search_oracle_vs_reference(name):
     g = np.load(f"{GOLD}/{name}.npz")
     cfg = dataclasses.replace(paraformer_tiny(), ctc_weight=0.3)
     w = make_weights(cfg, int(g["wseed"]))
+    if "eos_boost" in g and float(g["eos_boost"]):   # beam_tiny_nb: hypotheses end at many positions (nbest > beam)
+        w["decoder.output_layer.bias"] = w["decoder.output_layer.bias"].copy()
+        w["decoder.output_layer.bias"][cfg.eos] += float(g["eos_boost"])
     feats, lens = fbank_input(int(g["seed"]), int(g["B"]), int(g["T"]), g["lens"])
     r = paraformer_infer(feats, lens, w, cfg, keep_logits=True)
     assert np.array_equal(r["ntok"].numpy(), g["ntok"])
