@@ -59,8 +59,10 @@ constexpr int OPI = FFN2_OPI;                   // phase-0 output blocks interle
 constexpr int NB = 8;                    // fragment register slots (divides TF, CHF and OPF)
 // per-column vectors staged in LDS behind the ring (float offsets)
 constexpr int V_G = 0, V_B = 512, V_C2 = 1024, V_GN = 1536, V_BN = 2048, V_BO = 2560, V_C1 = 3072, V_B1 = 3584;
-constexpr int NVEC = V_B1 + FF;
-constexpr int LDS_BYTES = RING + NVEC * 4;   // 153,600 B
+constexpr int QKF = 3 * OPF;             // MODE 4 phase 3: the next layer's Wqkv, three passes of 512 output features
+constexpr int V_BQ = V_B1 + FF;          // MODE 4: the next layer's q|k|v biases
+constexpr int NVEC = V_BQ + 3 * FD;
+constexpr int LDS_BYTES = RING + NVEC * 4;   // 159,744 B
 static_assert(LDS_BYTES <= 163840, "LDS plan");
 static_assert(PD < TF && TF % NB == 0 && CHF % NB == 0 && OPF % NB == 0 && PD < NB, "stream plan");
 
@@ -138,6 +140,21 @@ __device__ __forceinline__ f32x4 vec_read(const float* lds) {
 // feature index (within its 32-block) of register reg of a 32x32 accumulator in lane half h
 __device__ __forceinline__ int acc_col(int reg, int h) { return (reg & 3) + 8 * (reg >> 2) + 4 * h; }
 
+// bf16 outputs of one 32-feature block as two 16-B stores per lane: lane half h holds features 8q + 4h .. +3 of the
+// four register groups q; permlane32 swaps hand each half-wave the other half's piece of groups q (h = 0: q even,
+// h = 1: q odd), so every lane stores 8 consecutive features of its row (8-B stores were store-issue bound)
+__device__ __forceinline__ void store_bf16_block(bf16* row, const bf16x4 (&o)[4], int h) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        uint2 pa, pb;
+        __builtin_memcpy(&pa, &o[2 * j], 8);
+        __builtin_memcpy(&pb, &o[2 * j + 1], 8);
+        const auto rx = __builtin_amdgcn_permlane32_swap(pa.x, pb.x, false, false);
+        const auto ry = __builtin_amdgcn_permlane32_swap(pa.y, pb.y, false, false);
+        *(uint4*)(row + 16 * j + 8 * h) = make_uint4(rx[0], ry[0], rx[1], ry[1]);
+    }
+}
+
 // VAR (diagnostic builds of tools/ffn2_bench.hip only; the library instantiates VAR 0): 1 = no weight DMA and no
 // DMA waits (stale ring), 2 = no MFMAs, 3 = neither DMA nor barriers (MFMA + fragment reads alone), 5 = the
 // prologue / transition / epilogue alone (no stream: zero chunks, no phase-0 MFMAs), 4 = every tile streamed from
@@ -154,8 +171,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int r = lane & 31, h = lane >> 5;
-    constexpr bool OP = MODE == 1 || MODE == 3, DEC = MODE == 2 || MODE == 3;
-    constexpr int F0 = OP ? OPF : 0, NF = F0 + NCH * CHF, NT = NF / TF;
+    constexpr bool OP = MODE == 1 || MODE == 3 || MODE == 4, DEC = MODE == 2 || MODE == 3;
+    constexpr bool EOP = MODE == 1 || MODE == 4, QK = MODE == 4;   // encoder out-projection; + the next QKV
+    constexpr int F0 = OP ? OPF : 0, F3 = F0 + NCH * CHF, NF = F3 + (QK ? QKF : 0), NT = NF / TF;
     const long long rg = (long long)blockIdx.x * BM + 32 * w + r;   // this lane's row
     const bool live = rg < M;
     const long long rc = live ? rg : (long long)M - 1;               // clamped for loads
@@ -170,6 +188,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         if constexpr (DEC) vec[V_C1 + i] = c1[i];
     }
     for (int i = tid; i < FF; i += 256) vec[V_B1 + i] = b1[i];
+    if constexpr (QK)
+        for (int i = tid; i < 3 * FD; i += 256) vec[V_BQ + i] = c1[i];
     __syncthreads();
 
     // ---- weight ring: tile t -> slot t % RS; this wave moves fragments GW w .. GW w + GW - 1 of each tile
@@ -288,9 +308,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(A[0]), "+v"(A[1]), "+v"(A[2]), "+v"(A[3]), "+v"(B[0]), "+v"(B[1]),
                      "+v"(B[2]), "+v"(B[3]));
     };
-    auto ln_block = [&](int ob, const f32x16& t, float mean, float rstd) {
+    auto ln_block = [&](int ob, const f32x16& t, float mean, float rstd, int vg = V_G, int vbb = V_B) {
         f32x4 G[4], Bt[4];
-        vec_block(V_G, V_B, ob, G, Bt);
+        vec_block(vg, vbb, ob, G, Bt);
 #pragma unroll
         for (int q = 0; q < 4; ++q)
 #pragma unroll
@@ -427,7 +447,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
                      "+v"(wf[5]), "+v"(wf[6]), "+v"(wf[7]));
         xdl_drain(acc);
         // x1 = ((Y0 + bo) + F) + x (the separate GEMM epilogue's order; layer 0: no x, the decoder: no F)
-        add_rows(false, X ? X : bo, X ? FD : 0, X ? 1.f : 0.f, MODE == 1 ? Fr : nullptr, V_BO);
+        add_rows(false, X ? X : bo, X ? FD : 0, X ? 1.f : 0.f, EOP ? Fr : nullptr, V_BO);
         if constexpr (MODE == 3) {   // the decoder keeps x1 (its FSMN step adds to it)
             if (live) {
 #pragma unroll
@@ -449,7 +469,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
             fence();
             const f32x16 t = acc_get(ob);
             ln_block(ob, t, mean, rstd);
-            acc_c2(ob, t, MODE == 1);
+            acc_c2(ob, t, EOP);
         }
         fence();
     }
@@ -547,6 +567,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #pragma unroll
         for (int k = 0; k < 32; ++k) p2(ft + k, k, k, hfb);   // tail: P2(63)
     }
+    if constexpr (QK)   // the read-ahead of phase 3's first fragments: retired before the epilogue (see phase 0)
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(wf[0]), "+v"(wf[1]), "+v"(wf[2]), "+v"(wf[3]), "+v"(wf[4]),
+                     "+v"(wf[5]), "+v"(wf[6]), "+v"(wf[7]));
     xdl_drain(acc);
 
     // ---- epilogue (no DMA in flight: the last tiles were waited for by their tops)
@@ -581,6 +604,70 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         }
         fence();
     }
+    if constexpr (QK) {
+        // ---- phase 3: the next layer's q|k|v = LN1_next(x2) Wqkv^T + b in three passes of 512 output features,
+        //      the LayerNorm output as the B operand in registers (the W1 k order: Wqkv packed by ffn2_pack_qkv);
+        //      Xn receives bf16 rows of 1536, c1 holds the biases
+        float mean, rstd;
+        acc_stats(mean, rstd);
+#pragma unroll
+        for (int ob = 0; ob < 16; ++ob) {
+            fence();
+            const f32x16 t = acc_get(ob);
+            ln_block(ob, t, mean, rstd, V_GN, V_BN);
+        }
+        fence();
+#pragma unroll
+        for (int ks = 0; ks < 32; ++ks) asm volatile("" : "+v"(act[ks]));
+#pragma unroll
+        for (int f = 0; f < PD; ++f) rd(F3 + f, f, wf[f % NB]);
+        valu_to_mfma();
+        // three passes of 512 output features (the whole accumulator); a pass's epilogue (bias, bf16, 16-B stores)
+        // runs between the passes. (Six passes of 256 with the previous pass's stores issued in the MFMA shadow from
+        // the other accumulator half spilled the LayerNorm operand to scratch inside the loop: not kept.)
+        for (int p = 0; p < 3; ++p) {
+            const int fp = F3 + OPF * p;
+#pragma unroll
+            for (int pp = 0; pp < 4; ++pp)
+#pragma unroll
+                for (int ks = 0; ks < 32; ++ks)
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const int fs = 128 * pp + 4 * ks + e, ob = 4 * pp + e;
+                        step_pre(fp + fs, fs);
+                        if (VAR == 2 || VAR == 5) asm volatile("" :: "v"(wf[fs % NB]));
+                        else if (ks == 0) mfma_a0(acc[ob], wf[fs % NB], act[0]);
+                        else mfma_a(acc[ob], wf[fs % NB], act[ks]);
+                    }
+            asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(wf[0]), "+v"(wf[1]), "+v"(wf[2]), "+v"(wf[3]), "+v"(wf[4]),
+                         "+v"(wf[5]), "+v"(wf[6]), "+v"(wf[7]));
+            xdl_drain(acc);
+            if (live) {
+#pragma unroll
+                for (int ob = 0; ob < 16; ++ob) {
+                    fence();
+                    const f32x16 t = acc_get(ob);
+                    f32x4 Bq[4];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) Bq[q] = vec_read(vec + V_BQ + FD * p + 32 * ob + 8 * q + 4 * h);
+                    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(Bq[0]), "+v"(Bq[1]), "+v"(Bq[2]), "+v"(Bq[3]));
+                    bf16x4 o[4];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q)
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) o[q][i] = f2bf(t[4 * q + i] + Bq[q][i]);
+                    store_bf16_block(Xn + rg * (3 * FD) + FD * p + 32 * ob, o, h);
+                }
+                fence();
+            }
+            if (p < 2) {
+#pragma unroll
+                for (int f = 0; f < PD; ++f) rd(fp + OPF + f, f, wf[f % NB]);
+            }
+            valu_to_mfma();
+        }
+        return;
+    }
     if (Xn) {
         float mean, rstd;
         acc_stats(mean, rstd);
@@ -591,13 +678,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
                 const f32x16 t = acc_get(ob);
                 f32x4 G[4], Bt[4];
                 vec_block(V_GN, V_BN, ob, G, Bt);
+                bf16x4 o[4];
 #pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    bf16x4 o;
+                for (int q = 0; q < 4; ++q)
 #pragma unroll
-                    for (int i = 0; i < 4; ++i) o[i] = f2bf((t[4 * q + i] - mean) * rstd * G[q][i] + Bt[q][i]);
-                    *(bf16x4*)(Xn + rg * FD + 32 * ob + 8 * q + 4 * h) = o;
-                }
+                    for (int i = 0; i < 4; ++i) o[q][i] = f2bf((t[4 * q + i] - mean) * rstd * G[q][i] + Bt[q][i]);
+                store_bf16_block(Xn + rg * FD + 32 * ob, o, h);
             }
             fence();
         }
@@ -659,6 +745,21 @@ __global__ __launch_bounds__(256) void ffn2_pack_o_kernel(const bf16* __restrict
     *(bf16x8*)(Wp + (long long)gid * 8) = *(const bf16x8*)(Wo + (long long)(32 * ob + m) * FD + 16 * ks + 8 * hh);
 }
 
+// the next layer's Wqkv [1536 out][512 in] -> phase-3 fragments: three passes of 512 output features (rows 512 p ..),
+// fragment f of a pass = output block 4 (f >> 7) + (f & 3), k step (f >> 2) & 31, with W1's permuted k (the B operand
+// is the LayerNorm output in act)
+__global__ __launch_bounds__(256) void ffn2_pack_qkv_kernel(const bf16* __restrict__ Wq, bf16* __restrict__ Wp) {
+    const int gid = blockIdx.x * 256 + threadIdx.x;   // < QKF * 64
+    const int fq = gid >> 6, l = gid & 63, m = l & 31, hh = l >> 5;
+    const int p = fq / OPF, f = fq % OPF;
+    const int ob = 4 * (f >> 7) + (f & 3), ks = (f >> 2) & 31;
+    bf16x8 o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+        o[e] = Wq[(long long)(FD * p + 32 * ob + m) * FD + 32 * (ks >> 1) + perm_k(ks & 1, hh, e)];
+    *(bf16x8*)(Wp + (long long)gid * 8) = o;
+}
+
 // c1[o] = sum_k bf16(W2[o][k] g[k]) (the packed values), c2[o] = sum_k W2[o][k] b[k]; one block per output row
 __global__ __launch_bounds__(256) void ffn2_dec_consts_kernel(const float* __restrict__ W2, const float* __restrict__ gF,
                                                               const float* __restrict__ bF, float* __restrict__ c1,
@@ -709,6 +810,13 @@ hipError_t pfm_ffn2_pack(const bf16* W1, const bf16* W2, bf16* Wp, hipStream_t s
     return hipSuccess;
 }
 
+// the next layer's Wqkv [1536][512] -> QKF fragments behind the layer's FFN tiles (ffn2_kernel MODE 4)
+hipError_t pfm_ffn2_pack_qkv(const bf16* Wqkv, bf16* Wp, hipStream_t st) {
+    hipLaunchKernelGGL(ffn2_pack_qkv_kernel, dim3(QKF * 64 / 256), dim3(256), 0, st, Wqkv, Wp);
+    PFM_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
 hipError_t pfm_ffn2_pack_o(const bf16* Wo, bf16* Wp, hipStream_t st) {
     hipLaunchKernelGGL(ffn2_pack_o_kernel, dim3(OPF * 64 / 256), dim3(256), 0, st, Wo, Wp);
     PFM_LAUNCH_CHECK();
@@ -742,6 +850,18 @@ hipError_t pfm_ffn2_fused_op(const bf16* o, const bf16* f, const float* bo, cons
         return hipErrorInvalidValue;
     if (!al16(x) || !al16(xo) || !al16(Wop) || !al16(xn) || !al16(o) || !al16(f) || !al16(bo)) return hipErrorInvalidValue;
     return ffn2_launch<1>(st, M, x, g2, be2, eps, Wop, b1, b2, xo, gn, bn, xn, o, f, bo, nullptr);
+}
+
+// MODE 4: pfm_ffn2_fused_op plus the next layer's q|k|v projection: x2 -> xo (f32), qkv = LN1_next(x2) Wqkv^T + bq
+// (bf16 [M, 1536]); Wop: the Wo fragments, the FFN stream and pfm_ffn2_pack_qkv's fragments, contiguous.
+hipError_t pfm_ffn2_fused_op_qkv(const bf16* o, const bf16* f, const float* bo, const float* x, int M, const float* g2,
+                                 const float* be2, float eps, const bf16* Wop, const float* b1, const float* b2, float* xo,
+                                 const float* gn, const float* bn, const float* bq, bf16* qkv, hipStream_t st) {
+    if (M <= 0) return hipSuccess;
+    if (!o || !f || !bo || !xo || !b1 || !b2 || !gn || !bn || !bq || !qkv) return hipErrorInvalidValue;
+    if (!al16(x) || !al16(xo) || !al16(Wop) || !al16(qkv) || !al16(o) || !al16(f) || !al16(bo) || !al16(bq))
+        return hipErrorInvalidValue;
+    return ffn2_launch<4>(st, M, x, g2, be2, eps, Wop, b1, b2, xo, gn, bn, qkv, o, f, bo, bq);
 }
 
 hipError_t pfm_ffn2_fused_dec(const float* x, int M, const float* g1, const float* be1, float eps, const bf16* Wp,

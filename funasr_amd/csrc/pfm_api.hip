@@ -102,6 +102,10 @@ hipError_t pfm_ffn2_fused_dec(const float* x, int M, const float* g1, const floa
 hipError_t pfm_ffn_fused_op(const bf16* o, const bf16* f, const float* bo, const float* x, int M, const float* g2,
                             const float* be2, float eps, const bf16* Wop, const float* b1, const float* b2, float* xo,
                             const float* gn, const float* bn, bf16* xn, hipStream_t st);
+hipError_t pfm_ffn2_fused_op_qkv(const bf16* o, const bf16* f, const float* bo, const float* x, int M, const float* g2,
+                                 const float* be2, float eps, const bf16* Wop, const float* b1, const float* b2, float* xo,
+                                 const float* gn, const float* bn, const float* bq, bf16* qkv, hipStream_t st);
+hipError_t pfm_ffn2_pack_qkv(const bf16* Wqkv, bf16* Wp, hipStream_t st);
 hipError_t pfm_ffn_fused(const float* x, int M, const float* g2, const float* be2, float eps, const bf16* Wp,
                          const float* b1, const float* b2, float* xo, const float* gn, const float* bn, bf16* xn,
                          hipStream_t st);
@@ -181,9 +185,10 @@ void pfm_knobs_refresh() {
     k.dec_subbatch = std::max(1, iv("PFM_DEC_SUBBATCH", 2));
     k.ffn_op = iv("PFM_FFN_OP", 1) != 0;
     k.dec_ffn_fused = iv("PFM_DEC_FFN_FUSED", 1) != 0;
-    k.ffn_kernel = iv("PFM_FFN_KERNEL", 1) == 2 ? 2 : 1;
+    k.ffn_kernel = iv("PFM_FFN_KERNEL", 2) == 1 ? 1 : 2;
     k.dec_ffn_kernel = iv("PFM_DEC_FFN_KERNEL", 1) == 2 ? 2 : 1;
     k.exact_terms = iv("PFM_EXACT_TERMS", 6) == 3 ? 3 : 6;
+    k.ffn_qkv = iv("PFM_FFN_QKV", 1) != 0;
     const int* f = &k.gemm_kernel;
     unsigned long long s = 1469598103934665603ull;   // FNV-1a over the fields
     for (int i = 0; i < PFM_KNOB_FIELDS; ++i) s = (s ^ (unsigned long long)(unsigned)f[i]) * 1099511628211ull;
@@ -234,6 +239,7 @@ struct EncLayer {
     size_t ln1g, ln1b, wqkv, bqkv, wo, bo, fsmn, ln2g, ln2b, w1, b1, w2, b2;
     int din;
     size_t ffp = 0;   // fast mode: element offset of the packed W1 | W2 ring tiles in ffn_pack (k_ffn.hip)
+    bool qkv_next = false;   // k_ffn2.hip: ... followed by the next layer's packed Wqkv (ffn2_kernel MODE 4)
 };
 struct DecLayer { size_t fsmn, wq, bq, wo, bo, w1, b1, w2, ng, nb, n1g, n1b, n2g, n2b, n3g, n3b; };
 
@@ -476,13 +482,18 @@ int ensure_bf16(pfm_handle* h, hipStream_t st) {
     auto pack = [&](const bf16* w1, const bf16* w2, bf16* wp) { return fk == 2 ? pfm_ffn2_pack(w1, w2, wp, st) : pfm_ffn_pack(w1, w2, wp, st); };
     auto pack_o = [&](int kind, const bf16* wo, bf16* wp) { return kind == 2 ? pfm_ffn2_pack_o(wo, wp, st) : pfm_ffn_pack_o(wo, wp, st); };
     if (!h->ffn_ready && ffn_shape_ok(h->cfg) && pfm_knobs().ffn_fused && !h->enc.empty()) {
-        // per layer: the out-projection's 32 tiles, then the FFN's 256 (ffp = the FFN tiles)
-        const size_t po = pfm_ffn_packed_o_elems(), per = po + pfm_ffn_packed_elems();
+        // per layer: the out-projection's 32 tiles, then the FFN's 256 (ffp = the FFN tiles); k_ffn2.hip layouts add
+        // the next layer's Wqkv as 3 x 32 more (ffn2_kernel MODE 4, the QKV projection as phase 3)
+        const size_t po = pfm_ffn_packed_o_elems(), pfe = pfm_ffn_packed_elems(), per = po + pfe + (fk == 2 ? 3 * po : 0);
+        const int D = h->cfg.d_model;
         HIP_TRY(h->ffn_pack.ensure(h->enc.size() * per * sizeof(bf16)));
         for (size_t l = 0; l < h->enc.size(); ++l) {
+            bf16* base = h->ffn_pack.as<bf16>() + l * per;
             h->enc[l].ffp = l * per + po;
-            HIP_TRY(pack_o(fk, h->wb(h->enc[l].wo), h->ffn_pack.as<bf16>() + l * per));
-            HIP_TRY(pack(h->wb(h->enc[l].w1), h->wb(h->enc[l].w2), h->ffn_pack.as<bf16>() + l * per + po));
+            HIP_TRY(pack_o(fk, h->wb(h->enc[l].wo), base));
+            HIP_TRY(pack(h->wb(h->enc[l].w1), h->wb(h->enc[l].w2), base + po));
+            h->enc[l].qkv_next = fk == 2 && l + 1 < h->enc.size() && h->enc[l + 1].din == D;
+            if (h->enc[l].qkv_next) HIP_TRY(pfm_ffn2_pack_qkv(h->wb(h->enc[l + 1].wqkv), base + po + pfe, st));
         }
         h->ffn_ready = true;
     }
@@ -902,6 +913,7 @@ int encoder_stack(const Run& r, const float* x_in, const int* lens, int B, int T
     const int Kp0 = (I + 63) / 64 * 64;
     const bool pad0 = fast && !r.raw_input && !r.ck && I % 64 && h->qkv0_pad.p && l0 == 0;
     const int lndt = x3 ? DT_X3 : dt;
+    bool qkv_ready = false;   // the previous layer's fused FFN kernel already wrote this layer's q|k|v (QKVb)
     for (int l = l0; l < l1; ++l) {
         const EncLayer& L = h->enc[l];
         const int din = L.din;
@@ -920,7 +932,7 @@ int encoder_stack(const Run& r, const float* x_in, const int* lens, int B, int T
         else if (!(ffn_fused && l > l0))   // fused FFN: the previous layer's kernel wrote LN1(x)
             HIP_TRY(pfm_layernorm(X, rowmap_plain(D), (int)M, D, r.P(L.ln1g), r.P(L.ln1b), c.ln_eps, nullptr, 0, 1.f,
                                   Xn, xmap3, lndt, nullptr, plain, 0, st));
-        {   // q|k|v = LN1(x) Wqkv^T + b   (fast mode: bf16 only — attention and FSMN read bf16)
+        if (!qkv_ready) {   // q|k|v = LN1(x) Wqkv^T + b   (fast mode: bf16 only — attention and FSMN read bf16)
             GemmEpi e = epi_default();
             e.bias = r.P(L.bqkv);
             if (fast) { e.out = QKVb; e.out_map = rowmap_plain(3 * D); e.out_dtype = DT_BF16; }
@@ -933,6 +945,7 @@ int encoder_stack(const Run& r, const float* x_in, const int* lens, int B, int T
                 HIP_TRY(r.gemm(dt, Xn, rowmap_plain(din), r.W(L.wqkv), din, (int)M, 3 * D, din, e));
             }
         }
+        qkv_ready = false;
         // FSMN memory on v (attention.py:207-223) + masked MHA. Fast mode: the FSMN runs in the attention
         // kernel's epilogue (each block owns its rows x head channels; V is L2-resident) when the shape
         // allows (K 11, left 5); bf16 in / bf16 out either way
@@ -1003,6 +1016,17 @@ int encoder_stack(const Run& r, const float* x_in, const int* lens, int B, int T
             if (ffn_op) {   // x1 = (x +) O Wo^T + bo + fsmn, then the FFN on x1 (encoder.py:120-145)
                 const double flo = fl + 2.0 * M * (double)D * D;
                 const double byo = by + (double)M * D * 2.0 * 2.0 + 2.0 * D * D - (din == D ? 0.0 : 4.0 * M * D);
+                if (nxt && L.qkv_next && h->ffn_kind == 2 && pfm_knobs().ffn_qkv) {
+                    // ... and the next layer's q|k|v = LN1_{l+1}(x2) Wqkv^T + b (phase 3: LN1_{l+1} stays in registers)
+                    const EncLayer& N = h->enc[l + 1];
+                    ProfScope ps(h, st, PFM_K_GEMM, flo + 6.0 * M * (double)D * D,
+                                 byo + (double)M * D * (6.0 - 2.0) + 6.0 * D * D);
+                    HIP_TRY(pfm_ffn2_fused_op_qkv(Ob, Fb, r.P(L.bo), din == D ? X : nullptr, (int)M, r.P(L.ln2g),
+                                                  r.P(L.ln2b), c.ln_eps, h->ffn_pack.as<bf16>() + L.ffp - pfm_ffn_packed_o_elems(),
+                                                  r.P(L.b1), r.P(L.b2), X, r.P(N.ln1g), r.P(N.ln1b), r.P(N.bqkv), QKVb, st));
+                    qkv_ready = true;
+                    continue;
+                }
                 ProfScope ps(h, st, PFM_K_GEMM, flo, byo);
                 HIP_TRY((h->ffn_kind == 2 ? pfm_ffn2_fused_op : pfm_ffn_fused_op)(Ob, Fb, r.P(L.bo), din == D ? X : nullptr, (int)M, r.P(L.ln2g), r.P(L.ln2b),
                                          c.ln_eps, h->ffn_pack.as<bf16>() + L.ffp - pfm_ffn_packed_o_elems(), r.P(L.b1),
@@ -1893,6 +1917,39 @@ int pfm_op_ffn_op(void* stream, const void* o, const void* f, const float* Wo, c
     HIP_TRY((k2 ? pfm_ffn2_pack : pfm_ffn_pack)(w1b, w2b, wp + po, st));
     HIP_TRY((k2 ? pfm_ffn2_fused_op : pfm_ffn_fused_op)((const bf16*)o, (const bf16*)f, bo, x, M, g2, b2n, eps, wp, b1, b2, xo, gn, bn, (bf16*)xn,
                              st));
+    HIP_TRY(hipStreamSynchronize(st));
+    return PFM_OK;
+}
+
+int pfm_op_ffn_op_qkv(void* stream, const void* o, const void* f, const float* Wo, const float* bo, const float* x, int M,
+                      const float* g2, const float* b2n, float eps, const float* W1, const float* b1, const float* W2,
+                      const float* b2, float* xo, const float* gn, const float* bn, const float* Wq, const float* bq,
+                      void* qkv) {
+    pfm_knobs_refresh();
+    if (!o || !f || !Wo || !bo || !xo || !W1 || !W2 || !g2 || !b2n || !b1 || !b2 || !gn || !bn || !Wq || !bq || !qkv ||
+        M < 0)
+        return fail(PFM_E_ARG, "pfm_op_ffn_op_qkv: null operand");
+    if (!all_aligned16({o, f, bo, x, xo, g2, b2n, b1, b2, gn, bn, bq, qkv}))
+        return fail(PFM_E_ARG, "pfm_op_ffn_op_qkv: operands must be 16-B aligned");
+    const hipStream_t st = (hipStream_t)stream;
+    const size_t nw = (size_t)2048 * 512, no = (size_t)512 * 512, po = pfm_ffn_packed_o_elems(),
+                 pfe = pfm_ffn_packed_elems();
+    OpScratch sc;
+    bf16 *w1b, *w2b, *wob, *wqb, *wp;
+    HIP_TRY(sc.alloc(&w1b, nw));
+    HIP_TRY(sc.alloc(&w2b, nw));
+    HIP_TRY(sc.alloc(&wob, no));
+    HIP_TRY(sc.alloc(&wqb, 3 * no));
+    HIP_TRY(sc.alloc(&wp, po + pfe + 3 * po));
+    HIP_TRY(pfm_f32_to_bf16(W1, w1b, (long long)nw, st));
+    HIP_TRY(pfm_f32_to_bf16(W2, w2b, (long long)nw, st));
+    HIP_TRY(pfm_f32_to_bf16(Wo, wob, (long long)no, st));
+    HIP_TRY(pfm_f32_to_bf16(Wq, wqb, (long long)(3 * no), st));
+    HIP_TRY(pfm_ffn2_pack_o(wob, wp, st));
+    HIP_TRY(pfm_ffn2_pack(w1b, w2b, wp + po, st));
+    HIP_TRY(pfm_ffn2_pack_qkv(wqb, wp + po + pfe, st));
+    HIP_TRY(pfm_ffn2_fused_op_qkv((const bf16*)o, (const bf16*)f, bo, x, M, g2, b2n, eps, wp, b1, b2, xo, gn, bn, bq,
+                                  (bf16*)qkv, st));
     HIP_TRY(hipStreamSynchronize(st));
     return PFM_OK;
 }

@@ -143,12 +143,14 @@ struct PfmKnobs {
     int dec_subbatch;       // PFM_DEC_SUBBATCH (default 2): decoder utterance groups on concurrent streams
     int ffn_op;             // PFM_FFN_OP (default 1): encoder out-projection folded into the fused FFN kernel
     int dec_ffn_fused;      // PFM_DEC_FFN_FUSED (default 1): decoder LN1-FFN(LN_F folded)-LN kernel (fast mode)
-    int ffn_kernel;         // PFM_FFN_KERNEL (default 1): encoder fused FFN as 64-row workgroups (k_ffn.hip);
-                            // 2 = 128-row workgroups (k_ffn2.hip; pays only when M / 128 fills the chip)
+    int ffn_kernel;         // PFM_FFN_KERNEL (default 2): encoder fused FFN as 128-row workgroups (k_ffn2.hip, with
+                            // the next layer's QKV projection folded in); 1 = 64-row workgroups (k_ffn.hip)
     int dec_ffn_kernel;     // PFM_DEC_FFN_KERNEL (default 1): the same choice for the decoder FFN
     int exact_terms;        // PFM_EXACT_TERMS (default 6): products per EXACT-mode split-bf16 GEMM; 3 = bf16x3
+    int ffn_qkv;            // PFM_FFN_QKV (default 1): with the 128-row fused FFN, the next layer's QKV projection as
+                            // its phase 3 (k_ffn2.hip MODE 4; the separate LN1 + QKV GEMM otherwise)
     unsigned long long sig;
 };
-#define PFM_KNOB_FIELDS 20
+#define PFM_KNOB_FIELDS 21
 const PfmKnobs& pfm_knobs();   // the calling thread's snapshot (refreshed lazily if no entry point did yet)
 void pfm_knobs_refresh();

@@ -25,7 +25,7 @@ MODES = {"exact": MODE_EXACT, "fp32": MODE_EXACT, "fast": MODE_FAST, "bf16": MOD
 # every symbol include/pfm.h declares (checked by tests/test_abi.py)
 ABI_SYMBOLS = ("pfm_config_default", "pfm_config_sensevoice", "pfm_create", "pfm_run_beam", "pfm_set_weight", "pfm_set_weight_device",
                "pfm_missing_weights", "pfm_reserve", "pfm_run", "pfm_run_ctc", "pfm_ctc_align", "pfm_op_ctc_collapse", "pfm_fbank", "pfm_lfr_frames", "pfm_last_error", "pfm_destroy", "pfm_op_gemm",
-               "pfm_op_attention", "pfm_op_layernorm", "pfm_op_fsmn", "pfm_op_cif", "pfm_op_ctc_beam", "pfm_profile", "pfm_op_ffn", "pfm_op_ffn_op", "pfm_op_ffn_dec", "pfm_op_fsmn_bf16", "pfm_op_layernorm_bf16",
+               "pfm_op_attention", "pfm_op_layernorm", "pfm_op_fsmn", "pfm_op_cif", "pfm_op_ctc_beam", "pfm_profile", "pfm_op_ffn", "pfm_op_ffn_op", "pfm_op_ffn_op_qkv", "pfm_op_ffn_dec", "pfm_op_fsmn_bf16", "pfm_op_layernorm_bf16",
                "pfm_profile_read", "pfm_streams_create", "pfm_streams_reset", "pfm_stream_step",
                "pfm_streams_destroy", "pfm_fbank_raw", "pfm_lfr_gather", "pfm_config_punc", "pfm_run_punc", "pfm_vad_config_default", "pfm_vad_create",
                "pfm_vad_set_weight", "pfm_vad_missing_weights", "pfm_vad_reset", "pfm_vad_run", "pfm_vad_destroy", "pfm_vad_fbank_raw",
@@ -124,6 +124,8 @@ def load_library(path: Optional[str] = None) -> ctypes.CDLL:
                                vp]
     lib.pfm_op_ffn_op.argtypes = [vp, vp, vp, f32p, f32p, f32p, i32, f32p, f32p, ctypes.c_float, f32p, f32p, f32p,
                                   f32p, f32p, f32p, f32p, vp]
+    lib.pfm_op_ffn_op_qkv.argtypes = [vp, vp, vp, f32p, f32p, f32p, i32, f32p, f32p, ctypes.c_float, f32p, f32p, f32p,
+                                      f32p, f32p, f32p, f32p, f32p, f32p, vp]
     lib.pfm_op_ffn_dec.argtypes = [vp, f32p, i32, f32p, f32p, ctypes.c_float, f32p, f32p, f32p, f32p, f32p, f32p,
                                    f32p, f32p, vp, vp, f32p, f32p]
     lib.pfm_streams_create.argtypes = [vp, i32, ctypes.POINTER(ctypes.c_int32), i32, i32, i32, ctypes.POINTER(vp)]
@@ -534,6 +536,22 @@ def op_ffn_op(o, f, Wo, bo, x, g2, b2n, eps, W1, b1, W2, b2, gn=None, bn=None):
                             _ptr(g2), _ptr(b2n), ctypes.c_float(eps), _ptr(W1.contiguous()), _ptr(b1),
                             _ptr(W2.contiguous()), _ptr(b2), _ptr(xo), _ptr(gn), _ptr(bn), _ptr(xn)), "pfm_op_ffn_op")
     return xo, xn
+
+
+def op_ffn_op_qkv(o, f, Wo, bo, x, g2, b2n, eps, W1, b1, W2, b2, gn, bn, Wq, bq):
+    """op_ffn_op plus the next layer's QKV projection in the same launch (pfm_op_ffn_op_qkv, 128-row kernel MODE 4):
+    -> (x2 f32 [M,512], qkv = LN_next(x2) Wq^T + bq bf16 [M,1536])."""
+    import torch
+    lib = load_library()
+    M = o.shape[0]
+    xo = torch.empty((M, 512), dtype=torch.float32, device=o.device)
+    qkv = torch.empty((M, 1536), dtype=torch.bfloat16, device=o.device)
+    check(lib.pfm_op_ffn_op_qkv(_stream_ptr(torch, o.device), _ptr(o.contiguous()), _ptr(f.contiguous()),
+                                _ptr(Wo.contiguous()), _ptr(bo), _ptr(x.contiguous() if x is not None else None), M,
+                                _ptr(g2), _ptr(b2n), ctypes.c_float(eps), _ptr(W1.contiguous()), _ptr(b1),
+                                _ptr(W2.contiguous()), _ptr(b2), _ptr(xo), _ptr(gn), _ptr(bn), _ptr(Wq.contiguous()),
+                                _ptr(bq), _ptr(qkv)), "pfm_op_ffn_op_qkv")
+    return xo, qkv
 
 
 def op_ffn_dec(x, g1, b1n, eps, W1, b1, W2, gF, bF, gn, bn, o=None, Wo=None, bo=None):

@@ -354,6 +354,15 @@ int pfm_op_ffn_op(void* stream, const void* o, const void* f, const float* Wo, c
                   int M, const float* g2, const float* b2n, float eps, const float* W1, const float* b1,
                   const float* W2, const float* b2, float* xo, const float* gn, const float* bn, void* xn);
 
+/* pfm_op_ffn_op followed by the next encoder layer's q|k|v projection in the same launch, as the fast path runs it
+ * with the 128-row fused FFN (k_ffn2.hip MODE 4): x2 -> xo (f32) and qkv = LN1_next(x2) Wq^T + bq, bf16
+ * [M, 1536] (Wq f32 [1536][512], bq [1536]; the next layer's attention.py:180-186 linear_q_k_v on its norm1).
+ * Synchronous. */
+int pfm_op_ffn_op_qkv(void* stream, const void* o, const void* f, const float* Wo, const float* bo, const float* x,
+                      int M, const float* g2, const float* b2n, float eps, const float* W1, const float* b1,
+                      const float* W2, const float* b2, float* xo, const float* gn, const float* bn, const float* Wq,
+                      const float* bq, void* qkv);
+
 /* Fused decoder feed-forward as the fast path runs it (k_ffn.hip DEC, LN_F folded through W2):
  *   x1 = x, or x + o Wo^T + bo when o is non-NULL (the previous block's cross-attention out-projection)
  *   y  = W2 LN_F(relu(W1 LN1(x1) + b1))  (w_2 has no bias) ;  xn = LN_next(y) bf16

@@ -105,6 +105,17 @@ def pack_tokens(tokens):
     return flat, off
 
 
+def topk_rows(logp, ntok, k=5):
+    """Per decoded position (utterance order): the k best ids (value desc, id asc) and their log-probs."""
+    ids, vals = [], []
+    for b in range(logp.shape[0]):
+        t = torch.from_numpy(np.ascontiguousarray(logp[b, : ntok[b]]))
+        v, i = torch.topk(t, k, dim=-1, sorted=True)
+        ids.append(i.numpy().astype(np.int32))
+        vals.append(v.numpy().astype(np.float32))
+    return np.concatenate(ids), np.concatenate(vals)
+
+
 def top2_margin(logp, ntok):
     out = []
     for b in range(logp.shape[0]):
@@ -170,10 +181,11 @@ def save_headline():
         csum = np.array([enc[b][valid[b]].astype(np.float64).sum() for b in range(B)])
         csq = np.array([(enc[b][valid[b]].astype(np.float64) ** 2).sum() for b in range(B)])
         am = np.concatenate([r["logp"][b, : r["ntok"][b]].argmax(-1) for b in range(B)]).astype(np.int32)
+        tid, tlp = topk_rows(r["logp"], r["ntok"])
         np.savez_compressed(f"{HERE}/{name}.npz", seed=seed, B=B, T=T, lens=lens, enc_rows=rows, enc_sum=csum,
                             enc_sumsq=csq, enc_lens=r["enc_lens"], token_num=r["token_num"], alphas=r["alphas"],
                             ntok=r["ntok"], tokens=flat, tokens_off=off, argmax=am,
-                            margin=top2_margin(r["logp"], r["ntok"]))
+                            margin=top2_margin(r["logp"], r["ntok"]), top_ids=tid, top_logp=tlp)
         mg = top2_margin(r["logp"], r["ntok"])
         print(name, "ntok mean", r["ntok"].mean(), "positions", len(mg), "min margin", mg.min(),
               "margins < 1e-3:", int((mg < 1e-3).sum()))
@@ -471,6 +483,37 @@ def save_sv_large():
                             enc_sumsq=csq, enc_lens=ol, frame_ids=r["frame_ids"], tokens=flat, tokens_off=off,
                             margin=_frame_margin(r["logp"], ol))
         print(name, "tokens", [len(t) for t in r["tokens"]], "min margin", _frame_margin(r["logp"], ol).min())
+
+
+SV_HEADLINE = {   # name: (seed, B, T, lens) — SenseVoiceSmall at BASELINE config C4 (B=64 x 500 frames, the bench's
+    # SenseVoice leg) and a ragged 24-utterance batch; group rows B/2 x (T+4) >= 4096 engage the fused OP-FFN (LN 1e-5)
+    "sv_large_b24": (8, 24, 500, [500 - 9 * i for i in range(24)]),
+    "sv_large_b64": (9, 64, 500, None),
+}
+
+
+def save_sv_headline():
+    """Reference SenseVoiceSmall.inference (sense_voice/model.py:809-906) at the C4 configuration: token ids, the
+    per-frame CTC argmax with its top-2 margin and the top-3 ids / log-probs of every frame, encoder rows
+    (0, 3, 4, n/2, n-1) and per-utterance sums / sums of squares of the encoder output."""
+    from funasr_amd.config import sense_voice_small
+    m = build_sv_ref(sense_voice_small())
+    for name, (seed, B, T, ln) in SV_HEADLINE.items():
+        feats, lens = fbank_input(seed=seed, B=B, T=T, lens=ln)
+        r = run_sv_ref(m, feats, lens)
+        flat, off = pack_tokens(r["tokens"])
+        enc, ol = r["enc"], r["enc_lens"]
+        rows = np.stack([enc[b, [0, 3, 4, int(ol[b]) // 2, int(ol[b]) - 1]] for b in range(B)])
+        valid = np.arange(enc.shape[1])[None, :] < ol[:, None]
+        csum = np.array([enc[b][valid[b]].astype(np.float64).sum() for b in range(B)])
+        csq = np.array([(enc[b][valid[b]].astype(np.float64) ** 2).sum() for b in range(B)])
+        tid, tlp = topk_rows(r["logp"], ol, k=3)
+        mg = _frame_margin(r["logp"], ol)
+        np.savez_compressed(f"{HERE}/{name}.npz", seed=seed, B=B, T=T, lens=lens, enc_rows=rows, enc_sum=csum,
+                            enc_sumsq=csq, enc_lens=ol, frame_ids=r["frame_ids"], tokens=flat, tokens_off=off,
+                            margin=mg, top_ids=tid, top_logp=tlp)
+        print(name, "tokens mean", np.mean([len(t) for t in r["tokens"]]), "frames", len(mg), "min margin", mg.min(),
+              "margins < 1e-3:", int((mg < 1e-3).sum()))
 
 
 def make_sv_bpe(path, vocab=300):
@@ -930,12 +973,27 @@ def save_vad_pipeline():
                                  strict=True)
     am.punc_model.load_state_dict({k: torch.from_numpy(v) for k, v in make_weights(pcfg, 0).items()}, strict=True)
     out = {}
+    calls = []   # per ASR batch of the pipeline: the decoder's per-position argmax, top-2 margin and token counts
+    dec = am.model.cal_decoder_with_predictor
+
+    def spy(*a, **k):
+        r = dec(*a, **k)
+        logp, ntok = r[0].detach(), a[3] if len(a) > 3 else k["pre_token_length"]
+        top2 = torch.topk(logp, 2, dim=-1).values
+        nt = [int(n) for n in ntok]
+        calls.append(dict(ntok=nt,
+                          argmax=[int(t) for b in range(len(nt)) for t in logp[b, : nt[b]].argmax(-1)],
+                          margin=[float(x) for b in range(len(nt)) for x in (top2[b, : nt[b], 0] - top2[b, : nt[b], 1])]))
+        return r
+
+    am.model.cal_decoder_with_predictor = spy
     for name, bs in (("v1", 300), ("v1_b4", 4)):
         gj = VAD_CASES["v1"]
         wav = vad_waveform(gj[0], gj[1], gj[2])
+        calls.clear()
         res = am.generate(input=wav, batch_size_s=bs)   # (a key= kwarg collides inside inference_with_vad)
         out[name] = dict(batch_size_s=bs, result=[{k: (v.tolist() if hasattr(v, "tolist") else v)
-                                                   for k, v in r.items()} for r in res])
+                                                   for k, v in r.items()} for r in res], asr_calls=list(calls))
         print(name, out[name]["result"][0]["text"][:80])
     with open(f"{HERE}/vad_pipeline.json", "w", encoding="utf-8") as f:
         json.dump(out, f, ensure_ascii=False, indent=1)

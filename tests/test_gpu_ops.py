@@ -298,7 +298,8 @@ def _ffn_params(g, dec=False):
 @pytest.mark.parametrize("kern", ["1", "2"])
 @pytest.mark.parametrize("M", [64, 200, 1000, 4100])
 @pytest.mark.parametrize("resid", [True, False])
-def test_ffn_fused_outproj(dev, M, resid, kern, monkeypatch):
+@pytest.mark.parametrize("eps", [1e-12, 1e-5])
+def test_ffn_fused_outproj(dev, M, resid, kern, eps, monkeypatch):
     """The encoder sub-layer tail exactly as the fast path's default dispatch runs it (ffn_fused_kernel OP mode:
     out-projection as phase 0, x1 in the accumulators, LN2 reduced across waves, FFN, next LN1) vs an fp64
     restatement of sanm/encoder.py:120-145 on the kernel's bf16 operand roundings:
@@ -306,7 +307,8 @@ def test_ffn_fused_outproj(dev, M, resid, kern, monkeypatch):
       x2 = x1 + h W2^T + b2,  xn = LN1_next(x2).
     Tolerances: the FFN increment x2 - x1 rel-L2 < 5e-3 (f32 accumulation order flips a few bf16 roundings of
     a / h), x2 rel < 1e-4, xn within 1.6e-2 abs of LN1_next of the kernel's own x2 (one bf16 ulp at |v| <= 4).
-    Both fused kernels: k_ffn.hip (64 rows per workgroup, PFM_FFN_KERNEL=1, the default) and k_ffn2.hip (128)."""
+    Both fused kernels: k_ffn.hip (64 rows per workgroup, PFM_FFN_KERNEL=1) and k_ffn2.hip (128, the default); LN eps
+    1e-12 (Paraformer) and 1e-5 (SenseVoiceSmall, BASELINE C4)."""
     monkeypatch.setenv("PFM_FFN_KERNEL", kern)
     g = torch.Generator().manual_seed(31 * M + resid)
     p = _ffn_params(g)
@@ -314,18 +316,45 @@ def test_ffn_fused_outproj(dev, M, resid, kern, monkeypatch):
     o = torch.randn(M, 512, generator=g).bfloat16()
     f = (0.5 * torch.randn(M, 512, generator=g)).bfloat16()
     d = lambda t: None if t is None else t.to(dev)  # noqa: E731
-    x2, xn = rt.op_ffn_op(d(o), d(f), d(p["Wo"]), d(p["bo"]), d(x), d(p["g2"]), d(p["b2n"]), 1e-12, d(p["W1"]),
+    x2, xn = rt.op_ffn_op(d(o), d(f), d(p["Wo"]), d(p["bo"]), d(x), d(p["g2"]), d(p["b2n"]), eps, d(p["W1"]),
                           d(p["b1"]), d(p["W2"]), d(p["b2"]), d(p["gn"]), d(p["bn"]))
     torch.cuda.synchronize()
     x1 = o.double() @ p["Wo"].bfloat16().double().T + p["bo"].double() + f.double()
     if resid:
         x1 = x1 + x.double()
-    want = _ffn_ref(x1, p["g2"], p["b2n"], 1e-12, p["W1"].bfloat16(), p["b1"], p["W2"].bfloat16(), p["b2"])
+    want = _ffn_ref(x1, p["g2"], p["b2n"], eps, p["W1"].bfloat16(), p["b1"], p["W2"].bfloat16(), p["b2"])
     yc = x2.double().cpu()
     assert rel(yc - x1, want - x1) < 5e-3
     assert rel(yc, want) < 1e-4
-    ln = _ln64(yc, p["gn"], p["bn"], 1e-12)
+    ln = _ln64(yc, p["gn"], p["bn"], eps)
     assert (xn.double().cpu() - ln).abs().max().item() < 1.6e-2
+
+
+@pytest.mark.parametrize("M", [64, 200, 4100])
+@pytest.mark.parametrize("eps", [1e-12, 1e-5])
+def test_ffn_fused_outproj_qkv(dev, M, eps):
+    """The 128-row kernel's MODE 4 (k_ffn2.hip): the encoder sub-layer tail of test_ffn_fused_outproj and then the
+    NEXT layer's q|k|v = LN1_next(x2) Wq^T + bq (attention.py:180-186 on its norm1) from the LayerNorm output held in
+    registers, vs fp64 on the kernel's own f32 x2 and the bf16 rounding of LN1_next(x2): qkv rel-L2 < 5e-3 (bf16
+    output), x2 as test_ffn_fused_outproj. eps 1e-5 is SenseVoiceSmall's LayerNorm (sense_voice/model.py)."""
+    g = torch.Generator().manual_seed(13 * M + int(eps == 1e-5))
+    p = _ffn_params(g)
+    Wq, bq = torch.randn(1536, 512, generator=g) / 512 ** 0.5, 0.1 * torch.randn(1536, generator=g)
+    x = torch.randn(M, 512, generator=g) * 2
+    o = torch.randn(M, 512, generator=g).bfloat16()
+    f = (0.5 * torch.randn(M, 512, generator=g)).bfloat16()
+    d = lambda t: None if t is None else t.to(dev)  # noqa: E731
+    x2, qkv = rt.op_ffn_op_qkv(d(o), d(f), d(p["Wo"]), d(p["bo"]), d(x), d(p["g2"]), d(p["b2n"]), eps, d(p["W1"]),
+                               d(p["b1"]), d(p["W2"]), d(p["b2"]), d(p["gn"]), d(p["bn"]), d(Wq), d(bq))
+    torch.cuda.synchronize()
+    x1 = o.double() @ p["Wo"].bfloat16().double().T + p["bo"].double() + f.double() + x.double()
+    want = _ffn_ref(x1, p["g2"], p["b2n"], eps, p["W1"].bfloat16(), p["b1"], p["W2"].bfloat16(), p["b2"])
+    yc = x2.double().cpu()
+    assert rel(yc - x1, want - x1) < 5e-3
+    assert rel(yc, want) < 1e-4
+    a = _ln64(yc, p["gn"], p["bn"], eps).bfloat16().double()
+    qw = a @ Wq.bfloat16().double().T + bq.double()
+    assert rel(qkv.double().cpu(), qw) < 5e-3
 
 
 def _dec_ffn_ref(x1, p, eps=1e-12):

@@ -138,6 +138,89 @@ def test_large_exact(sv, name):
         assert _tokens(r) == _tok(g)
 
 
+# ---------------------------------------------------------------- BASELINE config C4 itself
+# sv_large_b64 = the bench's SenseVoice leg (B=64 x 500 frames), sv_large_b24 a ragged batch: reference runs
+# (make_golden.py save_sv_headline). Group rows B/2 x 504 >= 4096 engage the fused out-projection + FFN kernel with
+# SenseVoice's LayerNorm eps 1e-5 through all 70 layers (50 + the 20 tp layers), and the next layer's QKV fold.
+SV_HEADLINE = ["sv_large_b24", "sv_large_b64"]
+# fast-mode frame-decision bounds (tests/fast_parity.py; tools/fast_parity_calib.py, profiles/r04_fast_parity_calib.json):
+# the default fast dispatch gives mean regret 9e-5 nat, flips at 2 % of the frames, 95-96 % of them to the reference's
+# second-best id, max regret 0.024, none outside the top 3; a 0.1-nat perturbation of the CTC head bias gives mean
+# regret 0.034 and 11 % of the frames outside the top 3
+SV_FAST_BOUNDS = dict(mean_regret=1e-3, flip_frac=0.05, outside_frac=1e-3, max_regret=0.1, second_best=0.9)
+
+
+def sv_fast_violations(st, bounds=SV_FAST_BOUNDS):
+    bad = []
+    for k in ("mean_regret", "flip_frac", "max_regret"):
+        if st[k] >= bounds[k]:
+            bad.append(f"{k} {st[k]:.4g} >= {bounds[k]}")
+    if st["outside_topk"] >= bounds["outside_frac"] * st["positions"]:
+        bad.append(f"{st['outside_topk']} frames outside the reference top 3")
+    if st["second_best"] < bounds["second_best"]:
+        bad.append(f"only {st['second_best']:.3f} of the flips to the second-best id")
+    return bad
+
+
+@pytest.mark.parametrize("name", SV_HEADLINE)
+def test_headline_exact(sv, name):
+    """EXACT mode at C4: per-frame CTC argmax identical wherever the reference's top-2 margin is >= 1e-4 (0 flips
+    measured at all), token ids identical, encoder rows < 1e-4 abs and per-utterance sums of squares < 1e-5 rel."""
+    e = sv["large"]
+    g = np.load(f"{GOLD}/{name}.npz")
+    r = _run(e, g, "exact")
+    torch.cuda.synchronize()
+    enc = r["enc"].cpu().numpy()
+    ol = g["enc_lens"]
+    rows = np.stack([enc[b, [0, 3, 4, int(ol[b]) // 2, int(ol[b]) - 1]] for b in range(len(ol))])
+    assert np.abs(rows - g["enc_rows"]).max() < 1e-4
+    for b in range(len(ol)):
+        s = enc[b, : int(ol[b])].astype(np.float64)
+        assert abs((s ** 2).sum() - g["enc_sumsq"][b]) < 1e-5 * g["enc_sumsq"][b]
+    flips = _frames_close(r["frame_ids"].cpu().numpy(), g["frame_ids"], g["lens"], g["margin"])
+    got, want = _tokens(r), _tok(g)
+    bad = [b for b in range(len(want)) if got[b] != want[b]]
+    print(f"{name} exact: {flips} close-call frame flips, {len(bad)} utterances with different tokens")
+    assert flips > 0 or not bad, bad[:5]
+    assert len(bad) <= flips
+
+
+@pytest.mark.parametrize("name", SV_HEADLINE)
+def test_headline_fast_default_dispatch(sv, name):
+    """FAST mode, default dispatch, at C4: encoder rows within bf16 tolerance (rel-L2 < 2e-2) and the CTC frame
+    decisions within SV_FAST_BOUNDS of the reference's own log-probs."""
+    from tests.fast_parity import frame_stats
+    e = sv["large"]
+    g = np.load(f"{GOLD}/{name}.npz")
+    r = _run(e, g, "fast")
+    torch.cuda.synchronize()
+    enc = r["enc"].cpu().numpy()
+    ol = g["enc_lens"]
+    rows = np.stack([enc[b, [0, 3, 4, int(ol[b]) // 2, int(ol[b]) - 1]] for b in range(len(ol))])
+    rel = np.linalg.norm(rows - g["enc_rows"]) / np.linalg.norm(g["enc_rows"])
+    st = frame_stats(r["frame_ids"].cpu().numpy(), ol, g)
+    print(f"{name} fast: enc rows rel-L2 {rel:.2e}; {st}")
+    assert rel < 2e-2, rel
+    assert not sv_fast_violations(st), sv_fast_violations(st)
+
+
+def test_headline_fast_bounds_catch_a_ctc_shift():
+    """The SenseVoice fast bounds can fail: the CTC head bias moved by N(0, 0.1) nat per id breaks them at C4."""
+    from tests.fast_parity import frame_stats
+    cfg = sense_voice_small()
+    w = make_weights(cfg, seed=0)
+    rng = np.random.default_rng(123)
+    w["ctc.ctc_lo.bias"] = (w["ctc.ctc_lo.bias"] + 0.1 * rng.standard_normal(w["ctc.ctc_lo.bias"].shape)).astype(np.float32)
+    e = PfmEngine(cfg, 0)
+    e.load_state_dict(w)
+    g = np.load(f"{GOLD}/sv_large_b64.npz")
+    r = _run(e, g, "fast")
+    torch.cuda.synchronize()
+    st = frame_stats(r["frame_ids"].cpu().numpy(), g["enc_lens"], g)
+    print(f"perturbed CTC head, fast: {st}")
+    assert sv_fast_violations(st), st
+
+
 @pytest.mark.parametrize("name", ["sv_large_ragged"])
 def test_large_fast_agreement(sv, name):
     e = sv["large"]

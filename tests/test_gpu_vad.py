@@ -127,19 +127,90 @@ def test_automodel_vad_asr_punc_pipeline_vs_reference(name):
     want = gj["result"][0]["text"]
     if name == "v1_b4":   # every segment decoded alone: exact
         assert res[0]["text"] == want
-    else:
-        # the three segments in one ragged batch: this GPU batch is bit-faithful to the oracle's batched
-        # semantics (tools/vad_batch_debug.py: alphas within 1.5e-7, tokens equal), but the golden's ASR
-        # frontend is the CPU fbank restatement, 2e-4 from the GPU fbank in log-mel, and one near-tie token
-        # of the random-weight tiny decoder flips: allow an edit distance of 2 characters
-        assert _edit_distance(res[0]["text"], want) <= 2, (res[0]["text"], want)
+        return
+    # v1: the three segments in one ragged batch. The golden's ASR frontend is the CPU fbank restatement (knf), 2e-4
+    # from the GPU fbank in log-mel, which can flip a near-tie token of the random-weight tiny decoder. Split the
+    # pipeline at that seam, each side exact:
+    #   (1) the model alone: the same pipeline (VAD, batching, order restore, join, punctuation) with the ASR model
+    #       replaced by the oracle on the GPU's OWN features of each batch reproduces the HIP pipeline's text exactly;
+    #   (2) the host pipeline alone: with the ASR model replaced by a replay of the reference decoder's own
+    #       per-batch decisions (the golden's asr_calls: token counts and per-position argmax) it reproduces the
+    #       reference's text exactly -- batching, order restore, join and punctuation are the reference's;
+    #   (3) the frontend alone: the decisions of (1) differ from the reference's only where the reference decoder's
+    #       top-2 margin is < 0.5 nat (token counts within +-1), the frontend's documented 2e-4 log-mel tolerance
+    #       (test_gpu_frontend.py).
+    from oracle.paraformer_ref import paraformer_infer
+    from funasr_amd.text import sentence_postprocess
+    w = make_weights(cfg)
+    eng = am.model.engine()
+    hip_front = am.kwargs["frontend"]
+    calls = gj["asr_calls"]
 
+    def gpu_feats(items):
+        speech, lens, _ = hip_front(eng, items)
+        torch.cuda.synchronize()
+        return speech.cpu().numpy(), lens.cpu().numpy()
 
-def _edit_distance(a, b):
-    d = list(range(len(b) + 1))
-    for i in range(1, len(a) + 1):
-        prev, d[0] = d[0], i
-        for j in range(1, len(b) + 1):
-            cur = min(d[j] + 1, d[j - 1] + 1, prev + (a[i - 1] != b[j - 1]))
-            prev, d[j] = d[j], cur
-    return d[len(b)]
+    def texts(batch_ids, key, n, tokenizer):
+        return [{"key": (key or [f"utt{i}"] * n)[i],
+                 "text": sentence_postprocess(tokenizer.ids2tokens(ids))[0]} for i, ids in enumerate(batch_ids)]
+
+    class OracleASR(torch.nn.Module):
+        """The oracle Paraformer on the GPU frontend's features, behind the HIP model's inference contract."""
+
+        def __init__(self):
+            super().__init__()
+            self.runs = []
+
+        def inference(self, data_in, data_lengths=None, key=None, tokenizer=None, frontend=None, **kw):
+            x, lens = gpu_feats(data_in if isinstance(data_in, (list, tuple)) else [data_in])
+            r = paraformer_infer(x, lens, w, cfg, keep_logits=True)
+            self.runs.append(r)
+            return texts(r["tokens"], key, len(lens), tokenizer), {}
+
+    class ReplayASR(torch.nn.Module):
+        """The reference decoder's recorded decisions, batch by batch, behind the same contract."""
+
+        def __init__(self):
+            super().__init__()
+            self.i = 0
+
+        def inference(self, data_in, data_lengths=None, key=None, tokenizer=None, frontend=None, **kw):
+            c = calls[self.i]
+            self.i += 1
+            n = len(data_in) if isinstance(data_in, (list, tuple)) else 1
+            assert n == len(c["ntok"])        # the same batch plan as the reference's
+            off = np.concatenate([[0], np.cumsum(c["ntok"])])
+            ids = [[t for t in c["argmax"][off[b]:off[b + 1]] if t not in (cfg.eos, cfg.sos, cfg.blank_id)]
+                   for b in range(n)]
+            return texts(ids, key, n, tokenizer), {}
+
+    hip_model = am.model
+    try:
+        am.model = OracleASR()
+        alone = am.generate(input=wav, batch_size_s=gj["batch_size_s"])[0]["text"]
+        runs_gpu = am.model.runs
+        am.model = ReplayASR()
+        host = am.generate(input=wav, batch_size_s=gj["batch_size_s"])[0]["text"]
+        assert am.model.i == len(calls)
+    finally:
+        am.model = hip_model
+    assert alone == res[0]["text"], (alone, res[0]["text"])          # (1)
+    assert host == want, (host, want)                                 # (2)
+    assert len(runs_gpu) == len(calls)                                # (3)
+    flips, worst = 0, 0.0
+    for rg, c in zip(runs_gpu, calls):
+        off = np.concatenate([[0], np.cumsum(c["ntok"])])
+        for b, nb in enumerate(c["ntok"]):
+            na = int(rg["ntok"][b])
+            assert abs(na - nb) <= 1
+            if na != nb:
+                continue
+            ref = np.asarray(c["argmax"][off[b]:off[b + 1]])
+            bad = np.nonzero(rg["argmax"][b, :na].numpy() != ref)[0]
+            flips += len(bad)
+            if len(bad):
+                worst = max(worst, float(np.asarray(c["margin"][off[b]:off[b + 1]])[bad].max()))
+    print(f"VAD pipeline v1: GPU vs reference features flip {flips} tokens, largest reference margin {worst:.4f} "
+          f"nat; pipeline {res[0]['text']!r} vs reference {want!r}")
+    assert worst < 0.5

@@ -54,14 +54,14 @@ int main(int argc, char** argv) {
     for (int i = 1; i < argc; ++i) Ms.push_back(atoi(argv[i]));
     if (Ms.empty()) Ms = {16000, 32000};
     const int Mmax = 32768;
-    const long long nx = (long long)Mmax * 512, nw = 262144 + 2097152;
+    const long long nx = (long long)Mmax * 512, nw = 262144 + 2097152 + 3 * 262144;
     float *X, *Xo, *vecs;
     bf16 *Wp, *O, *Fr, *Xn;
     CK(hipMalloc(&X, nx * 4));
     CK(hipMalloc(&Xo, nx * 4));
     CK(hipMalloc(&O, nx * 2));
     CK(hipMalloc(&Fr, nx * 2));
-    CK(hipMalloc(&Xn, nx * 2));
+    CK(hipMalloc(&Xn, nx * 2 * 3));
     CK(hipMalloc(&Wp, nw * 2));
     CK(hipMalloc(&vecs, 16 * 2048 * 4));
     hipLaunchKernelGGL(fill_f32, dim3((nx + 255) / 256), dim3(256), 0, 0, X, nx, 1u, 4.f, 0.f);
@@ -96,6 +96,8 @@ int main(int argc, char** argv) {
         printf("M=%6d OP   burst DMA   %8.1f us\n", M, t);
         t = run<1, 5>(M, reps, X, g, be, Wp, b1, b2, Xo, gn, bn, Xn, O, Fr, bo, c1);
         printf("M=%6d OP   pro/epi     %8.1f us\n", M, t);
+        t = run<4, 0>(M, reps, X, g, be, Wp, b1, b2, Xo, gn, bn, Xn, O, Fr, bo, c1);
+        printf("M=%6d OP+QKV full      %8.1f us  %7.1f TF/s\n", M, t, (fl1 + 2.0 * M * 1536 * 512) / t / 1e6);
         t = run<0, 0>(M, reps, X, g, be, Wp + 262144, b1, b2, Xo, gn, bn, Xn, O, Fr, bo, c1);
         printf("M=%6d FFN  full        %8.1f us  %7.1f TF/s\n", M, t, fl0 / t / 1e6);
         t = run<2, 0>(M, reps, X, g, be, Wp + 262144, b1, b2, Xo, gn, bn, Xn, O, Fr, bo, c1);
