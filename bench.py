@@ -410,15 +410,13 @@ def main():
                  if min(na[i], nb[i]) > 0]
         fl_ex = path_flops(T, nb)
         x6 = os.environ.get("PFM_EXACT_X6", "1") != "0"
-        terms = 3 if os.environ.get("PFM_EXACT_TERMS", "6") == "3" else 6
+        terms = 6
         tf_ex = fl_ex / dte / 1e12
         out["exact_mode"] = {
             "value": round(B * T * FRAME_SEC / dte, 1), "ms_per_step": round(dte * 1e3, 2), "dtype": "f32",
             "token_exact": True,   # token ids identical to the reference on every golden (tests/test_gpu_parity.py)
-            "arithmetic": (("split-bf16 x6 MFMA (x = x0+x1+x2 bf16, six products, f32 accumulate) for every GEMM "
-                            "and the attention") if x6 and terms == 6 else
-                           ("split-bf16 GEMMs with three products (bf16x3: a0b0 + a0b1 + a1b0), x6 attention")
-                           if x6 else "v_mfma_f32_32x32x2_f32"),
+            "arithmetic": ("split-bf16 x6 MFMA (x = x0+x1+x2 bf16, six products, f32 accumulate) for every GEMM "
+                           "and the attention" if x6 else "v_mfma_f32_32x32x2_f32"),
             "path_tflops_f32_equiv": round(tf_ex, 2),
             "path_roofline": ({"bound": "mfma", "achieved": round(terms * tf_ex, 2), "peak": PEAK_TFLOPS["fast"],
                                "unit": f"TFLOP/s (bf16 MFMA issued: about {terms} x f32-equivalent)",

@@ -409,84 +409,6 @@ __global__ __launch_bounds__(256) void fsmn_ln_kernel(const TIN* __restrict__ v,
     }
 }
 
-__device__ __forceinline__ float bf_lo(unsigned u) { return __uint_as_float(u << 16); }
-__device__ __forceinline__ float bf_hi(unsigned u) { return __uint_as_float(u & 0xffff0000u); }
-__device__ __forceinline__ void fma8(float4 a, float4 b, uint4 u, float (&y)[8]) {
-    y[0] = fmaf(a.x, bf_lo(u.x), y[0]); y[1] = fmaf(a.y, bf_hi(u.x), y[1]);
-    y[2] = fmaf(a.z, bf_lo(u.y), y[2]); y[3] = fmaf(a.w, bf_hi(u.y), y[3]);
-    y[4] = fmaf(b.x, bf_lo(u.z), y[4]); y[5] = fmaf(b.y, bf_hi(u.z), y[5]);
-    y[6] = fmaf(b.z, bf_lo(u.w), y[6]); y[7] = fmaf(b.w, bf_hi(u.w), y[7]);
-}
-
-// bf16-input variant with 8 channels per lane: 16-B window loads (one wave = one 512-channel row
-// per load instruction), the window kept packed in registers (masked frames zeroed once), taps
-// staged in LDS once per block (the block's waves share the channel range), tap-outer / frame-inner
-// accumulation so only one tap's 8 weights are live, 16-B bf16 stores. FRW frames per thread.
-template <int KK, int FRW>
-__global__ __launch_bounds__(256) void fsmn_win8_kernel(const bf16* __restrict__ v, RowMap vmap,
-                                                        const int* __restrict__ len, int B, int T, int D,
-                                                        const float* __restrict__ wT, int left,
-                                                        float* __restrict__ out, bf16* __restrict__ out_bf) {
-    extern __shared__ float wsm[];   // [KK][D]; tap `left` carries the "+ inputs" term as +1 (fast mode only:
-                                     // (w+1)x instead of wx + x, and no runtime-indexed window read)
-    for (int e = threadIdx.x * 4; e < KK * D; e += blockDim.x * 4) {
-        float4 t = *(const float4*)(wT + e);
-        if (e / D == left) { t.x += 1.f; t.y += 1.f; t.z += 1.f; t.w += 1.f; }
-        *(float4*)(wsm + e) = t;
-    }
-    __syncthreads();
-    const int qpr = D / 8;
-    const int nblk = (T + FRW - 1) / FRW;
-    const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (gid >= (long long)B * nblk * qpr) return;
-    const int c = (int)(gid % qpr) * 8;
-    const long long rb = gid / qpr;
-    const int b = (int)(rb / nblk), t0 = (int)(rb % nblk) * FRW;
-    const int L = min(len[b], T);
-    const long long ubase = vmap.rows_per_seg > 0 ? (long long)b * vmap.seg_stride : (long long)b * T * vmap.ld;
-    // window as raw 32-bit words (2 bf16 each): masking is an AND, widening a shift / mask
-    uint4 x[FRW + KK - 1];
-#pragma unroll
-    for (int i = 0; i < FRW + KK - 1; ++i) {
-        const int tc = min(max(t0 - left + i, 0), T - 1);
-        x[i] = *(const uint4*)(v + ubase + (long long)tc * vmap.ld + c);
-    }
-#pragma unroll
-    for (int i = 0; i < FRW + KK - 1; ++i) {
-        const int tt = t0 - left + i;
-        const unsigned m = (tt < 0 || tt >= L) ? 0u : 0xffffffffu;
-        x[i].x &= m; x[i].y &= m; x[i].z &= m; x[i].w &= m;
-    }
-    float y[FRW][8];
-#pragma unroll
-    for (int i = 0; i < FRW; ++i)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) y[i][j] = 0.f;
-#pragma unroll
-    for (int k = 0; k < KK; ++k) {
-        const float4 a = *(const float4*)(wsm + k * D + c), bq = *(const float4*)(wsm + k * D + c + 4);
-#pragma unroll
-        for (int i = 0; i < FRW; ++i) fma8(a, bq, x[i + k], y[i]);
-    }
-#pragma unroll
-    for (int i = 0; i < FRW; ++i) {
-        const int t = t0 + i;
-        if (t >= T) break;
-        float o[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) o[j] = t < L ? y[i][j] : 0.f;
-        const long long row = (long long)b * T + t;
-        if (out) {
-            *(float4*)(out + row * D + c) = make_float4(o[0], o[1], o[2], o[3]);
-            *(float4*)(out + row * D + c + 4) = make_float4(o[4], o[5], o[6], o[7]);
-        }
-        if (out_bf) {
-            bf16x8 tb = {f2bf(o[0]), f2bf(o[1]), f2bf(o[2]), f2bf(o[3]), f2bf(o[4]), f2bf(o[5]), f2bf(o[6]), f2bf(o[7])};
-            *(bf16x8*)(out_bf + row * D + c) = tb;
-        }
-    }
-}
-
 // ------------------------------------------------------------------------------------------
 // CIF predictor head (cif_predictor.py:214-242, 346-370):
 //   alpha[t] = relu(sigmoid(w . relu(conv)[t] + b) * smooth - noise) * mask[t],  t < T
@@ -834,25 +756,6 @@ hipError_t pfm_fsmn_bf16in(const bf16* v, RowMap vmap, const int* len, int B, in
     if (B <= 0 || T <= 0) return hipSuccess;
     if (D % 4 != 0 || K != 11 || left < 0 || left >= K) return hipErrorInvalidValue;
     if (vmap.rows_per_seg > 0 && vmap.rows_per_seg != T) return hipErrorInvalidValue;
-    // PFM_FSMN_V2: frames per thread of the 8-channel kernel (0 = 4-channel kernel);
-    const int frw = pfm_knobs().fsmn_v2;   // measured: the 4-channel kernel with static LEFT is fastest
-    if (!res && D % 8 == 0 && vmap.ld % 8 == 0 && (vmap.rows_per_seg <= 0 || vmap.seg_stride % 8 == 0) &&
-        ((uintptr_t)v % 16) == 0 && (!out_bf || ((uintptr_t)out_bf % 16) == 0) && (!out || ((uintptr_t)out % 16) == 0) &&
-        (frw == 4 || frw == 8 || frw == 16) && 11 * D * 4 <= 64 * 1024) {
-        const int fr = frw;
-        const long long n = (long long)B * ((T + fr - 1) / fr) * (D / 8);
-        if (fr == 4)
-            hipLaunchKernelGGL((fsmn_win8_kernel<11, 4>), dim3((unsigned)((n + 255) / 256)), dim3(256), 11 * D * 4, st, v,
-                               vmap, len, B, T, D, wT, left, out, out_bf);
-        else if (fr == 8)
-            hipLaunchKernelGGL((fsmn_win8_kernel<11, 8>), dim3((unsigned)((n + 255) / 256)), dim3(256), 11 * D * 4, st, v, vmap,
-                               len, B, T, D, wT, left, out, out_bf);
-        else
-            hipLaunchKernelGGL((fsmn_win8_kernel<11, 16>), dim3((unsigned)((n + 255) / 256)), dim3(256), 11 * D * 4, st, v,
-                               vmap, len, B, T, D, wT, left, out, out_bf);
-        PFM_LAUNCH_CHECK();
-        return hipSuccess;
-    }
     const long long n = (long long)B * ((T + FR - 1) / FR) * (D / 4);
     if (left == 5)
         hipLaunchKernelGGL((fsmn_win_kernel<11, bf16, 5>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, v, vmap,

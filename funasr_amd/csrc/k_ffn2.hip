@@ -1,11 +1,10 @@
-// Fused SAN-M feed-forward sub-layer, 128 rows per workgroup (gfx950, fast mode). Same four modes and the
-// same arithmetic as k_ffn.hip (see there for the reference citations):
+// Fused SAN-M encoder feed-forward sub-layer, 128 rows per workgroup (gfx950, fast mode). The encoder modes of
+// k_ffn.hip with the same arithmetic (see there for the reference citations), plus the next layer's QKV:
 //   MODE 0  encoder:       x2 = x + W2 relu(W1 LN2(x) + b1) + b2                 (sanm/encoder.py:138-145)
 //   MODE 1  encoder + OP:  x1 = O Wo^T + bo + F (+ x), then MODE 0 on x1          (sanm/encoder.py:120-145)
-//   MODE 2  decoder FFN:   y = W2 LN_F(relu(W1 LN1(x) + b1)), LN_F folded through W2
-//                          (sanm/positionwise_feed_forward.py:12-33)
-//   MODE 3  decoder + OP:  x1 = x + O Wo^T + bo -> xo, then MODE 2 on x1         (paraformer/decoder.py:97-119)
-// with the next LayerNorm of the result as a bf16 output (the consumer GEMM's operand).
+//   MODE 4  MODE 1, then the next layer's q|k|v = LN1_next(x2) Wqkv^T + bq        (sanm/attention.py:275-288)
+// with the next LayerNorm of the result as a bf16 output (the consumer GEMM's operand; MODE 4: the QKV rows).
+// (The decoder FFN runs on k_ffn.hip: its 128-row form here measured slower end to end and was removed.)
 //
 // Why a second kernel: k_ffn.hip owns 64 rows per workgroup, so every workgroup streams all 4.5 MB of the
 // layer's weights through L2 -> LDS for 64 rows (64 FLOP per weight byte), and its A / H images fill the LDS
@@ -58,11 +57,11 @@ constexpr int PD = 6;                    // fragment reads in flight ahead of th
 constexpr int OPI = FFN2_OPI;                   // phase-0 output blocks interleaved per k step (1 = back-to-back chains)
 constexpr int NB = 8;                    // fragment register slots (divides TF, CHF and OPF)
 // per-column vectors staged in LDS behind the ring (float offsets)
-constexpr int V_G = 0, V_B = 512, V_C2 = 1024, V_GN = 1536, V_BN = 2048, V_BO = 2560, V_C1 = 3072, V_B1 = 3584;
+constexpr int V_G = 0, V_B = 512, V_C2 = 1024, V_GN = 1536, V_BN = 2048, V_BO = 2560, V_B1 = 3072;
 constexpr int QKF = 3 * OPF;             // MODE 4 phase 3: the next layer's Wqkv, three passes of 512 output features
 constexpr int V_BQ = V_B1 + FF;          // MODE 4: the next layer's q|k|v biases
 constexpr int NVEC = V_BQ + 3 * FD;
-constexpr int LDS_BYTES = RING + NVEC * 4;   // 159,744 B
+constexpr int LDS_BYTES = RING + NVEC * 4;   // 157,696 B
 static_assert(LDS_BYTES <= 163840, "LDS plan");
 static_assert(PD < TF && TF % NB == 0 && CHF % NB == 0 && OPF % NB == 0 && PD < NB, "stream plan");
 
@@ -171,8 +170,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int r = lane & 31, h = lane >> 5;
-    constexpr bool OP = MODE == 1 || MODE == 3 || MODE == 4, DEC = MODE == 2 || MODE == 3;
-    constexpr bool EOP = MODE == 1 || MODE == 4, QK = MODE == 4;   // encoder out-projection; + the next QKV
+    static_assert(MODE == 0 || MODE == 1 || MODE == 4, "encoder modes");
+    constexpr bool OP = MODE == 1 || MODE == 4, QK = MODE == 4;   // encoder out-projection; + the next QKV
     constexpr int F0 = OP ? OPF : 0, F3 = F0 + NCH * CHF, NF = F3 + (QK ? QKF : 0), NT = NF / TF;
     const long long rg = (long long)blockIdx.x * BM + 32 * w + r;   // this lane's row
     const bool live = rg < M;
@@ -185,7 +184,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         vec[V_C2 + i] = b2[i];
         if (Xn) { vec[V_GN + i] = gn[i]; vec[V_BN + i] = bn[i]; }
         if constexpr (OP) vec[V_BO + i] = bo[i];
-        if constexpr (DEC) vec[V_C1 + i] = c1[i];
     }
     for (int i = tid; i < FF; i += 256) vec[V_B1 + i] = b1[i];
     if constexpr (QK)
@@ -386,7 +384,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         for (int ks = 0; ks < 32; ++ks) act[ks] = *(const bf16x8*)(O + rc * FD + 16 * ks + 8 * h);
     } else {
         // the row into the accumulators (batched loads), its LayerNorm -> act, then the accumulator start
-        // (MODE 0: x + b2, the residual the FFN output lands on; DEC: 0)
+        // (x + b2, the residual the FFN output lands on)
         add_rows(true, X, FD, 1.f, nullptr, -1);
         float mean, rstd;
         acc_stats(mean, rstd);
@@ -395,7 +393,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
             fence();
             const f32x16 t = acc_get(ob);
             ln_block(ob, t, mean, rstd);
-            acc_c2(ob, t, MODE == 0);
+            acc_c2(ob, t, true);
         }
         fence();
     }
@@ -446,30 +444,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(wf[0]), "+v"(wf[1]), "+v"(wf[2]), "+v"(wf[3]), "+v"(wf[4]),
                      "+v"(wf[5]), "+v"(wf[6]), "+v"(wf[7]));
         xdl_drain(acc);
-        // x1 = ((Y0 + bo) + F) + x (the separate GEMM epilogue's order; layer 0: no x, the decoder: no F)
-        add_rows(false, X ? X : bo, X ? FD : 0, X ? 1.f : 0.f, EOP ? Fr : nullptr, V_BO);
-        if constexpr (MODE == 3) {   // the decoder keeps x1 (its FSMN step adds to it)
-            if (live) {
-#pragma unroll
-                for (int ob = 0; ob < 16; ++ob) {
-                    fence();
-                    const f32x16 t = acc_get(ob);
-#pragma unroll
-                    for (int q = 0; q < 4; ++q)
-                        *(float4*)(Xo + rg * FD + 32 * ob + 8 * q + 4 * h) =
-                            make_float4(t[4 * q], t[4 * q + 1], t[4 * q + 2], t[4 * q + 3]);
-                }
-                fence();
-            }
-        }
+        // x1 = ((Y0 + bo) + F) + x (the separate GEMM epilogue's order; layer 0: no x)
+        add_rows(false, X ? X : bo, X ? FD : 0, X ? 1.f : 0.f, Fr, V_BO);
         float mean, rstd;
         acc_stats(mean, rstd);
 #pragma unroll
-        for (int ob = 0; ob < 16; ++ob) {   // LN2(x1) -> act; accumulators: x1 + b2 (encoder) / 0 (decoder)
+        for (int ob = 0; ob < 16; ++ob) {   // LN2(x1) -> act; accumulators: x1 + b2
             fence();
             const f32x16 t = acc_get(ob);
             ln_block(ob, t, mean, rstd);
-            acc_c2(ob, t, EOP);
+            acc_c2(ob, t, true);
         }
         fence();
     }
@@ -484,7 +468,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     valu_to_mfma();
 
     // ---- the FFN stream (see the header): head P1(0), bodies c = 0..62 (P1(c+1) under P2(c)), tail P2(63)
-    float rs = 0.f, rq = 0.f;   // DEC: sum / sum of squares of this lane's bf16 hidden values
     f32x16 acc1a, acc1b;        // phase 1 of one chunk as two accumulator chains (even / odd k steps)
     bf16x8 hfa[2], hfb[2];      // phase 2's B operand (hidden k steps 0, 1) of even / odd chunks
     f32x4 bq[4];                // b1 of the chunk being activated: features 8q + 4h .. +3 (accumulator register groups)
@@ -513,19 +496,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         asm volatile("s_waitcnt lgkmcnt(6)" : "+v"(bq[0]), "+v"(bq[1]), "+v"(bq[2]), "+v"(bq[3]));
         __builtin_amdgcn_sched_barrier(0);
     };
-    // relu((H_a + H_b) + b1) -> bf16 for register group q (4 features) into hb; DEC: the hidden's running statistics
+    // relu((H_a + H_b) + b1) -> bf16 for register group q (4 features) into hb
     auto relu_q = [&](int q, bf16x8 (&hb)[2]) __attribute__((always_inline)) {
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const bf16 v = f2bf(fmaxf((acc1a[4 * q + i] + acc1b[4 * q + i]) + bq[q][i], 0.f));
-            hb[q >> 1][4 * (q & 1) + i] = v;
-            if constexpr (DEC) {
-                const float fv = bf2f(v);
-                rs += fv;
-                rq += fv * fv;
-            }
-        }
+        for (int i = 0; i < 4; ++i) hb[q >> 1][4 * (q & 1) + i] = f2bf(fmaxf((acc1a[4 * q + i] + acc1b[4 * q + i]) + bq[q][i], 0.f));
         // pin the packed bf16 here: left alone, instruction selection sinks the v_cvt_pk_bf16_f32 next to the operand's
         // first MFMA, past every scheduling fence, with no wait state between the VALU write and the MFMA read
         asm volatile("" : "+v"(hb[q >> 1]));
@@ -573,27 +548,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     xdl_drain(acc);
 
     // ---- epilogue (no DMA in flight: the last tiles were waited for by their tops)
-    if constexpr (DEC) {   // y = rstd_h (W2g h - mu_h c1) + c2 ; the hidden's statistics over both lane halves
-        rs += __shfl_xor(rs, 32, 64);
-        rq += __shfl_xor(rq, 32, 64);
-        const float mu = rs * (1.f / FF);
-        const float var = fmaxf(rq * (1.f / FF) - mu * mu, 0.f);
-        const float rh = 1.f / sqrtf(var + eps);
-#pragma unroll
-        for (int ob = 0; ob < 16; ++ob) {
-            fence();
-            f32x16 t = acc_get(ob);
-            f32x4 C1[4], C2[4];
-            vec_block(V_C1, V_C2, ob, C1, C2);
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-#pragma unroll
-                for (int i = 0; i < 4; ++i) t[4 * q + i] = rh * (t[4 * q + i] - mu * C1[q][i]) + C2[q][i];
-            acc_put(ob, t);
-        }
-        fence();
-    }
-    if (live && Xo && MODE != 3) {
+    if (live && Xo) {
 #pragma unroll
         for (int ob = 0; ob < 16; ++ob) {
             fence();
@@ -696,7 +651,7 @@ __device__ __forceinline__ int perm_k(int s, int hh, int j) { return 16 * s + 8 
 
 // FFN stream position q (0..4095, see the header) -> hidden chunk c, W1 (P1) or W2 (P2) fragment, index j:
 // P1 j = W1 rows [32c, 32c+32) x k step j of the 512 inputs (permuted k); P2 j = W2 rows [32 (j & 15), +32) x hidden
-// k step j >> 4 of the chunk's 32 hidden (permuted). DEC: the W2 fragments hold bf16(W2 gamma_F) from the f32 W2.
+// k step j >> 4 of the chunk's 32 hidden (permuted).
 __device__ __forceinline__ void ffn2_stream_frag(int q, int& c, bool& w1, int& j) {
     constexpr int TAIL = 32 + (NCH - 1) * CHF;
     if (q < 32) { c = 0; w1 = true; j = q; return; }
@@ -711,8 +666,7 @@ __device__ __forceinline__ void ffn2_stream_frag(int q, int& c, bool& w1, int& j
     }
 }
 
-__global__ __launch_bounds__(256) void ffn2_pack_kernel(const bf16* __restrict__ W1, const bf16* __restrict__ W2b,
-                                                        const float* __restrict__ W2f, const float* __restrict__ gF,
+__global__ __launch_bounds__(256) void ffn2_pack_kernel(const bf16* __restrict__ W1, const bf16* __restrict__ W2,
                                                         bf16* __restrict__ Wp) {
     const int gid = blockIdx.x * 256 + threadIdx.x;   // < NCH * CHF * 64
     const int f = gid >> 6, l = gid & 63, m = l & 31, hh = l >> 5;
@@ -728,10 +682,7 @@ __global__ __launch_bounds__(256) void ffn2_pack_kernel(const bf16* __restrict__
         const int ob = j & 15, s = j >> 4;
         const long long rowb = (long long)(32 * ob + m) * FF + HC * c;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-            const int k = perm_k(s, hh, e);
-            o[e] = W2f ? f2bf(W2f[rowb + k] * gF[HC * c + k]) : W2b[rowb + k];
-        }
+        for (int e = 0; e < 8; ++e) o[e] = W2[rowb + perm_k(s, hh, e)];
     }
     *(bf16x8*)(Wp + (long long)gid * 8) = o;
 }
@@ -760,27 +711,6 @@ __global__ __launch_bounds__(256) void ffn2_pack_qkv_kernel(const bf16* __restri
     *(bf16x8*)(Wp + (long long)gid * 8) = o;
 }
 
-// c1[o] = sum_k bf16(W2[o][k] g[k]) (the packed values), c2[o] = sum_k W2[o][k] b[k]; one block per output row
-__global__ __launch_bounds__(256) void ffn2_dec_consts_kernel(const float* __restrict__ W2, const float* __restrict__ gF,
-                                                              const float* __restrict__ bF, float* __restrict__ c1,
-                                                              float* __restrict__ c2) {
-    __shared__ float r1[256], r2[256];
-    const int o = blockIdx.x, t = threadIdx.x;
-    float s1 = 0.f, s2 = 0.f;
-    for (int k = t; k < FF; k += 256) {
-        const float wv = W2[(long long)o * FF + k];
-        s1 += bf2f(f2bf(wv * gF[k]));
-        s2 += wv * bF[k];
-    }
-    r1[t] = s1; r2[t] = s2;
-    __syncthreads();
-    for (int n = 128; n > 0; n >>= 1) {
-        if (t < n) { r1[t] += r1[t + n]; r2[t] += r2[t + n]; }
-        __syncthreads();
-    }
-    if (t == 0) { c1[o] = r1[0]; c2[o] = r2[0]; }
-}
-
 template <int MODE>
 hipError_t ffn2_launch(hipStream_t st, int M, const float* x, const float* g, const float* be, float eps, const bf16* Wp,
                        const float* b1, const float* b2, float* xo, const float* gn, const float* bn, bf16* xn,
@@ -805,7 +735,7 @@ static_assert((size_t)NCH * CHF * FE == (size_t)2048 * 1024, "FFN pack size");
 static_assert((size_t)OPF * FE == (size_t)512 * 512, "Wo pack size");
 
 hipError_t pfm_ffn2_pack(const bf16* W1, const bf16* W2, bf16* Wp, hipStream_t st) {
-    hipLaunchKernelGGL(ffn2_pack_kernel, dim3(NCH * CHF * 64 / 256), dim3(256), 0, st, W1, W2, nullptr, nullptr, Wp);
+    hipLaunchKernelGGL(ffn2_pack_kernel, dim3(NCH * CHF * 64 / 256), dim3(256), 0, st, W1, W2, Wp);
     PFM_LAUNCH_CHECK();
     return hipSuccess;
 }
@@ -823,16 +753,7 @@ hipError_t pfm_ffn2_pack_o(const bf16* Wo, bf16* Wp, hipStream_t st) {
     return hipSuccess;
 }
 
-hipError_t pfm_ffn2_pack_dec(const bf16* W1, const float* W2, const float* gF, const float* bF, bf16* Wp, float* c1,
-                             float* c2, hipStream_t st) {
-    hipLaunchKernelGGL(ffn2_pack_kernel, dim3(NCH * CHF * 64 / 256), dim3(256), 0, st, W1, nullptr, W2, gF, Wp);
-    PFM_LAUNCH_CHECK();
-    hipLaunchKernelGGL(ffn2_dec_consts_kernel, dim3(FD), dim3(256), 0, st, W2, gF, bF, c1, c2);
-    PFM_LAUNCH_CHECK();
-    return hipSuccess;
-}
-
-// Same contracts as pfm_ffn_fused / pfm_ffn_fused_op / pfm_ffn_fused_dec (k_ffn.hip), pfm_ffn2_pack* weights.
+// Same contracts as pfm_ffn_fused / pfm_ffn_fused_op (k_ffn.hip), pfm_ffn2_pack* weights.
 hipError_t pfm_ffn2_fused(const float* x, int M, const float* g2, const float* be2, float eps, const bf16* Wp,
                           const float* b1, const float* b2, float* xo, const float* gn, const float* bn, bf16* xn,
                           hipStream_t st) {
@@ -862,15 +783,4 @@ hipError_t pfm_ffn2_fused_op_qkv(const bf16* o, const bf16* f, const float* bo, 
     if (!al16(x) || !al16(xo) || !al16(Wop) || !al16(qkv) || !al16(o) || !al16(f) || !al16(bo) || !al16(bq))
         return hipErrorInvalidValue;
     return ffn2_launch<4>(st, M, x, g2, be2, eps, Wop, b1, b2, xo, gn, bn, qkv, o, f, bo, bq);
-}
-
-hipError_t pfm_ffn2_fused_dec(const float* x, int M, const float* g1, const float* be1, float eps, const bf16* Wp,
-                              const float* b1, const float* c1, const float* c2, float* xo, const float* gn,
-                              const float* bn, bf16* xn, const bf16* o, const float* bo, hipStream_t st) {
-    if (M <= 0) return hipSuccess;
-    if (!xn || !gn || !bn || !c1 || !c2 || !x || (o && (!bo || !xo))) return hipErrorInvalidValue;
-    if (!al16(x) || !al16(xo) || !al16(Wp) || !al16(xn) || !al16(c1) || !al16(c2) || !al16(o) || !al16(bo))
-        return hipErrorInvalidValue;
-    if (o) return ffn2_launch<3>(st, M, x, g1, be1, eps, Wp, b1, c2, xo, gn, bn, xn, o, nullptr, bo, c1);
-    return ffn2_launch<2>(st, M, x, g1, be1, eps, Wp, b1, c2, xo, gn, bn, xn, nullptr, nullptr, nullptr, c1);
 }

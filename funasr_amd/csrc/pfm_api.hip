@@ -85,20 +85,15 @@ hipError_t pfm_ffn_fused_dec(const float* x, int M, const float* g1, const float
                              const float* b1, const float* c1, const float* c2, float* xo, const float* gn,
                              const float* bn, bf16* xn, const bf16* o, const float* bo, hipStream_t st);
 hipError_t pfm_ffn_pack_o(const bf16* Wo, bf16* Wp, hipStream_t st);
-// k_ffn2.hip: the same fused sub-layers at 128 rows per workgroup (same packed sizes, its own fragment order)
+// k_ffn2.hip: the encoder's fused sub-layers at 128 rows per workgroup (same packed sizes, its own fragment order)
 hipError_t pfm_ffn2_pack(const bf16* W1, const bf16* W2, bf16* Wp, hipStream_t st);
 hipError_t pfm_ffn2_pack_o(const bf16* Wo, bf16* Wp, hipStream_t st);
-hipError_t pfm_ffn2_pack_dec(const bf16* W1, const float* W2, const float* gF, const float* bF, bf16* Wp, float* c1,
-                             float* c2, hipStream_t st);
 hipError_t pfm_ffn2_fused(const float* x, int M, const float* g2, const float* be2, float eps, const bf16* Wp,
                           const float* b1, const float* b2, float* xo, const float* gn, const float* bn, bf16* xn,
                           hipStream_t st);
 hipError_t pfm_ffn2_fused_op(const bf16* o, const bf16* f, const float* bo, const float* x, int M, const float* g2,
                              const float* be2, float eps, const bf16* Wop, const float* b1, const float* b2, float* xo,
                              const float* gn, const float* bn, bf16* xn, hipStream_t st);
-hipError_t pfm_ffn2_fused_dec(const float* x, int M, const float* g1, const float* be1, float eps, const bf16* Wp,
-                              const float* b1, const float* c1, const float* c2, float* xo, const float* gn,
-                              const float* bn, bf16* xn, const bf16* o, const float* bo, hipStream_t st);
 hipError_t pfm_ffn_fused_op(const bf16* o, const bf16* f, const float* bo, const float* x, int M, const float* g2,
                             const float* be2, float eps, const bf16* Wop, const float* b1, const float* b2, float* xo,
                             const float* gn, const float* bn, bf16* xn, hipStream_t st);
@@ -168,13 +163,11 @@ void pfm_knobs_refresh() {
         return (e && e[0]) ? atoi(e) : dflt;
     };
     PfmKnobs k;
-    k.gemm_kernel = iv("PFM_GEMM_KERNEL", 0);
     k.attn_fsmn = iv("PFM_ATTN_FSMN", 1) != 0;
     k.attn_waves = iv("PFM_ATTN_WAVES", 8);
     k.kv_overlap = iv("PFM_KV_OVERLAP", 1) != 0;
     k.subbatch = std::max(1, std::min(iv("PFM_SUBBATCH", 2), 4));
     k.stream_graph = iv("PFM_STREAM_GRAPH", 1) != 0;
-    k.fsmn_v2 = iv("PFM_FSMN_V2", 0);
     k.gemm_gm = iv("PFM_GEMM_GM", -1);
     k.gemm_cfg = iv("PFM_GEMM_CFG", 0);
     k.gemm_st16 = iv("PFM_GEMM_ST16", 1) != 0;
@@ -186,10 +179,8 @@ void pfm_knobs_refresh() {
     k.ffn_op = iv("PFM_FFN_OP", 1) != 0;
     k.dec_ffn_fused = iv("PFM_DEC_FFN_FUSED", 1) != 0;
     k.ffn_kernel = iv("PFM_FFN_KERNEL", 2) == 1 ? 1 : 2;
-    k.dec_ffn_kernel = iv("PFM_DEC_FFN_KERNEL", 1) == 2 ? 2 : 1;
-    k.exact_terms = iv("PFM_EXACT_TERMS", 6) == 3 ? 3 : 6;
     k.ffn_qkv = iv("PFM_FFN_QKV", 1) != 0;
-    const int* f = &k.gemm_kernel;
+    const int* f = &k.attn_fsmn;
     unsigned long long s = 1469598103934665603ull;   // FNV-1a over the fields
     for (int i = 0; i < PFM_KNOB_FIELDS; ++i) s = (s ^ (unsigned long long)(unsigned)f[i]) * 1099511628211ull;
     k.sig = s;
@@ -258,10 +249,10 @@ struct pfm_handle {
     DevBuf ffn_pack;               // fused-FFN weight tiles of every encoder layer (bf16, LDS-image order)
     bool ffn_ready = false;
     DevBuf logits, ctcx, beam_fs, beam_is;   // pfm_run_beam: decoder / CTC log-probs and the search's scratch
+    DevBuf beam_nf;                          // pfm_stream_step_beam: CIF fire counts when the caller passes none
     bool want_logits = false;      // set by pfm_run_beam around its pfm_run: the output layer writes logits
     int last_L = 0;                // decoder positions of the last pfm_run (max token count)
     int ffn_kind = 0;              // which fused-FFN kernel the packed encoder weights (ffn_pack) are ordered for
-    int dffn_kind = 0;             // ... and the packed decoder weights (dffn_pack)
     DevBuf dffn_pack, dffn_c;      // decoder FFNs (16 blocks + decoders3): W1 | W2 diag(gamma_F) tiles; c1 | c2
     bool dffn_ready = false;
     DevBuf arena_x6;               // EXACT mode: three bf16 planes of every GEMM weight (x = x0 + x1 + x2)
@@ -475,10 +466,9 @@ int ensure_bf16(pfm_handle* h, hipStream_t st) {
         }
         h->bf_ready = true;
     }
-    // k_ffn.hip (1) and k_ffn2.hip (2) order their fragments differently; encoder and decoder choose separately
-    const int fk = pfm_knobs().ffn_kernel, dk = pfm_knobs().dec_ffn_kernel;
+    // k_ffn.hip (1) and k_ffn2.hip (2) order their fragments differently (the decoder always runs k_ffn.hip)
+    const int fk = pfm_knobs().ffn_kernel;
     if (h->ffn_kind != fk) { h->ffn_ready = false; h->ffn_kind = fk; }
-    if (h->dffn_kind != dk) { h->dffn_ready = false; h->dffn_kind = dk; }
     auto pack = [&](const bf16* w1, const bf16* w2, bf16* wp) { return fk == 2 ? pfm_ffn2_pack(w1, w2, wp, st) : pfm_ffn_pack(w1, w2, wp, st); };
     auto pack_o = [&](int kind, const bf16* wo, bf16* wp) { return kind == 2 ? pfm_ffn2_pack_o(wo, wp, st) : pfm_ffn_pack_o(wo, wp, st); };
     if (!h->ffn_ready && ffn_shape_ok(h->cfg) && pfm_knobs().ffn_fused && !h->enc.empty()) {
@@ -510,9 +500,9 @@ int ensure_bf16(pfm_handle* h, hipStream_t st) {
             const size_t w1 = d3 ? h->d3w1 : h->dec[j].w1, w2 = d3 ? h->d3w2 : h->dec[j].w2;
             const size_t gF = d3 ? h->d3ng : h->dec[j].ng, bF = d3 ? h->d3nb : h->dec[j].nb;
             float* cc = h->dffn_c.as<float>() + (size_t)j * 2 * D;
-            if (j > 0) HIP_TRY(pack_o(dk, h->wb(h->dec[j - 1].wo), h->dffn_pack.as<bf16>() + (size_t)j * per));
-            HIP_TRY((dk == 2 ? pfm_ffn2_pack_dec : pfm_ffn_pack_dec)(h->wb(w1), h->w(w2), h->w(gF), h->w(bF),
-                                     h->dffn_pack.as<bf16>() + (size_t)j * per + po, cc, cc + D, st));
+            if (j > 0) HIP_TRY(pfm_ffn_pack_o(h->wb(h->dec[j - 1].wo), h->dffn_pack.as<bf16>() + (size_t)j * per, st));
+            HIP_TRY(pfm_ffn_pack_dec(h->wb(w1), h->w(w2), h->w(gF), h->w(bF), h->dffn_pack.as<bf16>() + (size_t)j * per + po,
+                                     cc, cc + D, st));
         }
         h->dffn_ready = true;
     }
@@ -665,10 +655,8 @@ void prof_collect(pfm_handle* h) {
 // Kernel choice: bf16 operands go to the 256x256 LDS-DMA kernel whenever its alignment
 // contract holds (K % 64 == 0, 16-B aligned rows); f32 (exact mode) and odd shapes use the
 // 128x128 register-staged kernel.
-int gemm_kernel_override() { return pfm_knobs().gemm_kernel; }   // 128: force the 128x128 kernel (A/B)
-
 bool use_big_bf16(int dtype, RowMap amap, long long ldw, int K) {
-    return dtype == DT_BF16 && gemm_kernel_override() != 128 && pfm_gemm_bf16_256_ok(amap, ldw, K);
+    return dtype == DT_BF16 && pfm_gemm_bf16_256_ok(amap, ldw, K);
 }
 
 hipError_t gemm_dispatch(int dtype, const void* A, RowMap amap, const void* W, long long ldw, int M, int N, int K,
@@ -716,7 +704,7 @@ GemmEpi epi_default() {
 hipError_t gemm_x6(pfm_handle* h, const float* A, RowMap am, const float* W, int M, int N, int K, const GemmEpi& e,
                    hipStream_t s, const bf16* A3 = nullptr) {
     if (M <= 0 || N <= 0) return hipSuccess;
-    const int terms = pfm_knobs().exact_terms;   // 6 (f32-equivalent) or 3 (bf16x3)
+    constexpr int terms = 6;   // the six products of three bf16 planes that reproduce the f32 GEMM
     if (A3) {   // the producer already wrote [A0 | A1 | A2] (DT_X3 rows, am.ld = 3K)
         if (K % 64) return hipErrorInvalidValue;
         GemmEpi e2 = e;
@@ -1443,12 +1431,12 @@ int pfm_run(pfm_handle* h, void* stream, int mode, const float* feats, const int
                 const size_t po = pfm_ffn_packed_o_elems();
                 const bf16* blk = h->dffn_pack.as<bf16>() + (size_t)fi * (po + pfm_ffn_packed_elems());
                 if (op_from >= 0) {   // x = x + O Wo^T + bo of block op_from, then the FFN on it
-                    HIP_TRY((h->dffn_kind == 2 ? pfm_ffn2_fused_dec : pfm_ffn_fused_dec)(Xd, Mg, P(lng), P(lnb), c.ln_eps, blk, P(b1), cc, cc + D, Xd, P(pg),
-                                              P(pb), (bf16*)pout, Odb, P(h->dec[op_from].bo), s));
+                    HIP_TRY(pfm_ffn_fused_dec(Xd, Mg, P(lng), P(lnb), c.ln_eps, blk, P(b1), cc, cc + D, Xd, P(pg), P(pb),
+                                              (bf16*)pout, Odb, P(h->dec[op_from].bo), s));
                     op_from = -1;
                 } else {
-                    HIP_TRY((h->dffn_kind == 2 ? pfm_ffn2_fused_dec : pfm_ffn_fused_dec)(Xd, Mg, P(lng), P(lnb), c.ln_eps, blk + po, P(b1), cc, cc + D, nullptr,
-                                              P(pg), P(pb), (bf16*)pout, nullptr, nullptr, s));
+                    HIP_TRY(pfm_ffn_fused_dec(Xd, Mg, P(lng), P(lnb), c.ln_eps, blk + po, P(b1), cc, cc + D, nullptr, P(pg),
+                                              P(pb), (bf16*)pout, nullptr, nullptr, s));
                 }
                 return PFM_OK;
             }
@@ -1972,14 +1960,13 @@ int pfm_op_ffn_dec(void* stream, const float* x, int M, const float* g1, const f
     HIP_TRY(sc.alloc(&wob, no));
     HIP_TRY(sc.alloc(&wp, po + pfm_ffn_packed_elems()));
     HIP_TRY(sc.alloc(&cc, (size_t)2 * 512));
-    const bool k2 = pfm_knobs().dec_ffn_kernel == 2;
     HIP_TRY(pfm_f32_to_bf16(W1, w1b, (long long)nw, st));
     if (o) {
         HIP_TRY(pfm_f32_to_bf16(Wo, wob, (long long)no, st));
-        HIP_TRY((k2 ? pfm_ffn2_pack_o : pfm_ffn_pack_o)(wob, wp, st));
+        HIP_TRY(pfm_ffn_pack_o(wob, wp, st));
     }
-    HIP_TRY((k2 ? pfm_ffn2_pack_dec : pfm_ffn_pack_dec)(w1b, W2, gF, bF, wp + po, cc, cc + 512, st));
-    auto dec = k2 ? pfm_ffn2_fused_dec : pfm_ffn_fused_dec;
+    HIP_TRY(pfm_ffn_pack_dec(w1b, W2, gF, bF, wp + po, cc, cc + 512, st));
+    auto dec = pfm_ffn_fused_dec;
     if (o) {   // mode 3: x1 = x + o Wo^T + bo -> xo, then the FFN on x1 (x may alias xo)
         HIP_TRY(dec(x, M, g1, b1n, eps, wp, b1, cc, cc + 512, xo, gn, bn, (bf16*)xn, (const bf16*)o, bo, st));
     } else {
@@ -2158,7 +2145,7 @@ namespace {
 // causal FSMN (chunk cache) -> cross attention over [K/V cache ;] the window memory, decoders3, after_norm,
 // output layer with fused argmax.
 int stream_decoder(pfm_streams* s, const Run& r, int n, int Tw, int L, const SPrm* prm, const int* tw_d,
-                   const int* kld_d, const int* ntok, int32_t* tokens, int L_cap) {
+                   const int* kld_d, const int* ntok, int32_t* tokens, int L_cap, float* logits) {
     pfm_handle* h = s->h;
     const pfm_config& c = h->cfg;
     const hipStream_t st = r.st;
@@ -2249,6 +2236,13 @@ int stream_decoder(pfm_streams* s, const Run& r, int n, int Tw, int L, const SPr
     }
     int rc = ffn(Xd, h->d3n1g, h->d3n1b, h->d3w1, h->d3b1, h->d3ng, h->d3nb, h->d3w2, Xd, h->dan_g, h->dan_b, Xdn, dt);
     if (rc) return rc;
+    if (logits) {   // CTC prefix beam (pfm_stream_step_beam): the f32 logits [n][L][V] themselves
+        GemmEpi e = epi_default();
+        e.bias = r.P(h->out_b);
+        e.out = logits; e.out_map = rowmap_plain(c.vocab_size); e.out_dtype = DT_F32;
+        HIP_TRY(r.gemm(dt, Xdn, rowmap_plain(D), r.W(h->out_w), D, (int)Ml, c.vocab_size, D, e));
+        return PFM_OK;
+    }
     const int ntl = amax_tiles(dt, rowmap_plain(D), D, c.vocab_size, D, h, r.W(h->out_w));
     GemmEpi e = epi_default();
     e.bias = r.P(h->out_b);
@@ -2396,13 +2390,21 @@ int pfm_streams_reset(pfm_streams* s, void* stream, const int32_t* slot_ids, int
     return PFM_OK;
 }
 
-int pfm_stream_step(pfm_streams* s, void* stream, int n, const int32_t* slot_ids, const float* feats, int Tn,
-                    const int32_t* nfeat, const int32_t* is_final, int32_t* tokens, int L_cap, int32_t* ntok_out,
-                    float* enc_out, float* alphas_out) {
-    pfm_knobs_refresh();
-    if (!s || !slot_ids || !nfeat || !is_final || !tokens || !ntok_out)
-        return fail(PFM_E_ARG, "pfm_stream_step: null argument");
-    if (n < 1 || Tn < 0 || L_cap < 0) return fail(PFM_E_ARG, "pfm_stream_step: bad sizes");
+}  // extern "C"
+
+namespace {
+
+// The CTC prefix beam of one streaming step (pfm_stream_step_beam)
+struct StreamBeam {
+    int beam, P, nbest, end_detect, sos, eos, blank;
+    float ctc_weight, penalty;
+    int32_t* ntok_hyp;   // [n][nbest]
+    float* scores;       // [n][nbest]
+};
+
+int stream_step(pfm_streams* s, void* stream, int n, const int32_t* slot_ids, const float* feats, int Tn,
+                const int32_t* nfeat, const int32_t* is_final, int32_t* tokens, int L_cap, int32_t* ntok_out,
+                float* enc_out, float* alphas_out, const StreamBeam* sb) {
     pfm_handle* h = s->h;
     const pfm_config& c = h->cfg;
     if (h->missing) return fail(PFM_E_STATE, "pfm_stream_step: weights not set");
@@ -2500,6 +2502,11 @@ int pfm_stream_step(pfm_streams* s, void* stream, int n, const int32_t* slot_ids
     // HIP graphs replace the ~10 launches per encoder layer when no optional output is requested: kernels
     // read every per-step value from `prm`, so one graph per (n, maxn) replays any step of that shape
     const bool graphs = !enc_out && !alphas_out && !h->prof_on && pfm_knobs().stream_graph;
+    const int V = c.vocab_size;
+    if (sb) {   // the beam's f32 decoder / CTC log-probs, sized before any capture
+        HIP_TRY(h->logits.ensure((size_t)n * L_cap * V * sizeof(float)));
+        HIP_TRY(h->ctcx.ensure((size_t)n * Tw * V * sizeof(float)));
+    }
 
     // ---- phase A: encoder window + SANMEncoderChunkOpt.forward_chunk (scama/encoder.py:456-499) +
     // CifPredictorV2.forward_chunk (cif_predictor.py:255-344) -> acoustic embeds, ntok on the device
@@ -2556,7 +2563,39 @@ int pfm_stream_step(pfm_streams* s, void* stream, int n, const int32_t* slot_ids
         if (s->Cd && s->hntok[i] > 0) s->cld[sl] = std::min(s->Cd, s->cld[sl] + tw);
     }
     if (L < 1 || c.dec_blocks < 1) {   // model.py:490-491: nothing to decode
-        if (L_cap > 0) HIP_TRY(pfm_fill_i32(tokens, (long long)n * L_cap, -1, st));
+        const long long nb = sb ? sb->nbest : 1;
+        if (L_cap > 0) HIP_TRY(pfm_fill_i32(tokens, n * nb * L_cap, -1, st));
+        if (sb) {
+            HIP_TRY(pfm_fill_i32(sb->ntok_hyp, n * nb, -1, st));
+            HIP_TRY(hipMemsetAsync(sb->scores, 0, (size_t)(n * nb) * sizeof(float), st));
+        }
+        HIP_TRY(hipStreamSynchronize(st));
+        return PFM_OK;
+    }
+    if (sb) {   // model.py:510-519: BeamSearchPara per stream on its window's CTC log-probs and decoder log-probs
+        if (L > L_cap) return fail(PFM_E_ARG, "pfm_stream_step_beam: L_cap below the chunk's token count");
+        {
+            Run run(h, st, fast);
+            int rc2 = stream_decoder(s, run, n, Tw, L, prm, tw_d, kld_d, ntok, nullptr, 0, h->logits.as<float>());
+            if (rc2) return rc2;
+            // ctc.log_softmax of the window (encoder_out[i, :encoder_out_lens[i]], lens = the window rows)
+            GemmEpi e = epi_default();
+            e.bias = run.P(h->ctc_b);
+            e.out = h->ctcx.p; e.out_map = rowmap_plain(V); e.out_dtype = DT_F32;
+            const void* A = fast ? (const void*)(encpb + D) : (const void*)(encp + D);
+            HIP_TRY(run.gemm(run.dt, A, encmap, run.W(h->ctc_w), D, n * Tw, V, D, e));
+        }
+        HIP_TRY(pfm_logsoftmax_rows(h->ctcx.as<float>(), (long long)n * Tw, V, V, st));
+        HIP_TRY(pfm_logsoftmax_rows(h->logits.as<float>(), (long long)n * L, V, V, st));
+        HIP_TRY(hipMemsetAsync(sb->scores, 0, (size_t)n * sb->nbest * sizeof(float), st));
+        const long long fsz = pfm_ctc_beam_fscratch(sb->beam, sb->P, Tw, L);
+        const long long isz = pfm_ctc_beam_iscratch(sb->beam, sb->nbest, L);
+        HIP_TRY(h->beam_fs.ensure((size_t)n * fsz * sizeof(float)));
+        HIP_TRY(h->beam_is.ensure((size_t)n * isz * sizeof(int32_t)));
+        HIP_TRY(pfm_ctc_beam(h->logits.as<float>(), L, h->ctcx.as<float>(), Tw, tw_d, ntok, n, V, sb->beam, sb->P,
+                             sb->nbest, sb->ctc_weight, sb->penalty, sb->penalty != 0.f ? 1 : 0, sb->end_detect, sb->sos,
+                             sb->eos, sb->blank, h->beam_fs.as<float>(), h->beam_is.as<int>(), tokens, L_cap,
+                             sb->ntok_hyp, sb->scores, st));
         HIP_TRY(hipStreamSynchronize(st));
         return PFM_OK;
     }
@@ -2566,13 +2605,58 @@ int pfm_stream_step(pfm_streams* s, void* stream, int n, const int32_t* slot_ids
     auto phaseB = [&](hipStream_t q) -> int {
         if (L_cap > 0) HIP_TRY(pfm_fill_i32(tk, (long long)n * L_cap, -1, q));
         Run run(h, q, fast);
-        return stream_decoder(s, run, n, Tw, L, prm, tw_d, kld_d, ntok, tk, L_cap);
+        return stream_decoder(s, run, n, Tw, L, prm, tw_d, kld_d, ntok, tk, L_cap, nullptr);
     };
     rc = stream_graphed(s, {1, n, maxn, L * 4096 + L_cap}, graphs, st, phaseB);
     if (rc) return rc;
     if (L_cap > 0) HIP_TRY(hipMemcpyAsync(tokens, tk, (size_t)n * L_cap * 4, hipMemcpyDeviceToDevice, st));
     HIP_TRY(hipStreamSynchronize(st));
     return PFM_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int pfm_stream_step(pfm_streams* s, void* stream, int n, const int32_t* slot_ids, const float* feats, int Tn,
+                    const int32_t* nfeat, const int32_t* is_final, int32_t* tokens, int L_cap, int32_t* ntok_out,
+                    float* enc_out, float* alphas_out) {
+    pfm_knobs_refresh();
+    if (!s || !slot_ids || !nfeat || !is_final || !tokens || !ntok_out)
+        return fail(PFM_E_ARG, "pfm_stream_step: null argument");
+    if (n < 1 || Tn < 0 || L_cap < 0) return fail(PFM_E_ARG, "pfm_stream_step: bad sizes");
+    return stream_step(s, stream, n, slot_ids, feats, Tn, nfeat, is_final, tokens, L_cap, ntok_out, enc_out,
+                       alphas_out, nullptr);
+}
+
+int pfm_stream_step_beam(pfm_streams* s, void* stream, int n, const int32_t* slot_ids, const float* feats, int Tn,
+                         const int32_t* nfeat, const int32_t* is_final, int beam, float ctc_weight, float penalty,
+                         int nbest, int end_detect, int sos, int eos, int blank, int32_t* tokens, int L_cap,
+                         int32_t* ntok_out, float* scores_out, int32_t* nfire) {
+    pfm_knobs_refresh();
+    if (!s || !slot_ids || !nfeat || !is_final || !tokens || !ntok_out || !scores_out)
+        return fail(PFM_E_ARG, "pfm_stream_step_beam: null argument");
+    if (n < 1 || Tn < 0 || L_cap < 1) return fail(PFM_E_ARG, "pfm_stream_step_beam: bad sizes");
+    const pfm_config& c = s->h->cfg;
+    if (!c.ctc_head) return fail(PFM_E_STATE, "pfm_stream_step_beam: the model has no CTC head (ctc_weight 0.0)");
+    const int V = c.vocab_size;
+    const int pre = (int)(1.5 * beam), P = pre < V ? pre : V;
+    if (sos < 0 || sos >= V || eos < 0 || eos >= V || blank < 0 || blank >= V)
+        return fail(PFM_E_ARG, "pfm_stream_step_beam: sos / eos / blank outside the vocabulary");
+    if (beam < 1 || beam > 16 || nbest < 1 || nbest > 16 || P > 64 || !(ctc_weight > 1e-5f))
+        return fail(PFM_E_ARG,
+                    "pfm_stream_step_beam: need 1 <= beam <= 16, 1 <= nbest <= 16, ctc_weight > 1e-5, <= 64 candidates");
+    StreamBeam sb;
+    sb.beam = beam; sb.P = P; sb.nbest = nbest; sb.end_detect = end_detect; sb.sos = sos; sb.eos = eos;
+    sb.blank = blank; sb.ctc_weight = ctc_weight; sb.penalty = penalty; sb.ntok_hyp = ntok_out;
+    sb.scores = scores_out;
+    // the CIF fire counts go to nfire (or a scratch the step owns)
+    int32_t* nf = nfire;
+    if (!nf) {
+        HIP_TRY(s->h->beam_nf.ensure((size_t)n * sizeof(int32_t)));
+        nf = s->h->beam_nf.as<int32_t>();
+    }
+    return stream_step(s, stream, n, slot_ids, feats, Tn, nfeat, is_final, tokens, L_cap, nf, nullptr, nullptr, &sb);
 }
 
 void pfm_streams_destroy(pfm_streams* s) {

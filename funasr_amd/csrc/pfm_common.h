@@ -126,13 +126,11 @@ static inline int epi_vec_ok(const GemmEpi& e, int N) {
 // thread's snapshot through pfm_knobs(). `sig` hashes every field: captured streaming graphs are keyed
 // by it, so a changed knob never replays a graph recorded under other settings.
 struct PfmKnobs {
-    int gemm_kernel;        // PFM_GEMM_KERNEL=128: force the 128x128 kernel
     int attn_fsmn;          // PFM_ATTN_FSMN (default 1): encoder FSMN fused into the attention epilogue
     int attn_waves;         // PFM_ATTN_WAVES (default 8)
     int kv_overlap;         // PFM_KV_OVERLAP (default 1): memory K|V projection on the side stream
     int subbatch;           // PFM_SUBBATCH (default 2): concurrent encoder utterance groups
     int stream_graph;       // PFM_STREAM_GRAPH (default 1): streaming steps through HIP graphs
-    int fsmn_v2;            // PFM_FSMN_V2: frames per thread of the 8-channel FSMN kernel (0 = 4-channel)
     int gemm_gm;            // PFM_GEMM_GM: grouped tile order override (-1 = default)
     int gemm_cfg;           // PFM_GEMM_CFG: forced tile configuration (0 = policy)
     int gemm_st16;          // PFM_GEMM_ST16 (default 1): 16-B bf16 epilogue stores
@@ -145,12 +143,10 @@ struct PfmKnobs {
     int dec_ffn_fused;      // PFM_DEC_FFN_FUSED (default 1): decoder LN1-FFN(LN_F folded)-LN kernel (fast mode)
     int ffn_kernel;         // PFM_FFN_KERNEL (default 2): encoder fused FFN as 128-row workgroups (k_ffn2.hip, with
                             // the next layer's QKV projection folded in); 1 = 64-row workgroups (k_ffn.hip)
-    int dec_ffn_kernel;     // PFM_DEC_FFN_KERNEL (default 1): the same choice for the decoder FFN
-    int exact_terms;        // PFM_EXACT_TERMS (default 6): products per EXACT-mode split-bf16 GEMM; 3 = bf16x3
     int ffn_qkv;            // PFM_FFN_QKV (default 1): with the 128-row fused FFN, the next layer's QKV projection as
                             // its phase 3 (k_ffn2.hip MODE 4; the separate LN1 + QKV GEMM otherwise)
     unsigned long long sig;
 };
-#define PFM_KNOB_FIELDS 21
+#define PFM_KNOB_FIELDS 17
 const PfmKnobs& pfm_knobs();   // the calling thread's snapshot (refreshed lazily if no entry point did yet)
 void pfm_knobs_refresh();

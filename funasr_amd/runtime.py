@@ -26,7 +26,7 @@ MODES = {"exact": MODE_EXACT, "fp32": MODE_EXACT, "fast": MODE_FAST, "bf16": MOD
 ABI_SYMBOLS = ("pfm_config_default", "pfm_config_sensevoice", "pfm_create", "pfm_run_beam", "pfm_set_weight", "pfm_set_weight_device",
                "pfm_missing_weights", "pfm_reserve", "pfm_run", "pfm_run_ctc", "pfm_ctc_align", "pfm_op_ctc_collapse", "pfm_fbank", "pfm_lfr_frames", "pfm_last_error", "pfm_destroy", "pfm_op_gemm",
                "pfm_op_attention", "pfm_op_layernorm", "pfm_op_fsmn", "pfm_op_cif", "pfm_op_ctc_beam", "pfm_profile", "pfm_op_ffn", "pfm_op_ffn_op", "pfm_op_ffn_op_qkv", "pfm_op_ffn_dec", "pfm_op_fsmn_bf16", "pfm_op_layernorm_bf16",
-               "pfm_profile_read", "pfm_streams_create", "pfm_streams_reset", "pfm_stream_step",
+               "pfm_profile_read", "pfm_streams_create", "pfm_streams_reset", "pfm_stream_step", "pfm_stream_step_beam",
                "pfm_streams_destroy", "pfm_fbank_raw", "pfm_lfr_gather", "pfm_config_punc", "pfm_run_punc", "pfm_vad_config_default", "pfm_vad_create",
                "pfm_vad_set_weight", "pfm_vad_missing_weights", "pfm_vad_reset", "pfm_vad_run", "pfm_vad_destroy", "pfm_vad_fbank_raw",
                "pfm_vad_opts_default", "pfm_vad_detector_create", "pfm_vad_detector_push", "pfm_vad_detector_destroy")
@@ -133,6 +133,10 @@ def load_library(path: Optional[str] = None) -> ctypes.CDLL:
     lib.pfm_stream_step.argtypes = [vp, vp, i32, ctypes.POINTER(ctypes.c_int32), f32p, i32,
                                     ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32), i32p, i32, i32p,
                                     f32p, f32p]
+    lib.pfm_stream_step_beam.argtypes = [vp, vp, i32, ctypes.POINTER(ctypes.c_int32), f32p, i32,
+                                         ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32), i32,
+                                         ctypes.c_float, ctypes.c_float, i32, i32, i32, i32, i32, i32p, i32, i32p,
+                                         f32p, i32p]
     lib.pfm_fbank_raw.argtypes = [vp, vp, f32p, i32p, i32, i32, f32p, i32]
     lib.pfm_lfr_gather.argtypes = [vp, f32p, i32p, i32, i32, f32p, f32p]
     lib.pfm_config_punc.argtypes = [ctypes.POINTER(PfmConfig)]
@@ -494,6 +498,47 @@ class PfmStreams:
                                        I32(*fin), _ptr(tokens), L_cap, _ptr(ntok), _ptr(enc), _ptr(alphas)),
               "pfm_stream_step")
         return dict(tokens=tokens, ntok=ntok, enc=enc, alphas=alphas)
+
+    def _args(self, slot_ids, feats, nfeat, is_final):
+        torch = self.torch
+        dev = torch.device("cuda", self.engine.device)
+        ids = [int(x) for x in slot_ids]
+        n = len(ids)
+        nf = [int(x) for x in nfeat]
+        fin = [1 if x else 0 for x in is_final]
+        if len(nf) != n or len(fin) != n:
+            raise PfmError("slot_ids, nfeat and is_final must have one entry per stream")
+        Tn = 0
+        if feats is not None:
+            if feats.device != dev or feats.dtype != torch.float32 or not feats.is_contiguous():
+                feats = feats.to(device=dev, dtype=torch.float32).contiguous()
+            if feats.dim() != 3 or feats.shape[0] != n or feats.shape[2] != self.engine.cfg.input_size:
+                raise PfmError(f"feats must be [n, Tn, {self.engine.cfg.input_size}]")
+            Tn = feats.shape[1]
+        return dev, ids, n, nf, fin, feats, Tn
+
+    def step_beam(self, slot_ids, feats, nfeat, is_final, beam=2, ctc_weight=0.5, penalty=0.0, nbest=1,
+                  end_detect=True, L_cap: Optional[int] = None):
+        """One chunk with the joint decoder + CTC prefix beam search per stream (pfm_stream_step_beam,
+        paraformer_streaming/model.py:510-521; the model needs its CTC head) -> dict(tokens [n, nbest, L_cap],
+        ntok [n, nbest] (-1 = no hypothesis: no CIF fire this chunk), scores [n, nbest], nfire [n])."""
+        torch = self.torch
+        dev, ids, n, nf, fin, feats, Tn = self._args(slot_ids, feats, nfeat, is_final)
+        C0 = self.chunk_size[0] + self.chunk_size[2]
+        Tw = C0 + max(nf)
+        L_cap = Tw + 2 if L_cap is None else int(L_cap)
+        tokens = torch.empty((n, nbest, max(L_cap, 1)), dtype=torch.int32, device=dev)
+        ntok = torch.empty((n, nbest), dtype=torch.int32, device=dev)
+        scores = torch.empty((n, nbest), dtype=torch.float32, device=dev)
+        nfire = torch.empty((n,), dtype=torch.int32, device=dev)
+        c = self.engine.cfg
+        I32 = ctypes.c_int32 * n
+        check(self.lib.pfm_stream_step_beam(self.h, _stream_ptr(torch, dev), n, I32(*ids), _ptr(feats), Tn,
+                                            I32(*nf), I32(*fin), int(beam), float(ctc_weight), float(penalty),
+                                            int(nbest), 1 if end_detect else 0, int(c.sos), int(c.eos),
+                                            int(c.blank_id), _ptr(tokens), L_cap, _ptr(ntok), _ptr(scores),
+                                            _ptr(nfire)), "pfm_stream_step_beam")
+        return dict(tokens=tokens, ntok=ntok, scores=scores, nfire=nfire)
 
 
 def op_gemm(A, W, bias=None, res=None, relu=False, out_bf16=False):

@@ -9,6 +9,9 @@ Contract (funasr/models/paraformer_streaming/model.py:435-656, SURVEY §8f row 3
     (init_cache on first use and after is_final, prev_samples, 600 ms sample chunks, the tail chunk);
     results [{"key", "text"}] (text = sentence_postprocess of this call's tokens), or
     [{"key", "token_int"}] with tokenizer None.
+  * decoding_ctc_weight > 0 on a model with a CTC head (model_conf ctc_weight > 0) runs the joint decoder + CTC
+    prefix beam search per chunk (model.py:510-521, 567-575; pfm_stream_step_beam), beam_size / nbest / penalty /
+    maxlenratio as the reference's kwargs; the chunk's tokens are those of every n-best hypothesis in order;
   * `inference_streams(...)` advances many streams by one call each in a single batched pass — the
     serving entry point (the reference is batch 1, model.py:598).
 The per-stream state lives in HBM inside a pfm_streams object (one slot per live cache dict); the
@@ -111,8 +114,23 @@ class ParaformerStreaming(HipModel):
         """calls: (audio samples, cache dict, is_final) per stream -> per stream the tokens of this call
         (token strings with a tokenizer, else ids). Each stream is cut into 600 ms chunks as in
         inference() (model.py:591-642); chunk j of every stream runs in the same pfm_stream_step."""
-        if kwargs.get("decoding_ctc_weight", 0.0) > 1e-5 or kwargs.get("lm_weight", 0.0) > 1e-5:
-            raise NotImplementedError("Paraformer-streaming has no CTC head (ctc_weight 0.0); greedy only")
+        if kwargs.get("lm_weight", 0.0) > 1e-5 and kwargs.get("lm_file") is not None:
+            raise NotImplementedError("LM shallow fusion (lm_file) is not on the HIP streaming path")
+        # model.py:567-575: the joint decoder + CTC prefix beam search when decoding_ctc_weight > 1e-5 and the
+        # model has a CTC head (model_conf ctc_weight > 0); the released model has none and decodes greedily
+        beam = None
+        if kwargs.get("decoding_ctc_weight", 0.0) > 1e-5:
+            if self.cfg.ctc_weight > 0.0:
+                nbest = int(kwargs.get("nbest", 1))
+                if not 1 <= nbest <= 16:
+                    raise PfmError(f"nbest {nbest}: the HIP beam search keeps at most 16 ended hypotheses")
+                beam = dict(beam=int(kwargs.get("beam_size", 2)), ctc_weight=float(kwargs["decoding_ctc_weight"]),
+                            penalty=float(kwargs.get("penalty", 0.0)), nbest=nbest,
+                            end_detect=float(kwargs.get("maxlenratio", 0.0)) == 0.0)
+            else:
+                import warnings
+                warnings.warn("decoding_ctc_weight > 0 on a ParaformerStreaming without a CTC head (ctc_weight 0.0): "
+                              "greedy decoding, as the reference does when the model has no ctc module")
         fe = frontend if isinstance(frontend, WavFrontendOnline) else self._default_frontend(frontend)
         eng = self.engine()
         plans = []
@@ -159,12 +177,22 @@ class ParaformerStreaming(HipModel):
                         if nf[i]:
                             feats[i, : nf[i]] = rows[k]
                 fins = [plans[k][5] and j == plans[k][1] - 1 for k in run]
-                r = pool.streams.step([plans[k][4]["slot"].idx for k in run], feats, nf, fins)
-                toks = r["tokens"].cpu().numpy()
-                ntok = r["ntok"].cpu().numpy()
+                slots = [plans[k][4]["slot"].idx for k in run]
+                if beam is None:
+                    r = pool.streams.step(slots, feats, nf, fins)
+                    toks = r["tokens"].cpu().numpy()
+                    ntok = r["ntok"].cpu().numpy()
+                    hyps = [[[t for t in toks[i, : int(ntok[i])].tolist() if t not in (self.eos, self.sos, self.blank_id)]]
+                            for i in range(len(run))]
+                else:   # model.py:530-552: the tokens of every n-best hypothesis, concatenated
+                    r = pool.streams.step_beam(slots, feats, nf, fins, **beam)
+                    toks = r["tokens"].cpu().numpy()
+                    ntok = r["ntok"].cpu().numpy()
+                    hyps = [[toks[i, q, : int(ntok[i, q])].tolist() for q in range(toks.shape[1]) if ntok[i, q] >= 0]
+                            for i in range(len(run))]
                 for i, k in enumerate(run):
-                    ids = [t for t in toks[i, : int(ntok[i])].tolist() if t not in (self.eos, self.sos, self.blank_id)]
-                    out[k].extend(tokenizer.ids2tokens(ids) if tokenizer is not None else ids)
+                    for ids in hyps[i]:
+                        out[k].extend(tokenizer.ids2tokens(ids) if tokenizer is not None else ids)
         for a, n, m, stride, cache, fin in plans:
             cache["prev_samples"] = a[:-m] if m else a[:0]    # model.py:646 (keeps audio[:-m], as the reference)
             if fin:

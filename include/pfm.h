@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define PFM_ABI_VERSION 4
+#define PFM_ABI_VERSION 5
 
 enum pfm_status {
     PFM_OK = 0,
@@ -280,6 +280,25 @@ int pfm_streams_reset(pfm_streams* s, void* stream, const int32_t* slot_ids, int
 int pfm_stream_step(pfm_streams* s, void* stream, int n, const int32_t* slot_ids, const float* feats,
                     int Tn, const int32_t* nfeat, const int32_t* is_final, int32_t* tokens, int L_cap,
                     int32_t* ntok, float* enc_out, float* alphas);
+
+/* One chunk for n streams with the joint decoder + CTC prefix beam search instead of the argmax: the
+ * generate_chunk path of a ParaformerStreaming whose model has a CTC head (model_conf ctc_weight > 0)
+ * decoding with decoding_ctc_weight > 0 (paraformer_streaming/model.py:510-521, beam search built by
+ * Paraformer.init_beam_search, paraformer/model.py:396-441, per chunk as inference() at :567-575).
+ * Per stream: BeamSearchPara over the chunk's decoder log-probs (its CIF fires) and the CTC log-probs
+ * of its whole encoder window (encoder_out[i, :encoder_out_lens[i]], overlap + chunk rows).
+ *   slot_ids .. is_final   as pfm_stream_step
+ *   beam, ctc_weight, penalty, nbest, end_detect, sos, eos, blank   as pfm_run_beam
+ *   tokens    [n, nbest, L_cap] int32 out: hypothesis tokens without sos / eos / blank
+ *   ntok      [n, nbest] int32 out: tokens per hypothesis, -1 = none (the stream fired no token this
+ *             chunk: the reference's generate_chunk returns [] for it)
+ *   scores    [n, nbest] f32 out
+ *   nfire     [n] int32 out (or NULL): CIF fires of the chunk
+ * The stream caches advance exactly as in pfm_stream_step. Synchronous like pfm_stream_step. */
+int pfm_stream_step_beam(pfm_streams* s, void* stream, int n, const int32_t* slot_ids, const float* feats,
+                         int Tn, const int32_t* nfeat, const int32_t* is_final, int beam, float ctc_weight,
+                         float penalty, int nbest, int end_detect, int sos, int eos, int blank,
+                         int32_t* tokens, int L_cap, int32_t* ntok, float* scores, int32_t* nfire);
 
 void pfm_streams_destroy(pfm_streams* s);
 

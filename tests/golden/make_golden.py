@@ -782,6 +782,117 @@ def save_stream():
         json.dump(wout, f, ensure_ascii=False, indent=1)
 
 
+STREAM_BEAM_CASES = {   # name: (encoder / decoder look-back, decoding_ctc_weight, beam_size, penalty, nbest, tail chunk)
+    "sb_lb00": ((0, 0), 0.3, 3, 0.0, 1, False),
+    "sb_lb41_nb": ((4, 1), 0.5, 4, 0.5, 3, True),
+}
+
+
+def save_stream_beam():
+    """ParaformerStreaming with a CTC head (model_conf ctc_weight 0.3, tiny: enc 3 / dec 2) decoded per chunk by the
+    reference's joint decoder + CTC prefix beam search (generate_chunk with self.beam_search built by
+    init_beam_search, paraformer_streaming/model.py:510-552, 567-575). Chunk-level: seeded LFR+CMVN chunks of 10
+    frames; per chunk the generate_chunk ids (every n-best hypothesis, concatenated) and, from beam_search() itself,
+    the n-best yseqs and scores. Waveform-level: inference() over 600 ms sample chunks (kaldi.fbank patched to the
+    pinned restatement) with decoding_ctc_weight, as the reference's own streaming entry builds the search."""
+    import dataclasses
+    from funasr_amd.config import paraformer_streaming_tiny
+    import funasr.models.scama.encoder  # noqa: F401
+    import funasr.models.paraformer_streaming.model  # noqa: F401
+    cfg = dataclasses.replace(paraformer_streaming_tiny(), ctc_weight=0.3)
+    kw = cfg.reference_kwargs()
+
+    def build():
+        m = tables.model_classes["ParaformerStreaming"](
+            **{k: kw[k] for k in ("encoder", "encoder_conf", "decoder", "decoder_conf", "predictor", "predictor_conf")},
+            input_size=cfg.input_size, vocab_size=cfg.vocab_size, ctc_weight=0.3, predictor_bias=1)
+        m.load_state_dict({k: torch.from_numpy(v) for k, v in make_weights(cfg, seed=0).items()}, strict=True)
+        m.eval()
+        return m
+
+    toks = token_list(cfg.vocab_size)
+    rng = np.random.default_rng(22)
+    chunks = [rng.standard_normal((10, 560), dtype=np.float32) for _ in range(8)]
+    last = rng.standard_normal((7, 560), dtype=np.float32)
+    out = dict(seed=22, chunks=np.stack(chunks), last=last)
+    for name, ((elb, dlb), wctc, beam, pen, nbest, tail) in STREAM_BEAM_CASES.items():
+        m = build()
+        m.init_beam_search(token_list=toks, decoding_ctc_weight=wctc, beam_size=beam, penalty=pen)
+        m.nbest = nbest
+        calls = []
+        fwd = m.beam_search.forward
+
+        def spy(*a, **k):
+            r = fwd(*a, **k)
+            calls[-1].append([(h.yseq.tolist(), float(h.score)) for h in r[:nbest]])
+            return r
+
+        m.beam_search.forward = spy
+        cache = _stream_cache(m, elb, dlb)
+        ids, hyps = [], []
+        seq = chunks + ([None] if tail else [last])
+        for i, x in enumerate(seq):
+            fin = i == len(seq) - 1
+            if x is None:
+                cache["encoder"]["tail_chunk"] = True
+                t = cache["encoder"]["feats"]
+            else:
+                t = torch.from_numpy(x.copy())[None]
+            calls.append([])
+            with torch.no_grad():
+                ids.append(m.generate_chunk(t, torch.tensor([t.shape[1]]), key=["k"], tokenizer=_IdsTok(),
+                                            cache=cache, is_final=fin, device="cpu", maxlenratio=0.0,
+                                            minlenratio=0.0))
+            hyps.append(calls[-1][0] if calls[-1] else [])
+        flat, off = pack_tokens(ids)
+        yseq = [y for hs in hyps for (y, _) in hs]
+        yflat, yoff = pack_tokens(yseq)
+        out[f"{name}_ids"], out[f"{name}_ids_off"] = flat, off
+        out[f"{name}_yseq"], out[f"{name}_yseq_off"] = yflat, yoff
+        out[f"{name}_scores"] = np.array([sc for hs in hyps for (_, sc) in hs], np.float32)
+        out[f"{name}_nhyp"] = np.array([len(hs) for hs in hyps], np.int32)
+        out[f"{name}_opts"] = np.array([elb, dlb, beam, nbest, int(tail)], np.int32)
+        out[f"{name}_fopts"] = np.array([wctc, pen], np.float32)
+        print(name, "chunk ids", [len(t) for t in ids], "hyps", [len(h) for h in hyps])
+    np.savez_compressed(f"{HERE}/stream_beam_tiny.npz", **out)
+
+    # waveform path: inference() builds the search from its kwargs (model.py:567-575)
+    import funasr.frontends.wav_frontend as wf
+    from oracle import fbank_ref
+    from tests.golden.inputs import waveform
+
+    def kfbank(w, **k):
+        return torch.from_numpy(fbank_ref.fbank(w[0].numpy().astype(np.float32) / np.float32(32768.0)))
+
+    sys.modules["torchaudio.compliance.kaldi"].fbank = kfbank
+    wf.kaldi.fbank = kfbank
+    front = wf.WavFrontendOnline(cmvn_file=CMVN, fs=16000, window="hamming", n_mels=80, frame_length=25,
+                                 frame_shift=10, lfr_m=7, lfr_n=6, dither=0.0)
+
+    class Tok:
+        def ids2tokens(self, ids):
+            return [toks[i] for i in ids]
+
+    m = build()
+    wav = waveform(seed=33, n=57600 + 2000)
+    calls = [9600] * 6 + [2000]
+    cache, texts, pos = {}, [], 0
+    for j, n in enumerate(calls):
+        with torch.no_grad():
+            res, _ = m.inference([torch.from_numpy(wav[pos:pos + n].copy())], key=["s"], tokenizer=Tok(),
+                                 frontend=front, cache=cache, is_final=j == len(calls) - 1, chunk_size=[0, 10, 5],
+                                 encoder_chunk_look_back=4, decoder_chunk_look_back=1,
+                                 encoder_conf={"output_size": 512}, frontend_conf={"n_mels": 80, "lfr_m": 7},
+                                 device="cpu", data_type="sound", token_list=toks, decoding_ctc_weight=0.4,
+                                 beam_size=3, nbest=2, penalty=0.0)
+        texts.append(res[0]["text"])
+        pos += n
+    with open(f"{HERE}/stream_beam_wave.json", "w") as f:
+        json.dump(dict(seed=33, n=57600 + 2000, calls=calls, texts=texts, decoding_ctc_weight=0.4, beam_size=3,
+                       nbest=2), f, ensure_ascii=False, indent=1)
+    print("wave", texts)
+
+
 PUNC_TEXTS = {
     "short": 12,            # CJK tokens only, one mini-sentence
     "mixed": 47,            # CJK + ASCII words (split_words keeps ASCII runs as one word; unknown -> <unk>)

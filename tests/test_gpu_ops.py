@@ -186,14 +186,11 @@ def test_fsmn(dev, B, T, lens, left):
     assert (got.double().cpu() - want).abs().max().item() < 1e-5
 
 
-@pytest.mark.parametrize("variant", ["0", "4", "8", "16"])
 @pytest.mark.parametrize("B,T,lens,left", [(2, 50, [50, 17], 5), (1, 9, [9], 5), (3, 40, [1, 40, 11], 7),
                                            (4, 500, [500, 1, 250, 499], 5)])
-def test_fsmn_bf16(dev, B, T, lens, left, variant, monkeypatch):
-    """Fast-mode FSMN (bf16 in / bf16 out; PFM_FSMN_V2 selects the 4-channel kernel or the 8-channel
-    kernel's frames per thread) vs fp64 on the same bf16 inputs: one bf16 output rounding, so
+def test_fsmn_bf16(dev, B, T, lens, left):
+    """Fast-mode FSMN (bf16 in / bf16 out) vs fp64 on the same bf16 inputs: one bf16 output rounding, so
     rel-L2 <= 4e-3 and the padded rows exactly zero."""
-    monkeypatch.setenv("PFM_FSMN_V2", variant)
     D, K = 512, 11
     g = torch.Generator().manual_seed(T + left)
     v = torch.randn(B * T, D, generator=g).bfloat16()
@@ -371,16 +368,13 @@ def _dec_ffn_ref(x1, p, eps=1e-12):
     return y, exact
 
 
-@pytest.mark.parametrize("kern", ["1", "2"])
 @pytest.mark.parametrize("M", [64, 200, 1000, 4100])
 @pytest.mark.parametrize("outproj", [False, True])
-def test_ffn_fused_decoder(dev, M, outproj, kern, monkeypatch):
+def test_ffn_fused_decoder(dev, M, outproj):
     """The decoder FFN exactly as the fast path runs it (ffn_fused_kernel DEC: LN1 prologue, LN_F folded through
     W2, next LayerNorm epilogue; with outproj the previous block's cross-attention out-projection as phase 0,
     x1 = x + o Wo^T + bo written back) vs fp64 on the kernel's bf16 roundings: y rel-L2 < 5e-3 (and < 2e-2 vs
-    the unrounded W2 LN_F(h)), xn within 1.6e-2 of LN_next of the fp64 y plus the y error; x1 rel < 1e-6.
-    Both fused kernels (PFM_DEC_FFN_KERNEL 1 / 2)."""
-    monkeypatch.setenv("PFM_DEC_FFN_KERNEL", kern)
+    the unrounded W2 LN_F(h)), xn within 1.6e-2 of LN_next of the fp64 y plus the y error; x1 rel < 1e-6."""
     g = torch.Generator().manual_seed(17 * M + outproj)
     p = _ffn_params(g, dec=True)
     x = torch.randn(M, 512, generator=g) * 2

@@ -144,7 +144,12 @@ def test_automodel_vad_asr_punc_pipeline_vs_reference(name):
     w = make_weights(cfg)
     eng = am.model.engine()
     hip_front = am.kwargs["frontend"]
-    calls = gj["asr_calls"]
+    # the reference decoder's decisions per utterance, in the order the pipeline decoded them (the golden ran on the
+    # CPU, where AutoModel.inference decodes one utterance per call; the HIP pipeline batches the VAD batch)
+    utts = []
+    for c in gj["asr_calls"]:
+        off = np.concatenate([[0], np.cumsum(c["ntok"])])
+        utts += [(nb, c["argmax"][off[b]:off[b + 1]], c["margin"][off[b]:off[b + 1]]) for b, nb in enumerate(c["ntok"])]
 
     def gpu_feats(items):
         speech, lens, _ = hip_front(eng, items)
@@ -169,20 +174,17 @@ def test_automodel_vad_asr_punc_pipeline_vs_reference(name):
             return texts(r["tokens"], key, len(lens), tokenizer), {}
 
     class ReplayASR(torch.nn.Module):
-        """The reference decoder's recorded decisions, batch by batch, behind the same contract."""
+        """The reference decoder's recorded decisions, utterance by utterance, behind the same contract."""
 
         def __init__(self):
             super().__init__()
             self.i = 0
 
         def inference(self, data_in, data_lengths=None, key=None, tokenizer=None, frontend=None, **kw):
-            c = calls[self.i]
-            self.i += 1
             n = len(data_in) if isinstance(data_in, (list, tuple)) else 1
-            assert n == len(c["ntok"])        # the same batch plan as the reference's
-            off = np.concatenate([[0], np.cumsum(c["ntok"])])
-            ids = [[t for t in c["argmax"][off[b]:off[b + 1]] if t not in (cfg.eos, cfg.sos, cfg.blank_id)]
-                   for b in range(n)]
+            ids = [[t for t in am_ids if t not in (cfg.eos, cfg.sos, cfg.blank_id)]
+                   for _, am_ids, _ in utts[self.i:self.i + n]]
+            self.i += n
             return texts(ids, key, n, tokenizer), {}
 
     hip_model = am.model
@@ -192,25 +194,22 @@ def test_automodel_vad_asr_punc_pipeline_vs_reference(name):
         runs_gpu = am.model.runs
         am.model = ReplayASR()
         host = am.generate(input=wav, batch_size_s=gj["batch_size_s"])[0]["text"]
-        assert am.model.i == len(calls)
+        assert am.model.i == len(utts)
     finally:
         am.model = hip_model
     assert alone == res[0]["text"], (alone, res[0]["text"])          # (1)
     assert host == want, (host, want)                                 # (2)
-    assert len(runs_gpu) == len(calls)                                # (3)
+    gpu_utts = [(int(rg["ntok"][b]), rg["argmax"][b].numpy()) for rg in runs_gpu for b in range(len(rg["ntok"]))]
+    assert len(gpu_utts) == len(utts)                                 # (3)
     flips, worst = 0, 0.0
-    for rg, c in zip(runs_gpu, calls):
-        off = np.concatenate([[0], np.cumsum(c["ntok"])])
-        for b, nb in enumerate(c["ntok"]):
-            na = int(rg["ntok"][b])
-            assert abs(na - nb) <= 1
-            if na != nb:
-                continue
-            ref = np.asarray(c["argmax"][off[b]:off[b + 1]])
-            bad = np.nonzero(rg["argmax"][b, :na].numpy() != ref)[0]
-            flips += len(bad)
-            if len(bad):
-                worst = max(worst, float(np.asarray(c["margin"][off[b]:off[b + 1]])[bad].max()))
+    for (na, am_gpu), (nb, am_ref, mg) in zip(gpu_utts, utts):
+        assert abs(na - nb) <= 1
+        if na != nb:
+            continue
+        bad = np.nonzero(am_gpu[:na] != np.asarray(am_ref))[0]
+        flips += len(bad)
+        if len(bad):
+            worst = max(worst, float(np.asarray(mg)[bad].max()))
     print(f"VAD pipeline v1: GPU vs reference features flip {flips} tokens, largest reference margin {worst:.4f} "
           f"nat; pipeline {res[0]['text']!r} vs reference {want!r}")
     assert worst < 0.5
