@@ -41,6 +41,11 @@ HBM_PEAK_GBS = 8000.0
 FRAME_SEC = 0.06                                    # 10 ms shift x lfr_n 6 (paraformer/model.py:491-493)
 
 
+def progress(msg: str) -> None:
+    """One progress line on stderr per finished leg (a long default run stays visibly alive)."""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def path_flops(T: int, L: np.ndarray) -> float:
     """F(T,L) = 333,634,560 T + 102,400 T^2 + 96,866,304 L + 32,768 L T per utterance."""
     L = np.asarray(L, dtype=np.float64)
@@ -65,46 +70,60 @@ def cpu_model() -> str:
 
 
 def stream_leg(args, dev, torch, make_weights) -> dict:
+    import dataclasses
     from funasr_amd.config import paraformer_streaming
     from funasr_amd.runtime import PfmEngine, PfmStreams
     cfg = paraformer_streaming()
-    eng = PfmEngine(cfg, dev.index or 0)
-    eng.load_state_dict(make_weights(cfg, args.seed))
     C = args.stream_chunks
-    g = torch.Generator(device=dev)
-    g.manual_seed(2000)
     res = {"workload": f"Paraformer-large streaming, chunk [0,10,5] (600 ms), look-back 4/1, {C} chunks "
                        f"({C * 0.6:.0f} s) per stream, synthetic LFR+CMVN rows", "dtype": "bf16" if args.mode == "fast"
                        else "f32", "mode": args.mode}
-    for S in (1, args.stream_batch):
-        chunks = torch.randn((C, S, 10, cfg.input_size), generator=g, device=dev, dtype=torch.float32)
-        st = PfmStreams(eng, S, (0, 10, 5), 4, 1, args.mode)
-        ids = list(range(S))
+    # greedy (the released model: ctc_weight 0) and, as BASELINE C5 names it, the joint decoder + CTC prefix beam
+    # per chunk (a CTC head, decoding_ctc_weight 0.3, pfm_stream_step_beam)
+    for leg, lcfg in (("", cfg), ("beam_", dataclasses.replace(cfg, ctc_weight=0.3))):
+        eng = PfmEngine(lcfg, dev.index or 0)
+        eng.load_state_dict(make_weights(lcfg, args.seed))
+        g = torch.Generator(device=dev)
+        g.manual_seed(2000)
+        bkw = dict(beam=args.beam, ctc_weight=0.3, penalty=0.0, nbest=1)
+        for S in (1, args.stream_batch):
+            chunks = torch.randn((C, S, 10, cfg.input_size), generator=g, device=dev, dtype=torch.float32)
+            st = PfmStreams(eng, S, (0, 10, 5), 4, 1, args.mode)
+            ids = list(range(S))
 
-        def one_stream():
-            st.reset(ids)
-            toks = 0
-            lat = []
-            for c in range(C):
-                t0 = time.perf_counter()
-                r = st.step(ids, chunks[c], [10] * S, [c == C - 1] * S)
-                toks += int(r["ntok"].sum().item())    # the host needs the tokens of every chunk
-                lat.append(time.perf_counter() - t0)
-            return toks, lat
+            def one_stream():
+                st.reset(ids)
+                toks = 0
+                lat = []
+                for c in range(C):
+                    t0 = time.perf_counter()
+                    if leg:
+                        r = st.step_beam(ids, chunks[c], [10] * S, [c == C - 1] * S, **bkw)
+                        n = r["ntok"][:, 0]
+                        toks += int(n.clamp(min=0).sum().item())
+                    else:
+                        r = st.step(ids, chunks[c], [10] * S, [c == C - 1] * S)
+                        toks += int(r["ntok"].sum().item())    # the host needs the tokens of every chunk
+                    lat.append(time.perf_counter() - t0)
+                return toks, lat
 
-        one_stream()   # warmup (workspace growth, first-call setup)
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        toks, lat = one_stream()
-        torch.cuda.synchronize()
-        dt = time.perf_counter() - t0
-        key = "single" if S == 1 else f"streams_{S}"
-        res[key] = {"streams": S, "value": round(S * C * 0.6 / dt, 1), "unit": "audio-sec/sec",
-                    "chunk_ms_mean": round(float(np.mean(lat)) * 1e3, 3),
-                    "chunk_ms_p90": round(float(np.percentile(lat, 90)) * 1e3, 3),
-                    "tokens_per_chunk_mean": round(toks / (S * C), 2)}
-        del st, chunks
-    del eng
+            one_stream()   # warmup (workspace growth, first-call setup)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            toks, lat = one_stream()
+            torch.cuda.synchronize()
+            dt = time.perf_counter() - t0
+            key = leg + ("single" if S == 1 else f"streams_{S}")
+            res[key] = {"streams": S, "value": round(S * C * 0.6 / dt, 1), "unit": "audio-sec/sec",
+                        "chunk_ms_mean": round(float(np.mean(lat)) * 1e3, 3),
+                        "chunk_ms_p90": round(float(np.percentile(lat, 90)) * 1e3, 3),
+                        "tokens_per_chunk_mean": round(toks / (S * C), 2)}
+            progress(f"streaming {key}: {res[key]['chunk_ms_mean']} ms per chunk")
+            if leg:
+                res[key]["search"] = (f"beam {args.beam}, decoding_ctc_weight 0.3, CTC over each chunk's 15-row "
+                                      f"window, nbest 1")
+            del st, chunks
+        del eng
     if args.cpu_utts > 0:
         # the oracle's streaming restatement (torch-CPU fp32, one stream) on the first 10 chunks
         from oracle.streaming_ref import StreamState, chunk_step
@@ -343,21 +362,28 @@ def main():
     g_ach = gemm["flops"] / (gemm["ms"] / 1e3) / 1e12 if gemm["ms"] > 0 else 0.0
     # HBM bytes per launch of the same kernel set from the committed PMC passes (rocprofv3 --pmc FETCH_SIZE /
     # WRITE_SIZE, separate runs of this bench, gfx950-corrected by tools/pmc_traffic.py); null when absent
-    traffic, traffic_src = None, None
-    tname = next((n for n in ("r03_gemm_traffic.json", "r02b_gemm_traffic.json")
+    # and the class's MFMA-busy fraction from a third pass (SQ_VALU_MFMA_BUSY_CYCLES, GRBM_GUI_ACTIVE)
+    traffic, traffic_src, busy, busy_src = None, None, None, None
+    tname = next((n for n in ("r04_pmc_bench.json", "r03_gemm_traffic.json", "r02b_gemm_traffic.json")
                   if os.path.exists(os.path.join(ROOT, "profiles", n))), None)
     if args.mode == "fast" and tname:
         with open(os.path.join(ROOT, "profiles", tname)) as f:
-            traffic = round(json.load(f)["hbm_bytes_per_launch"])
+            pmc = json.load(f)
+        traffic = round(pmc["hbm_bytes_per_launch"])
         traffic_src = (f"profiles/{tname} (PMC FETCH_SIZE x2 + WRITE_SIZE per launch of the GEMM "
                        "class: bf16 GEMMs + fused FFN)")
+        if pmc.get("mfma_busy_gemm_class") is not None:
+            busy = round(pmc["mfma_busy_gemm_class"], 4)
+            busy_src = f"profiles/{tname}: " + pmc.get("mfma_busy_definition", "")
     roofline = {"bound": "mfma",
-                "kernel": ("gemm_bf16_kernel (QKV / out-proj / decoder / vocabulary) + ffn_fused_kernel (encoder "
-                           "LN2-FFN-LN1) (+gemm_nt_kernel<bf16> for K%64!=0)") if args.mode == "fast" else
+                "kernel": ("ffn2_kernel<4> (encoder out-proj + LN2-FFN + LN1 + next QKV) + ffn_fused_kernel (decoder "
+                           "FFNs) + gemm_bf16_kernel (layer-0 QKV / decoder / vocabulary)") if args.mode == "fast" else
                           "gemm_bf16_kernel, split-bf16 x6 emulation of f32 (flops counted as f32 2MNK)",
                 "achieved": round(g_ach, 2), "peak": peak, "unit": "TFLOP/s", "frac": round(g_ach / peak, 4),
                 "traffic": traffic,
                 "traffic_source": traffic_src,
+                "mfma_busy": busy,
+                "mfma_busy_source": busy_src,
                 "algorithmic_bytes_per_launch": round(gemm["bytes"] / max(1, gemm["launches"])),
                 "avg_launch_us": round(gemm["ms"] * 1e3 / max(1, gemm["launches"]), 2),
                 "avg_launch_us_raw": round(g_raw_ms * 1e3 / max(1, gemm["launches"]), 2),
@@ -395,6 +421,8 @@ def main():
         if shared:   # not an N-GPU result: N ranks time-share fewer devices
             out["metric"] = METRIC + " [REHEARSAL: ranks share a device, not a multi-GPU measurement]"
 
+    if rank == 0:
+        progress("headline leg done")
     # ---- exact (f32 MFMA) mode on the same batch: token-parity mode throughput + agreement
     if rank == 0 and args.mode == "fast" and args.exact_steps > 0:
         eng.run(feats, lens, mode="exact")
@@ -426,6 +454,8 @@ def main():
             "fast_vs_exact_token_agreement": round(float(np.mean(agree)), 4),
             "fast_vs_exact_ntok_equal": round(float(np.mean(na == nb)), 4)}
 
+    if rank == 0:
+        progress("exact leg done")
     # ---- SenseVoiceSmall (BASELINE config C4): B x 30 s on the same fbank batch, rank 0
     if rank == 0 and args.sv_steps > 0:
         from funasr_amd.config import sense_voice_small
@@ -450,6 +480,8 @@ def main():
                              "tokens_per_utt_mean": float(sv_last["ntok"].float().mean().item())}
         del seng
 
+    if rank == 0:
+        progress("SenseVoice leg done")
     # ---- joint decoder + CTC prefix beam search (BASELINE config C5's CTC prefix-beam; Paraformer.inference with
     # decoding_ctc_weight): Paraformer-large with a CTC head (ctc_weight 0.3), the same batch, rank 0
     if rank == 0 and args.beam_steps > 0:
@@ -475,20 +507,28 @@ def main():
                               "tokens_per_utt_mean": round(float(nb[nb >= 0].mean().item()), 2)}
         del beng
 
+    if rank == 0:
+        progress("beam-search leg done")
     # ---- streaming Paraformer (BASELINE config C5): 600 ms chunks ([0, 10, 5], look-back 4 / 1) of
     # 30 s streams through pfm_stream_step, synthetic LFR+CMVN chunk rows resident in HBM; one stream
     # (the reference's batch 1: per-chunk latency) and S concurrent streams (serving throughput), rank 0
     if rank == 0 and world == 1 and args.stream_chunks > 0:
         out["streaming"] = stream_leg(args, dev, torch, make_weights)
 
+    if rank == 0:
+        progress("streaming leg done")
     # ---- CT-Transformer punctuation: 64 word sequences x 200 words per pfm_run_punc
     if rank == 0 and world == 1 and args.punc_steps > 0:
         out["punctuation"] = punc_leg(args, dev, torch, make_weights)
 
+    if rank == 0:
+        progress("punctuation leg done")
     # ---- VAD-segmented long-audio transcription: FSMN-VAD -> ASR -> punctuation
     if rank == 0 and world == 1 and args.long_audio_s > 0:
         out["long_audio"] = long_audio_leg(args, sd, cfg)
 
+    if rank == 0:
+        progress("long-audio leg done")
     # ---- CPU baseline: the oracle torch-CPU restatement on a bounded sample (rank 0, N=1 only)
     if rank == 0 and world == 1 and args.cpu_utts > 0:
         from oracle.paraformer_ref import paraformer_infer

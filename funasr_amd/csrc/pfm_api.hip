@@ -61,8 +61,8 @@ hipError_t pfm_ctc_collapse(const int* ids, long long ld, const int* olen, int B
 hipError_t pfm_f32_to_bf16(const float* x, bf16* y, long long n, hipStream_t st);
 hipError_t pfm_swap_last2(const float* x, float* y, long long A, long long Bd, long long C, hipStream_t st);
 hipError_t pfm_logsoftmax_rows(float* x, long long rows, long long ld, int V, hipStream_t st);
-long long pfm_ctc_beam_fscratch(int K, int P, int T, int L);
-long long pfm_ctc_beam_iscratch(int K, int nbest, int L);
+long long pfm_ctc_beam_fscratch(int K, int P, int T, int L, int V);
+long long pfm_ctc_beam_iscratch(int K, int nbest, int L, int P, int V);
 hipError_t pfm_ctc_beam(const float* am, int L, const float* x, int T, const int* lens, const int* ntok, int B, int V,
                         int K, int P, int nbest, float wctc, float pen, int use_pen, int end_detect, int sos, int eos,
                         int blank, float* fs, int* is, int* tokens, int Lcap, int* olen, float* oscore,
@@ -1616,7 +1616,7 @@ int pfm_run_beam(pfm_handle* h, void* stream, int mode, const float* feats, cons
     HIP_TRY(pfm_logsoftmax_rows(h->ctcx.as<float>(), M, V, V, st));
     HIP_TRY(pfm_logsoftmax_rows(h->logits.as<float>(), (long long)B * L, V, V, st));   // decoder log_softmax
     // the search (ntok of the run: the device token counts behind pfm_run's ntok_out)
-    const long long fsz = pfm_ctc_beam_fscratch(beam, P, T, L), isz = pfm_ctc_beam_iscratch(beam, nbest, L);
+    const long long fsz = pfm_ctc_beam_fscratch(beam, P, T, L, V), isz = pfm_ctc_beam_iscratch(beam, nbest, L, P, V);
     // the device token counts (first B ints of beam_is) move behind the float scratch before beam_is is resized
     HIP_TRY(hipStreamSynchronize(st));
     HIP_TRY(h->beam_fs.ensure(((size_t)B * fsz + B) * sizeof(float)));
@@ -2080,8 +2080,8 @@ int pfm_op_ctc_beam(void* stream, const float* am, int L, const float* x, int T,
     OpScratch sc;
     float* fs;
     int* is;
-    HIP_TRY(sc.alloc(&fs, (size_t)B * pfm_ctc_beam_fscratch(beam, P, T, L)));
-    HIP_TRY(sc.alloc(&is, (size_t)B * pfm_ctc_beam_iscratch(beam, nbest, L)));
+    HIP_TRY(sc.alloc(&fs, (size_t)B * pfm_ctc_beam_fscratch(beam, P, T, L, V)));
+    HIP_TRY(sc.alloc(&is, (size_t)B * pfm_ctc_beam_iscratch(beam, nbest, L, P, V)));
     HIP_TRY(pfm_ctc_beam(am, L, x, T, lens, ntok, B, V, beam, P, nbest, ctc_weight, penalty, penalty != 0.f ? 1 : 0,
                          end_detect, sos, eos, blank, fs, is, tokens, L_cap, ntok_out, scores_out, st));
     HIP_TRY(hipStreamSynchronize(st));
@@ -2588,8 +2588,8 @@ int stream_step(pfm_streams* s, void* stream, int n, const int32_t* slot_ids, co
         HIP_TRY(pfm_logsoftmax_rows(h->ctcx.as<float>(), (long long)n * Tw, V, V, st));
         HIP_TRY(pfm_logsoftmax_rows(h->logits.as<float>(), (long long)n * L, V, V, st));
         HIP_TRY(hipMemsetAsync(sb->scores, 0, (size_t)n * sb->nbest * sizeof(float), st));
-        const long long fsz = pfm_ctc_beam_fscratch(sb->beam, sb->P, Tw, L);
-        const long long isz = pfm_ctc_beam_iscratch(sb->beam, sb->nbest, L);
+        const long long fsz = pfm_ctc_beam_fscratch(sb->beam, sb->P, Tw, L, V);
+        const long long isz = pfm_ctc_beam_iscratch(sb->beam, sb->nbest, L, sb->P, V);
         HIP_TRY(h->beam_fs.ensure((size_t)n * fsz * sizeof(float)));
         HIP_TRY(h->beam_is.ensure((size_t)n * isz * sizeof(int32_t)));
         HIP_TRY(pfm_ctc_beam(h->logits.as<float>(), L, h->ctcx.as<float>(), Tw, tw_d, ntok, n, V, sb->beam, sb->P,

@@ -72,11 +72,18 @@ int main(int argc, char** argv) {
     CK(hipDeviceSynchronize());
     const float *g = vecs, *be = vecs + 2048, *b1 = vecs + 4096, *b2 = vecs + 6144, *gn = vecs + 8192, *bn = vecs + 10240,
                 *bo = vecs + 12288, *c1 = vecs + 14336;
-    const bool only = getenv("FFN2_ONLY") != nullptr;   // PMC passes: the OP kernel alone
+    // PMC passes: FFN2_ONLY=1 the OP kernel alone (MODE 1), FFN2_ONLY=4 the OP + next-QKV kernel (MODE 4, the default)
+    const char* only_env = getenv("FFN2_ONLY");
+    const bool only = only_env != nullptr, only4 = only && atoi(only_env) == 4;
     for (int M : Ms) {
         const double fl1 = 2.0 * M * (2.0 * 512 * 2048 + 512.0 * 512), fl0 = 2.0 * M * 2.0 * 512 * 2048;
         const int reps = 20;
         float t;
+        if (only4) {
+            t = run<4, 0>(M, 5, X, g, be, Wp, b1, b2, Xo, gn, bn, Xn, O, Fr, bo, c1);
+            printf("M=%6d OP+QKV full      %8.1f us  %7.1f TF/s\n", M, t, (fl1 + 2.0 * M * 1536 * 512) / t / 1e6);
+            continue;
+        }
         if (only) {
             t = run<1, 0>(M, 5, X, g, be, Wp, b1, b2, Xo, gn, bn, Xn, O, Fr, bo, c1);
             printf("M=%6d OP   full        %8.1f us  %7.1f TF/s\n", M, t, fl1 / t / 1e6);
@@ -100,8 +107,6 @@ int main(int argc, char** argv) {
         printf("M=%6d OP+QKV full      %8.1f us  %7.1f TF/s\n", M, t, (fl1 + 2.0 * M * 1536 * 512) / t / 1e6);
         t = run<0, 0>(M, reps, X, g, be, Wp + 262144, b1, b2, Xo, gn, bn, Xn, O, Fr, bo, c1);
         printf("M=%6d FFN  full        %8.1f us  %7.1f TF/s\n", M, t, fl0 / t / 1e6);
-        t = run<2, 0>(M, reps, X, g, be, Wp + 262144, b1, b2, Xo, gn, bn, Xn, O, Fr, bo, c1);
-        printf("M=%6d DEC  full        %8.1f us  %7.1f TF/s\n", M, t, fl0 / t / 1e6);
     }
     return 0;
 }

@@ -4,7 +4,11 @@ MI355X_MICROARCH gfx950 corrections: FETCH_SIZE (KB) counts half the bytes of 16
 reads (the GEMM's global_load_lds_dwordx4 operand stream and float4 residual loads) -> x2;
 WRITE_SIZE (KB) is exact for 16-B-per-lane stores (the GEMM epilogue's float4 / bf16x8 stores).
 
-usage: python tools/pmc_traffic.py fetch_results.db write_results.db out.json
+With a third database (`--pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_BUSY_CYCLES`), the MFMA-busy fraction of
+each kernel: SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x GRBM_GUI_ACTIVE / 8), GRBM_GUI_ACTIVE being the sum over the 8
+XCDs of the dispatch's GPU-busy cycles (MI355X_MICROARCH.md, DVFS note).
+
+usage: python tools/pmc_traffic.py fetch_results.db write_results.db out.json [mfma_results.db]
 """
 import json
 import sqlite3
@@ -21,10 +25,39 @@ def per_dispatch(db, counter):
 
 def is_gemm(name):
     return ("gemm_bf16_kernel" in name or "gemm_nt_kernelIDF16b" in name or "gemm_nt_kernel<__bf16>" in name
-            or "ffn_fused_kernel" in name)
+            or "ffn_fused_kernel" in name or "ffn2_kernel" in name)
 
 
-def main(fdb, wdb, out):
+def short(name):
+    for k in ("ffn2_kernel<4", "ffn2_kernel<1", "ffn2_kernel<0", "ffn_fused_kernel<0, 3", "ffn_fused_kernel<0, 2",
+              "ffn_fused_kernel<0, 1", "ffn_fused_kernel<0, 0", "attn_bf16_kernel", "gemm_bf16_kernel", "gemm_nt_kernel"):
+        if k in name:
+            return k
+    return name[:40]
+
+
+def mfma_busy(db):
+    """per kernel class: launches, MFMA-busy cycles, GPU-busy cycles (GRBM_GUI_ACTIVE / 8) and their quotient per SIMD"""
+    c = sqlite3.connect(db)
+    rows = c.execute("select dispatch_id, kernel_name, counter_name, value from counters_collection").fetchall()
+    per = defaultdict(dict)
+    names = {}
+    for d, k, cn, v in rows:
+        per[d][cn] = per[d].get(cn, 0.0) + v
+        names[d] = k
+    agg = defaultdict(lambda: [0, 0.0, 0.0])
+    for d, cnt in per.items():
+        a = agg[short(names[d])]
+        a[0] += 1
+        a[1] += cnt.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0)
+        a[2] += cnt.get("GRBM_GUI_ACTIVE", 0.0) / 8.0
+    out = {k: {"launches": v[0], "mfma_busy": v[1] / (1024.0 * v[2]) if v[2] else None} for k, v in agg.items()}
+    g = [v for k, v in agg.items() if is_gemm(k)]
+    tot = [sum(x[1] for x in g), sum(x[2] for x in g)]
+    return out, (tot[0] / (1024.0 * tot[1]) if tot[1] else None)
+
+
+def main(fdb, wdb, out, mdb=None):
     f = per_dispatch(fdb, "FETCH_SIZE")
     w = per_dispatch(wdb, "WRITE_SIZE")
     shapes = defaultdict(lambda: [0, 0.0, 0.0])
@@ -49,8 +82,15 @@ def main(fdb, wdb, out):
                        "write_MB": v[2] / max(1, v[0]) / 1e6} for k, v in sorted(shapes.items(), key=lambda kv: -kv[1][1])],
     }
     res["hbm_bytes_per_launch"] = res["fetch_bytes_per_launch"] + res["write_bytes_per_launch"]
+    if mdb:
+        per_kernel, gemm_busy = mfma_busy(mdb)
+        res["mfma_busy_gemm_class"] = gemm_busy
+        res["mfma_busy_per_kernel"] = per_kernel
+        res["mfma_busy_definition"] = "SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x GRBM_GUI_ACTIVE / 8), summed per class"
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps({k: v for k, v in res.items() if k != "per_shape"}, indent=1))
+    for k, v in res.get("mfma_busy_per_kernel", {}).items():
+        print(f"  MFMA busy {k:30s} x{v['launches']:4d}: {v['mfma_busy']}")
     for s in res["per_shape"]:
         print(f"  {s['kernel'][-40:]:40s} blocks {s['blocks']:5d} x{s['launches']:3d}: fetch {s['fetch_MB']:8.1f} MB "
               f"write {s['write_MB']:8.1f} MB")

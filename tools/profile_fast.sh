@@ -10,7 +10,7 @@ mkdir -p "$R/gpurun_out/$name"
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/$name" -o run -- \
   python3 "$R/bench.py" --steps 5 --warmup 2 --exact-steps 0 --cpu-utts 0 --sv-steps 0 --stream-chunks 0 \
-  --punc-steps 0 --long-audio-s 0 "$@" > "$R/gpurun_out/$name/bench.log" 2>&1
+  --punc-steps 0 --long-audio-s 0 --beam-steps 0 "$@" > "$R/gpurun_out/$name/bench.log" 2>&1
 rc=$?
 cd "$R"
 [ $rc -eq 0 ] && python tools/rocpd_summary.py "gpurun_out/$name/run_results.db" "gpurun_out/$name/stats.csv" \
