@@ -89,7 +89,139 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(const bf16* __restrict
     }
 }
 
+// The same GEMM with the LayerNorm of its A rows in front (streaming: LN1 -> QKV, LN2 -> FFN w1, decoder LN -> w1 / q):
+// A = bf16(LN(X) g + b) for f32 rows X [M, K = 512]; every workgroup normalises the <= 64 rows of its row block into
+// LDS (one wave per row, the statistics of layernorm_v8_kernel: f64 sums in the same order, f32 affine), so the
+// LayerNorm's own launch and its bf16 round trip through HBM go away. Rows padded by 8 elements in LDS (conflict-free
+// 16-B fragment reads across the 16 rows of a tile).
+constexpr int LNK = 512, LNP = LNK + 8;
+template <int MT>
+__global__ __launch_bounds__(512) void gemm_skinny_ln_kernel(const float* __restrict__ X, RowMap xmap,
+                                                             const float* __restrict__ g, const float* __restrict__ bta,
+                                                             float eps, const bf16* __restrict__ W, long long ldw, int M,
+                                                             int N, GemmEpi e) {
+    __shared__ float red[SK_WAVES][MT][256];
+    __shared__ __attribute__((aligned(16))) bf16 As[MT * 16][LNP];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int mb = blockIdx.y * 64;
+    {   // LN of the block's rows (wave w: rows w, w + 8, ...)
+        const int c = lane * 8;
+        const float4 g0 = *(const float4*)(g + c), g1 = *(const float4*)(g + c + 4);
+        const float4 b0 = *(const float4*)(bta + c), b1 = *(const float4*)(bta + c + 4);
+        for (int rr = w; rr < MT * 16; rr += SK_WAVES) {
+            const int row = mb + rr;
+            bf16x8 o = {};
+            if (row < M) {
+                const float* xr = X + xmap.off(row);
+                const float4 v0 = *(const float4*)(xr + c), v1 = *(const float4*)(xr + c + 4);
+                double s = 0.0;
+                s += (double)v0.x + (double)v0.y + (double)v0.z + (double)v0.w;
+                s += (double)v1.x + (double)v1.y + (double)v1.z + (double)v1.w;
+                const double mean = wave_sum_d(s) / LNK;
+                double q = 0.0;
+                {
+                    const double a0 = v0.x - mean, a1 = v0.y - mean, a2 = v0.z - mean, a3 = v0.w - mean;
+                    q += a0 * a0 + a1 * a1 + a2 * a2 + a3 * a3;
+                }
+                {
+                    const double a0 = v1.x - mean, a1 = v1.y - mean, a2 = v1.z - mean, a3 = v1.w - mean;
+                    q += a0 * a0 + a1 * a1 + a2 * a2 + a3 * a3;
+                }
+                const double rstd = 1.0 / sqrt(wave_sum_d(q) / LNK + (double)eps);
+                float y[8];
+                y[0] = (float)((v0.x - mean) * rstd) * g0.x + b0.x;
+                y[1] = (float)((v0.y - mean) * rstd) * g0.y + b0.y;
+                y[2] = (float)((v0.z - mean) * rstd) * g0.z + b0.z;
+                y[3] = (float)((v0.w - mean) * rstd) * g0.w + b0.w;
+                y[4] = (float)((v1.x - mean) * rstd) * g1.x + b1.x;
+                y[5] = (float)((v1.y - mean) * rstd) * g1.y + b1.y;
+                y[6] = (float)((v1.z - mean) * rstd) * g1.z + b1.z;
+                y[7] = (float)((v1.w - mean) * rstd) * g1.w + b1.w;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) o[j] = f2bf(y[j]);
+            }
+            *(bf16x8*)&As[rr][c] = o;   // rows beyond M: zeros
+        }
+    }
+    __syncthreads();
+    const int r16 = lane & 15, gq = lane >> 4;
+    const int n0 = blockIdx.x * 16;
+    const int n = n0 + r16;
+    const bool nok = n < N;
+    const bf16* wrow = W + (long long)(nok ? n : 0) * ldw + gq * 8;
+    f32x4 acc[MT];
+#pragma unroll
+    for (int t = 0; t < MT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const bf16x8 zero8 = {};
+    constexpr int nsteps = LNK / 32;
+    for (int s0 = w; s0 < nsteps; s0 += SK_WAVES * SK_UNROLL) {
+        bf16x8 bw[SK_UNROLL], ba[SK_UNROLL][MT];
+#pragma unroll
+        for (int u = 0; u < SK_UNROLL; ++u) {
+            const int st = s0 + u * SK_WAVES;
+            const bool sok = st < nsteps;
+            bw[u] = (sok && nok) ? *(const bf16x8*)(wrow + st * 32) : zero8;
+#pragma unroll
+            for (int t = 0; t < MT; ++t) ba[u][t] = sok ? *(const bf16x8*)&As[t * 16 + r16][st * 32 + gq * 8] : zero8;
+        }
+#pragma unroll
+        for (int u = 0; u < SK_UNROLL; ++u)
+#pragma unroll
+            for (int t = 0; t < MT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ba[u][t], bw[u], acc[t], 0, 0, 0);
+    }
+#pragma unroll
+    for (int t = 0; t < MT; ++t)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) red[w][t][(4 * gq + q) * 16 + r16] = acc[t][q];
+    __syncthreads();
+    for (int idx = threadIdx.x; idx < MT * 256; idx += 512) {
+        const int t = idx >> 8, rc = idx & 255;
+        const int row = mb + t * 16 + (rc >> 4), col = n0 + (rc & 15);
+        if (row >= M || col >= N) continue;
+        float v = 0.f;
+#pragma unroll
+        for (int ww = 0; ww < SK_WAVES; ++ww) v += red[ww][t][rc];
+        v *= e.alpha;
+        if (e.bias) v += e.bias[col];
+        if (e.relu) v = fmaxf(v, 0.f);
+        if (e.res0) v += e.res0_bf16 ? bf2f(((const bf16*)e.res0)[(long long)row * e.ld_res0 + col])
+                                     : e.res0[(long long)row * e.ld_res0 + col];
+        if (e.res1) v += e.res1[(long long)row * e.ld_res1 + col];
+        const long long ob = e.out_map.off(row);
+        if (e.out_dtype == DT_F32) ((float*)e.out)[ob + col] = v;
+        else ((bf16*)e.out)[ob + col] = f2bf(v);
+        if (e.out2) ((bf16*)e.out2)[e.out2_map.off(row) + col] = f2bf(v);
+    }
+}
+
 }  // namespace
+
+// LN-fused form: X f32 rows of K = 512 (16-B aligned), LN(X) g + b as the bf16 A operand; M <= 64 per row block (any M,
+// grid.y = ceil(M / 64)); the same epilogue contract as pfm_gemm_skinny
+bool pfm_gemm_skinny_ln_ok(const float* X, RowMap xmap, const void* W, long long ldw, int M, int N, int K,
+                           const GemmEpi& e) {
+    if (K != LNK || M < 1 || M > 64 || ldw % 8 != 0 || xmap.ld % 4 != 0) return false;
+    if (xmap.rows_per_seg > 0 && xmap.seg_stride % 4 != 0) return false;
+    if (((uintptr_t)X | (uintptr_t)W) % 16 != 0) return false;
+    if (!e.out || e.amax_val) return false;
+    return pfm_knobs().gemm_skinny && pfm_knobs().gemm_cfg == 0;
+}
+
+hipError_t pfm_gemm_skinny_ln(const float* X, RowMap xmap, const float* g, const float* b, float eps, const void* W,
+                              long long ldw, int M, int N, const GemmEpi& e, hipStream_t st) {
+    if (M <= 0 || N <= 0) return hipSuccess;
+    const dim3 grid((N + 15) / 16, (M + 63) / 64), block(512);
+    const bf16* wt = (const bf16*)W;
+    switch ((M + 15) / 16) {
+        case 1: hipLaunchKernelGGL(gemm_skinny_ln_kernel<1>, grid, block, 0, st, X, xmap, g, b, eps, wt, ldw, M, N, e); break;
+        case 2: hipLaunchKernelGGL(gemm_skinny_ln_kernel<2>, grid, block, 0, st, X, xmap, g, b, eps, wt, ldw, M, N, e); break;
+        case 3: hipLaunchKernelGGL(gemm_skinny_ln_kernel<3>, grid, block, 0, st, X, xmap, g, b, eps, wt, ldw, M, N, e); break;
+        case 4: hipLaunchKernelGGL(gemm_skinny_ln_kernel<4>, grid, block, 0, st, X, xmap, g, b, eps, wt, ldw, M, N, e); break;
+        default: return hipErrorInvalidValue;
+    }
+    PFM_LAUNCH_CHECK();
+    return hipSuccess;
+}
 
 // Shapes this kernel takes: bf16 operands, M <= 64 or few 128x256 tiles, K % 32 == 0, 16-B aligned rows, and an epilogue
 // without the fused argmax / LayerNorm-statistics features of the tiled kernels.

@@ -109,6 +109,10 @@ hipError_t pfm_fbank_launch(const float* wav, const int* nsamp, int B, int S_max
                             hipStream_t st);
 bool pfm_gemm_skinny_ok(const void* A, RowMap amap, const void* W, long long ldw, int M, int N, int K,
                         const GemmEpi& e);
+bool pfm_gemm_skinny_ln_ok(const float* X, RowMap xmap, const void* W, long long ldw, int M, int N, int K,
+                           const GemmEpi& e);
+hipError_t pfm_gemm_skinny_ln(const float* X, RowMap xmap, const float* g, const float* b, float eps, const void* W,
+                              long long ldw, int M, int N, const GemmEpi& e, hipStream_t st);
 hipError_t pfm_gemm_skinny(const void* A, RowMap amap, const void* W, long long ldw, int M, int N, int K,
                            const GemmEpi& e, hipStream_t st);
 hipError_t pfm_punc_embed(const int* ids, const int* lens, int B, int T, const float* embed, int n_embed,
@@ -793,6 +797,23 @@ struct Run {
             return gemm_x6(h, (const float*)A, am, (const float*)Wt, Mm, N, Kk, e, s);
         return gemm_dispatch(dtp, A, am, Wt, ldw, Mm, N, Kk, e, s);
     }
+    // A = LN(x) g + b, then the GEMM: chunk-sized fast-mode steps (<= 64 rows, K 512) run both in one skinny kernel
+    // (the rows normalised into LDS, k_gemm_skinny.hip); otherwise the LayerNorm writes `xn` (layout xnm, the GEMM's
+    // operand dtype) and the GEMM reads it
+    hipError_t ln_gemm(const float* x, RowMap xm, size_t g, size_t b, void* xn, RowMap xnm, const void* Wt, long long ldw,
+                       int Mm, int N, int Kk, const GemmEpi& e) const {
+        const pfm_config& c = h->cfg;
+        if (fast && pfm_gemm_skinny_ln_ok(x, xm, Wt, ldw, Mm, N, Kk, e)) {
+            ProfScope ps(h, st, PFM_K_GEMM, 2.0 * Mm * N * Kk,
+                         (double)Mm * Kk * 4.0 + (double)N * Kk * 2.0 +
+                             (double)Mm * N * (e.out_dtype == DT_F32 ? 4.0 : 2.0));
+            return pfm_gemm_skinny_ln(x, xm, P(g), P(b), c.ln_eps, Wt, ldw, Mm, N, e, st);
+        }
+        hipError_t er = pfm_layernorm(x, xm, Mm, Kk, P(g), P(b), c.ln_eps, nullptr, 0, 1.f, xn, xnm, dt, nullptr,
+                                      rowmap_plain(0), 0, st);
+        if (er != hipSuccess) return er;
+        return gemm(dt, xn, xnm, Wt, ldw, Mm, N, Kk, e);
+    }
     // EXACT-mode GEMM whose A operand a producer wrote as DT_X3 rows (am.ld = 3K); weights f32 in the arena
     hipError_t gemm3(const void* A3, RowMap am, const void* Wt, long long ldw, int Mm, int N, int Kk, const GemmEpi& e,
                      hipStream_t s = nullptr) const {
@@ -917,10 +938,18 @@ int encoder_stack(const Run& r, const float* x_in, const int* lens, int B, int T
             HIP_TRY(pfm_layernorm(x_in, rowmap_plain(I), (int)M, I, r.P(L.ln1g), r.P(L.ln1b), c.ln_eps,
                                   h->pe.as<float>(), T, sqrtf((float)D), Xn, rowmap_plain(I), dt, nullptr, plain, 0,
                                   st));
-        else if (!(ffn_fused && l > l0))   // fused FFN: the previous layer's kernel wrote LN1(x)
+        else if (!(ffn_fused && l > l0) && (x3 || !fast))   // fused FFN: the previous layer's kernel wrote LN1(x)
             HIP_TRY(pfm_layernorm(X, rowmap_plain(D), (int)M, D, r.P(L.ln1g), r.P(L.ln1b), c.ln_eps, nullptr, 0, 1.f,
                                   Xn, xmap3, lndt, nullptr, plain, 0, st));
-        if (!qkv_ready) {   // q|k|v = LN1(x) Wqkv^T + b   (fast mode: bf16 only — attention and FSMN read bf16)
+        // fast mode, l > 0 without the fused FFN in front: LN1 and the QKV projection through Run::ln_gemm
+        const bool ln1_fold = l > 0 && fast && !x3 && !(ffn_fused && l > l0);
+        if (!qkv_ready && ln1_fold) {
+            GemmEpi e = epi_default();
+            e.bias = r.P(L.bqkv);
+            e.out = QKVb; e.out_map = rowmap_plain(3 * D); e.out_dtype = DT_BF16;
+            HIP_TRY(r.ln_gemm(X, rowmap_plain(D), L.ln1g, L.ln1b, Xn, rowmap_plain(D), r.W(L.wqkv), din, (int)M, 3 * D,
+                              din, e));
+        } else if (!qkv_ready) {   // q|k|v = LN1(x) Wqkv^T + b   (fast mode: bf16 only — attention and FSMN read bf16)
             GemmEpi e = epi_default();
             e.bias = r.P(L.bqkv);
             if (fast) { e.out = QKVb; e.out_map = rowmap_plain(3 * D); e.out_dtype = DT_BF16; }
@@ -993,7 +1022,7 @@ int encoder_stack(const Run& r, const float* x_in, const int* lens, int B, int T
             else
                 HIP_TRY(r.gemm(dt, fast ? (const void*)Ob : (const void*)O, rowmap_plain(D), r.W(L.wo), D, (int)M, D,
                                D, e));
-            if (!ffn_fused)
+            if (!ffn_fused && (x3 || !fast))   // (fast mode: LN2 runs with the w1 GEMM below, Run::ln_gemm)
                 HIP_TRY(pfm_layernorm(X, rowmap_plain(D), (int)M, D, r.P(L.ln2g), r.P(L.ln2b), c.ln_eps, nullptr, 0,
                                       1.f, Xn, xmap3, lndt, nullptr, plain, 0, st));
         }
@@ -1035,6 +1064,8 @@ int encoder_stack(const Run& r, const float* x_in, const int* lens, int B, int T
             if (x3) {   // h written as w2's split operand
                 e.out_map = rowmap_plain(3 * Fd); e.out_dtype = DT_X3;
                 HIP_TRY(r.gemm3(Xn, xmap3, r.W(L.w1), D, (int)M, Fd, D, e));
+            } else if (fast) {
+                HIP_TRY(r.ln_gemm(X, rowmap_plain(D), L.ln2g, L.ln2b, Xn, rowmap_plain(D), r.W(L.w1), D, (int)M, Fd, D, e));
             } else {
                 HIP_TRY(r.gemm(dt, Xn, rowmap_plain(D), r.W(L.w1), D, (int)M, Fd, D, e));
             }
@@ -1832,6 +1863,30 @@ int pfm_op_gemm(void* stream, int dtype, const void* A, const void* Wt, const fl
     return PFM_OK;
 }
 
+int pfm_op_ln_gemm(void* stream, const float* X, const float* g, const float* b, float eps, const void* W,
+                   const float* bias, const float* res, float* C, int M, int N, int act) {
+    pfm_knobs_refresh();
+    if (!X || !g || !b || !W || !C || M < 0 || N < 0) return fail(PFM_E_ARG, "pfm_op_ln_gemm: null operand or bad sizes");
+    const hipStream_t st = (hipStream_t)stream;
+    GemmEpi e = epi_default();
+    e.bias = bias; e.relu = act & 1;
+    if (res) { e.res0 = res; e.ld_res0 = N; }
+    e.out = C; e.out_map = rowmap_plain(N); e.out_dtype = (act & 2) ? DT_BF16 : DT_F32;
+    constexpr int K = 512;
+    if (pfm_gemm_skinny_ln_ok(X, rowmap_plain(K), W, K, M, N, K, e)) {
+        HIP_TRY(pfm_gemm_skinny_ln(X, rowmap_plain(K), g, b, eps, W, K, M, N, e, st));
+        return PFM_OK;
+    }
+    bf16* xn = nullptr;
+    HIP_TRY(hipMallocAsync((void**)&xn, (size_t)std::max(M, 1) * K * sizeof(bf16), st));
+    hipError_t er = pfm_layernorm(X, rowmap_plain(K), M, K, g, b, eps, nullptr, 0, 1.f, xn, rowmap_plain(K), DT_BF16,
+                                  nullptr, rowmap_plain(0), 0, st);
+    if (er == hipSuccess) er = gemm_dispatch(DT_BF16, xn, rowmap_plain(K), W, K, M, N, K, e, st);
+    (void)hipFreeAsync(xn, st);
+    HIP_TRY(er);
+    return PFM_OK;
+}
+
 }  // extern "C"
 
 // scratch device buffers of one single-op call, freed on every return path
@@ -2178,12 +2233,10 @@ int stream_decoder(pfm_streams* s, const Run& r, int n, int Tw, int L, const SPr
     }
     auto ffn = [&](const float* x, size_t lng, size_t lnb, size_t w1, size_t b1, size_t fng, size_t fnb, size_t w2,
                    float* out, size_t pg, size_t pb, void* pout, int pdt) -> int {
-        HIP_TRY(pfm_layernorm(x, rowmap_plain(D), (int)Ml, D, r.P(lng), r.P(lnb), c.ln_eps, nullptr, 0, 1.f, Xdn,
-                              rowmap_plain(D), dt, nullptr, plain, 0, st));
         GemmEpi e = epi_default();
         e.bias = r.P(b1); e.relu = 1;
         e.out = Hd; e.out_map = rowmap_plain(Fd); e.out_dtype = dt;
-        HIP_TRY(r.gemm(dt, Xdn, rowmap_plain(D), r.W(w1), D, (int)Ml, Fd, D, e));
+        HIP_TRY(r.ln_gemm(x, rowmap_plain(D), lng, lnb, Xdn, rowmap_plain(D), r.W(w1), D, (int)Ml, Fd, D, e));
         if (fast)
             HIP_TRY(pfm_layernorm_bf16in((const bf16*)Hd, rowmap_plain(Fd), (int)Ml, Fd, r.P(fng), r.P(fnb), c.ln_eps,
                                          Hdn, rowmap_plain(Fd), dt, st));
@@ -2205,13 +2258,11 @@ int stream_decoder(pfm_streams* s, const Run& r, int n, int Tw, int L, const SPr
         if (rc) return rc;
         HIP_TRY(pfm_dec_fsmn_stream(dt, Tdn, r.P(Lr.fsmn), K, s->dfs.as<float>() + (size_t)l * s->slots * (K - 1) * D,
                                     prm, ntok, n, L, D, Xd, st));
-        HIP_TRY(pfm_layernorm(Xd, rowmap_plain(D), (int)Ml, D, r.P(Lr.n3g), r.P(Lr.n3b), c.ln_eps, nullptr, 0, 1.f,
-                              Xdn, rowmap_plain(D), dt, nullptr, plain, 0, st));
         {
             GemmEpi e = epi_default();
             e.bias = r.P(Lr.bq);
             e.out = Qd; e.out_map = rowmap_plain(D); e.out_dtype = dt;
-            HIP_TRY(r.gemm(dt, Xdn, rowmap_plain(D), r.W(Lr.wq), D, (int)Ml, D, D, e));
+            HIP_TRY(r.ln_gemm(Xd, rowmap_plain(D), Lr.n3g, Lr.n3b, Xdn, rowmap_plain(D), r.W(Lr.wq), D, (int)Ml, D, D, e));
         }
         const char* kvl = (const char*)s->kvw.p + (size_t)l * 2 * D * es;
         if (s->dlb > 0) {

@@ -25,7 +25,7 @@ MODES = {"exact": MODE_EXACT, "fp32": MODE_EXACT, "fast": MODE_FAST, "bf16": MOD
 # every symbol include/pfm.h declares (checked by tests/test_abi.py)
 ABI_SYMBOLS = ("pfm_config_default", "pfm_config_sensevoice", "pfm_create", "pfm_run_beam", "pfm_set_weight", "pfm_set_weight_device",
                "pfm_missing_weights", "pfm_reserve", "pfm_run", "pfm_run_ctc", "pfm_ctc_align", "pfm_op_ctc_collapse", "pfm_fbank", "pfm_lfr_frames", "pfm_last_error", "pfm_destroy", "pfm_op_gemm",
-               "pfm_op_attention", "pfm_op_layernorm", "pfm_op_fsmn", "pfm_op_cif", "pfm_op_ctc_beam", "pfm_profile", "pfm_op_ffn", "pfm_op_ffn_op", "pfm_op_ffn_op_qkv", "pfm_op_ffn_dec", "pfm_op_fsmn_bf16", "pfm_op_layernorm_bf16",
+               "pfm_op_attention", "pfm_op_layernorm", "pfm_op_ln_gemm", "pfm_op_fsmn", "pfm_op_cif", "pfm_op_ctc_beam", "pfm_profile", "pfm_op_ffn", "pfm_op_ffn_op", "pfm_op_ffn_op_qkv", "pfm_op_ffn_dec", "pfm_op_fsmn_bf16", "pfm_op_layernorm_bf16",
                "pfm_profile_read", "pfm_streams_create", "pfm_streams_reset", "pfm_stream_step", "pfm_stream_step_beam",
                "pfm_streams_destroy", "pfm_fbank_raw", "pfm_lfr_gather", "pfm_config_punc", "pfm_run_punc", "pfm_vad_config_default", "pfm_vad_create",
                "pfm_vad_set_weight", "pfm_vad_missing_weights", "pfm_vad_reset", "pfm_vad_run", "pfm_vad_destroy", "pfm_vad_fbank_raw",
@@ -112,6 +112,7 @@ def load_library(path: Optional[str] = None) -> ctypes.CDLL:
     lib.pfm_profile_read.argtypes = [vp, i32, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
                                      ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64)]
     lib.pfm_op_gemm.argtypes = [vp, i32, vp, vp, f32p, f32p, f32p, i32, i32, i32, i32]
+    lib.pfm_op_ln_gemm.argtypes = [vp, f32p, f32p, f32p, ctypes.c_float, vp, f32p, f32p, vp, i32, i32, i32]
     lib.pfm_op_attention.argtypes = [vp, i32, vp, vp, vp, i32p, f32p, i32, i32, i32, i32, ctypes.c_float]
     lib.pfm_op_layernorm.argtypes = [vp, f32p, f32p, f32p, f32p, i32, i32, ctypes.c_float]
     lib.pfm_op_fsmn.argtypes = [vp, f32p, i32p, f32p, f32p, f32p, i32, i32, i32, i32, i32]
@@ -539,6 +540,21 @@ class PfmStreams:
                                             int(c.blank_id), _ptr(tokens), L_cap, _ptr(ntok), _ptr(scores),
                                             _ptr(nfire)), "pfm_stream_step_beam")
         return dict(tokens=tokens, ntok=ntok, scores=scores, nfire=nfire)
+
+
+def op_ln_gemm(X, g, b, eps, W, bias=None, res=None, relu=False, out_bf16=False):
+    """bf16(LN(X) g + b) . W^T (+ bias, relu, res): X [M, 512] f32, W [N, 512] bf16 (pfm_op_ln_gemm)."""
+    import torch
+    lib = load_library()
+    M, K = X.shape
+    N = W.shape[0]
+    if K != 512 or W.shape[1] != 512 or W.dtype != torch.bfloat16:
+        raise PfmError("op_ln_gemm: X [M, 512] f32 and W [N, 512] bf16 expected")
+    C = torch.empty((M, N), dtype=torch.bfloat16 if out_bf16 else torch.float32, device=X.device)
+    act = (1 if relu else 0) | (2 if out_bf16 else 0)
+    check(lib.pfm_op_ln_gemm(_stream_ptr(torch, X.device), _ptr(X.contiguous()), _ptr(g), _ptr(b), float(eps),
+                             _ptr(W.contiguous()), _ptr(bias), _ptr(res), _ptr(C), M, N, act), "pfm_op_ln_gemm")
+    return C
 
 
 def op_gemm(A, W, bias=None, res=None, relu=False, out_bf16=False):

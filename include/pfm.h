@@ -353,6 +353,13 @@ int pfm_profile_read(pfm_handle* h, int kclass, double* ms, double* flops, doubl
 int pfm_op_gemm(void* stream, int dtype, const void* A, const void* W, const float* bias,
                 const float* res, float* C, int M, int N, int K, int act);
 
+/* C[M,N] = act(bf16(LayerNorm(X) g + b) . W[N,512]^T + bias) (+ res) for f32 rows X [M, 512], W bf16: the fast-mode
+ * LayerNorm -> projection pair of chunk-sized steps (<= 64 rows) in one kernel (LN1 -> QKV, LN2 -> FFN w1, the
+ * decoder's LN -> w1 / q; sanm/encoder.py:114-145, paraformer/decoder.py:95-119); larger M runs the LayerNorm and
+ * the GEMM separately. act as pfm_op_gemm. */
+int pfm_op_ln_gemm(void* stream, const float* X, const float* g, const float* b, float eps, const void* W,
+                   const float* bias, const float* res, float* C, int M, int N, int act);
+
 /* Fused encoder feed-forward sub-layer (fast mode, bf16 MFMA, f32 accumulate / residual / statistics):
  *   x  = x + W2 relu(W1 LayerNorm2(x) + b1) + b2          -> xo [M, 512] f32 (may alias x)
  *   xn = LayerNorm_next(x) as bf16 [M, 512]               (optional: gn, bn, xn all non-null)

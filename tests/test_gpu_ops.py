@@ -108,6 +108,37 @@ def test_gemm_bf16_skinny(dev, M, N, K, epi, monkeypatch):
         assert rel(got, tiled) < 1e-5
 
 
+@pytest.mark.parametrize("M,N", [(1, 1536), (15, 1536), (15, 2048), (16, 512), (33, 2048), (64, 512), (65, 1536),
+                                 (200, 512)])
+@pytest.mark.parametrize("epi", ["bias_bf16", "bias_relu", "bias_res"])
+def test_ln_gemm(dev, M, N, epi):
+    """LayerNorm folded into the skinny GEMM's A load (streaming LN1 -> QKV, LN2 -> w1, decoder LN -> w1 / q;
+    pfm_op_ln_gemm): against fp64 on the kernel's own bf16 rounding of LN(x) (rel-L2 < 1e-5 for f32 outputs, one bf16
+    output rounding otherwise), and equal to the separate LayerNorm + GEMM of the unfused path (M > 64 takes that path
+    itself) up to the f32 summation order."""
+    g = torch.Generator().manual_seed(7 * M + N)
+    X = torch.randn(M, 512, generator=g) * 3 + 0.5
+    gm, bt = 1 + 0.1 * torch.randn(512, generator=g), 0.1 * torch.randn(512, generator=g)
+    W = (torch.randn(N, 512, generator=g) / 512 ** 0.5).bfloat16()
+    b = torch.randn(N, generator=g)
+    R = torch.randn(M, N, generator=g) if epi == "bias_res" else None
+    ln = _ln64(X.double(), gm, bt, 1e-12).float().bfloat16()   # the kernel's bf16 A operand (f64 statistics)
+    want = ln.double() @ W.double().T + b.double()
+    if epi == "bias_relu":
+        want = torch.relu(want)
+    if R is not None:
+        want = want + R.double()
+    kw = dict(relu=epi == "bias_relu", out_bf16=epi == "bias_bf16")
+    got = rt.op_ln_gemm(X.to(dev), gm.to(dev), bt.to(dev), 1e-12, W.to(dev), b.to(dev),
+                        None if R is None else R.to(dev), **kw)
+    sep = rt.op_gemm(rt.op_layernorm(X.to(dev), gm.to(dev), bt.to(dev), 1e-12).bfloat16(), W.to(dev), b.to(dev),
+                     None if R is None else R.to(dev), **kw)
+    torch.cuda.synchronize()
+    tol = 4e-3 if epi == "bias_bf16" else 1e-5
+    assert rel(got, want) < tol
+    assert rel(got, sep) < (1e-2 if epi == "bias_bf16" else 1e-5)
+
+
 def test_gemm_identity_asymmetric(dev):
     """A = I with an asymmetric W catches a transposed C write."""
     K = 256
