@@ -115,7 +115,7 @@ def test_ln_gemm(dev, M, N, epi):
     """LayerNorm folded into the skinny GEMM's A load (streaming LN1 -> QKV, LN2 -> w1, decoder LN -> w1 / q;
     pfm_op_ln_gemm): against fp64 on the kernel's own bf16 rounding of LN(x) (rel-L2 < 1e-5 for f32 outputs, one bf16
     output rounding otherwise), and equal to the separate LayerNorm + GEMM of the unfused path (M > 64 takes that path
-    itself) up to the f32 summation order."""
+    itself) up to bf16 operand rounding flips."""
     g = torch.Generator().manual_seed(7 * M + N)
     X = torch.randn(M, 512, generator=g) * 3 + 0.5
     gm, bt = 1 + 0.1 * torch.randn(512, generator=g), 0.1 * torch.randn(512, generator=g)
@@ -136,7 +136,9 @@ def test_ln_gemm(dev, M, N, epi):
     torch.cuda.synchronize()
     tol = 4e-3 if epi == "bias_bf16" else 1e-5
     assert rel(got, want) < tol
-    assert rel(got, sep) < (1e-2 if epi == "bias_bf16" else 1e-5)
+    # the two paths round LN(x) to bf16 from f32 values formed in a different operation order: a last-bit
+    # difference flips an operand element's bf16 rounding now and then (3e-5 measured at M = 64, N = 512)
+    assert rel(got, sep) < (1e-2 if epi == "bias_bf16" else 2e-4)
 
 
 def test_gemm_identity_asymmetric(dev):
