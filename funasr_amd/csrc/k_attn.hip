@@ -53,6 +53,18 @@ constexpr int LDS16 = 2 * (KT * KP16 + DK * VTP16);
 
 __device__ __forceinline__ int kappa(int e) { return (e & 3) + 8 * (e >> 2); }
 
+// x combined with lane ^ 32's x by one v_permlane32_swap (the swap of x with itself leaves {own, partner} in every lane,
+// in an order that depends on the half; max and + are commutative, so the result equals op(x, __shfl_xor(x, 32)) bit
+// for bit — without the ds_bpermute round trip through the LDS pipe)
+__device__ __forceinline__ float xor32_max(float x) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float xor32_add(float x) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
 template <typename T> struct AttnLds;
 
 __global__ __launch_bounds__(256) void attn_f32_kernel(AttnArgs a) {
@@ -130,7 +142,7 @@ __global__ __launch_bounds__(256) void attn_f32_kernel(AttnArgs a) {
             if (key >= klen) s[e] = -INFINITY;
             mt = fmaxf(mt, s[e]);
         }
-        mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+        mt = xor32_max(mt);
         const float mnew = fmaxf(mrun, mt);
         const float corr = expf(mrun - mnew);
         float ls = 0.f;
@@ -139,7 +151,7 @@ __global__ __launch_bounds__(256) void attn_f32_kernel(AttnArgs a) {
             s[e] = expf(s[e] - mnew);
             ls += s[e];
         }
-        ls += __shfl_xor(ls, 32, 64);
+        ls = xor32_add(ls);
         lrun = lrun * corr + ls;
         mrun = mnew;
 #pragma unroll
@@ -397,7 +409,7 @@ __global__ __launch_bounds__(512) void attn_x6_kernel(AttnArgs a) {
             if (key >= klen) s[e] = -INFINITY;
             mt = fmaxf(mt, s[e]);
         }
-        mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+        mt = xor32_max(mt);
         const float mnew = fmaxf(mrun, mt);
         const float corr = expf(mrun - mnew);
         float ls = 0.f;
@@ -406,7 +418,7 @@ __global__ __launch_bounds__(512) void attn_x6_kernel(AttnArgs a) {
             s[e] = expf(s[e] - mnew);
             ls += s[e];
         }
-        ls += __shfl_xor(ls, 32, 64);
+        ls = xor32_add(ls);
         lrun = lrun * corr + ls;
         mrun = mnew;
 #pragma unroll
@@ -695,7 +707,7 @@ __global__ __launch_bounds__(NWV * 64, 8 / NWV) void attn_bf16_kernel(AttnArgs a
         for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
             for (int e = 0; e < 16; ++e) mt = fmaxf(mt, s[kb][e]);
-        mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+        mt = xor32_max(mt);
         if (mt > mused + RESCALE_THR * 1.4426950408889634f) {   // lazy rescale (log2 units; rare after tile 0)
             const float corr = __builtin_amdgcn_exp2f(mused - mt);
             lrun *= corr;
@@ -713,7 +725,7 @@ __global__ __launch_bounds__(NWV * 64, 8 / NWV) void attn_bf16_kernel(AttnArgs a
                 s[kb][e] = __builtin_amdgcn_exp2f(s[kb][e] - mused);
                 ls += s[kb][e];
             }
-        ls += __shfl_xor(ls, 32, 64);
+        ls = xor32_add(ls);
         lrun += ls;
         } else {
             lrun = 1.f;

@@ -41,9 +41,11 @@ __device__ unsigned long long beam_prof[1024][8];
 #endif
 
 // log1p(u) for u in [0, 1) (u = exp(-|a - b|) of logaddexp): 2 atanh(s), s = u / (2 + u) in [0, 1/3), as a series
-// in f64 (terms to s^17: truncation < 2^-34 relative; 1 / (2 + u) by v_rcp_f64 + two Newton steps) rounded once to
-// f32 — the correctly rounded value in all but rare halfway cases (the C library's log1pf is within 1 ulp of it),
-// at about a tenth of the f32 library routine's instructions
+// in f64 (terms to s^17: truncation < 2^-34 relative; 1 / (2 + u) by v_rcp_f64 (2^-23) + one Newton step (2^-46))
+// rounded once to f32 — the correctly rounded value in all but rare near-halfway cases (the C library's log1pf is
+// within 1 ulp of it), at about a tenth of the f32 library routine's instructions. The series in z = s^2 is evaluated
+// in Estrin form (four dependent FMA levels instead of Horner's eight: logaddexp is the step of every sequential
+// recurrence of the search, so its dependency depth is the search's clock)
 // a * b + c as one VOP3 v_fma_f64 (the compiler's two-address v_fmac_f64 form copies the loop-invariant addend into
 // the destination first: one v_mov_b64 per Horner step)
 __device__ __forceinline__ double fma64(double a, double b, double c) {
@@ -56,17 +58,11 @@ __device__ __forceinline__ float log1p_unit(float u) {
     const double x = (double)u, d = 2.0 + x;
     double r = __builtin_amdgcn_rcp(d);
     r = fma(fma(-d, r, 1.0), r, r);
-    r = fma(fma(-d, r, 1.0), r, r);
-    const double sd = x * r, z = sd * sd;
-    double p = 1.0 / 17.0;
-    p = fma64(p, z, 1.0 / 15.0);
-    p = fma64(p, z, 1.0 / 13.0);
-    p = fma64(p, z, 1.0 / 11.0);
-    p = fma64(p, z, 1.0 / 9.0);
-    p = fma64(p, z, 1.0 / 7.0);
-    p = fma64(p, z, 1.0 / 5.0);
-    p = fma64(p, z, 1.0 / 3.0);
-    p = fma64(p, z, 1.0);
+    const double sd = x * r, z = sd * sd, z2 = z * z, z4 = z2 * z2, z8 = z4 * z4;
+    const double q0 = fma64(z, 1.0 / 3.0, 1.0), q1 = fma64(z, 1.0 / 7.0, 1.0 / 5.0);
+    const double q2 = fma64(z, 1.0 / 11.0, 1.0 / 9.0), q3 = fma64(z, 1.0 / 15.0, 1.0 / 13.0);
+    const double h0 = fma64(q1, z2, q0), h1 = fma64(q3, z2, q2);
+    const double p = fma64(1.0 / 17.0, z8, fma64(h1, z4, h0));
     return (float)(2.0 * sd * p);
 }
 
@@ -175,7 +171,8 @@ __global__ __launch_bounds__(NT) void ctc_beam_kernel(BeamArgs a) {
     const int kk = min(K, P), KP = K * P;
     // scratch (floats): xt [V][T] (the utterance's CTC log-probs, frame-contiguous per id: a candidate's column over the
     // frames is one contiguous row) | Rb [2][T][K*P] float2 | xch [2][2][K*P] (the columns' weighted scores and psi,
-    // per position parity) | per workgroup: Rs [K][T], bylen [S + 1]
+    // per position parity) | Rsum [2][T][K*P] (r_sum = logaddexp(r^n, r^b) of every column, written by the r^b chains
+    // as they go: a running hypothesis's r_sum at the next position is its column there) | per workgroup: bylen [S + 1]
     // The CTC states (r^n, r^b) of position i's candidates are column k*P + j of buffer i & 1 (frame-major: one
     // recurrence step's stores are contiguous across lanes); a running hypothesis is the column it was created in,
     // read from the other buffer at the next position, so nothing is copied between positions.
@@ -183,8 +180,8 @@ __global__ __launch_bounds__(NT) void ctc_beam_kernel(BeamArgs a) {
     const float* xb = xt + (long long)a.blank * a.T;   // the blank's row
     float2* Rb = (float2*)(a.fs + b * a.fstride + pfm_align2((long long)V * a.T));
     float* xch = (float*)(Rb + 2LL * a.T * KP);
-    float* Rs = xch + 4LL * KP + (long long)grp * ((long long)K * a.T + S + 1);
-    float* bylen = Rs + (long long)K * a.T;
+    float* Rsum = xch + 4LL * KP;
+    float* bylen = Rsum + 2LL * a.T * KP + (long long)grp * (S + 1);
     // (ints): bpar [L][K] parent slot, btok [L][K] token of the hypothesis in beam slot k after position i (written
     // by workgroup 0) | raw [S] (n-best output staging) | per workgroup: has_len [S + 1] (ended lengths reach S)
     unsigned* sync = (unsigned*)(a.is + b * a.istride);   // [0]: arrivals of the per-position barrier, [1]: timeout
@@ -227,11 +224,18 @@ __global__ __launch_bounds__(NT) void ctc_beam_kernel(BeamArgs a) {
         }
     }
     __syncthreads();
+    {   // ... and its r_sum (column 0 of Rsum buffer 1)
+        const float2* r0 = Rb + (long long)a.T * KP;
+        float* s0 = Rsum + (long long)a.T * KP;
+        for (int t = tid; t < Tb; t += NT) s0[(long long)t * KP] = lae(LOGZERO, r0[(long long)t * KP].y, l1p);
+    }
 
     for (int i = 0; i < maxlen && !stop; ++i) {
         const int nr = nrun;
         const float2* Rprev = Rb + (long long)((i + 1) & 1) * a.T * KP;
         float2* Rcur = Rb + (long long)(i & 1) * a.T * KP;
+        const float* RsPrev = Rsum + (long long)((i + 1) & 1) * a.T * KP;
+        float* RsCur = Rsum + (long long)(i & 1) * a.T * KP;
         // ---- pre-beam: the top P of ws0 (value desc, id asc) of this position, selected beforehand for every position
         // by prebeam_kernel (it depends on the decoder log-probs only)
         if (tid < P) {
@@ -241,21 +245,8 @@ __global__ __launch_bounds__(NT) void ctc_beam_kernel(BeamArgs a) {
         }
         __syncthreads();
         BPROF_MARK(0);
-        // ---- r_sum of every running hypothesis (logaddexp(r^n, r^b), the log_phi of a non-repeated label)
-        {
-            const int nb8 = (Tb + 7) >> 3;   // 8 consecutive frames of one hypothesis per item: the loads go together
-            for (int e = tid; e < nr * nb8; e += NT) {
-                const int k = e / nb8, t0 = (e - k * nb8) * 8;
-                const float2* rp = Rprev + hcol[k];
-                float2 q[8];
-#pragma unroll
-                for (int u = 0; u < 8; ++u) q[u] = rp[(long long)min(t0 + u, Tb - 1) * KP];
-#pragma unroll
-                for (int u = 0; u < 8; ++u)
-                    if (t0 + u < Tb) Rs[(long long)k * a.T + t0 + u] = lae(q[u].x, q[u].y, l1p);
-            }
-        }
-        __syncthreads();
+        // (the r_sum of every running hypothesis — logaddexp(r^n, r^b), the log_phi of a non-repeated label — is its
+        // column of RsPrev: the r^b chains wrote it at the previous position)
         BPROF_MARK(1);
         // ---- CTC prefix scores (CTCPrefixScore.__call__): this workgroup's chains of the columns c = kP + j < nr P
         const int ncol = nr * P;
@@ -270,12 +261,16 @@ __global__ __launch_bounds__(NT) void ctc_beam_kernel(BeamArgs a) {
             const int ol = hlen[0] - 1;
             const bool phi_b = ol > 0 && c == hlast[k]; // log_phi = r^b(g) for a repeated label
             const float2* rp = Rprev + hcol[k];         // frame t at rp[t * KP]
-            const float* rsum = Rs + (long long)k * a.T;
+            const float* rsum = RsPrev + hcol[k];       // frame t at rsum[t KP]
             float* rn = (float*)(Rcur + col) + half;    // this chain's component of frame t at rn[2 t KP]
+            float* rsc = RsCur + col;                   // r_sum of this column (r^b lanes)
             const int start = max(ol, 1);
             // r[start - 1] = (xs[0], logzero) at ol == 0, else (logzero, logzero)
             const float init0 = (ol == 0 && Tb > 0) ? xc[0] : LOGZERO;
-            if (act && start - 1 < Tb) rn[2LL * (start - 1) * KP] = half == 0 ? init0 : LOGZERO;
+            if (act && start - 1 < Tb) {
+                rn[2LL * (start - 1) * KP] = half == 0 ? init0 : LOGZERO;
+                if (half) rsc[(long long)(start - 1) * KP] = lae(init0, LOGZERO, l1p);
+            }
             const int nblk = Tb > start ? (Tb - start + BL - 1) / BL : 0;
             float r = half == 0 ? init0 : LOGZERO;
             float prev0 = init0;                         // r^b lanes: r^n of the frame before the block
@@ -288,7 +283,7 @@ __global__ __launch_bounds__(NT) void ctc_beam_kernel(BeamArgs a) {
                 for (int u = 0; u < BL; ++u) {
                     const int t = min(t0 + u, Tb - 1);
                     if (half == 0) {
-                        pa[u] = phi_b ? rp[(long long)(t - 1) * KP].y : rsum[t - 1];
+                        pa[u] = phi_b ? rp[(long long)(t - 1) * KP].y : rsum[(long long)(t - 1) * KP];
                         pb[u] = xc[t];
                     } else {
                         pb[u] = xb[t];
@@ -335,6 +330,8 @@ __global__ __launch_bounds__(NT) void ctc_beam_kernel(BeamArgs a) {
                                     r = lae(prev0, r, l1p) + cb[u0 + u];
                                     pr[(u0 + u) * stp] = r;
                                     prev0 = rq[u];
+                                    // off the chain: r_sum of frame t = logaddexp(r^n_t, r^b_t)
+                                    rsc[(long long)(t0 + u0 + u) * KP] = lae(prev0, r, l1p);
                                 }
                             } else {
 #pragma unroll
@@ -342,6 +339,7 @@ __global__ __launch_bounds__(NT) void ctc_beam_kernel(BeamArgs a) {
                                     if (t0 + u0 + u < Tb) {
                                         r = lae(prev0, r, l1p) + cb[u0 + u];
                                         pr[(u0 + u) * stp] = r;
+                                        rsc[(long long)(t0 + u0 + u) * KP] = lae(rq[u], r, l1p);
                                     }
                                     prev0 = rq[u];
                                 }
@@ -364,7 +362,7 @@ __global__ __launch_bounds__(NT) void ctc_beam_kernel(BeamArgs a) {
                 const int ol = hlen[0] - 1;
                 const bool phi_b = ol > 0 && c == hlast[k];
                 const float2* rp = Rprev + hcol[k];
-                const float* rsum = Rs + (long long)k * a.T;
+                const float* rsum = RsPrev + hcol[k];
                 const int start = max(ol, 1);
                 float lpsi = (ol == 0 && Tb > 0) ? xc[0] : LOGZERO;   // r[start - 1, 0]
                 // phi + x of 16 frames per batch, the next batch's loads in flight while one computes
@@ -374,7 +372,7 @@ __global__ __launch_bounds__(NT) void ctc_beam_kernel(BeamArgs a) {
 #pragma unroll
                     for (int u = 0; u < PB; ++u) {
                         const int t = min(t0 + u, Tb - 1);
-                        d[u] = (phi_b ? rp[(long long)(t - 1) * KP].y : rsum[t - 1]) + xc[t];
+                        d[u] = (phi_b ? rp[(long long)(t - 1) * KP].y : rsum[(long long)(t - 1) * KP]) + xc[t];
                     }
                 };
                 if (start < Tb) load_b(start, cs16);
@@ -389,7 +387,11 @@ __global__ __launch_bounds__(NT) void ctc_beam_kernel(BeamArgs a) {
                         for (int u = 0; u < PB; ++u) cs16[u] = nx[u];
                     }
                 }
-                if (c == a.eos) lpsi = Tb > 0 ? rsum[Tb - 1] : LOGZERO;   // r_sum[-1]
+                // r_sum[-1]; frames below the previous position's start were never computed (the reference's
+                // fresh logzero state there: logaddexp(logzero, logzero) = logzero in f32)
+                if (c == a.eos)
+                    lpsi = Tb > 0 ? (Tb - 1 >= max(ol - 2, 0) ? rsum[(long long)(Tb - 1) * KP] : lae(LOGZERO, LOGZERO, l1p))
+                                  : LOGZERO;
                 if (c == a.blank) lpsi = LOGZERO;
                 const float ts = lpsi - hprev[k];
                 float* xo = xch + (long long)(i & 1) * 2 * KP;
@@ -668,7 +670,7 @@ static int groups(int K, int P) { return pair_wgs(K, P) + (K * P + 255) / 256; }
 long long pfm_ctc_beam_fscratch(int K, int P, int T, int L, int V) {
     const long long KP = (long long)K * P, S = L + 2;
     return pfm_align2((long long)V * T) +
-           pfm_align2(4LL * T * KP + 4 * KP + groups(K, P) * ((long long)K * T + S + 1) + (long long)L * P);
+           pfm_align2(4LL * T * KP + 4 * KP + 2LL * T * KP + groups(K, P) * (S + 1) + (long long)L * P);
 }
 long long pfm_ctc_beam_iscratch(int K, int nbest, int L, int P, int V) {
     const long long S = L + 2;
