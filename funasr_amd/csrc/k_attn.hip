@@ -20,6 +20,7 @@
 #include <stdint.h>
 
 #include "pfm_common.h"
+#include "pfm_stream.h"
 
 namespace {
 
@@ -40,6 +41,14 @@ struct AttnArgs {
     // mask * (sum_k fw[k][h*DK + c] * vm[t - 5 + k] + vm[t]), vm = V rows masked by klen (K = 11, left 5)
     const float* fw; bf16* fout; long long fld; int fD;
     float* fout32 = nullptr;      // EXACT mode (x6 kernel): the same FSMN block in f32 (fout's row stride fld)
+    // optional streaming cache retain, fused (bf16 kernels; kv_retain_kernel of k_stream.hip): after the key loop the
+    // blocks of query tile 0 copy head h's K and V columns of stream b's new cache rows — the last min(C, cl + tw -
+    // drop) key rows — into the slot's cache rows (rt_W elements, V at rt_voff). The key rows are the gathered
+    // [cache ; window] buffer, the cache a different array, so no block reads what another writes.
+    const SPrm* rt_prm = nullptr;
+    bf16* rt_cache = nullptr;
+    int rt_C = 0, rt_drop = 0, rt_dec = 0, rt_W = 0, rt_voff = 0;
+    const int* rt_ntok = nullptr;   // decoder caches move only for streams whose decoder ran
 };
 
 // ---- f32 tile geometry (bytes)
@@ -825,6 +834,18 @@ __global__ __launch_bounds__(NWV * 64, 8 / NWV) void attn_bf16_kernel(AttnArgs a
     if constexpr (NWV == 8) {
         if (a.fout) fsmn_epilogue<QBLK, NT>(a, fxs, qt, h, b, klen);
     }
+    if (a.rt_cache && qt == 0 && !(a.rt_dec && a.rt_ntok[b] < 1)) {
+        const SPrm p = a.rt_prm[b];
+        const int len0 = (a.rt_dec ? p.cld : p.cle) + p.tw - a.rt_drop;
+        const int ncl = min(a.rt_C, len0);
+        for (int e = tid; e < ncl * 32; e += NT) {   // 16 16-B chunks of K and 16 of V per row (128 head dims)
+            const int j = e >> 5, c = e & 31;
+            const unsigned row = (unsigned)(len0 - ncl + j), cb = (unsigned)(c & 15) * 16u;
+            const uint4 val = c < 16 ? *(const uint4*)(kbase + (row * krb + cb)) : *(const uint4*)(vbase + (row * vrb + cb));
+            *(uint4*)((char*)a.rt_cache +
+                      (((long long)p.slot * a.rt_C + j) * a.rt_W + (c < 16 ? 0 : a.rt_voff) + h * DK) * 2 + cb) = val;
+        }
+    }
 }
 
 }  // namespace
@@ -915,6 +936,42 @@ hipError_t pfm_attention_x3(const float* q, RowMap qmap, const float* k, RowMap 
     }
     dim3 grid((Tq + 255) / 256, heads, B), block(512);
     hipLaunchKernelGGL(attn_x6_kernel<0>, grid, block, X6_LDS, st, a);
+    PFM_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+// bf16 attention over a streaming step's gathered keys with the cache retain fused (AttnArgs rt_*): the key buffer is
+// [n][Tk][2 heads 128] (K | V), the cache [slots][C][2 heads 128]. hipErrorNotSupported (nothing launched) for shapes
+// the bf16 kernels do not take: the caller then runs the attention and kv_retain_kernel separately.
+hipError_t pfm_attention_retain(const void* q, RowMap qmap, const void* kv, int B, int Tq, int Tk, void* o2, long long ldo,
+                                const int* klen, int heads, int dk, float scale, const SPrm* prm, void* cache, int C,
+                                int drop, int dec, const int* ntok, hipStream_t st) {
+    if (B <= 0 || Tq <= 0) return hipSuccess;
+    const int D = heads * DK;
+    if (dk != DK || !o2 || (dec && !ntok) || ((uintptr_t)kv % 16) || ((uintptr_t)cache % 16) ||
+        (long long)Tk * 2 * D * 2 >= (1ll << 31))
+        return hipErrorNotSupported;
+    AttnArgs a;
+    const RowMap km = rowmap_seg(Tk, (long long)Tk * 2 * D, 2 * D);
+    a.q = q; a.qmap = qmap; a.k = kv; a.kmap = km; a.v = (const bf16*)kv + D; a.vmap = km;
+    a.o = nullptr; a.ldo = ldo; a.o2 = o2; a.o2_dtype = DT_BF16; a.klen = klen; a.Tq = Tq; a.Tk = Tk; a.scale = scale;
+    a.fw = nullptr; a.fout = nullptr; a.fld = 0; a.fD = D;
+    a.rt_prm = prm; a.rt_cache = (bf16*)cache; a.rt_C = C; a.rt_drop = drop; a.rt_dec = dec; a.rt_W = 2 * D;
+    a.rt_voff = D; a.rt_ntok = ntok;
+    static bool attr_done = false;
+    if (!attr_done) {
+        attr_done = true;
+        (void)hipFuncSetAttribute((const void*)attn_bf16_kernel<4>, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * STG2);
+        (void)hipFuncSetAttribute((const void*)attn_bf16_kernel<8>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  LDS8_FS);
+    }
+    if (pfm_knobs().attn_waves == 8) {
+        dim3 grid((Tq + 255) / 256, heads, B), block(512);
+        hipLaunchKernelGGL((attn_bf16_kernel<8>), grid, block, 2 * STG2, st, a);
+    } else {
+        dim3 grid((Tq + 127) / 128, heads, B), block(256);
+        hipLaunchKernelGGL(attn_bf16_kernel<4>, grid, block, 2 * STG2, st, a);
+    }
     PFM_LAUNCH_CHECK();
     return hipSuccess;
 }

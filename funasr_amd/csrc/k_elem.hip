@@ -4,6 +4,7 @@
 #include <stdlib.h>
 
 #include "pfm_common.h"
+#include "pfm_stream.h"
 
 namespace {
 
@@ -246,15 +247,14 @@ template <> __device__ __forceinline__ float4 load4<bf16>(const bf16* p) {
 }
 
 template <int KK, typename TIN, int LEFT = -1>   // LEFT >= 0: compile-time offset (static window index)
-__global__ __launch_bounds__(256) void fsmn_win_kernel(const TIN* __restrict__ v, RowMap vmap,
-                                                       const int* __restrict__ len, int B, int T, int D,
-                                                       const float* __restrict__ wT, int left_rt,
-                                                       const float* __restrict__ res, float* __restrict__ out,
-                                                       bf16* __restrict__ out_bf) {
+__device__ __forceinline__ void fsmn_win_body(long long gid, const TIN* __restrict__ v, RowMap vmap,
+                                              const int* __restrict__ len, int B, int T, int D,
+                                              const float* __restrict__ wT, int left_rt,
+                                              const float* __restrict__ res, float* __restrict__ out,
+                                              bf16* __restrict__ out_bf) {
     const int left = LEFT >= 0 ? LEFT : left_rt;
     const int qpr = D / 4;
     const int nblk = (T + FR - 1) / FR;
-    const long long gid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (gid >= (long long)B * nblk * qpr) return;
     const int c = (int)(gid % qpr) * 4;
     const long long rb = gid / qpr;
@@ -315,6 +315,32 @@ __global__ __launch_bounds__(256) void fsmn_win_kernel(const TIN* __restrict__ v
             *(bf16x4*)(out_bf + row * D + c) = tb;
         }
     }
+}
+template <int KK, typename TIN, int LEFT = -1>
+__global__ __launch_bounds__(256) void fsmn_win_kernel(const TIN* __restrict__ v, RowMap vmap,
+                                                       const int* __restrict__ len, int B, int T, int D,
+                                                       const float* __restrict__ wT, int left_rt,
+                                                       const float* __restrict__ res, float* __restrict__ out,
+                                                       bf16* __restrict__ out_bf) {
+    fsmn_win_body<KK, TIN, LEFT>((long long)blockIdx.x * blockDim.x + threadIdx.x, v, vmap, len, B, T, D, wT, left_rt,
+                                 res, out, out_bf);
+}
+
+// streaming encoder layer: blocks [0, nf) run the window's FSMN (fsmn_win_kernel<11, bf16, 5>, lens = tw), blocks
+// nf + (i Tk + r) gather key row r of stream i (kv_gather_row): two independent launches of the chunk step as one
+__global__ __launch_bounds__(256) void kv_gather_fsmn_kernel(int nf, const bf16* __restrict__ cache, int C,
+                                                             const SPrm* __restrict__ prm, const bf16* __restrict__ src,
+                                                             long long src_ld, int Tw, bf16* __restrict__ buf, int Tk,
+                                                             int W, const bf16* __restrict__ v, RowMap vmap,
+                                                             const int* __restrict__ len, int B, int D,
+                                                             const float* __restrict__ wT, bf16* __restrict__ out_bf) {
+    if ((int)blockIdx.x < nf) {
+        fsmn_win_body<11, bf16, 5>((long long)blockIdx.x * blockDim.x + threadIdx.x, v, vmap, len, B, Tw, D, wT, 5,
+                                   nullptr, nullptr, out_bf);
+        return;
+    }
+    const int g = (int)blockIdx.x - nf, i = g / Tk, r = g - i * Tk;
+    kv_gather_row(cache, C, prm[i], 0, src, src_ld, Tw, buf, Tk, W, i, r, (int)threadIdx.x, 256);
 }
 
 // fsmn_win_kernel<11, TIN, 5> with the following LayerNorm fused (D = 512: a 256-thread block is two
@@ -763,6 +789,22 @@ hipError_t pfm_fsmn_bf16in(const bf16* v, RowMap vmap, const int* len, int B, in
     else
         hipLaunchKernelGGL((fsmn_win_kernel<11, bf16>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, v, vmap,
                            len, B, T, D, wT, left, res, out, out_bf);
+    PFM_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+hipError_t pfm_kv_gather_fsmn(const bf16* cache, int C, const SPrm* prm, int n, const bf16* src, long long src_ld, int Tw,
+                              bf16* buf, int Tk, int W, const bf16* v, RowMap vmap, const int* len, int D, const float* wT,
+                              bf16* out_bf, hipStream_t st) {
+    if (n <= 0 || Tk <= 0 || Tw <= 0) return hipSuccess;
+    if (D % 4 || (W * 2) % 16 || (src_ld * 2) % 16 || ((uintptr_t)src % 16) || ((uintptr_t)buf % 16) ||
+        ((uintptr_t)cache % 16) || (vmap.rows_per_seg > 0 && vmap.rows_per_seg != Tw))
+        return hipErrorInvalidValue;
+    const long long nfl = ((long long)n * ((Tw + FR - 1) / FR) * (D / 4) + 255) / 256;
+    const long long ng = (long long)n * Tk;
+    if (nfl + ng >= (1LL << 31)) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(kv_gather_fsmn_kernel, dim3((unsigned)(nfl + ng)), dim3(256), 0, st, (int)nfl, cache, C, prm, src,
+                       src_ld, Tw, buf, Tk, W, v, vmap, len, n, D, wT, out_bf);
     PFM_LAUNCH_CHECK();
     return hipSuccess;
 }

@@ -50,7 +50,10 @@ constexpr int GW = TF / NW;              // LDS-DMA pieces (1 KiB) per wave per 
 constexpr int RING = RS * TF * 1024;     // 128 KiB
 constexpr int OPF = 16 * 32;             // phase-0 fragments: Wo = 16 output blocks x 32 k steps
 constexpr int CHF = 64;                  // fragments per hidden chunk: 32 W1 k steps + 16 x 2 W2
-constexpr int PD = 6;                    // fragment reads in flight ahead of their MFMA
+#ifndef FFN2_PD
+#define FFN2_PD 6
+#endif
+constexpr int PD = FFN2_PD;              // fragment reads in flight ahead of their MFMA
 #ifndef FFN2_OPI
 #define FFN2_OPI 4
 #endif
@@ -415,7 +418,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     // that barrier freed, read fragment f+PD, wait for fragment f (then its MFMA)
     // (past the stream's end the read-ahead keeps going: in-bounds reads of stale ring slots nobody consumes,
     // so every step has the same wait)
-    static_assert(TF == 16 && PD == 6, "publish / DMA spread positions");
+    // (the publishing position TF - PD must differ from the piece positions 14, 2 and 6)
+    static_assert(TF == 16 && (PD == 5 || PD == 6 || PD == 7), "publish / DMA spread positions");
     auto step_pre = [&](int f, int fs) __attribute__((always_inline)) {
         __builtin_amdgcn_sched_barrier(0);
         const int ps = fs % TF;
@@ -499,7 +503,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     auto acc1_ready = [&]() __attribute__((always_inline)) {
         __builtin_amdgcn_sched_barrier(0);
         asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" : "+v"(acc1a), "+v"(acc1b));
-        asm volatile("s_waitcnt lgkmcnt(6)" : "+v"(bq[0]), "+v"(bq[1]), "+v"(bq[2]), "+v"(bq[3]));
+        asm volatile("s_waitcnt lgkmcnt(%4)" : "+v"(bq[0]), "+v"(bq[1]), "+v"(bq[2]), "+v"(bq[3]) : "i"(PD));
         __builtin_amdgcn_sched_barrier(0);
     };
     // relu((H_a + H_b) + b1) -> bf16 for register group q (4 features) into hb

@@ -49,24 +49,13 @@ __global__ __launch_bounds__(256) void stream_fcache_kernel(const float* __restr
     for (int c = threadIdx.x; c < I / 4; c += 256) dst[c] = src[c];
 }
 
-// ------------------------------------------------------------------------------------------
-// Attention keys of one layer = [K/V cache (cl rows) ; the window's K|V rows (tw rows)]
-// (sanm/attention.py:327-334 encoder, 733-737 decoder). buf: [n][Tk][W], W = 2d (K | V).
-// One block per (stream, key row); 16-B copies.
-// ------------------------------------------------------------------------------------------
+// Attention keys of one layer (kv_gather_row, pfm_stream.h): one block per (stream, key row)
 template <typename T>
 __global__ __launch_bounds__(128) void kv_gather_kernel(const T* __restrict__ cache, int C, const SPrm* __restrict__ prm,
                                                         int dec, const T* __restrict__ src, long long src_ld, int Tw,
                                                         T* __restrict__ buf, int Tk, int W) {
     const int i = blockIdx.y, r = blockIdx.x;
-    const SPrm p = prm[i];
-    const int cl = dec ? p.cld : p.cle;
-    constexpr int V = 16 / sizeof(T);
-    uint4* dst = (uint4*)(buf + ((long long)i * Tk + r) * W);
-    const uint4* s = nullptr;
-    if (r < cl) s = (const uint4*)(cache + ((long long)p.slot * C + r) * W);
-    else if (r < cl + p.tw) s = (const uint4*)(src + ((long long)i * Tw + (r - cl)) * src_ld);
-    for (int c = threadIdx.x; c < W / V; c += 128) dst[c] = s ? s[c] : make_uint4(0, 0, 0, 0);
+    kv_gather_row(cache, C, prm[i], dec, src, src_ld, Tw, buf, Tk, W, i, r, (int)threadIdx.x, 128);
 }
 
 // New cache = the last min(C, cl + tw - drop) rows of buf[i][0 .. cl + tw - drop): drop = chunk_size[2]

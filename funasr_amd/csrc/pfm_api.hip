@@ -62,6 +62,9 @@ hipError_t pfm_f32_to_bf16(const float* x, bf16* y, long long n, hipStream_t st)
 hipError_t pfm_swap_last2(const float* x, float* y, long long A, long long Bd, long long C, hipStream_t st);
 hipError_t pfm_logsoftmax_rows(float* x, long long rows, long long ld, int V, hipStream_t st);
 long long pfm_ctc_beam_fscratch(int K, int P, int T, int L, int V);
+hipError_t pfm_attention_retain(const void* q, RowMap qmap, const void* kv, int B, int Tq, int Tk, void* o2, long long ldo,
+                                const int* klen, int heads, int dk, float scale, const SPrm* prm, void* cache, int C,
+                                int drop, int dec, const int* ntok, hipStream_t st);
 long long pfm_ctc_beam_iscratch(int K, int nbest, int L, int P, int V);
 hipError_t pfm_ctc_beam(const float* am, int L, const float* x, int T, const int* lens, const int* ntok, int B, int V,
                         int K, int P, int nbest, float wctc, float pen, int use_pen, int end_detect, int sos, int eos,
@@ -839,6 +842,18 @@ struct Run {
         return pfm_attention_x3(q, qm, k, km, v, vm, out3, kl, Bb, Tq, Tk, c.heads, (int)dk, qscale, fsmn_wT,
                                 fsmn_out, c.d_model, st);
     }
+    // fast-mode streaming attention over the gathered [cache ; window] keys with the cache retain fused
+    // (pfm_attention_retain); hipErrorNotSupported: nothing ran, the caller takes the separate launches
+    hipError_t attn_rt(const bf16* q, RowMap qm, void* kv, bf16* o2, const int* kl, int Bb, int Tq, int Tk,
+                       const SPrm* prm, void* cache, int C, int drop, int dec, const int* ntok) const {
+        const pfm_config& c = h->cfg;
+        const double dk = c.d_model / c.heads;
+        const double fl = 4.0 * Bb * Tq * (double)Tk * dk * c.heads;
+        const double by = ((double)Bb * Tq + 2.0 * Bb * Tk) * c.d_model * 2.0 + (double)Bb * Tq * c.d_model * 2.0;
+        ProfScope ps(h, st, PFM_K_ATTN, fl, by);
+        return pfm_attention_retain(q, qm, kv, Bb, Tq, Tk, o2, c.d_model, kl, c.heads, (int)dk,
+                                    qscale, prm, cache, C, drop, dec, ntok, st);
+    }
     hipError_t attn(int dtp, const void* q, RowMap qm, const void* k, RowMap km, const void* v, RowMap vm, float* o,
                     long long ldo, void* o2, const int* kl, int Bb, int Tq, int Tk) const {
         const pfm_config& c = h->cfg;
@@ -971,18 +986,31 @@ int encoder_stack(const Run& r, const float* x_in, const int* lens, int B, int T
             const size_t es = fast ? 2 : 4;
             const void* qkv = fast ? (const void*)QKVb : (const void*)QKV;
             void* cache = (char*)ck.cache + (size_t)l * ck.layer_stride * es;
-            HIP_TRY(pfm_kv_gather(dt, cache, ck.C, ck.prm, B, 0, (const char*)qkv + (size_t)D * es, 3 * D, T, ck.buf,
-                                  ck.Tk, 2 * D, st));
-            if (fast)
-                HIP_TRY(pfm_fsmn_bf16in(QKVb + 2 * D, rowmap_plain(3 * D), lens, B, T, D, r.P(L.fsmn), K, lenc, nullptr,
-                                        nullptr, Fb, st));
-            else
-                HIP_TRY(pfm_fsmn(QKV + 2 * D, rowmap_plain(3 * D), lens, B, T, D, r.P(L.fsmn), K, lenc, nullptr, Fm,
-                                 nullptr, st));
-            const RowMap km = rowmap_seg(ck.Tk, (long long)ck.Tk * 2 * D, 2 * D);
-            HIP_TRY(r.attn(dt, qkv, rowmap_plain(3 * D), ck.buf, km, (const char*)ck.buf + (size_t)D * es, km,
-                           fast ? nullptr : O, D, fast ? (void*)Ob : nullptr, ck.klen, B, T, ck.Tk));
-            HIP_TRY(pfm_kv_retain(dt, ck.buf, ck.Tk, ck.prm, B, 0, ck.drop, nullptr, cache, ck.C, 2 * D, st));
+            if (fast && K == 11 && lenc == 5) {   // the gather and the window's FSMN as one launch
+                HIP_TRY(pfm_kv_gather_fsmn((const bf16*)cache, ck.C, ck.prm, B, QKVb + D, 3 * D, T, (bf16*)ck.buf, ck.Tk,
+                                           2 * D, QKVb + 2 * D, rowmap_plain(3 * D), lens, D, r.P(L.fsmn), Fb, st));
+            } else {
+                HIP_TRY(pfm_kv_gather(dt, cache, ck.C, ck.prm, B, 0, (const char*)qkv + (size_t)D * es, 3 * D, T, ck.buf,
+                                      ck.Tk, 2 * D, st));
+                if (fast)
+                    HIP_TRY(pfm_fsmn_bf16in(QKVb + 2 * D, rowmap_plain(3 * D), lens, B, T, D, r.P(L.fsmn), K, lenc,
+                                            nullptr, nullptr, Fb, st));
+                else
+                    HIP_TRY(pfm_fsmn(QKV + 2 * D, rowmap_plain(3 * D), lens, B, T, D, r.P(L.fsmn), K, lenc, nullptr, Fm,
+                                     nullptr, st));
+            }
+            // fast mode: the cache retain runs in the attention kernel's tail
+            const hipError_t ea = fast ? r.attn_rt(QKVb, rowmap_plain(3 * D), ck.buf, Ob, ck.klen, B, T, ck.Tk, ck.prm, cache, ck.C, ck.drop, 0,
+                                                   nullptr)
+                                       : hipErrorNotSupported;
+            if (ea != hipErrorNotSupported) {
+                HIP_TRY(ea);
+            } else {
+                const RowMap km = rowmap_seg(ck.Tk, (long long)ck.Tk * 2 * D, 2 * D);
+                HIP_TRY(r.attn(dt, qkv, rowmap_plain(3 * D), ck.buf, km, (const char*)ck.buf + (size_t)D * es, km,
+                               fast ? nullptr : O, D, fast ? (void*)Ob : nullptr, ck.klen, B, T, ck.Tk));
+                HIP_TRY(pfm_kv_retain(dt, ck.buf, ck.Tk, ck.prm, B, 0, ck.drop, nullptr, cache, ck.C, 2 * D, st));
+            }
         } else if (r.fuse_fsmn) {
             const double dk = c.d_model / c.heads;
             const double fl = 4.0 * B * (double)T * T * dk * c.heads;
@@ -2268,10 +2296,17 @@ int stream_decoder(pfm_streams* s, const Run& r, int n, int Tw, int L, const SPr
         if (s->dlb > 0) {
             void* cache = (char*)s->dkv.p + (size_t)l * s->slots * s->Cd * 2 * D * es;
             HIP_TRY(pfm_kv_gather(dt, cache, s->Cd, prm, n, 1, kvl, nkv, Tw, s->kvbuf.p, Tk, 2 * D, st));
-            const RowMap km = rowmap_seg(Tk, (long long)Tk * 2 * D, 2 * D);
-            HIP_TRY(r.attn(dt, Qd, rowmap_plain(D), s->kvbuf.p, km, (const char*)s->kvbuf.p + (size_t)D * es, km,
-                           fast ? nullptr : Od, D, fast ? (void*)Odb : nullptr, kld_d, n, L, Tk));
-            HIP_TRY(pfm_kv_retain(dt, s->kvbuf.p, Tk, prm, n, 1, 0, ntok, cache, s->Cd, 2 * D, st));
+            const hipError_t ea = fast ? r.attn_rt((const bf16*)Qd, rowmap_plain(D), s->kvbuf.p, (bf16*)Odb, kld_d, n, L, Tk, prm, cache,
+                                                   s->Cd, 0, 1, ntok)
+                                       : hipErrorNotSupported;
+            if (ea != hipErrorNotSupported) {
+                HIP_TRY(ea);
+            } else {
+                const RowMap km = rowmap_seg(Tk, (long long)Tk * 2 * D, 2 * D);
+                HIP_TRY(r.attn(dt, Qd, rowmap_plain(D), s->kvbuf.p, km, (const char*)s->kvbuf.p + (size_t)D * es, km,
+                               fast ? nullptr : Od, D, fast ? (void*)Odb : nullptr, kld_d, n, L, Tk));
+                HIP_TRY(pfm_kv_retain(dt, s->kvbuf.p, Tk, prm, n, 1, 0, ntok, cache, s->Cd, 2 * D, st));
+            }
         } else {
             HIP_TRY(r.attn(dt, Qd, rowmap_plain(D), kvl, rowmap_plain(nkv), kvl + (size_t)D * es, rowmap_plain(nkv),
                            fast ? nullptr : Od, D, fast ? (void*)Odb : nullptr, tw_d, n, L, Tw));

@@ -14,12 +14,33 @@ struct SPrm {
     int pad;
 };
 
+// Attention keys of one layer = [K/V cache (cl rows) ; the window's K|V rows (tw rows)] (sanm/attention.py:327-334
+// encoder, 733-737 decoder): key row r of stream i into buf [n][Tk][W] (W = 2d: K | V), 16-B copies by threads
+// tid, tid + nth, ...; rows past cl + tw are zeros
+template <typename T>
+__device__ __forceinline__ void kv_gather_row(const T* __restrict__ cache, int C, const SPrm& p, int dec,
+                                              const T* __restrict__ src, long long src_ld, int Tw, T* __restrict__ buf,
+                                              int Tk, int W, int i, int r, int tid, int nth) {
+    const int cl = dec ? p.cld : p.cle;
+    constexpr int V = 16 / sizeof(T);
+    uint4* dst = (uint4*)(buf + ((long long)i * Tk + r) * W);
+    const uint4* s = nullptr;
+    if (r < cl) s = (const uint4*)(cache + ((long long)p.slot * C + r) * W);
+    else if (r < cl + p.tw) s = (const uint4*)(src + ((long long)i * Tw + (r - cl)) * src_ld);
+    for (int c = tid; c < W / V; c += nth) dst[c] = s ? s[c] : make_uint4(0, 0, 0, 0);
+}
+
 hipError_t pfm_stream_window(const float* feats, int Tn, const SPrm* prm, int n, const float* fcache, const float* pe,
                              int I, int C0, int Tw, float scale, float* x, hipStream_t st);
 hipError_t pfm_stream_fcache(const float* x, const SPrm* prm, int n, int I, int C0, int Tw, float* fcache,
                              hipStream_t st);
 hipError_t pfm_kv_gather(int dtype, const void* cache, int C, const SPrm* prm, int n, int dec, const void* src,
                          long long src_ld, int Tw, void* buf, int Tk, int W, hipStream_t st);
+// streaming encoder layer, one launch: the key buffer gather above and the window's FSMN memory block
+// (fsmn_win_kernel<11, bf16, 5> of k_elem.hip on the window's V rows, lens = tw) side by side
+hipError_t pfm_kv_gather_fsmn(const bf16* cache, int C, const SPrm* prm, int n, const bf16* src, long long src_ld, int Tw,
+                              bf16* buf, int Tk, int W, const bf16* v, RowMap vmap, const int* len, int D, const float* wT,
+                              bf16* out_bf, hipStream_t st);
 hipError_t pfm_kv_retain(int dtype, const void* buf, int Tk, const SPrm* prm, int n, int dec, int drop, const int* ntok,
                          void* cache, int C, int W, hipStream_t st);
 hipError_t pfm_stream_mask_rows(float* encp, bf16* encpb, const SPrm* prm, int n, int Tw, int D, hipStream_t st);

@@ -1,0 +1,9 @@
+set -o pipefail
+mkdir -p gpurun_out/r04f
+timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/r04f/gpu_suite.log 2>&1 &&
+timeout -k 10 120 python tools/stream_prof.py --streams 1 --chunks 50 > gpurun_out/r04f/stream1.txt 2>&1 &&
+PFM_LIB=funasr_amd/_lib/var/prev/libpfm_hip.so timeout -k 10 120 python tools/stream_prof.py --streams 1 --chunks 50 > gpurun_out/r04f/stream1_prev.txt 2>&1 &&
+timeout -k 10 120 python tools/stream_prof.py --streams 64 --chunks 20 > gpurun_out/r04f/stream64.txt 2>&1 &&
+PFM_LIB=funasr_amd/_lib/var/prev/libpfm_hip.so timeout -k 10 120 python tools/stream_prof.py --streams 64 --chunks 20 > gpurun_out/r04f/stream64_prev.txt 2>&1 &&
+cd /tmp && export TMPDIR=/tmp &&
+timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/r04f/sprof -o run -- python3 $GRAFT_REPO_ROOT/tools/stream_prof.py --streams 1 --chunks 20 > $GRAFT_REPO_ROOT/gpurun_out/r04f/sprof.log 2>&1
