@@ -51,7 +51,7 @@ constexpr int RING = RS * TF * 1024;     // 128 KiB
 constexpr int OPF = 16 * 32;             // phase-0 fragments: Wo = 16 output blocks x 32 k steps
 constexpr int CHF = 64;                  // fragments per hidden chunk: 32 W1 k steps + 16 x 2 W2
 #ifndef FFN2_PD
-#define FFN2_PD 6
+#define FFN2_PD 7
 #endif
 constexpr int PD = FFN2_PD;              // fragment reads in flight ahead of their MFMA
 #ifndef FFN2_OPI
@@ -64,7 +64,7 @@ constexpr int OPI = FFN2_OPI;
 #endif
 // rows >= M of a phase-3 store go here, so every wave issues the same stores (the waits count them)
 __device__ __attribute__((aligned(16))) unsigned char ffn2_sink[4096];                   // phase-0 output blocks interleaved per k step (1 = back-to-back chains)
-constexpr int NB = 8;                    // fragment register slots (divides TF, CHF and OPF)
+constexpr int NB = 8;                    // fragment register slots (divides TF, CHF and OPF; the drains name all 8)
 // per-column vectors staged in LDS behind the ring (float offsets)
 constexpr int V_G = 0, V_B = 512, V_C2 = 1024, V_GN = 1536, V_BN = 2048, V_BO = 2560, V_B1 = 3072;
 constexpr int QKF = 3 * OPF;             // MODE 4 phase 3: the next layer's Wqkv, three passes of 512 output features
@@ -419,11 +419,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     // (past the stream's end the read-ahead keeps going: in-bounds reads of stale ring slots nobody consumes,
     // so every step has the same wait)
     // (the publishing position TF - PD must differ from the piece positions 14, 2 and 6)
-    static_assert(TF == 16 && (PD == 5 || PD == 6 || PD == 7), "publish / DMA spread positions");
+    static_assert(TF == 16 && PD >= 5 && PD <= 7, "publish / DMA spread positions");
     auto step_pre = [&](int f, int fs) __attribute__((always_inline)) {
         __builtin_amdgcn_sched_barrier(0);
         const int ps = fs % TF;
-        if (ps == TF - PD) top(f / TF + 1);        // position 10: publish tile f/16 + 1 (DMA piece 0 of tile f/16 + 7)
+        if (ps == TF - PD) top(f / TF + 1);        // position 9: publish tile f/16 + 1 (DMA piece 0 of tile f/16 + 7)
         else if constexpr (VAR != 6) {
             if (ps == 14) piece(f / TF - 1 + RS, 1);
             else if (ps == 2) piece(f / TF - 2 + RS, 2);
