@@ -57,13 +57,7 @@ constexpr int PD = FFN2_PD;              // fragment reads in flight ahead of th
 #ifndef FFN2_OPI
 #define FFN2_OPI 4
 #endif
-constexpr int OPI = FFN2_OPI;
-// MODE 4 phase 3 with its stores inside the MFMA stream (1) instead of between the passes (0): see phase 3 below
-#ifndef FFN2_P3I
-#define FFN2_P3I 0
-#endif
-// rows >= M of a phase-3 store go here, so every wave issues the same stores (the waits count them)
-__device__ __attribute__((aligned(16))) unsigned char ffn2_sink[4096];                   // phase-0 output blocks interleaved per k step (1 = back-to-back chains)
+constexpr int OPI = FFN2_OPI;           // phase-0 output blocks interleaved per k step (1 = back-to-back chains)
 constexpr int NB = 8;                    // fragment register slots (divides TF, CHF and OPF; the drains name all 8)
 // per-column vectors staged in LDS behind the ring (float offsets)
 constexpr int V_G = 0, V_B = 512, V_C2 = 1024, V_GN = 1536, V_BN = 2048, V_BO = 2560, V_B1 = 3072;
@@ -558,18 +552,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     xdl_drain(acc);
 
     // ---- epilogue (no DMA in flight: the last tiles were waited for by their tops)
-    if constexpr (QK && FFN2_P3I) {   // x2 of blocks 0..3; blocks 4..15 leave inside phase 3's first groups
-        float* xrow = live ? Xo + rg * FD : (float*)ffn2_sink;
-#pragma unroll
-        for (int ob = 0; ob < 4; ++ob) {
-            fence();
-            const f32x16 t = acc_get(ob);
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-                *(float4*)(xrow + 32 * ob + 8 * q + 4 * h) = make_float4(t[4 * q], t[4 * q + 1], t[4 * q + 2], t[4 * q + 3]);
-        }
-        fence();
-    } else if (live && Xo) {
+    if (live && Xo) {
 #pragma unroll
         for (int ob = 0; ob < 16; ++ob) {
             fence();
@@ -580,144 +563,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         }
         fence();
     }
-    if constexpr (QK && FFN2_P3I) {
-        // ---- phase 3: the next layer's q|k|v = LN1_next(x2) Wqkv^T + b, three passes of 512 output features = 12
-        //      groups of 4 output blocks (pass p, group pp: blocks 4pp..4pp+3, 128 fragments). A group's accumulators
-        //      start at the bias (LDS vectors), so its outputs need only the bf16 conversion and the stores, and those
-        //      go out inside the NEXT group's MFMA stream, one block every 32 fragments; x2's blocks 4..15 (still in
-        //      the accumulators until their group starts) leave inside pass 0's groups 0..2 the same way. Every wave
-        //      issues the same stores (rows >= M to a sink), so each tile's DMA wait allows for exactly the stores
-        //      issued after the tile's last piece (in-order vmcnt).
-        float mean, rstd;
-        acc_stats(mean, rstd);
-#pragma unroll
-        for (int ob = 0; ob < 16; ++ob) {
-            fence();
-            const f32x16 t = acc_get(ob);
-            ln_block(ob, t, mean, rstd, V_GN, V_BN);
-        }
-        fence();
-#pragma unroll
-        for (int ks = 0; ks < 32; ++ks) asm volatile("" : "+v"(act[ks]));
-        float* xrow = live ? Xo + rg * FD : (float*)ffn2_sink;
-        bf16* qrow = live ? Xn + rg * (3 * FD) : (bf16*)ffn2_sink;
-        // Stores issued at the end of iteration e of a pass (pass-local fragment index; negative: the previous pass,
-        // or -1 in pass 0: the x2 blocks 0..3 above). Events sit at e = 32 k + 8, k = 4 pp + j; passes 1 and 2 see
-        // the same pattern (2 stores per event, the previous pass's last group included), so they share one body.
-        auto p3_cnt = [&](bool first, int k) -> int {
-            if (!first) return (k >= -4 && k < 16) ? 2 : 0;
-            if (k < 0 || k >= 16) return 0;
-            const int pp = k >> 2;
-            return (pp < 3 ? 4 : 0) + (pp == 0 ? 0 : 2);
-        };
-        auto p3_stores_in = [&](bool first, int a, int b) -> int {   // stores at the ends of iterations a .. b-1
-            int n = (first && a <= -1 && -1 < b) ? 16 : 0;
-            const int k0 = a <= 8 ? -((8 - a) / 32) : (a - 8 + 31) / 32;
-#pragma unroll
-            for (int i = 0; i < 3; ++i) {
-                const int k = k0 + i, e = 32 * k + 8;
-                if (e >= a && e < b) n += p3_cnt(first, k);
-            }
-            return n;
-        };
-        // top(t) inside a pass (tile t = global index; fs = the pass-local fragment whose step publishes it)
-        auto top3 = [&](bool first, int t, int fs) __attribute__((always_inline)) {
-            if (t >= NT) return;
-            if (t + RS - 3 < NT) {
-                asm volatile("s_waitcnt vmcnt(%0)" ::"i"((RS - 3) * GW + p3_stores_in(first, fs - 84, fs)) : "memory");
-            } else {
-                vm_wait<0>();
-            }
-            __builtin_amdgcn_sched_barrier(0);
-            __builtin_amdgcn_s_barrier();
-            __builtin_amdgcn_sched_barrier(0);
-            piece(t - 2 + RS, 0);
-        };
-        auto step3 = [&](bool first, int f, int fs) __attribute__((always_inline)) {
-            __builtin_amdgcn_sched_barrier(0);
-            const int ps = fs % TF;
-            if (ps == TF - PD) top3(first, f / TF + 1, fs);
-            else if (ps == 14) piece(f / TF - 1 + RS, 1);
-            else if (ps == 2) piece(f / TF - 2 + RS, 2);
-            else if (ps == 6) piece(f / TF - 2 + RS, 3);
-            rd(f + PD, fs + PD, wf[(fs + PD) % NB]);
-            frag_wait(wf[fs % NB]);
-            __builtin_amdgcn_sched_barrier(0);
-        };
-        auto qkv_out = [&](int p, int ob) __attribute__((always_inline)) {   // bf16 of a finished block -> q|k|v row
-            fence();
-            const f32x16 t = acc_get(ob);
-            bf16x4 o[4];
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-#pragma unroll
-                for (int i = 0; i < 4; ++i) o[q][i] = f2bf(t[4 * q + i]);
-            store_bf16_block(qrow + FD * p + 32 * ob, o, h);
-            fence();
-        };
-        auto x2_out = [&](int ob) __attribute__((always_inline)) {
-            fence();
-            const f32x16 t = acc_get(ob);
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-                *(float4*)(xrow + 32 * ob + 8 * q + 4 * h) = make_float4(t[4 * q], t[4 * q + 1], t[4 * q + 2], t[4 * q + 3]);
-            fence();
-        };
-        auto bias_init = [&](int p, int pp) __attribute__((always_inline)) {   // acc[4pp + e] = q|k|v bias
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const int ob = 4 * pp + e;
-                fence();
-                f32x4 Bq[4];
-#pragma unroll
-                for (int q = 0; q < 4; ++q) Bq[q] = vec_read(vec + V_BQ + FD * p + 32 * ob + 8 * q + 4 * h);
-                asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(Bq[0]), "+v"(Bq[1]), "+v"(Bq[2]), "+v"(Bq[3]), "+v"(wf[0]),
-                             "+v"(wf[1]), "+v"(wf[2]), "+v"(wf[3]), "+v"(wf[4]), "+v"(wf[5]), "+v"(wf[6]), "+v"(wf[7]));
-                f32x16 t;
-#pragma unroll
-                for (int q = 0; q < 4; ++q)
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) t[4 * q + i] = Bq[q][i];
-                acc_put(ob, t);
-            }
-            fence();
-            asm volatile("s_nop 3" ::: "memory");
-            fence();
-        };
-#pragma unroll
-        for (int f = 0; f < PD; ++f) rd(F3 + f, f, wf[f % NB]);
-        valu_to_mfma();
-        auto pass3 = [&](bool first, int p) __attribute__((always_inline)) {   // first: p == 0 (compile time)
-#pragma unroll
-            for (int pp = 0; pp < 4; ++pp) {
-                bias_init(p, pp);
-#pragma unroll
-                for (int ks = 0; ks < 32; ++ks)
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) {
-                        const int l = 4 * ks + e, fs = 128 * pp + l;
-                        step3(first, F3 + OPF * p + fs, fs);
-                        if (VAR == 2 || VAR == 5) asm volatile("" :: "v"(wf[fs % NB]));
-                        else mfma_a(acc[4 * pp + e], wf[fs % NB], act[ks]);
-                        if (l % 32 == 8) {   // event j = l / 32: a block of the previous group (and of x2)
-                            const int j = l / 32;
-                            if (first && pp < 3) x2_out(4 * (pp + 1) + j);
-                            if (pp > 0) qkv_out(p, 4 * (pp - 1) + j);
-                            else if (!first) qkv_out(p - 1, 12 + j);
-                        }
-                    }
-            }
-        };
-        pass3(true, 0);
-        for (int p = 1; p < 3; ++p) pass3(false, p);
-        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(wf[0]), "+v"(wf[1]), "+v"(wf[2]), "+v"(wf[3]), "+v"(wf[4]),
-                     "+v"(wf[5]), "+v"(wf[6]), "+v"(wf[7]));
-        xdl_drain(acc);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) qkv_out(2, 12 + j);   // the last group
-        return;
-    }
-#if !FFN2_P3I
     if constexpr (QK) {
         // ---- phase 3: the next layer's q|k|v = LN1_next(x2) Wqkv^T + b in three passes of 512 output features,
         //      the LayerNorm output as the B operand in registers (the W1 k order: Wqkv packed by ffn2_pack_qkv);
@@ -782,7 +627,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         }
         return;
     }
-#endif
     if (Xn) {
         float mean, rstd;
         acc_stats(mean, rstd);
