@@ -501,7 +501,8 @@ def main():
         nb = bl["ntok"][:, 0].float()
         out["beam_search"] = {"workload": (f"Paraformer-large + CTC head, B={B} x 30 s, joint decoder + CTC prefix beam "
                                            f"search (beam {args.beam}, decoding_ctc_weight 0.3, pre-beam "
-                                           f"{int(1.5 * args.beam)}, end detection), one workgroup per utterance"),
+                                           f"{int(1.5 * args.beam)}, end detection), co-resident workgroups per utterance "
+                                           f"(r^n / r^b / log-psi chains on separate SIMDs)"),
                               "value": round(B * T * FRAME_SEC / dtb, 1), "unit": "audio-sec/sec",
                               "ms_per_step": round(dtb * 1e3, 2), "dtype": out["dtype"],
                               "tokens_per_utt_mean": round(float(nb[nb >= 0].mean().item()), 2)}
