@@ -192,12 +192,13 @@ __global__ __launch_bounds__(NT) void ctc_beam_kernel(BeamArgs a) {
 
     __shared__ int cs[MAXP];
     __shared__ float ws0c[MAXP];
-    __shared__ float psi[MAXK][MAXP], wsc[MAXK][MAXP];
+    __shared__ float psi[MAXK][MAXP];
+    __shared__ __attribute__((aligned(16))) float wsc[MAXK][MAXP];
     __shared__ float hscore[MAXK], hprev[MAXK];
     __shared__ int hlen[MAXK], hlast[MAXK], hcol[MAXK];   // running beam: length, last token, state column
     __shared__ float nscore[MAXK], nprev[MAXK];
     __shared__ int nsrc[MAXK], ntokn[MAXK], nlen[MAXK];
-    __shared__ float csc[MAXK * MAXK];
+    __shared__ __attribute__((aligned(16))) float csc[MAXK * MAXK];
     __shared__ int csrc[MAXK * MAXK];
     __shared__ float escore[MAXN];
     __shared__ int elen[MAXN], epos[MAXN], epar[MAXN], etok[MAXN], eeos[MAXN];   // n-best list, best first
@@ -429,7 +430,15 @@ __global__ __launch_bounds__(NT) void ctc_beam_kernel(BeamArgs a) {
             const int k = w / P, j = w - k * P;
             const float v = wsc[k][j];
             int r = 0;
-            for (int q = 0; q < P; ++q) r += (wsc[k][q] > v || (wsc[k][q] == v && q < j)) ? 1 : 0;
+            for (int q0 = 0; q0 < P; q0 += 4) {   // 16-B LDS reads (broadcast): four comparisons per round trip
+                const float4 c4 = *(const float4*)&wsc[k][q0];
+                const float c[4] = {c4.x, c4.y, c4.z, c4.w};
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int q = q0 + u;
+                    r += (q < P && (c[u] > v || (c[u] == v && q < j))) ? 1 : 0;
+                }
+            }
             if (r < kk) { csc[k * kk + r] = v; csrc[k * kk + r] = w; }
         }
         __syncthreads();
@@ -440,7 +449,15 @@ __global__ __launch_bounds__(NT) void ctc_beam_kernel(BeamArgs a) {
         for (int q = tid; q < nall; q += NT) {
             const float v = csc[q];
             int g = 0;
-            for (int o = 0; o < nall; ++o) g += (csc[o] > v || (csc[o] == v && o < q)) ? 1 : 0;
+            for (int o0 = 0; o0 < nall; o0 += 4) {
+                const float4 c4 = *(const float4*)&csc[o0];
+                const float c[4] = {c4.x, c4.y, c4.z, c4.w};
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int o = o0 + u;
+                    g += (o < nall && (c[u] > v || (c[u] == v && o < q))) ? 1 : 0;
+                }
+            }
             if (g < K) {
                 const int src = csrc[q], k = src / P, j = src - k * P;
                 nscore[g] = v;
