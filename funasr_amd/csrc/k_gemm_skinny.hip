@@ -94,53 +94,76 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(const bf16* __restrict
 // LDS (one wave per row, the statistics of layernorm_v8_kernel: f64 sums in the same order, f32 affine), so the
 // LayerNorm's own launch and its bf16 round trip through HBM go away. Rows padded by 8 elements in LDS (conflict-free
 // 16-B fragment reads across the 16 rows of a tile).
-constexpr int LNK = 512, LNP = LNK + 8;
-template <int MT>
-__global__ __launch_bounds__(512) void gemm_skinny_ln_kernel(const float* __restrict__ X, RowMap xmap,
+// VPL 512-wide segments per row (K = 512 VPL): f32 rows (the encoder / decoder inputs, VPL 1) or bf16 rows (the
+// decoder FFN's 2048-wide hidden before w2, VPL 4, M <= 16); lane l holds elements 512 i + 8 l .. + 7 of segment i,
+// summed in the order of layernorm_v8_kernel<VPL> (bit-identical LayerNorm output)
+template <typename TIN>
+__device__ __forceinline__ void ln_load8(const TIN* p, float4& a, float4& b) {
+    if constexpr (sizeof(TIN) == 4) {
+        a = *(const float4*)p;
+        b = *(const float4*)(p + 4);
+    } else {
+        const bf16x8 t = *(const bf16x8*)p;
+        a = make_float4(bf2f(t[0]), bf2f(t[1]), bf2f(t[2]), bf2f(t[3]));
+        b = make_float4(bf2f(t[4]), bf2f(t[5]), bf2f(t[6]), bf2f(t[7]));
+    }
+}
+template <int MT, int VPL, typename TIN>
+__global__ __launch_bounds__(512) void gemm_skinny_ln_kernel(const TIN* __restrict__ X, RowMap xmap,
                                                              const float* __restrict__ g, const float* __restrict__ bta,
                                                              float eps, const bf16* __restrict__ W, long long ldw, int M,
                                                              int N, GemmEpi e) {
+    constexpr int LNK = 512 * VPL, LNP = LNK + 8;
     __shared__ float red[SK_WAVES][MT][256];
     __shared__ __attribute__((aligned(16))) bf16 As[MT * 16][LNP];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int mb = blockIdx.y * 64;
-    {   // LN of the block's rows (wave w: rows w, w + 8, ...)
-        const int c = lane * 8;
-        const float4 g0 = *(const float4*)(g + c), g1 = *(const float4*)(g + c + 4);
-        const float4 b0 = *(const float4*)(bta + c), b1 = *(const float4*)(bta + c + 4);
-        for (int rr = w; rr < MT * 16; rr += SK_WAVES) {
-            const int row = mb + rr;
-            bf16x8 o = {};
-            if (row < M) {
-                const float* xr = X + xmap.off(row);
-                const float4 v0 = *(const float4*)(xr + c), v1 = *(const float4*)(xr + c + 4);
-                double s = 0.0;
-                s += (double)v0.x + (double)v0.y + (double)v0.z + (double)v0.w;
-                s += (double)v1.x + (double)v1.y + (double)v1.z + (double)v1.w;
-                const double mean = wave_sum_d(s) / LNK;
-                double q = 0.0;
-                {
-                    const double a0 = v0.x - mean, a1 = v0.y - mean, a2 = v0.z - mean, a3 = v0.w - mean;
+    for (int rr = w; rr < MT * 16; rr += SK_WAVES) {   // LN of the block's rows (wave w: rows w, w + 8, ...)
+        const int row = mb + rr;
+        if (row < M) {
+            const TIN* xr = X + xmap.off(row);
+            float4 v[VPL][2];
+#pragma unroll
+            for (int i = 0; i < VPL; ++i) ln_load8(xr + i * 512 + lane * 8, v[i][0], v[i][1]);
+            double s = 0.0;
+#pragma unroll
+            for (int i = 0; i < VPL; ++i)
+#pragma unroll
+                for (int hh = 0; hh < 2; ++hh)
+                    s += (double)v[i][hh].x + (double)v[i][hh].y + (double)v[i][hh].z + (double)v[i][hh].w;
+            const double mean = wave_sum_d(s) / LNK;
+            double q = 0.0;
+#pragma unroll
+            for (int i = 0; i < VPL; ++i)
+#pragma unroll
+                for (int hh = 0; hh < 2; ++hh) {
+                    const double a0 = v[i][hh].x - mean, a1 = v[i][hh].y - mean, a2 = v[i][hh].z - mean,
+                                 a3 = v[i][hh].w - mean;
                     q += a0 * a0 + a1 * a1 + a2 * a2 + a3 * a3;
                 }
-                {
-                    const double a0 = v1.x - mean, a1 = v1.y - mean, a2 = v1.z - mean, a3 = v1.w - mean;
-                    q += a0 * a0 + a1 * a1 + a2 * a2 + a3 * a3;
-                }
-                const double rstd = 1.0 / sqrt(wave_sum_d(q) / LNK + (double)eps);
+            const double rstd = 1.0 / sqrt(wave_sum_d(q) / LNK + (double)eps);
+#pragma unroll
+            for (int i = 0; i < VPL; ++i) {
+                const int c = i * 512 + lane * 8;
+                const float4 g0 = *(const float4*)(g + c), g1 = *(const float4*)(g + c + 4);
+                const float4 b0 = *(const float4*)(bta + c), b1 = *(const float4*)(bta + c + 4);
                 float y[8];
-                y[0] = (float)((v0.x - mean) * rstd) * g0.x + b0.x;
-                y[1] = (float)((v0.y - mean) * rstd) * g0.y + b0.y;
-                y[2] = (float)((v0.z - mean) * rstd) * g0.z + b0.z;
-                y[3] = (float)((v0.w - mean) * rstd) * g0.w + b0.w;
-                y[4] = (float)((v1.x - mean) * rstd) * g1.x + b1.x;
-                y[5] = (float)((v1.y - mean) * rstd) * g1.y + b1.y;
-                y[6] = (float)((v1.z - mean) * rstd) * g1.z + b1.z;
-                y[7] = (float)((v1.w - mean) * rstd) * g1.w + b1.w;
+                y[0] = (float)((v[i][0].x - mean) * rstd) * g0.x + b0.x;
+                y[1] = (float)((v[i][0].y - mean) * rstd) * g0.y + b0.y;
+                y[2] = (float)((v[i][0].z - mean) * rstd) * g0.z + b0.z;
+                y[3] = (float)((v[i][0].w - mean) * rstd) * g0.w + b0.w;
+                y[4] = (float)((v[i][1].x - mean) * rstd) * g1.x + b1.x;
+                y[5] = (float)((v[i][1].y - mean) * rstd) * g1.y + b1.y;
+                y[6] = (float)((v[i][1].z - mean) * rstd) * g1.z + b1.z;
+                y[7] = (float)((v[i][1].w - mean) * rstd) * g1.w + b1.w;
+                bf16x8 o;
 #pragma unroll
                 for (int j = 0; j < 8; ++j) o[j] = f2bf(y[j]);
+                *(bf16x8*)&As[rr][c] = o;
             }
-            *(bf16x8*)&As[rr][c] = o;   // rows beyond M: zeros
+        } else {
+#pragma unroll
+            for (int i = 0; i < VPL; ++i) *(bf16x8*)&As[rr][i * 512 + lane * 8] = bf16x8{};   // rows beyond M: zeros
         }
     }
     __syncthreads();
@@ -200,7 +223,7 @@ __global__ __launch_bounds__(512) void gemm_skinny_ln_kernel(const float* __rest
 // grid.y = ceil(M / 64)); the same epilogue contract as pfm_gemm_skinny
 bool pfm_gemm_skinny_ln_ok(const float* X, RowMap xmap, const void* W, long long ldw, int M, int N, int K,
                            const GemmEpi& e) {
-    if (K != LNK || M < 1 || M > 64 || ldw % 8 != 0 || xmap.ld % 4 != 0) return false;
+    if (K != 512 || M < 1 || M > 64 || ldw % 8 != 0 || xmap.ld % 4 != 0) return false;
     if (xmap.rows_per_seg > 0 && xmap.seg_stride % 4 != 0) return false;
     if (((uintptr_t)X | (uintptr_t)W) % 16 != 0) return false;
     if (!e.out || e.amax_val) return false;
@@ -213,12 +236,31 @@ hipError_t pfm_gemm_skinny_ln(const float* X, RowMap xmap, const float* g, const
     const dim3 grid((N + 15) / 16, (M + 63) / 64), block(512);
     const bf16* wt = (const bf16*)W;
     switch ((M + 15) / 16) {
-        case 1: hipLaunchKernelGGL(gemm_skinny_ln_kernel<1>, grid, block, 0, st, X, xmap, g, b, eps, wt, ldw, M, N, e); break;
-        case 2: hipLaunchKernelGGL(gemm_skinny_ln_kernel<2>, grid, block, 0, st, X, xmap, g, b, eps, wt, ldw, M, N, e); break;
-        case 3: hipLaunchKernelGGL(gemm_skinny_ln_kernel<3>, grid, block, 0, st, X, xmap, g, b, eps, wt, ldw, M, N, e); break;
-        case 4: hipLaunchKernelGGL(gemm_skinny_ln_kernel<4>, grid, block, 0, st, X, xmap, g, b, eps, wt, ldw, M, N, e); break;
+        case 1: hipLaunchKernelGGL((gemm_skinny_ln_kernel<1, 1, float>), grid, block, 0, st, X, xmap, g, b, eps, wt, ldw, M, N, e); break;
+        case 2: hipLaunchKernelGGL((gemm_skinny_ln_kernel<2, 1, float>), grid, block, 0, st, X, xmap, g, b, eps, wt, ldw, M, N, e); break;
+        case 3: hipLaunchKernelGGL((gemm_skinny_ln_kernel<3, 1, float>), grid, block, 0, st, X, xmap, g, b, eps, wt, ldw, M, N, e); break;
+        case 4: hipLaunchKernelGGL((gemm_skinny_ln_kernel<4, 1, float>), grid, block, 0, st, X, xmap, g, b, eps, wt, ldw, M, N, e); break;
         default: return hipErrorInvalidValue;
     }
+    PFM_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+// ... and for bf16 rows of K = 2048 (the decoder FFN's hidden before w2, streaming: <= 16 token rows)
+bool pfm_gemm_skinny_ln2048_ok(const bf16* X, RowMap xmap, const void* W, long long ldw, int M, int N, int K,
+                               const GemmEpi& e) {
+    if (K != 2048 || M < 1 || M > 16 || ldw % 8 != 0 || xmap.ld % 8 != 0) return false;
+    if (xmap.rows_per_seg > 0 && xmap.seg_stride % 8 != 0) return false;
+    if (((uintptr_t)X | (uintptr_t)W) % 16 != 0) return false;
+    if (!e.out || e.amax_val) return false;
+    return pfm_knobs().gemm_skinny && pfm_knobs().gemm_cfg == 0;
+}
+hipError_t pfm_gemm_skinny_ln2048(const bf16* X, RowMap xmap, const float* g, const float* b, float eps, const void* W,
+                                  long long ldw, int M, int N, const GemmEpi& e, hipStream_t st) {
+    if (M <= 0 || N <= 0) return hipSuccess;
+    if (M > 16) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((gemm_skinny_ln_kernel<1, 4, bf16>), dim3((N + 15) / 16, 1), dim3(512), 0, st, X, xmap, g, b, eps,
+                       (const bf16*)W, ldw, M, N, e);
     PFM_LAUNCH_CHECK();
     return hipSuccess;
 }

@@ -227,7 +227,92 @@ __global__ __launch_bounds__(256) void dec_fsmn_stream_kernel(const TIN* __restr
     for (int k = 0; k < K - 1; ++k) st[(long long)k * D] = hist[k];
 }
 
+// The same FSMN with the decoder layer's norm2 in front (fast mode): v = bf16(LN(t) g + b) of the FFN output rows t
+// (f32, [n][L][512]), the arithmetic of layernorm_v8_kernel<1, R> (f64 sums in its order, f32 affine, bf16 out), then
+// dec_fsmn_stream_kernel<bf16> on those rows: one 512-thread block per stream, the normalised rows in LDS (one wave per
+// row), a thread per channel for the causal FSMN. Replaces a LayerNorm launch and its bf16 round trip per layer.
+template <int K>
+__global__ __launch_bounds__(512) void dec_fsmn_ln_stream_kernel(const float* __restrict__ tin, const float* __restrict__ g,
+                                                                 const float* __restrict__ bta, float eps,
+                                                                 const float* __restrict__ wT, float* __restrict__ state,
+                                                                 const SPrm* __restrict__ prm, const int* __restrict__ ntok,
+                                                                 int L, float* __restrict__ x) {
+    constexpr int D = 512;
+    extern __shared__ __attribute__((aligned(16))) bf16 vn[];   // [nt][512]
+    const int i = blockIdx.x;
+    const int nt = min(ntok[i], L);
+    if (nt < 1) return;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    {
+        const int c = lane * 8;
+        const float4 g0 = *(const float4*)(g + c), g1 = *(const float4*)(g + c + 4);
+        const float4 b0 = *(const float4*)(bta + c), b1 = *(const float4*)(bta + c + 4);
+        for (int t = w; t < nt; t += 8) {
+            const float* xr = tin + ((long long)i * L + t) * D;
+            const float4 v0 = *(const float4*)(xr + c), v1 = *(const float4*)(xr + c + 4);
+            double s = 0.0;
+            s += (double)v0.x + (double)v0.y + (double)v0.z + (double)v0.w;
+            s += (double)v1.x + (double)v1.y + (double)v1.z + (double)v1.w;
+            const double mean = wave_sum_d(s) / D;
+            double q = 0.0;
+            {
+                const double a0 = v0.x - mean, a1 = v0.y - mean, a2 = v0.z - mean, a3 = v0.w - mean;
+                q += a0 * a0 + a1 * a1 + a2 * a2 + a3 * a3;
+            }
+            {
+                const double a0 = v1.x - mean, a1 = v1.y - mean, a2 = v1.z - mean, a3 = v1.w - mean;
+                q += a0 * a0 + a1 * a1 + a2 * a2 + a3 * a3;
+            }
+            const double rstd = 1.0 / sqrt(wave_sum_d(q) / D + (double)eps);
+            bf16x8 o;
+            o[0] = f2bf((float)((v0.x - mean) * rstd) * g0.x + b0.x);
+            o[1] = f2bf((float)((v0.y - mean) * rstd) * g0.y + b0.y);
+            o[2] = f2bf((float)((v0.z - mean) * rstd) * g0.z + b0.z);
+            o[3] = f2bf((float)((v0.w - mean) * rstd) * g0.w + b0.w);
+            o[4] = f2bf((float)((v1.x - mean) * rstd) * g1.x + b1.x);
+            o[5] = f2bf((float)((v1.y - mean) * rstd) * g1.y + b1.y);
+            o[6] = f2bf((float)((v1.z - mean) * rstd) * g1.z + b1.z);
+            o[7] = f2bf((float)((v1.w - mean) * rstd) * g1.w + b1.w);
+            *(bf16x8*)&vn[t * D + c] = o;
+        }
+    }
+    __syncthreads();
+    const int c = threadIdx.x;
+    const SPrm p = prm[i];
+    float* st = state + (long long)p.slot * (K - 1) * D + c;
+    float hist[K], wk[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) wk[k] = wT[(long long)k * D + c];
+#pragma unroll
+    for (int k = 0; k < K - 1; ++k) hist[k] = st[(long long)k * D];
+    for (int t = 0; t < nt; ++t) {
+        const long long row = (long long)i * L + t;
+        const float vt = bf2f(vn[t * D + c]);
+        hist[K - 1] = vt;
+        float acc = 0.f;
+#pragma unroll
+        for (int k = 0; k < K; ++k) acc = fmaf(wk[k], hist[k], acc);
+        x[row * D + c] = x[row * D + c] + (acc + vt);
+#pragma unroll
+        for (int k = 0; k < K - 1; ++k) hist[k] = hist[k + 1];
+    }
+#pragma unroll
+    for (int k = 0; k < K - 1; ++k) st[(long long)k * D] = hist[k];
+}
+
 }  // namespace
+
+hipError_t pfm_dec_fsmn_ln_stream(const float* tin, const float* g, const float* b, float eps, const float* wT, int K,
+                                  float* state, const SPrm* prm, const int* ntok, int n, int L, int D, float* x,
+                                  hipStream_t st) {
+    if (n <= 0 || L <= 0) return hipSuccess;
+    if (K != 11 || D != 512 || L > 64 || ((uintptr_t)tin % 16) || ((uintptr_t)g % 16) || ((uintptr_t)b % 16))
+        return hipErrorNotSupported;
+    hipLaunchKernelGGL((dec_fsmn_ln_stream_kernel<11>), dim3(n), dim3(512), (size_t)L * D * 2, st, tin, g, b, eps, wT,
+                       state, prm, ntok, L, x);
+    PFM_LAUNCH_CHECK();
+    return hipSuccess;
+}
 
 hipError_t pfm_stream_window(const float* feats, int Tn, const SPrm* prm, int n, const float* fcache, const float* pe,
                              int I, int C0, int Tw, float scale, float* x, hipStream_t st) {

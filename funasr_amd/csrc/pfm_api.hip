@@ -112,6 +112,10 @@ hipError_t pfm_fbank_launch(const float* wav, const int* nsamp, int B, int S_max
                             hipStream_t st);
 bool pfm_gemm_skinny_ok(const void* A, RowMap amap, const void* W, long long ldw, int M, int N, int K,
                         const GemmEpi& e);
+bool pfm_gemm_skinny_ln2048_ok(const bf16* X, RowMap xmap, const void* W, long long ldw, int M, int N, int K,
+                               const GemmEpi& e);
+hipError_t pfm_gemm_skinny_ln2048(const bf16* X, RowMap xmap, const float* g, const float* b, float eps, const void* W,
+                                  long long ldw, int M, int N, const GemmEpi& e, hipStream_t st);
 bool pfm_gemm_skinny_ln_ok(const float* X, RowMap xmap, const void* W, long long ldw, int M, int N, int K,
                            const GemmEpi& e);
 hipError_t pfm_gemm_skinny_ln(const float* X, RowMap xmap, const float* g, const float* b, float eps, const void* W,
@@ -2259,33 +2263,55 @@ int stream_decoder(pfm_streams* s, const Run& r, int n, int Tw, int L, const SPr
         const void* A = fast ? (const void*)(encpb + D) : (const void*)(encp + D);
         HIP_TRY(r.gemm(dt, A, encmap, r.W(h->wkv_all), D, (int)Mw, nkv, D, e));
     }
+    // pout == nullptr: the caller fuses the closing LayerNorm into its consumer (dec_fsmn_ln_stream_kernel)
     auto ffn = [&](const float* x, size_t lng, size_t lnb, size_t w1, size_t b1, size_t fng, size_t fnb, size_t w2,
                    float* out, size_t pg, size_t pb, void* pout, int pdt) -> int {
         GemmEpi e = epi_default();
         e.bias = r.P(b1); e.relu = 1;
         e.out = Hd; e.out_map = rowmap_plain(Fd); e.out_dtype = dt;
         HIP_TRY(r.ln_gemm(x, rowmap_plain(D), lng, lnb, Xdn, rowmap_plain(D), r.W(w1), D, (int)Ml, Fd, D, e));
-        if (fast)
-            HIP_TRY(pfm_layernorm_bf16in((const bf16*)Hd, rowmap_plain(Fd), (int)Ml, Fd, r.P(fng), r.P(fnb), c.ln_eps,
-                                         Hdn, rowmap_plain(Fd), dt, st));
-        else
-            HIP_TRY(pfm_layernorm(Hd, rowmap_plain(Fd), (int)Ml, Fd, r.P(fng), r.P(fnb), c.ln_eps, nullptr, 0, 1.f,
-                                  Hdn, rowmap_plain(Fd), dt, nullptr, plain, 0, st));
         GemmEpi e2 = epi_default();
         e2.out = out; e2.out_map = rowmap_plain(D); e2.out_dtype = DT_F32;
-        HIP_TRY(r.gemm(dt, Hdn, rowmap_plain(Fd), r.W(w2), Fd, (int)Ml, D, Fd, e2));
-        HIP_TRY(pfm_layernorm(out, rowmap_plain(D), (int)Ml, D, r.P(pg), r.P(pb), c.ln_eps, nullptr, 0, 1.f, pout,
-                              rowmap_plain(D), pdt, nullptr, plain, 0, st));
+        if (fast && pfm_gemm_skinny_ln2048_ok((const bf16*)Hd, rowmap_plain(Fd), r.W(w2), Fd, (int)Ml, D, Fd, e2)) {
+            // the hidden's LayerNorm (2048 wide) in the w2 GEMM's A load
+            ProfScope ps(h, st, PFM_K_GEMM, 2.0 * Ml * D * (double)Fd, (double)Ml * Fd * 2.0 + (double)D * Fd * 2.0 +
+                                                                      (double)Ml * D * 4.0);
+            HIP_TRY(pfm_gemm_skinny_ln2048((const bf16*)Hd, rowmap_plain(Fd), r.P(fng), r.P(fnb), c.ln_eps, r.W(w2), Fd,
+                                           (int)Ml, D, e2, st));
+        } else {
+            if (fast)
+                HIP_TRY(pfm_layernorm_bf16in((const bf16*)Hd, rowmap_plain(Fd), (int)Ml, Fd, r.P(fng), r.P(fnb), c.ln_eps,
+                                             Hdn, rowmap_plain(Fd), dt, st));
+            else
+                HIP_TRY(pfm_layernorm(Hd, rowmap_plain(Fd), (int)Ml, Fd, r.P(fng), r.P(fnb), c.ln_eps, nullptr, 0, 1.f,
+                                      Hdn, rowmap_plain(Fd), dt, nullptr, plain, 0, st));
+            HIP_TRY(r.gemm(dt, Hdn, rowmap_plain(Fd), r.W(w2), Fd, (int)Ml, D, Fd, e2));
+        }
+        if (pout)
+            HIP_TRY(pfm_layernorm(out, rowmap_plain(D), (int)Ml, D, r.P(pg), r.P(pb), c.ln_eps, nullptr, 0, 1.f, pout,
+                                  rowmap_plain(D), pdt, nullptr, plain, 0, st));
         return PFM_OK;
     };
     const int Tk = s->Cd + Tw;
     if (s->dlb > 0) HIP_TRY(s->kvbuf.ensure((size_t)n * std::max(Tk, s->Ce + Tw) * 2 * D * es));
     for (int l = 0; l < c.dec_blocks; ++l) {
         const DecLayer& Lr = h->dec[l];
-        int rc = ffn(Xd, Lr.n1g, Lr.n1b, Lr.w1, Lr.b1, Lr.ng, Lr.nb, Lr.w2, Td, Lr.n2g, Lr.n2b, Tdn, dt);
+        // fast mode: norm2 runs in the FSMN kernel's prologue (dec_fsmn_ln_stream_kernel)
+        const bool fuse_n2 = fast && K == 11 && D == 512 && L <= 64;
+        int rc = ffn(Xd, Lr.n1g, Lr.n1b, Lr.w1, Lr.b1, Lr.ng, Lr.nb, Lr.w2, Td, Lr.n2g, Lr.n2b, fuse_n2 ? nullptr : Tdn, dt);
         if (rc) return rc;
-        HIP_TRY(pfm_dec_fsmn_stream(dt, Tdn, r.P(Lr.fsmn), K, s->dfs.as<float>() + (size_t)l * s->slots * (K - 1) * D,
-                                    prm, ntok, n, L, D, Xd, st));
+        float* dstate = s->dfs.as<float>() + (size_t)l * s->slots * (K - 1) * D;
+        const hipError_t ef = fuse_n2 ? pfm_dec_fsmn_ln_stream(Td, r.P(Lr.n2g), r.P(Lr.n2b), c.ln_eps, r.P(Lr.fsmn), K,
+                                                               dstate, prm, ntok, n, L, D, Xd, st)
+                                      : hipErrorNotSupported;
+        if (ef != hipErrorNotSupported) {
+            HIP_TRY(ef);
+        } else {
+            if (fuse_n2)   // (unaligned vectors: the separate LayerNorm after all)
+                HIP_TRY(pfm_layernorm(Td, rowmap_plain(D), (int)Ml, D, r.P(Lr.n2g), r.P(Lr.n2b), c.ln_eps, nullptr, 0, 1.f,
+                                      Tdn, rowmap_plain(D), dt, nullptr, plain, 0, st));
+            HIP_TRY(pfm_dec_fsmn_stream(dt, Tdn, r.P(Lr.fsmn), K, dstate, prm, ntok, n, L, D, Xd, st));
+        }
         {
             GemmEpi e = epi_default();
             e.bias = r.P(Lr.bq);

@@ -50,5 +50,10 @@ hipError_t pfm_cif_chunk(const float* hc, const float* wout, const float* bout, 
                          hipStream_t st);
 hipError_t pfm_dec_fsmn_stream(int dtype, const void* v, const float* wT, int K, float* state, const SPrm* prm,
                                const int* ntok, int n, int L, int D, float* x, hipStream_t st);
+// fast mode: the decoder layer's norm2 (LayerNorm of the FFN output rows, f32) fused in front of the FSMN above;
+// hipErrorNotSupported (nothing launched) for shapes it does not take
+hipError_t pfm_dec_fsmn_ln_stream(const float* tin, const float* g, const float* b, float eps, const float* wT, int K,
+                                  float* state, const SPrm* prm, const int* ntok, int n, int L, int D, float* x,
+                                  hipStream_t st);
 hipError_t pfm_pad_rows_zero(float* encp, bf16* encpb, int n, int Tw, int D, hipStream_t st);
 hipError_t pfm_rows_copy(float* dst, long long dld, const float* src, long long sld, int w, int rows, hipStream_t st);

@@ -1,0 +1,9 @@
+set -o pipefail
+mkdir -p gpurun_out/r04n
+T="python -u -m pytest -x -q --timeout 120 --timeout-method thread"
+timeout -k 10 400 $T tests/test_gpu_streaming.py tests/test_gpu_stream_beam.py tests/test_gpu_ops.py -k "stream or ln_gemm or skinny" > gpurun_out/r04n/tests.log 2>&1 &&
+timeout -k 10 200 python tools/stream_tokens_dump.py gpurun_out/r04n/tok_new.npy 4 40 > gpurun_out/r04n/dump.txt 2>&1 &&
+PFM_LIB=funasr_amd/_lib/var/prev/libpfm_hip.so timeout -k 10 200 python tools/stream_tokens_dump.py gpurun_out/r04n/tok_prev.npy 4 40 >> gpurun_out/r04n/dump.txt 2>&1 &&
+timeout -k 10 120 python tools/stream_prof.py --streams 1 --chunks 50 > gpurun_out/r04n/stream1.txt 2>&1 &&
+PFM_LIB=funasr_amd/_lib/var/prev/libpfm_hip.so timeout -k 10 120 python tools/stream_prof.py --streams 1 --chunks 50 > gpurun_out/r04n/stream1_prev.txt 2>&1 &&
+timeout -k 10 120 python tools/stream_prof.py --streams 64 --chunks 20 > gpurun_out/r04n/stream64.txt 2>&1
