@@ -151,7 +151,14 @@ struct BeamArgs {
 // Every workgroup of an utterance keeps the whole search state (the pre-beam, the beam, the n-best list) and runs the
 // selection steps redundantly on identical data; the columns' scores and the states cross workgroups through global
 // memory and one arrival barrier per position. All workgroups of an utterance sit on one XCD (same L2).
-constexpr int BL = 32;   // frames per r^n -> r^b hand-off block
+#ifndef BEAM_BL
+#define BEAM_BL 16
+#endif
+// frames per r^n -> r^b hand-off block (a multiple of 8): the r^b chains start one block late, so a position costs
+// nblk + 1 rounds of BL frames; 16 measured best (21.4 ms per B = 64 batch vs 22.0 at 32 and 22.1 at 8: more rounds,
+// more barriers)
+constexpr int BL = BEAM_BL;
+static_assert(BL % 8 == 0 && BL <= 32, "hand-off block");
 
 __host__ __device__ __forceinline__ long long pfm_align2(long long n) { return (n + 1) & ~1LL; }   // float2 rows
 
