@@ -18,6 +18,7 @@
 // K chunk g (8 contiguous bf16) of a 16 x 32 operand; the accumulator element e of lane l is
 // row 4 (l >> 4) + e, column l & 15.
 #include "pfm_common.h"
+#include "pfm_stream.h"
 
 namespace {
 
@@ -108,11 +109,26 @@ __device__ __forceinline__ void ln_load8(const TIN* p, float4& a, float4& b) {
         b = make_float4(bf2f(t[4]), bf2f(t[5]), bf2f(t[6]), bf2f(t[7]));
     }
 }
-template <int MT, int VPL, typename TIN>
+// Streaming encoder layer (SQ): the LN1 -> QKV launch also builds the attention's key buffer and the window's FSMN
+// memory block, the work of kv_gather_fsmn_kernel, because both are per column over all rows of one stream and a
+// workgroup holds all M <= 64 rows of its 16 columns: K|V columns go to their buffer rows [cl, cl + tw) of each stream
+// with the cached rows [0, cl) and zero rows [cl + tw, Tk) beside them (kv_gather_row), and the V columns' bf16 values
+// (what QKVb holds) feed fsmn_win_body<11, bf16, 5>'s arithmetic from LDS.
+struct SkQkv {
+    const SPrm* prm;
+    const bf16* cache;   // this layer's [slots][C][2d]
+    bf16* buf;           // [n][Tk][2d]
+    const float* wT;     // FSMN taps [11][d]
+    bf16* fout;          // FSMN block output, [n Tw][d]
+    int Tw, Tk, C, D;
+};
+constexpr int SQ_K = 11, SQ_LEFT = 5;
+
+template <int MT, int VPL, typename TIN, bool SQ = false>
 __global__ __launch_bounds__(512) void gemm_skinny_ln_kernel(const TIN* __restrict__ X, RowMap xmap,
                                                              const float* __restrict__ g, const float* __restrict__ bta,
                                                              float eps, const bf16* __restrict__ W, long long ldw, int M,
-                                                             int N, GemmEpi e) {
+                                                             int N, GemmEpi e, SkQkv sq) {
     constexpr int LNK = 512 * VPL, LNP = LNK + 8;
     __shared__ float red[SK_WAVES][MT][256];
     __shared__ __attribute__((aligned(16))) bf16 As[MT * 16][LNP];
@@ -214,6 +230,50 @@ __global__ __launch_bounds__(512) void gemm_skinny_ln_kernel(const TIN* __restri
         if (e.out_dtype == DT_F32) ((float*)e.out)[ob + col] = v;
         else ((bf16*)e.out)[ob + col] = f2bf(v);
         if (e.out2) ((bf16*)e.out2)[e.out2_map.off(row) + col] = f2bf(v);
+        if constexpr (SQ) {
+            const int i = row / sq.Tw, t = row - i * sq.Tw;
+            if (n0 >= sq.D) {   // window K|V row t of stream i -> key row cl + t
+                const SPrm& p = sq.prm[i];
+                if (t < p.tw) sq.buf[((long long)i * sq.Tk + p.cle + t) * 2 * sq.D + (col - sq.D)] = f2bf(v);
+            }
+            // the V columns' bf16 values (what QKVb holds), for the FSMN below; As is free once the K loop is done
+            if (n0 >= 2 * sq.D) ((float*)&As[0][0])[row * 16 + (rc & 15)] = bf2f(f2bf(v));
+        }
+    }
+    if constexpr (SQ) {
+        const int D = sq.D, n = M / sq.Tw;
+        if (n0 >= D) {   // the cached rows [0, cl) and the zero rows [cl + tw, Tk) of this workgroup's 16 columns
+            for (int idx = threadIdx.x; idx < n * sq.Tk * 2; idx += 512) {
+                const int hh = idx & 1, ir = idx >> 1, i = ir / sq.Tk, r = ir - i * sq.Tk;
+                const SPrm& p = sq.prm[i];
+                if (r >= p.cle && r < p.cle + p.tw) continue;
+                const int c8 = n0 - D + 8 * hh;
+                uint4 val = make_uint4(0, 0, 0, 0);
+                if (r < p.cle) val = *(const uint4*)(sq.cache + ((long long)p.slot * sq.C + r) * 2 * D + c8);
+                *(uint4*)(sq.buf + ((long long)i * sq.Tk + r) * 2 * D + c8) = val;
+            }
+        }
+        if (n0 >= 2 * D) {   // FSMN over each stream's tw window rows, as fsmn_win_body<11, bf16, 5> (lens = tw)
+            __syncthreads();
+            const float* vs = (const float*)&As[0][0];
+            for (int idx = threadIdx.x; idx < M * 16; idx += 512) {
+                const int row = idx >> 4, cc = idx & 15, c = n0 - 2 * D + cc;
+                const int i = row / sq.Tw, t = row - i * sq.Tw;
+                const int L = min(sq.prm[i].tw, sq.Tw);
+                float y = 0.f;
+                if (t < L) {
+                    float acc = 0.f;
+#pragma unroll
+                    for (int k = 0; k < SQ_K; ++k) {
+                        const int tt = t - SQ_LEFT + k;
+                        const float x = (tt >= 0 && tt < L) ? vs[(i * sq.Tw + tt) * 16 + cc] : 0.f;
+                        acc = fmaf(sq.wT[k * D + c], x, acc);
+                    }
+                    y = acc + vs[row * 16 + cc];
+                }
+                sq.fout[(long long)row * D + c] = f2bf(y);
+            }
+        }
     }
 }
 
@@ -236,10 +296,10 @@ hipError_t pfm_gemm_skinny_ln(const float* X, RowMap xmap, const float* g, const
     const dim3 grid((N + 15) / 16, (M + 63) / 64), block(512);
     const bf16* wt = (const bf16*)W;
     switch ((M + 15) / 16) {
-        case 1: hipLaunchKernelGGL((gemm_skinny_ln_kernel<1, 1, float>), grid, block, 0, st, X, xmap, g, b, eps, wt, ldw, M, N, e); break;
-        case 2: hipLaunchKernelGGL((gemm_skinny_ln_kernel<2, 1, float>), grid, block, 0, st, X, xmap, g, b, eps, wt, ldw, M, N, e); break;
-        case 3: hipLaunchKernelGGL((gemm_skinny_ln_kernel<3, 1, float>), grid, block, 0, st, X, xmap, g, b, eps, wt, ldw, M, N, e); break;
-        case 4: hipLaunchKernelGGL((gemm_skinny_ln_kernel<4, 1, float>), grid, block, 0, st, X, xmap, g, b, eps, wt, ldw, M, N, e); break;
+        case 1: hipLaunchKernelGGL((gemm_skinny_ln_kernel<1, 1, float>), grid, block, 0, st, X, xmap, g, b, eps, wt, ldw, M, N, e, SkQkv{}); break;
+        case 2: hipLaunchKernelGGL((gemm_skinny_ln_kernel<2, 1, float>), grid, block, 0, st, X, xmap, g, b, eps, wt, ldw, M, N, e, SkQkv{}); break;
+        case 3: hipLaunchKernelGGL((gemm_skinny_ln_kernel<3, 1, float>), grid, block, 0, st, X, xmap, g, b, eps, wt, ldw, M, N, e, SkQkv{}); break;
+        case 4: hipLaunchKernelGGL((gemm_skinny_ln_kernel<4, 1, float>), grid, block, 0, st, X, xmap, g, b, eps, wt, ldw, M, N, e, SkQkv{}); break;
         default: return hipErrorInvalidValue;
     }
     PFM_LAUNCH_CHECK();
@@ -260,7 +320,7 @@ hipError_t pfm_gemm_skinny_ln2048(const bf16* X, RowMap xmap, const float* g, co
     if (M <= 0 || N <= 0) return hipSuccess;
     if (M > 16) return hipErrorInvalidValue;
     hipLaunchKernelGGL((gemm_skinny_ln_kernel<1, 4, bf16>), dim3((N + 15) / 16, 1), dim3(512), 0, st, X, xmap, g, b, eps,
-                       (const bf16*)W, ldw, M, N, e);
+                       (const bf16*)W, ldw, M, N, e, SkQkv{});
     PFM_LAUNCH_CHECK();
     return hipSuccess;
 }
@@ -292,6 +352,32 @@ hipError_t pfm_gemm_skinny(const void* A, RowMap amap, const void* W, long long 
         case 3: hipLaunchKernelGGL(gemm_skinny_kernel<3>, grid, block, 0, st, a, amap, wt, ldw, M, N, K, e); break;
         case 4: hipLaunchKernelGGL(gemm_skinny_kernel<4>, grid, block, 0, st, a, amap, wt, ldw, M, N, K, e); break;
         default: return hipErrorInvalidValue;
+    }
+    PFM_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+// Streaming encoder layer: LN1 -> QKV as above (M <= 64 rows = n streams x Tw window rows, K = 512, N = 3d, d % 16 == 0,
+// bf16 q|k|v rows) that also writes the attention's key buffer [n][Tk][2d] from this layer's K/V cache and the window's
+// FSMN memory block (11 taps, left 5, lens = tw): pfm_kv_gather_fsmn's two outputs, bit-identical, without its launch.
+// hipErrorNotSupported (nothing launched) for any other shape.
+hipError_t pfm_gemm_skinny_ln_qkv(const float* X, RowMap xmap, const float* g, const float* b, float eps, const void* W,
+                                  long long ldw, int M, int N, const GemmEpi& e, const SPrm* prm, int n, int Tw,
+                                  const bf16* cache, int C, bf16* buf, int Tk, const float* wT, bf16* fout, int D,
+                                  hipStream_t st) {
+    if (!pfm_gemm_skinny_ln_ok(X, xmap, W, ldw, M, N, 512, e)) return hipErrorNotSupported;
+    if (n < 1 || Tw < 1 || M != n * Tw || N != 3 * D || D % 16 || e.out_dtype != DT_BF16 || Tk < Tw)
+        return hipErrorNotSupported;
+    if (((uintptr_t)cache | (uintptr_t)buf) % 16 != 0 || !prm || !wT || !fout) return hipErrorNotSupported;
+    const SkQkv sq{prm, cache, buf, wT, fout, Tw, Tk, C, D};
+    const dim3 grid(N / 16, 1), block(512);
+    const bf16* wt = (const bf16*)W;
+    switch ((M + 15) / 16) {
+        case 1: hipLaunchKernelGGL((gemm_skinny_ln_kernel<1, 1, float, true>), grid, block, 0, st, X, xmap, g, b, eps, wt, ldw, M, N, e, sq); break;
+        case 2: hipLaunchKernelGGL((gemm_skinny_ln_kernel<2, 1, float, true>), grid, block, 0, st, X, xmap, g, b, eps, wt, ldw, M, N, e, sq); break;
+        case 3: hipLaunchKernelGGL((gemm_skinny_ln_kernel<3, 1, float, true>), grid, block, 0, st, X, xmap, g, b, eps, wt, ldw, M, N, e, sq); break;
+        case 4: hipLaunchKernelGGL((gemm_skinny_ln_kernel<4, 1, float, true>), grid, block, 0, st, X, xmap, g, b, eps, wt, ldw, M, N, e, sq); break;
+        default: return hipErrorNotSupported;
     }
     PFM_LAUNCH_CHECK();
     return hipSuccess;

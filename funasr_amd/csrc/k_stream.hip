@@ -51,11 +51,13 @@ __global__ __launch_bounds__(256) void stream_fcache_kernel(const float* __restr
 
 // Attention keys of one layer (kv_gather_row, pfm_stream.h): one block per (stream, key row)
 template <typename T>
-__global__ __launch_bounds__(128) void kv_gather_kernel(const T* __restrict__ cache, int C, const SPrm* __restrict__ prm,
-                                                        int dec, const T* __restrict__ src, long long src_ld, int Tw,
-                                                        T* __restrict__ buf, int Tk, int W) {
-    const int i = blockIdx.y, r = blockIdx.x;
-    kv_gather_row(cache, C, prm[i], dec, src, src_ld, Tw, buf, Tk, W, i, r, (int)threadIdx.x, 128);
+__global__ __launch_bounds__(128) void kv_gather_kernel(const T* __restrict__ cache, long long cache_ls, int C,
+                                                        const SPrm* __restrict__ prm, int dec, const T* __restrict__ src,
+                                                        long long src_ls, long long src_ld, int Tw, T* __restrict__ buf,
+                                                        long long buf_ls, int Tk, int W) {
+    const int i = blockIdx.y, r = blockIdx.x, l = blockIdx.z;   // grid.z: layers (strides in elements)
+    kv_gather_row(cache + l * cache_ls, C, prm[i], dec, src + l * src_ls, src_ld, Tw, buf + l * buf_ls, Tk, W, i, r,
+                  (int)threadIdx.x, 128);
 }
 
 // New cache = the last min(C, cl + tw - drop) rows of buf[i][0 .. cl + tw - drop): drop = chunk_size[2]
@@ -332,21 +334,28 @@ hipError_t pfm_stream_fcache(const float* x, const SPrm* prm, int n, int I, int 
     return hipSuccess;
 }
 
-hipError_t pfm_kv_gather(int dtype, const void* cache, int C, const SPrm* prm, int n, int dec, const void* src,
-                         long long src_ld, int Tw, void* buf, int Tk, int W, hipStream_t st) {
-    if (n <= 0 || Tk <= 0) return hipSuccess;
+hipError_t pfm_kv_gather_layers(int dtype, const void* cache, long long cache_ls, int C, const SPrm* prm, int n, int dec,
+                                const void* src, long long src_ls, long long src_ld, int Tw, void* buf, long long buf_ls,
+                                int Tk, int W, int layers, hipStream_t st) {
+    if (n <= 0 || Tk <= 0 || layers <= 0) return hipSuccess;
     const int es = dtype == DT_F32 ? 4 : 2;
     if ((W * es) % 16 || (src_ld * es) % 16 || ((uintptr_t)src % 16) || ((uintptr_t)buf % 16) ||
-        ((uintptr_t)cache % 16))
+        ((uintptr_t)cache % 16) || (cache_ls * es) % 16 || (src_ls * es) % 16 || (buf_ls * es) % 16)
         return hipErrorInvalidValue;
+    const dim3 grid(Tk, n, layers);
     if (dtype == DT_F32)
-        hipLaunchKernelGGL(kv_gather_kernel<float>, dim3(Tk, n), dim3(128), 0, st, (const float*)cache, C, prm, dec,
-                           (const float*)src, src_ld, Tw, (float*)buf, Tk, W);
+        hipLaunchKernelGGL(kv_gather_kernel<float>, grid, dim3(128), 0, st, (const float*)cache, cache_ls, C, prm, dec,
+                           (const float*)src, src_ls, src_ld, Tw, (float*)buf, buf_ls, Tk, W);
     else
-        hipLaunchKernelGGL(kv_gather_kernel<bf16>, dim3(Tk, n), dim3(128), 0, st, (const bf16*)cache, C, prm, dec,
-                           (const bf16*)src, src_ld, Tw, (bf16*)buf, Tk, W);
+        hipLaunchKernelGGL(kv_gather_kernel<bf16>, grid, dim3(128), 0, st, (const bf16*)cache, cache_ls, C, prm, dec,
+                           (const bf16*)src, src_ls, src_ld, Tw, (bf16*)buf, buf_ls, Tk, W);
     PFM_LAUNCH_CHECK();
     return hipSuccess;
+}
+
+hipError_t pfm_kv_gather(int dtype, const void* cache, int C, const SPrm* prm, int n, int dec, const void* src,
+                         long long src_ld, int Tw, void* buf, int Tk, int W, hipStream_t st) {
+    return pfm_kv_gather_layers(dtype, cache, 0, C, prm, n, dec, src, 0, src_ld, Tw, buf, 0, Tk, W, 1, st);
 }
 
 hipError_t pfm_kv_retain(int dtype, const void* buf, int Tk, const SPrm* prm, int n, int dec, int drop, const int* ntok,

@@ -122,6 +122,10 @@ hipError_t pfm_gemm_skinny_ln(const float* X, RowMap xmap, const float* g, const
                               long long ldw, int M, int N, const GemmEpi& e, hipStream_t st);
 hipError_t pfm_gemm_skinny(const void* A, RowMap amap, const void* W, long long ldw, int M, int N, int K,
                            const GemmEpi& e, hipStream_t st);
+hipError_t pfm_gemm_skinny_ln_qkv(const float* X, RowMap xmap, const float* g, const float* b, float eps, const void* W,
+                                  long long ldw, int M, int N, const GemmEpi& e, const SPrm* prm, int n, int Tw,
+                                  const bf16* cache, int C, bf16* buf, int Tk, const float* wT, bf16* fout, int D,
+                                  hipStream_t st);
 hipError_t pfm_punc_embed(const int* ids, const int* lens, int B, int T, const float* embed, int n_embed,
                           const float* pe, int D, float scale, float* X, hipStream_t st);
 hipError_t pfm_punc_head(const float* x, int B, int T, const int* lens, const float* W, const float* bias, int NP,
@@ -962,12 +966,27 @@ int encoder_stack(const Run& r, const float* x_in, const int* lens, int B, int T
                                   Xn, xmap3, lndt, nullptr, plain, 0, st));
         // fast mode, l > 0 without the fused FFN in front: LN1 and the QKV projection through Run::ln_gemm
         const bool ln1_fold = l > 0 && fast && !x3 && !(ffn_fused && l > l0);
+        bool kv_built = false;   // streaming: the QKV launch also wrote the key buffer and the FSMN block
         if (!qkv_ready && ln1_fold) {
             GemmEpi e = epi_default();
             e.bias = r.P(L.bqkv);
             e.out = QKVb; e.out_map = rowmap_plain(3 * D); e.out_dtype = DT_BF16;
-            HIP_TRY(r.ln_gemm(X, rowmap_plain(D), L.ln1g, L.ln1b, Xn, rowmap_plain(D), r.W(L.wqkv), din, (int)M, 3 * D,
-                              din, e));
+            if (r.ck && K == 11 && lenc == 5 && din == D) {
+                const ChunkKV& ck = *r.ck;
+                ProfScope ps(h, st, PFM_K_GEMM, 2.0 * M * 3 * D * din,
+                             (double)M * din * 4.0 + 3.0 * D * din * 2.0 + (double)M * 3 * D * 2.0);
+                const hipError_t eq = pfm_gemm_skinny_ln_qkv(
+                    X, rowmap_plain(D), r.P(L.ln1g), r.P(L.ln1b), c.ln_eps, r.W(L.wqkv), din, (int)M, 3 * D, e, ck.prm,
+                    B, T, (const bf16*)ck.cache + (size_t)l * ck.layer_stride, ck.C, (bf16*)ck.buf, ck.Tk, r.P(L.fsmn),
+                    Fb, D, st);
+                if (eq != hipErrorNotSupported) {
+                    HIP_TRY(eq);
+                    kv_built = true;
+                }
+            }
+            if (!kv_built)
+                HIP_TRY(r.ln_gemm(X, rowmap_plain(D), L.ln1g, L.ln1b, Xn, rowmap_plain(D), r.W(L.wqkv), din, (int)M,
+                                  3 * D, din, e));
         } else if (!qkv_ready) {   // q|k|v = LN1(x) Wqkv^T + b   (fast mode: bf16 only — attention and FSMN read bf16)
             GemmEpi e = epi_default();
             e.bias = r.P(L.bqkv);
@@ -990,7 +1009,8 @@ int encoder_stack(const Run& r, const float* x_in, const int* lens, int B, int T
             const size_t es = fast ? 2 : 4;
             const void* qkv = fast ? (const void*)QKVb : (const void*)QKV;
             void* cache = (char*)ck.cache + (size_t)l * ck.layer_stride * es;
-            if (fast && K == 11 && lenc == 5) {   // the gather and the window's FSMN as one launch
+            if (kv_built) {   // written by the QKV launch above
+            } else if (fast && K == 11 && lenc == 5) {   // the gather and the window's FSMN as one launch
                 HIP_TRY(pfm_kv_gather_fsmn((const bf16*)cache, ck.C, ck.prm, B, QKVb + D, 3 * D, T, (bf16*)ck.buf, ck.Tk,
                                            2 * D, QKVb + 2 * D, rowmap_plain(3 * D), lens, D, r.P(L.fsmn), Fb, st));
             } else {
@@ -2226,6 +2246,13 @@ struct pfm_streams {
     }
 };
 
+// gathered attention keys of a step: the encoder's one layer at a time, the decoder's all layers at once
+static size_t stream_kvbuf_bytes(const pfm_streams* s, int n, int Tw, int D, size_t es, int dec_layers) {
+    const size_t enc = s->Ce ? (size_t)n * (s->Ce + Tw) : 0;
+    const size_t dec = s->Cd ? (size_t)n * (s->Cd + Tw) * std::max(dec_layers, 1) : 0;
+    return std::max(enc, dec) * 2 * D * es;
+}
+
 namespace {
 
 // One streaming decoder pass (decoder.py:461-528 over n streams x L token rows): decoders with FFN ->
@@ -2293,7 +2320,14 @@ int stream_decoder(pfm_streams* s, const Run& r, int n, int Tw, int L, const SPr
         return PFM_OK;
     };
     const int Tk = s->Cd + Tw;
-    if (s->dlb > 0) HIP_TRY(s->kvbuf.ensure((size_t)n * std::max(Tk, s->Ce + Tw) * 2 * D * es));
+    // decoder look-back: the keys of every layer ([its K/V cache ; the window's memory K|V]) gathered in one launch
+    // before the layers run (each layer's retain then rewrites only its own cache)
+    const long long kv_ls = (long long)n * Tk * 2 * D;
+    if (s->dlb > 0) {
+        HIP_TRY(s->kvbuf.ensure(stream_kvbuf_bytes(s, n, Tw, D, es, c.dec_blocks)));
+        HIP_TRY(pfm_kv_gather_layers(dt, s->dkv.p, (long long)s->slots * s->Cd * 2 * D, s->Cd, prm, n, 1, s->kvw.p, 2 * D,
+                                     nkv, Tw, s->kvbuf.p, kv_ls, Tk, 2 * D, c.dec_blocks, st));
+    }
     for (int l = 0; l < c.dec_blocks; ++l) {
         const DecLayer& Lr = h->dec[l];
         // fast mode: norm2 runs in the FSMN kernel's prologue (dec_fsmn_ln_stream_kernel)
@@ -2321,17 +2355,17 @@ int stream_decoder(pfm_streams* s, const Run& r, int n, int Tw, int L, const SPr
         const char* kvl = (const char*)s->kvw.p + (size_t)l * 2 * D * es;
         if (s->dlb > 0) {
             void* cache = (char*)s->dkv.p + (size_t)l * s->slots * s->Cd * 2 * D * es;
-            HIP_TRY(pfm_kv_gather(dt, cache, s->Cd, prm, n, 1, kvl, nkv, Tw, s->kvbuf.p, Tk, 2 * D, st));
-            const hipError_t ea = fast ? r.attn_rt((const bf16*)Qd, rowmap_plain(D), s->kvbuf.p, (bf16*)Odb, kld_d, n, L, Tk, prm, cache,
+            void* kb = (char*)s->kvbuf.p + (size_t)l * kv_ls * es;
+            const hipError_t ea = fast ? r.attn_rt((const bf16*)Qd, rowmap_plain(D), kb, (bf16*)Odb, kld_d, n, L, Tk, prm, cache,
                                                    s->Cd, 0, 1, ntok)
                                        : hipErrorNotSupported;
             if (ea != hipErrorNotSupported) {
                 HIP_TRY(ea);
             } else {
                 const RowMap km = rowmap_seg(Tk, (long long)Tk * 2 * D, 2 * D);
-                HIP_TRY(r.attn(dt, Qd, rowmap_plain(D), s->kvbuf.p, km, (const char*)s->kvbuf.p + (size_t)D * es, km,
+                HIP_TRY(r.attn(dt, Qd, rowmap_plain(D), kb, km, (const char*)kb + (size_t)D * es, km,
                                fast ? nullptr : Od, D, fast ? (void*)Odb : nullptr, kld_d, n, L, Tk));
-                HIP_TRY(pfm_kv_retain(dt, s->kvbuf.p, Tk, prm, n, 1, 0, ntok, cache, s->Cd, 2 * D, st));
+                HIP_TRY(pfm_kv_retain(dt, kb, Tk, prm, n, 1, 0, ntok, cache, s->Cd, 2 * D, st));
             }
         } else {
             HIP_TRY(r.attn(dt, Qd, rowmap_plain(D), kvl, rowmap_plain(nkv), kvl + (size_t)D * es, rowmap_plain(nkv),
@@ -2565,7 +2599,7 @@ int stream_step(pfm_streams* s, void* stream, int n, const int32_t* slot_ids, co
     HIP_TRY(s->prm.ensure(pb + 3 * ib));
     HIP_TRY(s->xin.ensure((size_t)n * Tw * I * 4));
     HIP_TRY(s->fin.ensure((size_t)n * std::max(maxn, 1) * I * 4));
-    if (s->Ce || s->Cd) HIP_TRY(s->kvbuf.ensure((size_t)n * (std::max(s->Ce, s->Cd) + Tw) * 2 * D * es));
+    if (s->Ce || s->Cd) HIP_TRY(s->kvbuf.ensure(stream_kvbuf_bytes(s, n, Tw, D, es, c.dec_blocks)));
     if (c.dec_blocks > 0) HIP_TRY(s->kvw.ensure((size_t)n * Tw * nkv * es));
     HIP_TRY(s->tok.ensure((size_t)n * std::max(L_cap, 1) * 4));
     if (s->hntok_cap < n) {

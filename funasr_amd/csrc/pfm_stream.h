@@ -36,6 +36,11 @@ hipError_t pfm_stream_fcache(const float* x, const SPrm* prm, int n, int I, int 
                              hipStream_t st);
 hipError_t pfm_kv_gather(int dtype, const void* cache, int C, const SPrm* prm, int n, int dec, const void* src,
                          long long src_ld, int Tw, void* buf, int Tk, int W, hipStream_t st);
+// ... for `layers` layers in one launch (grid.z): layer l reads cache + l cache_ls and src + l src_ls, writes buf + l buf_ls
+// (strides in elements; the streaming decoder gathers all its layers' keys up front, before any layer's retain)
+hipError_t pfm_kv_gather_layers(int dtype, const void* cache, long long cache_ls, int C, const SPrm* prm, int n, int dec,
+                                const void* src, long long src_ls, long long src_ld, int Tw, void* buf, long long buf_ls,
+                                int Tk, int W, int layers, hipStream_t st);
 // streaming encoder layer, one launch: the key buffer gather above and the window's FSMN memory block
 // (fsmn_win_kernel<11, bf16, 5> of k_elem.hip on the window's V rows, lens = tw) side by side
 hipError_t pfm_kv_gather_fsmn(const bf16* cache, int C, const SPrm* prm, int n, const bf16* src, long long src_ld, int Tw,
