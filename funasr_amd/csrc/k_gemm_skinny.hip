@@ -25,6 +25,29 @@ namespace {
 constexpr int SK_WAVES = 8;
 constexpr int SK_UNROLL = 4;   // 32-wide K steps whose fragments are in flight per wave
 
+// The epilogue operands (bias, residuals) of the <= MT*256/512 elements a thread finishes, loaded at kernel start
+// so their memory round trip overlaps the operand loads instead of following the K loop (these launches are
+// latency-bound: each serial HBM / L2 round trip is a visible share of a 4-6 us kernel). Same values, same order.
+template <int MT>
+struct SkEpiPre {
+    static constexpr int EPT = (MT * 256 + 511) / 512;
+    float b[EPT], r0[EPT], r1[EPT];
+    __device__ __forceinline__ void load(const GemmEpi& e, int mb, int n0, int M, int N) {
+#pragma unroll
+        for (int j = 0; j < EPT; ++j) {
+            const int idx = threadIdx.x + j * 512;
+            const int t = idx >> 8, rc = idx & 255;
+            const int row = mb + t * 16 + (rc >> 4), col = n0 + (rc & 15);
+            b[j] = 0.f; r0[j] = 0.f; r1[j] = 0.f;
+            if (idx >= MT * 256 || row >= M || col >= N) continue;
+            if (e.bias) b[j] = e.bias[col];
+            if (e.res0) r0[j] = e.res0_bf16 ? bf2f(((const bf16*)e.res0)[(long long)row * e.ld_res0 + col])
+                                            : e.res0[(long long)row * e.ld_res0 + col];
+            if (e.res1) r1[j] = e.res1[(long long)row * e.ld_res1 + col];
+        }
+    }
+};
+
 template <int MT>
 __global__ __launch_bounds__(512) void gemm_skinny_kernel(const bf16* __restrict__ A, RowMap amap,
                                                           const bf16* __restrict__ W, long long ldw, int M, int N,
@@ -45,6 +68,8 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(const bf16* __restrict
         mok[t] = m < M;
         arow[t] = A + amap.off(mok[t] ? m : 0) + g * 8;
     }
+    SkEpiPre<MT> pre;
+    pre.load(e, mb, n0, M, N);
     f32x4 acc[MT];
 #pragma unroll
     for (int t = 0; t < MT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -70,19 +95,20 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(const bf16* __restrict
 #pragma unroll
         for (int q = 0; q < 4; ++q) red[w][t][(4 * g + q) * 16 + r16] = acc[t][q];
     __syncthreads();
-    for (int idx = threadIdx.x; idx < MT * 256; idx += 512) {
+#pragma unroll
+    for (int j = 0; j < SkEpiPre<MT>::EPT; ++j) {
+        const int idx = threadIdx.x + j * 512;
         const int t = idx >> 8, rc = idx & 255;
         const int row = mb + t * 16 + (rc >> 4), col = n0 + (rc & 15);
-        if (row >= M || col >= N) continue;
+        if (idx >= MT * 256 || row >= M || col >= N) continue;
         float v = 0.f;
 #pragma unroll
         for (int ww = 0; ww < SK_WAVES; ++ww) v += red[ww][t][rc];
         v *= e.alpha;
-        if (e.bias) v += e.bias[col];
+        if (e.bias) v += pre.b[j];
         if (e.relu) v = fmaxf(v, 0.f);
-        if (e.res0) v += e.res0_bf16 ? bf2f(((const bf16*)e.res0)[(long long)row * e.ld_res0 + col])
-                                     : e.res0[(long long)row * e.ld_res0 + col];
-        if (e.res1) v += e.res1[(long long)row * e.ld_res1 + col];
+        if (e.res0) v += pre.r0[j];
+        if (e.res1) v += pre.r1[j];
         const long long ob = e.out_map.off(row);
         if (e.out_dtype == DT_F32) ((float*)e.out)[ob + col] = v;
         else ((bf16*)e.out)[ob + col] = f2bf(v);
@@ -134,6 +160,23 @@ __global__ __launch_bounds__(512) void gemm_skinny_ln_kernel(const TIN* __restri
     __shared__ __attribute__((aligned(16))) bf16 As[MT * 16][LNP];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int mb = blockIdx.y * 64;
+    const int r16 = lane & 15, gq = lane >> 4;
+    const int n0 = blockIdx.x * 16;
+    const int n = n0 + r16;
+    const bool nok = n < N;
+    const bf16* wrow = W + (long long)(nok ? n : 0) * ldw + gq * 8;
+    const bf16x8 zero8 = {};
+    constexpr int nsteps = LNK / 32;
+    // the first K round's weight fragments and the epilogue operands go out before the LayerNorm prologue: neither
+    // depends on it, so their round trips overlap the X row loads
+    bf16x8 bw[SK_UNROLL];
+#pragma unroll
+    for (int u = 0; u < SK_UNROLL; ++u) {
+        const int st = w + u * SK_WAVES;
+        bw[u] = (st < nsteps && nok) ? *(const bf16x8*)(wrow + st * 32) : zero8;
+    }
+    SkEpiPre<MT> pre;
+    pre.load(e, mb, n0, M, N);
     for (int rr = w; rr < MT * 16; rr += SK_WAVES) {   // LN of the block's rows (wave w: rows w, w + 8, ...)
         const int row = mb + rr;
         if (row < M) {
@@ -183,23 +226,17 @@ __global__ __launch_bounds__(512) void gemm_skinny_ln_kernel(const TIN* __restri
         }
     }
     __syncthreads();
-    const int r16 = lane & 15, gq = lane >> 4;
-    const int n0 = blockIdx.x * 16;
-    const int n = n0 + r16;
-    const bool nok = n < N;
-    const bf16* wrow = W + (long long)(nok ? n : 0) * ldw + gq * 8;
     f32x4 acc[MT];
 #pragma unroll
     for (int t = 0; t < MT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-    const bf16x8 zero8 = {};
-    constexpr int nsteps = LNK / 32;
+#pragma unroll
     for (int s0 = w; s0 < nsteps; s0 += SK_WAVES * SK_UNROLL) {
-        bf16x8 bw[SK_UNROLL], ba[SK_UNROLL][MT];
+        bf16x8 ba[SK_UNROLL][MT];
 #pragma unroll
         for (int u = 0; u < SK_UNROLL; ++u) {
             const int st = s0 + u * SK_WAVES;
             const bool sok = st < nsteps;
-            bw[u] = (sok && nok) ? *(const bf16x8*)(wrow + st * 32) : zero8;
+            if (s0 != w) bw[u] = (sok && nok) ? *(const bf16x8*)(wrow + st * 32) : zero8;
 #pragma unroll
             for (int t = 0; t < MT; ++t) ba[u][t] = sok ? *(const bf16x8*)&As[t * 16 + r16][st * 32 + gq * 8] : zero8;
         }
@@ -213,19 +250,20 @@ __global__ __launch_bounds__(512) void gemm_skinny_ln_kernel(const TIN* __restri
 #pragma unroll
         for (int q = 0; q < 4; ++q) red[w][t][(4 * gq + q) * 16 + r16] = acc[t][q];
     __syncthreads();
-    for (int idx = threadIdx.x; idx < MT * 256; idx += 512) {
+#pragma unroll
+    for (int j = 0; j < SkEpiPre<MT>::EPT; ++j) {
+        const int idx = threadIdx.x + j * 512;
         const int t = idx >> 8, rc = idx & 255;
         const int row = mb + t * 16 + (rc >> 4), col = n0 + (rc & 15);
-        if (row >= M || col >= N) continue;
+        if (idx >= MT * 256 || row >= M || col >= N) continue;
         float v = 0.f;
 #pragma unroll
         for (int ww = 0; ww < SK_WAVES; ++ww) v += red[ww][t][rc];
         v *= e.alpha;
-        if (e.bias) v += e.bias[col];
+        if (e.bias) v += pre.b[j];
         if (e.relu) v = fmaxf(v, 0.f);
-        if (e.res0) v += e.res0_bf16 ? bf2f(((const bf16*)e.res0)[(long long)row * e.ld_res0 + col])
-                                     : e.res0[(long long)row * e.ld_res0 + col];
-        if (e.res1) v += e.res1[(long long)row * e.ld_res1 + col];
+        if (e.res0) v += pre.r0[j];
+        if (e.res1) v += pre.r1[j];
         const long long ob = e.out_map.off(row);
         if (e.out_dtype == DT_F32) ((float*)e.out)[ob + col] = v;
         else ((bf16*)e.out)[ob + col] = f2bf(v);
