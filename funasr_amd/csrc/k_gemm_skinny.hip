@@ -23,7 +23,10 @@
 namespace {
 
 constexpr int SK_WAVES = 8;
-constexpr int SK_UNROLL = 4;   // 32-wide K steps whose fragments are in flight per wave
+constexpr int SK_UNROLL = 4;   // 32-wide K steps whose fragments are in flight per wave (K <= 1024: one round)
+// K = 2048 (FFN w2): 8 steps in flight per wave, so all 64 steps of a workgroup are one round of loads instead of two
+// dependent ones (the accumulation order per wave is the same: steps w, w + 8, ..., w + 56)
+constexpr int SK_UNROLL_WIDE = 8;
 
 // The epilogue operands (bias, residuals) of the <= MT*256/512 elements a thread finishes, loaded at kernel start
 // so their memory round trip overlaps the operand loads instead of following the K loop (these launches are
@@ -48,7 +51,7 @@ struct SkEpiPre {
     }
 };
 
-template <int MT>
+template <int MT, int UNR = SK_UNROLL>
 __global__ __launch_bounds__(512) void gemm_skinny_kernel(const bf16* __restrict__ A, RowMap amap,
                                                           const bf16* __restrict__ W, long long ldw, int M, int N,
                                                           int K, GemmEpi e) {
@@ -75,10 +78,10 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(const bf16* __restrict
     for (int t = 0; t < MT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
     const bf16x8 zero8 = {};
     const int nsteps = K / 32;
-    for (int s0 = w; s0 < nsteps; s0 += SK_WAVES * SK_UNROLL) {
-        bf16x8 bw[SK_UNROLL], ba[SK_UNROLL][MT];
+    for (int s0 = w; s0 < nsteps; s0 += SK_WAVES * UNR) {
+        bf16x8 bw[UNR], ba[UNR][MT];
 #pragma unroll
-        for (int u = 0; u < SK_UNROLL; ++u) {
+        for (int u = 0; u < UNR; ++u) {
             const int s = s0 + u * SK_WAVES;
             const bool sok = s < nsteps;
             bw[u] = (sok && nok) ? *(const bf16x8*)(wrow + s * 32) : zero8;
@@ -86,7 +89,7 @@ __global__ __launch_bounds__(512) void gemm_skinny_kernel(const bf16* __restrict
             for (int t = 0; t < MT; ++t) ba[u][t] = (sok && mok[t]) ? *(const bf16x8*)(arow[t] + s * 32) : zero8;
         }
 #pragma unroll
-        for (int u = 0; u < SK_UNROLL; ++u)
+        for (int u = 0; u < UNR; ++u)
 #pragma unroll
             for (int t = 0; t < MT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ba[u][t], bw[u], acc[t], 0, 0, 0);
     }
@@ -156,6 +159,7 @@ __global__ __launch_bounds__(512) void gemm_skinny_ln_kernel(const TIN* __restri
                                                              float eps, const bf16* __restrict__ W, long long ldw, int M,
                                                              int N, GemmEpi e, SkQkv sq) {
     constexpr int LNK = 512 * VPL, LNP = LNK + 8;
+    constexpr int UNR = VPL >= 4 ? SK_UNROLL_WIDE : SK_UNROLL;
     __shared__ float red[SK_WAVES][MT][256];
     __shared__ __attribute__((aligned(16))) bf16 As[MT * 16][LNP];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -169,14 +173,38 @@ __global__ __launch_bounds__(512) void gemm_skinny_ln_kernel(const TIN* __restri
     constexpr int nsteps = LNK / 32;
     // the first K round's weight fragments and the epilogue operands go out before the LayerNorm prologue: neither
     // depends on it, so their round trips overlap the X row loads
-    bf16x8 bw[SK_UNROLL];
+    bf16x8 bw[UNR];
 #pragma unroll
-    for (int u = 0; u < SK_UNROLL; ++u) {
+    for (int u = 0; u < UNR; ++u) {
         const int st = w + u * SK_WAVES;
         bw[u] = (st < nsteps && nok) ? *(const bf16x8*)(wrow + st * 32) : zero8;
     }
     SkEpiPre<MT> pre;
     pre.load(e, mb, n0, M, N);
+    // SQ: per-stream parameters into LDS (read by the epilogue after the prologue's barrier), and the work the tail
+    // would otherwise start with a round trip — this workgroup's cached key rows and FSMN taps — loaded now
+    __shared__ int4 sqp[SQ ? 64 : 1];   // slot, cle, tw per stream (M <= 64 rows)
+    constexpr int SQC = 2;              // cached-row chunks (16 B) per thread prefetched
+    uint4 sqc[SQC];
+    float tap[SQ_K];
+    if constexpr (SQ) {
+        const int D = sq.D, ns = M / sq.Tw;
+        if ((int)threadIdx.x < ns) {
+            const SPrm p = sq.prm[threadIdx.x];
+            sqp[threadIdx.x] = make_int4(p.slot, p.cle, p.tw, 0);
+        }
+#pragma unroll
+        for (int u = 0; u < SQC; ++u) {
+            sqc[u] = make_uint4(0, 0, 0, 0);
+            const int idx = threadIdx.x + u * 512;
+            if (n0 < D || idx >= ns * sq.Tk * 2) continue;
+            const int hh = idx & 1, ir = idx >> 1, i = ir / sq.Tk, r = ir - i * sq.Tk;
+            const SPrm p = sq.prm[i];
+            if (r < p.cle) sqc[u] = *(const uint4*)(sq.cache + ((long long)p.slot * sq.C + r) * 2 * D + n0 - D + 8 * hh);
+        }
+#pragma unroll
+        for (int k = 0; k < SQ_K; ++k) tap[k] = n0 >= 2 * D ? sq.wT[k * D + n0 - 2 * D + (threadIdx.x & 15)] : 0.f;
+    }
     for (int rr = w; rr < MT * 16; rr += SK_WAVES) {   // LN of the block's rows (wave w: rows w, w + 8, ...)
         const int row = mb + rr;
         if (row < M) {
@@ -230,10 +258,10 @@ __global__ __launch_bounds__(512) void gemm_skinny_ln_kernel(const TIN* __restri
 #pragma unroll
     for (int t = 0; t < MT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int s0 = w; s0 < nsteps; s0 += SK_WAVES * SK_UNROLL) {
-        bf16x8 ba[SK_UNROLL][MT];
+    for (int s0 = w; s0 < nsteps; s0 += SK_WAVES * UNR) {
+        bf16x8 ba[UNR][MT];
 #pragma unroll
-        for (int u = 0; u < SK_UNROLL; ++u) {
+        for (int u = 0; u < UNR; ++u) {
             const int st = s0 + u * SK_WAVES;
             const bool sok = st < nsteps;
             if (s0 != w) bw[u] = (sok && nok) ? *(const bf16x8*)(wrow + st * 32) : zero8;
@@ -241,7 +269,7 @@ __global__ __launch_bounds__(512) void gemm_skinny_ln_kernel(const TIN* __restri
             for (int t = 0; t < MT; ++t) ba[u][t] = sok ? *(const bf16x8*)&As[t * 16 + r16][st * 32 + gq * 8] : zero8;
         }
 #pragma unroll
-        for (int u = 0; u < SK_UNROLL; ++u)
+        for (int u = 0; u < UNR; ++u)
 #pragma unroll
             for (int t = 0; t < MT; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ba[u][t], bw[u], acc[t], 0, 0, 0);
     }
@@ -271,8 +299,8 @@ __global__ __launch_bounds__(512) void gemm_skinny_ln_kernel(const TIN* __restri
         if constexpr (SQ) {
             const int i = row / sq.Tw, t = row - i * sq.Tw;
             if (n0 >= sq.D) {   // window K|V row t of stream i -> key row cl + t
-                const SPrm& p = sq.prm[i];
-                if (t < p.tw) sq.buf[((long long)i * sq.Tk + p.cle + t) * 2 * sq.D + (col - sq.D)] = f2bf(v);
+                const int4 p = sqp[i];
+                if (t < p.z) sq.buf[((long long)i * sq.Tk + p.y + t) * 2 * sq.D + (col - sq.D)] = f2bf(v);
             }
             // the V columns' bf16 values (what QKVb holds), for the FSMN below; As is free once the K loop is done
             if (n0 >= 2 * sq.D) ((float*)&As[0][0])[row * 16 + (rc & 15)] = bf2f(f2bf(v));
@@ -281,15 +309,18 @@ __global__ __launch_bounds__(512) void gemm_skinny_ln_kernel(const TIN* __restri
     if constexpr (SQ) {
         const int D = sq.D, n = M / sq.Tw;
         if (n0 >= D) {   // the cached rows [0, cl) and the zero rows [cl + tw, Tk) of this workgroup's 16 columns
-            for (int idx = threadIdx.x; idx < n * sq.Tk * 2; idx += 512) {
-                const int hh = idx & 1, ir = idx >> 1, i = ir / sq.Tk, r = ir - i * sq.Tk;
-                const SPrm& p = sq.prm[i];
-                if (r >= p.cle && r < p.cle + p.tw) continue;
-                const int c8 = n0 - D + 8 * hh;
-                uint4 val = make_uint4(0, 0, 0, 0);
-                if (r < p.cle) val = *(const uint4*)(sq.cache + ((long long)p.slot * sq.C + r) * 2 * D + c8);
-                *(uint4*)(sq.buf + ((long long)i * sq.Tk + r) * 2 * D + c8) = val;
-            }
+#pragma unroll
+            for (int u = 0; u < SQC + 1; ++u)
+                for (int idx = threadIdx.x + u * 512; idx < n * sq.Tk * 2; idx += (u < SQC ? n * sq.Tk * 2 : 512)) {
+                    const int hh = idx & 1, ir = idx >> 1, i = ir / sq.Tk, r = ir - i * sq.Tk;
+                    const int4 p = sqp[i];
+                    if (r >= p.y && r < p.y + p.z) continue;
+                    const int c8 = n0 - D + 8 * hh;
+                    uint4 val = make_uint4(0, 0, 0, 0);
+                    if (u < SQC) val = sqc[u];
+                    else if (r < p.y) val = *(const uint4*)(sq.cache + ((long long)p.x * sq.C + r) * 2 * D + c8);
+                    *(uint4*)(sq.buf + ((long long)i * sq.Tk + r) * 2 * D + c8) = val;
+                }
         }
         if (n0 >= 2 * D) {   // FSMN over each stream's tw window rows, as fsmn_win_body<11, bf16, 5> (lens = tw)
             __syncthreads();
@@ -297,7 +328,7 @@ __global__ __launch_bounds__(512) void gemm_skinny_ln_kernel(const TIN* __restri
             for (int idx = threadIdx.x; idx < M * 16; idx += 512) {
                 const int row = idx >> 4, cc = idx & 15, c = n0 - 2 * D + cc;
                 const int i = row / sq.Tw, t = row - i * sq.Tw;
-                const int L = min(sq.prm[i].tw, sq.Tw);
+                const int L = min(sqp[i].z, sq.Tw);
                 float y = 0.f;
                 if (t < L) {
                     float acc = 0.f;
@@ -305,7 +336,7 @@ __global__ __launch_bounds__(512) void gemm_skinny_ln_kernel(const TIN* __restri
                     for (int k = 0; k < SQ_K; ++k) {
                         const int tt = t - SQ_LEFT + k;
                         const float x = (tt >= 0 && tt < L) ? vs[(i * sq.Tw + tt) * 16 + cc] : 0.f;
-                        acc = fmaf(sq.wT[k * D + c], x, acc);
+                        acc = fmaf(tap[k], x, acc);
                     }
                     y = acc + vs[row * 16 + cc];
                 }
@@ -385,8 +416,14 @@ hipError_t pfm_gemm_skinny(const void* A, RowMap amap, const void* W, long long 
     const bf16* a = (const bf16*)A;
     const bf16* wt = (const bf16*)W;
     switch (M > 64 ? 4 : (M + 15) / 16) {
-        case 1: hipLaunchKernelGGL(gemm_skinny_kernel<1>, grid, block, 0, st, a, amap, wt, ldw, M, N, K, e); break;
-        case 2: hipLaunchKernelGGL(gemm_skinny_kernel<2>, grid, block, 0, st, a, amap, wt, ldw, M, N, K, e); break;
+        case 1:
+            if (K > 32 * SK_WAVES * SK_UNROLL) hipLaunchKernelGGL((gemm_skinny_kernel<1, SK_UNROLL_WIDE>), grid, block, 0, st, a, amap, wt, ldw, M, N, K, e);
+            else hipLaunchKernelGGL(gemm_skinny_kernel<1>, grid, block, 0, st, a, amap, wt, ldw, M, N, K, e);
+            break;
+        case 2:
+            if (K > 32 * SK_WAVES * SK_UNROLL) hipLaunchKernelGGL((gemm_skinny_kernel<2, SK_UNROLL_WIDE>), grid, block, 0, st, a, amap, wt, ldw, M, N, K, e);
+            else hipLaunchKernelGGL(gemm_skinny_kernel<2>, grid, block, 0, st, a, amap, wt, ldw, M, N, K, e);
+            break;
         case 3: hipLaunchKernelGGL(gemm_skinny_kernel<3>, grid, block, 0, st, a, amap, wt, ldw, M, N, K, e); break;
         case 4: hipLaunchKernelGGL(gemm_skinny_kernel<4>, grid, block, 0, st, a, amap, wt, ldw, M, N, K, e); break;
         default: return hipErrorInvalidValue;
