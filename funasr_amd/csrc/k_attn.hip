@@ -965,7 +965,10 @@ hipError_t pfm_attention_retain(const void* q, RowMap qmap, const void* kv, int 
         (void)hipFuncSetAttribute((const void*)attn_bf16_kernel<8>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   LDS8_FS);
     }
-    if (pfm_knobs().attn_waves == 8) {
+    // chunk-sized steps (<= 128 query rows: every streaming step) take the 4-wave kernel: the same per-wave arithmetic
+    // (bit-identical output), half the waves and a smaller kernel on a launch chain where only latency counts
+    // (2.20 -> 2.135 ms per chunk at one stream, profiles/r04y_stream_attn_waves.txt)
+    if (pfm_knobs().attn_waves == 8 && Tq > 128) {
         dim3 grid((Tq + 255) / 256, heads, B), block(512);
         hipLaunchKernelGGL((attn_bf16_kernel<8>), grid, block, 2 * STG2, st, a);
     } else {

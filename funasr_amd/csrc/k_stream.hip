@@ -106,23 +106,44 @@ __global__ __launch_bounds__(256) void cif_chunk_kernel(const float* __restrict_
                                                         float smooth, float noise, float tail, float thr,
                                                         float* __restrict__ chid, float* __restrict__ calpha,
                                                         float* __restrict__ emb, int Lcap, int* __restrict__ ntok,
-                                                        float* __restrict__ alphas_out) {
+                                                        float* __restrict__ alphas_out, int stage) {
     __shared__ float al[64];
+    extern __shared__ __attribute__((aligned(16))) float ers[];   // staged window rows [tw][D] (stage != 0)
     const int i = blockIdx.x;
     const SPrm p = prm[i];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    for (int t = wv; t < p.tw; t += 4) {
-        const float* hr = hc + ((long long)i * Tw + t) * D;
-        double s = 0.0;
-        for (int c = lane; c < D; c += 64) s += (double)hr[c] * (double)wout[c];
-        s = wave_sum_d(s);
-        if (lane == 0) {
-            const float z = (float)(s + (double)bout[0]);
-            const float sg = (float)(1.0 / (1.0 + exp(-(double)z)));
-            float a = fmaxf(sg * smooth - noise, 0.f);
-            if (t < cs0 || (!p.fin && t >= keep)) a = 0.f;
-            al[t] = a;
-            if (alphas_out) alphas_out[(long long)i * Tw + t] = a;
+    // the integrate loop below is sequential over the rows: with the rows read from global memory inside it, every row
+    // was a dependent round trip; they are staged into LDS up front (one parallel copy), as are 4 rows per wave of the
+    // alpha dot products (same per-row summation order)
+    const float* erow0 = encp + ((long long)i * (Tw + 2) + 1) * D;   // padded rows 1 .. tw == frames 0 .. tw - 1
+    if (stage)
+        for (int q = threadIdx.x; q < p.tw * D / 4; q += 256) ((float4*)ers)[q] = ((const float4*)erow0)[q];
+    constexpr int RW = 4;
+    for (int t0 = wv; t0 < p.tw; t0 += 4 * RW) {
+        double s[RW];
+#pragma unroll
+        for (int r = 0; r < RW; ++r) s[r] = 0.0;
+        for (int c = lane; c < D; c += 64) {
+            const double wc = (double)wout[c];
+#pragma unroll
+            for (int r = 0; r < RW; ++r) {
+                const int t = t0 + 4 * r;
+                if (t < p.tw) s[r] += (double)hc[((long long)i * Tw + t) * D + c] * wc;
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < RW; ++r) {
+            const int t = t0 + 4 * r;
+            if (t >= p.tw) break;
+            const double sr = wave_sum_d(s[r]);
+            if (lane == 0) {
+                const float z = (float)(sr + (double)bout[0]);
+                const float sg = (float)(1.0 / (1.0 + exp(-(double)z)));
+                float a = fmaxf(sg * smooth - noise, 0.f);
+                if (t < cs0 || (!p.fin && t >= keep)) a = 0.f;
+                al[t] = a;
+                if (alphas_out) alphas_out[(long long)i * Tw + t] = a;
+            }
         }
     }
     __syncthreads();
@@ -146,7 +167,7 @@ __global__ __launch_bounds__(256) void cif_chunk_kernel(const float* __restrict_
             for (int k = 0; k < CIF_CH; ++k) hv[k] = cache_h[k];
         } else if (s <= p.tw) {
             a = al[s - 1];
-            const float* er = encp + ((long long)i * (Tw + 2) + s) * D;   // padded row s == frame s - 1
+            const float* er = (stage ? (const float*)ers : erow0) + (long long)(s - 1) * D;   // frame s - 1
 #pragma unroll
             for (int k = 0; k < CIF_CH; ++k) {
                 const int c = threadIdx.x + k * 256;
@@ -384,8 +405,10 @@ hipError_t pfm_cif_chunk(const float* hc, const float* wout, const float* bout, 
                          hipStream_t st) {
     if (n <= 0) return hipSuccess;
     if (D > 256 * CIF_CH || Tw > 64) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(cif_chunk_kernel, dim3(n), dim3(256), 0, st, hc, wout, bout, encp, prm, Tw, D, cs0, keep, smooth,
-                       noise, tail, thr, chid, calpha, emb, Lcap, ntok, alphas_out);
+    const size_t lds = (size_t)Tw * D * 4;
+    const int stage = (lds <= 48 * 1024 && D % 4 == 0 && ((uintptr_t)encp % 16) == 0) ? 1 : 0;
+    hipLaunchKernelGGL(cif_chunk_kernel, dim3(n), dim3(256), stage ? lds : 0, st, hc, wout, bout, encp, prm, Tw, D, cs0, keep,
+                       smooth, noise, tail, thr, chid, calpha, emb, Lcap, ntok, alphas_out, stage);
     PFM_LAUNCH_CHECK();
     return hipSuccess;
 }
