@@ -305,6 +305,9 @@ struct pfm_handle {
     // side stream: the decoder's memory K|V projection overlaps the predictor / CIF / token-count sync
     hipStream_t st2 = nullptr;
     hipEvent_t ev_enc = nullptr, ev_kv = nullptr;
+    // fast mode: the projection in KVG layer groups, one event each (the decoder's layer l waits for its group only)
+    static constexpr int KVG = 4;
+    hipEvent_t ev_kvg[KVG] = {};
     // live profiling: event pairs per launch, per kernel class
     struct ProfRec { hipEvent_t a, b; int kc; double flops, bytes; };
     bool prof_on = false;
@@ -1252,6 +1255,8 @@ void pfm_destroy(pfm_handle* h) {
     for (auto e : h->ev_pool) (void)hipEventDestroy(e);
     if (h->ev_enc) (void)hipEventDestroy(h->ev_enc);
     if (h->ev_kv) (void)hipEventDestroy(h->ev_kv);
+    for (auto e : h->ev_kvg)
+        if (e) (void)hipEventDestroy(e);
     if (h->st2) (void)hipStreamDestroy(h->st2);
     for (int k = 0; k < pfm_handle::MAXSUB; ++k) {
         if (h->sub_st[k]) (void)hipStreamDestroy(h->sub_st[k]);
@@ -1407,28 +1412,39 @@ int pfm_run(pfm_handle* h, void* stream, int mode, const float* feats, const int
     // output, so it runs on the side stream while the predictor, the CIF and the host's token-count
     // sync proceed; the caller's stream joins it before the first cross-attention (or any return).
     void* KV = h->KV.p;
-    auto launch_kv = [&](hipStream_t s) -> hipError_t {
+    // layers [l0, l1) of it (columns l0 2D .. l1 2D of the [B*T, nL*2D] rows)
+    auto launch_kv = [&](hipStream_t s, int l0, int l1) -> hipError_t {
+        const int nc = (l1 - l0) * 2 * D;
         GemmEpi e = epi_default();
-        e.bias = P(h->bkv_all);
-        e.out = KV; e.out_map = rowmap_plain(nkv); e.out_dtype = dt;
+        e.bias = P(h->bkv_all + (size_t)l0 * 2 * D);
+        e.out = (char*)KV + (size_t)l0 * 2 * D * (fast ? 2 : 4); e.out_map = rowmap_plain(nkv); e.out_dtype = dt;
         const void* A = fast ? (const void*)(encpb + D) : (const void*)(encp + D);
-        const double fl = 2.0 * M * nkv * D;
-        const double by = ((double)M * D + (double)nkv * D) * es + (double)M * nkv * es;
+        const void* Wg = W(h->wkv_all + (size_t)l0 * 2 * D * D);
+        const double fl = 2.0 * M * nc * D;
+        const double by = ((double)M * D + (double)nc * D) * es + (double)M * nc * es;
         ProfScope ps(h, s, PFM_K_GEMM, fl, by);
-        if (!fast && x6_route(h, dt, W(h->wkv_all), D, D))
-            return gemm_x6(h, (const float*)A, encmap, (const float*)W(h->wkv_all), (int)M, nkv, D, e, s);
-        return gemm_dispatch(dt, A, encmap, W(h->wkv_all), D, (int)M, nkv, D, e, s);
+        if (!fast && x6_route(h, dt, Wg, D, D))
+            return gemm_x6(h, (const float*)A, encmap, (const float*)Wg, (int)M, nc, D, e, s);
+        return gemm_dispatch(dt, A, encmap, Wg, D, (int)M, nc, D, e, s);
     };
+    // fast mode: KVG launches of nL / KVG layers each, so the decoder's first layers start on their own group's K|V
+    // while the later groups run beside them (the layer loop below waits per group)
+    const int kv_groups = (fast && c.dec_blocks % pfm_handle::KVG == 0) ? pfm_handle::KVG : 1;
+    const int kv_lpg = std::max(c.dec_blocks / kv_groups, 1);
     const bool kv_async = kv_overlap_enabled() && c.dec_blocks > 0;
     if (kv_async) {
         if (!h->st2) {
             HIP_TRY(hipStreamCreateWithFlags(&h->st2, hipStreamNonBlocking));
             HIP_TRY(hipEventCreateWithFlags(&h->ev_enc, hipEventDisableTiming));
             HIP_TRY(hipEventCreateWithFlags(&h->ev_kv, hipEventDisableTiming));
+            for (auto& e : h->ev_kvg) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         }
         HIP_TRY(hipEventRecord(h->ev_enc, st));
         HIP_TRY(hipStreamWaitEvent(h->st2, h->ev_enc, 0));
-        HIP_TRY(launch_kv(h->st2));
+        for (int g = 0; g < kv_groups; ++g) {
+            HIP_TRY(launch_kv(h->st2, g * kv_lpg, g == kv_groups - 1 ? c.dec_blocks : (g + 1) * kv_lpg));
+            HIP_TRY(hipEventRecord(h->ev_kvg[g], h->st2));
+        }
         HIP_TRY(hipEventRecord(h->ev_kv, h->st2));
     }
 
@@ -1469,7 +1485,7 @@ int pfm_run(pfm_handle* h, void* stream, int mode, const float* feats, const int
     // compact CIF embeddings [B][T+1][D] -> decoder rows [B][L][D] (acoustic_embeds[:, :L])
     HIP_TRY(hipMemcpy2DAsync(h->Xd.p, (size_t)L * D * 4, h->emb.p, (size_t)Lc * D * 4, (size_t)L * D * 4, B,
                              hipMemcpyDeviceToDevice, st));
-    if (!kv_async) HIP_TRY(launch_kv(st));
+    if (!kv_async) HIP_TRY(launch_kv(st, 0, c.dec_blocks));
     // One utterance group [b0, b0 + nb) of the decoder on rg.st: every buffer is row-addressed (rows b*L + t,
     // memory K|V rows b*T + t), so a group is the same launch sequence over offset pointers.
     auto dec_group = [&](const Run& rg, int b0, int nb) -> int {
@@ -1569,7 +1585,8 @@ int pfm_run(pfm_handle* h, void* stream, int mode, const float* feats, const int
                 e.out = Qd; e.out_map = rowmap_plain(D); e.out_dtype = dt;
                 HIP_TRY(gemmA(Xdn, false, W(Lr.wq), D, D, e));
             }
-            if (l == 0 && kv_async) HIP_TRY(hipStreamWaitEvent(s, h->ev_kv, 0));   // join the side stream
+            if (kv_async && l % kv_lpg == 0 && l / kv_lpg < kv_groups)   // join the side stream (this layer group)
+                HIP_TRY(hipStreamWaitEvent(s, kv_groups > 1 ? h->ev_kvg[l / kv_lpg] : h->ev_kv, 0));
             {
                 const char* kvb = KVg + (size_t)l * 2 * D * esz;
                 if (x3d)
