@@ -12,8 +12,11 @@
 // LFR (apply_lfr, wav_frontend.py:58-74): row i = frames clamp(6i + j - 3, 0, N-1), j = 0..6.
 // CMVN (apply_cmvn, :41-55): (x + shift) * scale.
 //
-// One wave per frame: samples and the window in f32 (as knf), the FFT in f64 in LDS
-// (knf runs Ooura's rdft in double), power / mel sums in f32 in knf's order.
+// One wave per frame: samples, DC mean (sequential f32 sum) and the window in f32 (as knf), the FFT in
+// f64 in LDS (knf runs Ooura's rdft in double; after the f32 rounding of its outputs the two FFTs
+// agree), power / mel sums in f32 in knf's order, the log as f64 rounded to f32. Bit-identical to the
+// compiled knf on >= 99.9 % of log-mel entries (the rest differ by one ulp: glibc's logf is not
+// correctly rounded everywhere).
 #include <math.h>
 
 #include <vector>
@@ -41,7 +44,7 @@ __global__ __launch_bounds__(256) void fbank_kernel(const float* __restrict__ wa
                                                     const int* __restrict__ mlo, const int* __restrict__ mhi,
                                                     float* __restrict__ fb) {
     __shared__ double2 buf[FPB][NFFT];
-    __shared__ float xs[FPB][NFFT];
+    __shared__ __attribute__((aligned(16))) float xs[FPB][NFFT];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const long long gf = (long long)blockIdx.x * FPB + w;     // global frame slot = b * N_cap + f
     const int b = (int)(gf / N_cap), f = (int)(gf % N_cap);
@@ -50,16 +53,19 @@ __global__ __launch_bounds__(256) void fbank_kernel(const float* __restrict__ wa
     float* x = xs[w];
     if (active) {
         const float* src = wav + (long long)b * S_max + (long long)f * FS;
-        // 1. load + scale, mean (f64 reduction; knf sums in f32 sequentially)
-        double s = 0.0;
-        for (int i = lane; i < FL; i += 64) {
-            const float v = src[i] * 32768.0f;
-            x[i] = v;
-            s += v;
-        }
-        s = wave_sum_d(s);
-        const float mean = (float)(s / FL);
+        // 1. load + scale; the DC mean as knf's sequential f32 sum / 400 (feature-window.cc:179-190):
+        //    one lane walks the 400 samples in order (an f64 or tree sum rounds differently)
+        for (int i = lane; i < FL; i += 64) x[i] = src[i] * 32768.0f;
         wave_sync();
+        float s = 0.f;
+        if (lane == 0) {
+#pragma unroll 4
+            for (int i = 0; i < FL; i += 4) {
+                const float4 v = *reinterpret_cast<const float4*>(x + i);
+                s += v.x; s += v.y; s += v.z; s += v.w;
+            }
+        }
+        const float mean = __shfl(s, 0) / (float)FL;
         // 2. DC removal, pre-emphasis (uses the un-emphasised neighbour), window
         float y[7];
 #pragma unroll
@@ -108,7 +114,9 @@ __global__ __launch_bounds__(256) void fbank_kernel(const float* __restrict__ wa
         for (int m = lane; m < NMEL; m += 64) {
             float e = 0.f;
             for (int k = mlo[m]; k <= mhi[m]; ++k) e += melw[m * NBIN + k] * x[k];
-            out[m] = logf(fmaxf(e, 1.1920928955078125e-07f));
+            // log(max(e, FLT_EPSILON)) (feature-fbank.cc:102-108) as the f64 log rounded once: the
+            // correctly rounded logf (ocml's f32 logf is within an ulp, not rounded the same way)
+            out[m] = (float)log((double)fmaxf(e, 1.1920928955078125e-07f));
         }
     }
 }
@@ -203,9 +211,12 @@ int pfm_fbank_frames(int nsamp) {
 void pfm_fbank_tables(float* melw, int* lo, int* hi, float* window, double* tw /*[2*256]*/) {
     const double a = 2.0 * M_PI / (FL - 1);
     for (int i = 0; i < FL; ++i) window[i] = (float)(0.54 - 0.46 * cos(a * (double)i));
+    // knf evaluates MelScale at run time with the C library's logf; a constant-folded logf(20 Hz) /
+    // logf(8 kHz) is correctly rounded instead and moves the triangle edges by an ulp (bins 0, 9-12)
     auto mel = [](float f) { return 1127.0f * logf(1.0f + f / 700.0f); };
     const float fft_bin_width = 16000.0f / NFFT;
-    const float mlow = mel(20.0f), mhigh = mel(8000.0f);
+    volatile float f_low = 20.0f, f_high = 8000.0f;
+    const float mlow = mel(f_low), mhigh = mel(f_high);
     const float delta = (mhigh - mlow) / (NMEL + 1);
     for (int m = 0; m < NMEL; ++m) {
         const float left = mlow + m * delta, center = mlow + (m + 1) * delta, right = mlow + (m + 2) * delta;

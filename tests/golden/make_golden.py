@@ -1058,14 +1058,9 @@ def save_vad_pipeline():
     from funasr.auto.auto_model import AutoModel
     from funasr_amd.config import ct_transformer_tiny, fsmn_vad
     from funasr_amd.weights import vad_test_weights
-    from oracle import fbank_ref
     from tests.golden.inputs import vad_waveform
 
-    def kfbank(w, **kw):
-        return torch.from_numpy(fbank_ref.fbank(w[0].numpy().astype(np.float32) / np.float32(32768.0)))
-
-    sys.modules["torchaudio.compliance.kaldi"].fbank = kfbank
-    wf.kaldi.fbank = kfbank
+    _patch_kaldi_fbank_knf()   # both frontends (the VAD's WavFrontendOnline and the ASR WavFrontend)
     cfg, pcfg, vcfg = paraformer_tiny(), ct_transformer_tiny(), fsmn_vad()
     fconf = dict(fs=16000, window="hamming", n_mels=80, frame_length=25, frame_shift=10, dither=0.0)
     vad_kwargs = dict(model_conf={}, frontend="WavFrontendOnline", frontend_conf=dict(fconf, lfr_m=5, lfr_n=1),
@@ -1098,15 +1093,85 @@ def save_vad_pipeline():
         return r
 
     am.model.cal_decoder_with_predictor = spy
-    for name, bs in (("v1", 300), ("v1_b4", 4)):
+
+    class GpuLikeCpu(str):
+        """device "cpu" that does not compare equal to "cpu": inference_with_vad (auto_model.py:434-435) then keeps
+        the duration-packed batches it builds for a GPU device instead of decoding one segment per call, while
+        torch still runs on the CPU."""
+        def __eq__(self, other):
+            return False if other == "cpu" else str.__eq__(self, other)
+
+        __hash__ = str.__hash__
+
+    for name, bs, batched in (("v1", 300, False), ("v1_b4", 4, False), ("v1_batched", 300, True)):
         gj = VAD_CASES["v1"]
         wav = vad_waveform(gj[0], gj[1], gj[2])
         calls.clear()
+        am.kwargs["device"] = GpuLikeCpu("cpu") if batched else "cpu"
         res = am.generate(input=wav, batch_size_s=bs)   # (a key= kwarg collides inside inference_with_vad)
-        out[name] = dict(batch_size_s=bs, result=[{k: (v.tolist() if hasattr(v, "tolist") else v)
+        out[name] = dict(batch_size_s=bs, batched=batched, result=[{k: (v.tolist() if hasattr(v, "tolist") else v)
                                                    for k, v in r.items()} for r in res], asr_calls=list(calls))
         print(name, out[name]["result"][0]["text"][:80])
     with open(f"{HERE}/vad_pipeline.json", "w", encoding="utf-8") as f:
+        json.dump(out, f, ensure_ascii=False, indent=1)
+
+
+def _patch_kaldi_fbank_knf():
+    """Route the reference WavFrontend's kaldi.fbank to the reference's own kaldi-native-fbank, compiled from its
+    sources by oracle/Makefile (oracle/_ref/knf_fbank): torchaudio is absent here, and knf is the fbank of the
+    reference's C++ runtime. Returns the patched function."""
+    import funasr.frontends.wav_frontend as wf
+    from tests.golden.make_fbank_golden import knf
+
+    def kfbank(w, **kw):
+        return torch.from_numpy(knf(w[0].numpy().astype(np.float32) / np.float32(32768.0)))
+
+    sys.modules["torchaudio.compliance.kaldi"].fbank = kfbank
+    wf.kaldi.fbank = kfbank
+    return kfbank
+
+
+WAV_LARGE_CASES = [("c1", 61, 16000 * 5), ("w3", 62, 16000 * 3 + 517), ("w7", 63, 16000 * 7 + 3001)]
+
+
+def save_automodel_wav_large():
+    """Config C1: Paraformer-large (seeded weights), a single 5 s wav through the reference
+    AutoModel.generate() on the CPU (WavFrontend with CMVN, kaldi.fbank = compiled knf), one call per wav.
+    Records the result dicts and the decoder's per-position argmax / top-2 margins (diagnostics)."""
+    import funasr.tokenizer.char_tokenizer  # noqa: F401
+    from funasr.auto.auto_model import AutoModel
+    from tests.golden.inputs import waveform
+    _patch_kaldi_fbank_knf()
+    cfg = paraformer_large()
+    am = AutoModel(model="Paraformer", model_conf=dict(ctc_weight=0.0, predictor_bias=1),
+                   device="cpu", ncpu=8, disable_update=True, disable_pbar=True, disable_log=True,
+                   tokenizer="CharTokenizer", tokenizer_conf=dict(token_list=token_list(cfg.vocab_size)),
+                   frontend="WavFrontend", frontend_conf=dict(fs=16000, window="hamming", n_mels=80,
+                                                             frame_length=25, frame_shift=10, lfr_m=7,
+                                                             lfr_n=6, dither=0.0, cmvn_file=CMVN),
+                   **cfg.reference_kwargs())
+    am.model.load_state_dict({k: torch.from_numpy(v) for k, v in make_weights(cfg, seed=0).items()}, strict=True)
+    calls = []
+    dec = am.model.cal_decoder_with_predictor
+
+    def spy(*a, **k):
+        r = dec(*a, **k)
+        logp, ntok = r[0].detach(), a[3] if len(a) > 3 else k["pre_token_length"]
+        top2 = torch.topk(logp, 2, dim=-1).values
+        n = int(ntok[0])
+        calls.append(dict(ntok=n, argmax=[int(t) for t in logp[0, :n].argmax(-1)],
+                          margin=[float(x) for x in (top2[0, :n, 0] - top2[0, :n, 1])]))
+        return r
+
+    am.model.cal_decoder_with_predictor = spy
+    out = {}
+    for name, seed, n in WAV_LARGE_CASES:
+        calls.clear()
+        res = am.generate(input=waveform(seed, n), key=[name])
+        out[name] = dict(seed=seed, n=n, result=[{k: (v.tolist() if hasattr(v, "tolist") else v)
+                                                  for k, v in r.items()} for r in res], decoder=calls[0])
+        print(name, len(res[0]["text"]), "min margin", min(calls[0]["margin"] or [0]))
+    with open(f"{HERE}/automodel_wav_large.json", "w", encoding="utf-8") as f:
         json.dump(out, f, ensure_ascii=False, indent=1)
 
 

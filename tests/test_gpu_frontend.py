@@ -15,8 +15,29 @@ from oracle import fbank_ref  # noqa: E402
 from tests.golden.inputs import fbank_input, token_list, waveform  # noqa: E402
 
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
-# log-mel abs tolerance vs knf (f64 FFT, f32 mel sums in knf order); see DESIGN.md
-TOL_LOGMEL = 2e-4
+# pfm_fbank follows knf's float / double boundaries (sequential f32 DC mean, f64 FFT, f32 power and mel
+# sums in knf's order, run-time logf mel table); only the final log differs: the GPU rounds the f64 log
+# once (correctly rounded) where glibc's logf is off by an ulp on ~0.03 % of energies. So: bit-identical
+# on >= 99.9 % of entries, and no entry further than 1e-6 relative (one f32 ulp of a log-mel value).
+MIN_BITEXACT = 0.999
+TOL_REL = 1e-6
+
+
+def _check_close(got, want, what, scale=None):
+    """scale: the CMVN scale row when the features went through (x + shift) * scale -- an ulp of the log-mel x
+    is then judged against |x| * scale, not against the (possibly cancelled) output."""
+    got, want = np.asarray(got, np.float32), np.asarray(want, np.float32)
+    assert got.shape == want.shape, (what, got.shape, want.shape)
+    if got.size == 0:
+        return
+    frac = float((got == want).mean())
+    assert frac >= MIN_BITEXACT, (what, frac)
+    if scale is None:
+        rel = float((np.abs(got - want) / np.maximum(np.abs(want), 1e-3)).max())
+        assert rel <= TOL_REL, (what, rel)
+    else:
+        err = float(np.abs(got - want).max())
+        assert err <= 2 * TOL_REL * 30.0 * float(np.abs(scale).max()), (what, err)
 
 
 @pytest.fixture(scope="module")
@@ -56,8 +77,7 @@ def test_fbank_lfr_cmvn_batch(engine, with_cmvn):
             want = fbank_ref.apply_cmvn(want, cmvn)
         T = want.shape[0]
         assert tout[i] == T, (i, tout[i], T)
-        scale = 1.0 if cmvn is None else float(np.abs(cmvn[1]).max())
-        assert np.abs(feats[i, :T] - want).max() < TOL_LOGMEL * scale, i
+        _check_close(feats[i, :T], want, i, None if cmvn is None else cmvn[1])
         assert np.all(feats[i, T:] == 0)
 
 
@@ -67,7 +87,9 @@ def test_fbank_single_long(engine):
     torch.cuda.synchronize()
     want = fbank_ref.frontend(w)
     assert int(tout[0]) == 500 == want.shape[0]
-    assert np.abs(feats[0].cpu().numpy() - want).max() < TOL_LOGMEL
+    got = feats[0].cpu().numpy()
+    _check_close(got, want, "30 s")
+    assert float((got == want).mean()) >= 0.9999   # the oracle rounds the log the same way
 
 
 def _automodel(**extra):
