@@ -318,12 +318,16 @@ class AutoModel:
         world, rank = 1, 0
         if torch.distributed.is_available() and torch.distributed.is_initialized() and kwargs.get("dp", True):
             world, rank = torch.distributed.get_world_size(), torch.distributed.get_rank()
-        dp = world > 1 and len(items) > 1
+        dp = False
+        if world > 1:   # every rank takes the same branch: the decision is made on rank 0's input count
+            from .distributed import agree_item_count
+            dp = agree_item_count(len(items)) > 1
         mine = list(range(len(items)))
         if dp:   # longest-first round-robin: balanced padded work per rank, decided on rank 0
             from .distributed import shard_items
             mine = shard_items(items, world, rank)
         results = []
+        mats, mat_index = [], []   # greedy token matrices (device) of this rank's batches, for the tensor gather
         speech_s, wall_s = 0.0, 0.0
         for beg in range(0, len(mine), batch_size):
             idx = mine[beg:beg + batch_size]
@@ -336,6 +340,9 @@ class AutoModel:
                 res = model.inference(**batch, **{k: v for k, v in kwargs.items() if k not in ("key",)})
             t2 = time.perf_counter()
             out, meta = (res[0], res[1]) if isinstance(res, (list, tuple)) and len(res) > 1 else (res, {})
+            if dp and "token_matrix" in meta and hasattr(model, "results_from_token_matrix"):
+                mats.append(meta["token_matrix"])
+                mat_index.extend(idx)
             if dp:   # (input index, result) per result; n-best models give several per input (meta "owner")
                 owner = meta.get("owner")
                 if owner is None:
@@ -349,8 +356,21 @@ class AutoModel:
             speech_s += bt if bt > 0 else 0.0
             wall_s += t2 - t1
         self.last_speed = {"rtf": (wall_s / speech_s) if speech_s > 0 else None, "forward_s": wall_s}
-        if dp:   # (input index, result) pairs from every rank -> input order (stable: n-best order kept)
-            from .distributed import gather_results
+        if dp:
+            from .distributed import gather_results, gather_token_matrices
+            # every rank must take the same gather: tensors only when all of them decoded greedy token matrices
+            flag = torch.tensor([1 if len(mats) and len(mat_index) == len(mine) else 0], dtype=torch.int64)
+            if torch.distributed.get_backend() == "nccl":
+                flag = flag.cuda()
+            torch.distributed.all_reduce(flag, op=torch.distributed.ReduceOp.MIN)
+            if int(flag.item()) == 1:   # [n, L] int32 token matrices over RCCL; results built from them on every rank
+                toks, ntok, index = gather_token_matrices(mats, mat_index)
+                if sorted(index.tolist()) != list(range(len(items))):
+                    raise RuntimeError("data-parallel inference: the gathered token matrices do not cover the inputs")
+                order = np.argsort(index, kind="stable")
+                return model.results_from_token_matrix(toks[order], ntok[order], [keys[i] for i in index[order]],
+                                                       **{k: v for k, v in kwargs.items() if k != "key"})
+            # (input index, result) pairs from every rank -> input order (stable: n-best order kept)
             pairs = gather_results(results)
             if any(not 0 <= i < len(items) for i, _ in pairs):
                 raise RuntimeError("data-parallel inference: gathered a result for an unknown input index")

@@ -3,9 +3,13 @@ gloo on CPU for tests).
 
 The Paraformer path has no exchange inside a forward pass: utterances are
 independent. So the only collectives are
-  * one weight broadcast from rank 0 at start-up (`broadcast_state_dict`, one flat fp32
-    buffer — 880 MB for Paraformer-large, a single large RCCL broadcast over xGMI),
-  * (API path only) an all-gather of the per-rank results after a batch (`gather_results`).
+  * one weight broadcast from rank 0 at start-up (`broadcast_state_dict`: one flat fp32 buffer, 880 MB for
+    Paraformer-large, or for fast-mode serving the matrices as bf16 + the vectors as f32, 440 MB; large RCCL
+    broadcasts over xGMI),
+  * (API path only) after the rank's batches, an all-gather of its greedy token matrices as tensors
+    (`gather_token_matrices`: [n, L] int32 ids + counts + input indices, RCCL on the GPU), from which every rank
+    builds the results; result kinds that are not a function of the token matrix (timestamps, n-best, SenseVoice)
+    are all-gathered as Python objects (`gather_results`).
 The timed benchmark step has no collective at all: each rank decodes its own shard.
 The reference's only multi-GPU inference is one process per GPU over a split scp list
 (examples/aishell/paraformer/run.sh:136-170); `shard_range` is that split, in-process.
@@ -65,17 +69,57 @@ def item_lengths(items: Sequence) -> List[int]:
     return out
 
 
+# matrices that fast mode also reads in f32: the decoder FFN's w_2 (its LayerNorm is folded through it in f32,
+# W2g = bf16(W2 diag(gamma)), c2 = W2 beta) and the CIF alpha projection (f32 dot products in cif_alpha_kernel)
+_F32_MATRICES = ("feed_forward.w_2.weight", "predictor.cif_output.weight")
+
+
+def bf16_wire_key(key: str, shape) -> bool:
+    """True for the weights fast mode reads only through their bf16 copies (sent as bf16 by wire="bf16")."""
+    if len(shape) < 2:
+        return False
+    return not (key.startswith("decoder.") and key.endswith(_F32_MATRICES[0])) and key != _F32_MATRICES[1]
+
+
+def _wire_index(layout, dev):
+    """Flat indices of the bf16-wire elements and of the f32 ones."""
+    import torch
+    sizes = [int(np.prod(s)) for _, s, *_ in layout]
+    mat = np.zeros(int(sum(sizes)), dtype=bool)
+    off = 0
+    for (k, s, *_), n in zip(layout, sizes):
+        mat[off:off + n] = bf16_wire_key(k, s)
+        off += n
+    return torch.from_numpy(np.nonzero(mat)[0]).to(dev), torch.from_numpy(np.nonzero(~mat)[0]).to(dev)
+
+
+def bf16_wire_round(flat, layout):
+    """What a receiving rank holds after broadcast_state_dict(wire="bf16"): `flat` (f32, layout order) with the
+    bf16-wire matrices rounded to bf16 (in place; returned)."""
+    import torch
+    mi, _ = _wire_index(layout, flat.device)
+    flat[mi] = flat[mi].to(torch.bfloat16).to(torch.float32)
+    return flat
+
+
 def broadcast_state_dict(layout, sd: Optional[Dict[str, np.ndarray]], device=None, src: int = 0,
-                         keep_on_device: bool = False):
-    """Broadcast a state_dict from `src` as ONE flat fp32 tensor; returns it on every rank.
+                         keep_on_device: bool = False, wire: str = "f32"):
+    """Broadcast a state_dict from `src` in one (f32) or two (bf16 wire) flat collectives; returns it on every rank.
 
     layout: [(key, shape, ...)] in a fixed order known to all ranks (weights.param_layout).
     sd: the dict on `src` (ignored elsewhere). device: torch device of the collective
-    (cuda for RCCL, cpu for gloo). keep_on_device: return the flat tensor itself (for
+    (cuda for RCCL, cpu for gloo). keep_on_device: return the flat f32 tensor itself (for
     PfmEngine.load_flat_device: no device -> host -> device round trip) instead of a host dict.
+    wire: "f32" sends every weight as f32 (880 MB for Paraformer-large); "bf16" sends the matrices fast mode reads
+    only through their bf16 copies (`bf16_wire_key`) as bf16 and the rest as f32 -- about half the bytes. The
+    receiving ranks' matrices are then bf16-rounded, which fast mode does not see (bf16(bf16(w)) = bf16(w): its
+    decode is bit-identical, tests/test_gpu_automodel.py) but EXACT mode would: load them with
+    PfmEngine.load_flat_device(..., fast_only=True).
     """
     import torch
     import torch.distributed as dist
+    if wire not in ("f32", "bf16"):
+        raise ValueError(f"broadcast_state_dict: wire {wire!r} (f32 | bf16)")
     rank = dist.get_rank()
     sizes = [int(np.prod(s)) for _, s, *_ in layout]
     total = int(sum(sizes))
@@ -88,7 +132,16 @@ def broadcast_state_dict(layout, sd: Optional[Dict[str, np.ndarray]], device=Non
             host[off:off + n] = np.asarray(sd[k], dtype=np.float32).reshape(-1)
             off += n
         flat.copy_(torch.from_numpy(host))
-    dist.broadcast(flat, src)
+    if wire == "f32":
+        dist.broadcast(flat, src)
+    else:
+        mi, vi = _wire_index(layout, dev)
+        mb = flat[mi].to(torch.bfloat16) if rank == src else torch.empty(mi.numel(), dtype=torch.bfloat16, device=dev)
+        vf = flat[vi] if rank == src else torch.empty(vi.numel(), dtype=torch.float32, device=dev)
+        dist.broadcast(mb, src)
+        dist.broadcast(vf, src)
+        flat[mi] = mb.to(torch.float32)   # every rank, src included: all hold the same bf16-rounded matrices
+        flat[vi] = vf
     if keep_on_device:
         return flat
     host = flat.cpu().numpy() if dev.type != "cpu" else flat.numpy()
@@ -97,6 +150,75 @@ def broadcast_state_dict(layout, sd: Optional[Dict[str, np.ndarray]], device=Non
         out[k] = host[off:off + n].reshape(s)
         off += n
     return out
+
+
+def agree_item_count(n_items: int) -> int:
+    """The ranks' input counts, all-gathered before any data-parallel collective; every rank raises when they differ
+    (ranks whose views of the inputs differ would otherwise enter different collectives and hang)."""
+    import torch
+    import torch.distributed as dist
+    dev = _coll_device()
+    world = dist.get_world_size()
+    mine = torch.tensor([n_items], dtype=torch.int64, device=dev)
+    allc = torch.empty(world, dtype=torch.int64, device=dev)
+    _all_gather_flat(allc, mine)
+    counts = allc.cpu().tolist()
+    if len(set(counts)) != 1:
+        raise RuntimeError(f"data-parallel inference: the ranks see different input counts {counts}")
+    return counts[0]
+
+
+def _coll_device():
+    import torch
+    import torch.distributed as dist
+    if dist.get_backend() == "nccl":   # RCCL: device tensors over xGMI
+        return torch.device("cuda", torch.cuda.current_device())
+    return torch.device("cpu")
+
+
+def gather_token_matrices(parts, index: Sequence[int]):
+    """All-gather this rank's greedy token matrices as tensors.
+
+    parts: [(tokens [b, L_b] int32 device tensor, ntok [b] int32)] in decode order; index: the input index of every
+    row (len = sum b). Returns host arrays (tokens [N, L] int32 padded with -1, ntok [N], index [N]) of all ranks,
+    rows in rank order. Two collectives: the per-rank (rows, width) pair, then one padded [rows_max, width + 2]
+    int32 block per rank (ids | ntok | input index) with all_gather_into_tensor (RCCL) / all_gather (gloo)."""
+    import torch
+    import torch.distributed as dist
+    dev = _coll_device()
+    world = dist.get_world_size()
+    n = int(sum(int(t.shape[0]) for t, _ in parts))
+    L = max([int(t.shape[1]) for t, _ in parts] + [1])
+    shape = torch.tensor([n, L], dtype=torch.int64, device=dev)
+    shapes = torch.empty(world * 2, dtype=torch.int64, device=dev)
+    _all_gather_flat(shapes, shape)
+    sh = shapes.view(world, 2).cpu().numpy()
+    nmax, Lmax = int(sh[:, 0].max()), int(sh[:, 1].max())
+    blk = torch.full((max(nmax, 1), Lmax + 2), -1, dtype=torch.int32, device=dev)
+    r0 = 0
+    for t, nt in parts:
+        b, lb = int(t.shape[0]), int(t.shape[1])
+        blk[r0:r0 + b, :lb] = t.to(device=dev, dtype=torch.int32)
+        blk[r0:r0 + b, Lmax] = nt.reshape(-1).to(device=dev, dtype=torch.int32)
+        r0 += b
+    if n:
+        blk[:n, Lmax + 1] = torch.as_tensor(np.asarray(index, np.int32), device=dev)
+    allb = torch.empty((world * blk.shape[0], Lmax + 2), dtype=torch.int32, device=dev)
+    _all_gather_flat(allb, blk)
+    allh = allb.view(world, blk.shape[0], Lmax + 2).cpu().numpy()
+    rows = np.concatenate([allh[r, :int(sh[r, 0])] for r in range(world)], 0)
+    return rows[:, :Lmax], rows[:, Lmax], rows[:, Lmax + 1]
+
+
+def _all_gather_flat(out, t):
+    """out = concat of t over ranks (rank order): all_gather_into_tensor where the backend has it."""
+    import torch.distributed as dist
+    if dist.get_backend() == "nccl":
+        dist.all_gather_into_tensor(out, t.contiguous())
+        return
+    world = dist.get_world_size()
+    chunks = list(out.view(world, *t.shape).unbind(0))
+    dist.all_gather(chunks, t.contiguous())
 
 
 def gather_results(local: list) -> list:

@@ -23,6 +23,7 @@ import torch
 from .config import ParaformerConfig
 from .register import tables
 from .runtime import PfmEngine, PfmError
+from .writer import model_writer
 from .text import sentence_postprocess
 from .timestamp import ts_prediction_lfr6_standard
 from .weights import param_layout
@@ -155,6 +156,33 @@ class Paraformer(HipModel):
         self.blank_id, self.sos, self.eos = self.cfg.blank_id, self.cfg.sos, self.cfg.eos
         self._init_common(kwargs)
 
+    def _greedy_hyps(self, toks, ntok):
+        """[B, L_cap] per-position argmax ids + counts -> per utterance a one-entry n-best list of token ids with
+        blank / sos / eos dropped (model.py:541-565)."""
+        hyps = []
+        for i in range(toks.shape[0]):
+            n = int(ntok[i])
+            ids = toks[i, :n].tolist() if n <= toks.shape[1] else []
+            hyps.append([[t for t in ids if t not in (self.eos, self.sos, self.blank_id)]])
+        return hyps
+
+    def results_from_token_matrix(self, toks, ntok, key, tokenizer=None, **kwargs):
+        """Greedy results from a (gathered) host token matrix, exactly as inference() builds them."""
+        hyps = self._greedy_hyps(toks, ntok)
+        key = self._keys(key, len(hyps))
+        out = []
+        for i, hl in enumerate(hyps):
+            ids = hl[0]
+            if tokenizer is None:
+                out.append({"key": key[i], "token_int": ids})
+                continue
+            toks_i = tokenizer.ids2tokens(ids)
+            text = tokenizer.tokens2text(toks_i)
+            if not hasattr(tokenizer, "bpemodel"):
+                text, _ = sentence_postprocess(toks_i)
+            out.append({"key": key[i], "text": text})
+        return out
+
     # ---------------- inference (paraformer/model.py:443-596) ----------------
     @torch.no_grad()
     def inference(self, data_in, data_lengths=None, key: List[str] = None, tokenizer=None, frontend=None,
@@ -188,21 +216,22 @@ class Paraformer(HipModel):
                     for i in range(btok.shape[0])]
         else:
             r = eng.run(speech, lens, mode=mode, want_alphas=pred_ts)
+            if not pred_ts and kwargs.get("output_dir") is None:
+                # greedy text / token_int results are a function of the device token matrix alone: a data-parallel
+                # caller may gather the matrices across ranks as tensors and build the results afterwards
+                meta["token_matrix"] = (r["tokens"], r["ntok"])
             toks = r["tokens"].cpu().numpy()           # one device->host copy for the whole batch
             ntok = r["ntok"].cpu().numpy()
-            hyps = []
-            for i in range(toks.shape[0]):
-                n = int(ntok[i])
-                ids = toks[i, :n].tolist() if n <= toks.shape[1] else []
-                hyps.append([[t for t in ids if t not in (self.eos, self.sos, self.blank_id)]])
+            hyps = self._greedy_hyps(toks, ntok)
         if pred_ts:   # CIF outputs for ts_prediction_lfr6_standard (paraformer/model.py:572-582)
             peaks_h, alphas_h = r["peaks"].cpu(), r["alphas"].cpu()
         b = len(hyps)
         key = self._keys(key, b)
         results = []
         owner = []   # batch index of each result (n-best gives several per utterance, an unfinished search none)
+        writer = model_writer(self, kwargs)   # output_dir: {n}best_recog/{token,text} (model.py:548-552, 588-591)
         for i in range(b):
-            for ids in hyps[i]:   # n-best hypotheses of utterance i, best first (model.py:553)
+            for nb, ids in enumerate(hyps[i]):   # n-best hypotheses of utterance i, best first (model.py:553)
                 owner.append(i)
                 if tokenizer is not None:
                     # model.py:567-586: text = tokens2text(ids2tokens(ids)); sentence_postprocess replaces it
@@ -223,6 +252,9 @@ class Paraformer(HipModel):
                         if not bpe:
                             text, _ = sentence_postprocess(toks_i)
                         results.append({"key": key[i], "text": text})
+                    if writer is not None:
+                        writer[f"{nb + 1}best_recog"]["token"][key[i]] = " ".join(toks_i)
+                        writer[f"{nb + 1}best_recog"]["text"][key[i]] = text
                 else:
                     results.append({"key": key[i], "token_int": ids})
         meta["owner"] = owner

@@ -195,6 +195,7 @@ class PfmEngine:
         self.torch = torch
         self.cfg = cfg
         self.device = int(device)
+        self.fast_only = False   # set by load_flat_device(fast_only=True): bf16-rounded matrices, no EXACT mode
         self.lib = load_library()
         c = PfmConfig.from_config(cfg)
         h = ctypes.c_void_p()
@@ -224,12 +225,14 @@ class PfmEngine:
         if strict and miss:
             raise PfmError(f"{miss} required weights missing after load_state_dict")
 
-    def load_flat_device(self, flat, layout, strict: bool = True) -> None:
+    def load_flat_device(self, flat, layout, strict: bool = True, fast_only: bool = False) -> None:
         """Weights from ONE flat f32 device tensor on this engine's GPU, packed in `layout` order
         ([(key, shape, ...)], weights.param_layout) — e.g. the buffer a data-parallel rank received by
         RCCL broadcast (distributed.broadcast_state_dict(keep_on_device=True)). pfm_set_weight_device per
-        key: device-to-device copies, nothing round-trips through the host."""
+        key: device-to-device copies, nothing round-trips through the host. fast_only: the matrices were sent as
+        bf16 (broadcast_state_dict(wire="bf16")), so EXACT mode is refused on this engine."""
         torch = self.torch
+        self.fast_only = bool(fast_only)
         if flat.device.type != "cuda" or flat.device.index != self.device or flat.dtype != torch.float32:
             raise PfmError(f"load_flat_device: need an f32 tensor on cuda:{self.device}, got {flat.dtype} on {flat.device}")
         flat = flat.contiguous()
@@ -266,6 +269,13 @@ class PfmEngine:
                                         ctypes.byref(n)), "pfm_profile_read")
         return dict(ms=ms.value, flops=fl.value, bytes=by.value, launches=n.value)
 
+    def _mode(self, mode) -> int:
+        m = MODES[mode] if isinstance(mode, str) else int(mode)
+        if m == MODE_EXACT and self.fast_only:
+            raise PfmError("EXACT mode needs the f32 weights; this engine holds bf16-rounded matrices "
+                           "(broadcast_state_dict(wire='bf16') -> load_flat_device(fast_only=True))")
+        return m
+
     # ---- inference
     def run(self, feats, lens, mode="exact", L_cap: Optional[int] = None, want_enc=False, want_alphas=False):
         """feats [B,T,in] f32 cuda, lens [B] int32 cuda -> dict of cuda tensors."""
@@ -285,7 +295,7 @@ class PfmEngine:
         enc = torch.empty((B, T, self.cfg.d_model), dtype=torch.float32, device=dev) if want_enc else None
         alphas = torch.empty((B, T + 1), dtype=torch.float32, device=dev) if want_alphas else None
         peaks = torch.empty((B, T + 1), dtype=torch.float32, device=dev) if want_alphas else None
-        m = MODES[mode] if isinstance(mode, str) else int(mode)
+        m = self._mode(mode)
         check(self.lib.pfm_run(self.h, _stream_ptr(torch, dev), m, _ptr(feats), _ptr(lens), B, T, _ptr(tokens),
                                L_cap, _ptr(ntok), _ptr(enc), _ptr(alphas), _ptr(peaks)), "pfm_run")
         return dict(tokens=tokens, ntok=ntok, enc=enc, alphas=alphas, peaks=peaks)
@@ -308,7 +318,7 @@ class PfmEngine:
         scores = torch.empty((B, nbest), dtype=torch.float32, device=dev)
         alphas = torch.empty((B, T + 1), dtype=torch.float32, device=dev) if want_alphas else None
         peaks = torch.empty((B, T + 1), dtype=torch.float32, device=dev) if want_alphas else None
-        m = MODES[mode] if isinstance(mode, str) else int(mode)
+        m = self._mode(mode)
         c = self.cfg
         check(self.lib.pfm_run_beam(self.h, _stream_ptr(torch, dev), m, _ptr(feats), _ptr(lens), B, T, int(beam),
                                     float(ctc_weight), float(penalty), int(nbest), 1 if end_detect else 0,
@@ -332,7 +342,7 @@ class PfmEngine:
             raise PfmError("lens must have one entry per sequence")
         punc = torch.empty((B, T), dtype=torch.int32, device=dev)
         logits = torch.empty((B, T, self.cfg.n_punc), dtype=torch.float32, device=dev) if want_logits else None
-        m = MODES[mode] if isinstance(mode, str) else int(mode)
+        m = self._mode(mode)
         check(self.lib.pfm_run_punc(self.h, _stream_ptr(torch, dev), m, _ptr(ids), _ptr(lens), B, T, _ptr(punc),
                                     _ptr(logits)), "pfm_run_punc")
         return dict(punc=punc, logits=logits)
@@ -362,7 +372,7 @@ class PfmEngine:
         enc = torch.empty((B, T + 4, self.cfg.d_model), dtype=torch.float32, device=dev) if want_enc else None
         frames = torch.empty((B, T + 4), dtype=torch.int32, device=dev) if want_frames else None
         qa = (ctypes.c_int32 * 4)(*q)
-        m = MODES[mode] if isinstance(mode, str) else int(mode)
+        m = self._mode(mode)
         check(self.lib.pfm_run_ctc(self.h, _stream_ptr(torch, dev), m, _ptr(feats), _ptr(lens), B, T, qa,
                                    int(ban_token), _ptr(tokens), L_cap, _ptr(ntok), _ptr(enc), _ptr(frames)),
               "pfm_run_ctc")

@@ -27,6 +27,7 @@ import torch
 from .config import SenseVoiceConfig
 from .model import HipModel
 from .register import tables
+from .writer import model_writer
 
 
 @tables.register("model_classes", "SenseVoiceSmall")
@@ -76,12 +77,15 @@ class SenseVoiceSmall(HipModel):
             align = eng.ctc_align(r["enc"], olens, [ids[4:] for ids in ids_all], self.blank_id).cpu().numpy()
             nfr = (olens - 4).cpu().numpy()
         results = []
+        writer = model_writer(self, kwargs)   # output_dir: 1best_recog/text (sense_voice/model.py:899-915)
         for i in range(b):
             ids = ids_all[i]
             if tokenizer is None:
                 results.append({"key": key[i], "token_int": ids})
                 continue
             text = tokenizer.decode(ids)
+            if writer is not None:
+                writer["1best_recog"]["text"][key[i]] = text
             res = {"key": key[i], "text": text}
             if want_ts:
                 n = int(nfr[i])

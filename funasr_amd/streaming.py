@@ -32,6 +32,7 @@ from .model import HipModel
 from .register import tables
 from .runtime import PfmError, PfmStreams
 from .text import sentence_postprocess
+from .writer import model_writer
 
 CHUNK_SAMPLES_PER_FRAME = 960   # model.py:582: chunk_size[1] * 960 samples (60 ms per LFR frame)
 
@@ -229,4 +230,8 @@ class ParaformerStreaming(HipModel):
         if tokenizer is None:
             return [{"key": key[0], "token_int": tokens}], {}
         text, _ = sentence_postprocess(tokens)
+        if kwargs.get("output_dir"):   # paraformer_streaming/model.py:649-654
+            writer = model_writer(self, kwargs)
+            writer["1best_recog"]["token"][key[0]] = " ".join(tokens)
+            writer["1best_recog"]["text"][key[0]] = text
         return [{"key": key[0], "text": text}], {}

@@ -24,6 +24,7 @@ from .config import FsmnVADConfig
 from .frontend import WavFrontendOnline
 from .model import HipModel
 from .register import tables
+from .writer import model_writer
 
 # VadStateMachine / FrameState / AudioChangeState (model.py:22-41)
 START_NOT_DETECTED, IN_SPEECH, END_DETECTED = 1, 2, 3
@@ -391,4 +392,7 @@ class FsmnVADStreaming(HipModel):
         if is_final:
             self.init_cache(cache, **kwargs)
         key = self._keys(key, 1)
+        writer = model_writer(self, kwargs)   # output_dir: 1best_recog/text (fsmn_vad_streaming/model.py:730-744)
+        if writer is not None:
+            writer["1best_recog"]["text"][key[0]] = segments
         return [{"key": key[0], "value": segments}], {}

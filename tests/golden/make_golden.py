@@ -1175,6 +1175,73 @@ def save_automodel_wav_large():
         json.dump(out, f, ensure_ascii=False, indent=1)
 
 
+def _read_tree(root):
+    out = {}
+    for dp, _, fns in os.walk(root):
+        for fn in fns:
+            full = os.path.join(dp, fn)
+            with open(full, encoding="utf-8") as f:
+                out[os.path.relpath(full, root)] = f.read()
+    return out
+
+
+def save_output_dir():
+    """generate(..., output_dir=d) result files (funasr/utils/datadir_writer.py, paraformer/model.py:548-591,
+    sense_voice/model.py:899-915): Paraformer tiny greedy over two generate() calls (the writer is created once per
+    model, so the second call appends), Paraformer tiny + CTC head with the joint beam search and nbest=2
+    ({1,2}best_recog), SenseVoice tiny (1best_recog/text, the un-postprocessed decode)."""
+    import dataclasses
+    import tempfile
+    import funasr.tokenizer.char_tokenizer  # noqa: F401
+    import funasr.tokenizer.sentencepiece_tokenizer  # noqa: F401
+    import funasr.models.sense_voice.model  # noqa: F401
+    import funasr.frontends.wav_frontend  # noqa: F401
+    from funasr.auto.auto_model import AutoModel
+    from funasr_amd.config import sense_voice_tiny
+    front = dict(fs=16000, window="hamming", n_mels=80, frame_length=25, frame_shift=10, lfr_m=7, lfr_n=6,
+                 dither=0.0, cmvn_file=CMVN)
+    common = dict(device="cpu", ncpu=4, disable_update=True, disable_pbar=True, disable_log=True,
+                  frontend="WavFrontend", frontend_conf=front)
+    out = {}
+    feats, lens = fbank_input(seed=11, B=2, T=40, lens=[40, 27])
+    x, ln = torch.from_numpy(feats), torch.from_numpy(lens.astype(np.int32))
+    # (1) greedy, two calls
+    cfg = paraformer_tiny()
+    am = AutoModel(model="Paraformer", model_conf=dict(ctc_weight=0.0, predictor_bias=1), tokenizer="CharTokenizer",
+                   tokenizer_conf=dict(token_list=token_list(cfg.vocab_size)), **common, **cfg.reference_kwargs())
+    am.model.load_state_dict({k: torch.from_numpy(v) for k, v in make_weights(cfg, seed=0).items()}, strict=True)
+    with tempfile.TemporaryDirectory() as d:
+        am.generate(input=x, input_len=ln[:, None], data_type="fbank", key=["uttA", "uttB"], output_dir=d)
+        am.generate(input=x[1:, :27], input_len=ln[1:, None], data_type="fbank", key=["uttC"], output_dir=d)
+        am.model.writer.close()
+        out["greedy"] = _read_tree(d)
+    # (2) joint decoder + CTC prefix beam, nbest 2
+    cfg = dataclasses.replace(paraformer_tiny(), ctc_weight=0.3)
+    am = AutoModel(model="Paraformer", model_conf=dict(ctc_weight=0.3, predictor_bias=1), tokenizer="CharTokenizer",
+                   tokenizer_conf=dict(token_list=token_list(cfg.vocab_size)), **common, **cfg.reference_kwargs())
+    am.model.load_state_dict({k: torch.from_numpy(v) for k, v in make_weights(cfg, seed=4).items()}, strict=True)
+    with tempfile.TemporaryDirectory() as d:
+        res = am.generate(input=x, input_len=ln[:, None], data_type="fbank", key=["uttA", "uttB"], output_dir=d,
+                          decoding_ctc_weight=0.3, beam_size=3, nbest=2)
+        am.model.writer.close()
+        out["beam"] = _read_tree(d)
+        out["beam_results"] = [{k: v for k, v in r.items()} for r in res]
+    # (3) SenseVoice
+    bpe = f"{HERE}/sv_bpe.model"
+    cfg = sense_voice_tiny(vocab_size=300)
+    kw = cfg.reference_kwargs()
+    am = AutoModel(model="SenseVoiceSmall", model_conf={}, tokenizer="SentencepiecesTokenizer",
+                   tokenizer_conf=dict(bpemodel=bpe), encoder=kw["encoder"], encoder_conf=kw["encoder_conf"], **common)
+    am.model.load_state_dict({k: torch.from_numpy(v) for k, v in make_weights(cfg, seed=0).items()}, strict=True)
+    with tempfile.TemporaryDirectory() as d:
+        am.generate(input=x, input_len=ln, data_type="fbank", key=["uttA", "uttB"], batch_size=2, output_dir=d)
+        am.model.writer.close()
+        out["sensevoice"] = _read_tree(d)
+    with open(f"{HERE}/output_dir.json", "w", encoding="utf-8") as f:
+        json.dump(out, f, ensure_ascii=False, indent=1)
+    print({k: sorted(v) if isinstance(v, dict) else len(v) for k, v in out.items()})
+
+
 if __name__ == "__main__" and len(sys.argv) > 1:
     torch.manual_seed(0)
     for part in sys.argv[1:]:

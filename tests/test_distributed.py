@@ -48,11 +48,12 @@ def _worker(rank, world, port, q):
             rng = np.random.default_rng(0)
             sd = {k: rng.standard_normal(s).astype(np.float32) for k, s, _ in layout}
         got = broadcast_state_dict(layout, sd)
+        got16 = broadcast_state_dict(layout, sd, wire="bf16")
         items = list(range(11))
         lo, hi = shard_range(len(items), world, rank)
         local = [{"key": f"u{i}", "rank": rank} for i in items[lo:hi]]
         allres = gather_results(local)
-        q.put((rank, {k: v.tolist() for k, v in got.items()}, allres))
+        q.put((rank, {k: v.tolist() for k, v in got.items()}, allres, {k: v.tolist() for k, v in got16.items()}))
     finally:
         dist.destroy_process_group()
 
@@ -72,8 +73,12 @@ def test_gloo_world2_broadcast_and_gather():
     rng = np.random.default_rng(0)
     want = {k: rng.standard_normal(s).astype(np.float32).tolist() for k, s in
             [("a.weight", (3, 4)), ("b.bias", (5,)), ("c", (2, 2, 2))]}
-    for rank, sd, allres in out:
+    # bf16 wire: matrices (rank >= 2) arrive bf16-rounded, vectors exact (and "c" is a 3-D matrix)
+    want16 = {k: (torch.tensor(v).to(torch.bfloat16).float().tolist() if k != "b.bias" else v)
+              for k, v in want.items()}
+    for rank, sd, allres, sd16 in out:
         assert sd == want
+        assert sd16 == want16
         assert [r["key"] for r in allres] == [f"u{i}" for i in range(11)]
         assert [r["rank"] for r in allres] == [0] * 6 + [1] * 5
 
@@ -186,3 +191,75 @@ def test_gloo_world2_automodel_nbest_grouped_by_input():
     for rank, shard, res in out:
         assert shard == plan[rank]
         assert [{k: v for k, v in r.items() if k not in ("rank", "key")} for r in res] == want
+
+
+class _TokenModel(_EchoModel):
+    """A greedy model: per input a row of token ids (position p of input with n samples -> (n + 7 p) % 97, with
+    the specials 0 / 1 / 2 among them), count = n % 13; results built from the token matrix like
+    Paraformer.results_from_token_matrix, and the matrix returned in meta["token_matrix"]."""
+    L = 16
+
+    def _mat(self, data_in):
+        b = len(data_in)
+        t = torch.full((b, self.L), -1, dtype=torch.int32)
+        nt = torch.zeros(b, dtype=torch.int32)
+        for i, x in enumerate(data_in):
+            n = len(x)
+            nt[i] = n % 13
+            t[i, :] = torch.tensor([(n + 7 * p) % 97 for p in range(self.L)], dtype=torch.int32)
+        return t, nt
+
+    def results_from_token_matrix(self, toks, ntok, key, tokenizer=None, **kw):
+        return [{"key": key[i], "ids": [int(v) for v in toks[i, :int(ntok[i])] if v not in (0, 1, 2)]}
+                for i in range(len(ntok))]
+
+    def inference(self, data_in, key=None, **kw):
+        t, nt = self._mat(data_in)
+        return self.results_from_token_matrix(t.numpy(), nt.numpy(), key), {"token_matrix": (t, nt)}
+
+
+def _token_worker(rank, world, port, items, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from funasr_amd.auto_model import AutoModel
+        am = AutoModel.__new__(AutoModel)
+        am.kwargs, am.model = {"batch_size": 2}, _TokenModel()
+        called = []
+        import funasr_amd.distributed as D
+        orig = D.gather_results
+        D.gather_results = lambda local: called.append(1) or orig(local)
+        res = am.inference(items, key=[f"k{i}" for i in range(len(items))])
+        err = None
+        try:   # rank 1 sees one input fewer: every rank must raise instead of entering different collectives
+            am.inference(items if rank == 0 else items[:-1], key=None)
+        except RuntimeError as e:
+            err = str(e)
+        q.put((rank, res, len(called), err))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world2_token_matrix_tensor_gather():
+    """Greedy results under world 2 come from the token matrices gathered as int32 tensors (no pickled result
+    objects) and equal the one-process run in input order; mismatched input counts raise on every rank."""
+    from funasr_amd.auto_model import AutoModel
+    lens = [500, 83, 17, 431, 500, 120, 300, 222, 260]
+    items = [np.zeros(n, np.float32) for n in lens]
+    single = AutoModel.__new__(AutoModel)
+    single.kwargs, single.model = {"batch_size": 2}, _TokenModel()
+    want = single.inference(items, key=[f"k{i}" for i in range(len(items))])
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_token_worker, args=(r, world, port, items, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, res, n_obj_gathers, err in out:
+        assert res == want
+        assert n_obj_gathers == 0
+        assert err is not None and "different input counts" in err

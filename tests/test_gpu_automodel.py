@@ -224,3 +224,34 @@ def test_load_flat_device_matches_host_load():
         assert torch.equal(ra[k], rb[k]), k
     with pytest.raises(Exception):
         b.load_flat_device(flat[:100], lay)
+
+
+@pytest.mark.parametrize("large", [False, True])
+def test_bf16_wire_weights_fast_mode_bit_identical(large):
+    """broadcast_state_dict(wire="bf16") (the fast-mode data-parallel broadcast: 477 instead of 880 MB for
+    Paraformer-large) leaves every rank bf16-rounded matrices; fast mode reads those only through bf16 copies (or,
+    for the decoder w_2 / CIF projection, receives them in f32), so its decode is bit-identical to the f32-loaded
+    engine's; EXACT mode is refused on such an engine."""
+    from funasr_amd.config import paraformer_large
+    from funasr_amd.distributed import bf16_wire_round
+    from funasr_amd.runtime import PfmEngine, PfmError
+    from funasr_amd.weights import make_weights, param_layout
+    from tests.golden.inputs import fbank_input
+    cfg = paraformer_large() if large else paraformer_tiny()
+    sd = make_weights(cfg, 5)
+    a = PfmEngine(cfg, 0)
+    a.load_state_dict(sd)
+    lay = param_layout(cfg)
+    flat = torch.cat([torch.from_numpy(np.ascontiguousarray(sd[k], np.float32)).reshape(-1) for k, *_ in lay]).cuda()
+    b = PfmEngine(cfg, 0)
+    b.load_flat_device(bf16_wire_round(flat, lay), lay, fast_only=True)
+    B, T = (24, 500) if large else (3, 60)
+    feats, lens = fbank_input(seed=12, B=B, T=T, lens=[T - 7 * i for i in range(B)])
+    x, ln = torch.from_numpy(feats).cuda(), torch.from_numpy(lens).cuda()
+    ra = a.run(x, ln, mode="fast", want_enc=True, want_alphas=True)
+    rb = b.run(x, ln, mode="fast", want_enc=True, want_alphas=True)
+    torch.cuda.synchronize()
+    for k in ("tokens", "ntok", "enc", "alphas"):
+        assert torch.equal(ra[k], rb[k]), k
+    with pytest.raises(PfmError):
+        b.run(x, ln, mode="exact")

@@ -223,3 +223,23 @@ def test_sentencepiece_tokenizer_and_build_tokenizer():
     tok2, v2 = build_tokenizer("CharTokenizer", dict(token_list=["<blank>", "<s>", "</s>", "a", "<unk>"]))
     assert isinstance(tok2, CharTokenizer) and v2 == 5
     assert build_tokenizer(None, {}) == (None, -1)
+
+
+def test_datadir_writer_semantics(tmp_path):
+    """funasr_amd.writer.DatadirWriter behaves as funasr/utils/datadir_writer.py: nested dirs created on first write,
+    "key value" lines flushed at once, a duplicated key warns, a file writer refuses children."""
+    import warnings
+    from funasr_amd.writer import DatadirWriter
+    w = DatadirWriter(tmp_path / "out")
+    w["1best_recog"]["text"]["a"] = "x y"
+    assert (tmp_path / "out" / "1best_recog" / "text").read_text(encoding="utf-8") == "a x y\n"
+    with warnings.catch_warnings(record=True) as rec:
+        warnings.simplefilter("always")
+        w["1best_recog"]["text"]["a"] = "z"
+    assert any("Duplicated" in str(r.message) for r in rec)
+    with pytest.raises(RuntimeError):
+        w["1best_recog"]["text"]["sub"]
+    with pytest.raises(RuntimeError):
+        w["1best_recog"]["k"] = "v"
+    w.close()
+    assert (tmp_path / "out" / "1best_recog" / "text").read_text(encoding="utf-8") == "a x y\na z\n"
