@@ -18,6 +18,8 @@
 //
 // All arithmetic is f32 like the reference (numpy float32 state arrays, torch f32 scores); logaddexp follows
 // numpy's float32 npy_logaddexpf (equal operands -> x + ln 2, else max + log1p(exp(-|d|))).
+#include <cstdlib>
+
 #include "pfm_common.h"
 
 #include <hip/hip_runtime.h>
@@ -139,6 +141,7 @@ struct BeamArgs {
     int* olen;           // [B][nbest] token count of each n-best hypothesis, -1 = none
     float* oscore;       // [B][nbest]
     int B, G, Gr;        // utterances; workgroups per utterance (Gr pair workgroups, then the log-psi ones)
+    unsigned spin_cap;   // arrival-barrier wait bound (s_sleep rounds); past it the search fails (fail word set)
 };
 
 // Workgroups of one search (BeamSearchPara of one utterance). The prefix recurrences of position i are three
@@ -417,7 +420,7 @@ __global__ __launch_bounds__(NT) void ctc_beam_kernel(BeamArgs a) {
             unsigned spins = 0;
             while (__hip_atomic_load(sync, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
                 __builtin_amdgcn_s_sleep(2);
-                if (++spins > (1u << 24)) { atomicExch(sync + 1, 1u); stop = 1; break; }   // never expected
+                if (++spins > a.spin_cap) { atomicExch(sync + 1, 1u); stop = 1; break; }   // never expected
             }
             __threadfence();
         }
@@ -703,10 +706,27 @@ long long pfm_ctc_beam_iscratch(int K, int nbest, int L, int P, int V) {
     return 2 + 2LL * L * K + S + groups(K, P) * (S + 1) + (long long)L * P;
 }
 
+// OR of the utterances' fail words (a search whose arrival barrier timed out) into one device word
+__global__ __launch_bounds__(256) void beam_fail_kernel(const int* __restrict__ is, long long istride, int B,
+                                                        unsigned* __restrict__ fail) {
+    __shared__ int any;
+    if (threadIdx.x == 0) any = 0;
+    __syncthreads();
+    int f = 0;
+    for (int b = threadIdx.x; b < B; b += blockDim.x) f |= is[(long long)b * istride + 1];
+    if (f) atomicOr(&any, 1);
+    __syncthreads();
+    if (threadIdx.x == 0) fail[0] = any ? 1u : 0u;
+}
+
 hipError_t pfm_ctc_beam(const float* am, int L, const float* x, int T, const int* lens, const int* ntok, int B, int V,
                         int K, int P, int nbest, float wctc, float pen, int use_pen, int end_detect, int sos, int eos,
                         int blank, float* fs, int* is, int* tokens, int Lcap, int* olen, float* oscore,
-                        hipStream_t st) {
+                        unsigned* fail, hipStream_t st) {
+    if (fail) {
+        const hipError_t e0 = hipMemsetAsync(fail, 0, sizeof(unsigned), st);
+        if (e0 != hipSuccess) return e0;
+    }
     if (B <= 0) return hipSuccess;
     if (K < 1 || K > MAXK || P < 1 || P > MAXP || P > V || nbest < 1 || nbest > MAXN || Lcap < 0)
         return hipErrorInvalidValue;
@@ -717,6 +737,10 @@ hipError_t pfm_ctc_beam(const float* am, int L, const float* x, int T, const int
     a.istride = pfm_ctc_beam_iscratch(K, nbest, L, P, V); a.Lcap = Lcap;
     a.Gr = pair_wgs(K, P);
     a.G = groups(K, P);
+    {   // PFM_BEAM_SPIN_CAP: a small bound forces the timeout path (tests/test_gpu_beam.py); default 2^24 rounds
+        const char* sc = getenv("PFM_BEAM_SPIN_CAP");
+        a.spin_cap = (sc && sc[0]) ? (unsigned)strtoul(sc, nullptr, 10) : (1u << 24);
+    }
     hipError_t e;
     if (T > 0) {   // the CTC log-probs, frame-contiguous per id, at the head of each utterance's float scratch
         hipLaunchKernelGGL(transpose_tv_kernel, dim3((V + 63) / 64, (T + 63) / 64, B), dim3(256), 0, st, x, T, V, fs,
@@ -764,6 +788,10 @@ hipError_t pfm_ctc_beam(const float* am, int L, const float* x, int T, const int
         const dim3 grid((unsigned)(((nb + 7) / 8) * 8 * a.G));
         e = hipLaunchCooperativeKernel((const void*)ctc_beam_kernel, grid, dim3(NT), args, 0u, st);
         if (e != hipSuccess) return e;
+    }
+    if (fail) {
+        hipLaunchKernelGGL(beam_fail_kernel, dim3(1), dim3(256), 0, st, is, a.istride, B, fail);
+        PFM_LAUNCH_CHECK();
     }
     return hipSuccess;
 }

@@ -69,7 +69,7 @@ long long pfm_ctc_beam_iscratch(int K, int nbest, int L, int P, int V);
 hipError_t pfm_ctc_beam(const float* am, int L, const float* x, int T, const int* lens, const int* ntok, int B, int V,
                         int K, int P, int nbest, float wctc, float pen, int use_pen, int end_detect, int sos, int eos,
                         int blank, float* fs, int* is, int* tokens, int Lcap, int* olen, float* oscore,
-                        hipStream_t st);
+                        unsigned* fail, hipStream_t st);
 size_t pfm_ffn_packed_elems();
 hipError_t pfm_emis_stats(const float* logits, long long rows, int V, float* mx, float* inv, int* amax, hipStream_t st);
 hipError_t pfm_ctc_align_run(const float* logits, const float* mx, const float* inv, const int* amax, int B, int Tf,
@@ -150,6 +150,16 @@ static thread_local std::string g_err;
 static int fail(int code, const std::string& msg) {
     g_err = msg;
     return code;
+}
+
+// after a synchronised pfm_ctc_beam: the device fail word -> PFM_E_DEVICE (a search whose workgroups lost each other
+// at the per-position arrival barrier returns no hypotheses, which must not pass for "search found none")
+static int beam_failed(const unsigned* fail_dev, const char* who) {
+    unsigned f = 0;
+    if (hipMemcpy(&f, fail_dev, sizeof(f), hipMemcpyDeviceToHost) != hipSuccess)
+        return fail(PFM_E_HIP, std::string(who) + ": reading the search's fail word");
+    return f ? fail(PFM_E_DEVICE, std::string(who) + ": the beam search's cross-workgroup barrier timed out")
+             : PFM_OK;
 }
 // the host-only translation units (vad_detector.hip) report errors through the same thread-local string
 int pfm_fail(int code, const char* msg) { return fail(code, msg); }
@@ -264,6 +274,7 @@ struct pfm_handle {
     DevBuf ffn_pack;               // fused-FFN weight tiles of every encoder layer (bf16, LDS-image order)
     bool ffn_ready = false;
     DevBuf logits, ctcx, beam_fs, beam_is;   // pfm_run_beam: decoder / CTC log-probs and the search's scratch
+    DevBuf beam_fail;                        // one device word: a search's cross-workgroup barrier timed out
     DevBuf beam_nf;                          // pfm_stream_step_beam: CIF fire counts when the caller passes none
     bool want_logits = false;      // set by pfm_run_beam around its pfm_run: the output layer writes logits
     int last_L = 0;                // decoder positions of the last pfm_run (max token count)
@@ -1724,11 +1735,13 @@ int pfm_run_beam(pfm_handle* h, void* stream, int mode, const float* feats, cons
     HIP_TRY(hipMemcpyAsync(ntk, ntok_dev, (size_t)B * sizeof(int32_t), hipMemcpyDeviceToDevice, st));
     HIP_TRY(hipStreamSynchronize(st));
     HIP_TRY(h->beam_is.ensure((size_t)B * isz * sizeof(int32_t)));
+    HIP_TRY(h->beam_fail.ensure(sizeof(unsigned)));
     HIP_TRY(pfm_ctc_beam(h->logits.as<float>(), L, h->ctcx.as<float>(), T, lens, ntk, B, V, beam, P, nbest,
                          ctc_weight, penalty, penalty != 0.f ? 1 : 0, end_detect, sos, eos, blank,
-                         h->beam_fs.as<float>(), h->beam_is.as<int>(), tokens, L_cap, ntok_out, scores_out, st));
+                         h->beam_fs.as<float>(), h->beam_is.as<int>(), tokens, L_cap, ntok_out, scores_out,
+                         h->beam_fail.as<unsigned>(), st));
     HIP_TRY(hipStreamSynchronize(st));
-    return PFM_OK;
+    return beam_failed(h->beam_fail.as<unsigned>(), "pfm_run_beam");
 }
 
 int pfm_run_ctc(pfm_handle* h, void* stream, int mode, const float* feats, const int32_t* lens, int B, int T,
@@ -2206,10 +2219,12 @@ int pfm_op_ctc_beam(void* stream, const float* am, int L, const float* x, int T,
     int* is;
     HIP_TRY(sc.alloc(&fs, (size_t)B * pfm_ctc_beam_fscratch(beam, P, T, L, V)));
     HIP_TRY(sc.alloc(&is, (size_t)B * pfm_ctc_beam_iscratch(beam, nbest, L, P, V)));
+    unsigned* fw;
+    HIP_TRY(sc.alloc(&fw, 1));
     HIP_TRY(pfm_ctc_beam(am, L, x, T, lens, ntok, B, V, beam, P, nbest, ctc_weight, penalty, penalty != 0.f ? 1 : 0,
-                         end_detect, sos, eos, blank, fs, is, tokens, L_cap, ntok_out, scores_out, st));
+                         end_detect, sos, eos, blank, fs, is, tokens, L_cap, ntok_out, scores_out, fw, st));
     HIP_TRY(hipStreamSynchronize(st));
-    return PFM_OK;
+    return beam_failed(fw, "pfm_op_ctc_beam");
 }
 
 }  // extern "C"
@@ -2593,6 +2608,11 @@ int stream_step(pfm_streams* s, void* stream, int n, const int32_t* slot_ids, co
     const bool fast = s->mode == PFM_MODE_FAST;
     const int D = c.d_model, I = c.input_size, C0 = s->C0;
     const int Tw = C0 + maxn;
+    // the beam path writes whole hypotheses: check L_cap against the worst-case fire count (one per window row,
+    // plus the final chunk's tail fire) before any stream state moves, so a refused step can be retried
+    if (sb && L_cap < Tw + 1)
+        return fail(PFM_E_ARG, "pfm_stream_step_beam: L_cap " + std::to_string(L_cap) + " below the window's " +
+                                   std::to_string(Tw + 1) + " possible tokens");
     int rc = reserve(h, n, Tw + 2);
     if (rc) return rc;
     if (fast) { rc = ensure_bf16(h, st); if (rc) return rc; }
@@ -2755,12 +2775,13 @@ int stream_step(pfm_streams* s, void* stream, int n, const int32_t* slot_ids, co
         const long long isz = pfm_ctc_beam_iscratch(sb->beam, sb->nbest, L, sb->P, V);
         HIP_TRY(h->beam_fs.ensure((size_t)n * fsz * sizeof(float)));
         HIP_TRY(h->beam_is.ensure((size_t)n * isz * sizeof(int32_t)));
+        HIP_TRY(h->beam_fail.ensure(sizeof(unsigned)));
         HIP_TRY(pfm_ctc_beam(h->logits.as<float>(), L, h->ctcx.as<float>(), Tw, tw_d, ntok, n, V, sb->beam, sb->P,
                              sb->nbest, sb->ctc_weight, sb->penalty, sb->penalty != 0.f ? 1 : 0, sb->end_detect, sb->sos,
                              sb->eos, sb->blank, h->beam_fs.as<float>(), h->beam_is.as<int>(), tokens, L_cap,
-                             sb->ntok_hyp, sb->scores, st));
+                             sb->ntok_hyp, sb->scores, h->beam_fail.as<unsigned>(), st));
         HIP_TRY(hipStreamSynchronize(st));
-        return PFM_OK;
+        return beam_failed(h->beam_fail.as<unsigned>(), "pfm_stream_step_beam");
     }
     // ---- phase B: ParaformerSANMDecoder.forward_chunk (decoder.py:461-528) + greedy argmax, tokens into
     // the step's token buffer

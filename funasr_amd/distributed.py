@@ -4,7 +4,7 @@ gloo on CPU for tests).
 The Paraformer path has no exchange inside a forward pass: utterances are
 independent. So the only collectives are
   * one weight broadcast from rank 0 at start-up (`broadcast_state_dict`: one flat fp32 buffer, 880 MB for
-    Paraformer-large, or for fast-mode serving the matrices as bf16 + the vectors as f32, 440 MB; large RCCL
+    Paraformer-large, or for fast-mode serving the bf16-only matrices as bf16 and the rest as f32, 486 MB; large RCCL
     broadcasts over xGMI),
   * (API path only) after the rank's batches, an all-gather of its greedy token matrices as tensors
     (`gather_token_matrices`: [n, L] int32 ids + counts + input indices, RCCL on the GPU), from which every rank
@@ -69,16 +69,20 @@ def item_lengths(items: Sequence) -> List[int]:
     return out
 
 
-# matrices that fast mode also reads in f32: the decoder FFN's w_2 (its LayerNorm is folded through it in f32,
-# W2g = bf16(W2 diag(gamma)), c2 = W2 beta) and the CIF alpha projection (f32 dot products in cif_alpha_kernel)
-_F32_MATRICES = ("feed_forward.w_2.weight", "predictor.cif_output.weight")
+# The matrices fast mode reads ONLY through their bf16 copies (the library's GEMM-flagged weights, pfm_api.hip
+# add_entry(..., true)), minus the decoder FFNs' w_2 (their LayerNorm is folded through it in f32:
+# W2g = bf16(W2 diag(gamma)), c2 = W2 beta). Everything else -- FSMN taps (f32 depthwise arithmetic), the CIF alpha
+# projection, biases, LayerNorms -- is read in f32 and travels as f32.
+_BF16_WIRE_SUFFIXES = ("self_attn.linear_out.weight", "self_attn.linear_q_k_v.weight", "feed_forward.w_1.weight",
+                       "src_attn.linear_q.weight", "src_attn.linear_k_v.weight", "src_attn.linear_out.weight",
+                       "decoder.output_layer.weight", "ctc.ctc_lo.weight", "predictor.cif_conv1d.weight")
 
 
 def bf16_wire_key(key: str, shape) -> bool:
     """True for the weights fast mode reads only through their bf16 copies (sent as bf16 by wire="bf16")."""
-    if len(shape) < 2:
-        return False
-    return not (key.startswith("decoder.") and key.endswith(_F32_MATRICES[0])) and key != _F32_MATRICES[1]
+    if key.endswith(_BF16_WIRE_SUFFIXES):
+        return True
+    return key.startswith("encoder.") and key.endswith("feed_forward.w_2.weight")
 
 
 def _wire_index(layout, dev):

@@ -34,7 +34,9 @@ enum pfm_status {
     PFM_E_HIP = -2,      /* HIP runtime error */
     PFM_E_STATE = -3,    /* call out of order (e.g. run before all weights set) */
     PFM_E_NOMEM = -4,    /* device allocation failed */
-    PFM_E_NAME = -5      /* unknown weight name */
+    PFM_E_NAME = -5,     /* unknown weight name */
+    PFM_E_DEVICE = -6    /* device-side failure reported by a kernel (e.g. the beam search's cross-workgroup
+                            arrival barrier timed out): the outputs of the call are not valid */
 };
 
 enum pfm_dtype { PFM_F32 = 0, PFM_BF16 = 1 };

@@ -42,7 +42,8 @@ def _worker(rank, world, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        layout = [("a.weight", (3, 4), 4), ("b.bias", (5,), 4), ("c", (2, 2, 2), 8)]
+        layout = [("encoder.encoders.0.feed_forward.w_1.weight", (3, 4), 4), ("b.bias", (5,), 4),
+                  ("decoder.decoders.0.feed_forward.w_2.weight", (2, 2, 2), 8)]
         sd = None
         if rank == 0:
             rng = np.random.default_rng(0)
@@ -72,9 +73,11 @@ def test_gloo_world2_broadcast_and_gather():
     out.sort(key=lambda x: x[0])
     rng = np.random.default_rng(0)
     want = {k: rng.standard_normal(s).astype(np.float32).tolist() for k, s in
-            [("a.weight", (3, 4)), ("b.bias", (5,)), ("c", (2, 2, 2))]}
-    # bf16 wire: matrices (rank >= 2) arrive bf16-rounded, vectors exact (and "c" is a 3-D matrix)
-    want16 = {k: (torch.tensor(v).to(torch.bfloat16).float().tolist() if k != "b.bias" else v)
+            [("encoder.encoders.0.feed_forward.w_1.weight", (3, 4)), ("b.bias", (5,)),
+             ("decoder.decoders.0.feed_forward.w_2.weight", (2, 2, 2))]}
+    # bf16 wire: the encoder FFN matrix arrives bf16-rounded; the bias and the decoder w_2 (read in f32 by fast
+    # mode's folded LayerNorm) exact
+    want16 = {k: (torch.tensor(v).to(torch.bfloat16).float().tolist() if ".w_1." in k else v)
               for k, v in want.items()}
     for rank, sd, allres, sd16 in out:
         assert sd == want

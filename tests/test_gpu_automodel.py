@@ -228,7 +228,7 @@ def test_load_flat_device_matches_host_load():
 
 @pytest.mark.parametrize("large", [False, True])
 def test_bf16_wire_weights_fast_mode_bit_identical(large):
-    """broadcast_state_dict(wire="bf16") (the fast-mode data-parallel broadcast: 477 instead of 880 MB for
+    """broadcast_state_dict(wire="bf16") (the fast-mode data-parallel broadcast: 486 instead of 880 MB for
     Paraformer-large) leaves every rank bf16-rounded matrices; fast mode reads those only through bf16 copies (or,
     for the decoder w_2 / CIF projection, receives them in f32), so its decode is bit-identical to the f32-loaded
     engine's; EXACT mode is refused on such an engine."""

@@ -180,6 +180,24 @@ def test_automodel_beam_matches_reference_inference():
         assert [r["key"] for r in res] == [f"utt{int(o)}" for o in g["owner"]]
 
 
+def test_beam_barrier_timeout_is_an_error(monkeypatch):
+    """A search whose cross-workgroup arrival barrier times out (forced: PFM_BEAM_SPIN_CAP=0) fails the call with
+    PFM_E_DEVICE instead of returning 'no hypothesis' rows; the same engine decodes normally afterwards."""
+    from funasr_amd.runtime import PfmError
+    g = np.load(f"{GOLD}/beam_tiny.npz")
+    e, cfg = _engine(g)
+    feats, lens = fbank_input(seed=int(g["seed"]), B=int(g["B"]), T=int(g["T"]), lens=g["lens"])
+    x, l = torch.from_numpy(feats).cuda(), torch.from_numpy(lens).cuda()
+    kw = dict(mode="exact", beam=int(g["beam_size"]), ctc_weight=float(g["decoding_ctc_weight"]),
+              penalty=float(g["penalty"]), nbest=int(g["nbest"]))
+    monkeypatch.setenv("PFM_BEAM_SPIN_CAP", "0")
+    with pytest.raises(PfmError, match="barrier"):
+        e.run_beam(x, l, **kw)
+    monkeypatch.delenv("PFM_BEAM_SPIN_CAP")
+    r = e.run_beam(x, l, **kw)
+    assert int((r["ntok"][:, 0] >= 0).sum()) == int(g["B"])
+
+
 def test_beam_rejects_bad_arguments():
     from funasr_amd.runtime import PfmEngine, PfmError
     g = np.load(f"{GOLD}/beam_tiny.npz")

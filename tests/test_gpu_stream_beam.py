@@ -75,6 +75,28 @@ def test_stream_beam_golden(eng, name):
     assert decoded >= len(seq) - 1
 
 
+def test_stream_beam_small_lcap_refused_before_state_moves(eng):
+    """A step whose L_cap cannot hold the window's worst-case token count is refused before the stream's caches
+    advance: retrying it with a valid L_cap gives exactly the n-best lists of a stream that never saw the refusal."""
+    from funasr_amd.runtime import PfmError, PfmStreams
+    cfg, e = eng
+    g = np.load(f"{GOLD}/stream_beam_tiny.npz")
+    a = PfmStreams(e, 1, (0, 10, 5), 4, 1, "exact")
+    b = PfmStreams(e, 1, (0, 10, 5), 4, 1, "exact")
+    for i, x in enumerate(list(g["chunks"])[:4]):
+        feats = torch.from_numpy(np.ascontiguousarray(x[None])).cuda()
+        kw = dict(beam=3, ctc_weight=0.3, nbest=2)
+        if i == 2:
+            with pytest.raises(PfmError, match="L_cap"):
+                a.step_beam([0], feats, [x.shape[0]], [False], L_cap=3, **kw)
+        ra = a.step_beam([0], feats, [x.shape[0]], [False], **kw)
+        rb = b.step_beam([0], feats, [x.shape[0]], [False], **kw)
+        torch.cuda.synchronize()
+        ra, rb = {k: v.cpu() for k, v in ra.items()}, {k: v.cpu() for k, v in rb.items()}
+        assert _hyps(ra, 0) == _hyps(rb, 0), i
+        assert torch.equal(ra["scores"], rb["scores"]), i
+
+
 def test_stream_beam_batched_equals_single(eng):
     """Three streams with ragged chunks (one joins late, one ends on a tail chunk) in one step_beam per chunk give
     every stream the n-best lists it gets alone (the window lengths and token counts differ per stream)."""

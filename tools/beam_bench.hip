@@ -43,7 +43,7 @@ int main(int argc, char** argv) {
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
     auto run = [&]() {
-        CK(pfm_ctc_beam(am, L, x, T, lens, ntok, B, V, K, P, nbest, 0.3f, 0.f, 0, 0, 1, 2, 0, fs, is, tok, L + 1, ol, sc, 0));
+        CK(pfm_ctc_beam(am, L, x, T, lens, ntok, B, V, K, P, nbest, 0.3f, 0.f, 0, 0, 1, 2, 0, fs, is, tok, L + 1, ol, sc, nullptr, 0));
     };
     run();
     CK(hipDeviceSynchronize());
