@@ -285,7 +285,7 @@ def main():
     eng = PfmEngine(cfg, gpu)
     if world > 1:   # one flat RCCL broadcast, set straight from device memory (pfm_set_weight_device)
         bdev = dev if backend != "gloo" else torch.device("cpu")
-        # fast mode reads every matrix as bf16: send those as bf16 (440 instead of 880 MB over xGMI)
+        # fast mode reads every matrix as bf16: send those as bf16 (486 instead of 880 MB over xGMI)
         wire = "bf16" if args.mode == "fast" else "f32"
         flat = broadcast_state_dict(param_layout(cfg), make_weights(cfg, args.seed) if rank == 0 else None,
                                     device=bdev, keep_on_device=True, wire=wire)
@@ -333,6 +333,7 @@ def main():
     dt_instr = time.perf_counter() - ti
     gemm = eng.profile_read(0)
     attn = eng.profile_read(1)
+    dom = eng.profile_read(3)   # the dominant kernel alone (ffn2_kernel<4>, also inside class 0)
     eng.profile(False)
     # event-pair overhead on the launch stream (record -> record with nothing between), averaged over
     # 256 pairs queued behind real work; subtracted from each bracketed launch (reported raw as well)
@@ -361,6 +362,8 @@ def main():
     g_raw_ms = gemm["ms"]
     gemm["ms"] = max(1e-9, gemm["ms"] - ev_over_ms * gemm["launches"])
     attn["ms"] = max(1e-9, attn["ms"] - ev_over_ms * attn["launches"])
+    d_raw_ms = dom["ms"]
+    dom["ms"] = max(1e-9, dom["ms"] - ev_over_ms * dom["launches"])
     g_ach = gemm["flops"] / (gemm["ms"] / 1e3) / 1e12 if gemm["ms"] > 0 else 0.0
     # HBM bytes per launch of the same kernel set from the committed PMC passes (rocprofv3 --pmc FETCH_SIZE /
     # WRITE_SIZE, separate runs of this bench, gfx950-corrected by tools/pmc_traffic.py); null when absent
@@ -392,6 +395,18 @@ def main():
                 "event_pair_overhead_us": round(ev_over_ms * 1e3, 2),
                 "launches": int(gemm["launches"]), "share_of_step": round(gemm["ms"] / args.steps / step_ms, 3),
                 "instrumented_ms_per_step": round(dt_instr / args.steps * 1000.0, 3),
+                # the single dominant kernel, beside the class figure above: the encoder layer launch
+                # ffn2_kernel<4> (out-proj + LN2-FFN + LN1 + the next layer's QKV), 2 M 512 (512 + 2048 + 2048 + 1536)
+                # FLOP per launch at M = B T rows, live HIP events on its launch stream
+                "dominant": ({"kernel": "ffn2_kernel<4>", "launches": int(dom["launches"]),
+                              "gflop_per_launch": round(dom["flops"] / dom["launches"] / 1e9, 2),
+                              "avg_launch_us": round(dom["ms"] * 1e3 / dom["launches"], 2),
+                              "avg_launch_us_raw": round(d_raw_ms * 1e3 / dom["launches"], 2),
+                              "achieved": round(dom["flops"] / (dom["ms"] / 1e3) / 1e12, 2), "peak": peak,
+                              "unit": "TFLOP/s",
+                              "frac": round(dom["flops"] / (dom["ms"] / 1e3) / 1e12 / peak, 4),
+                              "share_of_step": round(dom["ms"] / args.steps / step_ms, 3)}
+                             if dom["launches"] else None),
                 "achieved_hbm_gbs": round(gemm["bytes"] / (gemm["ms"] / 1e3) / 1e9, 1) if gemm["ms"] > 0 else None}
     a_ach = attn["flops"] / (attn["ms"] / 1e3) / 1e12 if attn["ms"] > 0 else 0.0
     path_tf = fl_step / (step_ms / 1e3) / 1e12

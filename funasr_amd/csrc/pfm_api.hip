@@ -320,13 +320,13 @@ struct pfm_handle {
     static constexpr int KVG = 4;
     hipEvent_t ev_kvg[KVG] = {};
     // live profiling: event pairs per launch, per kernel class
-    struct ProfRec { hipEvent_t a, b; int kc; double flops, bytes; };
+    struct ProfRec { hipEvent_t a, b; int kc, kc2; double flops, bytes; };
     bool prof_on = false;
     std::vector<ProfRec> prof;
     std::vector<hipEvent_t> ev_pool;
     size_t ev_used = 0;
-    double prof_ms[3] = {0, 0, 0}, prof_fl[3] = {0, 0, 0}, prof_by[3] = {0, 0, 0};
-    long long prof_n[3] = {0, 0, 0};
+    double prof_ms[4] = {0, 0, 0, 0}, prof_fl[4] = {0, 0, 0, 0}, prof_by[4] = {0, 0, 0, 0};
+    long long prof_n[4] = {0, 0, 0, 0};
 
     GenUnbind gen_unbind_;                   // last member: DevBufs created later are unbound
 
@@ -653,9 +653,11 @@ hipEvent_t next_event(pfm_handle* h) {
 }
 
 // Bracket one launch with events when profiling is on.
+// kc2 >= 0: the launch is also counted in a second class (PFM_K_FFN2: the dominant kernel inside PFM_K_GEMM).
 struct ProfScope {
-    pfm_handle* h; hipStream_t st; int kc; double fl, by; hipEvent_t a = nullptr;
-    ProfScope(pfm_handle* h_, hipStream_t st_, int kc_, double fl_, double by_) : h(h_), st(st_), kc(kc_), fl(fl_), by(by_) {
+    pfm_handle* h; hipStream_t st; int kc, kc2; double fl, by; hipEvent_t a = nullptr;
+    ProfScope(pfm_handle* h_, hipStream_t st_, int kc_, double fl_, double by_, int kc2_ = -1)
+        : h(h_), st(st_), kc(kc_), kc2(kc2_), fl(fl_), by(by_) {
         if (h->prof_on) { a = next_event(h); if (a) (void)hipEventRecord(a, st); }
     }
     ~ProfScope() {
@@ -663,7 +665,7 @@ struct ProfScope {
         hipEvent_t b = next_event(h);
         if (!b) return;
         (void)hipEventRecord(b, st);
-        h->prof.push_back({a, b, kc, fl, by});
+        h->prof.push_back({a, b, kc, kc2, fl, by});
     }
 };
 
@@ -671,10 +673,13 @@ void prof_collect(pfm_handle* h) {
     for (auto& r : h->prof) {
         float ms = 0.f;
         if (hipEventSynchronize(r.b) == hipSuccess && hipEventElapsedTime(&ms, r.a, r.b) == hipSuccess) {
-            h->prof_ms[r.kc] += ms;
-            h->prof_fl[r.kc] += r.flops;
-            h->prof_by[r.kc] += r.bytes;
-            h->prof_n[r.kc] += 1;
+            for (const int k : {r.kc, r.kc2}) {
+                if (k < 0) continue;
+                h->prof_ms[k] += ms;
+                h->prof_fl[k] += r.flops;
+                h->prof_by[k] += r.bytes;
+                h->prof_n[k] += 1;
+            }
         }
     }
     h->prof.clear();
@@ -1103,7 +1108,7 @@ int encoder_stack(const Run& r, const float* x_in, const int* lens, int B, int T
                     // ... and the next layer's q|k|v = LN1_{l+1}(x2) Wqkv^T + b (phase 3: LN1_{l+1} stays in registers)
                     const EncLayer& N = h->enc[l + 1];
                     ProfScope ps(h, st, PFM_K_GEMM, flo + 6.0 * M * (double)D * D,
-                                 byo + (double)M * D * (6.0 - 2.0) + 6.0 * D * D);
+                                 byo + (double)M * D * (6.0 - 2.0) + 6.0 * D * D, PFM_K_FFN2);
                     HIP_TRY(pfm_ffn2_fused_op_qkv(Ob, Fb, r.P(L.bo), din == D ? X : nullptr, (int)M, r.P(L.ln2g),
                                                   r.P(L.ln2b), c.ln_eps, h->ffn_pack.as<bf16>() + L.ffp - pfm_ffn_packed_o_elems(),
                                                   r.P(L.b1), r.P(L.b2), X, r.P(N.ln1g), r.P(N.ln1b), r.P(N.bqkv), QKVb, st));
@@ -1917,13 +1922,13 @@ int pfm_fbank(pfm_handle* h, void* stream, const float* wav, const int32_t* nsam
 int pfm_profile(pfm_handle* h, int enable) {
     if (!h) return fail(PFM_E_ARG, "pfm_profile: null handle");
     prof_collect(h);
-    for (int k = 0; k < 3; ++k) { h->prof_ms[k] = h->prof_fl[k] = h->prof_by[k] = 0; h->prof_n[k] = 0; }
+    for (int k = 0; k < 4; ++k) { h->prof_ms[k] = h->prof_fl[k] = h->prof_by[k] = 0; h->prof_n[k] = 0; }
     h->prof_on = enable != 0;
     return PFM_OK;
 }
 
 int pfm_profile_read(pfm_handle* h, int kc, double* ms, double* flops, double* bytes, int64_t* launches) {
-    if (!h || kc < 0 || kc > 2) return fail(PFM_E_ARG, "pfm_profile_read: bad arguments");
+    if (!h || kc < 0 || kc > 3) return fail(PFM_E_ARG, "pfm_profile_read: bad arguments");
     prof_collect(h);
     if (ms) *ms = h->prof_ms[kc];
     if (flops) *flops = h->prof_fl[kc];

@@ -342,7 +342,9 @@ void pfm_destroy(pfm_handle* h);
  * its stream; pfm_profile_read sums, per kernel class (0 = MFMA GEMM, 1 = attention,
  * 2 = everything else), the event-measured milliseconds, the ALGORITHMIC flops and bytes of
  * those launches and their count. Reading synchronises the recorded events. */
-enum pfm_kclass { PFM_K_GEMM = 0, PFM_K_ATTN = 1, PFM_K_OTHER = 2 };
+enum pfm_kclass { PFM_K_GEMM = 0, PFM_K_ATTN = 1, PFM_K_OTHER = 2,
+                  PFM_K_FFN2 = 3 /* the dominant kernel alone: the encoder's fused layer launch (ffn2_kernel<4>:
+                                    out-proj + LN2-FFN + LN1 + next QKV), also counted in PFM_K_GEMM */ };
 int pfm_profile(pfm_handle* h, int enable);
 int pfm_profile_read(pfm_handle* h, int kclass, double* ms, double* flops, double* bytes,
                      int64_t* launches);

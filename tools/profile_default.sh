@@ -12,5 +12,5 @@ timeout -k 10 500 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/$name" -o r
 rc=$?
 cd "$R"
 [ $rc -eq 0 ] && python tools/rocpd_summary.py "gpurun_out/$name/run_results.db" "gpurun_out/$name/stats.csv" \
-  argmax_reduce_kernel "gpurun_out/$name/bench.log" 2 5 > "gpurun_out/$name/summary.md"
+  "gpurun_out/$name/bench.log" 2 5 > "gpurun_out/$name/summary.md"
 exit $rc

@@ -3,6 +3,8 @@
 # punctuation / long-audio / CPU legs), run on the GPU box from the repo root:
 #   tools/profile_fast.sh <out-name> [extra bench args]
 # -> gpurun_out/<out-name>/{run_results.db, bench.log, stats.csv, summary.md}
+# Set PFM_SUBBATCH=1 PFM_DEC_SUBBATCH=1 in the environment for a trace without concurrent streams (the kernel
+# trace serialises them), whose kernel time per call is the step.
 set -o pipefail
 name=$1; shift
 R=$(pwd)
@@ -14,5 +16,5 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/$name" -o r
 rc=$?
 cd "$R"
 [ $rc -eq 0 ] && python tools/rocpd_summary.py "gpurun_out/$name/run_results.db" "gpurun_out/$name/stats.csv" \
-  argmax_reduce_kernel "gpurun_out/$name/bench.log" 2 5 > "gpurun_out/$name/summary.md"
+  "gpurun_out/$name/bench.log" 2 5 > "gpurun_out/$name/summary.md"
 exit $rc
