@@ -438,6 +438,28 @@ def main():
         if shared:   # not an N-GPU result: N ranks time-share fewer devices
             out["metric"] = METRIC + " [REHEARSAL: ranks share a device, not a multi-GPU measurement]"
 
+    # fast-mode fidelity of the benched dispatch on the reference's own B = 64 x 500 run (tests/golden/para_large_b64:
+    # per-position top-5 log-probs of the reference decoder; regret statistics of tests/fast_parity.py) beside the
+    # CPU emulation of ideal bf16 operands (tests/golden/fast_emul.json)
+    if rank == 0 and world == 1 and args.mode == "fast":
+        gpath = os.path.join(ROOT, "tests", "golden", "para_large_b64.npz")
+        if os.path.exists(gpath):
+            from tests.fast_parity import paraformer_stats
+            from tests.golden.inputs import fbank_input
+            gg = np.load(gpath)
+            gx, gl = fbank_input(int(gg["seed"]), int(gg["B"]), int(gg["T"]), gg["lens"])
+            rr = eng.run(torch.from_numpy(gx).to(dev), torch.from_numpy(gl).to(dev), mode="fast")
+            st = paraformer_stats(rr["tokens"].cpu().numpy(), rr["ntok"].cpu().numpy(), gg, 0.5)
+            em = json.load(open(os.path.join(ROOT, "tests", "golden", "fast_emul.json")))["para_large_b64"]
+            out["fast_fidelity"] = {
+                "golden": "para_large_b64 (reference run, B=64 x 500, seeded weights)",
+                "pfm_fast_xw": int(os.environ.get("PFM_FAST_XW", "7")),
+                "flip_frac": round(st["flip_frac"], 4), "mean_regret_nat": round(st["mean_regret"], 5),
+                "max_regret_nat": round(st["max_regret"], 4),
+                "outside_top5_frac": round(st["outside_topk"] / max(1, st["positions"]), 5),
+                "equal_token_counts": round(st["equal_counts"], 4),
+                "ideal_bf16_emulation": {"flip_frac": round(em["G"]["flip_frac"], 4),
+                                         "mean_regret_nat": round(em["G"]["mean_regret"], 5)}}
     if rank == 0:
         progress("headline leg done")
     # ---- exact (f32 MFMA) mode on the same batch: token-parity mode throughput + agreement

@@ -3,6 +3,10 @@
 //   MODE 0  encoder:       x2 = x + W2 relu(W1 LN2(x) + b1) + b2                 (sanm/encoder.py:138-145)
 //   MODE 1  encoder + OP:  x1 = O Wo^T + bo + F (+ x), then MODE 0 on x1          (sanm/encoder.py:120-145)
 //   MODE 4  MODE 1, then the next layer's q|k|v = LN1_next(x2) Wqkv^T + bq        (sanm/attention.py:275-288)
+//   MODE 5  MODE 4 with the v rows of Wqkv as two bf16 planes (w = w0 + w1, fast mode's precise-weight option:
+//           PFM_FAST_XW bit 4): the v pass streams 32 more tiles, accumulated into the same registers
+//   MODE 6  MODE 5 with Wo as two bf16 planes too (PFM_FAST_XW bit 8): phase 0 streams 32 more tiles
+//   MODE 3  MODE 1 with Wo as two bf16 planes (the last layer under PFM_FAST_XW bit 8)
 // with the next LayerNorm of the result as a bf16 output (the consumer GEMM's operand; MODE 4: the QKV rows).
 // (The decoder FFN runs on k_ffn.hip: its 128-row form here measured slower end to end and was removed.)
 //
@@ -173,9 +177,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int r = lane & 31, h = lane >> 5;
-    static_assert(MODE == 0 || MODE == 1 || MODE == 4, "encoder modes");
-    constexpr bool OP = MODE == 1 || MODE == 4, QK = MODE == 4;   // encoder out-projection; + the next QKV
-    constexpr int F0 = OP ? OPF : 0, F3 = F0 + NCH * CHF, NF = F3 + (QK ? QKF : 0), NT = NF / TF;
+    static_assert(MODE == 0 || MODE == 1 || MODE == 3 || MODE == 4 || MODE == 5 || MODE == 6, "encoder modes");
+    constexpr bool OP = MODE == 1 || MODE == 3 || MODE >= 4, QK = MODE >= 4;   // out-projection; + the next QKV
+    constexpr bool XV = MODE >= 5;                 // + the v rows' second weight plane
+    constexpr bool XO = MODE == 3 || MODE == 6;    // + Wo's second weight plane
+    constexpr int F0 = OP ? (XO ? 2 : 1) * OPF : 0, F3 = F0 + NCH * CHF, NF = F3 + (QK ? QKF + (XV ? OPF : 0) : 0),
+                  NT = NF / TF;
     const long long rg = (long long)blockIdx.x * BM + 32 * w + r;   // this lane's row
     const bool live = rg < M;
     const long long rc = live ? rg : (long long)M - 1;               // clamped for loads
@@ -441,6 +448,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
                     else if (ks == 0) mfma_a0(acc[ob], wf[f % NB], act[0]);
                     else mfma_a(acc[ob], wf[f % NB], act[ks]);
                 }
+        if constexpr (XO) {   // Wo's second plane: the same fragment order, into the same accumulators
+#pragma unroll
+            for (int pp = 0; pp < 16 / OPI; ++pp)
+#pragma unroll
+                for (int ks = 0; ks < 32; ++ks)
+#pragma unroll
+                    for (int e = 0; e < OPI; ++e) {
+                        const int f = OPF + 32 * OPI * pp + OPI * ks + e, ob = OPI * pp + e;
+                        step_pre(f, f);
+                        if (VAR == 2 || VAR == 5) asm volatile("" :: "v"(wf[f % NB]));
+                        else mfma_a(acc[ob], wf[f % NB], act[ks]);
+                    }
+        }
         // The read-ahead of the stream's first PD fragments is in flight. An asm ds_read's destination counts as
         // written at the statement, so across the VALU-heavy transition the compiler spilled those registers to
         // scratch before the data landed (garbage operands for the first phase-1 MFMAs on some waves): retire the
@@ -598,6 +618,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
                         else if (ks == 0) mfma_a0(acc[ob], wf[fs % NB], act[0]);
                         else mfma_a(acc[ob], wf[fs % NB], act[ks]);
                     }
+            if constexpr (XV) {   // the v pass: the second plane's fragments, same order, into the same accumulators
+                if (p == 2) {
+#pragma unroll
+                    for (int pp = 0; pp < 4; ++pp)
+#pragma unroll
+                        for (int ks = 0; ks < 32; ++ks)
+#pragma unroll
+                            for (int e = 0; e < 4; ++e) {
+                                const int fs = OPF + 128 * pp + 4 * ks + e, ob = 4 * pp + e;
+                                step_pre(fp + fs, fs);
+                                if (VAR == 2 || VAR == 5) asm volatile("" :: "v"(wf[fs % NB]));
+                                else mfma_a(acc[ob], wf[fs % NB], act[ks]);
+                            }
+                }
+            }
             asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(wf[0]), "+v"(wf[1]), "+v"(wf[2]), "+v"(wf[3]), "+v"(wf[4]),
                          "+v"(wf[5]), "+v"(wf[6]), "+v"(wf[7]));
             xdl_drain(acc);
@@ -703,10 +738,10 @@ __global__ __launch_bounds__(256) void ffn2_pack_o_kernel(const bf16* __restrict
 // the next layer's Wqkv [1536 out][512 in] -> phase-3 fragments: three passes of 512 output features (rows 512 p ..),
 // fragment f of a pass = output block 4 (f >> 7) + (f & 3), k step (f >> 2) & 31, with W1's permuted k (the B operand
 // is the LayerNorm output in act)
-__global__ __launch_bounds__(256) void ffn2_pack_qkv_kernel(const bf16* __restrict__ Wq, bf16* __restrict__ Wp) {
-    const int gid = blockIdx.x * 256 + threadIdx.x;   // < QKF * 64
+__global__ __launch_bounds__(256) void ffn2_pack_qkv_kernel(const bf16* __restrict__ Wq, bf16* __restrict__ Wp, int p0) {
+    const int gid = blockIdx.x * 256 + threadIdx.x;   // < (3 - p0) * OPF * 64
     const int fq = gid >> 6, l = gid & 63, m = l & 31, hh = l >> 5;
-    const int p = fq / OPF, f = fq % OPF;
+    const int p = p0 + fq / OPF, f = fq % OPF;
     const int ob = 4 * (f >> 7) + (f & 3), ks = (f >> 2) & 31;
     bf16x8 o;
 #pragma unroll
@@ -746,7 +781,14 @@ hipError_t pfm_ffn2_pack(const bf16* W1, const bf16* W2, bf16* Wp, hipStream_t s
 
 // the next layer's Wqkv [1536][512] -> QKF fragments behind the layer's FFN tiles (ffn2_kernel MODE 4)
 hipError_t pfm_ffn2_pack_qkv(const bf16* Wqkv, bf16* Wp, hipStream_t st) {
-    hipLaunchKernelGGL(ffn2_pack_qkv_kernel, dim3(QKF * 64 / 256), dim3(256), 0, st, Wqkv, Wp);
+    hipLaunchKernelGGL(ffn2_pack_qkv_kernel, dim3(QKF * 64 / 256), dim3(256), 0, st, Wqkv, Wp, 0);
+    PFM_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
+// MODE 5: the v rows' second plane (rows 1024..1535 of a [1536][512] plane) -> OPF more fragments behind the QKV ones
+hipError_t pfm_ffn2_pack_qkv_v(const bf16* Wqkv_lo, bf16* Wp, hipStream_t st) {
+    hipLaunchKernelGGL(ffn2_pack_qkv_kernel, dim3(OPF * 64 / 256), dim3(256), 0, st, Wqkv_lo, Wp, 2);
     PFM_LAUNCH_CHECK();
     return hipSuccess;
 }
@@ -787,4 +829,29 @@ hipError_t pfm_ffn2_fused_op_qkv(const bf16* o, const bf16* f, const float* bo, 
     if (!al16(x) || !al16(xo) || !al16(Wop) || !al16(qkv) || !al16(o) || !al16(f) || !al16(bo) || !al16(bq))
         return hipErrorInvalidValue;
     return ffn2_launch<4>(st, M, x, g2, be2, eps, Wop, b1, b2, xo, gn, bn, qkv, o, f, bo, bq);
+}
+
+// MODE 5: MODE 4 with Wop's QKV fragments followed by pfm_ffn2_pack_qkv_v's (the v rows' second weight plane);
+// xo_planes: MODE 6, Wop starts with Wo's two planes (pfm_ffn2_pack_o of each, back to back)
+hipError_t pfm_ffn2_fused_op_qkv_xv(const bf16* o, const bf16* f, const float* bo, const float* x, int M,
+                                    const float* g2, const float* be2, float eps, const bf16* Wop, const float* b1,
+                                    const float* b2, float* xo, const float* gn, const float* bn, const float* bq,
+                                    bf16* qkv, bool xo_planes, hipStream_t st) {
+    if (M <= 0) return hipSuccess;
+    if (!o || !f || !bo || !xo || !b1 || !b2 || !gn || !bn || !bq || !qkv) return hipErrorInvalidValue;
+    if (!al16(x) || !al16(xo) || !al16(Wop) || !al16(qkv) || !al16(o) || !al16(f) || !al16(bo) || !al16(bq))
+        return hipErrorInvalidValue;
+    if (xo_planes) return ffn2_launch<6>(st, M, x, g2, be2, eps, Wop, b1, b2, xo, gn, bn, qkv, o, f, bo, bq);
+    return ffn2_launch<5>(st, M, x, g2, be2, eps, Wop, b1, b2, xo, gn, bn, qkv, o, f, bo, bq);
+}
+
+// MODE 3: pfm_ffn2_fused_op with Wop = Wo's two planes, then the FFN fragments (the last layer under bit 8)
+hipError_t pfm_ffn2_fused_op_xo(const bf16* o, const bf16* f, const float* bo, const float* x, int M, const float* g2,
+                                const float* be2, float eps, const bf16* Wop, const float* b1, const float* b2,
+                                float* xo, const float* gn, const float* bn, bf16* xn, hipStream_t st) {
+    if (M <= 0) return hipSuccess;
+    if ((xn != nullptr) != (gn != nullptr && bn != nullptr) || !o || !f || !bo || !xo || !b1 || !b2)
+        return hipErrorInvalidValue;
+    if (!al16(x) || !al16(xo) || !al16(Wop) || !al16(xn) || !al16(o) || !al16(f) || !al16(bo)) return hipErrorInvalidValue;
+    return ffn2_launch<3>(st, M, x, g2, be2, eps, Wop, b1, b2, xo, gn, bn, xn, o, f, bo, nullptr);
 }

@@ -106,15 +106,19 @@ __global__ __launch_bounds__(C::NT) void gemm_bf16_kernel(const bf16* __restrict
     // segment pa = {2,1,0,1,0,0}[s] and W plane pw = {0,1,2,0,1,0}[s] of segment s = k0 / x6_k (a K step
     // never straddles segments: x6_k % BK == 0). Small products first.
     // bf16x3 (x6_terms 3): segments 3..5 only.
-    const int xk = epi.x6_k, sg0 = epi.x6_terms == 3 ? 3 : 0;
+    // split WEIGHTS only (x6_terms 2, fast mode's precise-weight projections): A is one plain bf16 operand [M, x6_k],
+    // W two planes w = w0 + w1 (x6_ws apart); K' = 2 x6_k runs (A, W1) then (A, W0).
+    const int xk = epi.x6_k, xt = epi.x6_terms, sg0 = xt == 3 ? 3 : 0;
     auto koff_a = [&](int k0) -> int {
         if (!xk) return k0;
         const int s0 = k0 / xk, kk = k0 - s0 * xk, sg = s0 + sg0;
+        if (xt == 2) return kk;
         return (sg == 0 ? 2 : (sg == 1 || sg == 3) ? 1 : 0) * xk + kk;
     };
     auto koff_w = [&](int k0) -> long long {
         if (!xk) return k0;
         const int s0 = k0 / xk, kk = k0 - s0 * xk, sg = s0 + sg0;
+        if (xt == 2) return (long long)(s0 == 0 ? 1 : 0) * epi.x6_ws + kk;
         return (long long)(sg == 1 || sg == 4 ? 1 : sg == 2 ? 2 : 0) * epi.x6_ws + kk;
     };
     auto stage = [&](int k0, int s) {
@@ -1047,7 +1051,8 @@ hipError_t pfm_gemm_bf16_256(const void* A, RowMap amap, const void* W, long lon
     // faster in isolation — tools/gemm_cfg_scan.py SCAN_X6=1 — but slower on the two-group path, 99.3 and
     // 104.8 vs 98.0 ms/step; unsplit, C17 for the wide ones 100.9 vs 101.3, both 111.6)
     if (epi.x6_k && cfg != 1 && cfg != 3 && cfg != 4 && cfg != 13 && cfg != 15 && cfg != 16 && cfg != 17) cfg = 15;
-    if (epi.x6_k && (K != (epi.x6_terms == 3 ? 3 : 6) * epi.x6_k || epi.x6_k % 64)) return hipErrorInvalidValue;
+    if (epi.x6_k && (K != (epi.x6_terms == 3 ? 3 : epi.x6_terms == 2 ? 2 : 6) * epi.x6_k || epi.x6_k % 64))
+        return hipErrorInvalidValue;
     switch (cfg) {
         case 2: return launch<C2>(A, amap, W, ldw, M, N, K, e2, st);
         case 3: return launch<C3>(A, amap, W, ldw, M, N, K, e2, st);

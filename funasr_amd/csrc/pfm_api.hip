@@ -100,6 +100,14 @@ hipError_t pfm_ffn2_fused_op(const bf16* o, const bf16* f, const float* bo, cons
 hipError_t pfm_ffn_fused_op(const bf16* o, const bf16* f, const float* bo, const float* x, int M, const float* g2,
                             const float* be2, float eps, const bf16* Wop, const float* b1, const float* b2, float* xo,
                             const float* gn, const float* bn, bf16* xn, hipStream_t st);
+hipError_t pfm_ffn2_pack_qkv_v(const bf16* Wqkv_lo, bf16* Wp, hipStream_t st);
+hipError_t pfm_ffn2_fused_op_qkv_xv(const bf16* o, const bf16* f, const float* bo, const float* x, int M,
+                                    const float* g2, const float* be2, float eps, const bf16* Wop, const float* b1,
+                                    const float* b2, float* xo, const float* gn, const float* bn, const float* bq,
+                                    bf16* qkv, bool xo_planes, hipStream_t st);
+hipError_t pfm_ffn2_fused_op_xo(const bf16* o, const bf16* f, const float* bo, const float* x, int M, const float* g2,
+                                const float* be2, float eps, const bf16* Wop, const float* b1, const float* b2,
+                                float* xo, const float* gn, const float* bn, bf16* xn, hipStream_t st);
 hipError_t pfm_ffn2_fused_op_qkv(const bf16* o, const bf16* f, const float* bo, const float* x, int M, const float* g2,
                                  const float* be2, float eps, const bf16* Wop, const float* b1, const float* b2, float* xo,
                                  const float* gn, const float* bn, const float* bq, bf16* qkv, hipStream_t st);
@@ -205,6 +213,8 @@ void pfm_knobs_refresh() {
     k.dec_ffn_fused = iv("PFM_DEC_FFN_FUSED", 1) != 0;
     k.ffn_kernel = iv("PFM_FFN_KERNEL", 2) == 1 ? 1 : 2;
     k.ffn_qkv = iv("PFM_FFN_QKV", 1) != 0;
+    k.fast_xw = iv("PFM_FAST_XW", 7) & 15;
+    if (k.fast_xw & 8) k.fast_xw |= 4;   // the out-projection's planes ride on MODE 6 (v rows split too)
     const int* f = &k.attn_fsmn;
     unsigned long long s = 1469598103934665603ull;   // FNV-1a over the fields
     for (int i = 0; i < PFM_KNOB_FIELDS; ++i) s = (s ^ (unsigned long long)(unsigned)f[i]) * 1099511628211ull;
@@ -255,6 +265,7 @@ struct EncLayer {
     size_t ln1g, ln1b, wqkv, bqkv, wo, bo, fsmn, ln2g, ln2b, w1, b1, w2, b2;
     int din;
     size_t ffp = 0;   // fast mode: element offset of the packed W1 | W2 ring tiles in ffn_pack (k_ffn.hip)
+    size_t opp = 0;   // ... and of the layer's first packed tile (Wo, or Wo's two planes under PFM_FAST_XW bit 8)
     bool qkv_next = false;   // k_ffn2.hip: ... followed by the next layer's packed Wqkv (ffn2_kernel MODE 4)
 };
 struct DecLayer { size_t fsmn, wq, bq, wo, bo, w1, b1, w2, ng, nb, n1g, n1b, n2g, n2b, n3g, n3b; };
@@ -273,6 +284,12 @@ struct pfm_handle {
     DevBuf qkv0_pad;               // fast mode: layer 0's bf16 QKV weights with K padded to a multiple of 64
     DevBuf ffn_pack;               // fused-FFN weight tiles of every encoder layer (bf16, LDS-image order)
     bool ffn_ready = false;
+    // fast mode, PFM_FAST_XW: weights as two bf16 planes [hi | lo] (split3 planes 0, 1; plane 2 unused): the
+    // predictor conv ([D][3D]), encoder layer 0's QKV (K padded to 64) / Wo / W1 / W2, and layer 1's QKV with
+    // only its v rows' lo plane nonzero (bit 4: layer 1's QKV follows the unfused layer 0 as a GEMM)
+    DevBuf xw_pred, xw_qkv0, xw_wo0, xw_w10, xw_w20, xw_qkv1, xw_tmp;
+    int xw_kind = 0;               // the PFM_FAST_XW bits the planes / the ffn_pack layout were built for
+    bool xw_ready = false;
     DevBuf logits, ctcx, beam_fs, beam_is;   // pfm_run_beam: decoder / CTC log-probs and the search's scratch
     DevBuf beam_fail;                        // one device word: a search's cross-workgroup barrier timed out
     DevBuf beam_nf;                          // pfm_stream_step_beam: CIF fire counts when the caller passes none
@@ -479,6 +496,17 @@ void make_pe(std::vector<float>& pe, int T, int depth) {
 // the fused FFN kernel is written for the Paraformer / SenseVoice encoder width (512 -> 2048 -> 512)
 bool ffn_shape_ok(const pfm_config& c) { return c.d_model == 512 && c.ffn == 2048; }
 
+// PFM_FAST_XW bits that apply to this model: the 512 / 2048 encoder (the fused kernels' shapes), Paraformer's
+// predictor conv (bit 1) only where the handle has one
+int fast_xw_bits(const pfm_handle* h) {
+    const pfm_config& c = h->cfg;
+    if (c.d_model != 512 || c.ffn != 2048 || h->enc.empty()) return 0;
+    int b = pfm_knobs().fast_xw;
+    if (c.arch == PFM_ARCH_PUNC) return 0;
+    if (c.arch == PFM_ARCH_SENSEVOICE) b &= ~1;
+    return b;
+}
+
 int ensure_bf16(pfm_handle* h, hipStream_t st) {
     if (!h->bf_ready) {
         HIP_TRY(h->arena_bf.ensure(h->arena_elems * sizeof(bf16)));
@@ -498,21 +526,76 @@ int ensure_bf16(pfm_handle* h, hipStream_t st) {
     // k_ffn.hip (1) and k_ffn2.hip (2) order their fragments differently (the decoder always runs k_ffn.hip)
     const int fk = pfm_knobs().ffn_kernel;
     if (h->ffn_kind != fk) { h->ffn_ready = false; h->ffn_kind = fk; }
+    const int xw = fast_xw_bits(h);
+    if (h->xw_kind != xw) { h->xw_ready = false; h->ffn_ready = false; h->xw_kind = xw; }
+    if (!h->xw_ready && xw) {
+        const int D = h->cfg.d_model, Fd = h->cfg.ffn;
+        // planes of an f32 [N][K] weight into dst [3][N][Kp] (K zero-padded to Kp)
+        auto planes = [&](DevBuf& dst, const float* w, int N, int K, int Kp) -> hipError_t {
+            const size_t n = (size_t)N * Kp;
+            hipError_t e = dst.ensure(3 * n * sizeof(bf16));
+            if (e != hipSuccess) return e;
+            const float* src = w;
+            if (Kp != K) {
+                if ((e = h->xw_tmp.ensure(n * sizeof(float))) != hipSuccess) return e;
+                if ((e = hipMemsetAsync(h->xw_tmp.p, 0, n * sizeof(float), st)) != hipSuccess) return e;
+                if ((e = hipMemcpy2DAsync(h->xw_tmp.p, (size_t)Kp * 4, w, (size_t)K * 4, (size_t)K * 4, N,
+                                          hipMemcpyDeviceToDevice, st)) != hipSuccess)
+                    return e;
+                src = h->xw_tmp.as<float>();
+            }
+            return pfm_split3_planes(src, dst.as<bf16>(), (long long)n, (long long)n, st);
+        };
+        if (xw & 1) HIP_TRY(planes(h->xw_pred, h->w(h->cif_w), D, 3 * D, 3 * D));
+        if ((xw & 2) && !h->enc.empty()) {
+            const EncLayer& L0 = h->enc[0];
+            const int Kp0 = (L0.din + 63) / 64 * 64;
+            HIP_TRY(planes(h->xw_qkv0, h->w(L0.wqkv), 3 * D, L0.din, Kp0));
+            HIP_TRY(planes(h->xw_wo0, h->w(L0.wo), D, D, D));
+            HIP_TRY(planes(h->xw_w10, h->w(L0.w1), Fd, D, D));
+            HIP_TRY(planes(h->xw_w20, h->w(L0.w2), D, Fd, Fd));
+            if (h->enc.size() > 1) {   // layer 1's QKV as a split-weight GEMM: lo plane only where bit 4 asks
+                const size_t n = (size_t)3 * D * h->enc[1].din;
+                HIP_TRY(planes(h->xw_qkv1, h->w(h->enc[1].wqkv), 3 * D, h->enc[1].din, h->enc[1].din));
+                HIP_TRY(hipMemsetAsync(h->xw_qkv1.as<bf16>() + n, 0, (size_t)((xw & 4) ? 2 : 3) * D * h->enc[1].din * 2,
+                                       st));
+            }
+        }
+        h->xw_ready = true;
+    }
     auto pack = [&](const bf16* w1, const bf16* w2, bf16* wp) { return fk == 2 ? pfm_ffn2_pack(w1, w2, wp, st) : pfm_ffn_pack(w1, w2, wp, st); };
     auto pack_o = [&](int kind, const bf16* wo, bf16* wp) { return kind == 2 ? pfm_ffn2_pack_o(wo, wp, st) : pfm_ffn_pack_o(wo, wp, st); };
     if (!h->ffn_ready && ffn_shape_ok(h->cfg) && pfm_knobs().ffn_fused && !h->enc.empty()) {
         // per layer: the out-projection's 32 tiles, then the FFN's 256 (ffp = the FFN tiles); k_ffn2.hip layouts add
         // the next layer's Wqkv as 3 x 32 more (ffn2_kernel MODE 4, the QKV projection as phase 3)
-        const size_t po = pfm_ffn_packed_o_elems(), pfe = pfm_ffn_packed_elems(), per = po + pfe + (fk == 2 ? 3 * po : 0);
+        const bool xv = fk == 2 && (xw & 4);   // MODE 5: the v rows' lo-plane fragments behind the QKV passes
+        const bool xo = fk == 2 && (xw & 8);   // MODE 6 / 3: Wo's lo-plane fragments behind its hi ones
+        const size_t po = pfm_ffn_packed_o_elems(), pfe = pfm_ffn_packed_elems(),
+                     per = (xo ? 2 : 1) * po + pfe + (fk == 2 ? (xv ? 4 : 3) * po : 0);
         const int D = h->cfg.d_model;
         HIP_TRY(h->ffn_pack.ensure(h->enc.size() * per * sizeof(bf16)));
         for (size_t l = 0; l < h->enc.size(); ++l) {
+            // [Wo (hi) | Wo lo (bit 8) | FFN | next Wqkv (3 passes) | its v rows' lo plane (bit 4)]
             bf16* base = h->ffn_pack.as<bf16>() + l * per;
-            h->enc[l].ffp = l * per + po;
+            const size_t pw = (xo ? 2 : 1) * po;
+            h->enc[l].opp = l * per;
+            h->enc[l].ffp = l * per + pw;
             HIP_TRY(pack_o(fk, h->wb(h->enc[l].wo), base));
-            HIP_TRY(pack(h->wb(h->enc[l].w1), h->wb(h->enc[l].w2), base + po));
+            if (xo) {
+                const size_t n = (size_t)D * D;
+                HIP_TRY(h->xw_tmp.ensure(3 * n * sizeof(bf16)));
+                HIP_TRY(pfm_split3_planes(h->w(h->enc[l].wo), h->xw_tmp.as<bf16>(), (long long)n, (long long)n, st));
+                HIP_TRY(pack_o(fk, h->xw_tmp.as<bf16>() + n, base + po));
+            }
+            HIP_TRY(pack(h->wb(h->enc[l].w1), h->wb(h->enc[l].w2), base + pw));
             h->enc[l].qkv_next = fk == 2 && l + 1 < h->enc.size() && h->enc[l + 1].din == D;
-            if (h->enc[l].qkv_next) HIP_TRY(pfm_ffn2_pack_qkv(h->wb(h->enc[l + 1].wqkv), base + po + pfe, st));
+            if (h->enc[l].qkv_next) HIP_TRY(pfm_ffn2_pack_qkv(h->wb(h->enc[l + 1].wqkv), base + pw + pfe, st));
+            if (h->enc[l].qkv_next && xv) {   // lo plane of the next layer's Wqkv; only its v rows are packed
+                const size_t n = (size_t)3 * D * D;
+                HIP_TRY(h->xw_tmp.ensure(3 * n * sizeof(bf16)));
+                HIP_TRY(pfm_split3_planes(h->w(h->enc[l + 1].wqkv), h->xw_tmp.as<bf16>(), (long long)n, (long long)n, st));
+                HIP_TRY(pfm_ffn2_pack_qkv_v(h->xw_tmp.as<bf16>() + n, base + pw + pfe + 3 * po, st));
+            }
         }
         h->ffn_ready = true;
     }
@@ -827,6 +910,22 @@ struct Run {
             return gemm_x6(h, (const float*)A, am, (const float*)Wt, Mm, N, Kk, e, s);
         return gemm_dispatch(dtp, A, am, Wt, ldw, Mm, N, Kk, e, s);
     }
+    // fast mode, PFM_FAST_XW: bf16 A [Mm, Kk] times a weight kept as two bf16 planes (planes: [hi | lo], `plane`
+    // elements apart, rows of ldw): the 256-tile kernel's split-weight mode, K' = 2 Kk (2 M N K algorithmic flops)
+    hipError_t gemm_xw(const void* A, RowMap am, const bf16* planes, long long ldw, long long plane, int Mm, int N,
+                       int Kk, const GemmEpi& e, hipStream_t s = nullptr) const {
+        if (!s) s = st;
+        const double fl = 2.0 * Mm * N * Kk;
+        const double by = ((double)Mm * Kk + 2.0 * N * Kk) * 2.0 +
+                          (double)Mm * N * (e.out ? (e.out_dtype == DT_F32 ? 4.0 : 2.0) : 0.0) +
+                          (e.res0 ? (e.res0_bf16 ? 2.0 : 4.0) * Mm * N : 0.0) + (e.res1 ? 4.0 * Mm * N : 0.0);
+        ProfScope ps(h, s, PFM_K_GEMM, fl, by);
+        GemmEpi e2 = e;
+        e2.x6_k = Kk;
+        e2.x6_ws = plane;
+        e2.x6_terms = 2;
+        return pfm_gemm_bf16_256(A, am, planes, ldw, Mm, N, 2 * Kk, e2, s);
+    }
     // A = LN(x) g + b, then the GEMM: chunk-sized fast-mode steps (<= 64 rows, K 512) run both in one skinny kernel
     // (the rows normalised into LDS, k_gemm_skinny.hip); otherwise the LayerNorm writes `xn` (layout xnm, the GEMM's
     // operand dtype) and the GEMM reads it
@@ -965,9 +1064,14 @@ int encoder_stack(const Run& r, const float* x_in, const int* lens, int B, int T
     const bool pad0 = fast && !r.raw_input && !r.ck && I % 64 && h->qkv0_pad.p && l0 == 0;
     const int lndt = x3 ? DT_X3 : dt;
     bool qkv_ready = false;   // the previous layer's fused FFN kernel already wrote this layer's q|k|v (QKVb)
+    // PFM_FAST_XW bit 2: layer 0 with split-plane weights, unfused (offline full batches on the fused path only)
+    const int xw = fast && !r.ck && !r.raw_input && ffn_fused && h->xw_ready ? h->xw_kind : 0;
+    const bool xw0 = (xw & 2) && l0 == 0 && pad0;
     for (int l = l0; l < l1; ++l) {
         const EncLayer& L = h->enc[l];
         const int din = L.din;
+        // the previous layer's fused kernel wrote this layer's LN1 (and, MODE 4/5, its q|k|v)
+        const bool prev_fused = ffn_fused && l > l0 && !(xw0 && l == 1);
         if (l == 0 && r.raw_input)   // streaming: the window already holds x sqrt(d) + PE
             HIP_TRY(pfm_layernorm(x_in, rowmap_plain(I), (int)M, I, r.P(L.ln1g), r.P(L.ln1b), c.ln_eps, nullptr, 0,
                                   1.f, Xn, rowmap_plain(I), dt, nullptr, plain, 0, st));
@@ -980,11 +1084,21 @@ int encoder_stack(const Run& r, const float* x_in, const int* lens, int B, int T
             HIP_TRY(pfm_layernorm(x_in, rowmap_plain(I), (int)M, I, r.P(L.ln1g), r.P(L.ln1b), c.ln_eps,
                                   h->pe.as<float>(), T, sqrtf((float)D), Xn, rowmap_plain(I), dt, nullptr, plain, 0,
                                   st));
-        else if (!(ffn_fused && l > l0) && (x3 || !fast))   // fused FFN: the previous layer's kernel wrote LN1(x)
+        else if (!prev_fused && (x3 || !fast))   // fused FFN: the previous layer's kernel wrote LN1(x)
             HIP_TRY(pfm_layernorm(X, rowmap_plain(D), (int)M, D, r.P(L.ln1g), r.P(L.ln1b), c.ln_eps, nullptr, 0, 1.f,
                                   Xn, xmap3, lndt, nullptr, plain, 0, st));
+        // layer 1 behind the split-weight layer 0, v rows with split weights too: LN1 -> Xn, then the 2-plane GEMM
+        if (xw0 && l == 1 && (xw & 4) && !qkv_ready) {
+            HIP_TRY(pfm_layernorm(X, rowmap_plain(D), (int)M, D, r.P(L.ln1g), r.P(L.ln1b), c.ln_eps, nullptr, 0, 1.f,
+                                  Xn, rowmap_plain(D), DT_BF16, nullptr, plain, 0, st));
+            GemmEpi e = epi_default();
+            e.bias = r.P(L.bqkv);
+            e.out = QKVb; e.out_map = rowmap_plain(3 * D); e.out_dtype = DT_BF16;
+            HIP_TRY(r.gemm_xw(Xn, rowmap_plain(din), h->xw_qkv1.as<bf16>(), din, 3LL * D * din, (int)M, 3 * D, din, e));
+            qkv_ready = true;
+        }
         // fast mode, l > 0 without the fused FFN in front: LN1 and the QKV projection through Run::ln_gemm
-        const bool ln1_fold = l > 0 && fast && !x3 && !(ffn_fused && l > l0);
+        const bool ln1_fold = l > 0 && fast && !x3 && !prev_fused;
         bool kv_built = false;   // streaming: the QKV launch also wrote the key buffer and the FSMN block
         if (!qkv_ready && ln1_fold) {
             GemmEpi e = epi_default();
@@ -1013,6 +1127,9 @@ int encoder_stack(const Run& r, const float* x_in, const int* lens, int B, int T
             else { e.out = QKV; e.out_map = rowmap_plain(3 * D); e.out_dtype = DT_F32; }
             if (x3 && l > 0) {
                 HIP_TRY(r.gemm3(Xn, xmap3, r.W(L.wqkv), din, (int)M, 3 * D, din, e));
+            } else if (l == 0 && xw0) {
+                HIP_TRY(r.gemm_xw(Xn, rowmap_plain(Kp0), h->xw_qkv0.as<bf16>(), Kp0, 3LL * D * Kp0, (int)M, 3 * D, Kp0,
+                                  e));
             } else if (l == 0 && pad0) {
                 HIP_TRY(r.gemm(dt, Xn, rowmap_plain(Kp0), h->qkv0_pad.p, Kp0, (int)M, 3 * D, Kp0, e));
             } else {
@@ -1080,6 +1197,33 @@ int encoder_stack(const Run& r, const float* x_in, const int* lens, int B, int T
                 HIP_TRY(r.attn(DT_F32, QKV, rowmap_plain(3 * D), QKV + D, rowmap_plain(3 * D), QKV + 2 * D,
                                rowmap_plain(3 * D), O, D, nullptr, lens, B, T, T));
         }
+        if (xw0 && l == 0) {   // layer 0, split-plane weights, unfused: x1 = O Wo + bo + F (no residual: in 560,
+                               // out 512), h = relu(LN2(x1) W1 + b1), x = x1 + h W2 + b2 (encoder.py:120-145)
+            {
+                GemmEpi e = epi_default();
+                e.bias = r.P(L.bo);
+                e.res0 = (const float*)Fb; e.ld_res0 = D; e.res0_bf16 = 1;
+                if (din == D) { e.res1 = X; e.ld_res1 = D; }
+                e.out = X; e.out_map = rowmap_plain(D); e.out_dtype = DT_F32;
+                HIP_TRY(r.gemm_xw(Ob, rowmap_plain(D), h->xw_wo0.as<bf16>(), D, (long long)D * D, (int)M, D, D, e));
+            }
+            HIP_TRY(pfm_layernorm(X, rowmap_plain(D), (int)M, D, r.P(L.ln2g), r.P(L.ln2b), c.ln_eps, nullptr, 0, 1.f,
+                                  Xn, rowmap_plain(D), DT_BF16, nullptr, plain, 0, st));
+            {
+                GemmEpi e = epi_default();
+                e.bias = r.P(L.b1); e.relu = 1;
+                e.out = Hh; e.out_map = rowmap_plain(Fd); e.out_dtype = DT_BF16;
+                HIP_TRY(r.gemm_xw(Xn, rowmap_plain(D), h->xw_w10.as<bf16>(), D, (long long)Fd * D, (int)M, Fd, D, e));
+            }
+            {
+                GemmEpi e = epi_default();
+                e.bias = r.P(L.b2);
+                e.res0 = X; e.ld_res0 = D;
+                e.out = X; e.out_map = rowmap_plain(D); e.out_dtype = DT_F32;
+                HIP_TRY(r.gemm_xw(Hh, rowmap_plain(Fd), h->xw_w20.as<bf16>(), Fd, (long long)D * Fd, (int)M, D, Fd, e));
+            }
+            continue;
+        }
         // fast mode, full batches: the out-projection runs inside the fused FFN kernel (its phase 0)
         const bool ffn_op = ffn_fused && !r.ck && pfm_knobs().ffn_op;
         if (!ffn_op) {   // x = (x +) linear_out(att) + fsmn   (encoder.py:120-137: no residual when in != out)
@@ -1109,17 +1253,27 @@ int encoder_stack(const Run& r, const float* x_in, const int* lens, int B, int T
                     const EncLayer& N = h->enc[l + 1];
                     ProfScope ps(h, st, PFM_K_GEMM, flo + 6.0 * M * (double)D * D,
                                  byo + (double)M * D * (6.0 - 2.0) + 6.0 * D * D, PFM_K_FFN2);
-                    HIP_TRY(pfm_ffn2_fused_op_qkv(Ob, Fb, r.P(L.bo), din == D ? X : nullptr, (int)M, r.P(L.ln2g),
-                                                  r.P(L.ln2b), c.ln_eps, h->ffn_pack.as<bf16>() + L.ffp - pfm_ffn_packed_o_elems(),
-                                                  r.P(L.b1), r.P(L.b2), X, r.P(N.ln1g), r.P(N.ln1b), r.P(N.bqkv), QKVb, st));
+                    // PFM_FAST_XW bit 4: MODE 5 (the v rows' lo-plane fragments packed behind the QKV passes); bit 8:
+                    // MODE 6 (Wo's two planes in front)
+                    const bf16* wop = h->ffn_pack.as<bf16>() + L.opp;
+                    if (xw & 4)
+                        HIP_TRY(pfm_ffn2_fused_op_qkv_xv(Ob, Fb, r.P(L.bo), din == D ? X : nullptr, (int)M, r.P(L.ln2g),
+                                                         r.P(L.ln2b), c.ln_eps, wop, r.P(L.b1), r.P(L.b2), X,
+                                                         r.P(N.ln1g), r.P(N.ln1b), r.P(N.bqkv), QKVb, (xw & 8) != 0,
+                                                         st));
+                    else
+                        HIP_TRY(pfm_ffn2_fused_op_qkv(Ob, Fb, r.P(L.bo), din == D ? X : nullptr, (int)M, r.P(L.ln2g),
+                                                      r.P(L.ln2b), c.ln_eps, wop, r.P(L.b1), r.P(L.b2), X, r.P(N.ln1g),
+                                                      r.P(N.ln1b), r.P(N.bqkv), QKVb, st));
                     qkv_ready = true;
                     continue;
                 }
                 ProfScope ps(h, st, PFM_K_GEMM, flo, byo);
-                HIP_TRY((h->ffn_kind == 2 ? pfm_ffn2_fused_op : pfm_ffn_fused_op)(Ob, Fb, r.P(L.bo), din == D ? X : nullptr, (int)M, r.P(L.ln2g), r.P(L.ln2b),
-                                         c.ln_eps, h->ffn_pack.as<bf16>() + L.ffp - pfm_ffn_packed_o_elems(), r.P(L.b1),
-                                         r.P(L.b2), X, nxt ? r.P(h->enc[l + 1].ln1g) : nullptr,
-                                         nxt ? r.P(h->enc[l + 1].ln1b) : nullptr, nxt ? (bf16*)Xn : nullptr, st));
+                HIP_TRY(((xw & 8) && h->ffn_kind == 2 ? pfm_ffn2_fused_op_xo
+                         : h->ffn_kind == 2 ? pfm_ffn2_fused_op : pfm_ffn_fused_op)(
+                    Ob, Fb, r.P(L.bo), din == D ? X : nullptr, (int)M, r.P(L.ln2g), r.P(L.ln2b), c.ln_eps,
+                    h->ffn_pack.as<bf16>() + L.opp, r.P(L.b1), r.P(L.b2), X, nxt ? r.P(h->enc[l + 1].ln1g) : nullptr,
+                    nxt ? r.P(h->enc[l + 1].ln1b) : nullptr, nxt ? (bf16*)Xn : nullptr, st));
                 continue;
             }
             ProfScope ps(h, st, PFM_K_GEMM, fl, by);
@@ -1470,7 +1624,11 @@ int pfm_run(pfm_handle* h, void* stream, int mode, const float* feats, const int
         e.bias = P(h->cif_b); e.relu = 1;
         e.out = h->Hc.p; e.out_map = rowmap_plain(D); e.out_dtype = DT_F32;
         const void* A = fast ? (const void*)encpb : (const void*)encp;
-        HIP_TRY(GEMM(dt, A, rowmap_seg(T, (long long)(T + 2) * D, D), W(h->cif_w), 3 * D, (int)M, D, 3 * D, e));
+        if (fast && h->xw_ready && (h->xw_kind & 1))   // PFM_FAST_XW bit 1: the conv weights as two bf16 planes
+            HIP_TRY(run.gemm_xw(A, rowmap_seg(T, (long long)(T + 2) * D, D), h->xw_pred.as<bf16>(), 3 * D,
+                                3LL * D * D, (int)M, D, 3 * D, e));
+        else
+            HIP_TRY(GEMM(dt, A, rowmap_seg(T, (long long)(T + 2) * D, D), W(h->cif_w), 3 * D, (int)M, D, 3 * D, e));
     }
     float* alphas = h->alphas.as<float>();
     float* peaks = h->peaks.as<float>();
@@ -1946,6 +2104,12 @@ int pfm_op_gemm(void* stream, int dtype, const void* A, const void* Wt, const fl
     e.bias = bias; e.relu = act & 1;
     if (res) { e.res0 = res; e.ld_res0 = N; }
     e.out = C; e.out_map = rowmap_plain(N); e.out_dtype = (act & 2) ? DT_BF16 : DT_F32;
+    if (act & 4) {   // split weights: Wt = two bf16 planes [2][N][K] (fast mode's PFM_FAST_XW projections)
+        if (dtype != DT_BF16 || K % 64) return fail(PFM_E_ARG, "pfm_op_gemm: split weights need bf16 and K % 64 == 0");
+        e.x6_k = K; e.x6_ws = (long long)N * K; e.x6_terms = 2;
+        HIP_TRY(pfm_gemm_bf16_256(A, rowmap_plain(K), Wt, K, M, N, 2 * K, e, (hipStream_t)stream));
+        return PFM_OK;
+    }
     HIP_TRY(gemm_dispatch(dtype, A, rowmap_plain(K), Wt, K, M, N, K, e, (hipStream_t)stream));
     return PFM_OK;
 }
@@ -2070,16 +2234,32 @@ int pfm_op_ffn_op_qkv(void* stream, const void* o, const void* f, const float* W
     HIP_TRY(sc.alloc(&w2b, nw));
     HIP_TRY(sc.alloc(&wob, no));
     HIP_TRY(sc.alloc(&wqb, 3 * no));
-    HIP_TRY(sc.alloc(&wp, po + pfe + 3 * po));
+    // PFM_FAST_XW: bit 4 = MODE 5 (the v rows of Wq as two bf16 planes), bit 8 = MODE 6 (Wo too)
+    const bool xv = (pfm_knobs().fast_xw & 4) != 0, xop = (pfm_knobs().fast_xw & 8) != 0;
+    const size_t pw = (xop ? 2 : 1) * po;
+    HIP_TRY(sc.alloc(&wp, pw + pfe + (xv ? 4 : 3) * po));
     HIP_TRY(pfm_f32_to_bf16(W1, w1b, (long long)nw, st));
     HIP_TRY(pfm_f32_to_bf16(W2, w2b, (long long)nw, st));
     HIP_TRY(pfm_f32_to_bf16(Wo, wob, (long long)no, st));
     HIP_TRY(pfm_f32_to_bf16(Wq, wqb, (long long)(3 * no), st));
     HIP_TRY(pfm_ffn2_pack_o(wob, wp, st));
-    HIP_TRY(pfm_ffn2_pack(w1b, w2b, wp + po, st));
-    HIP_TRY(pfm_ffn2_pack_qkv(wqb, wp + po + pfe, st));
-    HIP_TRY(pfm_ffn2_fused_op_qkv((const bf16*)o, (const bf16*)f, bo, x, M, g2, b2n, eps, wp, b1, b2, xo, gn, bn, bq,
-                                  (bf16*)qkv, st));
+    bf16* pl;
+    HIP_TRY(sc.alloc(&pl, 9 * no));
+    if (xop) {
+        HIP_TRY(pfm_split3_planes(Wo, pl, (long long)no, (long long)no, st));
+        HIP_TRY(pfm_ffn2_pack_o(pl + no, wp + po, st));
+    }
+    HIP_TRY(pfm_ffn2_pack(w1b, w2b, wp + pw, st));
+    HIP_TRY(pfm_ffn2_pack_qkv(wqb, wp + pw + pfe, st));
+    if (xv) {
+        HIP_TRY(pfm_split3_planes(Wq, pl, (long long)(3 * no), (long long)(3 * no), st));
+        HIP_TRY(pfm_ffn2_pack_qkv_v(pl + 3 * no, wp + pw + pfe + 3 * po, st));
+        HIP_TRY(pfm_ffn2_fused_op_qkv_xv((const bf16*)o, (const bf16*)f, bo, x, M, g2, b2n, eps, wp, b1, b2, xo, gn, bn,
+                                         bq, (bf16*)qkv, xop, st));
+    } else {
+        HIP_TRY(pfm_ffn2_fused_op_qkv((const bf16*)o, (const bf16*)f, bo, x, M, g2, b2n, eps, wp, b1, b2, xo, gn, bn, bq,
+                                      (bf16*)qkv, st));
+    }
     HIP_TRY(hipStreamSynchronize(st));
     return PFM_OK;
 }

@@ -102,7 +102,8 @@ struct GemmEpi {
     // ([M, 3 x6_k], x = x0 + x1 + x2 exactly), W = three bf16 planes x6_ws elements apart; the kernel runs
     // K' = 6 x6_k over the segments (A2,W0) (A1,W1) (A0,W2) (A1,W0) (A0,W1) (A0,W0). 0 = plain GEMM.
     // x6_terms 3 (bf16x3): only the last three segments (A1,W0) (A0,W1) (A0,W0), K' = 3 x6_k (relative
-    // error ~2^-16 instead of ~2^-24); 0 / 6 = all six.
+    // error ~2^-16 instead of ~2^-24); 0 / 6 = all six. x6_terms 2 (fast mode, precise weights): A is ONE bf16
+    // operand [M, x6_k], W = w0 + w1 two planes x6_ws apart, K' = 2 x6_k over (A, W1) (A, W0).
     int x6_k;
     long long x6_ws;
     int x6_terms;
@@ -145,8 +146,15 @@ struct PfmKnobs {
                             // the next layer's QKV projection folded in); 1 = 64-row workgroups (k_ffn.hip)
     int ffn_qkv;            // PFM_FFN_QKV (default 1): with the 128-row fused FFN, the next layer's QKV projection as
                             // its phase 3 (k_ffn2.hip MODE 4; the separate LN1 + QKV GEMM otherwise)
+    int fast_xw;            // PFM_FAST_XW (bitmask, default 7): fast mode keeps these weights as two bf16 planes
+                            // w = w0 + w1 (~2^-17 relative; activations stay bf16): 1 = the CIF predictor conv,
+                            // 2 = encoder layer 0 (QKV, out-projection, FFN; runs unfused), 4 = the v rows of every
+                            // QKV projection (ffn2_kernel MODE 5), 8 = every encoder out-projection (MODE 6 / 3;
+                            // implies 4). tools/fast_emul.py: the weights' bf16 rounding, not the activations', is
+                            // what moves the fast path's decisions off the reference's (7: B=64 flips 25 -> 10 %,
+                            // +3-5 % step; 15: 5 %, +9 %)
     unsigned long long sig;
 };
-#define PFM_KNOB_FIELDS 17
+#define PFM_KNOB_FIELDS 18
 const PfmKnobs& pfm_knobs();   // the calling thread's snapshot (refreshed lazily if no entry point did yet)
 void pfm_knobs_refresh();

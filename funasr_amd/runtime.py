@@ -568,13 +568,14 @@ def op_ln_gemm(X, g, b, eps, W, bias=None, res=None, relu=False, out_bf16=False)
 
 
 def op_gemm(A, W, bias=None, res=None, relu=False, out_bf16=False):
+    """W [N, K], or [2, N, K] bf16 planes (w = w0 + w1: the split-weight GEMM of PFM_FAST_XW)."""
     import torch
     lib = load_library()
     dt = PFM_BF16 if A.dtype == torch.bfloat16 else PFM_F32
     M, K = A.shape
-    N = W.shape[0]
+    N = W.shape[-2]
     C = torch.empty((M, N), dtype=torch.bfloat16 if out_bf16 else torch.float32, device=A.device)
-    act = (1 if relu else 0) | (2 if out_bf16 else 0)
+    act = (1 if relu else 0) | (2 if out_bf16 else 0) | (4 if W.dim() == 3 else 0)
     check(lib.pfm_op_gemm(_stream_ptr(torch, A.device), dt, _ptr(A.contiguous()), _ptr(W.contiguous()), _ptr(bias),
                           _ptr(res), _ptr(C), M, N, K, act), "pfm_op_gemm")
     return C

@@ -353,7 +353,8 @@ int pfm_profile_read(pfm_handle* h, int kclass, double* ms, double* flops, doubl
 
 /* C[M,N] = act(A[M,K] . W[N,K]^T + bias) (+ res), dtype of A/W = PFM_F32 or PFM_BF16.
  * act bit 0: relu; act bit 1: C is bf16 (bf16 operands only; the fast-mode QKV / FFN1 output
- * form), otherwise C is f32. */
+ * form), otherwise C is f32; act bit 2: W is two bf16 planes [2][N][K], w = w0 + w1 (fast mode's split-weight
+ * projections, PFM_FAST_XW; K % 64 == 0). */
 int pfm_op_gemm(void* stream, int dtype, const void* A, const void* W, const float* bias,
                 const float* res, float* C, int M, int N, int K, int act);
 
@@ -387,7 +388,7 @@ int pfm_op_ffn_op(void* stream, const void* o, const void* f, const float* Wo, c
 /* pfm_op_ffn_op followed by the next encoder layer's q|k|v projection in the same launch, as the fast path runs it
  * with the 128-row fused FFN (k_ffn2.hip MODE 4): x2 -> xo (f32) and qkv = LN1_next(x2) Wq^T + bq, bf16
  * [M, 1536] (Wq f32 [1536][512], bq [1536]; the next layer's attention.py:180-186 linear_q_k_v on its norm1).
- * Synchronous. */
+ * With PFM_FAST_XW bit 4 set the v rows of Wq are used as two bf16 planes (MODE 5). Synchronous. */
 int pfm_op_ffn_op_qkv(void* stream, const void* o, const void* f, const float* Wo, const float* bo, const float* x,
                       int M, const float* g2, const float* b2n, float eps, const float* W1, const float* b1,
                       const float* W2, const float* b2, float* xo, const float* gn, const float* bn, const float* Wq,

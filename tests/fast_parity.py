@@ -72,3 +72,38 @@ def _summary(reg, rank, k) -> dict:
                 max_regret=float(reg.max()) if len(reg) else 0.0,
                 second_best=float((rank[flips] == 1).mean()) if nf else 1.0,
                 outside_topk=int((rank >= k).sum()))
+
+
+def bounds_from_emulation(em: dict) -> dict:
+    """Fast-mode bounds derived from the CPU emulation of the same rounding points (tools/fast_emul.py: the oracle with
+    the fast path's bf16 roundings on the reference's inputs, tests/golden/fast_emul.json), NOT from the kernel's own
+    output: the GPU must sit at the emulation's level -- flips within 3 points, mean regret within 1.5x (+0.001 nat),
+    choices outside the reference top 5 within 2x (at least 0.2 % of the positions), the largest regret within
+    0.15 nat, equal token counts within 5 points."""
+    pos = max(1, em["positions"])
+    return dict(flip_frac=em["flip_frac"] + 0.03, mean_regret=1.5 * em["mean_regret"] + 0.001,
+                outside_frac=max(2.0 * em["outside_topk"] / pos, 0.002), max_regret=em["max_regret"] + 0.15,
+                equal_counts=em["equal_counts"] - 0.05)
+
+
+def stream_stats(chunks, g, margin: float) -> dict:
+    """Streaming: chunks = [(per-position argmax ids of a chunk (specials included), count)] in order; g a streaming
+    golden with the reference's per-chunk decoder counts (ntok) and per-position top-k (top_ids / top_logp, chunks
+    concatenated). Chunks whose counts differ are compared up to their first break, as paraformer_stats does."""
+    off = np.concatenate([[0], np.cumsum(g["ntok"])]).astype(np.int64)
+    k = g["top_ids"].shape[1]
+    reg_all, rank_all, equal = [], [], 0
+    for i, (ids, n_got) in enumerate(chunks):
+        n_ref = int(g["ntok"][i])
+        n = min(n_ref, int(n_got))
+        r, rk = regrets(np.asarray(ids[:n], np.int64), g["top_ids"][off[i]:off[i] + n], g["top_logp"][off[i]:off[i] + n])
+        if n_ref == int(n_got):
+            equal += 1
+        else:
+            brk = np.nonzero((rk >= k) | (r >= margin))[0]
+            cut = int(brk[0]) if len(brk) else n
+            r, rk = r[:cut], rk[:cut]
+        reg_all.append(r)
+        rank_all.append(rk)
+    reg, rank = np.concatenate(reg_all), np.concatenate(rank_all)
+    return _summary(reg, rank, k) | dict(equal_counts=equal / max(1, len(chunks)))

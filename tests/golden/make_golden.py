@@ -893,6 +893,107 @@ def save_stream_beam():
     print("wave", texts)
 
 
+def save_stream_large():
+    """ParaformerStreaming at Paraformer-large size, greedy (config C5's model), look-back 4 / 1, 24 seeded chunks
+    of 10 rows + a final 4-row chunk through the reference generate_chunk: per chunk the token ids, and per decoded
+    position the decoder's top-5 log-probs (cal_decoder_with_predictor_chunk, paraformer_streaming/model.py:427-433)
+    for the fast-mode regret statistics (tests/fast_parity.py)."""
+    from funasr_amd.config import paraformer_streaming
+    cfg = paraformer_streaming()
+    m = build_stream_ref(cfg)
+    rows = []
+    dec = m.cal_decoder_with_predictor_chunk
+
+    def spy(*a, **k):
+        r = dec(*a, **k)
+        lp, n = r[0].detach(), int(r[1][0]) if r[1] is not None else r[0].shape[1]
+        v, i = torch.topk(lp[0, :n], 5, dim=-1)
+        rows.append((i.numpy().astype(np.int32), v.numpy().astype(np.float32)))
+        return r
+
+    m.cal_decoder_with_predictor_chunk = spy
+    rng = np.random.default_rng(26)
+    ns = [10] * 24 + [4]
+    chunks = [rng.standard_normal((n, 560), dtype=np.float32) for n in ns]
+    cache = _stream_cache(m, 4, 1)
+    toks, ntok, top_ids, top_lp = [], [], [], []
+    for i, x in enumerate(chunks):
+        rows.clear()
+        with torch.no_grad():
+            t = m.generate_chunk(torch.from_numpy(x.copy())[None], torch.tensor([x.shape[0]]), key=["k"],
+                                 tokenizer=_IdsTok(), cache=cache, is_final=i == len(chunks) - 1, device="cpu")
+        toks.append(t)
+        if rows:
+            top_ids.append(rows[0][0])
+            top_lp.append(rows[0][1])
+            ntok.append(rows[0][0].shape[0])
+        else:
+            ntok.append(0)
+    flat, off = pack_tokens(toks)
+    np.savez_compressed(f"{HERE}/stream_large.npz", seed=26, ns=np.array(ns, np.int32), tokens=flat, tokens_off=off,
+                        ntok=np.array(ntok, np.int32),
+                        top_ids=np.concatenate(top_ids) if top_ids else np.zeros((0, 5), np.int32),
+                        top_logp=np.concatenate(top_lp) if top_lp else np.zeros((0, 5), np.float32))
+    print("stream large: tokens per chunk", [len(t) for t in toks], "positions", sum(ntok))
+
+
+def save_stream_beam_large():
+    """Config C5 as benched: ParaformerStreaming at Paraformer-large size with a CTC head (ctc_weight 0.3), chunk
+    [0, 10, 5], look-back 4 / 1, decoded per chunk by the reference's joint decoder + CTC prefix beam search
+    (generate_chunk, decoding_ctc_weight 0.3, beam 10, nbest 2; paraformer_streaming/model.py:510-552, 567-575) on
+    six seeded LFR+CMVN-like chunks and a final tail chunk. Per chunk: generate_chunk's ids and, from beam_search()
+    itself, the n-best yseqs and scores, plus the decoder's per-position argmax / top-2 margin (diagnostics)."""
+    import dataclasses
+    from funasr_amd.config import paraformer_streaming
+    import funasr.models.scama.encoder  # noqa: F401
+    import funasr.models.paraformer_streaming.model  # noqa: F401
+    cfg = dataclasses.replace(paraformer_streaming(), ctc_weight=0.3)
+    kw = cfg.reference_kwargs()
+    m = tables.model_classes["ParaformerStreaming"](
+        **{k: kw[k] for k in ("encoder", "encoder_conf", "decoder", "decoder_conf", "predictor", "predictor_conf")},
+        input_size=cfg.input_size, vocab_size=cfg.vocab_size, ctc_weight=0.3, predictor_bias=1)
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in make_weights(cfg, seed=0).items()}, strict=True)
+    m.eval()
+    toks = token_list(cfg.vocab_size)
+    elb, dlb, wctc, beam, pen, nbest = 4, 1, 0.3, 10, 0.0, 2
+    m.init_beam_search(token_list=toks, decoding_ctc_weight=wctc, beam_size=beam, penalty=pen)
+    m.nbest = nbest
+    calls = []
+    fwd = m.beam_search.forward
+
+    def spy(*a, **k):
+        r = fwd(*a, **k)
+        calls[-1].append([(h.yseq.tolist(), float(h.score)) for h in r[:nbest]])
+        return r
+
+    m.beam_search.forward = spy
+    rng = np.random.default_rng(25)
+    chunks = [rng.standard_normal((10, 560), dtype=np.float32) for _ in range(6)]
+    cache = _stream_cache(m, elb, dlb)
+    ids, hyps = [], []
+    seq = chunks + [None]
+    for i, x in enumerate(seq):
+        fin = i == len(seq) - 1
+        if x is None:
+            cache["encoder"]["tail_chunk"] = True
+            t = cache["encoder"]["feats"]
+        else:
+            t = torch.from_numpy(x.copy())[None]
+        calls.append([])
+        with torch.no_grad():
+            ids.append(m.generate_chunk(t, torch.tensor([t.shape[1]]), key=["k"], tokenizer=_IdsTok(), cache=cache,
+                                        is_final=fin, device="cpu", maxlenratio=0.0, minlenratio=0.0))
+        hyps.append(calls[-1][0] if calls[-1] else [])
+        print("chunk", i, "ids", len(ids[-1]), "hyps", [(len(y), round(sc, 3)) for y, sc in hyps[-1]], flush=True)
+    flat, off = pack_tokens(ids)
+    yseq = [y for hs in hyps for (y, _) in hs]
+    yflat, yoff = pack_tokens(yseq)
+    np.savez_compressed(f"{HERE}/stream_beam_large.npz", seed=25, chunks=np.stack(chunks), ids=flat, ids_off=off,
+                        yseq=yflat, yseq_off=yoff, scores=np.array([sc for hs in hyps for (_, sc) in hs], np.float32),
+                        nhyp=np.array([len(hs) for hs in hyps], np.int32),
+                        opts=np.array([elb, dlb, beam, nbest, 1], np.int32), fopts=np.array([wctc, pen], np.float32))
+
+
 PUNC_TEXTS = {
     "short": 12,            # CJK tokens only, one mini-sentence
     "mixed": 47,            # CJK + ASCII words (split_words keeps ASCII runs as one word; unknown -> <unk>)

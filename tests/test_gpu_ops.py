@@ -387,6 +387,57 @@ def test_ffn_fused_outproj_qkv(dev, M, eps):
     assert rel(qkv.double().cpu(), qw) < 5e-3
 
 
+@pytest.mark.parametrize("M", [200, 4100])
+@pytest.mark.parametrize("xw", [4, 8])
+def test_ffn_fused_outproj_qkv_split_v(dev, monkeypatch, M, xw):
+    """MODE 5 (PFM_FAST_XW bit 4): MODE 4 with the v rows of Wq as two bf16 planes w0 + w1 (~2^-17 relative).
+    q | k as MODE 4 (bf16 weights); v within the bf16 output's rounding of fp64 with the f32 weights, and clearly
+    closer to it than to the bf16-weight product (the lo plane is applied). MODE 6 (bit 8): Wo split too -- x2
+    within 1e-4 of fp64 with the f32 Wo (the f32 residual stream shows the out-projection's precision)."""
+    monkeypatch.setenv("PFM_FAST_XW", str(xw))
+    g = torch.Generator().manual_seed(29 * M)
+    p = _ffn_params(g)
+    Wq, bq = torch.randn(1536, 512, generator=g) / 512 ** 0.5, 0.1 * torch.randn(1536, generator=g)
+    x = torch.randn(M, 512, generator=g) * 2
+    o = torch.randn(M, 512, generator=g).bfloat16()
+    f = (0.5 * torch.randn(M, 512, generator=g)).bfloat16()
+    d = lambda t: None if t is None else t.to(dev)  # noqa: E731
+    x2, qkv = rt.op_ffn_op_qkv(d(o), d(f), d(p["Wo"]), d(p["bo"]), d(x), d(p["g2"]), d(p["b2n"]), 1e-12, d(p["W1"]),
+                               d(p["b1"]), d(p["W2"]), d(p["b2"]), d(p["gn"]), d(p["bn"]), d(Wq), d(bq))
+    torch.cuda.synchronize()
+    if xw & 8:
+        x1 = o.double() @ p["Wo"].double().T + p["bo"].double() + f.double() + x.double()
+        want = _ffn_ref(x1, p["g2"], p["b2n"], 1e-12, p["W1"].bfloat16(), p["b1"], p["W2"].bfloat16(), p["b2"])
+        x1b = o.double() @ p["Wo"].bfloat16().double().T + p["bo"].double() + f.double() + x.double()
+        assert rel(x2.double().cpu(), want) < 1e-4
+        assert rel(x2.double().cpu() - x1b, want - x1b) < 5e-3 and rel(x1, x1b) > 1e-4
+    a = _ln64(x2.double().cpu(), p["gn"], p["bn"], 1e-12).bfloat16().double()
+    got = qkv.double().cpu()
+    qk_bf = a @ Wq[:1024].bfloat16().double().T + bq[:1024].double()
+    assert rel(got[:, :1024], qk_bf) < 5e-3
+    v_exact = a @ Wq[1024:].double().T + bq[1024:].double()
+    v_bf = a @ Wq[1024:].bfloat16().double().T + bq[1024:].double()
+    e_exact, e_bf = rel(got[:, 1024:], v_exact), rel(got[:, 1024:], v_bf)
+    print(f"MODE 5 v rows: rel-L2 vs f32 weights {e_exact:.2e}, vs bf16 weights {e_bf:.2e}")
+    assert e_exact < 5e-3 and e_exact < 0.85 * e_bf
+
+
+@pytest.mark.parametrize("M,N,K", [(100, 512, 576), (4096, 1536, 512), (777, 512, 2048)])
+def test_gemm_split_weights(dev, M, N, K):
+    """The split-weight GEMM (x6_terms 2: bf16 A times w = w0 + w1, two bf16 planes) vs fp64 of the same operands:
+    the products are exact, so rel < 1e-5 (f32 accumulation); relu + bias and the residual epilogue."""
+    g = torch.Generator().manual_seed(M + N + K)
+    A = torch.randn(M, K, generator=g).bfloat16()
+    W = torch.randn(N, K, generator=g) / K ** 0.5
+    w0 = W.bfloat16()
+    w1 = (W - w0.float()).bfloat16()
+    bias, res = torch.randn(N, generator=g), torch.randn(M, N, generator=g)
+    C = rt.op_gemm(A.to(dev), torch.stack([w0, w1]).to(dev), bias=bias.to(dev), res=res.to(dev), relu=True)
+    torch.cuda.synchronize()
+    want = torch.relu(A.double() @ (w0.double() + w1.double()).T + bias.double()) + res.double()
+    assert rel(C.double().cpu(), want) < 1e-5
+
+
 def _dec_ffn_ref(x1, p, eps=1e-12):
     """fp64 sanm/positionwise_feed_forward.py:26-33 on the kernel's roundings: a = bf16(LN1(x1)),
     h = bf16(relu(a W1^T + b1)); LN_F over the 2048 hidden folded through W2 with W2g = bf16(W2 diag(gamma_F)):

@@ -182,3 +182,79 @@ def test_stream_beam_bad_args(eng):
     e2.load_state_dict(make_weights(plain, seed=0))
     with pytest.raises(PfmError):
         PfmStreams(e2, 1, (0, 10, 5), 0, 0, "exact").step_beam([0], x, [10], [False])
+
+
+@pytest.fixture(scope="module")
+def eng_large():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from funasr_amd.config import paraformer_streaming
+    from funasr_amd.runtime import PfmEngine
+    cfg = dataclasses.replace(paraformer_streaming(), ctc_weight=0.3)
+    e = PfmEngine(cfg, 0)
+    e.load_state_dict(make_weights(cfg, seed=0))
+    return cfg, e
+
+
+def _large_chunks(e, mode, g):
+    from funasr_amd.runtime import PfmStreams
+    elb, dlb, beam, nbest, tail = g["opts"].tolist()
+    wctc, pen = g["fopts"].tolist()
+    s = PfmStreams(e, 1, (0, 10, 5), elb, dlb, mode)
+    seq = list(g["chunks"]) + ([None] if tail else [])
+    out = []
+    for i, x in enumerate(seq):
+        fin = i == len(seq) - 1
+        feats = None if x is None else torch.from_numpy(np.ascontiguousarray(x[None])).cuda()
+        r = s.step_beam([0], feats, [0 if x is None else x.shape[0]], [fin], beam=beam, ctc_weight=wctc, penalty=pen,
+                        nbest=nbest)
+        torch.cuda.synchronize()
+        r = {k: v.cpu() for k, v in r.items()}
+        out.append((_hyps(r, 0), r["scores"][0].numpy()))
+    return out
+
+
+def _large_want(g, i):
+    yoff, nh = g["yseq_off"], g["nhyp"]
+    hoff = np.concatenate([[0], np.cumsum(nh)])
+    large_drop = (0, 1, 2)
+    hyps = [[t for t in g["yseq"][yoff[q]:yoff[q + 1]][1:-1].tolist() if t not in large_drop]
+            for q in range(hoff[i], hoff[i + 1])]
+    return hyps, g["scores"][hoff[i]:hoff[i + 1]]
+
+
+def test_stream_beam_large_exact_vs_reference(eng_large):
+    """Config C5 as benched, EXACT mode: Paraformer-large streaming with a CTC head, beam 10, decoding_ctc_weight 0.3,
+    look-back 4 / 1: every chunk's n-best (nbest 2) token sequences identical to the reference generate_chunk's
+    BeamSearchPara and the scores within 1e-4 relative (tests/golden/stream_beam_large.npz, make_golden.py
+    save_stream_beam_large)."""
+    cfg, e = eng_large
+    g = np.load(f"{GOLD}/stream_beam_large.npz")
+    got = _large_chunks(e, "exact", g)
+    ioff = g["ids_off"]
+    for i, (hyps, scores) in enumerate(got):
+        want, wsc = _large_want(g, i)
+        assert hyps == want, i
+        np.testing.assert_allclose(scores[: len(want)], wsc, rtol=1e-4, atol=1e-4)
+        assert sum(hyps, []) == g["ids"][ioff[i]:ioff[i + 1]].tolist(), i
+
+
+def test_stream_beam_large_fast_close(eng_large):
+    """The same chunks in fast mode (bf16 operands): each chunk's best hypothesis scores within 0.5 of the reference's
+    best (log-prob units of the joint score; bf16 logits move it by O(0.1) per chunk) and agrees with the reference
+    1-best on >= 60 % of the positions overall; a 0.3-nat decoder bias perturbation, checked in
+    tests/test_gpu_parity.py, moves single positions by more than that."""
+    cfg, e = eng_large
+    g = np.load(f"{GOLD}/stream_beam_large.npz")
+    got = _large_chunks(e, "fast", g)
+    agree, tot, worst = 0, 0, 0.0
+    for i, (hyps, scores) in enumerate(got):
+        want, wsc = _large_want(g, i)
+        assert hyps, i
+        worst = max(worst, abs(float(scores[0]) - float(wsc[0])))
+        a, b = hyps[0], want[0]
+        tot += max(len(a), len(b))
+        agree += sum(int(x == y) for x, y in zip(a, b))
+    print(f"stream beam large fast: 1-best position agreement {agree}/{tot}, largest best-score gap {worst:.3f}")
+    assert worst < 0.5
+    assert agree >= 0.6 * tot

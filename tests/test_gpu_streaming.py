@@ -164,6 +164,36 @@ def test_stream_large_exact_vs_oracle():
         assert np.linalg.norm(d) / np.linalg.norm(ref["enc"].numpy()) < 1e-5, i
 
 
+def test_stream_large_fast_regret():
+    """Paraformer-streaming large, fast mode (bf16 operands; the chunk path keeps plain bf16 weights), 25 chunks of one
+    stream against the reference generate_chunk's per-position top-5 log-probs (tests/golden/stream_large.npz): the
+    regret bounds the offline path is held to for plain bf16 operands (the CPU emulation of ideal bf16 at B = 64,
+    tests/golden/fast_emul.json), and the token counts of >= 90 % of the chunks equal."""
+    import json
+    from tests.fast_parity import bounds_from_emulation, stream_stats
+    cfg = paraformer_streaming()
+    e, _ = _eng(cfg)
+    g = np.load(f"{GOLD}/stream_large.npz")
+    s = PfmStreams(e, 1, (0, 10, 5), 4, 1, "fast")
+    rng = np.random.default_rng(int(g["seed"]))
+    ns = g["ns"].tolist()
+    chunks = []
+    for i, n in enumerate(ns):
+        x = rng.standard_normal((n, cfg.input_size), dtype=np.float32)
+        r = s.step([0], torch.from_numpy(x[None]).cuda(), [n], [i == len(ns) - 1])
+        torch.cuda.synchronize()
+        nt = int(r["ntok"][0])
+        chunks.append((r["tokens"][0, :max(nt, 0)].cpu().numpy(), nt))
+    st = stream_stats(chunks, g, 0.5)
+    em = json.load(open(f"{GOLD}/fast_emul.json", encoding="utf-8"))["para_large_b64"]["G"]
+    b = bounds_from_emulation(em)
+    print(f"stream large fast: {st}; bounds {b}")
+    assert st["positions"] > 100
+    assert st["mean_regret"] < b["mean_regret"] and st["flip_frac"] < b["flip_frac"]
+    assert st["max_regret"] < b["max_regret"] and st["outside_topk"] <= b["outside_frac"] * st["positions"] + 1
+    assert st["equal_counts"] >= 0.9
+
+
 def test_stream_bad_args(tiny):
     from funasr_amd.runtime import PfmError
     cfg, e, _ = tiny

@@ -58,9 +58,13 @@ class Emu:
         self.wb = {}
 
     def _wscope(self, key):
-        """fine scope of a weight for XW: enc0 / encq / enco / enc1w / enc2w / pred / dec / out"""
+        """fine scope of a weight for XW: enc0 (enc0q / enc0o / enc0f: its QKV / out-proj / FFN) / encq / enco /
+        enc1w / enc2w / pred / dec / out"""
         if key.startswith("encoder."):
             if key.startswith("encoder.encoders0."):
+                for tag, sub in (("enc0q", "linear_q_k_v"), ("enc0o", "linear_out"), ("enc0f", "feed_forward")):
+                    if sub in key and tag in self.xw:
+                        return tag
                 return "enc0"
             for tag, sub in (("encq", "linear_q_k_v"), ("enco", "linear_out"), ("enc1w", "w_1"), ("enc2w", "w_2")):
                 if sub in key:
@@ -90,8 +94,10 @@ class Emu:
             wq = bf(self.w[key])
             if "linear_q_k_v" in key and key.startswith("encoder.encoders."):
                 D = wq.shape[0] // 3
+                layer = int(key.split(".")[2])
+                lim = [int(x[6:]) for x in self.xw if x.startswith("encqv<")]   # encqv<N: layers 1..N-1 only
                 for i, part in enumerate(("encqq", "encqk", "encqv")):
-                    if part in self.xw:
+                    if part in self.xw or (part == "encqv" and lim and layer + 1 < lim[0]):
                         wq[i * D:(i + 1) * D] = self.w[key][i * D:(i + 1) * D]
             self.wb[key] = wq
         return self.wb[key]
@@ -254,16 +260,25 @@ def main():
     w = R.as_torch_weights(make_weights(cfg, seed=0))
     feats, lens = fbank_input(seed=int(g["seed"]), B=int(g["B"]), T=int(g["T"]), lens=g["lens"])
     x, ln = torch.from_numpy(feats), torch.from_numpy(lens.astype(np.int64))
+    out_json = os.environ.get("EMUL_JSON")
+    res = {}
     for knobs in variants:
         for kk in knobs:
             assert kk in ALL or kk.startswith("XW:"), kk
         t0 = time.time()
         enc, ntok, ids = Emu(w, cfg, knobs).run(x, ln)
         s = score(gpath, ntok, ids, enc)
+        res["+".join(knobs) or "f32"] = s
         print(f"{'+'.join(knobs) or 'f32':22s} flips {s['flip_frac_equal_counts']:.4f} "
               f"mean_regret {s['mean_regret']:.4f} max_regret {s['max_regret']:.3f} "
               f"outside_top5 {s['outside_topk']} equal_counts {s['equal_counts']:.3f} "
               f"enc_rel {s['enc_rows_rel']:.2e} ({time.time() - t0:.0f} s)", flush=True)
+    if out_json:   # merge into a JSON file: {golden: {variant: stats}}
+        import json
+        allr = json.load(open(out_json)) if os.path.exists(out_json) else {}
+        allr.setdefault(f"para_large_{name}", {}).update(res)
+        with open(out_json, "w") as f:
+            json.dump(allr, f, indent=1)
 
 
 if __name__ == "__main__":
