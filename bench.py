@@ -285,7 +285,7 @@ def main():
     eng = PfmEngine(cfg, gpu)
     if world > 1:   # one flat RCCL broadcast, set straight from device memory (pfm_set_weight_device)
         bdev = dev if backend != "gloo" else torch.device("cpu")
-        # fast mode reads every matrix as bf16: send those as bf16 (486 instead of 880 MB over xGMI)
+        # fast mode reads every matrix as bf16: send those as bf16 (520 instead of 880 MB over xGMI)
         wire = "bf16" if args.mode == "fast" else "f32"
         flat = broadcast_state_dict(param_layout(cfg), make_weights(cfg, args.seed) if rank == 0 else None,
                                     device=bdev, keep_on_device=True, wire=wire)
@@ -380,8 +380,12 @@ def main():
         if pmc.get("mfma_busy_gemm_class") is not None:
             busy = round(pmc["mfma_busy_gemm_class"], 4)
             busy_src = f"profiles/{tname}: " + pmc.get("mfma_busy_definition", "")
+    xw_bits = int(os.environ.get("PFM_FAST_XW", "7") or 7) & 15
+    # the encoder layer launch: MODE 4, or with PFM_FAST_XW bit 4 / 8 MODE 5 / 6 (the v rows' / Wo's second weight
+    # plane streamed too; algorithmic FLOPs are the same)
+    dom_kernel = "ffn2_kernel<%d>" % (6 if xw_bits & 8 else 5 if xw_bits & 4 else 4)
     roofline = {"bound": "mfma",
-                "kernel": ("ffn2_kernel<4> (encoder out-proj + LN2-FFN + LN1 + next QKV) + ffn_fused_kernel (decoder "
+                "kernel": (f"{dom_kernel} (encoder out-proj + LN2-FFN + LN1 + next QKV) + ffn_fused_kernel (decoder "
                            "FFNs) + gemm_bf16_kernel (layer-0 QKV / decoder / vocabulary)") if args.mode == "fast" else
                           "gemm_bf16_kernel, split-bf16 x6 emulation of f32 (flops counted as f32 2MNK)",
                 "achieved": round(g_ach, 2), "peak": peak, "unit": "TFLOP/s", "frac": round(g_ach / peak, 4),
@@ -398,7 +402,7 @@ def main():
                 # the single dominant kernel, beside the class figure above: the encoder layer launch
                 # ffn2_kernel<4> (out-proj + LN2-FFN + LN1 + the next layer's QKV), 2 M 512 (512 + 2048 + 2048 + 1536)
                 # FLOP per launch at M = B T rows, live HIP events on its launch stream
-                "dominant": ({"kernel": "ffn2_kernel<4>", "launches": int(dom["launches"]),
+                "dominant": ({"kernel": dom_kernel, "launches": int(dom["launches"]),
                               "gflop_per_launch": round(dom["flops"] / dom["launches"] / 1e9, 2),
                               "avg_launch_us": round(dom["ms"] * 1e3 / dom["launches"], 2),
                               "avg_launch_us_raw": round(d_raw_ms * 1e3 / dom["launches"], 2),

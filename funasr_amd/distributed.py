@@ -4,7 +4,7 @@ gloo on CPU for tests).
 The Paraformer path has no exchange inside a forward pass: utterances are
 independent. So the only collectives are
   * one weight broadcast from rank 0 at start-up (`broadcast_state_dict`: one flat fp32 buffer, 880 MB for
-    Paraformer-large, or for fast-mode serving the bf16-only matrices as bf16 and the rest as f32, 486 MB; large RCCL
+    Paraformer-large, or for fast-mode serving the bf16-only matrix rows as bf16 and the rest as f32, 520 MB; large RCCL
     broadcasts over xGMI),
   * (API path only) after the rank's batches, an all-gather of its greedy token matrices as tensors
     (`gather_token_matrices`: [n, L] int32 ids + counts + input indices, RCCL on the GPU), from which every rank
@@ -78,30 +78,61 @@ _BF16_WIRE_SUFFIXES = ("self_attn.linear_out.weight", "self_attn.linear_q_k_v.we
                        "decoder.output_layer.weight", "ctc.ctc_lo.weight", "predictor.cif_conv1d.weight")
 
 
-def bf16_wire_key(key: str, shape) -> bool:
-    """True for the weights fast mode reads only through their bf16 copies (sent as bf16 by wire="bf16")."""
-    if key.endswith(_BF16_WIRE_SUFFIXES):
-        return True
-    return key.startswith("encoder.") and key.endswith("feed_forward.w_2.weight")
+def fast_xw_bits() -> int:
+    """The library's PFM_FAST_XW (default 7; bit 8 implies 4), as pfm_api.hip reads it."""
+    import os
+    v = os.environ.get("PFM_FAST_XW", "")
+    b = (int(v) if v.strip() else 7) & 15
+    return b | 4 if b & 8 else b
 
 
-def _wire_index(layout, dev):
+def bf16_wire_rows(key: str, shape, xw: int = None):
+    """Rows [r0, r1) of weight `key` that fast mode reads only through their bf16 copies (sent as bf16 by
+    wire="bf16"; the rest of the tensor travels as f32). Under PFM_FAST_XW the split-plane weights are read in f32
+    (their lo planes w - bf16(w)): bit 1 the predictor conv, bit 2 encoder layer 0 (and layer 1's QKV GEMM), bit 4
+    the v rows of every encoder QKV projection, bit 8 every encoder out-projection."""
+    xw = fast_xw_bits() if xw is None else xw
+    rows = int(shape[0]) if len(shape) else 0
+    bf = key.endswith(_BF16_WIRE_SUFFIXES) or (key.startswith("encoder.") and key.endswith("feed_forward.w_2.weight"))
+    if not bf:
+        return 0, 0
+    if (xw & 1) and key.startswith("predictor."):
+        return 0, 0
+    if (xw & 2) and key.startswith("encoder.encoders0."):
+        return 0, 0
+    if (xw & 8) and key.startswith("encoder.") and key.endswith("self_attn.linear_out.weight"):
+        return 0, 0
+    if (xw & 4) and key.startswith("encoder.") and key.endswith("self_attn.linear_q_k_v.weight"):
+        return 0, 2 * rows // 3   # q | k rows bf16, the v rows f32
+    return 0, rows
+
+
+def bf16_wire_key(key: str, shape, xw: int = None) -> bool:
+    """True when every element of the weight travels as bf16 under wire="bf16"."""
+    r0, r1 = bf16_wire_rows(key, shape, xw)
+    return r1 > r0 and r1 - r0 == int(shape[0])
+
+
+def _wire_index(layout, dev, xw: int = None):
     """Flat indices of the bf16-wire elements and of the f32 ones."""
     import torch
     sizes = [int(np.prod(s)) for _, s, *_ in layout]
     mat = np.zeros(int(sum(sizes)), dtype=bool)
     off = 0
     for (k, s, *_), n in zip(layout, sizes):
-        mat[off:off + n] = bf16_wire_key(k, s)
+        r0, r1 = bf16_wire_rows(k, s, xw)
+        if r1 > r0:
+            row = n // int(s[0])
+            mat[off + r0 * row:off + r1 * row] = True
         off += n
     return torch.from_numpy(np.nonzero(mat)[0]).to(dev), torch.from_numpy(np.nonzero(~mat)[0]).to(dev)
 
 
-def bf16_wire_round(flat, layout):
+def bf16_wire_round(flat, layout, xw: int = None):
     """What a receiving rank holds after broadcast_state_dict(wire="bf16"): `flat` (f32, layout order) with the
-    bf16-wire matrices rounded to bf16 (in place; returned)."""
+    bf16-wire elements rounded to bf16 (in place; returned)."""
     import torch
-    mi, _ = _wire_index(layout, flat.device)
+    mi, _ = _wire_index(layout, flat.device, xw)
     flat[mi] = flat[mi].to(torch.bfloat16).to(torch.float32)
     return flat
 
@@ -114,8 +145,9 @@ def broadcast_state_dict(layout, sd: Optional[Dict[str, np.ndarray]], device=Non
     sd: the dict on `src` (ignored elsewhere). device: torch device of the collective
     (cuda for RCCL, cpu for gloo). keep_on_device: return the flat f32 tensor itself (for
     PfmEngine.load_flat_device: no device -> host -> device round trip) instead of a host dict.
-    wire: "f32" sends every weight as f32 (880 MB for Paraformer-large); "bf16" sends the matrices fast mode reads
-    only through their bf16 copies (`bf16_wire_key`) as bf16 and the rest as f32 -- about half the bytes. The
+    wire: "f32" sends every weight as f32 (880 MB for Paraformer-large); "bf16" sends the matrix rows fast mode reads
+    only through their bf16 copies (`bf16_wire_rows`, for the PFM_FAST_XW in effect) as bf16 and the rest as f32
+    (486 MB at PFM_FAST_XW=0, 520 MB at the default 7). The
     receiving ranks' matrices are then bf16-rounded, which fast mode does not see (bf16(bf16(w)) = bf16(w): its
     decode is bit-identical, tests/test_gpu_automodel.py) but EXACT mode would: load them with
     PfmEngine.load_flat_device(..., fast_only=True).

@@ -226,12 +226,14 @@ def test_load_flat_device_matches_host_load():
         b.load_flat_device(flat[:100], lay)
 
 
+@pytest.mark.parametrize("xw", [7, 0])
 @pytest.mark.parametrize("large", [False, True])
-def test_bf16_wire_weights_fast_mode_bit_identical(large):
-    """broadcast_state_dict(wire="bf16") (the fast-mode data-parallel broadcast: 486 instead of 880 MB for
+def test_bf16_wire_weights_fast_mode_bit_identical(monkeypatch, large, xw):
+    """broadcast_state_dict(wire="bf16") (the fast-mode data-parallel broadcast: 520 instead of 880 MB for
     Paraformer-large) leaves every rank bf16-rounded matrices; fast mode reads those only through bf16 copies (or,
     for the decoder w_2 / CIF projection, receives them in f32), so its decode is bit-identical to the f32-loaded
-    engine's; EXACT mode is refused on such an engine."""
+    engine's (under PFM_FAST_XW the split-plane weights travel as f32); EXACT mode is refused on such an engine."""
+    monkeypatch.setenv("PFM_FAST_XW", str(xw))
     from funasr_amd.config import paraformer_large
     from funasr_amd.distributed import bf16_wire_round
     from funasr_amd.runtime import PfmEngine, PfmError
