@@ -121,9 +121,8 @@ __device__ __forceinline__ void valu_to_mfma() {
 }
 
 template <int N> __device__ __forceinline__ void vm_wait() {
-    if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    else if constexpr (N == 20) asm volatile("s_waitcnt vmcnt(20)" ::: "memory");
-    else static_assert(N < 0, "vm_wait: unsupported count");
+    static_assert(N >= 0 && N <= 63, "vm_wait: vmcnt is 6 bits");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 static_assert((RS - 3) * GW == 20, "vm_wait counts");
 
@@ -165,7 +164,9 @@ __device__ __forceinline__ void store_bf16_block(bf16* row, const bf16x4 (&o)[4]
 // DMA waits (stale ring), 2 = no MFMAs, 3 = neither DMA nor barriers (MFMA + fragment reads alone), 5 = the
 // prologue / transition / epilogue alone (no stream: zero chunks, no phase-0 MFMAs), 4 = every tile streamed from
 // the same L2-hot 64 KiB (wrong math; prices L2 misses of the weight stream), 6 = the DMA of a tile issued as one
-// burst at its publishing barrier (the pre-round-4 schedule)
+// burst at its publishing barrier (the pre-round-4 schedule), 7 = no phase-3 (q|k|v) stores, 8 = no x2 store,
+// 9 = the full kernel with phase timestamps (s_memrealtime, 100 MHz) of wave 0 written past row M of Xo
+// (16 x u64 per workgroup: the caller provides the room)
 template <int MODE, int VAR = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void ffn2_kernel(
     const float* __restrict__ X, int M, const float* __restrict__ g, const float* __restrict__ be, float eps,
@@ -186,6 +187,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     const long long rg = (long long)blockIdx.x * BM + 32 * w + r;   // this lane's row
     const bool live = rg < M;
     const long long rc = live ? rg : (long long)M - 1;               // clamped for loads
+    unsigned long long tsv[16];                                       // VAR 9: phase timestamps (uniform)
+    auto stamp = [&](int i) __attribute__((always_inline)) {
+        if constexpr (VAR == 9) {
+            __builtin_amdgcn_sched_barrier(0);
+            tsv[i] = __builtin_amdgcn_s_memrealtime();
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    };
+    stamp(0);
 
     // ---- per-column vectors -> LDS (before any LDS-DMA is in flight: their waits drain nothing)
     for (int i = tid; i < FD; i += 256) {
@@ -411,6 +421,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     // ---- tile 0 landed everywhere (the compiler's wait for the activation loads drained the ring DMA too)
     vm_wait<0>();
     bar();
+    stamp(1);
 #pragma unroll
     for (int f = 0; f < PD; ++f) rd(f, f, wf[f]);
 
@@ -465,6 +476,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         // written at the statement, so across the VALU-heavy transition the compiler spilled those registers to
         // scratch before the data landed (garbage operands for the first phase-1 MFMAs on some waves): retire the
         // reads here and issue them again after the transition.
+        stamp(2);
         asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(wf[0]), "+v"(wf[1]), "+v"(wf[2]), "+v"(wf[3]), "+v"(wf[4]),
                      "+v"(wf[5]), "+v"(wf[6]), "+v"(wf[7]));
         xdl_drain(acc);
@@ -490,6 +502,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         for (int f = 0; f < PD; ++f) rd(F0 + f, f, wf[f % NB]);
     }
     valu_to_mfma();
+    stamp(3);
 
     // ---- the FFN stream (see the header): head P1(0), bodies c = 0..62 (P1(c+1) under P2(c)), tail P2(63)
     f32x16 acc1a, acc1b;        // phase 1 of one chunk as two accumulator chains (even / odd k steps)
@@ -566,13 +579,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #pragma unroll
         for (int k = 0; k < 32; ++k) p2(ft + k, k, k, hfb);   // tail: P2(63)
     }
+    stamp(4);
     if constexpr (QK)   // the read-ahead of phase 3's first fragments: retired before the epilogue (see phase 0)
         asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(wf[0]), "+v"(wf[1]), "+v"(wf[2]), "+v"(wf[3]), "+v"(wf[4]),
                      "+v"(wf[5]), "+v"(wf[6]), "+v"(wf[7]));
     xdl_drain(acc);
 
     // ---- epilogue (no DMA in flight: the last tiles were waited for by their tops)
-    if (live && Xo) {
+    if (live && Xo && VAR != 8) {
 #pragma unroll
         for (int ob = 0; ob < 16; ++ob) {
             fence();
@@ -583,6 +597,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         }
         fence();
     }
+    stamp(5);
     if constexpr (QK) {
         // ---- phase 3: the next layer's q|k|v = LN1_next(x2) Wqkv^T + b in three passes of 512 output features,
         //      the LayerNorm output as the B operand in registers (the W1 k order: Wqkv packed by ffn2_pack_qkv);
@@ -601,6 +616,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #pragma unroll
         for (int f = 0; f < PD; ++f) rd(F3 + f, f, wf[f % NB]);
         valu_to_mfma();
+        stamp(6);
         // three passes of 512 output features (the whole accumulator); a pass's epilogue (bias, bf16, 16-B stores)
         // runs between the passes. (Six passes of 256 with the previous pass's stores issued in the MFMA shadow from
         // the other accumulator half spilled the LayerNorm operand to scratch inside the loop: not kept.)
@@ -636,7 +652,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
             asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(wf[0]), "+v"(wf[1]), "+v"(wf[2]), "+v"(wf[3]), "+v"(wf[4]),
                          "+v"(wf[5]), "+v"(wf[6]), "+v"(wf[7]));
             xdl_drain(acc);
-            if (live) {
+            if (p == 0) stamp(7);
+            else if (p == 1) stamp(9);
+            else stamp(11);
+            if (live && VAR != 7) {
 #pragma unroll
                 for (int ob = 0; ob < 16; ++ob) {
                     fence();
@@ -659,6 +678,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
                 for (int f = 0; f < PD; ++f) rd(fp + OPF + f, f, wf[f % NB]);
             }
             valu_to_mfma();
+            if (p == 0) stamp(8);
+            else if (p == 1) stamp(10);
+            else stamp(12);
+        }
+        if constexpr (VAR == 9) {   // the stores retired, then the record
+            vm_wait<0>();
+            stamp(13);
+            if (tid < 14) {
+                unsigned long long v = tsv[0];
+#pragma unroll
+                for (int i = 1; i < 14; ++i) v = tid == i ? tsv[i] : v;
+                ((unsigned long long*)(Xo + (long long)M * FD))[16 * blockIdx.x + tid] = v;
+            }
         }
         return;
     }

@@ -16,6 +16,7 @@ Rounding points (names used on the command line):
         y = rstd (W2g h - mu c1) + c2 with W2g = bf16(W2 diag(gamma)))
   DF    the decoder FSMN's input (LN2 output) and output stored as bf16
   WONLY / AONLY  with a G* scope: round only the weights / only the activation rows
+  A16   EXACT-mode x4 candidate: every GEMM activation as two bf16 planes (~2^-16), weights f32 (attention f32)
   XW:<s>  keep the weights of scope s exact (s = enc0 encq (encqq / encqk / encqv: its q / k / v rows) enco enc1w enc2w pred dec out; a split-bf16 weight)
 
     python tools/fast_emul.py b24 G G,QKV G,QKV,P ...
@@ -42,11 +43,17 @@ from tests.golden.inputs import fbank_input  # noqa: E402
 ALL = ("G", "GE", "GP", "GD", "GO", "QKV", "KV", "P", "F", "DH", "DF")
 SCOPE = {"G": ("enc", "pred", "dec", "out"), "GE": ("enc",), "GP": ("pred",), "GD": ("dec",), "GO": ("out",),
          "GE0": ("enc0",), "GE1": ("enc1",), "GEQ": ("encq",), "GEO": ("enco",), "GE1W": ("enc1w",), "GE2W": ("enc2w",)}
-ALL = ALL + ("GE0", "GE1", "GEQ", "GEO", "GE1W", "GE2W", "WONLY", "AONLY")
+ALL = ALL + ("GE0", "GE1", "GEQ", "GEO", "GE1W", "GE2W", "WONLY", "AONLY", "A16")
 
 
 def bf(x):
     return x.to(torch.bfloat16).to(torch.float32)
+
+
+def bf2(x):
+    """x0 + x1 (two bf16 planes, ~16 significant bits): the A operand of an EXACT-mode x4 GEMM"""
+    x0 = bf(x)
+    return x0 + bf(x - x0)
 
 
 class Emu:
@@ -103,6 +110,8 @@ class Emu:
         return self.wb[key]
 
     def lin(self, x, wkey, bkey=None):
+        if "A16" in self.k:   # EXACT x4: activations as two bf16 planes, f32 weights
+            return F.linear(bf2(x), self.w[wkey], self.w[bkey] if bkey else None)
         a = bf(x) if self._scope(wkey) in self.g and "WONLY" not in self.k else x
         return F.linear(a, self.W(wkey), self.w[bkey] if bkey else None)
 
@@ -159,7 +168,7 @@ class Emu:
     def alphas(self, enc, lens):
         cfg, w = self.cfg, self.w
         m = R.pad_mask(lens, enc.shape[1])
-        e = bf(enc) if "pred" in self.g else enc
+        e = bf2(enc) if "A16" in self.k else bf(enc) if "pred" in self.g else enc
         q = F.pad(e.transpose(1, 2), (cfg.cif_l_order, cfg.cif_r_order))
         wc = (bf(w["predictor.cif_conv1d.weight"]) if "pred" in self.g and "pred" not in self.xw
               else w["predictor.cif_conv1d.weight"])

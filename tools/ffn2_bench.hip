@@ -54,7 +54,7 @@ int main(int argc, char** argv) {
     for (int i = 1; i < argc; ++i) Ms.push_back(atoi(argv[i]));
     if (Ms.empty()) Ms = {16000, 32000};
     const int Mmax = 32768;
-    const long long nx = (long long)Mmax * 512, nw = 262144 + 2097152 + 3 * 262144;
+    const long long nx = (long long)Mmax * 512, nw = 2 * 262144 + 2097152 + 4 * 262144;   // MODE 6's stream
     float *X, *Xo, *vecs;
     bf16 *Wp, *O, *Fr, *Xn;
     CK(hipMalloc(&X, nx * 4));
@@ -73,6 +73,75 @@ int main(int argc, char** argv) {
     const float *g = vecs, *be = vecs + 2048, *b1 = vecs + 4096, *b2 = vecs + 6144, *gn = vecs + 8192, *bn = vecs + 10240,
                 *bo = vecs + 12288, *c1 = vecs + 14336;
     // PMC passes: FFN2_ONLY=1 the OP kernel alone (MODE 1), FFN2_ONLY=4 the OP + next-QKV kernel (MODE 4, the default)
+    // FFN2_ANAT=1: the anatomy of the default encoder launch (MODE 5, PFM_FAST_XW 7) and of MODE 4 / 6 beside it
+    if (getenv("FFN2_ANAT")) {
+        for (int M : Ms) {
+            const double fl = 2.0 * M * 512.0 * (512 + 2048 + 2048 + 1536);
+            const int reps = 20;
+            float t;
+            t = run<4, 0>(M, reps, X, g, be, Wp, b1, b2, Xo, gn, bn, Xn, O, Fr, bo, c1);
+            printf("M=%6d MODE4 full       %8.1f us  %7.1f TF/s\n", M, t, fl / t / 1e6);
+            t = run<6, 0>(M, reps, X, g, be, Wp, b1, b2, Xo, gn, bn, Xn, O, Fr, bo, c1);
+            printf("M=%6d MODE6 full       %8.1f us  %7.1f TF/s (algorithmic)\n", M, t, fl / t / 1e6);
+            t = run<5, 0>(M, reps, X, g, be, Wp, b1, b2, Xo, gn, bn, Xn, O, Fr, bo, c1);
+            printf("M=%6d MODE5 full       %8.1f us  %7.1f TF/s (algorithmic)\n", M, t, fl / t / 1e6);
+            t = run<5, 1>(M, reps, X, g, be, Wp, b1, b2, Xo, gn, bn, Xn, O, Fr, bo, c1);
+            printf("M=%6d MODE5 no DMA     %8.1f us\n", M, t);
+            t = run<5, 2>(M, reps, X, g, be, Wp, b1, b2, Xo, gn, bn, Xn, O, Fr, bo, c1);
+            printf("M=%6d MODE5 no MFMA    %8.1f us\n", M, t);
+            t = run<5, 3>(M, reps, X, g, be, Wp, b1, b2, Xo, gn, bn, Xn, O, Fr, bo, c1);
+            printf("M=%6d MODE5 no DMA/bar %8.1f us\n", M, t);
+            t = run<5, 4>(M, reps, X, g, be, Wp, b1, b2, Xo, gn, bn, Xn, O, Fr, bo, c1);
+            printf("M=%6d MODE5 L2-hot W   %8.1f us\n", M, t);
+            t = run<5, 5>(M, reps, X, g, be, Wp, b1, b2, Xo, gn, bn, Xn, O, Fr, bo, c1);
+            printf("M=%6d MODE5 pro/epi    %8.1f us\n", M, t);
+            t = run<5, 7>(M, reps, X, g, be, Wp, b1, b2, Xo, gn, bn, Xn, O, Fr, bo, c1);
+            printf("M=%6d MODE5 no qkv st  %8.1f us\n", M, t);
+            t = run<5, 8>(M, reps, X, g, be, Wp, b1, b2, Xo, gn, bn, Xn, O, Fr, bo, c1);
+            printf("M=%6d MODE5 no x2 st   %8.1f us\n", M, t);
+            t = run<5, 0>(M, reps, X, g, be, Wp, b1, b2, Xo, gn, bn, Xn, O, Fr, bo, c1);
+            printf("M=%6d MODE5 full again %8.1f us\n", M, t);
+            t = run<4, 0>(M, reps, X, g, be, Wp, b1, b2, Xo, gn, bn, Xn, O, Fr, bo, c1);
+            printf("M=%6d MODE4 full again %8.1f us\n", M, t);
+        }
+        return 0;
+    }
+    // FFN2_TS=1: per-phase timeline of MODE 5 and MODE 4 (VAR 9: wave 0's s_memrealtime stamps, 100 MHz)
+    if (getenv("FFN2_TS")) {
+        const char* names[13] = {"vectors + prologue loads", "phase 0 (out-proj) stream", "transition (x, F loads, LN2)",
+                                 "FFN stream", "x2 store issue", "LN1_next", "QKV pass 0 stream", "pass 0 stores",
+                                 "QKV pass 1 stream", "pass 1 stores", "QKV pass 2 stream (+ v plane)",
+                                 "pass 2 stores issue", "stores retire"};
+        for (int M : Ms) {
+            const int nb = (M + BM - 1) / BM;
+            std::vector<unsigned long long> ts(16 * nb);
+            for (int mode = 5; mode >= 4; --mode) {
+                float t = mode == 5 ? run<5, 9>(M, 5, X, g, be, Wp, b1, b2, Xo, gn, bn, Xn, O, Fr, bo, c1)
+                                    : run<4, 9>(M, 5, X, g, be, Wp, b1, b2, Xo, gn, bn, Xn, O, Fr, bo, c1);
+                CK(hipMemcpy(ts.data(), Xo + (long long)M * 512, ts.size() * 8, hipMemcpyDeviceToHost));
+                unsigned long long t0 = ~0ull, t1 = 0, e0 = ~0ull;
+                for (int b = 0; b < nb; ++b) {
+                    t0 = std::min(t0, ts[16 * b]);
+                    t1 = std::max(t1, ts[16 * b + 13]);
+                    e0 = std::min(e0, ts[16 * b + 13]);
+                }
+                printf("M=%d MODE%d launch %.1f us (events); stamps: first start -> last end %.1f us, start skew %.1f us, "
+                       "end skew %.1f us\n", M, mode, t, (t1 - t0) / 100.0, 0.0, (t1 - e0) / 100.0);
+                double sk = 0;
+                for (int b = 0; b < nb; ++b) sk = std::max(sk, (ts[16 * b] - t0) / 100.0);
+                printf("  start skew (max over workgroups) %.1f us\n", sk);
+                for (int i = 0; i < 13; ++i) {
+                    double mn = 1e30, mx = 0, sum = 0;
+                    for (int b = 0; b < nb; ++b) {
+                        const double d = (ts[16 * b + i + 1] - ts[16 * b + i]) / 100.0;
+                        mn = std::min(mn, d); mx = std::max(mx, d); sum += d;
+                    }
+                    printf("  %-32s mean %7.2f us  min %7.2f  max %7.2f\n", names[i], sum / nb, mn, mx);
+                }
+            }
+        }
+        return 0;
+    }
     const char* only_env = getenv("FFN2_ONLY");
     const bool only = only_env != nullptr, only4 = only && atoi(only_env) == 4;
     for (int M : Ms) {
