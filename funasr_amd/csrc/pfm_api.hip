@@ -2099,6 +2099,9 @@ int pfm_profile_read(pfm_handle* h, int kc, double* ms, double* flops, double* b
 int pfm_op_gemm(void* stream, int dtype, const void* A, const void* Wt, const float* bias, const float* res, float* C,
                 int M, int N, int K, int act) {
     pfm_knobs_refresh();
+    if (!A || !Wt || !C) return fail(PFM_E_ARG, "pfm_op_gemm: null operand");
+    if (M < 0 || N < 1 || K < 1) return fail(PFM_E_ARG, "pfm_op_gemm: bad sizes");
+    if (dtype != DT_F32 && dtype != DT_BF16) return fail(PFM_E_ARG, "pfm_op_gemm: dtype must be PFM_F32 or PFM_BF16");
     if ((act & 2) && dtype != DT_BF16) return fail(PFM_E_ARG, "pfm_op_gemm: bf16 output needs bf16 operands");
     GemmEpi e = epi_default();
     e.bias = bias; e.relu = act & 1;
@@ -2301,6 +2304,9 @@ int pfm_op_ffn_dec(void* stream, const float* x, int M, const float* g1, const f
 int pfm_op_attention(void* stream, int dtype, const void* q, const void* k, const void* v, const int32_t* klen,
                      float* out, int B, int Tq, int Tk, int heads, float scale) {
     pfm_knobs_refresh();
+    if (!q || !k || !v || !klen || !out || B < 0 || Tq < 0 || Tk < 0 || heads < 1)
+        return fail(PFM_E_ARG, "pfm_op_attention: null operand or bad sizes");
+    if (dtype != DT_F32 && dtype != DT_BF16) return fail(PFM_E_ARG, "pfm_op_attention: dtype must be PFM_F32 or PFM_BF16");
     const int D = heads * 128;
     HIP_TRY(pfm_attention(dtype, q, rowmap_plain(D), k, rowmap_plain(D), v, rowmap_plain(D), out, D, nullptr, klen, B,
                           Tq, Tk, heads, 128, scale, (hipStream_t)stream));
@@ -2310,6 +2316,7 @@ int pfm_op_attention(void* stream, int dtype, const void* q, const void* k, cons
 int pfm_op_layernorm(void* stream, const float* x, const float* g, const float* b, float* out, int M, int D,
                      float eps) {
     pfm_knobs_refresh();
+    if (!x || !g || !b || !out || M < 0 || D < 1) return fail(PFM_E_ARG, "pfm_op_layernorm: null operand or bad sizes");
     HIP_TRY(pfm_layernorm(x, rowmap_plain(D), M, D, g, b, eps, nullptr, 0, 1.f, out, rowmap_plain(D), DT_F32,
                           nullptr, rowmap_plain(0), 0, (hipStream_t)stream));
     return PFM_OK;
@@ -2318,12 +2325,16 @@ int pfm_op_layernorm(void* stream, const float* x, const float* g, const float* 
 int pfm_op_fsmn(void* stream, const float* v, const int32_t* len, const float* w, const float* res, float* out,
                 int B, int T, int D, int K, int left) {
     pfm_knobs_refresh();
+    if (!v || !len || !w || !out || B < 0 || T < 0 || D < 1 || K < 1 || left < 0)
+        return fail(PFM_E_ARG, "pfm_op_fsmn: null operand or bad sizes");
     HIP_TRY(pfm_fsmn(v, rowmap_plain(D), len, B, T, D, w, K, left, res, out, nullptr, (hipStream_t)stream));
     return PFM_OK;
 }
 
 int pfm_op_layernorm_bf16(void* stream, const void* x, const float* g, const float* b, float* out, int M, int D,
                           float eps) {
+    if (!x || !g || !b || !out || M < 0 || (D != 512 && D != 1024 && D != 2048))
+        return fail(PFM_E_ARG, "pfm_op_layernorm_bf16: null operand or bad sizes (D 512 / 1024 / 2048)");
     HIP_TRY(pfm_layernorm_bf16in((const bf16*)x, rowmap_plain(D), M, D, g, b, eps, out, rowmap_plain(D), DT_F32,
                                  (hipStream_t)stream));
     return PFM_OK;
@@ -2331,6 +2342,8 @@ int pfm_op_layernorm_bf16(void* stream, const void* x, const float* g, const flo
 
 int pfm_op_fsmn_bf16(void* stream, const void* v, const int32_t* len, const float* w, void* out, int B, int T, int D,
                      int K, int left) {
+    if (!v || !len || !w || !out || B < 0 || T < 0 || D < 1 || K < 1 || left < 0)
+        return fail(PFM_E_ARG, "pfm_op_fsmn_bf16: null operand or bad sizes");
     HIP_TRY(pfm_fsmn_bf16in((const bf16*)v, rowmap_plain(D), len, B, T, D, w, K, left, nullptr, nullptr, (bf16*)out,
                             (hipStream_t)stream));
     return PFM_OK;
@@ -2345,6 +2358,8 @@ int pfm_op_ctc_collapse(void* stream, const int32_t* ids, int64_t ld, const int3
 
 int pfm_op_cif(void* stream, const float* alphas, const float* hidden, float* emb, float* peaks, int32_t* n_fire,
                int32_t* ntok, int B, int T, int D, int L_cap) {
+    if (!alphas || !hidden || !emb || !peaks || !n_fire || !ntok || B < 0 || T < 0 || D < 1 || L_cap < 0)
+        return fail(PFM_E_ARG, "pfm_op_cif: null operand or bad sizes");
     HIP_TRY(pfm_cif_fire(alphas, hidden, rowmap_plain(D), B, T, D, L_cap, emb, peaks, n_fire, ntok,
                          (hipStream_t)stream));
     return PFM_OK;
