@@ -27,13 +27,14 @@
 //
 // Weight stream (pfm_ffn2_pack*), one 1 KiB fragment per MFMA, in MFMA issue order:
 //   [OP: Wo fragments, four output blocks interleaved per k step: (ob 4g, ks) .. (ob 4g+3, ks), then ks+1]
-//   head  P1(0): the 32 W1 fragments of hidden chunk 0 (k steps 0..31, alternating accumulator chains a / b)
-//   body c (c = 0..62), 64 fragments: slots 3m, 3m+1 = P1(c+1) k steps 2m, 2m+1 (chains a, b), slot 3m+2 = P2(c)
+//   head  P1(0): the 32 W1 fragments of hidden chunk 0 (k steps 0..31, one accumulator chain seeded with b1)
+//   body c (c = 0..62), 64 fragments: slots 3m, 3m+1 = P1(c+1) k steps 2m, 2m+1, slot 3m+2 = P2(c)
 //         output block m, hidden k step 0 (m < 16); slots 48..63 = P2(c) output blocks 0..15, hidden k step 1
 //   tail  P2(63): output blocks 0..15 of k step 0, then of k step 1
 // so phase 1 of chunk c+1 runs under phase 2 of chunk c (a software pipeline), and relu(H + b1) of chunk c+1 -> bf16
-// (phase 2's B operand, double-buffered) is issued
-// between the last 16 MFMAs of the body, in their VALU-issue shadow, instead of in a drain between the phases.
+// (phase 2's B operand, double-buffered) is issued between the last 16 MFMAs of the body instead of in a drain
+// between the phases. (Phase 1 first in the body — slots 0..31 — with the relu spread over the other 30 gaps: its
+// compute was faster without DMA / barriers, 192.5 vs 197.4 us, but the launch 0.7 % slower; not kept.)
 // Tile t is published (landed + every wave done with tile t-2) by one barrier placed PD fragments before its
 // first read; the DMA of tile t-2+RS into the freed slot is spread over the following 16 MFMAs (one 1 KiB piece
 // per wave every 4 fragments), so no wave issues a burst of LDS-DMA beside an idle matrix pipe.
@@ -44,6 +45,7 @@
 namespace {
 
 typedef __attribute__((address_space(3))) void lds_void;
+typedef float f32x8 __attribute__((ext_vector_type(8)));
 typedef const __attribute__((address_space(1))) void gbl_void;
 
 constexpr int FD = 512, FF = 2048, BM = 128, NW = 4, HC = 32, NCH = FF / HC;   // 64 hidden chunks
@@ -82,7 +84,7 @@ __device__ __forceinline__ f32x16 mfma32(bf16x8 a, bf16x8 b, f32x16 c) {
 // hipcc pads no hazards around inline asm (cdna_hip_programming.md §5.7 item 2), so the kernel keeps them:
 //   * the first MFMA of a chain takes the inline constant 0 as C; later ones accumulate into the same registers,
 //     back to back (XDL D -> the next XDL's whole C: 0 wait states) or with other MFMAs in between (phase 0
-//     interleaves four output blocks, phase 1's two chains alternate; 1, 2 and 4 interleaved blocks measured
+//     interleaves four output blocks, phase 1 is one chain of 32 from its C = b1; 1, 2 and 4 interleaved blocks measured
 //     bit-identical);
 //   * D -> any other reader: 24 wait states (covers the 16-pass XDL distance of 19; xdl_drain(), fenced by
 //     sched_barrier, before the transition / epilogue VALU reads the accumulators; mfma_v_drain() before the relu
@@ -98,6 +100,9 @@ __device__ __forceinline__ void mfma_a(f32x16& d, const bf16x8& a, const bf16x8&
 }
 __device__ __forceinline__ void mfma32_v0(f32x16& d, const bf16x8& a, const bf16x8& b) {
     asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=&v"(d) : "v"(a), "v"(b));
+}
+__device__ __forceinline__ void mfma32_vc(f32x16& d, const bf16x8& a, const bf16x8& b, const f32x16& c) {
+    asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %3" : "=&v"(d) : "v"(a), "v"(b), "v"(c));
 }
 __device__ __forceinline__ void mfma32_v(f32x16& d, const bf16x8& a, const bf16x8& b) {
     asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(d) : "v"(a), "v"(b));
@@ -166,7 +171,8 @@ __device__ __forceinline__ void store_bf16_block(bf16* row, const bf16x4 (&o)[4]
 // the same L2-hot 64 KiB (wrong math; prices L2 misses of the weight stream), 6 = the DMA of a tile issued as one
 // burst at its publishing barrier (the pre-round-4 schedule), 7 = no phase-3 (q|k|v) stores, 8 = no x2 store,
 // 9 = the full kernel with phase timestamps (s_memrealtime, 100 MHz) of wave 0 written past row M of Xo
-// (16 x u64 per workgroup: the caller provides the room)
+// (16 x u64 per workgroup: the caller provides the room), 10 = no relu VALU (the hidden operand stale: prices the
+// activation's VALU inside the stream), 11 = no wait states between phase 1's last MFMAs and the relu (wrong math), 12 = 10 with the stamps of 9
 template <int MODE, int VAR = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void ffn2_kernel(
     const float* __restrict__ X, int M, const float* __restrict__ g, const float* __restrict__ be, float eps,
@@ -189,9 +195,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     const long long rc = live ? rg : (long long)M - 1;               // clamped for loads
     unsigned long long tsv[16];                                       // VAR 9: phase timestamps (uniform)
     auto stamp = [&](int i) __attribute__((always_inline)) {
-        if constexpr (VAR == 9) {
+        if constexpr (VAR == 9 || VAR == 12) {
             __builtin_amdgcn_sched_barrier(0);
             tsv[i] = __builtin_amdgcn_s_memrealtime();
+            if (i == 3) tsv[14] = __builtin_amdgcn_s_memtime();   // shader clock across the FFN stream
+            if (i == 4) tsv[15] = __builtin_amdgcn_s_memtime();
+            __builtin_amdgcn_s_waitcnt(0xC07F);                    // lgkmcnt(0): no stamp left in flight
             __builtin_amdgcn_sched_barrier(0);
         }
     };
@@ -505,53 +514,75 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     stamp(3);
 
     // ---- the FFN stream (see the header): head P1(0), bodies c = 0..62 (P1(c+1) under P2(c)), tail P2(63)
-    f32x16 acc1a, acc1b;        // phase 1 of one chunk as two accumulator chains (even / odd k steps)
+    // Phase 1 is one accumulator chain seeded with b1 (the first MFMA takes the chunk's biases as C: back-to-back
+    // MFMAs on one accumulator issue at the same rate as on several), so the activation is relu(H) alone: two
+    // v_cvt_pk_bf16_f32 and two v_pk_max_i16 per group of 4 features (a bf16 is negative iff its 16-bit pattern is,
+    // so the integer max with 0 is the relu, and it commutes with the round-to-nearest). The f32 add + max + convert
+    // per feature it replaces cost 12 us of a 215 us launch (VAR 10): the stream's MFMA gaps are full (a ds_read, its
+    // counted wait and the MFMA's issue), so every VALU instruction added there costs its issue time.
+    f32x16 acc1;                // phase 1 of one chunk (H^T = W1 . act + b1)
     bf16x8 hfa[2], hfb[2];      // phase 2's B operand (hidden k steps 0, 1) of even / odd chunks
-    f32x4 bq[4];                // b1 of the chunk being activated: features 8q + 4h .. +3 (accumulator register groups)
-    auto b1_issue = [&](int c) __attribute__((always_inline)) {
+    f32x4 bqa[4], bqb[4];       // b1 of even / odd chunks: features 8q + 4h .. +3 (accumulator register groups)
+    auto b1_issue = [&](int c, f32x4 (&bq)[4]) __attribute__((always_inline)) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) b1_read(bq[q], vec + V_B1 + HC * c + 8 * q + 4 * h);
     };
-    auto p1 = [&](int f, int fs, int j) __attribute__((always_inline)) {   // phase 1, k step j of a chunk (stream fragment f, position fs)
+    // phase 1, k step j of a chunk (stream fragment f, position fs); k step 0 starts the chain from the biases
+    // (read a body earlier: the named wait only tells the compiler they landed — the step's own fragment wait,
+    // lgkmcnt(PD), already covered them)
+    auto p1 = [&](int f, int fs, int j, f32x4 (&bq)[4]) __attribute__((always_inline)) {
         step_pre(f, fs);
-        if (VAR == 2) asm volatile("" :: "v"(wf[fs % NB]));
-        else if (j == 0) mfma32_v0(acc1a, wf[fs % NB], act[0]);
-        else if (j == 1) mfma32_v0(acc1b, wf[fs % NB], act[1]);
-        else if (j & 1) mfma32_v(acc1b, wf[fs % NB], act[j]);
-        else mfma32_v(acc1a, wf[fs % NB], act[j]);
+        if (VAR == 2) {
+            asm volatile("" :: "v"(wf[fs % NB]));
+        } else if (j == 0) {
+            asm volatile("s_waitcnt lgkmcnt(%4)" : "+v"(bq[0]), "+v"(bq[1]), "+v"(bq[2]), "+v"(bq[3]) : "i"(PD));
+            const f32x8 c01 = __builtin_shufflevector(bq[0], bq[1], 0, 1, 2, 3, 4, 5, 6, 7);
+            const f32x8 c23 = __builtin_shufflevector(bq[2], bq[3], 0, 1, 2, 3, 4, 5, 6, 7);
+            const f32x16 cb = __builtin_shufflevector(c01, c23, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15);
+            mfma32_vc(acc1, wf[fs % NB], act[0], cb);
+        } else {
+            mfma32_v(acc1, wf[fs % NB], act[j]);
+        }
     };
     auto p2 = [&](int f, int fs, int k, const bf16x8 (&hb)[2]) __attribute__((always_inline)) {   // phase 2: output block k & 15, hidden k step k >> 4
         step_pre(f, fs);
         if (VAR == 2) asm volatile("" :: "v"(wf[fs % NB]), "v"(hb[k >> 4]));
         else mfma_a(acc[k & 15], wf[fs % NB], hb[k >> 4]);
     };
-    // phase 1's last MFMAs drained (24 wait states before a VALU reads their results) and b1 landed (at most the PD
-    // younger fragment reads outstanding)
+    // phase 1's last MFMAs drained (24 wait states before a VALU reads their results)
     auto acc1_ready = [&]() __attribute__((always_inline)) {
         __builtin_amdgcn_sched_barrier(0);
-        asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" : "+v"(acc1a), "+v"(acc1b));
-        asm volatile("s_waitcnt lgkmcnt(%4)" : "+v"(bq[0]), "+v"(bq[1]), "+v"(bq[2]), "+v"(bq[3]) : "i"(PD));
+        if constexpr (VAR != 11) asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" : "+v"(acc1));
         __builtin_amdgcn_sched_barrier(0);
     };
-    // relu((H_a + H_b) + b1) -> bf16 for register group q (4 features) into hb
+    // relu(H) -> bf16 for register group q (4 features) into hb
     auto relu_q = [&](int q, bf16x8 (&hb)[2]) __attribute__((always_inline)) {
         __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) hb[q >> 1][4 * (q & 1) + i] = f2bf(fmaxf((acc1a[4 * q + i] + acc1b[4 * q + i]) + bq[q][i], 0.f));
+        if constexpr (VAR != 10 && VAR != 12) {
+            const bf16x4 t = {f2bf(acc1[4 * q]), f2bf(acc1[4 * q + 1]), f2bf(acc1[4 * q + 2]), f2bf(acc1[4 * q + 3])};
+            uint2 u;
+            __builtin_memcpy(&u, &t, 8);
+            asm volatile("v_pk_max_i16 %0, %0, 0\n\tv_pk_max_i16 %1, %1, 0" : "+v"(u.x), "+v"(u.y));
+            __builtin_memcpy(((char*)&hb[q >> 1]) + 8 * (q & 1), &u, 8);
+        } else {
+            asm volatile("" :: "v"(acc1));
+        }
         // pin the packed bf16 here: left alone, instruction selection sinks the v_cvt_pk_bf16_f32 next to the operand's
         // first MFMA, past every scheduling fence, with no wait state between the VALU write and the MFMA read
         asm volatile("" : "+v"(hb[q >> 1]));
         __builtin_amdgcn_sched_barrier(0);
     };
     // body c: slots 3m, 3m+1 = P1(c+1) k steps 2m, 2m+1; slot 3m+2 = P2(c) block m, hidden k step 0; slots 48..63 =
-    // P2(c) blocks 0..15, hidden k step 1, with relu(c+1) in four groups behind slots 50, 52, 54, 56
-    auto body = [&](int c, const bf16x8 (&hcur)[2], bf16x8 (&hnext)[2]) __attribute__((always_inline)) {
+    // P2(c) blocks 0..15, hidden k step 1, with relu(c+1) in four groups behind slots 50, 52, 54, 56; b1 of chunk
+    // c+2 is read at the body's start (bqn: the buffer chunk c's biases left)
+    auto body = [&](int c, const bf16x8 (&hcur)[2], bf16x8 (&hnext)[2], f32x4 (&bqc)[4], f32x4 (&bqn)[4])
+        __attribute__((always_inline)) {
         const int fb = F0 + 32 + CHF * c;
-        b1_issue(c + 1);
+        if (c + 2 < NCH) b1_issue(c + 2, bqn);
 #pragma unroll
         for (int m = 0; m < 16; ++m) {
-            p1(fb + 3 * m, 3 * m, 2 * m);
-            p1(fb + 3 * m + 1, 3 * m + 1, 2 * m + 1);
+            p1(fb + 3 * m, 3 * m, 2 * m, bqc);
+            p1(fb + 3 * m + 1, 3 * m + 1, 2 * m + 1, bqc);
             p2(fb + 3 * m + 2, 3 * m + 2, m, hcur);
         }
 #pragma unroll
@@ -563,18 +594,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         valu_to_mfma();
     };
     if constexpr (VAR != 5) {
-        b1_issue(0);
+        b1_issue(0, bqa);
+        b1_issue(1, bqb);
 #pragma unroll
-        for (int j = 0; j < 32; ++j) p1(F0 + j, j, j);   // head: P1(0)
+        for (int j = 0; j < 32; ++j) p1(F0 + j, j, j, bqa);   // head: P1(0)
         acc1_ready();
 #pragma unroll
         for (int q = 0; q < 4; ++q) relu_q(q, hfa);
         valu_to_mfma();
         for (int c = 0; c < NCH - 2; c += 2) {
-            body(c, hfa, hfb);
-            body(c + 1, hfb, hfa);
+            body(c, hfa, hfb, bqb, bqa);
+            body(c + 1, hfb, hfa, bqa, bqb);
         }
-        body(NCH - 2, hfa, hfb);
+        body(NCH - 2, hfa, hfb, bqb, bqa);
         const int ft = F0 + 32 + CHF * (NCH - 1);
 #pragma unroll
         for (int k = 0; k < 32; ++k) p2(ft + k, k, k, hfb);   // tail: P2(63)
@@ -682,13 +714,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
             else if (p == 1) stamp(10);
             else stamp(12);
         }
-        if constexpr (VAR == 9) {   // the stores retired, then the record
+        if constexpr (VAR == 9 || VAR == 12) {   // the stores retired, then the record
             vm_wait<0>();
             stamp(13);
-            if (tid < 14) {
+            if (tid < 16) {
                 unsigned long long v = tsv[0];
 #pragma unroll
-                for (int i = 1; i < 14; ++i) v = tid == i ? tsv[i] : v;
+                for (int i = 1; i < 16; ++i) v = tid == i ? tsv[i] : v;
                 ((unsigned long long*)(Xo + (long long)M * FD))[16 * blockIdx.x + tid] = v;
             }
         }

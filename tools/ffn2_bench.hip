@@ -74,6 +74,20 @@ int main(int argc, char** argv) {
                 *bo = vecs + 12288, *c1 = vecs + 14336;
     // PMC passes: FFN2_ONLY=1 the OP kernel alone (MODE 1), FFN2_ONLY=4 the OP + next-QKV kernel (MODE 4, the default)
     // FFN2_ANAT=1: the anatomy of the default encoder launch (MODE 5, PFM_FAST_XW 7) and of MODE 4 / 6 beside it
+    if (getenv("FFN2_ANAT") && atoi(getenv("FFN2_ANAT")) == 2) {   // the stream's VALU / wait-state diagnostics
+        for (int M : Ms) {
+            run<4, 0>(M, 8000, X, g, be, Wp, b1, b2, Xo, gn, bn, Xn, O, Fr, bo, c1);   // ~2 s: sustained clock
+            for (int round = 0; round < 2; ++round) {
+                float t0 = run<4, 0>(M, 2000, X, g, be, Wp, b1, b2, Xo, gn, bn, Xn, O, Fr, bo, c1);
+                float t10 = run<4, 10>(M, 2000, X, g, be, Wp, b1, b2, Xo, gn, bn, Xn, O, Fr, bo, c1);
+                float t11 = run<4, 11>(M, 2000, X, g, be, Wp, b1, b2, Xo, gn, bn, Xn, O, Fr, bo, c1);
+                float t3 = run<4, 3>(M, 2000, X, g, be, Wp, b1, b2, Xo, gn, bn, Xn, O, Fr, bo, c1);
+                printf("M=%d MODE4 round %d: full %.1f  no-relu %.1f  no-nops %.1f  no-DMA/bar %.1f us\n", M, round, t0,
+                       t10, t11, t3);
+            }
+        }
+        return 0;
+    }
     if (getenv("FFN2_ANAT")) {
         for (int M : Ms) {
             const double fl = 2.0 * M * 512.0 * (512 + 2048 + 2048 + 1536);
@@ -115,9 +129,15 @@ int main(int argc, char** argv) {
         for (int M : Ms) {
             const int nb = (M + BM - 1) / BM;
             std::vector<unsigned long long> ts(16 * nb);
-            for (int mode = 5; mode >= 4; --mode) {
+            for (int mode = 5; mode >= 3; --mode) {   // 3 here = MODE 4 without the relu VALU (VAR 12)
+                // ~2 s of back-to-back launches first: the clock the chip holds under sustained load (DVFS)
+                const float hot = mode == 5 ? run<5, 0>(M, 8000, X, g, be, Wp, b1, b2, Xo, gn, bn, Xn, O, Fr, bo, c1)
+                                  : mode == 4 ? run<4, 0>(M, 8000, X, g, be, Wp, b1, b2, Xo, gn, bn, Xn, O, Fr, bo, c1)
+                                              : run<4, 10>(M, 8000, X, g, be, Wp, b1, b2, Xo, gn, bn, Xn, O, Fr, bo, c1);
+                printf("M=%d MODE%d sustained (8000 launches): %.1f us per launch\n", M, mode, hot);
                 float t = mode == 5 ? run<5, 9>(M, 5, X, g, be, Wp, b1, b2, Xo, gn, bn, Xn, O, Fr, bo, c1)
-                                    : run<4, 9>(M, 5, X, g, be, Wp, b1, b2, Xo, gn, bn, Xn, O, Fr, bo, c1);
+                        : mode == 4 ? run<4, 9>(M, 5, X, g, be, Wp, b1, b2, Xo, gn, bn, Xn, O, Fr, bo, c1)
+                                    : run<4, 12>(M, 5, X, g, be, Wp, b1, b2, Xo, gn, bn, Xn, O, Fr, bo, c1);
                 CK(hipMemcpy(ts.data(), Xo + (long long)M * 512, ts.size() * 8, hipMemcpyDeviceToHost));
                 unsigned long long t0 = ~0ull, t1 = 0, e0 = ~0ull;
                 for (int b = 0; b < nb; ++b) {
@@ -127,6 +147,12 @@ int main(int argc, char** argv) {
                 }
                 printf("M=%d MODE%d launch %.1f us (events); stamps: first start -> last end %.1f us, start skew %.1f us, "
                        "end skew %.1f us\n", M, mode, t, (t1 - t0) / 100.0, 0.0, (t1 - e0) / 100.0);
+                std::vector<double> clk;
+                for (int b = 0; b < nb; ++b)
+                    clk.push_back((double)(ts[16 * b + 15] - ts[16 * b + 14]) / (double)(ts[16 * b + 4] - ts[16 * b + 3]) * 0.1);
+                std::sort(clk.begin(), clk.end());
+                printf("  in-kernel shader clock over the FFN stream: median %.3f GHz (min %.3f, max %.3f)\n",
+                       clk[clk.size() / 2], clk.front(), clk.back());
                 double sk = 0;
                 for (int b = 0; b < nb; ++b) sk = std::max(sk, (ts[16 * b] - t0) / 100.0);
                 printf("  start skew (max over workgroups) %.1f us\n", sk);
