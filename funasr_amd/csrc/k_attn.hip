@@ -76,9 +76,27 @@ __device__ __forceinline__ float xor32_add(float x) {
 
 template <typename T> struct AttnLds;
 
+// XCD-aware block order: consecutive linear block ids go to the 8 XCDs round-robin, so with the plain order the
+// query blocks of one (utterance, head) land on different XCDs and each fetches the K / V rows from HBM into its own
+// L2. Here the nq query blocks of one (utterance, head) take linear ids 8 apart (i, i + 8, ...): the same XCD, dispatched
+// together, so the later ones read the key tiles from that L2. A bijection of the grid; results are unchanged.
+__device__ __forceinline__ void attn_block(int& qt, int& h, int& b) {
+    qt = blockIdx.x; h = blockIdx.y; b = blockIdx.z;
+    const int nq = gridDim.x, nbh = gridDim.y * gridDim.z;
+    if (nq > 1 && (nbh & 7) == 0) {
+        const int id = blockIdx.x + nq * (blockIdx.y + gridDim.y * blockIdx.z);
+        const int g = id / (8 * nq), r = id - g * 8 * nq;
+        const int bh = 8 * g + (r & 7);
+        qt = r >> 3;
+        h = bh % gridDim.y;
+        b = bh / gridDim.y;
+    }
+}
+
 __global__ __launch_bounds__(256) void attn_f32_kernel(AttnArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int qt = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+    int qt, h, b;
+    attn_block(qt, h, b);
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int fr = lane & 31, fh = lane >> 5;
     const int klen = min(a.klen[b], a.Tk);
@@ -301,7 +319,8 @@ __device__ __forceinline__ void fsmn_epilogue_f32(const AttnArgs& a, int qt, int
 template <int VAR = 0>
 __global__ __launch_bounds__(512) void attn_x6_kernel(AttnArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int qt = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+    int qt, h, b;
+    attn_block(qt, h, b);
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int fr = lane & 31, fh = lane >> 5;
     const int klen = min(a.klen[b], a.Tk);
@@ -572,7 +591,8 @@ template <int NWV, int VAR = 0>
 __global__ __launch_bounds__(NWV * 64, 8 / NWV) void attn_bf16_kernel(AttnArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr int NT = NWV * 64, QBLK = NWV * QW;
-    const int qt = blockIdx.x, h = blockIdx.y, b = blockIdx.z;
+    int qt, h, b;
+    attn_block(qt, h, b);
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int fr = lane & 31, fh = lane >> 5;
     const int klen = min(a.klen[b], a.Tk);
