@@ -6,7 +6,7 @@ import torch
 from funasr_amd import runtime as rt
 
 SHAPES = [("qkv", 32000, 1536, 512), ("out", 32000, 512, 512), ("ffn1", 32000, 2048, 512),
-          ("ffn2", 32000, 512, 2048), ("conv", 32000, 512, 1536), ("kv_all", 32000, 16384, 512),
+          ("ffn2", 32000, 512, 2048), ("conv", 32000, 512, 1536), ("kv_all", 32000, 16384, 512), ("kv_grp", 32000, 4096, 512),
           ("dffn1", 14784, 2048, 512), ("dffn2", 14784, 512, 2048), ("dq", 14784, 512, 512),
           ("vocab", 14784, 8404, 512), ("sq4k", 4096, 4096, 4096)]
 
