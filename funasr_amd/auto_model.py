@@ -356,6 +356,7 @@ class AutoModel:
             speech_s += bt if bt > 0 else 0.0
             wall_s += t2 - t1
         self.last_speed = {"rtf": (wall_s / speech_s) if speech_s > 0 else None, "forward_s": wall_s}
+        self.last_gather = None   # data-parallel runs: "tensor" (token matrices over RCCL / gloo) or "objects"
         if dp:
             from .distributed import gather_results, gather_token_matrices
             # every rank must take the same gather: tensors only when all of them decoded greedy token matrices
@@ -364,6 +365,7 @@ class AutoModel:
                 flag = flag.cuda()
             torch.distributed.all_reduce(flag, op=torch.distributed.ReduceOp.MIN)
             if int(flag.item()) == 1:   # [n, L] int32 token matrices over RCCL; results built from them on every rank
+                self.last_gather = "tensor"
                 toks, ntok, index = gather_token_matrices(mats, mat_index)
                 if sorted(index.tolist()) != list(range(len(items))):
                     raise RuntimeError("data-parallel inference: the gathered token matrices do not cover the inputs")
@@ -371,6 +373,7 @@ class AutoModel:
                 return model.results_from_token_matrix(toks[order], ntok[order], [keys[i] for i in index[order]],
                                                        **{k: v for k, v in kwargs.items() if k != "key"})
             # (input index, result) pairs from every rank -> input order (stable: n-best order kept)
+            self.last_gather = "objects"
             pairs = gather_results(results)
             if any(not 0 <= i < len(items) for i, _ in pairs):
                 raise RuntimeError("data-parallel inference: gathered a result for an unknown input index")

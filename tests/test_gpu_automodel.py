@@ -171,7 +171,7 @@ def _dp_worker(rank, world, port, paths, q):
         res = am.generate(input=paths, batch_size=1)
         from funasr_amd.distributed import item_lengths, length_sorted_shards
         mine = length_sorted_shards(item_lengths(paths), world)[rank]
-        q.put((rank, res, mine))
+        q.put((rank, res, mine, am.last_gather))
     finally:
         dist.destroy_process_group()
 
@@ -194,10 +194,11 @@ def test_dp_world2_shared_device_matches_single_rank(tmp_path):
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    shards = [m for _, _, m in out]
+    shards = [m for _, _, m, _ in out]
     assert sorted(shards[0] + shards[1]) == list(range(len(paths)))
     assert min(len(s) for s in shards) >= len(paths) // world
-    for rank, res, _ in out:
+    for rank, res, _, how in out:
+        assert how == "tensor", (rank, how)   # the greedy token matrices went over the collective as int32 tensors
         assert res == one, rank   # gathered in input order, token for token
 
 
