@@ -151,6 +151,9 @@ int pfm_run(pfm_handle* h, void* stream, int mode, const float* feats, const int
  *   scores_out[B, nbest] f32 out: the hypothesis score
  * Optional outputs (NULL to skip; ABI 4): alphas / peaks [B, T+1] f32, the CIF weights and fire values of the same
  * encoder pass (pfm_run's; what pred_timestamp needs, model.py:572-582).
+ * Device scratch (held by the handle, grown on demand): per utterance the CTC log-probs transposed frame-contiguous
+ * (V x T floats) plus the search state (~ 7 T beam P floats), i.e. about 4 B x B x V x T in total — 2.1 GB at B = 64,
+ * T = 1000, V = 8404; an allocation failure returns PFM_E_HIP before any launch.
  * The call synchronises `stream`. */
 int pfm_run_beam(pfm_handle* h, void* stream, int mode, const float* feats, const int32_t* lens, int B, int T,
                  int beam, float ctc_weight, float penalty, int nbest, int end_detect, int sos, int eos, int blank,
