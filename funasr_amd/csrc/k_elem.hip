@@ -481,7 +481,10 @@ __global__ __launch_bounds__(256) void cif_alpha_kernel(const float* __restrict_
 // Grid (D/64 channel slabs, B): one wave per (slab, utterance), one channel per lane. Every wave
 // recomputes the (uniform) fire schedule, so each channel's operations and their order are those of
 // the sequential reference loop; h rows are prefetched CIF_PF frames ahead of the recurrence.
-constexpr int CIF_PF = 16;   // frames per batch; the next batch is in flight while one is scanned
+#ifndef CIF_PF_N
+#define CIF_PF_N 16
+#endif
+constexpr int CIF_PF = CIF_PF_N;   // frames per batch; the next batch is in flight while one is scanned
 __global__ __launch_bounds__(64) void cif_fire_kernel(const float* __restrict__ alphas, const float* __restrict__ h,
                                                       RowMap hmap, int T, int D, int Lcap,
                                                       float* __restrict__ emb, float* __restrict__ peaks,

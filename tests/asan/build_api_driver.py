@@ -48,7 +48,8 @@ def build_api_driver() -> str:
                       if f.endswith(".o") and f[:-2] not in SANITIZED)
     deps = objs + [drv_obj] + lib_objs
     if _newer(OUT, deps):
-        subprocess.run([cc, f"--offload-arch={ARCH}", "-fsanitize=address,undefined", "-o", OUT + ".tmp"] + deps,
+        subprocess.run([cc, f"--offload-arch={ARCH}", "-fsanitize=address,undefined", "-fno-gpu-sanitize", "-o",
+                        OUT + ".tmp"] + deps,
                        check=True, capture_output=True, text=True)
         os.replace(OUT + ".tmp", OUT)
     return OUT

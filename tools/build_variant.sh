@@ -1,11 +1,12 @@
 #!/bin/bash
 # Build a variant of libpfm_hip.so with one source recompiled under extra defines, for A/B runs (PFM_LIB):
-#   tools/build_variant.sh NAME SRC.hip -DMACRO=V ...   -> funasr_amd/_lib/var/NAME/libpfm_hip.so
+#   tools/build_variant.sh NAME SRC.hip -DMACRO=V ...   -> abvar/NAME/libpfm_hip.so (git-ignored, outside the product
+#   package; delete after the A/B)
 set -e
 name=$1; src=$2; shift 2
 R=$(cd "$(dirname "$0")/.." && pwd)
 python -c "import sys; sys.path.insert(0, '$R'); import funasr_amd.build as b; b.build()" > /dev/null
-out=$R/funasr_amd/_lib/var/$name; mkdir -p $out
+out=$R/abvar/$name; mkdir -p $out
 objs=""
 for o in $R/funasr_amd/_lib/obj/*.o; do
   if [ "$(basename $o)" = "$(basename $src).o" ]; then
