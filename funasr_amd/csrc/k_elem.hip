@@ -482,7 +482,7 @@ __global__ __launch_bounds__(256) void cif_alpha_kernel(const float* __restrict_
 // recomputes the (uniform) fire schedule, so each channel's operations and their order are those of
 // the sequential reference loop; h rows are prefetched CIF_PF frames ahead of the recurrence.
 #ifndef CIF_PF_N
-#define CIF_PF_N 16
+#define CIF_PF_N 32
 #endif
 constexpr int CIF_PF = CIF_PF_N;   // frames per batch; the next batch is in flight while one is scanned
 __global__ __launch_bounds__(64) void cif_fire_kernel(const float* __restrict__ alphas, const float* __restrict__ h,
