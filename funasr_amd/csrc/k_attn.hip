@@ -701,79 +701,41 @@ __global__ __launch_bounds__(NWV * 64, 8 / NWV) void attn_bf16_kernel(AttnArgs a
         f32x16 s[2];
         // all 16 K fragments of the tile are read before the first product (graduated lgkmcnt waits): left to
         // the scheduler, each ds_read was followed by lgkmcnt(0) and its MFMA, one LDS latency per product
-        auto qk = [&]() {
-            bf16x8 kx[2][8];
+        bf16x8 kx[2][8];
 #pragma unroll
-            for (int kb = 0; kb < 2; ++kb) {
-                const int row = kb * 32 + fr;
+        for (int kb = 0; kb < 2; ++kb) {
+            const int row = kb * 32 + fr;
 #pragma unroll
-                for (int kq = 0; kq < 8; ++kq)
-                    kx[kb][kq] = *(const bf16x8*)(Ks + row * KROW + (((2 * kq + fh) ^ (row & 15)) << 4));
-            }
-            __builtin_amdgcn_sched_barrier(0);
+            for (int kq = 0; kq < 8; ++kq) kx[kb][kq] = *(const bf16x8*)(Ks + row * KROW + (((2 * kq + fh) ^ (row & 15)) << 4));
+        }
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-            for (int kb = 0; kb < 2; ++kb) {
+        for (int kb = 0; kb < 2; ++kb) {
 #pragma unroll
-                for (int e = 0; e < 16; ++e) s[kb][e] = 0.f;
-                if constexpr (VAR == 4) continue;
+            for (int e = 0; e < 16; ++e) s[kb][e] = 0.f;
+            if constexpr (VAR == 4) continue;
 #pragma unroll
-                for (int kq = 0; kq < 8; ++kq)
-                    s[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kx[kb][kq], qf[kq], s[kb], 0, 0, 0);
-            }
-            // lane holds S^T[key = t*64 + kb*32 + kappa(e) + 4fh][q = fr]
-            if ((t + 1) * KT2 > klen) {   // only the last tile can hold keys past klen
-                // a real branch: as a plain `if` the compiler if-converted the masking onto every tile (32 compares +
-                // 32 selects per tile); the empty volatile asm keeps it out of the common path
-                asm volatile("" ::: "memory");
-#pragma unroll
-                for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-                    for (int e = 0; e < 16; ++e) {
-                        const int key = t * KT2 + kb * 32 + kappa(e) + 4 * fh;
-                        if (key >= klen) s[kb][e] = -INFINITY;
-                    }
-            }
-        };
-        qk();
+            for (int kq = 0; kq < 8; ++kq) s[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kx[kb][kq], qf[kq], s[kb], 0, 0, 0);
+        }
+        // lane holds S^T[key = t*64 + kb*32 + kappa(e) + 4fh][q = fr]
         if constexpr (VAR != 2) {
+        if ((t + 1) * KT2 > klen) {   // only the last tile can hold keys past klen
+            // a real branch: as a plain `if` the compiler if-converted the masking onto every tile (32 compares +
+            // 32 selects per tile); the empty volatile asm keeps it out of the common path
+            asm volatile("" ::: "memory");
+#pragma unroll
+            for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+                for (int e = 0; e < 16; ++e) {
+                    const int key = t * KT2 + kb * 32 + kappa(e) + 4 * fh;
+                    if (key >= klen) s[kb][e] = -INFINITY;
+                }
+        }
         float mt = -INFINITY;
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
             for (int e = 0; e < 16; ++e) mt = fmaxf(mt, s[kb][e]);
-        float ls = 0.f;
-        if (VAR == 6 && t > 0) {
-            // the exponentials against the running max need not wait for this tile's max, which only decides the
-            // (rare) rescale: then the tile is redone from its K tile, still in LDS, exactly as below
-            const float m0 = mused;
-#pragma unroll
-            for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-                for (int e = 0; e < 16; ++e) {
-                    s[kb][e] = __builtin_amdgcn_exp2f(s[kb][e] - m0);
-                    ls += s[kb][e];
-                }
-            mt = xor32_max(mt);
-            if (mt > m0 + RESCALE_THR * 1.4426950408889634f) {
-                asm volatile("" ::: "memory");
-                const float corr = __builtin_amdgcn_exp2f(m0 - mt);
-                lrun *= corr;
-#pragma unroll
-                for (int d = 0; d < 4; ++d)
-#pragma unroll
-                    for (int e = 0; e < 16; ++e) o[d][e] *= corr;
-                mused = mt;
-                qk();
-                ls = 0.f;
-#pragma unroll
-                for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-                    for (int e = 0; e < 16; ++e) {
-                        s[kb][e] = __builtin_amdgcn_exp2f(s[kb][e] - mused);
-                        ls += s[kb][e];
-                    }
-            }
-        } else {
         mt = xor32_max(mt);
         if (mt > mused + RESCALE_THR * 1.4426950408889634f) {   // lazy rescale (log2 units; rare after tile 0)
             const float corr = __builtin_amdgcn_exp2f(mused - mt);
@@ -784,6 +746,7 @@ __global__ __launch_bounds__(NWV * 64, 8 / NWV) void attn_bf16_kernel(AttnArgs a
                 for (int e = 0; e < 16; ++e) o[d][e] *= corr;
             mused = mt;
         }
+        float ls = 0.f;
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
@@ -791,7 +754,6 @@ __global__ __launch_bounds__(NWV * 64, 8 / NWV) void attn_bf16_kernel(AttnArgs a
                 s[kb][e] = __builtin_amdgcn_exp2f(s[kb][e] - mused);
                 ls += s[kb][e];
             }
-        }
         ls = xor32_add(ls);
         lrun += ls;
         } else {

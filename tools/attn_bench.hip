@@ -121,30 +121,6 @@ int main(int argc, char** argv) {
     std::vector<int> hl(Bmax, T);
     CK(hipMemcpy(lens, hl.data(), Bmax * 4, hipMemcpyHostToDevice));
     const int reps = argc > 1 ? atoi(argv[1]) : 20;
-    if (argc > 2 && atoi(argv[2]) == 6) {   // VAR 6 (exponentials before the tile max) vs VAR 0: identical bytes, time
-        const int B = 64;
-        AttnArgs a;
-        a.q = qkv; a.qmap = rowmap_plain(3 * D); a.k = qkv + D; a.kmap = rowmap_plain(3 * D);
-        a.v = qkv + 2 * D; a.vmap = rowmap_plain(3 * D);
-        a.o = nullptr; a.ldo = D; a.o2 = ob; a.o2_dtype = DT_BF16; a.klen = lens; a.Tq = T; a.Tk = T;
-        a.scale = 1.f / sqrtf(128.f); a.fw = fw; a.fout = fb; a.fld = D; a.fD = D;
-        const size_t nb = (size_t)B * T * D * 2;
-        std::vector<char> o0(nb), f0(nb), o6(nb), f6(nb);
-        (void)run<0>(a, B, T, 1);
-        CK(hipMemcpy(o0.data(), ob, nb, hipMemcpyDeviceToHost));
-        CK(hipMemcpy(f0.data(), fb, nb, hipMemcpyDeviceToHost));
-        CK(hipMemset(ob, 0, nb));
-        (void)run<6>(a, B, T, 1);
-        CK(hipMemcpy(o6.data(), ob, nb, hipMemcpyDeviceToHost));
-        CK(hipMemcpy(f6.data(), fb, nb, hipMemcpyDeviceToHost));
-        printf("VAR 6 identical to VAR 0: out %d fsmn %d\n", o0 == o6, f0 == f6);
-        const double fl = 4.0 * B * (double)T * T * 128 * H;
-        for (int round = 0; round < 5; ++round) {
-            const float t0 = run<0>(a, B, T, reps), t6 = run<6>(a, B, T, reps);
-            printf("B=%d: VAR 0 %.1f us (%.0f TF) | VAR 6 %.1f us (%.0f TF)\n", B, t0, fl / t0 / 1e6, t6, fl / t6 / 1e6);
-        }
-        return 0;
-    }
     bench_x6(reps);
     for (int B : {32, 64}) {
         AttnArgs a;
