@@ -125,20 +125,24 @@ def stream_leg(args, dev, torch, make_weights) -> dict:
             del st, chunks
         del eng
     if args.cpu_utts > 0:
-        # the oracle's streaming restatement (torch-CPU fp32, one stream) on the first 10 chunks
+        # the oracle's streaming restatement (torch-CPU fp32, one stream): chunks until >= 5 s of CPU time (at most
+        # the leg's C chunks), so the sample is seconds, not a few chunk latencies
         from oracle.streaming_ref import StreamState, chunk_step
         w = make_weights(cfg, args.seed)
         torch.set_num_threads(int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)))
         ss = StreamState(cfg, (0, 10, 5), 4, 1)
-        xs = torch.randn((10, 10, cfg.input_size), generator=torch.Generator().manual_seed(5))
+        xs = torch.randn((C, 10, cfg.input_size), generator=torch.Generator().manual_seed(5))
+        chunk_step(xs[0], StreamState(cfg, (0, 10, 5), 4, 1), w, cfg, False)   # warmup (allocator, MKL)
         tc = time.perf_counter()
-        for c in range(10):
-            chunk_step(xs[c], ss, w, cfg, c == 9)
+        nc = 0
+        while nc < C and (nc < 10 or time.perf_counter() - tc < 5.0):
+            chunk_step(xs[nc], ss, w, cfg, nc == C - 1)
+            nc += 1
         dtc = time.perf_counter() - tc
-        res["cpu_baseline"] = {"value": round(10 * 0.6 / dtc, 2), "unit": "audio-sec/sec",
+        res["cpu_baseline"] = {"value": round(nc * 0.6 / dtc, 2), "unit": "audio-sec/sec",
                                "cores": torch.get_num_threads(), "kind": "port",
-                               "sample": f"1 stream x 10 chunks (6 s) through oracle/streaming_ref.chunk_step "
-                                         f"(torch-CPU fp32), {dtc:.2f} s on {cpu_model()}"}
+                               "sample": f"1 stream x {nc} chunks ({nc * 0.6:.1f} s of audio) through "
+                                         f"oracle/streaming_ref.chunk_step (torch-CPU fp32), {dtc:.2f} s on {cpu_model()}"}
     return res
 
 
@@ -168,13 +172,18 @@ def punc_leg(args, dev, torch, make_weights) -> dict:
     if args.cpu_utts > 0:
         from oracle.punc_ref import punc_forward
         torch.set_num_threads(int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)))
-        x = ids[:8].cpu().numpy()
+        x = ids.cpu().numpy()
+        punc_forward(x[:2], [T] * 2, w, cfg)   # warmup
         tc = time.perf_counter()
-        punc_forward(x, [T] * 8, w, cfg)
+        reps = 0
+        while reps < 1 or time.perf_counter() - tc < 3.0:   # the whole B x T batch, repeated for >= 3 s
+            punc_forward(x, [T] * B, w, cfg)
+            reps += 1
         dtc = time.perf_counter() - tc
-        res["cpu_baseline"] = {"value": round(8 * T / dtc, 1), "unit": "words/sec", "cores": torch.get_num_threads(),
-                               "kind": "port", "sample": f"8 sequences x {T} words through oracle/punc_ref.punc_forward "
-                                                         f"(torch-CPU fp32), {dtc:.2f} s on {cpu_model()}"}
+        res["cpu_baseline"] = {"value": round(reps * B * T / dtc, 1), "unit": "words/sec",
+                               "cores": torch.get_num_threads(), "kind": "port",
+                               "sample": f"{reps} x {B} sequences x {T} words through oracle/punc_ref.punc_forward "
+                                         f"(torch-CPU fp32), {dtc:.2f} s on {cpu_model()}"}
     del eng
     return res
 
@@ -221,6 +230,34 @@ def long_audio_leg(args, sd, cfg) -> dict:
             "text_chars": len(res[0]["text"]) if res else 0}
 
 
+def generate_leg(args, sd, cfg, feats, lens) -> dict:
+    """AutoModel.generate(input=fbank, input_len=lens, data_type="fbank") with a tokenizer: what §8(d) times, the
+    reference's model.inference inside AutoModel.inference (funasr/auto/auto_model.py:343-348) -- the decode, the
+    token-id readback, detokenisation, sentence_postprocess and the result dicts -- on the headline batch."""
+    import torch
+    from funasr_amd.auto_model import AutoModel
+    from tests.golden.inputs import token_list
+    am = AutoModel(model="Paraformer", model_conf=dict(ctc_weight=0.0, predictor_bias=1), device="cuda",
+                   mode=args.mode, tokenizer_conf=dict(token_list=token_list(cfg.vocab_size)), **cfg.reference_kwargs())
+    am.model.load_state_dict(sd)
+    B, T = int(feats.shape[0]), int(feats.shape[1])
+    kw = dict(input=feats, input_len=lens, data_type="fbank", batch_size=B)
+    for _ in range(2):
+        res = am.generate(**kw)
+    torch.cuda.synchronize()
+    steps = max(1, args.steps)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        res = am.generate(**kw)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    return {"workload": f"AutoModel.generate(fbank [{B},{T},560], data_type='fbank', batch_size={B}) with a "
+                        f"{cfg.vocab_size}-token CharTokenizer: decode + readback + detokenise + sentence_postprocess "
+                        "+ result dicts (reference auto_model.py:343-348)",
+            "value": round(B * T * FRAME_SEC / dt, 1), "unit": "audio-sec/sec", "ms_per_step": round(dt * 1e3, 3),
+            "results": len(res), "chars_mean": round(float(np.mean([len(r["text"]) for r in res])), 1)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -242,6 +279,7 @@ def main():
     ap.add_argument("--beam-steps", type=int, default=2,
                     help="timed joint decoder + CTC prefix beam search steps (Paraformer-large + CTC head; 0 = skip)")
     ap.add_argument("--beam", type=int, default=10, help="beam size of the beam-search leg")
+    ap.add_argument("--generate", type=int, default=1, help="time AutoModel.generate on the headline batch (0 = skip)")
     ap.add_argument("--long-audio-s", type=int, default=300,
                     help="seconds of synthetic audio for the VAD + ASR + punctuation leg (0 = skip)")
     args = ap.parse_args()
@@ -287,9 +325,9 @@ def main():
         bdev = dev if backend != "gloo" else torch.device("cpu")
         # fast mode reads every matrix as bf16: send those as bf16 (520 instead of 880 MB over xGMI)
         wire = "bf16" if args.mode == "fast" else "f32"
-        flat = broadcast_state_dict(param_layout(cfg), make_weights(cfg, args.seed) if rank == 0 else None,
-                                    device=bdev, keep_on_device=True, wire=wire)
-        eng.load_flat_device(flat.to(dev), param_layout(cfg), fast_only=wire == "bf16")
+        flat, wire_xw = broadcast_state_dict(param_layout(cfg), make_weights(cfg, args.seed) if rank == 0 else None,
+                                             device=bdev, keep_on_device=True, wire=wire, with_xw=True)
+        eng.load_flat_device(flat.to(dev), param_layout(cfg), fast_only=wire == "bf16", wire_xw=wire_xw)
         sd = None   # the host-side legs (long audio, CPU baseline) run at N=1 only
         del flat
     else:
@@ -380,7 +418,8 @@ def main():
         if pmc.get("mfma_busy_gemm_class") is not None:
             busy = round(pmc["mfma_busy_gemm_class"], 4)
             busy_src = f"profiles/{tname}: " + pmc.get("mfma_busy_definition", "")
-    xw_bits = int(os.environ.get("PFM_FAST_XW", "7") or 7) & 15
+    from funasr_amd.distributed import fast_xw_bits
+    xw_bits = fast_xw_bits()
     # the encoder layer launch: MODE 4, or with PFM_FAST_XW bit 4 / 8 MODE 5 / 6 (the v rows' / Wo's second weight
     # plane streamed too; algorithmic FLOPs are the same)
     dom_kernel = "ffn2_kernel<%d>" % (6 if xw_bits & 8 else 5 if xw_bits & 4 else 4)
@@ -457,7 +496,7 @@ def main():
             em = json.load(open(os.path.join(ROOT, "tests", "golden", "fast_emul.json")))["para_large_b64"]
             out["fast_fidelity"] = {
                 "golden": "para_large_b64 (reference run, B=64 x 500, seeded weights)",
-                "pfm_fast_xw": int(os.environ.get("PFM_FAST_XW", "7")),
+                "pfm_fast_xw": fast_xw_bits(),
                 "flip_frac": round(st["flip_frac"], 4), "mean_regret_nat": round(st["mean_regret"], 5),
                 "max_regret_nat": round(st["max_regret"], 4),
                 "outside_top5_frac": round(st["outside_topk"] / max(1, st["positions"]), 5),
@@ -497,6 +536,11 @@ def main():
             "fast_vs_exact_token_agreement": round(float(np.mean(agree)), 4),
             "fast_vs_exact_ntok_equal": round(float(np.mean(na == nb)), 4)}
 
+    # ---- AutoModel.generate() on the same batch: the metric as SURVEY §8(d) defines it (decode + host result dicts)
+    if rank == 0 and world == 1 and args.generate:
+        g = generate_leg(args, sd, cfg, feats, lens)
+        out["generate"] = g
+        out["generate_value"] = g["value"]
     if rank == 0:
         progress("exact leg done")
     # ---- SenseVoiceSmall (BASELINE config C4): B x 30 s on the same fbank batch, rank 0
@@ -582,8 +626,16 @@ def main():
         tc = time.perf_counter()
         paraformer_infer(x, ln, sd, cfg)
         dtc = time.perf_counter() - tc
+        ncpu = os.cpu_count() or 1
+        try:
+            aff = len(os.sched_getaffinity(0))
+        except AttributeError:
+            aff = ncpu
         out["cpu_baseline"] = {"value": round(args.cpu_utts * T * FRAME_SEC / dtc, 2), "unit": "audio-sec/sec",
                                "cores": torch.get_num_threads(), "kind": "port",
+                               "cores_note": (f"{torch.get_num_threads()} threads = this job's CPU share on the GPU box "
+                                              f"(OMP_NUM_THREADS, the pool's per-GPU allotment); os.cpu_count() = "
+                                              f"{ncpu} and sched_getaffinity = {aff} report the whole host"),
                                "sample": f"{args.cpu_utts} utts x 30 s (T=500) of the same batch, one call of "
                                          f"oracle/paraformer_ref.py (torch-CPU fp32, op-for-op restatement), "
                                          f"{dtc:.1f} s on {cpu_model()}"}

@@ -164,6 +164,44 @@ def merge_vad(vad_result, max_length=15000, min_length=0):
     return out
 
 
+def _dp_world(kwargs) -> Tuple[int, int]:
+    """(world, rank) of the data-parallel group a generate() call runs over: the initialised default process group,
+    unless the call passes dp=False. Under data parallelism generate() / inference() are COLLECTIVE calls: every
+    rank must make them, with the same number of inputs (a rank-0-only call would wait for the others forever)."""
+    if kwargs.get("dp", True) and torch.distributed.is_available() and torch.distributed.is_initialized():
+        return torch.distributed.get_world_size(), torch.distributed.get_rank()
+    return 1, 0
+
+
+def _merge_rank_dirs(model, out_dir: str, rank_dirs: List[str], keys: List[str], kwargs) -> None:
+    """Data-parallel output_dir: every rank wrote its share into its own directory (as the reference's multi-GPU
+    recipe writes one output dir per job, examples/aishell/paraformer/run.sh:136-170); rank 0 appends their lines to
+    the model's writer under out_dir in input order (key order of `keys`) and removes the rank directories."""
+    import shutil
+    from .writer import model_writer
+    order = {}
+    for i, k in enumerate(keys):
+        order.setdefault(str(k), i)
+    files: Dict[Tuple[str, ...], list] = {}
+    for rd in rank_dirs:
+        for root, _, names in os.walk(rd):
+            for n in names:
+                rel = tuple(os.path.relpath(os.path.join(root, n), rd).split(os.sep))
+                with open(os.path.join(root, n), encoding="utf-8") as f:
+                    for line in f:
+                        k, _, v = line.rstrip("\n").partition(" ")
+                        files.setdefault(rel, []).append((k, v))
+    writer = model_writer(model, {**kwargs, "output_dir": out_dir})
+    for rel in sorted(files):
+        w = writer
+        for part in rel:
+            w = w[part]
+        for k, v in sorted(files[rel], key=lambda kv: order.get(kv[0], len(order))):
+            w[k] = v
+    for rd in rank_dirs:
+        shutil.rmtree(rd, ignore_errors=True)
+
+
 class AutoModel:
     """funasr.auto.auto_model.AutoModel on the HIP path: model / vad_model / punc_model are built from
     registered names or local model dirs (auto_model.py:110-170); generate() runs inference_with_vad when
@@ -241,13 +279,42 @@ class AutoModel:
         kwargs.update(cfg)
         vad_kw = dict(self.vad_kwargs)
         vad_kw.update(cfg)
+        keys, items = prepare_data_iterator(input, input_len=input_len, data_type=kwargs.get("data_type"))
+        world, rank = _dp_world(kwargs)
+        if world > 1:   # data parallel over whole inputs: each rank runs VAD -> ASR -> punctuation on its own share
+            from .distributed import agree_item_count, gather_results, shard_items
+            if agree_item_count(len(items)) > 1:
+                mine = shard_items(items, world, rank)
+                sub = {**cfg, "dp": False}
+                out_dir = kwargs.get("output_dir")
+                if out_dir is not None:   # the ASR writer of each rank writes into a directory of its own
+                    saved, self.model.writer = getattr(self.model, "writer", None), None
+                    sub["output_dir"] = os.path.join(out_dir, f".dp_rank{rank}")
+                local = self._vad_pipeline([items[i] for i in mine], None, sub, {**kwargs, **sub}, vad_kw)
+                if out_dir is not None:
+                    if getattr(self.model, "writer", None) is not None:
+                        self.model.writer.close()
+                    self.model.writer = saved
+                    torch.distributed.barrier()
+                    if rank == 0:
+                        _merge_rank_dirs(self.model, out_dir,
+                                         [os.path.join(out_dir, f".dp_rank{r}") for r in range(world)], keys, kwargs)
+                    torch.distributed.barrier()
+                pairs = gather_results([(mine[j], r) for j, r in local])
+                return [r for _, r in sorted(pairs, key=lambda p: p[0])]
+        return [r for _, r in self._vad_pipeline(input, input_len, cfg, kwargs, vad_kw)]
+
+    def _vad_pipeline(self, input, input_len, cfg, kwargs, vad_kw):
+        """(input index, result) pairs of inference_with_vad on this process (inputs whose text is empty give none,
+        as in the reference)."""
+        vad_kw = {**vad_kw, "dp": cfg.get("dp", vad_kw.get("dp", True))}
         res = self.inference(input, input_len=input_len, model=self.vad_model, kwargs=vad_kw)
         if cfg.get("merge_vad", False):
             for r in res:
                 r["value"] = merge_vad(r["value"], kwargs.get("merge_length_s", 15) * 1000)
         batch_ms = max(int(kwargs.get("batch_size_s", 300)) * 1000, 1)
         thres_ms = int(kwargs.get("batch_size_threshold_s", 60)) * 1000
-        keys, items = prepare_data_iterator(input, input_len=input_len, data_type=kwargs.get("data_type"))
+        _, items = prepare_data_iterator(input, input_len=input_len, data_type=kwargs.get("data_type"))
         asr_kw = dict(kwargs)
         asr_kw.pop("batch_size_s", None)
         asr_kw["dp"] = False   # the segment batches of one input stay on this rank
@@ -258,7 +325,7 @@ class AutoModel:
             n = len(segs)
             order = sorted(range(n), key=lambda j: segs[j][1] - segs[j][0])
             if n == 0:
-                out.append({"key": key, "text": "", "timestamp": []})
+                out.append((i, {"key": key, "text": "", "timestamp": []}))
                 continue
             bsz = max(batch_ms, segs[order[0]][1] - segs[order[0]][0])
             results_sorted, beg, end, max_len = [], 0, 1, 0
@@ -277,7 +344,7 @@ class AutoModel:
                 results_sorted.extend(self.inference(batch, input_len=None, model=self.model, kwargs=asr_kw))
                 beg, end, max_len = end, end + 1, slen
             if len(results_sorted) != n:
-                out.append({"key": key, "text": "", "timestamp": []})
+                out.append((i, {"key": key, "text": "", "timestamp": []}))
                 continue
             restored = [None] * n
             for j in range(n):
@@ -300,12 +367,13 @@ class AutoModel:
             if self.punc_model is not None:
                 punc_kw = dict(self.punc_kwargs)
                 punc_kw.update(cfg)
+                punc_kw["dp"] = False   # one text of this rank's input: no collective
                 pres = self.inference(result["text"], model=self.punc_model, kwargs=punc_kw)
                 if kwargs.get("return_raw_text", False):
                     result["raw_text"] = result["text"]
                 result["text"] = pres[0]["text"]
             result["key"] = key
-            out.append(result)
+            out.append((i, result))
         return out
 
     def inference(self, input, input_len=None, model=None, kwargs=None, key=None, **cfg):
@@ -315,17 +383,23 @@ class AutoModel:
         model.eval()
         batch_size = int(kwargs.get("batch_size", 1))
         keys, items = prepare_data_iterator(input, input_len=input_len, data_type=kwargs.get("data_type"), key=key)
-        world, rank = 1, 0
-        if torch.distributed.is_available() and torch.distributed.is_initialized() and kwargs.get("dp", True):
-            world, rank = torch.distributed.get_world_size(), torch.distributed.get_rank()
+        world, rank = _dp_world(kwargs)
         dp = False
         if world > 1:   # every rank takes the same branch: the decision is made on rank 0's input count
             from .distributed import agree_item_count
             dp = agree_item_count(len(items)) > 1
         mine = list(range(len(items)))
+        out_dir, saved_writer = kwargs.get("output_dir"), None
         if dp:   # longest-first round-robin: balanced padded work per rank, decided on rank 0
             from .distributed import shard_items
             mine = shard_items(items, world, rank)
+            kb = [keys]   # rank 0's keys on every rank (generated keys are random per process)
+            torch.distributed.broadcast_object_list(kb, src=0)
+            keys = kb[0]
+            if out_dir is not None:   # each rank writes its share into a directory of its own (merged below)
+                saved_writer = getattr(model, "writer", None)
+                model.writer = None
+                kwargs["output_dir"] = os.path.join(out_dir, f".dp_rank{rank}")
         results = []
         mats, mat_index = [], []   # greedy token matrices (device) of this rank's batches, for the tensor gather
         speech_s, wall_s = 0.0, 0.0
@@ -357,6 +431,15 @@ class AutoModel:
             wall_s += t2 - t1
         self.last_speed = {"rtf": (wall_s / speech_s) if speech_s > 0 else None, "forward_s": wall_s}
         self.last_gather = None   # data-parallel runs: "tensor" (token matrices over RCCL / gloo) or "objects"
+        if dp and out_dir is not None:
+            if getattr(model, "writer", None) is not None:
+                model.writer.close()
+            model.writer = saved_writer
+            torch.distributed.barrier()   # every rank's files are complete
+            if rank == 0:
+                _merge_rank_dirs(model, out_dir, [os.path.join(out_dir, f".dp_rank{r}") for r in range(world)], keys,
+                                 kwargs)
+            torch.distributed.barrier()
         if dp:
             from .distributed import gather_results, gather_token_matrices
             # every rank must take the same gather: tensors only when all of them decoded greedy token matrices

@@ -178,6 +178,38 @@ int pfm_fail(int code, const char* msg) { return fail(code, msg); }
             return fail(PFM_E_HIP, std::string(#expr) + ": " + hipGetErrorString(_e));           \
     } while (0)
 
+// Device operands of the C ABI must be device memory of the call's GPU: a host (pageable or pinned) or unregistered
+// address handed to a kernel faults the device instead of failing the call, so every entry point asks the runtime
+// what each operand is before it launches anything and refuses with PFM_E_ARG, naming the operand. Interior pointers
+// of an allocation (tensor slices) resolve to the allocation. `dev` < 0: the calling thread's current device.
+struct DevOp { const char* name; const void* p; };
+static int check_dev(const char* fn, int dev, std::initializer_list<DevOp> ops) {
+    if (dev < 0 && hipGetDevice(&dev) != hipSuccess) {
+        (void)hipGetLastError();
+        return fail(PFM_E_HIP, std::string(fn) + ": no current HIP device");
+    }
+    for (const DevOp& o : ops) {
+        if (!o.p) continue;   // optional operand not given (required ones are null-checked before this)
+        hipPointerAttribute_t a{};
+        const hipError_t e = hipPointerGetAttributes(&a, o.p);
+        if (e != hipSuccess) (void)hipGetLastError();   // an unknown address sets the sticky error: clear it
+        const bool device = e == hipSuccess && (a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged);
+        if (!device)
+            return fail(PFM_E_ARG, std::string(fn) + ": operand '" + o.name +
+                                       "' is not device memory (host or unregistered address); device operands must be "
+                                       "allocated on the GPU");
+        if (a.type == hipMemoryTypeDevice && a.device != dev)
+            return fail(PFM_E_ARG, std::string(fn) + ": operand '" + o.name + "' is on device " +
+                                       std::to_string(a.device) + ", the call runs on device " + std::to_string(dev));
+    }
+    return PFM_OK;
+}
+#define CHECK_DEV(fn, dev, ...)                                 \
+    do {                                                        \
+        const int _rc = check_dev(fn, dev, {__VA_ARGS__});      \
+        if (_rc) return _rc;                                    \
+    } while (0)
+
 // Every field is an int; the FNV hash below walks them all. A thread that reads the knobs before any
 // C-ABI entry point refreshed them gets the documented defaults (lazy first refresh), never zero-fill.
 static_assert(sizeof(PfmKnobs) == (PFM_KNOB_FIELDS * sizeof(int) + 7) / 8 * 8 + sizeof(unsigned long long),
@@ -1444,6 +1476,7 @@ static void weight_written(pfm_handle* h, WEntry& e) {
     h->ffn_ready = false;
     h->dffn_ready = false;
     h->x6_ready = false;   // ensure_x6 re-splits arena_x6 and the padded planes in place (stable addresses)
+    h->xw_ready = false;   // PFM_FAST_XW split planes (predictor conv, layer 0, v rows) are rebuilt from the new weights
     h->ban_tok = -1;   // the banned-token bias copy follows ctc.ctc_lo.bias
 }
 
@@ -1497,6 +1530,7 @@ int pfm_set_weight_device(pfm_handle* h, const char* name, const void* dev_ptr, 
         if (e.shape[i] != shape[i])
             return fail(PFM_E_ARG, std::string("pfm_set_weight_device: shape mismatch for ") + name);
     if (e.kind == 2) return PFM_OK;
+    CHECK_DEV("pfm_set_weight_device", h->device, {"dev_ptr", dev_ptr});
     HIP_TRY(hipSetDevice(h->device));
     const hipStream_t st = (hipStream_t)stream;
     const float* src = (const float*)dev_ptr;
@@ -1530,6 +1564,8 @@ int pfm_run(pfm_handle* h, void* stream, int mode, const float* feats, const int
     if (mode != PFM_MODE_EXACT && mode != PFM_MODE_FAST) return fail(PFM_E_ARG, "pfm_run: bad mode");
     if (h->missing) return fail(PFM_E_STATE, "pfm_run: " + std::to_string(h->missing) + " weights not set");
     if (h->cfg.arch != PFM_ARCH_PARAFORMER) return fail(PFM_E_STATE, "pfm_run: handle is not a Paraformer");
+    CHECK_DEV("pfm_run", h->device, {"feats", feats}, {"lens", lens}, {"tokens", tokens}, {"ntok", ntok_out},
+              {"enc_out", enc_out}, {"alphas", alphas_out}, {"peaks", peaks_out});
     HIP_TRY(hipSetDevice(h->device));
     hipStream_t st = (hipStream_t)stream;
     int rc = reserve(h, B, T);
@@ -1855,6 +1891,8 @@ int pfm_run_beam(pfm_handle* h, void* stream, int mode, const float* feats, cons
         return fail(PFM_E_ARG, "pfm_run_beam: sos / eos / blank outside the vocabulary");
     if (beam < 1 || beam > 16 || nbest < 1 || nbest > 16 || P > 64 || !(ctc_weight > 1e-5f) || L_cap < 0)
         return fail(PFM_E_ARG, "pfm_run_beam: need 1 <= beam <= 16, 1 <= nbest <= 16, ctc_weight > 1e-5, <= 64 candidates");
+    CHECK_DEV("pfm_run_beam", h->device, {"feats", feats}, {"lens", lens}, {"tokens", tokens}, {"ntok", ntok_out},
+              {"scores", scores_out}, {"alphas", alphas_out}, {"peaks", peaks_out});
     HIP_TRY(hipSetDevice(h->device));
     hipStream_t st = (hipStream_t)stream;
     int32_t* ntok_dev = nullptr;
@@ -1921,6 +1959,8 @@ int pfm_run_ctc(pfm_handle* h, void* stream, int mode, const float* feats, const
     for (int i = 0; i < NQ; ++i)
         if (query[i] < 0 || query[i] >= c.n_embed) return fail(PFM_E_ARG, "pfm_run_ctc: query id out of range");
     if (ban_token >= c.vocab_size) return fail(PFM_E_ARG, "pfm_run_ctc: ban_token out of range");
+    CHECK_DEV("pfm_run_ctc", h->device, {"feats", feats}, {"lens", lens}, {"tokens", tokens}, {"ntok", ntok_out},
+              {"enc_out", enc_out}, {"frame_ids", frame_ids});
     HIP_TRY(hipSetDevice(h->device));
     hipStream_t st = (hipStream_t)stream;
     const int Tq = T + NQ;
@@ -1988,6 +2028,7 @@ int pfm_run_punc(pfm_handle* h, void* stream, int mode, const int32_t* ids, cons
     if (mode != PFM_MODE_EXACT && mode != PFM_MODE_FAST) return fail(PFM_E_ARG, "pfm_run_punc: bad mode");
     if (h->missing) return fail(PFM_E_STATE, "pfm_run_punc: weights not set");
     const pfm_config& c = h->cfg;
+    CHECK_DEV("pfm_run_punc", h->device, {"ids", ids}, {"lens", lens}, {"punc", punc}, {"logits", logits});
     HIP_TRY(hipSetDevice(h->device));
     hipStream_t st = (hipStream_t)stream;
     const bool fast = mode == PFM_MODE_FAST;
@@ -2044,6 +2085,7 @@ int pfm_fbank_raw(pfm_handle* h, void* stream, const float* wav, const int32_t* 
     if (!h || !wav || !nsamp || !fb) return fail(PFM_E_ARG, "pfm_fbank_raw: null argument");
     if (B < 1 || S_max < 1 || N_cap < 1) return fail(PFM_E_ARG, "pfm_fbank_raw: bad sizes");
     if (pfm_fbank_nframes(S_max) > N_cap) return fail(PFM_E_ARG, "pfm_fbank_raw: N_cap smaller than frames of S_max");
+    CHECK_DEV("pfm_fbank_raw", h->device, {"wav", wav}, {"nsamp", nsamp}, {"fb", fb});
     HIP_TRY(hipSetDevice(h->device));
     int rc = fbank_tables_ready(h);
     if (rc) return rc;
@@ -2055,6 +2097,7 @@ int pfm_lfr_gather(void* stream, const float* frames, const int32_t* idx, int ro
                    float* out) {
     if (rows < 0 || m < 1 || (m * 80) % 4) return fail(PFM_E_ARG, "pfm_lfr_gather: bad sizes");
     if (rows > 0 && (!frames || !idx || !out)) return fail(PFM_E_ARG, "pfm_lfr_gather: null argument");
+    if (rows > 0) CHECK_DEV("pfm_lfr_gather", -1, {"frames", frames}, {"idx", idx}, {"cmvn", cmvn}, {"out", out});
     HIP_TRY(pfm_lfr_gather_launch(frames, idx, rows, m, cmvn, out, (hipStream_t)stream));
     return PFM_OK;
 }
@@ -2065,6 +2108,7 @@ int pfm_fbank(pfm_handle* h, void* stream, const float* wav, const int32_t* nsam
     if (!h || !wav || !nsamp || !feats || !T_out) return fail(PFM_E_ARG, "pfm_fbank: null argument");
     if (B < 1 || S_max < 1 || T_cap < 1) return fail(PFM_E_ARG, "pfm_fbank: bad sizes");
     if (pfm_fbank_frames(S_max) > T_cap) return fail(PFM_E_ARG, "pfm_fbank: T_cap smaller than LFR frames of S_max");
+    CHECK_DEV("pfm_fbank", h->device, {"wav", wav}, {"nsamp", nsamp}, {"cmvn", cmvn}, {"feats", feats}, {"T_out", T_out});
     HIP_TRY(hipSetDevice(h->device));
     hipStream_t st = (hipStream_t)stream;
     int rc = fbank_tables_ready(h);
@@ -2103,6 +2147,7 @@ int pfm_op_gemm(void* stream, int dtype, const void* A, const void* Wt, const fl
     if (M < 0 || N < 1 || K < 1) return fail(PFM_E_ARG, "pfm_op_gemm: bad sizes");
     if (dtype != DT_F32 && dtype != DT_BF16) return fail(PFM_E_ARG, "pfm_op_gemm: dtype must be PFM_F32 or PFM_BF16");
     if ((act & 2) && dtype != DT_BF16) return fail(PFM_E_ARG, "pfm_op_gemm: bf16 output needs bf16 operands");
+    CHECK_DEV("pfm_op_gemm", -1, {"A", A}, {"W", Wt}, {"bias", bias}, {"res", res}, {"C", C});
     GemmEpi e = epi_default();
     e.bias = bias; e.relu = act & 1;
     if (res) { e.res0 = res; e.ld_res0 = N; }
@@ -2121,6 +2166,7 @@ int pfm_op_ln_gemm(void* stream, const float* X, const float* g, const float* b,
                    const float* bias, const float* res, float* C, int M, int N, int act) {
     pfm_knobs_refresh();
     if (!X || !g || !b || !W || !C || M < 0 || N < 0) return fail(PFM_E_ARG, "pfm_op_ln_gemm: null operand or bad sizes");
+    CHECK_DEV("pfm_op_ln_gemm", -1, {"X", X}, {"g", g}, {"b", b}, {"W", W}, {"bias", bias}, {"res", res}, {"C", C});
     const hipStream_t st = (hipStream_t)stream;
     GemmEpi e = epi_default();
     e.bias = bias; e.relu = act & 1;
@@ -2173,6 +2219,8 @@ int pfm_op_ffn(void* stream, const float* x, int M, const float* g2, const float
     if (!x || !xo || !W1 || !W2 || !g2 || !b2n || !b1 || !b2 || M < 0) return fail(PFM_E_ARG, "pfm_op_ffn: null operand");
     if ((xn != nullptr) != (gn != nullptr && bn != nullptr)) return fail(PFM_E_ARG, "pfm_op_ffn: xn needs gn and bn");
     if (!all_aligned16({x, xo, g2, b2n, b1, b2, xn, gn, bn})) return fail(PFM_E_ARG, "pfm_op_ffn: operands must be 16-B aligned");
+    CHECK_DEV("pfm_op_ffn", -1, {"x", x}, {"g2", g2}, {"b2n", b2n}, {"W1", W1}, {"b1", b1}, {"W2", W2}, {"b2", b2},
+              {"xo", xo}, {"gn", gn}, {"bn", bn}, {"xn", xn});
     const hipStream_t st = (hipStream_t)stream;
     const size_t nw = (size_t)2048 * 512;
     OpScratch sc;
@@ -2198,6 +2246,8 @@ int pfm_op_ffn_op(void* stream, const void* o, const void* f, const float* Wo, c
     if ((xn != nullptr) != (gn != nullptr && bn != nullptr)) return fail(PFM_E_ARG, "pfm_op_ffn_op: xn needs gn and bn");
     if (!all_aligned16({o, f, bo, x, xo, g2, b2n, b1, b2, xn, gn, bn}))
         return fail(PFM_E_ARG, "pfm_op_ffn_op: operands must be 16-B aligned");
+    CHECK_DEV("pfm_op_ffn_op", -1, {"o", o}, {"f", f}, {"Wo", Wo}, {"bo", bo}, {"x", x}, {"g2", g2}, {"b2n", b2n},
+              {"W1", W1}, {"b1", b1}, {"W2", W2}, {"b2", b2}, {"xo", xo}, {"gn", gn}, {"bn", bn}, {"xn", xn});
     const hipStream_t st = (hipStream_t)stream;
     const size_t nw = (size_t)2048 * 512, no = (size_t)512 * 512, po = pfm_ffn_packed_o_elems();
     OpScratch sc;
@@ -2228,6 +2278,9 @@ int pfm_op_ffn_op_qkv(void* stream, const void* o, const void* f, const float* W
         return fail(PFM_E_ARG, "pfm_op_ffn_op_qkv: null operand");
     if (!all_aligned16({o, f, bo, x, xo, g2, b2n, b1, b2, gn, bn, bq, qkv}))
         return fail(PFM_E_ARG, "pfm_op_ffn_op_qkv: operands must be 16-B aligned");
+    CHECK_DEV("pfm_op_ffn_op_qkv", -1, {"o", o}, {"f", f}, {"Wo", Wo}, {"bo", bo}, {"x", x}, {"g2", g2}, {"b2n", b2n},
+              {"W1", W1}, {"b1", b1}, {"W2", W2}, {"b2", b2}, {"xo", xo}, {"gn", gn}, {"bn", bn}, {"Wq", Wq}, {"bq", bq},
+              {"qkv", qkv});
     const hipStream_t st = (hipStream_t)stream;
     const size_t nw = (size_t)2048 * 512, no = (size_t)512 * 512, po = pfm_ffn_packed_o_elems(),
                  pfe = pfm_ffn_packed_elems();
@@ -2276,6 +2329,8 @@ int pfm_op_ffn_dec(void* stream, const float* x, int M, const float* g1, const f
     if (o && (!Wo || !bo || !xo)) return fail(PFM_E_ARG, "pfm_op_ffn_dec: o needs Wo, bo and xo");
     if (!all_aligned16({x, g1, b1n, b1, gF, bF, xo, gn, bn, xn, o, bo}))
         return fail(PFM_E_ARG, "pfm_op_ffn_dec: operands must be 16-B aligned");
+    CHECK_DEV("pfm_op_ffn_dec", -1, {"x", x}, {"g1", g1}, {"b1n", b1n}, {"W1", W1}, {"b1", b1}, {"W2", W2}, {"gF", gF},
+              {"bF", bF}, {"xo", xo}, {"gn", gn}, {"bn", bn}, {"xn", xn}, {"o", o}, {"Wo", Wo}, {"bo", bo});
     const hipStream_t st = (hipStream_t)stream;
     const size_t nw = (size_t)2048 * 512, no = (size_t)512 * 512, po = pfm_ffn_packed_o_elems();
     OpScratch sc;
@@ -2307,6 +2362,7 @@ int pfm_op_attention(void* stream, int dtype, const void* q, const void* k, cons
     if (!q || !k || !v || !klen || !out || B < 0 || Tq < 0 || Tk < 0 || heads < 1)
         return fail(PFM_E_ARG, "pfm_op_attention: null operand or bad sizes");
     if (dtype != DT_F32 && dtype != DT_BF16) return fail(PFM_E_ARG, "pfm_op_attention: dtype must be PFM_F32 or PFM_BF16");
+    CHECK_DEV("pfm_op_attention", -1, {"q", q}, {"k", k}, {"v", v}, {"klen", klen}, {"out", out});
     const int D = heads * 128;
     HIP_TRY(pfm_attention(dtype, q, rowmap_plain(D), k, rowmap_plain(D), v, rowmap_plain(D), out, D, nullptr, klen, B,
                           Tq, Tk, heads, 128, scale, (hipStream_t)stream));
@@ -2317,6 +2373,7 @@ int pfm_op_layernorm(void* stream, const float* x, const float* g, const float* 
                      float eps) {
     pfm_knobs_refresh();
     if (!x || !g || !b || !out || M < 0 || D < 1) return fail(PFM_E_ARG, "pfm_op_layernorm: null operand or bad sizes");
+    CHECK_DEV("pfm_op_layernorm", -1, {"x", x}, {"gamma", g}, {"beta", b}, {"out", out});
     HIP_TRY(pfm_layernorm(x, rowmap_plain(D), M, D, g, b, eps, nullptr, 0, 1.f, out, rowmap_plain(D), DT_F32,
                           nullptr, rowmap_plain(0), 0, (hipStream_t)stream));
     return PFM_OK;
@@ -2327,6 +2384,7 @@ int pfm_op_fsmn(void* stream, const float* v, const int32_t* len, const float* w
     pfm_knobs_refresh();
     if (!v || !len || !w || !out || B < 0 || T < 0 || D < 1 || K < 1 || left < 0)
         return fail(PFM_E_ARG, "pfm_op_fsmn: null operand or bad sizes");
+    CHECK_DEV("pfm_op_fsmn", -1, {"v", v}, {"len", len}, {"w", w}, {"res", res}, {"out", out});
     HIP_TRY(pfm_fsmn(v, rowmap_plain(D), len, B, T, D, w, K, left, res, out, nullptr, (hipStream_t)stream));
     return PFM_OK;
 }
@@ -2335,6 +2393,7 @@ int pfm_op_layernorm_bf16(void* stream, const void* x, const float* g, const flo
                           float eps) {
     if (!x || !g || !b || !out || M < 0 || (D != 512 && D != 1024 && D != 2048))
         return fail(PFM_E_ARG, "pfm_op_layernorm_bf16: null operand or bad sizes (D 512 / 1024 / 2048)");
+    CHECK_DEV("pfm_op_layernorm_bf16", -1, {"x", x}, {"gamma", g}, {"beta", b}, {"out", out});
     HIP_TRY(pfm_layernorm_bf16in((const bf16*)x, rowmap_plain(D), M, D, g, b, eps, out, rowmap_plain(D), DT_F32,
                                  (hipStream_t)stream));
     return PFM_OK;
@@ -2344,6 +2403,7 @@ int pfm_op_fsmn_bf16(void* stream, const void* v, const int32_t* len, const floa
                      int K, int left) {
     if (!v || !len || !w || !out || B < 0 || T < 0 || D < 1 || K < 1 || left < 0)
         return fail(PFM_E_ARG, "pfm_op_fsmn_bf16: null operand or bad sizes");
+    CHECK_DEV("pfm_op_fsmn_bf16", -1, {"v", v}, {"len", len}, {"w", w}, {"out", out});
     HIP_TRY(pfm_fsmn_bf16in((const bf16*)v, rowmap_plain(D), len, B, T, D, w, K, left, nullptr, nullptr, (bf16*)out,
                             (hipStream_t)stream));
     return PFM_OK;
@@ -2352,6 +2412,7 @@ int pfm_op_fsmn_bf16(void* stream, const void* v, const int32_t* len, const floa
 int pfm_op_ctc_collapse(void* stream, const int32_t* ids, int64_t ld, const int32_t* olen, int B, int blank,
                         int32_t* tokens, int L_cap, int32_t* ntok) {
     if (!ids || !olen || !tokens || !ntok || B < 0 || L_cap < 0) return fail(PFM_E_ARG, "pfm_op_ctc_collapse: bad arguments");
+    CHECK_DEV("pfm_op_ctc_collapse", -1, {"ids", ids}, {"olen", olen}, {"tokens", tokens}, {"ntok", ntok});
     HIP_TRY(pfm_ctc_collapse(ids, ld, olen, B, blank, L_cap, tokens, ntok, (hipStream_t)stream));
     return PFM_OK;
 }
@@ -2360,6 +2421,8 @@ int pfm_op_cif(void* stream, const float* alphas, const float* hidden, float* em
                int32_t* ntok, int B, int T, int D, int L_cap) {
     if (!alphas || !hidden || !emb || !peaks || !n_fire || !ntok || B < 0 || T < 0 || D < 1 || L_cap < 0)
         return fail(PFM_E_ARG, "pfm_op_cif: null operand or bad sizes");
+    CHECK_DEV("pfm_op_cif", -1, {"alphas", alphas}, {"hidden", hidden}, {"emb", emb}, {"peaks", peaks},
+              {"n_fire", n_fire}, {"ntok", ntok});
     HIP_TRY(pfm_cif_fire(alphas, hidden, rowmap_plain(D), B, T, D, L_cap, emb, peaks, n_fire, ntok,
                          (hipStream_t)stream));
     return PFM_OK;
@@ -2377,6 +2440,8 @@ int pfm_ctc_align(pfm_handle* h, void* stream, const float* enc, int B, int Tq, 
     if (blank < 0 || blank >= V) return fail(PFM_E_ARG, "pfm_ctc_align: blank outside the vocabulary");
     if (2 * (2 * (long long)Lmax + 3) * 4 > 64 * 1024) return fail(PFM_E_ARG, "pfm_ctc_align: Lmax too large");
     if (B == 0 || Tf <= 0) return PFM_OK;
+    CHECK_DEV("pfm_ctc_align", h->device, {"enc", enc}, {"olens", olens}, {"targets", Lmax > 0 ? targets : nullptr},
+              {"tlens", Lmax > 0 ? tlens : nullptr}, {"align", align});
     HIP_TRY(hipSetDevice(h->device));
     const hipStream_t st = (hipStream_t)stream;
     const long long M = (long long)B * Tf;
@@ -2413,6 +2478,8 @@ int pfm_op_ctc_beam(void* stream, const float* am, int L, const float* x, int T,
     if (beam < 1 || beam > 16 || nbest < 1 || nbest > 16 || P > 64 || L_cap < 0)
         return fail(PFM_E_ARG, "pfm_op_ctc_beam: need 1 <= beam <= 16, 1 <= nbest <= 16, <= 64 candidates");
     if (B == 0) return PFM_OK;
+    CHECK_DEV("pfm_op_ctc_beam", -1, {"am", am}, {"x", x}, {"lens", lens}, {"ntok", ntok}, {"tokens", tokens},
+              {"ntok_out", ntok_out}, {"scores", scores_out});
     const hipStream_t st = (hipStream_t)stream;
     OpScratch sc;
     float* fs;
@@ -3009,6 +3076,8 @@ int pfm_stream_step(pfm_streams* s, void* stream, int n, const int32_t* slot_ids
     if (!s || !slot_ids || !nfeat || !is_final || !tokens || !ntok_out)
         return fail(PFM_E_ARG, "pfm_stream_step: null argument");
     if (n < 1 || Tn < 0 || L_cap < 0) return fail(PFM_E_ARG, "pfm_stream_step: bad sizes");
+    CHECK_DEV("pfm_stream_step", s->h->device, {"feats", feats}, {"tokens", tokens}, {"ntok", ntok_out},
+              {"enc_out", enc_out}, {"alphas", alphas_out});
     return stream_step(s, stream, n, slot_ids, feats, Tn, nfeat, is_final, tokens, L_cap, ntok_out, enc_out,
                        alphas_out, nullptr);
 }
@@ -3030,6 +3099,8 @@ int pfm_stream_step_beam(pfm_streams* s, void* stream, int n, const int32_t* slo
     if (beam < 1 || beam > 16 || nbest < 1 || nbest > 16 || P > 64 || !(ctc_weight > 1e-5f))
         return fail(PFM_E_ARG,
                     "pfm_stream_step_beam: need 1 <= beam <= 16, 1 <= nbest <= 16, ctc_weight > 1e-5, <= 64 candidates");
+    CHECK_DEV("pfm_stream_step_beam", s->h->device, {"feats", feats}, {"tokens", tokens}, {"ntok", ntok_out},
+              {"scores", scores_out}, {"nfire", nfire});
     StreamBeam sb;
     sb.beam = beam; sb.P = P; sb.nbest = nbest; sb.end_detect = end_detect; sb.sos = sos; sb.eos = eos;
     sb.blank = blank; sb.ctc_weight = ctc_weight; sb.penalty = penalty; sb.ntok_hyp = ntok_out;
@@ -3159,6 +3230,7 @@ int pfm_vad_run(pfm_vad* v, void* stream, const float* feats, int T, float* p_si
     if (v->missing) return fail(PFM_E_STATE, "pfm_vad_run: weights not set");
     if (T == 0) return PFM_OK;
     const pfm_vad_config& c = v->cfg;
+    CHECK_DEV("pfm_vad_run", v->device, {"feats", feats}, {"p_sil", p_sil}, {"probs", probs});
     HIP_TRY(hipSetDevice(v->device));
     hipStream_t st = (hipStream_t)stream;
     if (T > v->capT) {
@@ -3209,6 +3281,7 @@ int pfm_vad_fbank_raw(pfm_vad* v, void* stream, const float* wav, const int32_t*
     if (!v || !wav || !nsamp || !fb) return fail(PFM_E_ARG, "pfm_vad_fbank_raw: null argument");
     if (B < 1 || S_max < 1 || N_cap < 1) return fail(PFM_E_ARG, "pfm_vad_fbank_raw: bad sizes");
     if (pfm_fbank_nframes(S_max) > N_cap) return fail(PFM_E_ARG, "pfm_vad_fbank_raw: N_cap smaller than frames of S_max");
+    CHECK_DEV("pfm_vad_fbank_raw", v->device, {"wav", wav}, {"nsamp", nsamp}, {"fb", fb});
     HIP_TRY(hipSetDevice(v->device));
     if (!v->fb_ready) {
         int rc = fbank_tables_build(v->fb_tab);

@@ -138,7 +138,7 @@ def bf16_wire_round(flat, layout, xw: int = None):
 
 
 def broadcast_state_dict(layout, sd: Optional[Dict[str, np.ndarray]], device=None, src: int = 0,
-                         keep_on_device: bool = False, wire: str = "f32"):
+                         keep_on_device: bool = False, wire: str = "f32", with_xw: bool = False):
     """Broadcast a state_dict from `src` in one (f32) or two (bf16 wire) flat collectives; returns it on every rank.
 
     layout: [(key, shape, ...)] in a fixed order known to all ranks (weights.param_layout).
@@ -150,7 +150,12 @@ def broadcast_state_dict(layout, sd: Optional[Dict[str, np.ndarray]], device=Non
     (486 MB at PFM_FAST_XW=0, 520 MB at the default 7). The
     receiving ranks' matrices are then bf16-rounded, which fast mode does not see (bf16(bf16(w)) = bf16(w): its
     decode is bit-identical, tests/test_gpu_automodel.py) but EXACT mode would: load them with
-    PfmEngine.load_flat_device(..., fast_only=True).
+    PfmEngine.load_flat_device(..., fast_only=True, wire_xw=xw).
+    The bf16 / f32 split depends on PFM_FAST_XW (its split-plane rows travel as f32), so under wire="bf16" the bits
+    of `src` are broadcast first and every rank splits by them, whatever its own environment says (ranks that
+    disagreed would otherwise post collectives of different sizes). with_xw=True returns (state, xw): pass xw to
+    load_flat_device, which then refuses fast runs under any other PFM_FAST_XW (their split planes would be built
+    from bf16-rounded weights with zero lo planes).
     """
     import torch
     import torch.distributed as dist
@@ -168,10 +173,14 @@ def broadcast_state_dict(layout, sd: Optional[Dict[str, np.ndarray]], device=Non
             host[off:off + n] = np.asarray(sd[k], dtype=np.float32).reshape(-1)
             off += n
         flat.copy_(torch.from_numpy(host))
+    xw = fast_xw_bits()
     if wire == "f32":
         dist.broadcast(flat, src)
     else:
-        mi, vi = _wire_index(layout, dev)
+        xwt = torch.tensor([xw], dtype=torch.int64, device=dev)
+        dist.broadcast(xwt, src)
+        xw = int(xwt.item())
+        mi, vi = _wire_index(layout, dev, xw)
         mb = flat[mi].to(torch.bfloat16) if rank == src else torch.empty(mi.numel(), dtype=torch.bfloat16, device=dev)
         vf = flat[vi] if rank == src else torch.empty(vi.numel(), dtype=torch.float32, device=dev)
         dist.broadcast(mb, src)
@@ -179,13 +188,13 @@ def broadcast_state_dict(layout, sd: Optional[Dict[str, np.ndarray]], device=Non
         flat[mi] = mb.to(torch.float32)   # every rank, src included: all hold the same bf16-rounded matrices
         flat[vi] = vf
     if keep_on_device:
-        return flat
+        return (flat, xw) if with_xw else flat
     host = flat.cpu().numpy() if dev.type != "cpu" else flat.numpy()
     out, off = {}, 0
     for (k, s, *_), n in zip(layout, sizes):
         out[k] = host[off:off + n].reshape(s)
         off += n
-    return out
+    return (out, xw) if with_xw else out
 
 
 def agree_item_count(n_items: int) -> int:

@@ -196,6 +196,7 @@ class PfmEngine:
         self.cfg = cfg
         self.device = int(device)
         self.fast_only = False   # set by load_flat_device(fast_only=True): bf16-rounded matrices, no EXACT mode
+        self.wire_xw = None      # the PFM_FAST_XW the bf16 wire split was made for (fast runs need the same bits)
         self.lib = load_library()
         c = PfmConfig.from_config(cfg)
         h = ctypes.c_void_p()
@@ -225,14 +226,20 @@ class PfmEngine:
         if strict and miss:
             raise PfmError(f"{miss} required weights missing after load_state_dict")
 
-    def load_flat_device(self, flat, layout, strict: bool = True, fast_only: bool = False) -> None:
+    def load_flat_device(self, flat, layout, strict: bool = True, fast_only: bool = False,
+                         wire_xw: Optional[int] = None) -> None:
         """Weights from ONE flat f32 device tensor on this engine's GPU, packed in `layout` order
         ([(key, shape, ...)], weights.param_layout) — e.g. the buffer a data-parallel rank received by
         RCCL broadcast (distributed.broadcast_state_dict(keep_on_device=True)). pfm_set_weight_device per
         key: device-to-device copies, nothing round-trips through the host. fast_only: the matrices were sent as
-        bf16 (broadcast_state_dict(wire="bf16")), so EXACT mode is refused on this engine."""
+        bf16 (broadcast_state_dict(wire="bf16")), so EXACT mode is refused on this engine. wire_xw: the PFM_FAST_XW
+        bits that wire split was made for (broadcast_state_dict(with_xw=True)); fast runs under other bits are refused,
+        since the library would build split planes from weights that reached this rank bf16-rounded."""
         torch = self.torch
         self.fast_only = bool(fast_only)
+        if fast_only:
+            from .distributed import fast_xw_bits
+            self.wire_xw = fast_xw_bits() if wire_xw is None else int(wire_xw)
         if flat.device.type != "cuda" or flat.device.index != self.device or flat.dtype != torch.float32:
             raise PfmError(f"load_flat_device: need an f32 tensor on cuda:{self.device}, got {flat.dtype} on {flat.device}")
         flat = flat.contiguous()
@@ -274,6 +281,12 @@ class PfmEngine:
         if m == MODE_EXACT and self.fast_only:
             raise PfmError("EXACT mode needs the f32 weights; this engine holds bf16-rounded matrices "
                            "(broadcast_state_dict(wire='bf16') -> load_flat_device(fast_only=True))")
+        if self.fast_only and self.wire_xw is not None:
+            from .distributed import fast_xw_bits
+            if fast_xw_bits() != self.wire_xw:   # the library re-reads PFM_FAST_XW on every call
+                raise PfmError(f"PFM_FAST_XW is {fast_xw_bits()} but this engine's weights came over the bf16 wire "
+                               f"split for {self.wire_xw}: its split-plane rows would be built from bf16-rounded "
+                               "weights (set PFM_FAST_XW back or reload the weights in f32)")
         return m
 
     # ---- inference

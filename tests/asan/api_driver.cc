@@ -122,8 +122,8 @@ static void validation() {
 }
 
 // ---- the single-op entry points: null operands and bad sizes are refused with PFM_E_ARG before any launch (a
-// launch failure would be PFM_E_HIP). Host pointers stand in for device operands, so this runs without a device
-// only: on a GPU an op that launched instead of refusing would hand the kernel host addresses.
+// launch failure would be PFM_E_HIP). Host pointers stand in for device operands; every entry point also refuses a
+// host address before launching (check_dev in pfm_api.hip), so this runs on the GPU too.
 static void op_validation() {
     float f4[4];
     int32_t i1 = 1, tok[4];
@@ -253,6 +253,70 @@ static pfm_handle* create_and_load(const Model& m, const char* tag) {
     return h;
 }
 
+// ---- host memory where the ABI wants device memory: every entry point returns PFM_E_ARG naming the operand and
+// launches nothing (before round 6 such a call faulted the GPU). One host operand per call, the rest valid device
+// buffers; afterwards the handle still decodes (the refused lookups leave no sticky HIP error behind).
+static void expect_host_refused(int rc, const char* what, const char* operand) {
+    expect_rc(rc, PFM_E_ARG, what);
+    expect(strstr(pfm_last_error(), operand) != nullptr, "refusal names the operand", pfm_last_error());
+}
+static void host_pointer_refusals(pfm_handle* h, const Model& m, float* dfe, int32_t* dln, int32_t* dtok,
+                                  int32_t* dnt, int B, int T, int L_cap) {
+    const int D = m.cfg.input_size, dm = m.cfg.d_model;
+    std::vector<float> hfe((size_t)B * T * D, 0.f);
+    std::vector<int32_t> hln(B, T), htok((size_t)B * L_cap), hnt(B);
+    expect_host_refused(pfm_run(h, nullptr, PFM_MODE_FAST, hfe.data(), dln, B, T, dtok, L_cap, dnt, nullptr, nullptr,
+                                nullptr), "run host feats", "feats");
+    expect_host_refused(pfm_run(h, nullptr, PFM_MODE_FAST, dfe, hln.data(), B, T, dtok, L_cap, dnt, nullptr, nullptr,
+                                nullptr), "run host lens", "lens");
+    expect_host_refused(pfm_run(h, nullptr, PFM_MODE_FAST, dfe, dln, B, T, htok.data(), L_cap, dnt, nullptr, nullptr,
+                                nullptr), "run host tokens", "tokens");
+    expect_host_refused(pfm_run(h, nullptr, PFM_MODE_EXACT, dfe, dln, B, T, dtok, L_cap, hnt.data(), nullptr, nullptr,
+                                nullptr), "run host ntok", "ntok");
+    std::vector<float> henc((size_t)B * T * dm);
+    expect_host_refused(pfm_run(h, nullptr, PFM_MODE_FAST, dfe, dln, B, T, dtok, L_cap, dnt, henc.data(), nullptr,
+                                nullptr), "run host enc_out", "enc_out");
+    // pinned host memory is host memory too (the kernels would read it over PCIe; the ABI takes device buffers)
+    float* pinned = nullptr;
+    HCK(hipHostMalloc((void**)&pinned, hfe.size() * sizeof(float), 0));
+    expect_host_refused(pfm_run(h, nullptr, PFM_MODE_FAST, pinned, dln, B, T, dtok, L_cap, dnt, nullptr, nullptr,
+                                nullptr), "run pinned feats", "feats");
+    HCK(hipHostFree(pinned));
+    if (m.cfg.ctc_head) {
+        std::vector<float> hsc((size_t)B * 2);
+        expect_host_refused(pfm_run_beam(h, nullptr, PFM_MODE_FAST, dfe, dln, B, T, 4, 0.3f, 0.f, 2, 0, 1, 2, 0, dtok,
+                                         L_cap, dnt, hsc.data(), nullptr, nullptr), "run_beam host scores", "scores");
+    }
+    // single ops: device buffers big enough for the shapes below, one operand on the host
+    const int M = 64, N = 64, K = 64, hd = 4 * 128, Bq = 1, Tq = 8;
+    std::vector<float> zf((size_t)std::max(M * K, Bq * Tq * hd), 0.f);
+    std::vector<int32_t> zi(64, 1);
+    float* da = dev_upload(zf);
+    float* dw = dev_upload(zf);
+    float* dc = dev_upload(zf);
+    int32_t* di = dev_upload(zi);
+    expect_host_refused(pfm_op_gemm(nullptr, PFM_F32, zf.data(), dw, nullptr, nullptr, dc, M, N, K, 0), "op_gemm host A", "'A'");
+    expect_host_refused(pfm_op_gemm(nullptr, PFM_F32, da, dw, nullptr, nullptr, zf.data(), M, N, K, 0), "op_gemm host C", "'C'");
+    expect_host_refused(pfm_op_attention(nullptr, PFM_F32, zf.data(), da, da, di, dc, Bq, Tq, Tq, 4, 1.f),
+                        "op_attention host q", "'q'");
+    expect_host_refused(pfm_op_attention(nullptr, PFM_F32, da, da, da, zi.data(), dc, Bq, Tq, Tq, 4, 1.f),
+                        "op_attention host klen", "klen");
+    expect_host_refused(pfm_op_layernorm(nullptr, da, dw, dw, zf.data(), 8, 64, 1e-5f), "op_layernorm host out", "out");
+    expect_host_refused(pfm_op_fsmn(nullptr, zf.data(), di, dw, nullptr, dc, 1, 8, 64, 3, 1), "op_fsmn host v", "'v'");
+    expect_host_refused(pfm_op_cif(nullptr, da, zf.data(), dc, dc, di, di, 1, 8, 4, 4), "op_cif host hidden", "hidden");
+    expect_host_refused(pfm_op_ctc_collapse(nullptr, zi.data(), 8, di, 1, 0, di, 4, di), "op_ctc_collapse host ids", "ids");
+    expect_host_refused(pfm_op_ctc_beam(nullptr, zf.data(), 2, da, 4, di, di, 1, 8, 2, 0.3f, 0.f, 1, 0, 1, 2, 0, di, 4,
+                                        di, dc), "op_ctc_beam host am", "'am'");
+    std::vector<int32_t> hns(1, 400);
+    expect_host_refused(pfm_fbank(h, nullptr, da, hns.data(), 1, 400, nullptr, dc, 8, di), "fbank host nsamp", "nsamp");
+    expect_host_refused(pfm_fbank(h, nullptr, zf.data(), di, 1, 400, nullptr, dc, 8, di), "fbank host wav", "wav");
+    HCK(hipFree(da)); HCK(hipFree(dw)); HCK(hipFree(dc)); HCK(hipFree(di));
+    // the handle still runs after the refusals
+    expect_rc(pfm_run(h, nullptr, PFM_MODE_FAST, dfe, dln, B, T, dtok, L_cap, dnt, nullptr, nullptr, nullptr), PFM_OK,
+              "run after host-pointer refusals");
+    HCK(hipDeviceSynchronize());
+}
+
 static void offline(const Model& m) {
     pfm_handle* h = create_and_load(m, "create offline model");
     if (!h) return;
@@ -331,6 +395,7 @@ static void offline(const Model& m) {
         expect(sane, "run_beam counts");
         HCK(hipFree(dsc));
     }
+    host_pointer_refusals(h, m, dfe, dln, dtok, dnt, B, T, L_cap);
     expect_rc(pfm_profile(h, 1), PFM_OK, "profile on");
     expect_rc(pfm_run(h, nullptr, PFM_MODE_FAST, dfe, dln, B, T, dtok, L_cap, dnt, nullptr, nullptr, nullptr), PFM_OK,
               "run profiled");
@@ -372,6 +437,12 @@ static void streaming(const Model& m) {
                   "stream_step");
         HCK(hipFree(df));
     }
+    {
+        const int32_t nfeat[2] = {Tn, Tn};
+        const int32_t fin[2] = {0, 0};
+        expect_host_refused(pfm_stream_step(s, nullptr, n, slots, f.data(), Tn, nfeat, fin, dtok, L_cap, dnt, nullptr,
+                                            nullptr), "stream_step host feats", "feats");
+    }
     const int32_t dup[2] = {1, 1};
     expect_rc(pfm_streams_reset(s, nullptr, slots, 2), PFM_OK, "streams_reset");
     const int32_t three[3] = {0, 1, 5};
@@ -400,7 +471,7 @@ int main(int argc, char** argv) {
     }
     validation();
     vad_validation();
-    if (strcmp(argv[1], "gpu")) op_validation();
+    op_validation();
     if (!strcmp(argv[1], "gpu")) {
         if (argc < 3) return 2;
         Model m, ms;

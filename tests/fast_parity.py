@@ -11,7 +11,11 @@ produces flips at wider margins, to lower-ranked ids, and a mean regret many tim
 
 Paraformer positions come from the CIF: where the fast path's token count differs from the reference's, the
 positions after the point where the fire patterns diverge are not comparable. Such utterances are compared up to
-their first "break" (a chosen id outside the reference's top-k or a regret >= the margin bound), which is reported.
+their first "break" (a chosen id outside the reference's top-k or a regret >= the margin bound). The break and the
+positions behind it are not dropped silently: `trunc_positions` / `trunc_frac` count them, `break_max_regret` is
+the largest regret AT a break (the first decision where a count-mismatched utterance left the reference; a lower
+bound when the id is outside the top-k) and `max_regret_all` the largest regret over every position of the run,
+breaks and misaligned tails included; each has its own bound from the emulation (bounds_from_emulation).
 """
 from __future__ import annotations
 
@@ -34,17 +38,24 @@ def paraformer_stats(tokens: np.ndarray, ntok: np.ndarray, g, margin: float) -> 
     k = g["top_ids"].shape[1]
     reg_all, rank_all = [], []
     equal_counts, prefix_frac = 0, []
+    trunc, break_reg, all_max, total = 0, [], 0.0, 0
     for b in range(len(g["ntok"])):
         n_ref, n_got = int(g["ntok"][b]), int(ntok[b])
         n = min(n_ref, n_got)
         ids, lp = g["top_ids"][off[b]:off[b] + n], g["top_logp"][off[b]:off[b] + n]
         r, rk = regrets(tokens[b, :n].astype(np.int64), ids, lp)
+        total += n
+        if n:
+            all_max = max(all_max, float(r.max()))
         if n_ref == n_got:
             equal_counts += 1
         else:   # count-mismatched: comparable up to the first break of the position alignment
             brk = np.nonzero((rk >= k) | (r >= margin))[0]
             cut = int(brk[0]) if len(brk) else n
             prefix_frac.append(cut / max(1, n_ref))
+            trunc += n - cut
+            if len(brk):
+                break_reg.append(float(r[cut]))
             r, rk = r[:cut], rk[:cut]
         reg_all.append(r)
         rank_all.append(rk)
@@ -52,7 +63,11 @@ def paraformer_stats(tokens: np.ndarray, ntok: np.ndarray, g, margin: float) -> 
     return _summary(reg, rank, k) | dict(equal_counts=equal_counts / len(g["ntok"]),
                                          max_count_diff=int(np.abs(ntok - g["ntok"]).max()),
                                          mismatched=len(prefix_frac),
-                                         mismatched_prefix=float(np.mean(prefix_frac)) if prefix_frac else 1.0)
+                                         mismatched_prefix=float(np.mean(prefix_frac)) if prefix_frac else 1.0,
+                                         trunc_positions=int(trunc), trunc_frac=trunc / max(1, total),
+                                         breaks=len(break_reg),
+                                         break_max_regret=max(break_reg) if break_reg else 0.0,
+                                         max_regret_all=all_max)
 
 
 def frame_stats(frame_ids: np.ndarray, olens: np.ndarray, g) -> dict:
@@ -81,9 +96,13 @@ def bounds_from_emulation(em: dict) -> dict:
     choices outside the reference top 5 within 2x (at least 0.2 % of the positions), the largest regret within
     0.15 nat, equal token counts within 5 points."""
     pos = max(1, em["positions"])
-    return dict(flip_frac=em["flip_frac"] + 0.03, mean_regret=1.5 * em["mean_regret"] + 0.001,
-                outside_frac=max(2.0 * em["outside_topk"] / pos, 0.002), max_regret=em["max_regret"] + 0.15,
-                equal_counts=em["equal_counts"] - 0.05)
+    b = dict(flip_frac=em["flip_frac"] + 0.03, mean_regret=1.5 * em["mean_regret"] + 0.001,
+             outside_frac=max(2.0 * em["outside_topk"] / pos, 0.002), max_regret=em["max_regret"] + 0.15,
+             equal_counts=em["equal_counts"] - 0.05)
+    if "trunc_frac" in em:   # the positions count-mismatched utterances lose at their breaks, bounded too
+        b.update(trunc_frac=2.0 * em["trunc_frac"] + 0.01, break_max_regret=em["break_max_regret"] + 0.5,
+                 max_regret_all=em["max_regret_all"] + 0.5)
+    return b
 
 
 def stream_stats(chunks, g, margin: float) -> dict:

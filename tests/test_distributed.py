@@ -266,3 +266,110 @@ def test_gloo_world2_token_matrix_tensor_gather():
         assert res == want
         assert n_obj_gathers == 0
         assert err is not None and "different input counts" in err
+
+
+class _WriterModel(_EchoModel):
+    """Writes output_dir files like Paraformer.inference (model_writer: {n}best_recog/{token,text})."""
+
+    def inference(self, data_in, key=None, **kw):
+        from funasr_amd.writer import model_writer
+        w = model_writer(self, kw)
+        res = []
+        for k, x in zip(key, data_in):
+            if w is not None:
+                w["1best_recog"]["token"][k] = " ".join(["t"] * (len(x) % 5 + 1))
+                w["1best_recog"]["text"][k] = f"len{len(x)}"
+            res.append({"key": k, "n": int(len(x))})
+        return res, {}
+
+
+def _writer_worker(rank, world, port, items, out_dir, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from funasr_amd.auto_model import AutoModel
+        am = AutoModel.__new__(AutoModel)
+        am.kwargs, am.model = {"batch_size": 2}, _WriterModel()
+        res = am.inference(items, key=None, output_dir=out_dir)
+        # dp=False: a call on one rank alone enters no collective (it would hang here otherwise)
+        solo = am.inference(items[:3], key=None, dp=False) if rank == 0 else None
+        q.put((rank, res, solo))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world2_output_dir_merged_in_input_order(tmp_path):
+    """generate(..., output_dir) under world 2: each rank writes its share into a directory of its own and rank 0
+    merges them into output_dir/1best_recog/{token,text} in input order -- the files a one-process run writes,
+    nothing truncated or overwritten; the rank directories are gone afterwards. dp=False calls are rank-local."""
+    from funasr_amd.auto_model import AutoModel
+    lens = [500, 83, 17, 431, 500, 120, 300, 222, 260]
+    items = [np.zeros(n, np.float32) for n in lens]
+    d1, d2 = tmp_path / "one", tmp_path / "two"
+    single = AutoModel.__new__(AutoModel)
+    single.kwargs, single.model = {"batch_size": 2}, _WriterModel()
+    want_res = single.inference(items, key=None, output_dir=str(d1))
+    single.model.writer.close()
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_writer_worker, args=(r, world, port, items, str(d2), q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    keys = None
+    for rank, res, solo in out:
+        assert [r["n"] for r in res] == lens
+        keys = [r["key"] for r in res] if keys is None else keys
+        assert [r["key"] for r in res] == keys   # one key list on every rank (rank 0's)
+        if rank == 0:
+            assert [r["n"] for r in solo] == lens[:3]
+    assert sorted(os.listdir(d2)) == ["1best_recog"]
+    for name in ("token", "text"):
+        got = (d2 / "1best_recog" / name).read_text(encoding="utf-8").splitlines()
+        ref = (d1 / "1best_recog" / name).read_text(encoding="utf-8").splitlines()
+        assert [g.split(" ", 1)[0] for g in got] == keys
+        assert [g.split(" ", 1)[1] for g in got] == [r.split(" ", 1)[1] for r in ref]
+    assert [r["n"] for r in want_res] == lens
+
+
+def _xw_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    os.environ["PFM_FAST_XW"] = "7" if rank == 0 else "0"   # the ranks disagree: src's bits must win
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        layout = [("encoder.encoders.3.self_attn.linear_q_k_v.weight", (6, 4), 4), ("b.bias", (5,), 4)]
+        sd = None
+        if rank == 0:
+            rng = np.random.default_rng(1)
+            sd = {k: rng.standard_normal(s).astype(np.float32) for k, s, _ in layout}
+        got, xw = broadcast_state_dict(layout, sd, wire="bf16", with_xw=True)
+        q.put((rank, xw, {k: v.tolist() for k, v in got.items()}))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world2_bf16_wire_uses_src_xw_bits():
+    """broadcast_state_dict(wire="bf16") splits by the source rank's PFM_FAST_XW even where another rank's
+    environment says otherwise (the two would post collectives of different sizes): with bit 4 the q|k rows of an
+    encoder QKV arrive bf16-rounded and the v rows exact on every rank, and both report xw = 7."""
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_xw_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    rng = np.random.default_rng(1)
+    w = rng.standard_normal((6, 4)).astype(np.float32)
+    want = torch.tensor(w)
+    want[:4] = want[:4].to(torch.bfloat16).float()
+    for rank, xw, got in out:
+        assert xw == 7
+        assert got["encoder.encoders.3.self_attn.linear_q_k_v.weight"] == want.tolist()

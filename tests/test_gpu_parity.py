@@ -232,6 +232,13 @@ def fast_violations(st, bounds=FAST_BOUNDS):
         bad.append(f"equal token counts {st['equal_counts']:.3f} < {bounds['equal_counts']}")
     if st.get("max_count_diff", 0) > 1:
         bad.append(f"token count off by {st['max_count_diff']}")
+    # the positions count-mismatched utterances lose at their alignment break (not dropped silently: bounded too)
+    if "trunc_frac" in bounds and st["trunc_frac"] >= bounds["trunc_frac"]:
+        bad.append(f"truncated positions {st['trunc_frac']:.4f} >= {bounds['trunc_frac']:.4f}")
+    if "break_max_regret" in bounds and st["break_max_regret"] >= bounds["break_max_regret"]:
+        bad.append(f"regret at a break {st['break_max_regret']:.3f} >= {bounds['break_max_regret']:.3f}")
+    if "max_regret_all" in bounds and st["max_regret_all"] >= bounds["max_regret_all"]:
+        bad.append(f"max regret over all positions {st['max_regret_all']:.3f} >= {bounds['max_regret_all']:.3f}")
     return bad
 
 
@@ -400,3 +407,34 @@ def test_exact_first_run_after_reload(monkeypatch, sub):
     r = _run(e, g, "exact")
     torch.cuda.synchronize()
     assert _tokens_from_run(r, e.cfg) == _golden_tokens(g)
+
+
+def test_fast_split_planes_follow_weight_reload():
+    """PFM_FAST_XW keeps some weights as two bf16 planes (the predictor conv, encoder layer 0, the v rows of every
+    QKV). A weight uploaded after a fast run must rebuild those planes: an engine that ran fast, then took new
+    values for one weight of each kind, decodes exactly like a fresh engine loaded with the new values (and not
+    like its old self)."""
+    cfg = paraformer_large()
+    w = make_weights(cfg, seed=0)
+    rng = np.random.default_rng(7)
+    keys = ["predictor.cif_conv1d.weight", "encoder.encoders0.0.feed_forward.w_1.weight",
+            "encoder.encoders.5.self_attn.linear_q_k_v.weight"]
+    w2 = dict(w)
+    for k in keys:
+        w2[k] = (w[k] + 0.5 * w[k].std() * rng.standard_normal(w[k].shape)).astype(np.float32)
+    g = np.load(f"{GOLD}/para_large_ragged.npz")
+    e = PfmEngine(cfg, 0)
+    e.load_state_dict(w)
+    r0 = _run(e, g, "fast")
+    torch.cuda.synchronize()
+    for k in keys:
+        e.set_weight(k, w2[k])
+    r1 = _run(e, g, "fast")
+    f = PfmEngine(cfg, 0)
+    f.load_state_dict(w2)
+    rf = _run(f, g, "fast")
+    torch.cuda.synchronize()
+    assert torch.equal(r1["enc"], rf["enc"])
+    assert torch.equal(r1["alphas"], rf["alphas"])
+    assert torch.equal(r1["tokens"], rf["tokens"])
+    assert not torch.equal(r0["enc"], r1["enc"])

@@ -270,7 +270,7 @@ def main():
     feats, lens = fbank_input(seed=int(g["seed"]), B=int(g["B"]), T=int(g["T"]), lens=g["lens"])
     x, ln = torch.from_numpy(feats), torch.from_numpy(lens.astype(np.int64))
     out_json = os.environ.get("EMUL_JSON")
-    res = {}
+    res, toks = {}, {}
     for knobs in variants:
         for kk in knobs:
             assert kk in ALL or kk.startswith("XW:"), kk
@@ -278,6 +278,8 @@ def main():
         enc, ntok, ids = Emu(w, cfg, knobs).run(x, ln)
         s = score(gpath, ntok, ids, enc)
         res["+".join(knobs) or "f32"] = s
+        toks[("+".join(knobs) or "f32") + "/ids"] = ids.numpy().astype(np.int16)
+        toks[("+".join(knobs) or "f32") + "/ntok"] = ntok.numpy().astype(np.int16)
         print(f"{'+'.join(knobs) or 'f32':22s} flips {s['flip_frac_equal_counts']:.4f} "
               f"mean_regret {s['mean_regret']:.4f} max_regret {s['max_regret']:.3f} "
               f"outside_top5 {s['outside_topk']} equal_counts {s['equal_counts']:.3f} "
@@ -288,6 +290,10 @@ def main():
         allr.setdefault(f"para_large_{name}", {}).update(res)
         with open(out_json, "w") as f:
             json.dump(allr, f, indent=1)
+        # the emulated decisions themselves, so later statistics can be recomputed without re-running the emulation
+        tpath = os.path.join(os.path.dirname(out_json), f"fast_emul_tokens_{name}.npz")
+        old = dict(np.load(tpath)) if os.path.exists(tpath) else {}
+        np.savez_compressed(tpath, **(old | toks))
 
 
 if __name__ == "__main__":
