@@ -998,6 +998,8 @@ hipError_t launch_persist(const void* A, RowMap amap, const void* W, long long l
     return hipSuccess;
 }
 
+int f_gemm_cfg_forced() { const int f = pfm_knobs().gemm_cfg; return f >= 1 && f <= 17 ? f : 0; }
+
 int pick_cfg(int M, int N, int K, bool amax) {
     const int f = pfm_knobs().gemm_cfg;   // PFM_GEMM_CFG (per call): lets one process A/B configurations
     if (f >= 1 && f <= 17) return f;
@@ -1047,10 +1049,18 @@ hipError_t pfm_gemm_bf16_256(const void* A, RowMap amap, const void* W, long lon
         e2.res_batch = 0;
     }
     int cfg = pick_cfg(M, N, K, epi.amax_val != nullptr);
-    // (EXACT mode x6 GEMMs keep the fast-mode tiles: C17 for N >= 1024 and C16 for 512-wide x6 GEMMs were
-    // faster in isolation — tools/gemm_cfg_scan.py SCAN_X6=1 — but slower on the two-group path, 99.3 and
-    // 104.8 vs 98.0 ms/step; unsplit, C17 for the wide ones 100.9 vs 101.3, both 111.6)
-    if (epi.x6_k && cfg != 1 && cfg != 3 && cfg != 4 && cfg != 13 && cfg != 15 && cfg != 16 && cfg != 17) cfg = 15;
+    // EXACT mode's x6 GEMMs (x6_terms 6) stay on ONE MFMA shape whatever the grid: every output element is then
+    // the same chain of v_mfma_f32_16x16x32_bf16 over k = 0, 32, 64, ... (C15 / C16 / C17 differ in tile size and
+    // schedule, not in any element's accumulation order), so a row's result does not depend on how many rows
+    // share the launch — a batch of 1 and a batch of 64 (or one data-parallel shard) decode an utterance
+    // identically. The grid only picks the tile: >= 256 256-tiles C15, the 8-phase C17 for N <= 512 / K >= 1024,
+    // else the 128 x 256 C16 (the 32x32x16 C3 / C4 it replaces rounded differently).
+    if (epi.x6_k && epi.x6_terms != 2 && epi.x6_terms != 3 && f_gemm_cfg_forced() == 0) {
+        const long long big = (long long)((M + 255) / 256) * ((N + 255) / 256);
+        cfg = (N <= 512 && K % 128 == 0 && K >= 1024 && big >= 120) ? 17 : big >= 256 ? 15 : 16;
+    } else if (epi.x6_k && cfg != 1 && cfg != 3 && cfg != 4 && cfg != 13 && cfg != 15 && cfg != 16 && cfg != 17) {
+        cfg = 15;
+    }
     if (epi.x6_k && (K != (epi.x6_terms == 3 ? 3 : epi.x6_terms == 2 ? 2 : 6) * epi.x6_k || epi.x6_k % 64))
         return hipErrorInvalidValue;
     switch (cfg) {

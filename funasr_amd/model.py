@@ -159,12 +159,12 @@ class Paraformer(HipModel):
     def _greedy_hyps(self, toks, ntok):
         """[B, L_cap] per-position argmax ids + counts -> per utterance a one-entry n-best list of token ids with
         blank / sos / eos dropped (model.py:541-565)."""
-        hyps = []
-        for i in range(toks.shape[0]):
-            n = int(ntok[i])
-            ids = toks[i, :n].tolist() if n <= toks.shape[1] else []
-            hyps.append([[t for t in ids if t not in (self.eos, self.sos, self.blank_id)]])
-        return hyps
+        toks, ntok = np.asarray(toks), np.asarray(ntok).reshape(-1)
+        n = np.where(ntok <= toks.shape[1], ntok, 0)   # a count past L_cap: the row was not decoded (empty result)
+        keep = np.arange(toks.shape[1])[None, :] < n[:, None]
+        for sp in (self.eos, self.sos, self.blank_id):
+            keep &= toks != sp
+        return [[toks[i][keep[i]].tolist()] for i in range(toks.shape[0])]
 
     def results_from_token_matrix(self, toks, ntok, key, tokenizer=None, **kwargs):
         """Greedy results from a (gathered) host token matrix, exactly as inference() builds them."""
@@ -177,8 +177,9 @@ class Paraformer(HipModel):
                 out.append({"key": key[i], "token_int": ids})
                 continue
             toks_i = tokenizer.ids2tokens(ids)
-            text = tokenizer.tokens2text(toks_i)
-            if not hasattr(tokenizer, "bpemodel"):
+            if hasattr(tokenizer, "bpemodel"):
+                text = tokenizer.tokens2text(toks_i)
+            else:
                 text, _ = sentence_postprocess(toks_i)
             out.append({"key": key[i], "text": text})
         return out
@@ -237,8 +238,9 @@ class Paraformer(HipModel):
                     # model.py:567-586: text = tokens2text(ids2tokens(ids)); sentence_postprocess replaces it
                     # only for tokenizers without a `bpemodel` (a SentencepiecesTokenizer keeps tokens2text)
                     toks_i = tokenizer.ids2tokens(ids)
-                    text = tokenizer.tokens2text(toks_i)
                     bpe = hasattr(tokenizer, "bpemodel")
+                    # (without a bpemodel sentence_postprocess replaces the tokens2text result: not computed then)
+                    text = tokenizer.tokens2text(toks_i) if bpe else None
                     if pred_ts:
                         if bpe:   # model.py:580-582 reads time_stamp_postprocessed, which only the non-bpe branch binds
                             raise UnboundLocalError("pred_timestamp with a bpemodel tokenizer: the reference leaves "

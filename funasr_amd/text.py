@@ -11,9 +11,10 @@ from __future__ import annotations
 
 import json
 import os
+from functools import lru_cache
 from typing import Optional, Iterable, List, Sequence, Union
 
-_SPECIAL = ("<s>", "</s>", "<unk>", "<OOV>")
+_SPECIAL = frozenset(("<s>", "</s>", "<unk>", "<OOV>"))
 
 
 def load_token_list(token_list: Union[str, Sequence[str], None]) -> List[str]:
@@ -46,6 +47,9 @@ class CharTokenizer:
         return [self.token_list[int(i)] for i in ids]
 
     def tokens2text(self, tokens: Iterable[str]) -> str:
+        tokens = tokens if isinstance(tokens, list) else list(tokens)
+        if self.space_symbol not in tokens:
+            return "".join(tokens)
         return "".join(" " if t == self.space_symbol else t for t in tokens)
 
     def text2tokens(self, line: str) -> List[str]:
@@ -108,23 +112,35 @@ def _is_zh(w: str) -> bool:
     return ("一" <= w <= "鿿") or ("0" <= w <= "9") or w == "@"
 
 
+# Per-token properties, memoised: a vocabulary has at most a few ten thousand distinct tokens, and the greedy results of
+# a 64-utterance batch walk ~15k of them through these tests (uncached they cost ~20 ms per batch of host time).
+@lru_cache(maxsize=1 << 16)
+def _zh_word(w: str) -> bool:
+    return _is_zh(_strip_specials(w))
+
+
+@lru_cache(maxsize=1 << 16)
+def _alpha_word(w: str) -> int:
+    """_all_alpha of one stripped word: 1 alphabetic (or "'") and not Chinese, 0 otherwise."""
+    w = _strip_specials(w)
+    if not w.isalpha() and w != "'":
+        return 0
+    return 0 if (w.isalpha() and _is_zh(w)) else 1
+
+
 def _all_zh(words) -> bool:
-    ws = [_strip_specials(w) for w in words]
-    return len(ws) > 0 and all(_is_zh(w) for w in ws)
+    if isinstance(words, str):   # the reference calls isAllChinese on single words too (a str is its characters)
+        return len(words) > 0 and all(_zh_word(c) for c in words)
+    return len(words) > 0 and all(_zh_word(w) for w in words)
 
 
 def _all_alpha(words) -> bool:
-    ws = [_strip_specials(w) for w in words]
-    if not ws:
-        return False
-    for w in ws:
-        if not w.isalpha() and w != "'":
-            return False
-        if w.isalpha() and _is_zh(w):
-            return False
-    return True
+    if isinstance(words, str):
+        return len(words) > 0 and all(_alpha_word(c) for c in words)
+    return len(words) > 0 and all(_alpha_word(w) for w in words)
 
 
+@lru_cache(maxsize=1 << 16)
 def _single_letter(w: str) -> bool:
     return len(w) == 1 and w.encode("utf-8").isalpha()
 
@@ -215,16 +231,14 @@ def sentence_postprocess(words: Sequence[Union[str, bytes]], time_stamp: Optiona
     (sentence, word spans, word list), words then joined by spaces (postprocess_utils.py:144-251).
     Chinese chars joined, BPE '@@' pieces merged, alphabetic words space-separated, single-letter
     runs joined as upper-case abbreviations."""
-    mid = []
-    for w in words:
-        w = w if isinstance(w, str) else w.decode("utf-8")
-        if w not in _SPECIAL:
-            mid.append(w)
+    mid = [w if isinstance(w, str) else w.decode("utf-8") for w in words]
+    mid = [w for w in mid if w not in _SPECIAL]
     ts = time_stamp is not None
     out: List[str] = []
     spans: List[List[int]] = []
-    if _all_zh(mid):
-        out = [w.replace(" ", "") for w in mid]
+    all_zh = _all_zh(mid)
+    if all_zh:
+        out = [w.replace(" ", "") for w in mid] if any(" " in w for w in mid) else mid
         if ts:
             spans = time_stamp
     elif _all_alpha(mid):
@@ -278,6 +292,7 @@ def sentence_postprocess(words: Sequence[Union[str, bytes]], time_stamp: Optiona
         out, spans = _abbreviations_with_spans(out, spans)
         real = [w for w in out if w != " "]
         return " ".join(real).strip(), spans, real
-    out = _join_abbreviations(out)
+    if not all_zh:   # an all-Chinese list holds no single ASCII letter: the abbreviation pass would be the identity
+        out = _join_abbreviations(out)
     real = [w for w in out if w != " "]
     return "".join(out).strip(), real
