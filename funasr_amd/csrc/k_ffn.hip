@@ -796,6 +796,13 @@ hipError_t pfm_ffn_pack_dec(const bf16* W1, const float* W2, const float* gF, co
     return hipSuccess;
 }
 
+// the LN_F fold constants alone (c1 = rowsum(bf16(W2 diag(gamma_F))), c2 = W2 beta_F), for k_ffn2.hip's split decoder pack
+hipError_t pfm_ffn_dec_consts(const float* W2, const float* gF, const float* bF, float* c1, float* c2, hipStream_t st) {
+    hipLaunchKernelGGL(ffn_dec_consts_kernel, dim3(FD), dim3(256), 0, st, W2, gF, bF, c1, c2);
+    PFM_LAUNCH_CHECK();
+    return hipSuccess;
+}
+
 // Fused decoder feed-forward (ffn_fused_kernel DEC): x f32 [M, 512] -> xn = LN_next(W2 LN_F(relu(W1 LN1(x) + b1)))
 // bf16 [M, 512] (+ the f32 FFN output in xo when non-null). Wp / c1 / c2 from pfm_ffn_pack_dec.
 // With o (bf16 [M, 512], the previous block's cross-attention output) and bo: that block's out-projection runs

@@ -7,8 +7,24 @@
 //           PFM_FAST_XW bit 4): the v pass streams 32 more tiles, accumulated into the same registers
 //   MODE 6  MODE 5 with Wo as two bf16 planes too (PFM_FAST_XW bit 8): phase 0 streams 32 more tiles
 //   MODE 3  MODE 1 with Wo as two bf16 planes (the last layer under PFM_FAST_XW bit 8)
+//   MODE 7  decoder FFN (PositionwiseFeedForwardDecoderSANM, sanm/positionwise_feed_forward.py:12-33, in a
+//           DecoderLayerSANM, paraformer/decoder.py:95-101): y = W2 LN_F(relu(W1 LN1(x) + b1)), xn = LN_next(y),
+//           the 2048-wide hidden SPLIT over two workgroups per 128-row tile (below)
+//   MODE 8  MODE 7 with the previous block's cross-attention out-projection in front (decoder.py:113-119):
+//           x1 = x + O Wo^T + bo -> Xo (the residual the FSMN step adds back), the FFN on LN1(x1)
 // with the next LayerNorm of the result as a bf16 output (the consumer GEMM's operand; MODE 4: the QKV rows).
-// (The decoder FFN runs on k_ffn.hip: its 128-row form here measured slower end to end and was removed.)
+//
+// Decoder split (MODE 7 / 8). A decoder group has ~7.4k rows (B x L): 58 row tiles of 128, too few workgroups for
+// the chip when each streams all 4.5 MB of a block's weights. Each tile is owned by TWO workgroups, one per half of
+// the hidden (1024 units: 32 chunks of W1 rows / W2 columns, 2048 stream fragments each): both compute the tile's
+// LN1 (and phase 0), then each its half of y = W2g h (W2g = W2 diag(gamma_F), LN_F folded through W2 as in
+// k_ffn.hip DEC: y = rstd (W2g h - mu c1) + c2) and its half of the LN_F statistics (sum, sum of squares of the bf16
+// hidden, by v_dot2c_f32_bf16 on the packed relu output). Both publish their f32 partial (256 KiB, accumulator
+// order) and statistics, then one agent-scope acq_rel add on the tile's counter: the workgroup that arrives second
+// adds the other's partial (float addition commutes: the result does not depend on the arrival order), applies the
+// fold and LN_next, stores xn and resets the counter; the first one exits. No workgroup waits for another, so the
+// protocol needs no co-residency. The two halves of a tile take block ids b and b + 8 (one XCD: the partner's
+// partial and the shared input rows come from the same L2).
 //
 // Why a second kernel: k_ffn.hip owns 64 rows per workgroup, so every workgroup streams all 4.5 MB of the
 // layer's weights through L2 -> LDS for 64 rows (64 FLOP per weight byte), and its A / H images fill the LDS
@@ -46,6 +62,7 @@ namespace {
 
 typedef __attribute__((address_space(3))) void lds_void;
 typedef float f32x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef const __attribute__((address_space(1))) void gbl_void;
 
 constexpr int FD = 512, FF = 2048, BM = 128, NW = 4, HC = 32, NCH = FF / HC;   // 64 hidden chunks
@@ -178,19 +195,28 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     const float* __restrict__ X, int M, const float* __restrict__ g, const float* __restrict__ be, float eps,
     const bf16* __restrict__ Wp, const float* __restrict__ b1, const float* __restrict__ b2, float* Xo,
     const float* __restrict__ gn, const float* __restrict__ bn, bf16* __restrict__ Xn, const bf16* __restrict__ O,
-    const bf16* __restrict__ Fr, const float* __restrict__ bo, const float* __restrict__ c1) {
+    const bf16* __restrict__ Fr, const float* __restrict__ bo, const float* __restrict__ c1, float* part,
+    unsigned* cnt) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     float* vec = (float*)(smem + RING);
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int r = lane & 31, h = lane >> 5;
-    static_assert(MODE == 0 || MODE == 1 || MODE == 3 || MODE == 4 || MODE == 5 || MODE == 6, "encoder modes");
-    constexpr bool OP = MODE == 1 || MODE == 3 || MODE >= 4, QK = MODE >= 4;   // out-projection; + the next QKV
-    constexpr bool XV = MODE >= 5;                 // + the v rows' second weight plane
+    static_assert(MODE == 0 || MODE == 1 || MODE == 3 || MODE == 4 || MODE == 5 || MODE == 6 || MODE == 7 || MODE == 8,
+                  "encoder / decoder modes");
+    constexpr bool DEC = MODE >= 7;                // decoder FFN, hidden split over two workgroups per tile
+    constexpr bool OP = MODE == 1 || MODE == 3 || (MODE >= 4 && MODE <= 6) || MODE == 8;   // out-projection in front
+    constexpr bool QK = MODE >= 4 && MODE <= 6;    // + the next layer's QKV
+    constexpr bool XV = MODE == 5 || MODE == 6;    // + the v rows' second weight plane
     constexpr bool XO = MODE == 3 || MODE == 6;    // + Wo's second weight plane
-    constexpr int F0 = OP ? (XO ? 2 : 1) * OPF : 0, F3 = F0 + NCH * CHF, NF = F3 + (QK ? QKF + (XV ? OPF : 0) : 0),
+    constexpr int NCHK = DEC ? NCH / 2 : NCH;      // hidden chunks this workgroup streams
+    constexpr int F0 = OP ? (XO ? 2 : 1) * OPF : 0, F3 = F0 + NCHK * CHF, NF = F3 + (QK ? QKF + (XV ? OPF : 0) : 0),
                   NT = NF / TF;
-    const long long rg = (long long)blockIdx.x * BM + 32 * w + r;   // this lane's row
+    // DEC: tile t's halves are blocks 16 (t >> 3) + (t & 7) and that + 8 (the same XCD)
+    const int bid = blockIdx.x;
+    const int tile = DEC ? ((bid >> 4) << 3) | (bid & 7) : bid, half = DEC ? (bid >> 3) & 1 : 0;
+    if (DEC && (long long)tile * BM >= M) return;   // grid padding (both halves of such a tile leave)
+    const long long rg = (long long)tile * BM + 32 * w + r;   // this lane's row
     const bool live = rg < M;
     const long long rc = live ? rg : (long long)M - 1;               // clamped for loads
     unsigned long long tsv[16];                                       // VAR 9: phase timestamps (uniform)
@@ -214,13 +240,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         if (Xn) { vec[V_GN + i] = gn[i]; vec[V_BN + i] = bn[i]; }
         if constexpr (OP) vec[V_BO + i] = bo[i];
     }
-    for (int i = tid; i < FF; i += 256) vec[V_B1 + i] = b1[i];
+    for (int i = tid; i < NCHK * HC; i += 256) vec[V_B1 + i] = b1[NCHK * HC * half + i];   // DEC: this half's biases
     if constexpr (QK)
         for (int i = tid; i < 3 * FD; i += 256) vec[V_BQ + i] = c1[i];
+    if constexpr (DEC)   // LN_F folded through W2: c1 = rowsum(W2g) (c2 = W2 beta_F arrives as b2)
+        for (int i = tid; i < FD; i += 256) vec[V_BQ + i] = c1[i];
     __syncthreads();
 
     // ---- weight ring: tile t -> slot t % RS; this wave moves fragments GW w .. GW w + GW - 1 of each tile
-    const bf16* wsrc = Wp + (long long)GW * w * FE + lane * 8;
+    // DEC: the layer block holds [Wo | half-0 stream][Wo | half-1 stream]; MODE 7 (no out-projection) skips the Wo slot
+    const bf16* wbase = DEC ? Wp + (long long)half * (OPF + NCHK * CHF) * FE + (OP ? 0 : (long long)OPF * FE) : Wp;
+    const bf16* wsrc = wbase + (long long)GW * w * FE + lane * 8;
     // piece p (0..3) of tile t: one 1 KiB LDS-DMA per wave. The four pieces of a wave are 1 KiB apart in both
     // spaces, so they share one address and one M0 and differ only in the instruction's immediate offset.
     static_assert(GW == 4, "LDS-DMA pieces per tile");
@@ -422,7 +452,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
             fence();
             const f32x16 t = acc_get(ob);
             ln_block(ob, t, mean, rstd);
-            acc_c2(ob, t, true);
+            // the decoder FFN output has no residual (and w_2 no bias): its first phase-2 MFMAs start from C = 0
+            // instead (zeroed accumulators here made the allocator spill the stream's operands)
+            if constexpr (!DEC) acc_c2(ob, t, true);
         }
         fence();
     }
@@ -489,16 +521,30 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(wf[0]), "+v"(wf[1]), "+v"(wf[2]), "+v"(wf[3]), "+v"(wf[4]),
                      "+v"(wf[5]), "+v"(wf[6]), "+v"(wf[7]));
         xdl_drain(acc);
-        // x1 = ((Y0 + bo) + F) + x (the separate GEMM epilogue's order; layer 0: no x)
-        add_rows(false, X ? X : bo, X ? FD : 0, X ? 1.f : 0.f, Fr, V_BO);
+        // x1 = ((Y0 + bo) + F) + x (the separate GEMM epilogue's order; layer 0: no x; the decoder: no F)
+        add_rows(false, X ? X : bo, X ? FD : 0, X ? 1.f : 0.f, DEC ? nullptr : Fr, V_BO);
+        if constexpr (DEC) {   // the decoder keeps x1 (its FSMN step adds the FFN's LN_next output back onto it)
+            if (half == 0 && live) {
+#pragma unroll
+                for (int ob = 0; ob < 16; ++ob) {
+                    fence();
+                    const f32x16 t = acc_get(ob);
+#pragma unroll
+                    for (int q = 0; q < 4; ++q)
+                        *(float4*)(Xo + rg * FD + 32 * ob + 8 * q + 4 * h) =
+                            make_float4(t[4 * q], t[4 * q + 1], t[4 * q + 2], t[4 * q + 3]);
+                }
+                fence();
+            }
+        }
         float mean, rstd;
         acc_stats(mean, rstd);
 #pragma unroll
-        for (int ob = 0; ob < 16; ++ob) {   // LN2(x1) -> act; accumulators: x1 + b2
+        for (int ob = 0; ob < 16; ++ob) {   // LN2(x1) -> act; accumulators: x1 + b2 (decoder: LN1(x1), from zero)
             fence();
             const f32x16 t = acc_get(ob);
             ln_block(ob, t, mean, rstd);
-            acc_c2(ob, t, true);
+            if constexpr (!DEC) acc_c2(ob, t, true);   // decoder: phase 2 starts from C = 0 (see the prologue)
         }
         fence();
     }
@@ -521,6 +567,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     // per feature it replaces cost 12 us of a 215 us launch (VAR 10): the stream's MFMA gaps are full (a ds_read, its
     // counted wait and the MFMA's issue), so every VALU instruction added there costs its issue time.
     f32x16 acc1;                // phase 1 of one chunk (H^T = W1 . act + b1)
+    float hs = 0.f, hq = 0.f;   // DEC: sum / sum of squares of this lane's bf16 hidden (LN_F statistics)
     bf16x8 hfa[2], hfb[2];      // phase 2's B operand (hidden k steps 0, 1) of even / odd chunks
     f32x4 bqa[4], bqb[4];       // b1 of even / odd chunks: features 8q + 4h .. +3 (accumulator register groups)
     auto b1_issue = [&](int c, f32x4 (&bq)[4]) __attribute__((always_inline)) {
@@ -544,9 +591,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
             mfma32_v(acc1, wf[fs % NB], act[j]);
         }
     };
-    auto p2 = [&](int f, int fs, int k, const bf16x8 (&hb)[2]) __attribute__((always_inline)) {   // phase 2: output block k & 15, hidden k step k >> 4
+    // phase 2: output block k & 15, hidden k step k >> 4; first: chunk 0's k step 0 of a decoder launch (C = 0)
+    auto p2 = [&](int f, int fs, int k, const bf16x8 (&hb)[2], bool first = false) __attribute__((always_inline)) {
         step_pre(f, fs);
         if (VAR == 2) asm volatile("" :: "v"(wf[fs % NB]), "v"(hb[k >> 4]));
+        else if (DEC && first && k < 16) mfma_a0(acc[k & 15], wf[fs % NB], hb[k >> 4]);
         else mfma_a(acc[k & 15], wf[fs % NB], hb[k >> 4]);
     };
     // phase 1's last MFMAs drained (24 wait states before a VALU reads their results)
@@ -564,6 +613,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
             __builtin_memcpy(&u, &t, 8);
             asm volatile("v_pk_max_i16 %0, %0, 0\n\tv_pk_max_i16 %1, %1, 0" : "+v"(u.x), "+v"(u.y));
             __builtin_memcpy(((char*)&hb[q >> 1]) + 8 * (q & 1), &u, 8);
+            if constexpr (DEC) {   // LN_F statistics of the values phase 2 consumes: two packed pairs per group
+                bf16x2 p0, p1, one;
+                const unsigned uo = 0x3f803f80u;   // (1.0, 1.0)
+                __builtin_memcpy(&p0, &u.x, 4);
+                __builtin_memcpy(&p1, &u.y, 4);
+                __builtin_memcpy(&one, &uo, 4);
+                hs = __builtin_amdgcn_fdot2_f32_bf16(p0, one, hs, false);
+                hs = __builtin_amdgcn_fdot2_f32_bf16(p1, one, hs, false);
+                hq = __builtin_amdgcn_fdot2_f32_bf16(p0, p0, hq, false);
+                hq = __builtin_amdgcn_fdot2_f32_bf16(p1, p1, hq, false);
+            }
         } else {
             asm volatile("" :: "v"(acc1));
         }
@@ -575,15 +635,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     // body c: slots 3m, 3m+1 = P1(c+1) k steps 2m, 2m+1; slot 3m+2 = P2(c) block m, hidden k step 0; slots 48..63 =
     // P2(c) blocks 0..15, hidden k step 1, with relu(c+1) in four groups behind slots 50, 52, 54, 56; b1 of chunk
     // c+2 is read at the body's start (bqn: the buffer chunk c's biases left)
-    auto body = [&](int c, const bf16x8 (&hcur)[2], bf16x8 (&hnext)[2], f32x4 (&bqc)[4], f32x4 (&bqn)[4])
-        __attribute__((always_inline)) {
+    auto body = [&](int c, const bf16x8 (&hcur)[2], bf16x8 (&hnext)[2], f32x4 (&bqc)[4], f32x4 (&bqn)[4],
+                    bool first = false) __attribute__((always_inline)) {
         const int fb = F0 + 32 + CHF * c;
-        if (c + 2 < NCH) b1_issue(c + 2, bqn);
+        if (c + 2 < NCHK) b1_issue(c + 2, bqn);
 #pragma unroll
         for (int m = 0; m < 16; ++m) {
             p1(fb + 3 * m, 3 * m, 2 * m, bqc);
             p1(fb + 3 * m + 1, 3 * m + 1, 2 * m + 1, bqc);
-            p2(fb + 3 * m + 2, 3 * m + 2, m, hcur);
+            p2(fb + 3 * m + 2, 3 * m + 2, m, hcur, first);
         }
 #pragma unroll
         for (int i = 48; i < 64; ++i) {
@@ -602,23 +662,104 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #pragma unroll
         for (int q = 0; q < 4; ++q) relu_q(q, hfa);
         valu_to_mfma();
-        for (int c = 0; c < NCH - 2; c += 2) {
+        int c0 = 0;
+        if constexpr (DEC) {   // chunk 0's phase 2 starts the accumulators (C = 0): its body peeled
+            body(0, hfa, hfb, bqb, bqa, true);
+            body(1, hfb, hfa, bqa, bqb);
+            c0 = 2;
+        }
+        for (int c = c0; c < NCHK - 2; c += 2) {
             body(c, hfa, hfb, bqb, bqa);
             body(c + 1, hfb, hfa, bqa, bqb);
         }
-        body(NCH - 2, hfa, hfb, bqb, bqa);
-        const int ft = F0 + 32 + CHF * (NCH - 1);
+        body(NCHK - 2, hfa, hfb, bqb, bqa);
+        const int ft = F0 + 32 + CHF * (NCHK - 1);
 #pragma unroll
         for (int k = 0; k < 32; ++k) p2(ft + k, k, k, hfb);   // tail: P2(63)
     }
     stamp(4);
-    if constexpr (QK)   // the read-ahead of phase 3's first fragments: retired before the epilogue (see phase 0)
+    if constexpr (QK || DEC)   // the stream's read-ahead (phase 3's first fragments): retired before the epilogue
         asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(wf[0]), "+v"(wf[1]), "+v"(wf[2]), "+v"(wf[3]), "+v"(wf[4]),
                      "+v"(wf[5]), "+v"(wf[6]), "+v"(wf[7]));
     xdl_drain(acc);
 
+    // ---- DEC: publish this half's partial y and LN_F statistics; the second workgroup of the tile to arrive
+    //      combines both halves (see the header), the first one is done
+    if constexpr (DEC) {
+        hs += __shfl_xor(hs, 32, 64);   // lanes r and r + 32 hold the two halves of each 32-feature group
+        hq += __shfl_xor(hq, 32, 64);
+        constexpr long long WPART = 16 * 1024;   // floats of one wave's partial: 16 blocks x 16 registers x 64 lanes
+        float* mine = part + ((long long)(2 * tile + half) * NW + w) * WPART;
+#pragma unroll
+        for (int ob = 0; ob < 16; ++ob) {
+            fence();
+            const f32x16 t = acc_get(ob);
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                *(float4*)(mine + ob * 1024 + q * 256 + lane * 4) = make_float4(t[4 * q], t[4 * q + 1], t[4 * q + 2],
+                                                                                  t[4 * q + 3]);
+        }
+        fence();
+        float2* stats = (float2*)(part + (long long)2 * gridDim.x / 2 * NW * WPART);   // behind every tile's partials
+        if (h == 0) stats[(long long)(2 * tile + half) * BM + 32 * w + r] = make_float2(hs, hq);
+        vm_wait<0>();      // every store of this wave completed (visible at the device's coherence point)
+        __syncthreads();   // ... of every wave
+        unsigned* arrived = (unsigned*)smem;   // the ring is idle: no DMA in flight after the stream
+        if (tid == 0)   // release this workgroup's partial; acquire the partner's when it came first
+            arrived[0] = __hip_atomic_fetch_add(cnt + tile, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();
+        if (*(volatile unsigned*)arrived == 0) return;   // first: the partner combines the tile
+        if (tid == 0) __hip_atomic_store(cnt + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // next launch
+        const float* other = part + ((long long)(2 * tile + (half ^ 1)) * NW + w) * WPART;
+#pragma unroll
+        for (int bt = 0; bt < 4; ++bt) {   // the partner's partial in four batches of 4 blocks (16 float4 in flight)
+            fence();
+            float4 ov[16];
+#pragma unroll
+            for (int k = 0; k < 16; ++k)
+                ov[k] = *(const float4*)(other + (4 * bt + k / 4) * 1024 + (k % 4) * 256 + lane * 4);
+            fence();
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int ob = 4 * bt + j;
+                f32x16 t = acc_get(ob);
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const float4 o4 = ov[4 * j + q];
+                    t[4 * q] += o4.x; t[4 * q + 1] += o4.y; t[4 * q + 2] += o4.z; t[4 * q + 3] += o4.w;
+                }
+                acc_put(ob, t);
+                fence();
+            }
+        }
+        const float2 so = stats[(long long)(2 * tile + (half ^ 1)) * BM + 32 * w + r];
+        hs += so.x;
+        hq += so.y;
+        // y = rstd (W2g h - mu c1) + c2 over the whole hidden (k_ffn.hip DEC's fold; one-pass variance of the bf16 h)
+        const float mu = hs * (1.f / FF);
+        const float rsf = 1.f / sqrtf(fmaxf(hq * (1.f / FF) - mu * mu, 0.f) + eps);
+#pragma unroll
+        for (int ob = 0; ob < 16; ++ob) {
+            fence();
+            f32x16 t = acc_get(ob);
+            f32x4 C1[4], C2[4];
+            vec_block(V_BQ, V_C2, ob, C1, C2);
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) t[4 * q + i] = rsf * (t[4 * q + i] - mu * C1[q][i]) + C2[q][i];
+            if (!OP && Xo && live) {   // MODE 7 with xo: the FFN output y itself (the op tests; the path passes none)
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    *(float4*)(Xo + rg * FD + 32 * ob + 8 * q + 4 * h) =
+                        make_float4(t[4 * q], t[4 * q + 1], t[4 * q + 2], t[4 * q + 3]);
+            }
+            acc_put(ob, t);
+        }
+        fence();
+    }
     // ---- epilogue (no DMA in flight: the last tiles were waited for by their tops)
-    if (live && Xo && VAR != 8) {
+    if (!DEC && live && Xo && VAR != 8) {
 #pragma unroll
         for (int ob = 0; ob < 16; ++ob) {
             fence();
@@ -814,17 +955,60 @@ __global__ __launch_bounds__(256) void ffn2_pack_qkv_kernel(const bf16* __restri
     *(bf16x8*)(Wp + (long long)gid * 8) = o;
 }
 
+// decoder half stream h (MODE 7 / 8): fragment q of the 32-chunk stream of hidden chunks 32 h .. 32 h + 31, W1 rows of
+// the chunk (permuted k, as ffn2_pack_kernel) and W2g = bf16(W2 diag(gamma_F)) columns of the chunk (the value
+// k_ffn.hip's DEC pack and ffn_dec_consts_kernel use, so c1 = rowsum of exactly these bf16 values)
+__global__ __launch_bounds__(256) void ffn2_pack_dec_kernel(const bf16* __restrict__ W1, const float* __restrict__ W2,
+                                                            const float* __restrict__ gF, bf16* __restrict__ Wp, int hh0) {
+    constexpr int NCHH = NCH / 2, TAIL = 32 + (NCHH - 1) * CHF;
+    const int gid = blockIdx.x * 256 + threadIdx.x;   // < NCHH * CHF * 64
+    const int q = gid >> 6, l = gid & 63, m = l & 31, hh = l >> 5;
+    int c, j;
+    bool w1;
+    if (q < 32) { c = 0; w1 = true; j = q; }
+    else if (q >= TAIL) { c = NCHH - 1; w1 = false; j = q - TAIL; }
+    else {
+        const int b = (q - 32) / CHF, i = (q - 32) % CHF;
+        if (i < 48) {
+            const int mm = i / 3, rr = i % 3;
+            if (rr < 2) { c = b + 1; w1 = true; j = 2 * mm + rr; }
+            else { c = b; w1 = false; j = mm; }
+        } else {
+            c = b; w1 = false; j = 16 + (i - 48);
+        }
+    }
+    const int cg = NCHH * hh0 + c;   // global hidden chunk
+    bf16x8 o;
+    if (w1) {
+        const int kb = j >> 1, s = j & 1;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = W1[(long long)(HC * cg + m) * FD + 32 * kb + perm_k(s, hh, e)];
+    } else {
+        const int ob = j & 15, s = j >> 4;
+        const long long rowb = (long long)(32 * ob + m) * FF;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const int k = HC * cg + perm_k(s, hh, e);
+            o[e] = f2bf(W2[rowb + k] * gF[k]);
+        }
+    }
+    *(bf16x8*)(Wp + (long long)gid * 8) = o;
+}
+
 template <int MODE>
 hipError_t ffn2_launch(hipStream_t st, int M, const float* x, const float* g, const float* be, float eps, const bf16* Wp,
                        const float* b1, const float* b2, float* xo, const float* gn, const float* bn, bf16* xn,
-                       const bf16* o, const bf16* f, const float* bo, const float* c1) {
+                       const bf16* o, const bf16* f, const float* bo, const float* c1, float* part = nullptr,
+                       unsigned* cnt = nullptr) {
     static bool attr_done = false;   // one flag per instantiation
     if (!attr_done) {
         attr_done = true;
         (void)hipFuncSetAttribute((const void*)ffn2_kernel<MODE>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
     }
-    hipLaunchKernelGGL(ffn2_kernel<MODE>, dim3((M + BM - 1) / BM), dim3(64 * NW), LDS_BYTES, st, x, M, g, be, eps, Wp,
-                       b1, b2, xo, gn, bn, xn, o, f, bo, c1);
+    const int tiles = (M + BM - 1) / BM;
+    const int grid = MODE >= 7 ? 16 * ((tiles + 7) / 8) : tiles;   // DEC: two halves per tile, pairs 8 blocks apart
+    hipLaunchKernelGGL(ffn2_kernel<MODE>, dim3(grid), dim3(64 * NW), LDS_BYTES, st, x, M, g, be, eps, Wp, b1, b2, xo, gn,
+                       bn, xn, o, f, bo, c1, part, cnt);
     PFM_LAUNCH_CHECK();
     return hipSuccess;
 }
@@ -907,6 +1091,48 @@ hipError_t pfm_ffn2_fused_op_qkv_xv(const bf16* o, const bf16* f, const float* b
         return hipErrorInvalidValue;
     if (xo_planes) return ffn2_launch<6>(st, M, x, g2, be2, eps, Wop, b1, b2, xo, gn, bn, qkv, o, f, bo, bq);
     return ffn2_launch<5>(st, M, x, g2, be2, eps, Wop, b1, b2, xo, gn, bn, qkv, o, f, bo, bq);
+}
+
+// ---- decoder FFN, hidden split over two workgroups per 128-row tile (ffn2_kernel MODE 7 / 8)
+// Packed block of one decoder FFN: [Wo fragments | half-0 stream][Wo fragments | half-1 stream] (the Wo slots hold the
+// previous block's out-projection, packed twice; MODE 7 leaves them unused).
+size_t pfm_ffn2_dec_packed_elems() { return (size_t)2 * (OPF + NCH / 2 * CHF) * FE; }
+
+hipError_t pfm_ffn2_pack_dec(const bf16* W1, const float* W2, const float* gF, const bf16* Wo, bf16* Wp, hipStream_t st) {
+    const size_t hs = (size_t)(OPF + NCH / 2 * CHF) * FE;
+    for (int hh = 0; hh < 2; ++hh) {
+        if (Wo) {
+            hipLaunchKernelGGL(ffn2_pack_o_kernel, dim3(OPF * 64 / 256), dim3(256), 0, st, Wo, Wp + hh * hs);
+            PFM_LAUNCH_CHECK();
+        }
+        hipLaunchKernelGGL(ffn2_pack_dec_kernel, dim3(NCH / 2 * CHF * 64 / 256), dim3(256), 0, st, W1, W2, gF,
+                           Wp + hh * hs + (size_t)OPF * FE, hh);
+        PFM_LAUNCH_CHECK();
+    }
+    return hipSuccess;
+}
+
+// scratch of one launch over M rows: the partials (two halves x 128 rows x 512 f32 per tile slot of the grid) and the
+// LN_F statistics behind them; counters: one per tile slot, zero before the first launch (every launch leaves them 0)
+size_t pfm_ffn2_dec_scratch_floats(int M) {
+    const size_t slots = (size_t)8 * (((M + BM - 1) / BM + 7) / 8);
+    return slots * 2 * NW * 16 * 1024 + slots * 2 * BM * 2;
+}
+size_t pfm_ffn2_dec_counters(int M) { return (size_t)8 * (((M + BM - 1) / BM + 7) / 8); }
+
+// x f32 [M, 512] -> xn = LN_next(W2 LN_F(relu(W1 LN1(x1) + b1))) bf16 [M, 512]; with o (bf16 [M, 512]) and bo: x1 = x +
+// o Wo^T + bo, written to xo (f32, may alias x); else x1 = x and xo (optional) receives y. Wp: pfm_ffn2_pack_dec; c1 / c2: the LN_F fold constants
+// (pfm_ffn_pack_dec); part / cnt: pfm_ffn2_dec_scratch_floats(M) floats / pfm_ffn2_dec_counters(M) zeroed counters,
+// private to this launch's stream.
+hipError_t pfm_ffn2_fused_dec(const float* x, int M, const float* g1, const float* be1, float eps, const bf16* Wp,
+                              const float* b1, const float* c1, const float* c2, float* xo, const float* gn,
+                              const float* bn, bf16* xn, const bf16* o, const float* bo, float* part, unsigned* cnt,
+                              hipStream_t st) {
+    if (M <= 0) return hipSuccess;
+    if (!x || !xn || !gn || !bn || !c1 || !c2 || !b1 || !part || !cnt || (o && (!bo || !xo))) return hipErrorInvalidValue;
+    if (!al16(x) || !al16(xo) || !al16(Wp) || !al16(xn) || !al16(o) || !al16(bo) || !al16(part)) return hipErrorInvalidValue;
+    if (o) return ffn2_launch<8>(st, M, x, g1, be1, eps, Wp, b1, c2, xo, gn, bn, xn, o, nullptr, bo, c1, part, cnt);
+    return ffn2_launch<7>(st, M, x, g1, be1, eps, Wp, b1, c2, xo, gn, bn, xn, nullptr, nullptr, nullptr, c1, part, cnt);
 }
 
 // MODE 3: pfm_ffn2_fused_op with Wop = Wo's two planes, then the FFN fragments (the last layer under bit 8)

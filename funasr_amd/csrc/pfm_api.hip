@@ -88,6 +88,16 @@ hipError_t pfm_ffn_fused_dec(const float* x, int M, const float* g1, const float
                              const float* b1, const float* c1, const float* c2, float* xo, const float* gn,
                              const float* bn, bf16* xn, const bf16* o, const float* bo, hipStream_t st);
 hipError_t pfm_ffn_pack_o(const bf16* Wo, bf16* Wp, hipStream_t st);
+hipError_t pfm_ffn_dec_consts(const float* W2, const float* gF, const float* bF, float* c1, float* c2, hipStream_t st);
+// k_ffn2.hip: the decoder FFN with its hidden split over two workgroups per 128-row tile (MODE 7 / 8)
+size_t pfm_ffn2_dec_packed_elems();
+hipError_t pfm_ffn2_pack_dec(const bf16* W1, const float* W2, const float* gF, const bf16* Wo, bf16* Wp, hipStream_t st);
+size_t pfm_ffn2_dec_scratch_floats(int M);
+size_t pfm_ffn2_dec_counters(int M);
+hipError_t pfm_ffn2_fused_dec(const float* x, int M, const float* g1, const float* be1, float eps, const bf16* Wp,
+                              const float* b1, const float* c1, const float* c2, float* xo, const float* gn,
+                              const float* bn, bf16* xn, const bf16* o, const float* bo, float* part, unsigned* cnt,
+                              hipStream_t st);
 // k_ffn2.hip: the encoder's fused sub-layers at 128 rows per workgroup (same packed sizes, its own fragment order)
 hipError_t pfm_ffn2_pack(const bf16* W1, const bf16* W2, bf16* Wp, hipStream_t st);
 hipError_t pfm_ffn2_pack_o(const bf16* Wo, bf16* Wp, hipStream_t st);
@@ -242,7 +252,8 @@ void pfm_knobs_refresh() {
     k.exact_x6 = iv("PFM_EXACT_X6", 1) != 0;
     k.dec_subbatch = std::max(1, iv("PFM_DEC_SUBBATCH", 2));
     k.ffn_op = iv("PFM_FFN_OP", 1) != 0;
-    k.dec_ffn_fused = iv("PFM_DEC_FFN_FUSED", 1) != 0;
+    // 0 unfused; 1 the 64-row k_ffn.hip DEC kernel; 2 the 128-row k_ffn2.hip kernel, hidden split over two workgroups
+    k.dec_ffn_fused = std::max(0, std::min(iv("PFM_DEC_FFN_FUSED", 2), 2));
     k.ffn_kernel = iv("PFM_FFN_KERNEL", 2) == 1 ? 1 : 2;
     k.ffn_qkv = iv("PFM_FFN_QKV", 1) != 0;
     k.fast_xw = iv("PFM_FAST_XW", 7) & 15;
@@ -330,6 +341,9 @@ struct pfm_handle {
     int ffn_kind = 0;              // which fused-FFN kernel the packed encoder weights (ffn_pack) are ordered for
     DevBuf dffn_pack, dffn_c;      // decoder FFNs (16 blocks + decoders3): W1 | W2 diag(gamma_F) tiles; c1 | c2
     bool dffn_ready = false;
+    int dffn_kind = 0;             // PFM_DEC_FFN_FUSED the decoder pack is ordered for (1 k_ffn.hip, 2 k_ffn2.hip split)
+    DevBuf dffn2_part, dffn2_cnt;  // split decoder FFN: per-group partial y / LN_F statistics, tile counters (zeroed)
+    size_t dffn2_cnt_n = 0;
     DevBuf arena_x6;               // EXACT mode: three bf16 planes of every GEMM weight (x = x0 + x1 + x2)
     bool x6_ready = false;
     std::map<hipStream_t, std::unique_ptr<DevBuf>> x6_scratch;   // split A operands, one buffer per stream
@@ -632,10 +646,12 @@ int ensure_bf16(pfm_handle* h, hipStream_t st) {
         h->ffn_ready = true;
     }
     const int ndf = h->cfg.dec_blocks > 0 ? h->cfg.dec_blocks + 1 : 0;
-    if (!h->dffn_ready && ffn_shape_ok(h->cfg) && pfm_knobs().dec_ffn_fused && ndf > 0 && !h->dec.empty()) {
-        // per FFN j: the 32 out-projection tiles of decoder block j - 1 (folded in front; none for j = 0),
-        // then the FFN's 256 tiles
-        const size_t po = pfm_ffn_packed_o_elems(), per = po + pfm_ffn_packed_elems();
+    const int dk = pfm_knobs().dec_ffn_fused;
+    if (h->dffn_kind != dk) { h->dffn_ready = false; h->dffn_kind = dk; }
+    if (!h->dffn_ready && ffn_shape_ok(h->cfg) && dk && ndf > 0 && !h->dec.empty()) {
+        // k_ffn.hip (1): per FFN j the 32 out-projection tiles of decoder block j - 1 (folded in front; none for j = 0),
+        // then the FFN's 256 tiles; k_ffn2.hip (2): [Wo | half-0 stream][Wo | half-1 stream] (pfm_ffn2_pack_dec)
+        const size_t po = pfm_ffn_packed_o_elems(), per = dk == 2 ? pfm_ffn2_dec_packed_elems() : po + pfm_ffn_packed_elems();
         const int D = h->cfg.d_model;
         HIP_TRY(h->dffn_pack.ensure((size_t)ndf * per * sizeof(bf16)));
         HIP_TRY(h->dffn_c.ensure((size_t)ndf * 2 * D * sizeof(float)));
@@ -644,9 +660,15 @@ int ensure_bf16(pfm_handle* h, hipStream_t st) {
             const size_t w1 = d3 ? h->d3w1 : h->dec[j].w1, w2 = d3 ? h->d3w2 : h->dec[j].w2;
             const size_t gF = d3 ? h->d3ng : h->dec[j].ng, bF = d3 ? h->d3nb : h->dec[j].nb;
             float* cc = h->dffn_c.as<float>() + (size_t)j * 2 * D;
-            if (j > 0) HIP_TRY(pfm_ffn_pack_o(h->wb(h->dec[j - 1].wo), h->dffn_pack.as<bf16>() + (size_t)j * per, st));
-            HIP_TRY(pfm_ffn_pack_dec(h->wb(w1), h->w(w2), h->w(gF), h->w(bF), h->dffn_pack.as<bf16>() + (size_t)j * per + po,
-                                     cc, cc + D, st));
+            bf16* blk = h->dffn_pack.as<bf16>() + (size_t)j * per;
+            if (dk == 2) {
+                HIP_TRY(pfm_ffn2_pack_dec(h->wb(w1), h->w(w2), h->w(gF), j > 0 ? h->wb(h->dec[j - 1].wo) : nullptr, blk,
+                                          st));
+                HIP_TRY(pfm_ffn_dec_consts(h->w(w2), h->w(gF), h->w(bF), cc, cc + D, st));
+                continue;
+            }
+            if (j > 0) HIP_TRY(pfm_ffn_pack_o(h->wb(h->dec[j - 1].wo), blk, st));
+            HIP_TRY(pfm_ffn_pack_dec(h->wb(w1), h->w(w2), h->w(gF), h->w(bF), blk + po, cc, cc + D, st));
         }
         h->dffn_ready = true;
     }
@@ -1698,7 +1720,20 @@ int pfm_run(pfm_handle* h, void* stream, int mode, const float* feats, const int
     if (!kv_async) HIP_TRY(launch_kv(st, 0, c.dec_blocks));
     // One utterance group [b0, b0 + nb) of the decoder on rg.st: every buffer is row-addressed (rows b*L + t,
     // memory K|V rows b*T + t), so a group is the same launch sequence over offset pointers.
-    auto dec_group = [&](const Run& rg, int b0, int nb) -> int {
+    // split decoder FFN (PFM_DEC_FFN_FUSED=2): every concurrent group gets its own partials and tile counters
+    const int ngd = std::max(1, std::min({pfm_knobs().dec_subbatch, (int)pfm_handle::MAXSUB, B, h->prof_on ? 1 : 64}));
+    const int gmax = (int)(((long long)B + ngd - 1) / ngd * L);
+    const size_t part_n = pfm_ffn2_dec_scratch_floats(gmax), cnt_n = pfm_ffn2_dec_counters(gmax);
+    if (fast && h->dffn_ready && h->dffn_kind == 2) {
+        HIP_TRY(h->dffn2_part.ensure((size_t)ngd * part_n * sizeof(float)));
+        if (h->dffn2_cnt_n < (size_t)ngd * cnt_n) {   // counters start at zero; every launch leaves them zero
+            HIP_TRY(hipStreamSynchronize(st));
+            HIP_TRY(h->dffn2_cnt.ensure((size_t)ngd * cnt_n * sizeof(unsigned)));
+            HIP_TRY(hipMemsetAsync(h->dffn2_cnt.p, 0, (size_t)ngd * cnt_n * sizeof(unsigned), st));
+            h->dffn2_cnt_n = (size_t)ngd * cnt_n;
+        }
+    }
+    auto dec_group = [&](const Run& rg, int b0, int nb, int gi) -> int {
         hipStream_t s = rg.st;
         const size_t esz = fast ? 2 : 4;
         // EXACT mode on split-bf16 x6: the LayerNorms feeding a GEMM (LN1, LN3, LN_F, after_norm) and the
@@ -1732,6 +1767,21 @@ int pfm_run(pfm_handle* h, void* stream, int mode, const float* feats, const int
         auto ffn = [&](int fi, size_t lng, size_t lnb, size_t w1, size_t b1, size_t fng, size_t fnb,
                        size_t w2, float* out, size_t pg, size_t pb, void* pout, int pdt) -> int {
             // out = W2 . LN_F(relu(W1 . LN(x) + b1)); pout = LN_P(out)   (sanm/positionwise_feed_forward.py:26-33)
+            if (dffn && pdt == DT_BF16 && h->dffn_kind == 2) {   // k_ffn2.hip: hidden split over two workgroups
+                const double flo = 4.0 * Mg * (double)D * Fd + (op_from >= 0 ? 2.0 * Mg * (double)D * D : 0.0);
+                const double byo = (double)Mg * D * (4.0 + 2.0) + 2.0 * 2.0 * D * Fd;
+                ProfScope ps(h, s, PFM_K_GEMM, flo, byo);
+                const float* cc = h->dffn_c.as<float>() + (size_t)fi * 2 * D;
+                const bf16* blk = h->dffn_pack.as<bf16>() + (size_t)fi * pfm_ffn2_dec_packed_elems();
+                float* part = h->dffn2_part.as<float>() + (size_t)gi * part_n;
+                unsigned* cnt = h->dffn2_cnt.as<unsigned>() + (size_t)gi * cnt_n;
+                const bool opf = op_from >= 0;   // x = x + O Wo^T + bo of block op_from, then the FFN on it
+                HIP_TRY(pfm_ffn2_fused_dec(Xd, Mg, P(lng), P(lnb), c.ln_eps, blk, P(b1), cc, cc + D, opf ? Xd : nullptr,
+                                           P(pg), P(pb), (bf16*)pout, opf ? Odb : nullptr,
+                                           opf ? P(h->dec[op_from].bo) : nullptr, part, cnt, s));
+                op_from = -1;
+                return PFM_OK;
+            }
             if (dffn && pdt == DT_BF16) {   // out itself is dead in the decoder: only LN_P(out) is consumed
                 const double flo = 4.0 * Mg * (double)D * Fd;
                 const double byo = (double)Mg * D * (4.0 + 2.0) + 2.0 * 2.0 * D * Fd;
@@ -1850,10 +1900,10 @@ int pfm_run(pfm_handle* h, void* stream, int mode, const float* feats, const int
     // PFM_DEC_SUBBATCH=n: utterance groups on concurrent streams (default 2: with the fused decoder FFN kernels
     // the two groups overlap, 19.74 vs 19.90 ms/step in three interleaved rounds of tools/bench_ab.py; before
     // the FFN fusion they measured equal, 23.5-24.0 ms/step either way)
-    const int ng = std::max(1, std::min({pfm_knobs().dec_subbatch, (int)pfm_handle::MAXSUB, B, h->prof_on ? 1 : 64}));
+    const int ng = ngd;
     (void)Ml;
     if (ng == 1) {
-        rc = dec_group(run, 0, B);
+        rc = dec_group(run, 0, B, 0);
         return rc ? rc : finish();
     }
     if (!h->ev_fork) HIP_TRY(hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming));
@@ -1868,7 +1918,7 @@ int pfm_run(pfm_handle* h, void* stream, int mode, const float* feats, const int
         HIP_TRY(hipStreamWaitEvent(h->sub_st[k], h->ev_fork, 0));
         Run rk = run;
         rk.st = h->sub_st[k];
-        rc = dec_group(rk, b0, b1 - b0);
+        rc = dec_group(rk, b0, b1 - b0, k);
         if (rc) return rc;
         HIP_TRY(hipEventRecord(h->ev_join[k], h->sub_st[k]));
         HIP_TRY(hipStreamWaitEvent(st, h->ev_join[k], 0));
@@ -2344,6 +2394,21 @@ int pfm_op_ffn_dec(void* stream, const float* x, int M, const float* g1, const f
     if (o) {
         HIP_TRY(pfm_f32_to_bf16(Wo, wob, (long long)no, st));
         HIP_TRY(pfm_ffn_pack_o(wob, wp, st));
+    }
+    if (pfm_knobs().dec_ffn_fused == 2) {   // k_ffn2.hip: the hidden split over two workgroups per 128-row tile
+        bf16* wp2;
+        float* part;
+        unsigned* cnt;
+        HIP_TRY(sc.alloc(&wp2, pfm_ffn2_dec_packed_elems()));
+        HIP_TRY(sc.alloc(&part, pfm_ffn2_dec_scratch_floats(std::max(M, 1))));
+        HIP_TRY(sc.alloc(&cnt, pfm_ffn2_dec_counters(std::max(M, 1))));
+        HIP_TRY(hipMemsetAsync(cnt, 0, pfm_ffn2_dec_counters(std::max(M, 1)) * sizeof(unsigned), st));
+        HIP_TRY(pfm_ffn2_pack_dec(w1b, W2, gF, o ? wob : nullptr, wp2, st));
+        HIP_TRY(pfm_ffn_dec_consts(W2, gF, bF, cc, cc + 512, st));
+        HIP_TRY(pfm_ffn2_fused_dec(x, M, g1, b1n, eps, wp2, b1, cc, cc + 512, xo, gn, bn, (bf16*)xn, (const bf16*)o, bo,
+                                   part, cnt, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        return PFM_OK;
     }
     HIP_TRY(pfm_ffn_pack_dec(w1b, W2, gF, bF, wp + po, cc, cc + 512, st));
     auto dec = pfm_ffn_fused_dec;

@@ -170,6 +170,9 @@ class Paraformer(HipModel):
         """Greedy results from a (gathered) host token matrix, exactly as inference() builds them."""
         hyps = self._greedy_hyps(toks, ntok)
         key = self._keys(key, len(hyps))
+        if tokenizer is not None and hasattr(tokenizer, "postprocessed_texts"):
+            return [{"key": key[i], "text": t} for i, t in
+                    enumerate(tokenizer.postprocessed_texts([hl[0] for hl in hyps]))]
         out = []
         for i, hl in enumerate(hyps):
             ids = hl[0]
@@ -231,9 +234,20 @@ class Paraformer(HipModel):
         results = []
         owner = []   # batch index of each result (n-best gives several per utterance, an unfinished search none)
         writer = model_writer(self, kwargs)   # output_dir: {n}best_recog/{token,text} (model.py:548-552, 588-591)
+        # the texts of a character tokenizer in one vectorised pass (CharTokenizer.postprocessed_texts)
+        fast_txt = None
+        if tokenizer is not None and not pred_ts and hasattr(tokenizer, "postprocessed_texts"):
+            fast_txt = iter(tokenizer.postprocessed_texts([ids for i in range(b) for ids in hyps[i]]))
         for i in range(b):
             for nb, ids in enumerate(hyps[i]):   # n-best hypotheses of utterance i, best first (model.py:553)
                 owner.append(i)
+                if fast_txt is not None:
+                    text = next(fast_txt)
+                    results.append({"key": key[i], "text": text})
+                    if writer is not None:
+                        writer[f"{nb + 1}best_recog"]["token"][key[i]] = " ".join(tokenizer.ids2tokens(ids))
+                        writer[f"{nb + 1}best_recog"]["text"][key[i]] = text
+                    continue
                 if tokenizer is not None:
                     # model.py:567-586: text = tokens2text(ids2tokens(ids)); sentence_postprocess replaces it
                     # only for tokenizers without a `bpemodel` (a SentencepiecesTokenizer keeps tokens2text)

@@ -61,6 +61,29 @@ class CharTokenizer:
     def decode(self, ids: Iterable[int]) -> str:
         return self.tokens2text(self.ids2tokens(ids))
 
+    def postprocessed_texts(self, rows: Sequence[Sequence[int]]) -> List[str]:
+        """sentence_postprocess(ids2tokens(ids))[0] for every id row, with the common case vectorised: a row whose
+        tokens (specials dropped) are all Chinese / digit-led / "@" without spaces comes out as their concatenation
+        (sentence_postprocess's all-Chinese branch), every other row takes sentence_postprocess itself."""
+        import numpy as np
+        tab = getattr(self, "_pp_tab", None)
+        if tab is None:
+            spec = np.array([t in _SPECIAL for t in self.token_list], bool)
+            simple = np.array([(t in _SPECIAL) or (_zh_word(t) and " " not in t) for t in self.token_list], bool)
+            tab = self._pp_tab = (spec, simple)
+        spec, simple = tab
+        out = []
+        tl = self.token_list
+        for ids in rows:
+            a = np.asarray(ids, dtype=np.int64)
+            if a.size and bool(simple[a].all()):
+                kept = a[~spec[a]]
+                if kept.size:   # an all-special row is not "all Chinese" (len(mid) == 0): the general path
+                    out.append("".join([tl[i] for i in kept.tolist()]).strip())
+                    continue
+            out.append(sentence_postprocess(self.ids2tokens(ids))[0])
+        return out
+
     def encode(self, text, **kwargs) -> List[int]:
         """text (a string, or a list of words as the punctuation model passes) -> ids
         (abs_tokenizer.py:65-69; unknown tokens -> unk id)."""

@@ -452,13 +452,17 @@ def _dec_ffn_ref(x1, p, eps=1e-12):
     return y, exact
 
 
+@pytest.mark.parametrize("kernel", ["1", "2"])
 @pytest.mark.parametrize("M", [64, 200, 1000, 4100])
 @pytest.mark.parametrize("outproj", [False, True])
-def test_ffn_fused_decoder(dev, M, outproj):
-    """The decoder FFN exactly as the fast path runs it (ffn_fused_kernel DEC: LN1 prologue, LN_F folded through
-    W2, next LayerNorm epilogue; with outproj the previous block's cross-attention out-projection as phase 0,
-    x1 = x + o Wo^T + bo written back) vs fp64 on the kernel's bf16 roundings: y rel-L2 < 5e-3 (and < 2e-2 vs
-    the unrounded W2 LN_F(h)), xn within 1.6e-2 of LN_next of the fp64 y plus the y error; x1 rel < 1e-6."""
+def test_ffn_fused_decoder(dev, monkeypatch, M, outproj, kernel):
+    """The decoder FFN exactly as the fast path runs it (kernel 1: k_ffn.hip's 64-row DEC mode; kernel 2, the default:
+    k_ffn2.hip MODE 7 / 8, 128-row tiles with the hidden split over two workgroups that combine their partials
+    through a tile counter: LN1 prologue, LN_F folded through W2, next LayerNorm epilogue; with outproj the previous
+    block's cross-attention out-projection as phase 0, x1 = x + o Wo^T + bo written back) vs fp64 on the kernel's
+    bf16 roundings: y rel-L2 < 5e-3 (and < 2e-2 vs the unrounded W2 LN_F(h)), xn within 1e-2 of LN_next of the fp64
+    y; x1 rel < 1e-6. M = 200 / 1000 / 4100 leave partial tiles and grid padding (tiles past M)."""
+    monkeypatch.setenv("PFM_DEC_FFN_FUSED", kernel)
     g = torch.Generator().manual_seed(17 * M + outproj)
     p = _ffn_params(g, dec=True)
     x = torch.randn(M, 512, generator=g) * 2

@@ -243,3 +243,22 @@ def test_datadir_writer_semantics(tmp_path):
         w["1best_recog"]["k"] = "v"
     w.close()
     assert (tmp_path / "out" / "1best_recog" / "text").read_text(encoding="utf-8") == "a x y\na z\n"
+
+
+def test_postprocessed_texts_equal_sentence_postprocess():
+    """CharTokenizer.postprocessed_texts (the vectorised greedy-result path of Paraformer.inference) equals
+    sentence_postprocess(ids2tokens(ids))[0] row for row: all-Chinese rows (the fast path), rows with ASCII words,
+    BPE pieces, single-letter runs, specials, spaces and empty rows (the general path)."""
+    import numpy as np
+    from funasr_amd.text import CharTokenizer, sentence_postprocess
+    vocab = ["<blank>", "<s>", "</s>", "一", "丁", "中", "国", "1", "23", "@", "a", "b", "C", "hello", "wor@@", "ld",
+             "<unk>", "<OOV>", "'", "x y", "é", "<s>中", "，", "9a"]
+    tok = CharTokenizer(token_list=vocab)
+    rng = np.random.default_rng(3)
+    rows = [[], [1], [16, 17], [3, 4, 5], [3, 16, 4], [7, 8, 9, 3]]
+    for _ in range(4000):
+        n = int(rng.integers(0, 12))
+        hi = 10 if rng.random() < 0.5 else len(vocab)
+        rows.append([int(v) for v in rng.integers(1, hi, n)])
+    want = [sentence_postprocess(tok.ids2tokens(r))[0] for r in rows]
+    assert tok.postprocessed_texts(rows) == want
