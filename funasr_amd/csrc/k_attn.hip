@@ -519,6 +519,12 @@ constexpr int STG2 = KTILE + VTILE;             // 36 KiB per stage
 constexpr int FSMN_LDS = (256 + 10) * DK * 2 + 11 * DK * 4;   // fused FSMN window + taps (8-wave kernel)
 constexpr int LDS8_FS = 2 * STG2 + FSMN_LDS;            // K/V stages + the FSMN window captured beside them
 constexpr float RESCALE_THR = 8.0f;             // lazy O rescale: only when a row max grows by > 8
+#ifndef ATTN_CSUB
+#define ATTN_CSUB 0
+#endif
+#ifndef ATTN_LMFMA
+#define ATTN_LMFMA 0
+#endif
 
 typedef short v4i16 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
@@ -626,6 +632,11 @@ __global__ __launch_bounds__(NWV * 64, 8 / NWV) void attn_bf16_kernel(AttnArgs a
 #pragma unroll
         for (int e = 0; e < 16; ++e) o[d][e] = 0.f;
     float mused = -INFINITY, lrun = 0.f;
+    // ATTN_LMFMA: the row sums come from the matrix core, P^T against an all-ones A fragment (every accumulator register
+    // of lane q then holds sum_key bf16(P[q][key]): the normaliser of exactly the P the PV products used)
+    f32x16 ol;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) ol[e] = 0.f;
     const int ntiles = (klen + KT2 - 1) / KT2;
 
     // register staging: each thread moves (64 rows x 16 chunks) / NT chunks of K and of V per tile.
@@ -709,10 +720,13 @@ __global__ __launch_bounds__(NWV * 64, 8 / NWV) void attn_bf16_kernel(AttnArgs a
             for (int kq = 0; kq < 8; ++kq) kx[kb][kq] = *(const bf16x8*)(Ks + row * KROW + (((2 * kq + fh) ^ (row & 15)) << 4));
         }
         __builtin_amdgcn_sched_barrier(0);
+        // ATTN_CSUB: the QK^T chain starts from C = -mused (the running max; 0 before the first tile), so the common
+        // path's probabilities are exp2(s) with no per-score subtract (only a tile that moves the max subtracts)
+        const float mb = ATTN_CSUB ? (mused == -INFINITY ? 0.f : mused) : 0.f;
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb) {
 #pragma unroll
-            for (int e = 0; e < 16; ++e) s[kb][e] = 0.f;
+            for (int e = 0; e < 16; ++e) s[kb][e] = ATTN_CSUB ? -mb : 0.f;
             if constexpr (VAR == 4) continue;
 #pragma unroll
             for (int kq = 0; kq < 8; ++kq) s[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kx[kb][kq], qf[kq], s[kb], 0, 0, 0);
@@ -737,13 +751,29 @@ __global__ __launch_bounds__(NWV * 64, 8 / NWV) void attn_bf16_kernel(AttnArgs a
 #pragma unroll
             for (int e = 0; e < 16; ++e) mt = fmaxf(mt, s[kb][e]);
         mt = xor32_max(mt);
-        if (mt > mused + RESCALE_THR * 1.4426950408889634f) {   // lazy rescale (log2 units; rare after tile 0)
+        if constexpr (ATTN_CSUB) {   // s holds QK^T - mb: the max test and the rare subtract in those units
+            if (mt + mb > mused + RESCALE_THR * 1.4426950408889634f) {   // lazy rescale (log2 units)
+                const float corr = __builtin_amdgcn_exp2f(mused - (mt + mb));
+                lrun *= corr;
+#pragma unroll
+                for (int d = 0; d < 4; ++d)
+#pragma unroll
+                    for (int e = 0; e < 16; ++e) o[d][e] *= corr;
+                if constexpr (ATTN_LMFMA) ol *= corr;
+                mused = mt + mb;
+#pragma unroll
+                for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+                    for (int e = 0; e < 16; ++e) s[kb][e] -= mt;
+            }
+        } else if (mt > mused + RESCALE_THR * 1.4426950408889634f) {   // lazy rescale (log2 units; rare after tile 0)
             const float corr = __builtin_amdgcn_exp2f(mused - mt);
             lrun *= corr;
 #pragma unroll
             for (int d = 0; d < 4; ++d)
 #pragma unroll
                 for (int e = 0; e < 16; ++e) o[d][e] *= corr;
+            if constexpr (ATTN_LMFMA) ol *= corr;
             mused = mt;
         }
         float ls = 0.f;
@@ -751,11 +781,13 @@ __global__ __launch_bounds__(NWV * 64, 8 / NWV) void attn_bf16_kernel(AttnArgs a
         for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
             for (int e = 0; e < 16; ++e) {
-                s[kb][e] = __builtin_amdgcn_exp2f(s[kb][e] - mused);
-                ls += s[kb][e];
+                s[kb][e] = __builtin_amdgcn_exp2f(ATTN_CSUB ? s[kb][e] : s[kb][e] - mused);
+                if constexpr (!ATTN_LMFMA) ls += s[kb][e];
             }
-        ls = xor32_add(ls);
-        lrun += ls;
+        if constexpr (!ATTN_LMFMA) {
+            ls = xor32_add(ls);
+            lrun += ls;
+        }
         } else {
             lrun = 1.f;
         }
@@ -779,6 +811,12 @@ __global__ __launch_bounds__(NWV * 64, 8 / NWV) void attn_bf16_kernel(AttnArgs a
                     __builtin_memcpy(&va, &lo, 8);
                     __builtin_memcpy(((char*)&va) + 8, &hi, 8);
                     o[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va, pb, o[d], 0, 0, 0);
+                }
+                if constexpr (ATTN_LMFMA) {
+                    bf16x8 ones;
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) ones[j] = (bf16)1.f;
+                    ol = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, pb, ol, 0, 0, 0);
                 }
             }
         }
@@ -808,6 +846,9 @@ __global__ __launch_bounds__(NWV * 64, 8 / NWV) void attn_bf16_kernel(AttnArgs a
         compute(t);
         if (t + 1 < ntiles) sstore((t + 1) & 1, nx, t + 1);
         __syncthreads();
+    }
+    if constexpr (ATTN_LMFMA) {
+        if constexpr (VAR != 2) lrun = ol[0];
     }
     {
         if (!a.o && a.o2) {   // bf16 rows only: 8 x 16-B stores per lane (the two half-waves hold 8-B pieces of a row)

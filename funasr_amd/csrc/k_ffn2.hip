@@ -202,20 +202,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int r = lane & 31, h = lane >> 5;
-    static_assert(MODE == 0 || MODE == 1 || MODE == 3 || MODE == 4 || MODE == 5 || MODE == 6 || MODE == 7 || MODE == 8,
-                  "encoder / decoder modes");
-    constexpr bool DEC = MODE >= 7;                // decoder FFN, hidden split over two workgroups per tile
-    constexpr bool OP = MODE == 1 || MODE == 3 || (MODE >= 4 && MODE <= 6) || MODE == 8;   // out-projection in front
+    static_assert(MODE == 0 || MODE == 1 || MODE == 3 || (MODE >= 4 && MODE <= 10), "encoder / decoder modes");
+    constexpr bool DEC = MODE >= 7;                // decoder FFN (LN_F folded through W2)
+    constexpr bool SPLIT = MODE == 7 || MODE == 8; // ... its hidden split over two workgroups per tile
+    constexpr bool OP = MODE == 1 || MODE == 3 || (MODE >= 4 && MODE <= 6) || MODE == 8 || MODE == 10;   // Wo in front
     constexpr bool QK = MODE >= 4 && MODE <= 6;    // + the next layer's QKV
     constexpr bool XV = MODE == 5 || MODE == 6;    // + the v rows' second weight plane
     constexpr bool XO = MODE == 3 || MODE == 6;    // + Wo's second weight plane
-    constexpr int NCHK = DEC ? NCH / 2 : NCH;      // hidden chunks this workgroup streams
+    constexpr int NCHK = SPLIT ? NCH / 2 : NCH;    // hidden chunks this workgroup streams
     constexpr int F0 = OP ? (XO ? 2 : 1) * OPF : 0, F3 = F0 + NCHK * CHF, NF = F3 + (QK ? QKF + (XV ? OPF : 0) : 0),
                   NT = NF / TF;
     // DEC: tile t's halves are blocks 16 (t >> 3) + (t & 7) and that + 8 (the same XCD)
     const int bid = blockIdx.x;
-    const int tile = DEC ? ((bid >> 4) << 3) | (bid & 7) : bid, half = DEC ? (bid >> 3) & 1 : 0;
-    if (DEC && (long long)tile * BM >= M) return;   // grid padding (both halves of such a tile leave)
+    const int tile = SPLIT ? ((bid >> 4) << 3) | (bid & 7) : bid, half = SPLIT ? (bid >> 3) & 1 : 0;
+    if (SPLIT && (long long)tile * BM >= M) return;   // grid padding (both halves of such a tile leave)
     const long long rg = (long long)tile * BM + 32 * w + r;   // this lane's row
     const bool live = rg < M;
     const long long rc = live ? rg : (long long)M - 1;               // clamped for loads
@@ -248,7 +248,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     __syncthreads();
 
     // ---- weight ring: tile t -> slot t % RS; this wave moves fragments GW w .. GW w + GW - 1 of each tile
-    // DEC: the layer block holds [Wo | half-0 stream][Wo | half-1 stream]; MODE 7 (no out-projection) skips the Wo slot
+    // DEC: the layer block holds [Wo | half-0 stream][Wo | half-1 stream] (split) or [Wo | stream]; no out-projection
+    // in front (MODE 7 / 9): the Wo slot is skipped
     const bf16* wbase = DEC ? Wp + (long long)half * (OPF + NCHK * CHF) * FE + (OP ? 0 : (long long)OPF * FE) : Wp;
     const bf16* wsrc = wbase + (long long)GW * w * FE + lane * 8;
     // piece p (0..3) of tile t: one 1 KiB LDS-DMA per wave. The four pieces of a wave are 1 KiB apart in both
@@ -688,6 +689,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     if constexpr (DEC) {
         hs += __shfl_xor(hs, 32, 64);   // lanes r and r + 32 hold the two halves of each 32-feature group
         hq += __shfl_xor(hq, 32, 64);
+    }
+    if constexpr (SPLIT) {
         constexpr long long WPART = 16 * 1024;   // floats of one wave's partial: 16 blocks x 16 registers x 64 lanes
         float* mine = part + ((long long)(2 * tile + half) * NW + w) * WPART;
 #pragma unroll
@@ -735,6 +738,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         const float2 so = stats[(long long)(2 * tile + (half ^ 1)) * BM + 32 * w + r];
         hs += so.x;
         hq += so.y;
+    }
+    if constexpr (DEC) {
         // y = rstd (W2g h - mu c1) + c2 over the whole hidden (k_ffn.hip DEC's fold; one-pass variance of the bf16 h)
         const float mu = hs * (1.f / FF);
         const float rsf = 1.f / sqrtf(fmaxf(hq * (1.f / FF) - mu * mu, 0.f) + eps);
@@ -748,7 +753,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
             for (int q = 0; q < 4; ++q)
 #pragma unroll
                 for (int i = 0; i < 4; ++i) t[4 * q + i] = rsf * (t[4 * q + i] - mu * C1[q][i]) + C2[q][i];
-            if (!OP && Xo && live) {   // MODE 7 with xo: the FFN output y itself (the op tests; the path passes none)
+            if (!OP && Xo && live) {   // MODE 7 / 9 with xo: the FFN output y itself (the op tests; the path passes none)
 #pragma unroll
                 for (int q = 0; q < 4; ++q)
                     *(float4*)(Xo + rg * FD + 32 * ob + 8 * q + 4 * h) =
@@ -959,8 +964,9 @@ __global__ __launch_bounds__(256) void ffn2_pack_qkv_kernel(const bf16* __restri
 // the chunk (permuted k, as ffn2_pack_kernel) and W2g = bf16(W2 diag(gamma_F)) columns of the chunk (the value
 // k_ffn.hip's DEC pack and ffn_dec_consts_kernel use, so c1 = rowsum of exactly these bf16 values)
 __global__ __launch_bounds__(256) void ffn2_pack_dec_kernel(const bf16* __restrict__ W1, const float* __restrict__ W2,
-                                                            const float* __restrict__ gF, bf16* __restrict__ Wp, int hh0) {
-    constexpr int NCHH = NCH / 2, TAIL = 32 + (NCHH - 1) * CHF;
+                                                            const float* __restrict__ gF, bf16* __restrict__ Wp, int hh0,
+                                                            int NCHH) {
+    const int TAIL = 32 + (NCHH - 1) * CHF;
     const int gid = blockIdx.x * 256 + threadIdx.x;   // < NCHH * CHF * 64
     const int q = gid >> 6, l = gid & 63, m = l & 31, hh = l >> 5;
     int c, j;
@@ -1006,7 +1012,7 @@ hipError_t ffn2_launch(hipStream_t st, int M, const float* x, const float* g, co
         (void)hipFuncSetAttribute((const void*)ffn2_kernel<MODE>, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
     }
     const int tiles = (M + BM - 1) / BM;
-    const int grid = MODE >= 7 ? 16 * ((tiles + 7) / 8) : tiles;   // DEC: two halves per tile, pairs 8 blocks apart
+    const int grid = (MODE == 7 || MODE == 8) ? 16 * ((tiles + 7) / 8) : tiles;   // split: two halves per tile, 8 apart
     hipLaunchKernelGGL(ffn2_kernel<MODE>, dim3(grid), dim3(64 * NW), LDS_BYTES, st, x, M, g, be, eps, Wp, b1, b2, xo, gn,
                        bn, xn, o, f, bo, c1, part, cnt);
     PFM_LAUNCH_CHECK();
@@ -1096,17 +1102,20 @@ hipError_t pfm_ffn2_fused_op_qkv_xv(const bf16* o, const bf16* f, const float* b
 // ---- decoder FFN, hidden split over two workgroups per 128-row tile (ffn2_kernel MODE 7 / 8)
 // Packed block of one decoder FFN: [Wo fragments | half-0 stream][Wo fragments | half-1 stream] (the Wo slots hold the
 // previous block's out-projection, packed twice; MODE 7 leaves them unused).
+// (split = false: one [Wo | full stream] block of the same size, for the unsplit 128-row MODE 9 / 10)
 size_t pfm_ffn2_dec_packed_elems() { return (size_t)2 * (OPF + NCH / 2 * CHF) * FE; }
 
-hipError_t pfm_ffn2_pack_dec(const bf16* W1, const float* W2, const float* gF, const bf16* Wo, bf16* Wp, hipStream_t st) {
-    const size_t hs = (size_t)(OPF + NCH / 2 * CHF) * FE;
-    for (int hh = 0; hh < 2; ++hh) {
+hipError_t pfm_ffn2_pack_dec(const bf16* W1, const float* W2, const float* gF, const bf16* Wo, bf16* Wp, hipStream_t st,
+                             bool split) {
+    const int nh = split ? 2 : 1, nchh = NCH / nh;
+    const size_t hs = (size_t)(OPF + nchh * CHF) * FE;
+    for (int hh = 0; hh < nh; ++hh) {
         if (Wo) {
             hipLaunchKernelGGL(ffn2_pack_o_kernel, dim3(OPF * 64 / 256), dim3(256), 0, st, Wo, Wp + hh * hs);
             PFM_LAUNCH_CHECK();
         }
-        hipLaunchKernelGGL(ffn2_pack_dec_kernel, dim3(NCH / 2 * CHF * 64 / 256), dim3(256), 0, st, W1, W2, gF,
-                           Wp + hh * hs + (size_t)OPF * FE, hh);
+        hipLaunchKernelGGL(ffn2_pack_dec_kernel, dim3(nchh * CHF * 64 / 256), dim3(256), 0, st, W1, W2, gF,
+                           Wp + hh * hs + (size_t)OPF * FE, hh, nchh);
         PFM_LAUNCH_CHECK();
     }
     return hipSuccess;
@@ -1123,13 +1132,18 @@ size_t pfm_ffn2_dec_counters(int M) { return (size_t)8 * (((M + BM - 1) / BM + 7
 // x f32 [M, 512] -> xn = LN_next(W2 LN_F(relu(W1 LN1(x1) + b1))) bf16 [M, 512]; with o (bf16 [M, 512]) and bo: x1 = x +
 // o Wo^T + bo, written to xo (f32, may alias x); else x1 = x and xo (optional) receives y. Wp: pfm_ffn2_pack_dec; c1 / c2: the LN_F fold constants
 // (pfm_ffn_pack_dec); part / cnt: pfm_ffn2_dec_scratch_floats(M) floats / pfm_ffn2_dec_counters(M) zeroed counters,
-// private to this launch's stream.
+// private to this launch's stream (the split MODE 7 / 8; both null: the unsplit MODE 9 / 10 on a split = false pack).
 hipError_t pfm_ffn2_fused_dec(const float* x, int M, const float* g1, const float* be1, float eps, const bf16* Wp,
                               const float* b1, const float* c1, const float* c2, float* xo, const float* gn,
                               const float* bn, bf16* xn, const bf16* o, const float* bo, float* part, unsigned* cnt,
                               hipStream_t st) {
     if (M <= 0) return hipSuccess;
-    if (!x || !xn || !gn || !bn || !c1 || !c2 || !b1 || !part || !cnt || (o && (!bo || !xo))) return hipErrorInvalidValue;
+    if (!x || !xn || !gn || !bn || !c1 || !c2 || !b1 || (o && (!bo || !xo))) return hipErrorInvalidValue;
+    if (!part || !cnt) {   // unsplit: one workgroup per 128-row tile streams the whole hidden (MODE 9 / 10)
+        if (!al16(x) || !al16(xo) || !al16(Wp) || !al16(xn) || !al16(o) || !al16(bo)) return hipErrorInvalidValue;
+        if (o) return ffn2_launch<10>(st, M, x, g1, be1, eps, Wp, b1, c2, xo, gn, bn, xn, o, nullptr, bo, c1);
+        return ffn2_launch<9>(st, M, x, g1, be1, eps, Wp, b1, c2, xo, gn, bn, xn, nullptr, nullptr, nullptr, c1);
+    }
     if (!al16(x) || !al16(xo) || !al16(Wp) || !al16(xn) || !al16(o) || !al16(bo) || !al16(part)) return hipErrorInvalidValue;
     if (o) return ffn2_launch<8>(st, M, x, g1, be1, eps, Wp, b1, c2, xo, gn, bn, xn, o, nullptr, bo, c1, part, cnt);
     return ffn2_launch<7>(st, M, x, g1, be1, eps, Wp, b1, c2, xo, gn, bn, xn, nullptr, nullptr, nullptr, c1, part, cnt);

@@ -121,7 +121,66 @@ __global__ __launch_bounds__(256) void vad_softmax_kernel(const float* __restric
     if (lane == 0) p_sil[row] = expf(l[0] - mx) / s;
 }
 
+// ComputeDecibel's frame energy (fsmn_vad_streaming/model.py:326-348: 10 log10(sum(frame^2) + 1e-6) over numpy float32
+// frames) -- the sum exactly as numpy's float32 add.reduce forms it along a contiguous row: pairwise_sum (blocks of
+// <= 128 elements summed by 8 interleaved accumulators combined ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)), the tail added in
+// order; longer runs split at n/2 rounded down to a multiple of 8), starting from 0, each square rounded before its add
+// (contraction off). The log10 stays on the host in numpy (the values it sees are then the reference's bit for bit).
+#pragma clang fp contract(off)
+__device__ float vad_pw_leaf(const float* x, int n) {
+    if (n < 8) {
+        float res = 0.f;
+        for (int i = 0; i < n; ++i) {
+            const float q = x[i] * x[i];
+            res = res + q;
+        }
+        return res;
+    }
+    float r[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] = x[j] * x[j];
+    int i = 8;
+    for (; i < n - (n % 8); i += 8)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const float q = x[i + j] * x[i + j];
+            r[j] = r[j] + q;
+        }
+    float res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+    for (; i < n; ++i) {
+        const float q = x[i] * x[i];
+        res = res + q;
+    }
+    return res;
+}
+template <int D> __device__ float vad_pw(const float* x, int n) {
+    if (n <= 128) return vad_pw_leaf(x, n);
+    if constexpr (D == 0) {
+        return __builtin_nanf("");   // deeper than the launcher allows (frame_len <= 2048)
+    } else {
+        int n2 = n / 2;
+        n2 -= n2 % 8;
+        const float a = vad_pw<D - 1>(x, n2);
+        const float b = vad_pw<D - 1>(x + n2, n - n2);
+        return a + b;
+    }
+}
+__global__ __launch_bounds__(256) void vad_frame_energy_kernel(const float* __restrict__ w, int nframes, int fl, int fs,
+                                                               float* __restrict__ e) {
+    const int f = blockIdx.x * 256 + threadIdx.x;
+    if (f < nframes) e[f] = vad_pw<4>(w + (long long)f * fs, fl);
+}
+#pragma clang fp contract(on)
+
 }  // namespace
+
+hipError_t pfm_vad_frame_energy(const float* wav, int nframes, int fl, int fs, float* e, hipStream_t st) {
+    if (nframes <= 0) return hipSuccess;
+    if (fl < 1 || fl > 2048 || fs < 1) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(vad_frame_energy_kernel, dim3((nframes + 255) / 256), dim3(256), 0, st, wav, nframes, fl, fs, e);
+    PFM_LAUNCH_CHECK();
+    return hipSuccess;
+}
 
 hipError_t pfm_vad_dense(const float* X, int ldx, int M, int K, const float* W, const float* b, int N, int relu,
                          float* Y, int ldy, hipStream_t st) {

@@ -91,7 +91,8 @@ hipError_t pfm_ffn_pack_o(const bf16* Wo, bf16* Wp, hipStream_t st);
 hipError_t pfm_ffn_dec_consts(const float* W2, const float* gF, const float* bF, float* c1, float* c2, hipStream_t st);
 // k_ffn2.hip: the decoder FFN with its hidden split over two workgroups per 128-row tile (MODE 7 / 8)
 size_t pfm_ffn2_dec_packed_elems();
-hipError_t pfm_ffn2_pack_dec(const bf16* W1, const float* W2, const float* gF, const bf16* Wo, bf16* Wp, hipStream_t st);
+hipError_t pfm_ffn2_pack_dec(const bf16* W1, const float* W2, const float* gF, const bf16* Wo, bf16* Wp, hipStream_t st,
+                             bool split);
 size_t pfm_ffn2_dec_scratch_floats(int M);
 size_t pfm_ffn2_dec_counters(int M);
 hipError_t pfm_ffn2_fused_dec(const float* x, int M, const float* g1, const float* be1, float eps, const bf16* Wp,
@@ -153,6 +154,7 @@ hipError_t pfm_vad_dense(const float* X, int ldx, int M, int K, const float* W, 
 hipError_t pfm_vad_fsmn(const float* x, int T, int D, float* cache, float* cache_tmp, const float* w, int L, float* y,
                         hipStream_t st);
 hipError_t pfm_vad_softmax(const float* logits, int M, int N, float* p_sil, float* probs, hipStream_t st);
+hipError_t pfm_vad_frame_energy(const float* wav, int nframes, int fl, int fs, float* e, hipStream_t st);
 hipError_t pfm_fbank_raw_launch(const float* wav, const int* nsamp, int B, int S_max, const unsigned char* tables,
                                 float* fb, int N_cap, hipStream_t st);
 hipError_t pfm_lfr_gather_launch(const float* frames, const int* idx, int rows, int m, const float* cmvn, float* out,
@@ -252,8 +254,9 @@ void pfm_knobs_refresh() {
     k.exact_x6 = iv("PFM_EXACT_X6", 1) != 0;
     k.dec_subbatch = std::max(1, iv("PFM_DEC_SUBBATCH", 2));
     k.ffn_op = iv("PFM_FFN_OP", 1) != 0;
-    // 0 unfused; 1 the 64-row k_ffn.hip DEC kernel; 2 the 128-row k_ffn2.hip kernel, hidden split over two workgroups
-    k.dec_ffn_fused = std::max(0, std::min(iv("PFM_DEC_FFN_FUSED", 2), 2));
+    // 0 unfused; 1 the 64-row k_ffn.hip DEC kernel; 2 the 128-row k_ffn2.hip kernel, hidden split over two workgroups;
+    // 3 the 128-row k_ffn2.hip kernel, whole hidden per workgroup
+    k.dec_ffn_fused = std::max(0, std::min(iv("PFM_DEC_FFN_FUSED", 1), 3));
     k.ffn_kernel = iv("PFM_FFN_KERNEL", 2) == 1 ? 1 : 2;
     k.ffn_qkv = iv("PFM_FFN_QKV", 1) != 0;
     k.fast_xw = iv("PFM_FAST_XW", 7) & 15;
@@ -368,6 +371,9 @@ struct pfm_handle {
     bool fb_tab_ready = false;
     int32_t* host_ntok = nullptr;
     int host_ntok_cap = 0;
+    DevBuf punc_io;                // pfm_run_punc_host: device ids | lens | punc of one call
+    int32_t* punc_pin = nullptr;   // ... and their pinned host staging
+    int punc_cap = 0;
     // encoder sub-batch streams: the batch is split into NSUB utterance groups whose layer sequences run
     // concurrently, so one group's HBM-bound phases (LayerNorm, GEMM epilogues, attention) overlap the
     // other's MFMA main loops
@@ -651,7 +657,7 @@ int ensure_bf16(pfm_handle* h, hipStream_t st) {
     if (!h->dffn_ready && ffn_shape_ok(h->cfg) && dk && ndf > 0 && !h->dec.empty()) {
         // k_ffn.hip (1): per FFN j the 32 out-projection tiles of decoder block j - 1 (folded in front; none for j = 0),
         // then the FFN's 256 tiles; k_ffn2.hip (2): [Wo | half-0 stream][Wo | half-1 stream] (pfm_ffn2_pack_dec)
-        const size_t po = pfm_ffn_packed_o_elems(), per = dk == 2 ? pfm_ffn2_dec_packed_elems() : po + pfm_ffn_packed_elems();
+        const size_t po = pfm_ffn_packed_o_elems(), per = dk >= 2 ? pfm_ffn2_dec_packed_elems() : po + pfm_ffn_packed_elems();
         const int D = h->cfg.d_model;
         HIP_TRY(h->dffn_pack.ensure((size_t)ndf * per * sizeof(bf16)));
         HIP_TRY(h->dffn_c.ensure((size_t)ndf * 2 * D * sizeof(float)));
@@ -661,9 +667,9 @@ int ensure_bf16(pfm_handle* h, hipStream_t st) {
             const size_t gF = d3 ? h->d3ng : h->dec[j].ng, bF = d3 ? h->d3nb : h->dec[j].nb;
             float* cc = h->dffn_c.as<float>() + (size_t)j * 2 * D;
             bf16* blk = h->dffn_pack.as<bf16>() + (size_t)j * per;
-            if (dk == 2) {
+            if (dk >= 2) {
                 HIP_TRY(pfm_ffn2_pack_dec(h->wb(w1), h->w(w2), h->w(gF), j > 0 ? h->wb(h->dec[j - 1].wo) : nullptr, blk,
-                                          st));
+                                          st, dk == 2));
                 HIP_TRY(pfm_ffn_dec_consts(h->w(w2), h->w(gF), h->w(bF), cc, cc + D, st));
                 continue;
             }
@@ -1488,6 +1494,7 @@ void pfm_destroy(pfm_handle* h) {
     }
     if (h->ev_fork) (void)hipEventDestroy(h->ev_fork);
     if (h->host_ntok) (void)hipHostFree(h->host_ntok);
+    if (h->punc_pin) (void)hipHostFree(h->punc_pin);
     delete h;
 }
 
@@ -1767,14 +1774,14 @@ int pfm_run(pfm_handle* h, void* stream, int mode, const float* feats, const int
         auto ffn = [&](int fi, size_t lng, size_t lnb, size_t w1, size_t b1, size_t fng, size_t fnb,
                        size_t w2, float* out, size_t pg, size_t pb, void* pout, int pdt) -> int {
             // out = W2 . LN_F(relu(W1 . LN(x) + b1)); pout = LN_P(out)   (sanm/positionwise_feed_forward.py:26-33)
-            if (dffn && pdt == DT_BF16 && h->dffn_kind == 2) {   // k_ffn2.hip: hidden split over two workgroups
+            if (dffn && pdt == DT_BF16 && h->dffn_kind >= 2) {   // k_ffn2.hip: 128-row tiles (2: hidden split)
                 const double flo = 4.0 * Mg * (double)D * Fd + (op_from >= 0 ? 2.0 * Mg * (double)D * D : 0.0);
                 const double byo = (double)Mg * D * (4.0 + 2.0) + 2.0 * 2.0 * D * Fd;
                 ProfScope ps(h, s, PFM_K_GEMM, flo, byo);
                 const float* cc = h->dffn_c.as<float>() + (size_t)fi * 2 * D;
                 const bf16* blk = h->dffn_pack.as<bf16>() + (size_t)fi * pfm_ffn2_dec_packed_elems();
-                float* part = h->dffn2_part.as<float>() + (size_t)gi * part_n;
-                unsigned* cnt = h->dffn2_cnt.as<unsigned>() + (size_t)gi * cnt_n;
+                float* part = h->dffn_kind == 2 ? h->dffn2_part.as<float>() + (size_t)gi * part_n : nullptr;
+                unsigned* cnt = h->dffn_kind == 2 ? h->dffn2_cnt.as<unsigned>() + (size_t)gi * cnt_n : nullptr;
                 const bool opf = op_from >= 0;   // x = x + O Wo^T + bo of block op_from, then the FFN on it
                 HIP_TRY(pfm_ffn2_fused_dec(Xd, Mg, P(lng), P(lnb), c.ln_eps, blk, P(b1), cc, cc + D, opf ? Xd : nullptr,
                                            P(pg), P(pb), (bf16*)pout, opf ? Odb : nullptr,
@@ -2102,6 +2109,35 @@ int pfm_run_punc(pfm_handle* h, void* stream, int mode, const int32_t* ids, cons
     return PFM_OK;
 }
 
+// One mini-sentence of the CT-Transformer text loop with host word ids in and host labels out (the per-call form
+// CTTransformer.punc_forward is used in, model.py:277-316): one pinned staging copy each way and pfm_run_punc on the
+// handle's own device buffers, so a caller's sequential loop costs one C call per sentence.
+int pfm_run_punc_host(pfm_handle* h, void* stream, int mode, const int32_t* ids, int n, int32_t* punc) {
+    pfm_knobs_refresh();
+    if (!h || !ids || !punc || n < 1) return fail(PFM_E_ARG, "pfm_run_punc_host: null argument or n < 1");
+    if (h->cfg.arch != PFM_ARCH_PUNC) return fail(PFM_E_STATE, "pfm_run_punc_host: handle is not a punctuation model");
+    HIP_TRY(hipSetDevice(h->device));
+    hipStream_t st = (hipStream_t)stream;
+    if (h->punc_cap < n) {
+        const int cap = std::max(n, 256);
+        if (h->punc_pin) { HIP_TRY(hipStreamSynchronize(st)); HIP_TRY(hipHostFree(h->punc_pin)); h->punc_pin = nullptr; }
+        HIP_TRY(hipHostMalloc((void**)&h->punc_pin, (size_t)(2 * cap + 1) * sizeof(int32_t), 0));
+        HIP_TRY(h->punc_io.ensure((size_t)(2 * cap + 1) * sizeof(int32_t)));
+        h->punc_cap = cap;
+    }
+    int32_t* pin = h->punc_pin;
+    memcpy(pin, ids, (size_t)n * sizeof(int32_t));
+    pin[n] = n;
+    int32_t* dio = h->punc_io.as<int32_t>();
+    HIP_TRY(hipMemcpyAsync(dio, pin, (size_t)(n + 1) * sizeof(int32_t), hipMemcpyHostToDevice, st));
+    const int rc = pfm_run_punc(h, stream, mode, dio, dio + n, 1, n, dio + n + 1, nullptr);
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(pin + n + 1, dio + n + 1, (size_t)n * sizeof(int32_t), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    memcpy(punc, pin + n + 1, (size_t)n * sizeof(int32_t));
+    return PFM_OK;
+}
+
 static int fbank_tables_build(DevBuf& dst) {
     std::vector<unsigned char> tab(pfm_fbank_table_bytes(), 0);
     float* melw = (float*)tab.data();
@@ -2395,7 +2431,7 @@ int pfm_op_ffn_dec(void* stream, const float* x, int M, const float* g1, const f
         HIP_TRY(pfm_f32_to_bf16(Wo, wob, (long long)no, st));
         HIP_TRY(pfm_ffn_pack_o(wob, wp, st));
     }
-    if (pfm_knobs().dec_ffn_fused == 2) {   // k_ffn2.hip: the hidden split over two workgroups per 128-row tile
+    if (pfm_knobs().dec_ffn_fused >= 2) {   // k_ffn2.hip: 128-row tiles (2: the hidden split over two workgroups)
         bf16* wp2;
         float* part;
         unsigned* cnt;
@@ -2403,10 +2439,11 @@ int pfm_op_ffn_dec(void* stream, const float* x, int M, const float* g1, const f
         HIP_TRY(sc.alloc(&part, pfm_ffn2_dec_scratch_floats(std::max(M, 1))));
         HIP_TRY(sc.alloc(&cnt, pfm_ffn2_dec_counters(std::max(M, 1))));
         HIP_TRY(hipMemsetAsync(cnt, 0, pfm_ffn2_dec_counters(std::max(M, 1)) * sizeof(unsigned), st));
-        HIP_TRY(pfm_ffn2_pack_dec(w1b, W2, gF, o ? wob : nullptr, wp2, st));
+        const bool split = pfm_knobs().dec_ffn_fused == 2;
+        HIP_TRY(pfm_ffn2_pack_dec(w1b, W2, gF, o ? wob : nullptr, wp2, st, split));
         HIP_TRY(pfm_ffn_dec_consts(W2, gF, bF, cc, cc + 512, st));
         HIP_TRY(pfm_ffn2_fused_dec(x, M, g1, b1n, eps, wp2, b1, cc, cc + 512, xo, gn, bn, (bf16*)xn, (const bf16*)o, bo,
-                                   part, cnt, st));
+                                   split ? part : nullptr, split ? cnt : nullptr, st));
         HIP_TRY(hipStreamSynchronize(st));
         return PFM_OK;
     }
@@ -3338,6 +3375,19 @@ int pfm_vad_run(pfm_vad* v, void* stream, const float* feats, int T, float* p_si
                           v->p("encoder.out_linear2.linear.bias"), c.output_dim, 0, v->lg.as<float>(), c.output_dim,
                           st));
     HIP_TRY(pfm_vad_softmax(v->lg.as<float>(), T, c.output_dim, p_sil, probs, st));
+    return PFM_OK;
+}
+
+int pfm_vad_frame_energy(pfm_vad* v, void* stream, const float* wav, int nsamp, int frame_len, int frame_shift,
+                         float* energy) {
+    if (!v || nsamp < 0 || frame_len < 1 || frame_len > 2048 || frame_shift < 1)
+        return fail(PFM_E_ARG, "pfm_vad_frame_energy: bad arguments (1 <= frame_len <= 2048, frame_shift >= 1)");
+    const int nf = nsamp >= frame_len ? (nsamp - frame_len) / frame_shift + 1 : 0;
+    if (nf == 0) return PFM_OK;
+    if (!wav || !energy) return fail(PFM_E_ARG, "pfm_vad_frame_energy: null argument");
+    CHECK_DEV("pfm_vad_frame_energy", v->device, {"wav", wav}, {"energy", energy});
+    HIP_TRY(hipSetDevice(v->device));
+    HIP_TRY(pfm_vad_frame_energy(wav, nf, frame_len, frame_shift, energy, (hipStream_t)stream));
     return PFM_OK;
 }
 

@@ -143,14 +143,8 @@ class CTTransformer(HipModel):
 
     def punc_forward(self, ids: np.ndarray) -> np.ndarray:
         """One mini-sentence: word ids [n] -> argmax punctuation id per word (pfm_run_punc)."""
-        eng = self.engine()
-        dev = torch.device("cuda", eng.device)
-        n = len(ids)
-        # ids and their length in ONE host->device copy (the text loop is latency-bound, one call per
-        # mini-sentence)
-        buf = torch.from_numpy(np.append(np.asarray(ids, dtype=np.int32), np.int32(n))).to(dev)
-        r = eng.run_punc(buf[:n][None], buf[n:], mode=self.mode)
-        return r["punc"][0].cpu().numpy()
+        # the text loop is latency-bound (one call per mini-sentence): host ids in, host labels out, one C call
+        return self.engine().run_punc_host(ids, mode=self.mode)
 
     @torch.no_grad()
     def inference(self, data_in, data_lengths=None, key: List[str] = None, tokenizer=None, frontend=None,

@@ -28,7 +28,7 @@ ABI_SYMBOLS = ("pfm_config_default", "pfm_config_sensevoice", "pfm_create", "pfm
                "pfm_op_attention", "pfm_op_layernorm", "pfm_op_ln_gemm", "pfm_op_fsmn", "pfm_op_cif", "pfm_op_ctc_beam", "pfm_profile", "pfm_op_ffn", "pfm_op_ffn_op", "pfm_op_ffn_op_qkv", "pfm_op_ffn_dec", "pfm_op_fsmn_bf16", "pfm_op_layernorm_bf16",
                "pfm_profile_read", "pfm_streams_create", "pfm_streams_reset", "pfm_stream_step", "pfm_stream_step_beam",
                "pfm_streams_destroy", "pfm_fbank_raw", "pfm_lfr_gather", "pfm_config_punc", "pfm_run_punc", "pfm_vad_config_default", "pfm_vad_create",
-               "pfm_vad_set_weight", "pfm_vad_missing_weights", "pfm_vad_reset", "pfm_vad_run", "pfm_vad_destroy", "pfm_vad_fbank_raw",
+               "pfm_vad_set_weight", "pfm_vad_missing_weights", "pfm_vad_reset", "pfm_vad_run", "pfm_vad_destroy", "pfm_vad_fbank_raw", "pfm_vad_frame_energy", "pfm_run_punc_host",
                "pfm_vad_opts_default", "pfm_vad_detector_create", "pfm_vad_detector_push", "pfm_vad_detector_destroy")
 
 
@@ -151,6 +151,8 @@ def load_library(path: Optional[str] = None) -> ctypes.CDLL:
     lib.pfm_vad_reset.argtypes = [vp, vp]
     lib.pfm_vad_run.argtypes = [vp, vp, f32p, i32, f32p, f32p]
     lib.pfm_vad_fbank_raw.argtypes = [vp, vp, f32p, i32p, i32, i32, f32p, i32]
+    lib.pfm_vad_frame_energy.argtypes = [vp, vp, f32p, i32, i32, i32, f32p]
+    lib.pfm_run_punc_host.argtypes = [vp, vp, i32, vp, i32, vp]
     lib.pfm_vad_opts_default.argtypes = [ctypes.POINTER(PfmVadOpts)]
     lib.pfm_vad_opts_default.restype = None
     lib.pfm_vad_detector_create.argtypes = [ctypes.POINTER(PfmVadOpts), ctypes.POINTER(vp)]
@@ -359,6 +361,19 @@ class PfmEngine:
         check(self.lib.pfm_run_punc(self.h, _stream_ptr(torch, dev), m, _ptr(ids), _ptr(lens), B, T, _ptr(punc),
                                     _ptr(logits)), "pfm_run_punc")
         return dict(punc=punc, logits=logits)
+
+    def run_punc_host(self, ids: np.ndarray, mode="exact") -> np.ndarray:
+        """One word-id sequence (host int32 [n]) -> host labels [n] (pfm_run_punc_host: one C call, pinned staging)."""
+        if not isinstance(self.cfg, CTTransformerConfig):
+            raise PfmError("run_punc_host needs a CT-Transformer engine")
+        a = np.ascontiguousarray(np.asarray(ids, dtype=np.int32).reshape(-1))
+        out = np.empty_like(a)
+        if a.size == 0:
+            return out
+        dev = self.torch.device("cuda", self.device)
+        check(self.lib.pfm_run_punc_host(self.h, _stream_ptr(self.torch, dev), self._mode(mode), a.ctypes.data,
+                                         int(a.size), out.ctypes.data), "pfm_run_punc_host")
+        return out
 
     def run_ctc(self, feats, lens, query, mode="exact", ban_token: int = -1, L_cap: Optional[int] = None,
                 want_enc=False, want_frames=False):
@@ -798,6 +813,22 @@ class PfmVad:
     def reset(self):
         dev = self.torch.device("cuda", self.device)
         check(self.lib.pfm_vad_reset(self.h, _stream_ptr(self.torch, dev)), "pfm_vad_reset")
+
+    def frame_energy(self, wav, frame_len: int = 400, frame_shift: int = 160) -> np.ndarray:
+        """ComputeDecibel's per-frame energies of a host waveform chunk (pfm_vad_frame_energy: numpy's float32 pairwise
+        sum of the squared samples, bit for bit) -> host f32 [frames]."""
+        torch = self.torch
+        dev = torch.device("cuda", self.device)
+        w = np.ascontiguousarray(np.asarray(wav, np.float32).reshape(-1))
+        n = w.shape[0]
+        nf = (n - frame_len) // frame_shift + 1 if n >= frame_len else 0
+        if nf <= 0:
+            return np.zeros((0,), np.float32)
+        wd = torch.from_numpy(w).to(dev)
+        e = torch.empty((nf,), dtype=torch.float32, device=dev)
+        check(self.lib.pfm_vad_frame_energy(self.h, _stream_ptr(torch, dev), _ptr(wd), n, frame_len, frame_shift, _ptr(e)),
+              "pfm_vad_frame_energy")
+        return e.cpu().numpy()
 
     def fbank_raw(self, wav, nsamp_host):
         """Raw fbank frames [B, N_cap, 80] of the VAD's online frontend (pfm_vad_fbank_raw)."""

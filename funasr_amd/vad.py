@@ -378,14 +378,20 @@ class FsmnVADStreaming(HipModel):
         eng = self.engine()
         det = cache["detector"]          # native state machine (pfm_vad_detector)
         dbc: VadDetector = cache["db_calc"]
+        fl_s = int(dbc.o["frame_length_ms"] * dbc.o["sample_rate"] / 1000)
+        fs_s = int(dbc.frame_ms * dbc.o["sample_rate"] / 1000)
         segments: List[List[int]] = []
         for i in range(n):
             fin = is_final and i == n - 1
             seg = audio[i * stride:(i + 1) * stride]
             feats = fe.step(eng, [(seg, fin, cache["frontend"])])[0]
             wv = cache["frontend"].get("waveforms")
-            # ComputeDecibel in numpy float32, as the reference
-            db_new = dbc.frame_decibels(wv).astype(np.float64) if wv is not None else np.zeros((0,))
+            # ComputeDecibel: the frame energies on the device (numpy's float32 summation order), the log in numpy
+            # float32 as the reference (dbc.frame_decibels is the host statement of the same values)
+            if wv is not None and len(wv) >= fl_s:
+                db_new = (10 * np.log10(eng.frame_energy(wv, fl_s, fs_s) + 0.000001)).astype(np.float64)
+            else:
+                db_new = np.zeros((0,))
             p = eng.run(feats).cpu().numpy() if feats.shape[0] else np.zeros((0,), np.float32)
             segments.extend(det.push(db_new, p, fin, streaming))
         cache["prev_samples"] = audio[:-m] if m else audio[:0]

@@ -204,6 +204,11 @@ void pfm_config_punc(pfm_config* c);   /* the released punc_ct-transformer (voca
 int pfm_run_punc(pfm_handle* h, void* stream, int mode, const int32_t* ids, const int32_t* lens, int B, int T,
                  int32_t* punc, float* logits);
 
+/* One mini-sentence with HOST word ids [n] in and HOST labels [n] out (CTTransformer.punc_forward as the text loop
+ * calls it, model.py:277-316): the ids go to the handle's device buffers through pinned staging, pfm_run_punc runs,
+ * the labels come back; synchronises `stream`. */
+int pfm_run_punc_host(pfm_handle* h, void* stream, int mode, const int32_t* ids, int n, int32_t* punc);
+
 /* ---- FSMN-VAD (fsmn_vad_streaming/encoder.py:200-279; model.py:350-360 ComputeScores) ----
  * One pfm_vad object = the FSMN encoder of one stream with its per-layer memory caches in HBM
  * (cache["encoder"]); the VAD state machine (model.py:493-916) runs on the host over the posteriors. */
@@ -240,6 +245,13 @@ int pfm_vad_detector_create(const pfm_vad_opts* o, pfm_vad_detector** out);
 int pfm_vad_detector_push(pfm_vad_detector* d, const double* decibel, int n_db, const float* p_sil, int n,
                           int is_final, int streaming, int32_t* segs, int cap, int32_t* n_segs);
 void pfm_vad_detector_destroy(pfm_vad_detector* d);
+
+/* ComputeDecibel's frame energies (fsmn_vad_streaming/model.py:326-348) of one waveform chunk: energy[f] =
+ * sum_i wav[f * frame_shift + i]^2 over frame_len samples, f < (nsamp - frame_len) / frame_shift + 1, in float32 with
+ * numpy's pairwise summation order (the values the reference's np.sum gives, bit for bit); the caller takes
+ * 10 log10(energy + 1e-6). wav [nsamp] f32 device, energy [frames] f32 device out. frame_len <= 2048. */
+int pfm_vad_frame_energy(pfm_vad* v, void* stream, const float* wav, int nsamp, int frame_len, int frame_shift,
+                         float* energy);
 
 /* pfm_fbank_raw on the VAD object (its online frontend runs without a model handle). */
 int pfm_vad_fbank_raw(pfm_vad* v, void* stream, const float* wav, const int32_t* nsamp, int B, int S_max,

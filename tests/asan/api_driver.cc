@@ -98,6 +98,7 @@ static void validation() {
                            nullptr), "run_beam null handle");
     expect_err(pfm_run_ctc(nullptr, nullptr, 0, f4, &i1, 1, 1, tok, -1, tok, 4, tok, nullptr, nullptr), "run_ctc null handle");
     expect_err(pfm_run_punc(nullptr, nullptr, 0, tok, &i1, 1, 1, tok, nullptr), "run_punc null handle");
+    expect_err(pfm_run_punc_host(nullptr, nullptr, 0, tok, 1, tok), "run_punc_host null handle");
     expect_err(pfm_ctc_align(nullptr, nullptr, f4, 1, 5, &i1, tok, 1, &i1, 0, tok), "ctc_align null");
     expect_err(pfm_profile(nullptr, 1), "profile null");
     double d;
@@ -164,6 +165,7 @@ static void vad_validation() {
     expect(pfm_vad_missing_weights(nullptr) == -1, "vad_missing null");
     expect_err(pfm_vad_reset(nullptr, nullptr), "vad_reset null");
     expect_err(pfm_vad_run(nullptr, nullptr, f4, 1, f4, nullptr), "vad_run null");
+    expect_err(pfm_vad_frame_energy(nullptr, nullptr, f4, 4, 400, 160, f4), "vad_frame_energy null");
     pfm_vad_destroy(nullptr);
     pfm_vad_opts o;
     pfm_vad_opts_default(&o);

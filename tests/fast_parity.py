@@ -95,14 +95,14 @@ def bounds_from_emulation(em: dict) -> dict:
     output: the GPU must sit at the emulation's level -- flips within 3 points, mean regret within 1.5x (+0.001 nat),
     choices outside the reference top 5 within 2x (at least 0.2 % of the positions), the largest regret within
     0.15 nat, equal token counts within 5 points; the positions count-mismatched utterances lose at their alignment
-    breaks within 2x (+1 point), and the regret at a break and over every position within 0.3 nat of the emulation's."""
+    breaks within 2x (+2 points, about half an utterance at B = 24), and the regret at a break and over every position within 0.3 nat of the emulation's."""
     pos = max(1, em["positions"])
     b = dict(flip_frac=em["flip_frac"] + 0.03, mean_regret=1.5 * em["mean_regret"] + 0.001,
              outside_frac=max(2.0 * em["outside_topk"] / pos, 0.002), max_regret=em["max_regret"] + 0.15,
              equal_counts=em["equal_counts"] - 0.05)
     if "trunc_frac" in em:   # the positions count-mismatched utterances lose at their breaks, bounded too
         # a break is a decision too: bounded from the larger of the emulation's break and decision regrets
-        b.update(trunc_frac=2.0 * em["trunc_frac"] + 0.01,
+        b.update(trunc_frac=2.0 * em["trunc_frac"] + 0.02,
                  break_max_regret=max(em["break_max_regret"], em["max_regret"]) + 0.3,
                  max_regret_all=em["max_regret_all"] + 0.3)
     return b

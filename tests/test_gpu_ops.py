@@ -452,7 +452,7 @@ def _dec_ffn_ref(x1, p, eps=1e-12):
     return y, exact
 
 
-@pytest.mark.parametrize("kernel", ["1", "2"])
+@pytest.mark.parametrize("kernel", ["1", "2", "3"])
 @pytest.mark.parametrize("M", [64, 200, 1000, 4100])
 @pytest.mark.parametrize("outproj", [False, True])
 def test_ffn_fused_decoder(dev, monkeypatch, M, outproj, kernel):

@@ -131,3 +131,29 @@ def test_automodel_vad_asr_punc_pipeline_vs_reference(name):
     # frontends are the reference's compiled kaldi-native-fbank (make_golden.py _patch_kaldi_fbank_knf), which
     # pfm_fbank reproduces to float rounding (test_gpu_frontend.py), so wav -> text is asserted end to end.
     assert res[0]["text"] == want, (res[0]["text"], want)
+
+
+def test_frame_energy_bit_identical_to_numpy(vad):
+    """pfm_vad_frame_energy (ComputeDecibel's frame energies on the device, fsmn_vad_streaming/model.py:326-348)
+    equals numpy's float32 np.sum(np.square(frames), axis=1) bit for bit -- numpy's pairwise summation order --
+    on speech-like, silent, loud, tiny and odd-length chunks, and the decibels the VAD derives from them equal the
+    host statement's (VadDetector.frame_decibels, the reference's numpy code)."""
+    from funasr_amd.vad import VadDetector
+    _, v, _, _ = vad
+    rng = np.random.default_rng(11)
+    waves = [vad_waveform(61, 7.3, [(1.0, 2.5), (4.0, 4.4)]),
+             np.zeros(16000, np.float32),
+             (rng.standard_normal(48000) * 0.9).astype(np.float32),
+             (rng.standard_normal(20011) * 1e-4).astype(np.float32),
+             rng.uniform(-1, 1, 399).astype(np.float32),
+             rng.uniform(-1, 1, 400).astype(np.float32),
+             rng.uniform(-1, 1, 963).astype(np.float32)]
+    det = VadDetector(dict(fsmn_vad().vad_opts))
+    for w in waves:
+        fr = np.lib.stride_tricks.sliding_window_view(w, 400)[::160] if len(w) >= 400 else np.zeros((0, 400), np.float32)
+        want = np.sum(np.square(fr), axis=1).astype(np.float32)
+        got = v.frame_energy(w)
+        assert got.dtype == np.float32 and got.shape == want.shape
+        assert np.array_equal(got.view(np.int32), want.view(np.int32)), len(w)
+        db = 10 * np.log10(got + 0.000001)
+        assert np.array_equal(db, det.frame_decibels(w))
