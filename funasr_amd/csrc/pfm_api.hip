@@ -245,6 +245,7 @@ void pfm_knobs_refresh() {
     k.kv_overlap = iv("PFM_KV_OVERLAP", 1) != 0;
     k.subbatch = std::max(1, std::min(iv("PFM_SUBBATCH", 2), 4));
     k.stream_graph = iv("PFM_STREAM_GRAPH", 1) != 0;
+    k.punc_graph = iv("PFM_PUNC_GRAPH", 1) != 0;
     k.gemm_gm = iv("PFM_GEMM_GM", -1);
     k.gemm_cfg = iv("PFM_GEMM_CFG", 0);
     k.gemm_st16 = iv("PFM_GEMM_ST16", 1) != 0;
@@ -296,6 +297,28 @@ struct DevBuf {
         return e;
     }
     template <typename T> T* as() const { return (T*)p; }
+};
+
+// Captured HIP graphs of one owner's launch sequences, keyed by (shape..., knob signature). At most MAX execs
+// are kept; the least recently replayed one is evicted (a server's active-stream and token counts vary without
+// bound). A graph is valid while its owner's workspace generation is the one it was captured at.
+struct GraphCache {
+    struct Graph {
+        hipGraphExec_t exec = nullptr;
+        unsigned long long gen = 0, last_use = 0;
+        int seen = 0;
+        bool bad = false;
+    };
+    static constexpr size_t MAX = 64;
+    std::map<std::array<unsigned long long, 5>, Graph> graphs;
+    unsigned long long use_clock = 0;
+    GraphCache() = default;
+    GraphCache(const GraphCache&) = delete;
+    GraphCache& operator=(const GraphCache&) = delete;
+    ~GraphCache() {
+        for (auto& kv : graphs)
+            if (kv.second.exec) (void)hipGraphExecDestroy(kv.second.exec);
+    }
 };
 
 // One registry entry per reference state_dict tensor we consume.
@@ -374,6 +397,9 @@ struct pfm_handle {
     DevBuf punc_io;                // pfm_run_punc_host: device ids | lens | punc of one call
     int32_t* punc_pin = nullptr;   // ... and their pinned host staging
     int punc_cap = 0;
+    hipStream_t punc_st = nullptr;   // ... its work stream (graph capture needs a non-null stream) and entry event
+    hipEvent_t punc_ev = nullptr;
+    GraphCache punc_graphs;          // ... and one HIP graph of the model's launches per (mode, word count)
     // encoder sub-batch streams: the batch is split into NSUB utterance groups whose layer sequences run
     // concurrently, so one group's HBM-bound phases (LayerNorm, GEMM epilogues, attention) overlap the
     // other's MFMA main loops
@@ -1495,6 +1521,8 @@ void pfm_destroy(pfm_handle* h) {
     if (h->ev_fork) (void)hipEventDestroy(h->ev_fork);
     if (h->host_ntok) (void)hipHostFree(h->host_ntok);
     if (h->punc_pin) (void)hipHostFree(h->punc_pin);
+    if (h->punc_st) (void)hipStreamDestroy(h->punc_st);
+    if (h->punc_ev) (void)hipEventDestroy(h->punc_ev);
     delete h;
 }
 
@@ -2076,23 +2104,69 @@ int pfm_run_ctc(pfm_handle* h, void* stream, int mode, const float* feats, const
     return PFM_OK;
 }
 
-int pfm_run_punc(pfm_handle* h, void* stream, int mode, const int32_t* ids, const int32_t* lens, int B, int T,
-                 int32_t* punc, float* logits) {
-    pfm_knobs_refresh();
-    if (!h || !ids || !lens || !punc) return fail(PFM_E_ARG, "pfm_run_punc: null argument");
-    if (h->cfg.arch != PFM_ARCH_PUNC) return fail(PFM_E_STATE, "pfm_run_punc: handle is not a punctuation model");
-    if (B < 1 || T < 1) return fail(PFM_E_ARG, "pfm_run_punc: bad sizes");
-    if (mode != PFM_MODE_EXACT && mode != PFM_MODE_FAST) return fail(PFM_E_ARG, "pfm_run_punc: bad mode");
-    if (h->missing) return fail(PFM_E_STATE, "pfm_run_punc: weights not set");
+// Run `body` on `st`, through a HIP graph of its launches when `use`: the first call of a shape runs eagerly
+// (one-time launcher setup happens there), the second captures and every later one replays. A graph is rebuilt
+// when the owner's workspace generation `gen()` moved since its capture; graphs are keyed by the calling
+// thread's knob snapshot as well. `st` must not be the legacy null stream (it cannot be captured).
+extern "C++" {
+template <class G, class F>
+int graphed(GraphCache& gc, const char* tag, std::array<int, 4> shape, bool use, hipStream_t st, G&& gen_of,
+            F&& body) {
+    if (!use) return body(st);
+    const std::array<unsigned long long, 5> key = {(unsigned long long)shape[0], (unsigned long long)shape[1],
+                                                   (unsigned long long)shape[2], (unsigned long long)shape[3],
+                                                   pfm_knobs().sig};
+    if (!gc.graphs.count(key) && gc.graphs.size() >= GraphCache::MAX) {   // evict the LRU entry
+        auto lru = gc.graphs.begin();
+        for (auto it = gc.graphs.begin(); it != gc.graphs.end(); ++it)
+            if (it->second.last_use < lru->second.last_use) lru = it;
+        if (lru->second.exec) (void)hipGraphExecDestroy(lru->second.exec);
+        gc.graphs.erase(lru);
+    }
+    auto& g = gc.graphs[key];
+    g.last_use = ++gc.use_clock;
+    const unsigned long long gen = gen_of();
+    static const bool log = getenv("PFM_STREAM_GRAPH_LOG") != nullptr;
+    if (log)
+        fprintf(stderr, "[%s graph] key %d/%d/%d/%d %s gen %llu/%llu seen %d (%zu graphs)\n", tag, shape[0], shape[1],
+                shape[2], shape[3], g.exec && g.gen == gen ? "replay" : (g.bad || g.seen == 0 ? "eager" : "capture"),
+                g.gen, gen, g.seen, gc.graphs.size());
+    if (g.exec && g.gen == gen) {
+        HIP_TRY(hipGraphLaunch(g.exec, st));
+        return PFM_OK;
+    }
+    if (g.exec) { (void)hipGraphExecDestroy(g.exec); g.exec = nullptr; }
+    if (g.bad || g.seen++ == 0) return body(st);
+    HIP_TRY(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
+    const int rc = body(st);
+    hipGraph_t graph = nullptr;
+    const hipError_t e = hipStreamEndCapture(st, &graph);
+    if (rc != PFM_OK || e != hipSuccess || gen_of() != gen) {   // run this call eagerly instead
+        if (graph) (void)hipGraphDestroy(graph);
+        (void)hipGetLastError();
+        if (rc != PFM_OK) return rc;
+        g.bad = e != hipSuccess;   // not capturable: this shape stays eager
+        return body(st);
+    }
+    const hipError_t ei = hipGraphInstantiate(&g.exec, graph, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(graph);
+    if (ei != hipSuccess) {
+        g.exec = nullptr;
+        g.bad = true;
+        (void)hipGetLastError();
+        return body(st);
+    }
+    g.gen = gen;
+    HIP_TRY(hipGraphLaunch(g.exec, st));
+    return PFM_OK;
+}
+}  // extern "C++"
+
+// CTTransformer.punc_forward's model (ct_transformer/model.py:70-79 forward): embedding * sqrt(d) + PE, the
+// SAN-M blocks, after_norm, the punctuation head and its argmax; workspace reserved and weights converted already
+static int punc_body(pfm_handle* h, hipStream_t st, bool fast, const int32_t* ids, const int32_t* lens, int B, int T,
+                     int32_t* punc, float* logits) {
     const pfm_config& c = h->cfg;
-    CHECK_DEV("pfm_run_punc", h->device, {"ids", ids}, {"lens", lens}, {"punc", punc}, {"logits", logits});
-    HIP_TRY(hipSetDevice(h->device));
-    hipStream_t st = (hipStream_t)stream;
-    const bool fast = mode == PFM_MODE_FAST;
-    int rc = reserve(h, B, T);
-    if (rc) return rc;
-    if (fast) { rc = ensure_bf16(h, st); if (rc) return rc; }
-    else { rc = ensure_x6(h, st); if (rc) return rc; }
     const int D = c.d_model;
     float* X = h->X.as<float>();
     // X = embed[ids] * sqrt(d) + PE: the encoder input AND layer 0's residual (input_size == d_model)
@@ -2102,22 +2176,56 @@ int pfm_run_punc(pfm_handle* h, void* stream, int mode, const int32_t* ids, cons
     run.raw_input = true;
     const FinalLN fin = {h->an_g, h->an_b, h->Xf.as<float>(), rowmap_plain(D), DT_F32, nullptr, rowmap_plain(D),
                          DT_BF16};
-    rc = encoder_stack(run, X, lens, B, T, 0, c.enc_blocks, X, fin, enc_ws(h, 0));
+    const int rc = encoder_stack(run, X, lens, B, T, 0, c.enc_blocks, X, fin, enc_ws(h, 0));
     if (rc) return rc;
     HIP_TRY(pfm_punc_head(h->Xf.as<float>(), B, T, lens, h->w(h->ctc_w), h->w(h->ctc_b), c.vocab_size, D, punc,
                           logits, st));
     return PFM_OK;
 }
 
+static int punc_prepare(pfm_handle* h, hipStream_t st, bool fast, int B, int T) {
+    int rc = reserve(h, B, T);
+    if (rc) return rc;
+    return fast ? ensure_bf16(h, st) : ensure_x6(h, st);
+}
+
+int pfm_run_punc(pfm_handle* h, void* stream, int mode, const int32_t* ids, const int32_t* lens, int B, int T,
+                 int32_t* punc, float* logits) {
+    pfm_knobs_refresh();
+    if (!h || !ids || !lens || !punc) return fail(PFM_E_ARG, "pfm_run_punc: null argument");
+    if (h->cfg.arch != PFM_ARCH_PUNC) return fail(PFM_E_STATE, "pfm_run_punc: handle is not a punctuation model");
+    if (B < 1 || T < 1) return fail(PFM_E_ARG, "pfm_run_punc: bad sizes");
+    if (mode != PFM_MODE_EXACT && mode != PFM_MODE_FAST) return fail(PFM_E_ARG, "pfm_run_punc: bad mode");
+    if (h->missing) return fail(PFM_E_STATE, "pfm_run_punc: weights not set");
+    CHECK_DEV("pfm_run_punc", h->device, {"ids", ids}, {"lens", lens}, {"punc", punc}, {"logits", logits});
+    HIP_TRY(hipSetDevice(h->device));
+    hipStream_t st = (hipStream_t)stream;
+    const bool fast = mode == PFM_MODE_FAST;
+    const int rc = punc_prepare(h, st, fast, B, T);
+    if (rc) return rc;
+    return punc_body(h, st, fast, ids, lens, B, T, punc, logits);
+}
+
 // One mini-sentence of the CT-Transformer text loop with host word ids in and host labels out (the per-call form
-// CTTransformer.punc_forward is used in, model.py:277-316): one pinned staging copy each way and pfm_run_punc on the
-// handle's own device buffers, so a caller's sequential loop costs one C call per sentence.
+// CTTransformer.punc_forward is used in, model.py:277-316): one pinned staging copy each way around the model on
+// the handle's own device buffers, so a caller's sequential loop costs one C call per sentence. The model's ~35
+// launches are replayed from a HIP graph per (mode, word count) from the second call of a count on (the loop's
+// counts repeat: 20 new words plus the carried tail), on the handle's own stream, ordered after the caller's
+// queued work by one event; the call returns with that stream drained.
 int pfm_run_punc_host(pfm_handle* h, void* stream, int mode, const int32_t* ids, int n, int32_t* punc) {
     pfm_knobs_refresh();
     if (!h || !ids || !punc || n < 1) return fail(PFM_E_ARG, "pfm_run_punc_host: null argument or n < 1");
     if (h->cfg.arch != PFM_ARCH_PUNC) return fail(PFM_E_STATE, "pfm_run_punc_host: handle is not a punctuation model");
+    if (mode != PFM_MODE_EXACT && mode != PFM_MODE_FAST) return fail(PFM_E_ARG, "pfm_run_punc_host: bad mode");
+    if (h->missing) return fail(PFM_E_STATE, "pfm_run_punc_host: weights not set");
     HIP_TRY(hipSetDevice(h->device));
-    hipStream_t st = (hipStream_t)stream;
+    if (!h->punc_st) {
+        HIP_TRY(hipStreamCreateWithFlags(&h->punc_st, hipStreamNonBlocking));
+        HIP_TRY(hipEventCreateWithFlags(&h->punc_ev, hipEventDisableTiming));
+    }
+    HIP_TRY(hipEventRecord(h->punc_ev, (hipStream_t)stream));
+    HIP_TRY(hipStreamWaitEvent(h->punc_st, h->punc_ev, 0));
+    hipStream_t st = h->punc_st;
     if (h->punc_cap < n) {
         const int cap = std::max(n, 256);
         if (h->punc_pin) { HIP_TRY(hipStreamSynchronize(st)); HIP_TRY(hipHostFree(h->punc_pin)); h->punc_pin = nullptr; }
@@ -2125,12 +2233,17 @@ int pfm_run_punc_host(pfm_handle* h, void* stream, int mode, const int32_t* ids,
         HIP_TRY(h->punc_io.ensure((size_t)(2 * cap + 1) * sizeof(int32_t)));
         h->punc_cap = cap;
     }
+    const bool fast = mode == PFM_MODE_FAST;
+    int rc = punc_prepare(h, st, fast, 1, n);
+    if (rc) return rc;
     int32_t* pin = h->punc_pin;
     memcpy(pin, ids, (size_t)n * sizeof(int32_t));
     pin[n] = n;
     int32_t* dio = h->punc_io.as<int32_t>();
     HIP_TRY(hipMemcpyAsync(dio, pin, (size_t)(n + 1) * sizeof(int32_t), hipMemcpyHostToDevice, st));
-    const int rc = pfm_run_punc(h, stream, mode, dio, dio + n, 1, n, dio + n + 1, nullptr);
+    const bool use = pfm_knobs().punc_graph && !h->prof_on;
+    rc = graphed(h->punc_graphs, "punc", {mode, n, 0, 0}, use, st, [h] { return h->buf_gen.load(); },
+                 [&](hipStream_t s) { return punc_body(h, s, fast, dio, dio + n, 1, n, dio + n + 1, nullptr); });
     if (rc) return rc;
     HIP_TRY(hipMemcpyAsync(pin + n + 1, dio + n + 1, (size_t)n * sizeof(int32_t), hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
@@ -2621,18 +2734,9 @@ struct pfm_streams {
     int32_t* hntok = nullptr;
     int hntok_cap = 0;
     DevBuf fin, tok;                    // chunk rows [n][maxn][I] (graph-stable copy), tokens [n][L_cap]
-    // HIP graphs of the two launch sequences of a step (encoder + CIF; decoder), keyed by shape
-    // key: (phase, n, maxn, L * 4096 + L_cap, knob signature); at most MAX_GRAPHS execs are kept, the least
-    // recently replayed one is evicted (a server's active-stream and token counts vary without bound)
-    struct Graph {
-        hipGraphExec_t exec = nullptr;
-        unsigned long long gen = 0, last_use = 0;
-        int seen = 0;
-        bool bad = false;
-    };
-    static constexpr size_t MAX_GRAPHS = 64;
-    std::map<std::array<unsigned long long, 5>, Graph> graphs;
-    unsigned long long use_clock = 0;
+    // HIP graphs of the two launch sequences of a step (encoder + CIF; decoder),
+    // key: (phase, n, maxn, L * 4096 + L_cap, knob signature)
+    GraphCache gc;
     hipStream_t cap = nullptr;          // work stream of every step: eager launches, graph capture and replay
     hipEvent_t ev_in = nullptr;
     GenUnbind gen_unbind_;
@@ -2640,8 +2744,6 @@ struct pfm_streams {
     unsigned long long gen() const { return h->buf_gen.load() + buf_gen.load(); }
     ~pfm_streams() {
         if (ev_in) (void)hipEventDestroy(ev_in);
-        for (auto& kv : graphs)
-            if (kv.second.exec) (void)hipGraphExecDestroy(kv.second.exec);
         if (cap) (void)hipStreamDestroy(cap);
         if (hprm) (void)hipHostFree(hprm);
     }
@@ -2802,59 +2904,9 @@ int stream_decoder(pfm_streams* s, const Run& r, int n, int Tw, int L, const SPr
     return PFM_OK;
 }
 
-// Run `body` on `st`, through a HIP graph of its launches when `use`: the first step of a shape runs eagerly
-// (one-time launcher setup happens there), the second captures on the object's capture stream and every
-// later one replays. A graph is rebuilt when the handle's or the streams object's workspace was reallocated
-// since its capture; graphs are keyed by the calling thread's knob snapshot as well.
 template <class F>
 int stream_graphed(pfm_streams* s, std::array<int, 4> shape, bool use, hipStream_t st, F&& body) {
-    if (!use) return body(st);
-    const std::array<unsigned long long, 5> key = {(unsigned long long)shape[0], (unsigned long long)shape[1],
-                                                   (unsigned long long)shape[2], (unsigned long long)shape[3],
-                                                   pfm_knobs().sig};
-    if (!s->graphs.count(key) && s->graphs.size() >= pfm_streams::MAX_GRAPHS) {   // evict the LRU entry
-        auto lru = s->graphs.begin();
-        for (auto it = s->graphs.begin(); it != s->graphs.end(); ++it)
-            if (it->second.last_use < lru->second.last_use) lru = it;
-        if (lru->second.exec) (void)hipGraphExecDestroy(lru->second.exec);
-        s->graphs.erase(lru);
-    }
-    auto& g = s->graphs[key];
-    g.last_use = ++s->use_clock;
-    const unsigned long long gen = s->gen();
-    static const bool log = getenv("PFM_STREAM_GRAPH_LOG") != nullptr;
-    if (log)
-        fprintf(stderr, "[stream graph] key %d/%d/%d/%d %s gen %llu/%llu seen %d (%zu graphs)\n", shape[0], shape[1],
-                shape[2], shape[3], g.exec && g.gen == gen ? "replay" : (g.bad || g.seen == 0 ? "eager" : "capture"),
-                g.gen, gen, g.seen, s->graphs.size());
-    if (g.exec && g.gen == gen) {
-        HIP_TRY(hipGraphLaunch(g.exec, st));
-        return PFM_OK;
-    }
-    if (g.exec) { (void)hipGraphExecDestroy(g.exec); g.exec = nullptr; }
-    if (g.bad || g.seen++ == 0) return body(st);
-    HIP_TRY(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
-    const int rc = body(st);
-    hipGraph_t graph = nullptr;
-    const hipError_t e = hipStreamEndCapture(st, &graph);
-    if (rc != PFM_OK || e != hipSuccess || s->gen() != gen) {   // run this step eagerly instead
-        if (graph) (void)hipGraphDestroy(graph);
-        (void)hipGetLastError();
-        if (rc != PFM_OK) return rc;
-        g.bad = e != hipSuccess;   // not capturable: this shape stays eager
-        return body(st);
-    }
-    const hipError_t ei = hipGraphInstantiate(&g.exec, graph, nullptr, nullptr, 0);
-    (void)hipGraphDestroy(graph);
-    if (ei != hipSuccess) {
-        g.exec = nullptr;
-        g.bad = true;
-        (void)hipGetLastError();
-        return body(st);
-    }
-    g.gen = gen;
-    HIP_TRY(hipGraphLaunch(g.exec, st));
-    return PFM_OK;
+    return graphed(s->gc, "stream", shape, use, st, [s] { return s->gen(); }, std::forward<F>(body));
 }
 
 int streams_zero(pfm_streams* s, hipStream_t st, int slot) {

@@ -132,6 +132,7 @@ struct PfmKnobs {
     int kv_overlap;         // PFM_KV_OVERLAP (default 1): memory K|V projection on the side stream
     int subbatch;           // PFM_SUBBATCH (default 2): concurrent encoder utterance groups
     int stream_graph;       // PFM_STREAM_GRAPH (default 1): streaming steps through HIP graphs
+    int punc_graph;         // PFM_PUNC_GRAPH (default 1): pfm_run_punc_host's model launches through HIP graphs
     int gemm_gm;            // PFM_GEMM_GM: grouped tile order override (-1 = default)
     int gemm_cfg;           // PFM_GEMM_CFG: forced tile configuration (0 = policy)
     int gemm_st16;          // PFM_GEMM_ST16 (default 1): 16-B bf16 epilogue stores
@@ -155,6 +156,6 @@ struct PfmKnobs {
                             // +3-5 % step; 15: 5 %, +9 %)
     unsigned long long sig;
 };
-#define PFM_KNOB_FIELDS 18
+#define PFM_KNOB_FIELDS 19
 const PfmKnobs& pfm_knobs();   // the calling thread's snapshot (refreshed lazily if no entry point did yet)
 void pfm_knobs_refresh();

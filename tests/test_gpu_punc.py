@@ -124,3 +124,36 @@ def test_punc_bad_args(tiny):
     cfg, e, _ = tiny
     with pytest.raises(PfmError):
         e.run_punc(torch.zeros((2, 4), dtype=torch.int32).cuda(), torch.tensor([4], dtype=torch.int32).cuda())
+
+
+@pytest.mark.parametrize("mode", ["exact", "fast"])
+def test_punc_host_graph_replay_matches_device_path(mode):
+    """pfm_run_punc_host replays one HIP graph per (mode, word count) from a count's second call on: the first
+    (eager), second (capture) and later (replay) calls of every count, interleaved, equal pfm_run_punc's labels
+    on device operands; after new weights are loaded, the replayed graphs follow them."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    cfg = ct_transformer()
+    e = PfmEngine(cfg, 0)
+    e.load_state_dict(make_weights(cfg, seed=0))
+    rng = np.random.default_rng(11)
+    seqs = [rng.integers(3, cfg.vocab_size, n).astype(np.int32) for n in (20, 27, 33, 20, 41)]
+
+    def device(x):
+        r = e.run_punc(torch.from_numpy(x[None]).cuda(), torch.tensor([len(x)], dtype=torch.int32).cuda(), mode=mode)
+        torch.cuda.synchronize()
+        return r["punc"][0].cpu().numpy()
+
+    for weights_seed in (0, 1):
+        if weights_seed:
+            e.load_state_dict(make_weights(cfg, seed=weights_seed))
+        want = [device(x) for x in seqs]
+        for rep in range(3):
+            for x, wv in zip(seqs, want):
+                got = e.run_punc_host(x, mode=mode)
+                assert np.array_equal(got, wv), (weights_seed, rep, len(x))
+    os.environ["PFM_PUNC_GRAPH"] = "0"
+    try:
+        assert all(np.array_equal(e.run_punc_host(x, mode=mode), wv) for x, wv in zip(seqs, want))
+    finally:
+        del os.environ["PFM_PUNC_GRAPH"]
