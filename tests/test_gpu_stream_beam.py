@@ -240,21 +240,34 @@ def test_stream_beam_large_exact_vs_reference(eng_large):
 
 
 def test_stream_beam_large_fast_close(eng_large):
-    """The same chunks in fast mode (bf16 operands): each chunk's best hypothesis scores within 0.5 of the reference's
-    best (log-prob units of the joint score; bf16 logits move it by O(0.1) per chunk) and agrees with the reference
-    1-best on >= 60 % of the positions overall; a 0.3-nat decoder bias perturbation, checked in
-    tests/test_gpu_parity.py, moves single positions by more than that."""
+    """The same chunks in fast mode (bf16 operands; the chunk path keeps plain bf16 weights), held to bounds derived
+    from the CPU emulation of plain bf16 rounding (tests/golden/fast_emul.json "G", tests/fast_parity.py
+    bounds_from_emulation), not from the kernel's own output: the 1-best's positions disagree with the reference's
+    1-best no more often than the emulation's flip bound; the best joint score (log-prob units: a sum over the
+    hypothesis' tokens) moves per token no more than the emulation's mean-regret bound, and in any chunk by less than
+    0.5 (tighter than the emulation's single-decision bound, max_regret + 0.15). A 0.3-nat decoder bias perturbation,
+    checked in tests/test_gpu_parity.py, moves single positions by more than that."""
+    import json
+    from tests.fast_parity import bounds_from_emulation
     cfg, e = eng_large
     g = np.load(f"{GOLD}/stream_beam_large.npz")
+    em = json.load(open(f"{GOLD}/fast_emul.json", encoding="utf-8"))["para_large_b64"]["G"]
+    b = bounds_from_emulation(em)
     got = _large_chunks(e, "fast", g)
-    agree, tot, worst = 0, 0, 0.0
+    agree, tot, worst, gap, ntok = 0, 0, 0.0, 0.0, 0
     for i, (hyps, scores) in enumerate(got):
         want, wsc = _large_want(g, i)
         assert hyps, i
-        worst = max(worst, abs(float(scores[0]) - float(wsc[0])))
-        a, b = hyps[0], want[0]
-        tot += max(len(a), len(b))
-        agree += sum(int(x == y) for x, y in zip(a, b))
-    print(f"stream beam large fast: 1-best position agreement {agree}/{tot}, largest best-score gap {worst:.3f}")
-    assert worst < 0.5
-    assert agree >= 0.6 * tot
+        d = abs(float(scores[0]) - float(wsc[0]))
+        worst = max(worst, d)
+        a, r = hyps[0], want[0]
+        tot += max(len(a), len(r))
+        agree += sum(int(x == y) for x, y in zip(a, r))
+        gap += d
+        ntok += max(1, len(r))
+        print(f"chunk {i}: {len(a)} / {len(r)} tokens, best-score gap {d:.4f}")
+    print(f"stream beam large fast: 1-best position agreement {agree}/{tot}, best-score gap per token {gap / ntok:.4f} "
+          f"(bound {b['mean_regret']:.4f}), largest {worst:.3f}; flip bound {b['flip_frac']:.3f}")
+    assert worst < min(0.5, b["max_regret"])
+    assert gap / ntok < b["mean_regret"]
+    assert agree >= (1.0 - b["flip_frac"]) * tot
