@@ -1,34 +1,29 @@
-"""Streaming (config C5) leg alone, for rocprofv3: S streams x C chunks of Paraformer-large streaming."""
-import argparse
-import os
-import sys
-import time
-
-import torch
-
+"""One Paraformer-large streaming stream (fast mode, chunk [0, 10, 5], look-back 4 / 1), 2 x 50 chunks (the second pass
+replays the captured HIP graphs), for a rocprofv3 kernel trace of the per-chunk launch chain:
+python tools/stream_prof.py [chunks] -> mean ms per chunk of the second pass."""
+import os, sys, time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from funasr_amd.config import paraformer_streaming  # noqa: E402
-from funasr_amd.runtime import PfmEngine, PfmStreams  # noqa: E402
-from funasr_amd.weights import make_weights  # noqa: E402
+import torch
+from funasr_amd.config import paraformer_streaming
+from funasr_amd.runtime import PfmEngine, PfmStreams
+from funasr_amd.weights import make_weights
 
-ap = argparse.ArgumentParser()
-ap.add_argument("--streams", type=int, default=1)
-ap.add_argument("--chunks", type=int, default=50)
-ap.add_argument("--mode", default="fast")
-a = ap.parse_args()
+C = int(sys.argv[1]) if len(sys.argv) > 1 else 50
 cfg = paraformer_streaming()
-e = PfmEngine(cfg, 0)
-e.load_state_dict(make_weights(cfg, 0))
-S, C = a.streams, a.chunks
-x = torch.randn((C, S, 10, cfg.input_size), device="cuda")
-st = PfmStreams(e, S, (0, 10, 5), 4, 1, a.mode)
-ids = list(range(S))
+eng = PfmEngine(cfg, 0)
+eng.load_state_dict(make_weights(cfg, 0))
+dev = torch.device("cuda", 0)
+g = torch.Generator(device=dev)
+g.manual_seed(2000)
+chunks = torch.randn((C, 1, 10, cfg.input_size), generator=g, device=dev, dtype=torch.float32)
+st = PfmStreams(eng, 1, (0, 10, 5), 4, 1, "fast")
 for rep in range(2):
-    st.reset(ids)
+    st.reset([0])
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for c in range(C):
-        r = st.step(ids, x[c], [10] * S, [c == C - 1] * S)
-        int(r["ntok"].sum())
+        r = st.step([0], chunks[c], [10], [c == C - 1])
+        int(r["ntok"].sum().item())
     torch.cuda.synchronize()
-    print(f"rep {rep}: {(time.perf_counter() - t0) / C * 1e3:.3f} ms/chunk", flush=True)
+    dt = time.perf_counter() - t0
+print(f"{dt / C * 1e3:.3f} ms per chunk", flush=True)
