@@ -411,7 +411,7 @@ def main():
     # WRITE_SIZE, separate runs of this bench, gfx950-corrected by tools/pmc_traffic.py); null when absent
     # and the class's MFMA-busy fraction from a third pass (SQ_VALU_MFMA_BUSY_CYCLES, GRBM_GUI_ACTIVE)
     traffic, traffic_src, busy, busy_src = None, None, None, None
-    tname = next((n for n in ("r05_pmc_bench.json", "r04_pmc_bench.json", "r03_gemm_traffic.json", "r02b_gemm_traffic.json")
+    tname = next((n for n in ("r06_pmc_bench.json", "r05_pmc_bench.json", "r04_pmc_bench.json", "r03_gemm_traffic.json", "r02b_gemm_traffic.json")
                   if os.path.exists(os.path.join(ROOT, "profiles", n))), None)
     if args.mode == "fast" and tname:
         with open(os.path.join(ROOT, "profiles", tname)) as f:
