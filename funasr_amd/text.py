@@ -70,8 +70,11 @@ class CharTokenizer:
         if tab is None:
             spec = np.array([t in _SPECIAL for t in self.token_list], bool)
             simple = np.array([(t in _SPECIAL) or (_zh_word(t) and " " not in t) for t in self.token_list], bool)
-            tab = self._pp_tab = (spec, simple)
-        spec, simple = tab
+            # one-character tokens as a '<U1' table: a row of them joins as one '<U{k}' view of its gathered codes
+            single = np.array([len(t) == 1 for t in self.token_list], bool)
+            u1 = np.array([t if len(t) == 1 else " " for t in self.token_list], dtype="<U1")
+            tab = self._pp_tab = (spec, simple, single, u1)
+        spec, simple, single, u1 = tab
         out = []
         tl = self.token_list
         for ids in rows:
@@ -79,7 +82,10 @@ class CharTokenizer:
             if a.size and bool(simple[a].all()):
                 kept = a[~spec[a]]
                 if kept.size:   # an all-special row is not "all Chinese" (len(mid) == 0): the general path
-                    out.append("".join([tl[i] for i in kept.tolist()]).strip())
+                    if bool(single[kept].all()):
+                        out.append(np.ascontiguousarray(u1[kept]).view(f"<U{kept.size}")[0].strip())
+                    else:
+                        out.append("".join([tl[i] for i in kept.tolist()]).strip())
                     continue
             out.append(sentence_postprocess(self.ids2tokens(ids))[0])
         return out
