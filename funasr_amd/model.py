@@ -168,6 +168,10 @@ class Paraformer(HipModel):
 
     def results_from_token_matrix(self, toks, ntok, key, tokenizer=None, **kwargs):
         """Greedy results from a (gathered) host token matrix, exactly as inference() builds them."""
+        if tokenizer is not None and hasattr(tokenizer, "postprocessed_texts_matrix"):
+            texts = tokenizer.postprocessed_texts_matrix(toks, ntok, (self.eos, self.sos, self.blank_id))
+            key = self._keys(key, len(texts))
+            return [{"key": key[i], "text": t} for i, t in enumerate(texts)]
         hyps = self._greedy_hyps(toks, ntok)
         key = self._keys(key, len(hyps))
         if tokenizer is not None and hasattr(tokenizer, "postprocessed_texts"):
@@ -226,6 +230,13 @@ class Paraformer(HipModel):
                 meta["token_matrix"] = (r["tokens"], r["ntok"])
             toks = r["tokens"].cpu().numpy()           # one device->host copy for the whole batch
             ntok = r["ntok"].cpu().numpy()
+            if (tokenizer is not None and not pred_ts and kwargs.get("output_dir") is None and
+                    hasattr(tokenizer, "postprocessed_texts_matrix")):
+                # text results only: detokenised from the matrix itself (no per-utterance id lists)
+                texts = tokenizer.postprocessed_texts_matrix(toks, ntok, (self.eos, self.sos, self.blank_id))
+                key = self._keys(key, len(texts))
+                meta["owner"] = list(range(len(texts)))
+                return [{"key": key[i], "text": t} for i, t in enumerate(texts)], meta
             hyps = self._greedy_hyps(toks, ntok)
         if pred_ts:   # CIF outputs for ts_prediction_lfr6_standard (paraformer/model.py:572-582)
             peaks_h, alphas_h = r["peaks"].cpu(), r["alphas"].cpu()

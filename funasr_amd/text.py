@@ -90,6 +90,39 @@ class CharTokenizer:
             out.append(sentence_postprocess(self.ids2tokens(ids))[0])
         return out
 
+    def postprocessed_texts_matrix(self, toks, ntok, drop: Sequence[int] = ()) -> List[str]:
+        """postprocessed_texts of the rows toks[i, :ntok[i]] with the ids in `drop` removed (a count past the row width:
+        an empty row), straight from the [B, L] host token matrix: the masks, table lookups and the gather of every
+        simple one-character row's codes run over the whole matrix at once, each such row is then one '<U{k}' view of
+        its slice; other rows take postprocessed_texts."""
+        import numpy as np
+        toks = np.asarray(toks)
+        ntok = np.asarray(ntok).reshape(-1)
+        B, L = toks.shape
+        self.postprocessed_texts([])   # builds the tables
+        spec, simple, single, u1 = self._pp_tab
+        n = np.where(ntok <= L, ntok, 0)
+        keep = np.arange(L)[None, :] < n[:, None]
+        for d in drop:
+            keep &= toks != d
+        ids = np.where(keep, toks, 0)
+        ok = (simple[ids] | ~keep).all(1)
+        kept = keep & ~spec[ids]
+        ok &= (single[ids] | ~kept).all(1)
+        cnt = kept.sum(1)
+        ok &= cnt > 0
+        codes = u1[toks[kept & ok[:, None]]]   # row-major: the fast rows' codes back to back
+        out: List[str] = []
+        o = 0
+        for i in range(B):
+            if ok[i]:
+                c = int(cnt[i])
+                out.append(codes[o:o + c].view(f"<U{c}")[0].strip())
+                o += c
+            else:
+                out.append(self.postprocessed_texts([toks[i][keep[i]].tolist()])[0])
+        return out
+
     def encode(self, text, **kwargs) -> List[int]:
         """text (a string, or a list of words as the punctuation model passes) -> ids
         (abs_tokenizer.py:65-69; unknown tokens -> unk id)."""

@@ -246,9 +246,10 @@ def test_datadir_writer_semantics(tmp_path):
 
 
 def test_postprocessed_texts_equal_sentence_postprocess():
-    """CharTokenizer.postprocessed_texts (the vectorised greedy-result path of Paraformer.inference) equals
-    sentence_postprocess(ids2tokens(ids))[0] row for row: all-Chinese rows (the fast path), rows with ASCII words,
-    BPE pieces, single-letter runs, specials, spaces and empty rows (the general path)."""
+    """CharTokenizer.postprocessed_texts (the vectorised greedy-result path of Paraformer.inference) and its matrix
+    form postprocessed_texts_matrix equal sentence_postprocess(ids2tokens(ids))[0] row for row: all-Chinese rows (the
+    fast path), rows with ASCII words, BPE pieces, single-letter runs, specials, spaces and empty rows (the general
+    path)."""
     import numpy as np
     from funasr_amd.text import CharTokenizer, sentence_postprocess
     vocab = ["<blank>", "<s>", "</s>", "一", "丁", "中", "国", "1", "23", "@", "a", "b", "C", "hello", "wor@@", "ld",
@@ -262,3 +263,11 @@ def test_postprocessed_texts_equal_sentence_postprocess():
         rows.append([int(v) for v in rng.integers(1, hi, n)])
     want = [sentence_postprocess(tok.ids2tokens(r))[0] for r in rows]
     assert tok.postprocessed_texts(rows) == want
+    # the matrix form: rows toks[i, :ntok[i]] minus blank / sos / eos (a count past the width: an empty row)
+    B, L = 600, 14
+    toks = rng.integers(0, len(vocab), (B, L)).astype(np.int32)
+    toks[:200] = rng.integers(0, 10, (200, L))    # mostly the one-character / simple fast path
+    ntok = rng.integers(0, L + 3, B).astype(np.int32)
+    rows_m = [[int(t) for t in toks[i, :ntok[i]] if t not in (0, 1, 2)] if ntok[i] <= L else [] for i in range(B)]
+    assert tok.postprocessed_texts_matrix(toks, ntok, (2, 1, 0)) == [sentence_postprocess(tok.ids2tokens(r))[0]
+                                                                     for r in rows_m]
