@@ -166,11 +166,13 @@ class WavFrontendOnline(WavFrontend):
         for wav, _, cache in items:
             if not cache:
                 self.init_cache(cache)
-            x = np.concatenate([cache["input_cache"], self.load(wav)])
+            w = self.load(wav)
+            x = np.concatenate([cache["input_cache"], w]) if cache["input_cache"].size else w   # (no copy of a fresh chunk)
             nfr = int((x.shape[0] - self.FL) / self.FS + 1)
             nfr = nfr if nfr >= 1 and x.shape[0] >= self.FL else 0
             keep = x.shape[0] - nfr * self.FS
-            cache["input_cache"] = x[-keep:] if keep else x     # x[-0:] is all of x (:331-333)
+            cache["input_cache"] = (x[-keep:] if keep else x).copy()     # x[-0:] is all of x (:331-333); never a view
+                                                                        # of the caller's buffer
             xs.append(x[: (nfr - 1) * self.FS + self.FL] if nfr else x[:0])
             nfrs.append(nfr)
         fb = None

@@ -370,8 +370,10 @@ class FsmnVADStreaming(HipModel):
         if isinstance(x, str):
             from .frontend import read_wav
             x, is_final = read_wav(x), True
-        x = x.detach().cpu().numpy() if hasattr(x, "detach") else np.asarray(x, np.float32)
-        audio = np.concatenate([cache["prev_samples"], x.reshape(-1).astype(np.float32)])
+        x = x.detach().cpu().numpy() if hasattr(x, "detach") else x
+        x = np.asarray(x, np.float32).reshape(-1)   # no copy of a float32 waveform (300 s: 19 MB)
+        prev = cache["prev_samples"]
+        audio = np.concatenate([prev, x]) if prev.size else x
         stride = int(chunk_ms * fe.fs / 1000)
         n = int(len(audio) // stride + int(is_final))
         m = int(len(audio) % stride * (1 - int(is_final)))
@@ -394,7 +396,8 @@ class FsmnVADStreaming(HipModel):
                 db_new = np.zeros((0,))
             p = eng.run(feats).cpu().numpy() if feats.shape[0] else np.zeros((0,), np.float32)
             segments.extend(det.push(db_new, p, fin, streaming))
-        cache["prev_samples"] = audio[:-m] if m else audio[:0]
+        # (a copy: the caller's waveform is neither kept alive nor aliased by the cache)
+        cache["prev_samples"] = audio[:-m].copy() if m else np.zeros((0,), np.float32)
         if is_final:
             self.init_cache(cache, **kwargs)
         key = self._keys(key, 1)
