@@ -245,7 +245,7 @@ void pfm_knobs_refresh() {
     k.kv_overlap = iv("PFM_KV_OVERLAP", 1) != 0;
     k.subbatch = std::max(1, std::min(iv("PFM_SUBBATCH", 2), 4));
     k.stream_graph = iv("PFM_STREAM_GRAPH", 1) != 0;
-    k.punc_graph = iv("PFM_PUNC_GRAPH", 0) != 0;
+    k.punc_graph = iv("PFM_PUNC_GRAPH", 1) != 0;
     k.gemm_gm = iv("PFM_GEMM_GM", -1);
     k.gemm_cfg = iv("PFM_GEMM_CFG", 0);
     k.gemm_st16 = iv("PFM_GEMM_ST16", 1) != 0;
@@ -2210,8 +2210,9 @@ int pfm_run_punc(pfm_handle* h, void* stream, int mode, const int32_t* ids, cons
 // CTTransformer.punc_forward is used in, model.py:277-316): one pinned staging copy each way around the model on
 // the handle's own device buffers, so a caller's sequential loop costs one C call per sentence. The model's ~35
 // launches run on the handle's own stream, ordered after the caller's queued work by one event; the call returns
-// with that stream drained. PFM_PUNC_GRAPH=1 replays them from a HIP graph per (mode, word count) from the second
-// call of a count on (measured: 234 vs 249 us per 30-word call; the kernels' own dispatch latency dominates).
+// with that stream drained. Fast mode (PFM_PUNC_GRAPH, default 1): the sentence is padded to a multiple of 16 words and
+// the launches replay from a HIP graph per padded length from its second call on (192 vs 207 us per 30-word call,
+// 287 vs 295 at 200: the kernels' own latency dominates; labels identical to the unpadded call, tests/test_gpu_punc.py).
 int pfm_run_punc_host(pfm_handle* h, void* stream, int mode, const int32_t* ids, int n, int32_t* punc) {
     pfm_knobs_refresh();
     if (!h || !ids || !punc || n < 1) return fail(PFM_E_ARG, "pfm_run_punc_host: null argument or n < 1");
@@ -2226,28 +2227,33 @@ int pfm_run_punc_host(pfm_handle* h, void* stream, int mode, const int32_t* ids,
     HIP_TRY(hipEventRecord(h->punc_ev, (hipStream_t)stream));
     HIP_TRY(hipStreamWaitEvent(h->punc_st, h->punc_ev, 0));
     hipStream_t st = h->punc_st;
-    if (h->punc_cap < n) {
-        const int cap = std::max(n, 256);
+    const bool fast = mode == PFM_MODE_FAST;
+    const bool use = fast && pfm_knobs().punc_graph && !h->prof_on;
+    // with graphs (fast mode) the sentence is padded to a multiple of 16 words: every kernel of the chain reads the
+    // length from the device (masked keys / FSMN rows, -1 labels beyond it) and computes each row alone, so the labels
+    // are the unpadded call's, and the <= 16 padded shapes of a text loop replay from a handful of graphs
+    const int Tp = use ? (n + 15) / 16 * 16 : n;
+    if (h->punc_cap < Tp) {
+        const int cap = std::max(Tp, 256);
         if (h->punc_pin) { HIP_TRY(hipStreamSynchronize(st)); HIP_TRY(hipHostFree(h->punc_pin)); h->punc_pin = nullptr; }
         HIP_TRY(hipHostMalloc((void**)&h->punc_pin, (size_t)(2 * cap + 1) * sizeof(int32_t), 0));
         HIP_TRY(h->punc_io.ensure((size_t)(2 * cap + 1) * sizeof(int32_t)));
         h->punc_cap = cap;
     }
-    const bool fast = mode == PFM_MODE_FAST;
-    int rc = punc_prepare(h, st, fast, 1, n);
+    int rc = punc_prepare(h, st, fast, 1, Tp);
     if (rc) return rc;
     int32_t* pin = h->punc_pin;
     memcpy(pin, ids, (size_t)n * sizeof(int32_t));
-    pin[n] = n;
+    for (int i = n; i < Tp; ++i) pin[i] = 0;
+    pin[Tp] = n;
     int32_t* dio = h->punc_io.as<int32_t>();
-    HIP_TRY(hipMemcpyAsync(dio, pin, (size_t)(n + 1) * sizeof(int32_t), hipMemcpyHostToDevice, st));
-    const bool use = pfm_knobs().punc_graph && !h->prof_on;
-    rc = graphed(h->punc_graphs, "punc", {mode, n, 0, 0}, use, st, [h] { return h->buf_gen.load(); },
-                 [&](hipStream_t s) { return punc_body(h, s, fast, dio, dio + n, 1, n, dio + n + 1, nullptr); });
+    HIP_TRY(hipMemcpyAsync(dio, pin, (size_t)(Tp + 1) * sizeof(int32_t), hipMemcpyHostToDevice, st));
+    rc = graphed(h->punc_graphs, "punc", {mode, Tp, 0, 0}, use, st, [h] { return h->buf_gen.load(); },
+                 [&](hipStream_t s) { return punc_body(h, s, fast, dio, dio + Tp, 1, Tp, dio + Tp + 1, nullptr); });
     if (rc) return rc;
-    HIP_TRY(hipMemcpyAsync(pin + n + 1, dio + n + 1, (size_t)n * sizeof(int32_t), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(pin + Tp + 1, dio + Tp + 1, (size_t)n * sizeof(int32_t), hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
-    memcpy(punc, pin + n + 1, (size_t)n * sizeof(int32_t));
+    memcpy(punc, pin + Tp + 1, (size_t)n * sizeof(int32_t));
     return PFM_OK;
 }
 

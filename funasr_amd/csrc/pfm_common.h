@@ -132,9 +132,8 @@ struct PfmKnobs {
     int kv_overlap;         // PFM_KV_OVERLAP (default 1): memory K|V projection on the side stream
     int subbatch;           // PFM_SUBBATCH (default 2): concurrent encoder utterance groups
     int stream_graph;       // PFM_STREAM_GRAPH (default 1): streaming steps through HIP graphs
-    int punc_graph;         // PFM_PUNC_GRAPH (default 0): pfm_run_punc_host's model launches through HIP graphs
-                            // per word count (6 % off a repeated 30-word call; a capture costs more than a call saves
-                            // until ~30 replays, and the text loop's counts mostly do not repeat within a file)
+    int punc_graph;         // PFM_PUNC_GRAPH (default 1): fast-mode pfm_run_punc_host pads the sentence to a multiple
+                            // of 16 words and replays its launches from one HIP graph per padded length
     int gemm_gm;            // PFM_GEMM_GM: grouped tile order override (-1 = default)
     int gemm_cfg;           // PFM_GEMM_CFG: forced tile configuration (0 = policy)
     int gemm_st16;          // PFM_GEMM_ST16 (default 1): 16-B bf16 epilogue stores

@@ -128,13 +128,14 @@ def test_punc_bad_args(tiny):
 
 @pytest.mark.parametrize("mode", ["exact", "fast"])
 def test_punc_host_graph_replay_matches_device_path(mode):
-    """PFM_PUNC_GRAPH=1: pfm_run_punc_host replays one HIP graph per (mode, word count) from a count's second call
-    on: the first (eager), second (capture) and later (replay) calls of every count, interleaved, equal
-    pfm_run_punc's labels on device operands; after new weights are loaded, the replayed graphs follow them. The
-    default (eager) path gives the same labels."""
+    """PFM_PUNC_GRAPH=1 (the default): fast-mode pfm_run_punc_host pads the sentence to a multiple of 16 words and
+    replays one HIP graph per padded length from its second call on — 20- and 27-word sentences share one graph, 33 and
+    41 another: the first (eager), second (capture) and later (replay) calls, interleaved, equal pfm_run_punc's labels
+    on unpadded device operands; after new weights are loaded, the replayed graphs follow them. EXACT mode and
+    PFM_PUNC_GRAPH=0 run unpadded and eager, with the same labels."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    os.environ["PFM_PUNC_GRAPH"] = "1"
+    os.environ.pop("PFM_PUNC_GRAPH", None)
     cfg = ct_transformer()
     e = PfmEngine(cfg, 0)
     e.load_state_dict(make_weights(cfg, seed=0))
@@ -156,8 +157,11 @@ def test_punc_host_graph_replay_matches_device_path(mode):
                     got = e.run_punc_host(x, mode=mode)
                     assert np.array_equal(got, wv), (weights_seed, rep, len(x))
     finally:
+        os.environ["PFM_PUNC_GRAPH"] = "0"
+    try:
+        assert all(np.array_equal(e.run_punc_host(x, mode=mode), wv) for x, wv in zip(seqs, want))
+    finally:
         del os.environ["PFM_PUNC_GRAPH"]
-    assert all(np.array_equal(e.run_punc_host(x, mode=mode), wv) for x, wv in zip(seqs, want))
 
 
 @pytest.mark.parametrize("n", [30, 100, 200])
